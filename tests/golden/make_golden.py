@@ -1,0 +1,254 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE code.
+
+Run in the build container only (the reference tree does not exist on the GPU box):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+The reference's fp32 path imports third-party packages that are absent here
+(snntorch, brevitas).  They are replaced by *import-only* stubs inserted into
+``sys.modules``; the only stub that executes arithmetic is ``snntorch.Leaky``,
+which is the oracle's restatement (``oracle.lif_ref.LeakyRef``) -- so fixtures
+that go through ``SNNtorch_ConvLIF*`` / ``LIFFireNet`` pin the reference's conv,
+BatchNorm, state and model wiring but NOT snntorch's LIF arithmetic (parity
+unpinned for that piece).  Fixtures for ``utils/iwe.py``, ``loss/flow.py``,
+``models/spiking_submodules.py`` and ``models/submodules.py:ConvLayer`` are
+produced by reference code end to end.
+
+Outputs are small .npz files (inputs + expected outputs), nothing else.
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+from oracle.lif_ref import LeakyRef  # noqa: E402
+
+
+def install_stubs():
+    class _Unavailable:
+        def __init__(self, *a, **k):
+            raise RuntimeError("quantized path is not part of the fixtures")
+
+    snn = types.ModuleType("snntorch")
+
+    class Leaky(LeakyRef):
+        def __init__(self, beta, threshold=1.0, learn_beta=False, learn_threshold=False,
+                     reset_mechanism="subtract", reset_delay=True, state_quant=False, **_):
+            assert reset_delay is False and not state_quant
+            super().__init__(torch.as_tensor(beta), torch.as_tensor(threshold), reset_mechanism)
+
+    snn.Leaky = Leaky
+    func = types.ModuleType("snntorch.functional")
+    func.quant = types.SimpleNamespace(state_quant=_Unavailable)
+    snn.functional = func
+    sys.modules["snntorch"] = snn
+    sys.modules["snntorch.functional"] = func
+    bre = types.ModuleType("brevitas")
+    bnn = types.ModuleType("brevitas.nn")
+    for n in ("QuantConv2d", "QuantIdentity", "QuantTanh", "QuantReLU"):
+        setattr(bnn, n, _Unavailable)
+    bq = types.ModuleType("brevitas.quant")
+    for n in ("Int8WeightPerTensorFloat", "Int8ActPerTensorFloat", "Int8Bias"):
+        setattr(bq, n, object)
+    bql = types.ModuleType("brevitas.nn.quant_layer")
+    bql.QuantLayerMixin = object
+    bcore = types.ModuleType("brevitas.core")
+    bcq = types.ModuleType("brevitas.core.quant")
+    bcq.QuantType = object
+    bre.nn, bre.quant, bre.core = bnn, bq, bcore
+    for name, mod in {"brevitas": bre, "brevitas.nn": bnn, "brevitas.quant": bq,
+                      "brevitas.nn.quant_layer": bql, "brevitas.core": bcore,
+                      "brevitas.core.quant": bcq}.items():
+        sys.modules[name] = mod
+
+
+def synth_events(gen, B, N, H, W):
+    """Synthetic window in the reference's list layout [B,N,4] = (ts, y, x, p)."""
+    ys = torch.randint(0, H, (B, N), generator=gen).float()
+    xs = torch.randint(0, W, (B, N), generator=gen).float()
+    ts = torch.sort(torch.rand(B, N, generator=gen), dim=1).values
+    ts = (ts - ts[:, :1]) / (ts[:, -1:] - ts[:, :1])
+    ps = torch.randint(0, 2, (B, N), generator=gen).float() * 2 - 1
+    ev = torch.stack([ts, ys, xs, ps], dim=2)
+    pol = torch.stack([(ps > 0).float(), (ps < 0).float()], dim=2)
+    cnt = torch.zeros(B, 2, H, W)
+    mask = torch.zeros(B, 1, H, W)
+    for b in range(B):
+        pos = ps[b] > 0
+        cnt[b, 0].index_put_((ys[b][pos].long(), xs[b][pos].long()), torch.ones(int(pos.sum())), accumulate=True)
+        cnt[b, 1].index_put_((ys[b][~pos].long(), xs[b][~pos].long()), torch.ones(int((~pos).sum())), accumulate=True)
+        mask[b, 0, ys[b].long(), xs[b].long()] = 1
+    return ev, pol, cnt, mask
+
+
+def iwe_case(ref_iwe, out):
+    """utils/iwe.py get_interpolation / interpolate incl. edge cases."""
+    gen = torch.Generator().manual_seed(11)
+    H, W, B, M = 12, 20, 2, 160
+    ev, pol, _, _ = synth_events(gen, B, M, H, W)
+    flow = (torch.rand(B, M, 2, generator=gen) - 0.5) * 0.3
+    # edge cases: zero flow (exact-integer warps), exact half/integer displacements,
+    # boundary pixels, far out-of-range warps, values that straddle floor(w + 1).
+    flow[:, :8] = 0.0
+    ev[:, 8:16, 0] = 0.5
+    flow[:, 8:16, 0] = torch.tensor([2.0, -2.0, 1.0, -1.0, 0.25, -0.25, 4.0, -4.0]) / 20.0
+    flow[:, 8:16, 1] = torch.tensor([-4.0, 4.0, 0.5, -0.5, 2.0, -2.0, 1.0, -1.0]) / 20.0
+    ev[:, 16:20, 1] = torch.tensor([0.0, H - 1.0, 0.0, H - 1.0])
+    ev[:, 16:20, 2] = torch.tensor([0.0, 0.0, W - 1.0, W - 1.0])
+    flow[:, 20:24] = torch.tensor([[3.0, 3.0], [-3.0, -3.0], [3.0, -3.0], [-3.0, 3.0]])
+    ev[:, 24, 1] = 3.0
+    ev[:, 24, 0] = 1.0 - 2.0 ** -24
+    flow[:, 24, 0] = -1e-8
+    res = [H, W]
+    rec = {"events": ev.numpy(), "flow_ev": flow.numpy(), "pol": pol.numpy(), "res": np.array(res)}
+    for name, tref in (("fw", 3), ("bw", 0)):
+        evk = ev.clone()
+        evk[:, :, 0] += 1.0  # a second-pass window (ts + pass index)
+        idx, w = ref_iwe.get_interpolation(evk, flow, tref, res, 20)
+        pol4 = torch.cat([pol] * 4, dim=1)
+        img_p = ref_iwe.interpolate(idx.long(), w, res, polarity_mask=pol4[:, :, 0:1])
+        img_n = ref_iwe.interpolate(idx.long(), w, res, polarity_mask=pol4[:, :, 1:2])
+        rec[f"{name}_idx"] = idx.long().numpy()[:, :, 0]
+        rec[f"{name}_w"] = w.numpy()[:, :, 0]
+        rec[f"{name}_iwe_pos"] = img_p.numpy()
+        rec[f"{name}_iwe_neg"] = img_n.numpy()
+    ridx, rw = ref_iwe.get_interpolation(ev, flow, 1, res, 20, round_idx=True)
+    rec["round_idx"] = ridx.long().numpy()[:, :, 0]
+    rec["round_w"] = rw.numpy()[:, :, 0]
+    np.savez_compressed(os.path.join(out, "iwe_case.npz"), **rec)
+
+
+def loss_case(ref_flow, out):
+    """loss/flow.py EventWarping: value and dL/dflow over T windows."""
+    gen = torch.Generator().manual_seed(12)
+    H, W, B, N, T = 12, 20, 2, 96, 3
+    config = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001,
+              "overwrite_intermediate": False}, "model": {"mask_output": True}}
+    lossf = ref_flow.EventWarping(config, "cpu")
+    flows, rec = [], {"res": np.array([H, W]), "T": T}
+    for t in range(T):
+        ev, pol, cnt, mask = synth_events(gen, B, N, H, W)
+        f = ((torch.rand(B, 2, H, W, generator=gen) - 0.5) * 0.2).requires_grad_(True)
+        if t == 1:
+            with torch.no_grad():
+                f[:, :, :3] = 0.0  # exact-integer warps on some rows
+        flows.append(f)
+        rec[f"events_{t}"] = ev.numpy().copy()
+        rec[f"pol_{t}"] = pol.numpy()
+        rec[f"mask_{t}"] = mask.numpy()
+        rec[f"flow_{t}"] = f.detach().numpy().copy()
+        lossf.event_flow_association([f], ev, pol, mask)
+    loss = lossf()
+    loss.backward()
+    rec["loss"] = np.array(loss.item(), dtype=np.float32)
+    for t in range(T):
+        rec[f"grad_{t}"] = flows[t].grad.numpy()
+    np.savez_compressed(os.path.join(out, "loss_case.npz"), **rec)
+
+
+def spiking_cells_case(ref_sub, out):
+    """models/spiking_submodules.py ConvLIF / ConvLIFRecurrent (U-Net flavour)."""
+    torch.manual_seed(13)
+    B, Cin, C, H, W, T = 2, 3, 4, 9, 11, 3
+    rec = {}
+    for tag, cls in (("ff", ref_sub.ConvLIF), ("rec", ref_sub.ConvLIFRecurrent)):
+        cell = cls(Cin, C, 3, leak=(0.0, 1.0), thresh=(0.8, 0.1))
+        xs = [(torch.rand(B, Cin, H, W) < 0.4).float() * 2.0 for _ in range(T)]
+        state, outs, loss = None, [], 0
+        for t in range(T):
+            z, state = cell(xs[t], state)
+            outs.append(z)
+            loss = loss + (z * torch.linspace(-1, 1, z.numel()).view_as(z)).sum() + 0.3 * state[0].sum()
+        loss.backward()
+        for k, v in cell.state_dict().items():
+            rec[f"{tag}.p.{k}"] = v.numpy()
+        for n, p in cell.named_parameters():
+            rec[f"{tag}.g.{n}"] = p.grad.numpy()
+        for t in range(T):
+            rec[f"{tag}.x_{t}"] = xs[t].numpy()
+            rec[f"{tag}.z_{t}"] = outs[t].detach().numpy()
+        rec[f"{tag}.v_last"] = state[0].detach().numpy()
+    np.savez_compressed(os.path.join(out, "spiking_cells_case.npz"), **rec)
+
+
+def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4):
+    """models/model.py LIFFireNet (reference wiring, conv, BN, states) with the
+    restated Leaky; T forwards + EventWarping + backward, train mode."""
+    sys.path.insert(0, REPO)
+    from oracle.lif_ref import make_unet_kwargs
+
+    torch.manual_seed(14)
+    gen = torch.Generator().manual_seed(15)
+    H, W, B, N, T = 16, 16, 2, 128, 3
+    kw = make_unet_kwargs(base_num_channels=C)
+    kw["name"] = name
+    model = getattr(ref_model, name)(dict(kw))
+    model.train()
+    config = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001,
+              "overwrite_intermediate": False}, "model": {"mask_output": True}}
+    lossf = ref_flow.EventWarping(config, "cpu")
+    rec = {"res": np.array([H, W]), "T": T, "C": C}
+    for k, v in model.state_dict().items():
+        rec[f"p0.{k}"] = v.numpy().copy()
+    for t in range(T):
+        ev, pol, cnt, mask = synth_events(gen, B, N, H, W)
+        x = model(None, cnt)
+        lossf.event_flow_association(x["flow"], ev.clone(), pol, mask)
+        rec[f"cnt_{t}"] = cnt.numpy()
+        rec[f"events_{t}"] = ev.numpy()
+        rec[f"pol_{t}"] = pol.numpy()
+        rec[f"mask_{t}"] = mask.numpy()
+        rec[f"flow_{t}"] = x["flow"][0].detach().numpy()
+        for i, s in enumerate(model._states):
+            rec[f"state_{t}_{i}"] = s.detach().numpy()
+    loss = lossf()
+    loss.backward()
+    rec["loss"] = np.array(loss.item(), dtype=np.float32)
+    for n, p in model.named_parameters():
+        rec[f"g.{n}"] = p.grad.numpy()
+    for k, v in model.state_dict().items():
+        rec[f"p1.{k}"] = v.numpy().copy()
+    np.savez_compressed(os.path.join(out, f"{name.lower()}_case.npz"), **rec)
+
+
+def convlayer_case(ref_sub, out):
+    torch.manual_seed(16)
+    layer = ref_sub.ConvLayer(6, 2, 1, activation="tanh", w_scale=0.3)
+    with torch.no_grad():
+        layer.conv2d.bias.uniform_(-0.2, 0.2)
+    x = (torch.rand(2, 6, 5, 7) < 0.5).float()
+    y = layer(x)
+    (y * torch.arange(y.numel()).view_as(y).float()).sum().backward()
+    np.savez_compressed(os.path.join(out, "convlayer_case.npz"), x=x.numpy(), y=y.detach().numpy(),
+                        w=layer.conv2d.weight.detach().numpy(), b=layer.conv2d.bias.detach().numpy(),
+                        gw=layer.conv2d.weight.grad.numpy(), gb=layer.conv2d.bias.grad.numpy())
+
+
+def main():
+    ref_root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    install_stubs()
+    sys.path.insert(0, ref_root)
+    import loss.flow as ref_flow
+    import models.model as ref_model
+    import models.spiking_submodules as ref_sub_sp
+    import models.submodules as ref_sub
+    import utils.iwe as ref_iwe
+
+    out = HERE
+    torch.set_num_threads(1)
+    iwe_case(ref_iwe, out)
+    loss_case(ref_flow, out)
+    spiking_cells_case(ref_sub_sp, out)
+    convlayer_case(ref_sub, out)
+    liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 4)
+    liffirenet_case(ref_model, ref_flow, out, "LIFFireNet_short", 4)
+    print("golden fixtures written to", out)
+
+
+if __name__ == "__main__":
+    main()
