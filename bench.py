@@ -1,0 +1,339 @@
+"""LIFFireNet train-step throughput on MI355X (events/s), the BASELINE.json metric.
+
+One step = the reference training loop's inner iteration (train_flow.py:231-279):
+T=10 forwards of LIFFireNet on 1000-event windows, EventWarping loss, backward,
+SUM all-reduce of gradients across ranks (data parallel, weak scaling), clip_grad_norm_
+(1.0), Adam (lr 2e-4), truncated-BPTT state detach, loss reset.  Synthetic seeded
+event windows resident in HBM (configs/train_SNN.yml shapes: 128x128, batch 8 per
+GPU, base_num_channels 8).  The whole step is captured once into a HIP graph
+(torch.cuda.graph) and replayed; every kernel on the path is in libsnnflow.so.
+
+    python bench.py [--gpus N --steps K --warmup W --channels C --res R --batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU, RCCL)
+
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel, timed live with
+HIP events around each of its launches in one extra eager step after the timed
+region; `cpu_baseline` times the CPU oracle (oracle/, a restatement of the
+reference's PyTorch path) on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "snn_event-based_optical_flow_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--channels", type=int, default=8)
+    p.add_argument("--res", type=int, default=128)
+    p.add_argument("--batch", type=int, default=8, help="per-GPU batch (cfg2/cfg4: 8)")
+    p.add_argument("--T", type=int, default=10, help="windows per loss (window_loss / window)")
+    p.add_argument("--events", type=int, default=1000, help="events per window (data.window)")
+    p.add_argument("--model", default="LIFFireNet")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pool", type=int, default=3, help="distinct synthetic batches cycled in HBM")
+    return p.parse_args()
+
+
+def algorithmic_bytes(name, C, P, cin0):
+    """Algorithmic HBM bytes of one launch (each tensor read/written once; fp32)."""
+    f = 4 * P
+    if name.startswith("conv_fwd[0]"):
+        return f * (cin0 + C)                      # x in, y out
+    if name.startswith("conv_fwd_rec"):
+        return f * (2 * C + 2 * C + C + C)         # prev y, prev mem in; prev state out; s_prev in; y out
+    if name.startswith("conv_fwd"):
+        return f * (2 * C + 2 * C + C)
+    if name == "lif_fwd":
+        return f * (2 * C + 2 * C + 2)             # y, mem in; state out; flow out
+    if name == "lif_bwd":
+        return f * (2 * C + 4 + C)                 # y, mem, flow, g_flow in; g_cur out
+    if name.startswith("layer_bwd_head"):
+        return f * (2 * C + cin0)                  # g_cur, y, x in
+    if name.startswith("layer_bwd_rec"):
+        return f * (3 * C + C + 2 * C + 2 * C + C)  # g_cur,y,x ; s_prev ; g_state_prev out ; prev y,mem ; prev g_cur
+    if name.startswith("layer_bwd"):
+        return f * (3 * C + 2 * C + C)
+    return None
+
+
+def classify(name, rec_layers):
+    """Map engine launch names to kernel classes with one byte formula each."""
+    if name.startswith("conv_fwd["):
+        l = int(name[9:-1])
+        if l == 0:
+            return "conv_fwd[0]"
+        return "conv_fwd_rec" if l in rec_layers else "conv_fwd"
+    if name.startswith("layer_bwd["):
+        l = int(name[10:-1])
+        if l == 0:
+            return "layer_bwd_head"
+        return "layer_bwd_rec" if l in rec_layers else "layer_bwd"
+    return name
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+
+    import snnflow
+    from snnflow import _lib
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(0)  # configs/parser.py:92-96 (loader.seed = 0): identical init on every rank
+    kw = {"name": args.model, "encoding": "cnt", "round_encoding": False, "norm_input": False, "num_bins": 2,
+          "base_num_channels": args.channels, "kernel_size": 3, "activations": ["arctanspike", "arctanspike"],
+          "mask_output": True, "quantization": {"enabled": False}, "tebn": {"enabled": False},
+          "mpbn": {"enabled": False}, "spiking_neuron": {"leak": [0.0, 1.0], "thresh": [0.0, 0.8]}}
+    model = getattr(snnflow, args.model)(kw).to(dev).train()
+    R, B, T, N = args.res, args.batch, args.T, args.events
+    cfg = {"loader": {"resolution": [R, R]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    loss_fn = snnflow.EventWarping(cfg, dev)
+    params = list(model.parameters())
+    opt = torch.optim.Adam(params, lr=2e-4, capturable=not args.no_graph)
+
+    # synthetic data, resident in HBM; per-rank stream seeded by (seed, rank)
+    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
+    pool = [[make_window(B, N, R, R, gen, dev) for _ in range(T)] for _ in range(args.pool)]
+    static = [{k: v.clone() for k, v in w.items()} for w in pool[0]]
+
+    def load_batch(i):
+        for dst, src in zip(static, pool[i % len(pool)]):
+            for k in dst:
+                dst[k].copy_(src[k], non_blocking=True)
+
+    # persistent state buffers: detach_states() == copy into them (the reference clones)
+    state_bufs = None
+
+    def fwd_bwd():
+        loss_fn.reset()
+        for t in range(T):
+            w = static[t]
+            out = model(w["event_voxel"], w["event_cnt"])
+            loss_fn.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        loss = loss_fn()
+        loss.backward()
+        return loss
+
+    def sync_grads():
+        """One SUM all-reduce of all gradients (the loss is a SUM over samples, loss/flow.py:228,
+        so SUM reproduces the single-device gradient of the global batch)."""
+        if world == 1:
+            return
+        flat = getattr(model.engine, "last_flat", None)
+        if flat is not None and _views_of(flat, [p.grad for p in params]):
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM)  # grads are views of the engine's flat buffer
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+        off = 0
+        for p in params:
+            p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+            off += p.numel()
+
+    def update():
+        torch.nn.utils.clip_grad_norm_(params, 1.0)
+        opt.step()
+        nonlocal state_bufs
+        if state_bufs is None:
+            state_bufs = [s.detach().clone() for s in model._states]
+        for dst, s in zip(state_bufs, model._states):
+            dst.copy_(s.detach())
+        model._states = list(state_bufs)
+
+    def step_eager():
+        opt.zero_grad(set_to_none=True)
+        fwd_bwd()
+        sync_grads()
+        update()
+
+    # warmup (eager; builds workspaces, optimizer state, persistent state buffers)
+    s_side = torch.cuda.Stream(dev)
+    s_side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s_side):
+        for i in range(max(args.warmup, 3)):
+            load_batch(i)
+            step_eager()
+    torch.cuda.current_stream(dev).wait_stream(s_side)
+    torch.cuda.synchronize(dev)
+
+    graphs = []
+    if not args.no_graph:
+        opt.zero_grad(set_to_none=True)
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            fwd_bwd()
+            if world == 1:
+                update()
+        graphs.append(g1)
+        if world > 1:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2, pool=g1.pool()):
+                update()
+            graphs.append(g2)
+
+    def step(i):
+        load_batch(i)
+        if graphs:
+            graphs[0].replay()
+            if world > 1:
+                sync_grads()
+                graphs[1].replay()
+        else:
+            step_eager()
+
+    for i in range(2):  # graph warm replays
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    events_per_step = world * B * T * N
+    value = events_per_step * args.steps / elapsed
+
+    # live per-kernel timing: one extra eager step with HIP events around every launch
+    timer = _lib.KernelTimer()
+    _lib.TIMER = timer
+    load_batch(0)
+    step_eager()
+    _lib.TIMER = None
+    kern = timer.summary()
+    rec_layers = {i for i, (_, r) in enumerate(model.layer_spec) if r}
+    classes = {}
+    for name, v in kern.items():
+        c = classify(name, rec_layers)
+        n, tot = classes.get(c, (0, 0.0))
+        classes[c] = (n + v["launches"], tot + v["total_ms"])
+    P = B * R * R
+    dominant = max(classes, key=lambda k: classes[k][1])
+    n_dom, tot_dom = classes[dominant]
+    avg_us = 1000.0 * tot_dom / n_dom
+    abytes = algorithmic_bytes(dominant, args.channels, P, 2)
+    achieved = abytes / (avg_us * 1e-6) / 1e9 if abytes else None
+    kernels = {k: {"launches": n, "avg_us": round(1000.0 * t / n, 2), "share": round(t / sum(x[1] for x in classes.values()), 3)}
+               for k, (n, t) in sorted(classes.items(), key=lambda kv: -kv[1][1])}
+    roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": _pmc_traffic(dominant, args), "bytes_per_launch": abytes, "avg_us": round(avg_us, 2)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, pool[0])
+
+    if rank == 0:
+        line = {
+            "metric": "events/sec (train step) LIFFireNet T=10 128x128",
+            "value": round(value, 1), "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"{args.model} train step: T={T} x {N}-event windows, {R}x{R}, "
+                                   f"batch {B}/GPU, base_num_channels {args.channels}, EventWarping + Adam",
+                       "global_batch": B * world, "parallelism": f"dp{world}",
+                       "hip_graph": not args.no_graph},
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _views_of(flat, grads):
+    lo, hi = flat.data_ptr(), flat.data_ptr() + flat.numel() * flat.element_size()
+    return all(g is not None and lo <= g.data_ptr() < hi for g in grads) and \
+        sum(g.numel() for g in grads) == flat.numel()
+
+
+def _pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate --pmc passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM), if it was measured on this config."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    key = f"C{args.channels}_R{args.res}_B{args.batch}"
+    return d.get(key, {}).get(kernel)
+
+
+def cpu_baseline(args, windows):
+    """The CPU oracle (pure-PyTorch restatement of the reference path, same op sequence)
+    timed on this host: one full train step of the same workload after one warm-up
+    step (bounded sample: 2 train steps)."""
+    from oracle import iwe_ref, lif_ref
+
+    threads = len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 16))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=args.channels)
+    model = lif_ref.LIFFireNetRef(kw, args.model).train()
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+    cpu_w = [{k: v.cpu() for k, v in w.items()} for w in windows]
+    R = args.res
+
+    def one():
+        lf = iwe_ref.EventWarpingRef([R, R])
+        for w in cpu_w:
+            out = model(None, w["event_cnt"])
+            lf.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        loss = lf()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        opt.zero_grad()
+        model.detach_states()
+
+    one()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:  # bounded sample: whole train steps until ~10 s of CPU work (>= 1 step)
+        one()
+        n += 1
+        if time.perf_counter() - t0 > 10.0:
+            break
+    dt = time.perf_counter() - t0
+    ev = n * args.batch * args.T * args.events
+    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"{n} timed train steps (after 1 warm-up) of the same workload: {args.batch}x{args.T} windows "
+                      f"of {args.events} events, {R}x{R}, C={args.channels}, Adam; oracle/ pure-PyTorch CPU "
+                      f"restatement of the reference path, {threads} threads", "seconds": round(dt, 3)}
+
+
+if __name__ == "__main__":
+    main()

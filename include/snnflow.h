@@ -1,0 +1,208 @@
+/*
+ * snnflow.h -- C-ABI of the MI355X-native LIFFireNet / event-warping hot path.
+ *
+ * Plain pointers (device memory, fp32 unless stated), sizes and a HIP stream.
+ * No torch types.  Every entry point enqueues work on `stream` and returns
+ * 0 on success, a negative SNNFLOW_E* code on bad arguments, or a positive
+ * hipError_t; `snnflow_last_error()` describes the last failure (thread-local).
+ * Nothing allocates or frees memory; all scratch is caller-provided, so every
+ * call is capturable into a hipGraph.
+ *
+ * Layouts:
+ *   activations  NHWC  [B][H][W][C]          (torch channels_last)
+ *   cell state   [2][B][H][W][C]  (mem, spk)  (reference: torch.stack([mem, spk]))
+ *   flow map     NCHW  [B][2][H][W]
+ *   weights      torch [Cout][Cin][3][3]; kernels read the transposed copies made by
+ *                snnflow_prep_weights.
+ *
+ * The reference has no native operators on this path (its only native op is the
+ * forward-only CPU ONNX export op, ONNX_LIF_operator/src/lif_op.cpp:8-82); each entry
+ * point below names the reference Python it replaces.
+ */
+#ifndef SNNFLOW_H
+#define SNNFLOW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNNFLOW_ABI_VERSION 2
+
+#define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
+#define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
+
+/* Tile geometry of the conv kernels (block = SNNFLOW_TILE_H x SNNFLOW_TILE_W pixels). */
+#define SNNFLOW_TILE_H 8
+#define SNNFLOW_TILE_W 32
+
+/* Per-layer neuron + BatchNorm parameters
+ * (SNNtorch_spiking_submodules.py:230-251 / :451-475: bn = BatchNorm2d(C, 0.1, 1e-5),
+ *  lif = snn.Leaky(beta, threshold, reset_mechanism, reset_delay=False)). */
+typedef struct snnflow_neuron {
+    const float* bn_weight;     /* [C] gamma                                   */
+    const float* bn_bias;       /* [C]                                          */
+    float* running_mean;        /* [C] updated in place when bn_train          */
+    float* running_var;         /* [C]                                          */
+    int64_t* num_batches_tracked; /* [1] incremented when bn_train (may be NULL) */
+    const float* beta;          /* [C] lif.beta (clamped to [0,1] on use)       */
+    const float* threshold;     /* [C] lif.threshold (clamp_min 0.01 done by prep) */
+    double momentum, eps;
+    int bn_train;               /* 1: batch statistics (train), 0: running stats */
+    int zero_reset;             /* 1: reset_mechanism="zero", 0: "subtract"     */
+} snnflow_neuron;
+
+/* ---- weight preparation -------------------------------------------------
+ * Transposes a conv weight [C][Cin][3][3] into wt_fwd [3][3][Cin][C] and
+ * wt_bwd [3][3][C][Cin] (skipped when w == NULL); if threshold != NULL clamps its
+ * first c entries in place to >= 0.01
+ * (SNNtorch_spiking_submodules.py:284 / :516 `threshold.data.clamp_(min=0.01)`). */
+int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* wt_bwd,
+                         float* threshold, void* stream);
+
+/* ---- forward: [LIF of layer l on a halo tile] + conv3x3(layer l+1) + BN statistics
+ * Replaces, per time step, `lif(bn(...))` of layer l fused with `ff(input_)`
+ * [+ `rec(prev_spk)`] of layer l+1 and the batch-stat part of its `bn`
+ * (SNNtorch_spiking_submodules.py:289-305 and :521-550).
+ * lif_in = 0: x is a strided tensor (e.g. event_cnt NCHW) with cin channels.
+ * lif_in = 1: the input spikes are computed from the previous layer's pre-BN conv
+ *             output prev_y (NHWC), its membrane prev_mem (NULL = zeros) and
+ *             prev_stats [2][cin] (mean, invstd); prev_state [2][B][H][W][cin]
+ *             receives (mem_out, spk) of the previous layer. */
+typedef struct snnflow_conv_fwd_args {
+    int B, H, W, cin, c;
+    int lif_in;
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* lif_in == 0 */
+    const float* prev_y; const float* prev_mem; const float* prev_stats;  /* lif_in == 1 */
+    snnflow_neuron prev; float* prev_state;
+    const float* wt_ff;         /* [3][3][cin][c]                      */
+    const float* wt_rec;        /* [3][3][c][c] or NULL (feed-forward) */
+    const float* s_prev;        /* NHWC [B][H][W][c] previous-step spikes; NULL = zeros */
+    snnflow_neuron self;        /* BN of this layer (running stats / train flag) */
+    float* y;                   /* out NHWC [B][H][W][c] pre-BN current           */
+    float* stats;               /* out [2][c] (mean, invstd) for the LIF of this layer */
+    double* partials;           /* scratch >= snnflow_conv_blocks(B,H,W) * 2c doubles */
+    unsigned* counter;          /* scratch, zero on first use, left zero           */
+} snnflow_conv_fwd_args;
+int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream);
+int snnflow_conv_blocks(int B, int H, int W);
+
+/* ---- forward: LIF of the last layer [+ pred ConvLayer(C->2,1x1,bias)+tanh]
+ * Replaces `lif(bn(.))` (SNNtorch_spiking_submodules.py:293-320) and
+ * `pred` (models/submodules.py:96-113, models/model.py:182). */
+typedef struct snnflow_lif_fwd_args {
+    int B, H, W, c;
+    const float* y; const float* mem; const float* stats;
+    snnflow_neuron n; float* state;
+    const float* pred_w;        /* [2][c] or NULL (no pred) */
+    const float* pred_b;        /* [2] */
+    float* flow;                /* NCHW [B][2][H][W] */
+} snnflow_lif_fwd_args;
+int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream);
+
+/* Gradient accumulators of one layer's neuron parameters (fp32, [C] each). */
+typedef struct snnflow_neuron_grad {
+    float* bn_weight; float* bn_bias; float* beta; float* threshold;
+} snnflow_neuron_grad;
+
+/* ---- backward of the top layer: [pred backward] + LIF/ATan surrogate backward
+ * g_s = g_out + g_state_spk + pred_w^T (g_flow * (1 - flow^2)); g_v = g_s * sg(v - theta).
+ * Writes g_cur (= dL/d BN-output, NHWC) and bstats [2][c] (sum g, sum (y-mean) g)
+ * for the BatchNorm backward, and accumulates (accumulate=1) or writes (0) the
+ * neuron-parameter gradients (and pred gradients). */
+typedef struct snnflow_lif_bwd_args {
+    int B, H, W, c;
+    const float* y; const float* mem; const float* stats; snnflow_neuron n;
+    const float* g_out;         /* NHWC grad of the spike output or NULL          */
+    const float* g_state;       /* [2][B][H][W][c] grad of the state output or NULL */
+    const float* pred_w; const float* flow; const float* g_flow;  /* pred or NULL    */
+    int64_t gflow_sb, gflow_sc; /* element strides of g_flow (batch, channel); HW dense */
+    float* g_cur; float* bstats;
+    float* g_mem;               /* NHWC grad of the membrane input (beta*(1-r)*g_v) or NULL */
+    snnflow_neuron_grad ng; float* g_pred_w; float* g_pred_b;
+    int accumulate;
+    double* partials; unsigned* counter;
+} snnflow_lif_bwd_args;
+int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream);
+
+/* ---- backward of one layer: BN backward + conv dgrad/wgrad of layer l
+ * [+ LIF backward of layer l-1 on the dgrad result] (the reverse of
+ * snnflow_conv_fwd).  Weight gradients go to per-block slabs
+ * (snnflow_conv_blocks() x c*cin*9 floats), written or accumulated across
+ * time steps; snnflow_slab_reduce turns them into gradients. */
+typedef struct snnflow_layer_bwd_args {
+    int B, H, W, cin, c;
+    const float* y; const float* stats; const float* g_cur; const float* bstats;
+    snnflow_neuron n;           /* BN parameters of layer l */
+    const float* wt_bwd_ff;     /* [3][3][c][cin]  (NULL: no input gradient)        */
+    const float* wt_bwd_rec;    /* [3][3][c][c] or NULL                             */
+    /* input of layer l (for wgrad): strided x (lif_in=0) or prev layer spikes      */
+    int lif_in;
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;
+    const float* s_prev;        /* NHWC previous-step spikes of layer l or NULL     */
+    float* slab_ff; float* slab_rec; int accumulate;
+    /* outputs */
+    float* g_x; int64_t gxs_b, gxs_c, gxs_h, gxs_w;   /* lif_in=0: input gradient (strided) or NULL */
+    float* g_state_prev;        /* [2][B][H][W][c] grad of the previous state (rec) or NULL */
+    int zero_mem_half;          /* 1: Stage B also zero-fills the membrane half of g_state_prev */
+    /* lif_in = 1: LIF backward of layer l-1 */
+    const float* prev_y; const float* prev_mem; const float* prev_stats; snnflow_neuron prev;
+    const float* prev_g_state;  /* [2][B][H][W][cin] or NULL */
+    float* prev_g_cur; float* prev_bstats; snnflow_neuron_grad prev_ng;
+    float* prev_g_mem;          /* NHWC grad of layer l-1's membrane input or NULL */
+    double* partials; unsigned* counter;
+} snnflow_layer_bwd_args;
+int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
+
+/* Sums per-block weight-gradient slabs: out[i][e] = sum_b slab[i][b][e]. */
+typedef struct snnflow_slab_desc { const float* slab; float* out; int elems; } snnflow_slab_desc;
+#define SNNFLOW_MAX_SLABS 16
+int snnflow_slab_reduce(const snnflow_slab_desc* d, int n, int nblk, void* stream);
+
+/* ---- event warping / contrast-maximisation loss (loss/flow.py:178-303) ----
+ * events [B][M][4] (ts,y,x,p) with per-window offsets (pass k owns events
+ * [off[k], off[k+1]) of every sample; its timestamps are ts + k, flow.py:92),
+ * pol [B][M][2], flows [B][T][2][H][W] (NCHW per window), masks [B][T][H][W]. */
+typedef struct snnflow_iwe_loss_args {
+    int B, M, T, H, W;
+    int tf;                     /* flow/mask windows: T, or 1 when overwrite_intermediate
+                                   (all events use the last flow; loss/flow.py:123-150) */
+    const float* events; const float* pol; const float* flows; const float* masks;
+    int32_t off[65];            /* pass offsets off[0..T] (T <= 64), by value */
+    float flow_scaling, weight;
+    int smoothing_mask, overwrite_intermediate, loss_scaling;
+    float* images;              /* scratch [2 dir][4 img][B][H*W]: cnt+, cnt-, ts+, ts- */
+    float* persample;           /* scratch [2 dir][B][4]: S+, S-, nz, loss_b          */
+    float* smooth;              /* scratch [8]                                         */
+    float* loss;                /* out [1]                                             */
+    double* partials; unsigned* counter;
+} snnflow_iwe_loss_args;
+int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
+/* g_loss: device scalar; g_flows out [B][T][2][H][W] (fully written). gimg scratch
+ * like images. */
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
+                         float* g_flows, void* stream);
+int snnflow_iwe_scratch_floats(int B, int H, int W);
+
+/* utils/iwe.py:20-71 get_interpolation (+ purge_unfeasible :4-17) for one pass:
+ * idx out [B][K*M] int32 (corner-major, K=4 bilinear / 1 rounded), w out [B][K*M]. */
+int snnflow_iwe_corners(const float* events, const float* flow_ev, int B, int M, float tref,
+                        int H, int W, float flow_scaling, int round_idx, int32_t* idx, float* w,
+                        void* stream);
+/* utils/iwe.py:74-93 interpolate: img[b][idx] += w * pol (img zeroed by the call). */
+int snnflow_iwe_interpolate(const int32_t* idx, const float* w, const float* pol, int64_t pol_sb,
+                            int B, int K, int H, int W, float* img, void* stream);
+
+/* HIP twin of the export op SNN_implementation::LIF (ONNX_LIF_operator/src/lif_op.cpp:8-56):
+ * m' = beta[c]*mem + x; spk = m' >= thr[c]; mem_out = spk ? 0 : m'  (NCHW). */
+int snnflow_lif_export(const float* x, const float* mem, const float* beta, const float* thr,
+                       int N, int C, int HW, float* spk, float* mem_out, void* stream);
+
+const char* snnflow_last_error(void);
+int snnflow_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

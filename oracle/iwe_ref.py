@@ -171,6 +171,22 @@ class EventWarpingRef:
             per_sample = per_sample / torch.sum(nz.reshape(events.shape[0], -1), dim=1)
         return torch.sum(per_sample)
 
+    def overwrite_intermediate_flow(self, flow_list):
+        """``loss/flow.py:123-150``: re-gather every event's flow from the final map,
+        keep a single flow map and a single (clipped) event mask."""
+        flow = flow_list[-1]
+        B = flow.shape[0]
+        events = torch.cat(self.events, dim=1)
+        pix = (events[:, :, 1] * self.res[1] + events[:, :, 2]).long()
+        f = flow.reshape(B, 2, -1)
+        self.flows_ev = [torch.stack([torch.gather(f[:, 1, :], 1, pix), torch.gather(f[:, 0, :], 1, pix)], dim=2)]
+        self.events = [events]
+        self.pols = [torch.cat(self.pols, dim=1)]
+        m = torch.cat(self.masks, dim=1).sum(dim=1, keepdim=True)
+        m[m > 1] = 1
+        self.masks = [m]
+        self.maps = [flow]
+
     def __call__(self):
         T = self._passes
         events = torch.cat(self.events, dim=1)
@@ -206,5 +222,5 @@ class EventWarpingRef:
         smooth = terms[0].sum()
         for t in terms[1:]:
             smooth = smooth + t.sum()
-        smooth = smooth / len(terms) / T
+        smooth = smooth / len(terms) / fx.shape[1]  # flow_dx.shape[1]: number of flow maps (flow.py:293)
         return fw + bw + self.weight * smooth

@@ -101,6 +101,7 @@ class LeakyRef(nn.Module):
             v = b * ((1 - r) * self.mem) + current
         else:
             v = b * self.mem + current - r * self.threshold
+        self.last_v = v.detach()  # pre-reset membrane, kept for near-threshold parity checks
         s = ATanHeaviside.apply(v - self.threshold) * self.graded_spikes_factor
         do_reset = s / self.graded_spikes_factor - r
         out = v - do_reset * v if self.zero_reset else v - do_reset * self.threshold

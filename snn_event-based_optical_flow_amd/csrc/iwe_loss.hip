@@ -1,0 +1,478 @@
+// Event warping, bilinear IWE splatting and the contrast-maximisation loss (fwd + bwd)
+// for gfx950.  Reference: utils/iwe.py:4-93 (purge_unfeasible, get_interpolation,
+// interpolate) and loss/flow.py:58-121, 178-303 (EventWarping); restated in
+// oracle/iwe_ref.py.
+//
+// Bit-exactness contract for the corner indices:
+//   w = pos + ((tref - ts_k) * f) * s    ts_k = ts + k (f32), no FMA (-ffp-contract=off)
+//   y0 = floor(wy), y1 = floor(wy + 1)    (not floor(wy) + 1)
+//   idx = (cy*inb)*W + cx*inb computed in f32
+#include <cmath>
+
+#include "snnflow_dev.h"
+
+using namespace snnflow;
+
+int snnflow_set_error(int code, const char* msg);
+#define SNN_FAIL(code, msg) return snnflow_set_error((code), (msg))
+#define SNN_CHECK_LAUNCH()                                                        \
+    do {                                                                          \
+        hipError_t e_ = hipGetLastError();                                        \
+        if (e_ != hipSuccess) return snnflow_set_error((int)e_, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+struct Corner {
+    int idx;      // flat pixel index (0 when out of bounds, like purge_unfeasible)
+    bool inb;
+    float ay, ax; // per-axis bilinear factors max(0, 1-|w-c|)
+    float dy, dx; // w - c per axis
+    float wt;     // ay*ax*inb
+};
+
+// get_interpolation for one event and one reference time (4 corners, corner-major order).
+__device__ inline void warp4(float ts, float y, float x, float fy, float fx, float tref, float s, int H, int W,
+                             Corner (&c)[4], float& wy, float& wx) {
+    const float dt = tref - ts;
+    wy = y + (dt * fy) * s;
+    wx = x + (dt * fx) * s;
+    const float y0 = floorf(wy), y1 = floorf(wy + 1.0f);
+    const float x0 = floorf(wx), x1 = floorf(wx + 1.0f);
+    const float cy[4] = {y0, y0, y1, y1}, cx[4] = {x0, x1, x0, x1};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const bool inb = (cy[k] >= 0.0f) && (cy[k] < (float)H) && (cx[k] >= 0.0f) && (cx[k] < (float)W);
+        const float m = inb ? 1.0f : 0.0f;
+        c[k].inb = inb;
+        c[k].dy = wy - cy[k];
+        c[k].dx = wx - cx[k];
+        c[k].ay = fmaxf(0.0f, 1.0f - fabsf(c[k].dy));
+        c[k].ax = fmaxf(0.0f, 1.0f - fabsf(c[k].dx));
+        c[k].wt = (c[k].ay * c[k].ax) * m;
+        c[k].idx = (int)((cy[k] * m) * (float)W + cx[k] * m);
+    }
+}
+
+__device__ inline int pass_of(const int32_t* off, int T, int i) {
+    int k = 0;
+    while (k + 1 < T && i >= off[k + 1]) ++k;
+    return k;
+}
+
+// d/dz of max(0, z) as torch.maximum(zeros, z) backward: 1 above, 1/2 on the tie, 0 below.
+__device__ inline float relu_tie(float z) { return z > 0.0f ? 1.0f : (z == 0.0f ? 0.5f : 0.0f); }
+__device__ inline float sgnf(float d) { return d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f); }
+
+// images layout: [dir 2][img 4][B][HW], img = cnt+, cnt-, ts+, ts-
+__global__ __launch_bounds__(NT) void k_iwe_scatter(snnflow_iwe_loss_args a) {
+    const int64_t HWp = (int64_t)a.H * a.W;
+    const int64_t n = (int64_t)a.B * a.M;
+    const int64_t img = (int64_t)a.B * HWp;
+    for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
+        const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
+        const int k = pass_of(a.off, a.T, i);
+        const float* ev = a.events + e * 4;
+        const float ts = ev[0] + (float)k, y = ev[1], x = ev[2];
+        const int pix = (int)(y * (float)a.W + x);
+        const int kf = a.tf == 1 ? 0 : k;
+        const float* fl = a.flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+        const float fy = fl[HWp + pix], fx = fl[pix];
+        const float pm0 = a.pol[e * 2], pm1 = a.pol[e * 2 + 1];
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const float tref = d == 0 ? (float)a.T : 0.0f;
+            const float tsw = d == 0 ? ts : (float)a.T - ts;
+            Corner c[4];
+            float wy, wx;
+            warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+            float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float wt = c[q].wt;
+                if (wt == 0.0f) continue;
+                const float wts = wt * tsw;
+                if (pm0 != 0.0f) {
+                    atomicAdd(base + c[q].idx, wt * pm0);
+                    atomicAdd(base + 2 * img + c[q].idx, wts * pm0);
+                }
+                if (pm1 != 0.0f) {
+                    atomicAdd(base + img + c[q].idx, wt * pm1);
+                    atomicAdd(base + 3 * img + c[q].idx, wts * pm1);
+                }
+            }
+        }
+    }
+}
+
+// Smoothness terms where pixel (h,w) of window t is the first element 'a' of the pair.
+struct SmoothTerms { float v[5]; };
+
+__device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
+
+__device__ inline SmoothTerms smooth_at(const snnflow_iwe_loss_args& a, int b, int t, int h, int w) {
+    const int64_t HWp = (int64_t)a.H * a.W;
+    const float* fx = a.flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+    const float* fy = fx + HWp;
+    const float* m = a.masks + ((int64_t)b * a.tf + t) * HWp;
+    const int p = h * a.W + w;
+    SmoothTerms r;
+    const bool sm = a.smoothing_mask != 0;
+    auto term = [&](int pb, const float* fxb, const float* fyb, const float* mb) {
+        const float d = (fx[p] - fxb[pb]) + (fy[p] - fyb[pb]);
+        const float c = charb(d);
+        return sm ? (m[p] * mb[pb]) * c : c;
+    };
+    r.v[0] = (w + 1 < a.W) ? term(p + 1, fx, fy, m) : 0.0f;                         // dx
+    r.v[1] = (h + 1 < a.H) ? term(p + a.W, fx, fy, m) : 0.0f;                       // dy
+    r.v[2] = (h + 1 < a.H && w + 1 < a.W) ? term(p + a.W + 1, fx, fy, m) : 0.0f;    // dxdy_dr
+    r.v[3] = (h >= 1 && w + 1 < a.W) ? term(p - a.W + 1, fx, fy, m) : 0.0f;         // dxdy_ur
+    r.v[4] = 0.0f;                                                                  // dt
+    if (t + 1 < a.tf && !a.overwrite_intermediate) {
+        const float* fx2 = fx + 2 * HWp;
+        const float* fy2 = fx2 + HWp;
+        const float* m2 = m + HWp;
+        r.v[4] = term(p, fx2, fy2, m2);
+    }
+    return r;
+}
+
+// Per pixel: IWE loss terms for both directions + smoothness; last block finalises.
+// blocks: B * chunks (each block covers NT pixels of one sample).
+__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks) {
+    constexpr int NV = 11;
+    __shared__ float red[4][NV];
+    __shared__ double scratch[NT];
+    __shared__ int is_last;
+    const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
+    const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
+    const int p = chunk * NT + tid;
+    float v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = 0.0f;
+    if (p < HWp) {
+        const float T = (float)a.T;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+            const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
+            const float A = (tp / (cp + 1e-9f)) / T;
+            const float Bv = (tn / (cn + 1e-9f)) / T;
+            v[3 * d + 0] = A * A;
+            v[3 * d + 1] = Bv * Bv;
+            v[3 * d + 2] = (cp + cn > 0.0f) ? 1.0f : 0.0f;
+        }
+        const int h = p / a.W, w = p - h * a.W;
+        for (int t = 0; t < a.tf; ++t) {
+            const SmoothTerms s = smooth_at(a, b, t, h, w);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) v[6 + j] += s.v[j];
+        }
+    }
+    const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const float s = wave_sum(v[j]);
+        if (lane == 0) red[wv][j] = s;
+    }
+    __syncthreads();
+    if (tid < NV)
+        a.partials[(int64_t)blockIdx.x * NV + tid] =
+            (((double)red[0][tid] + (double)red[1][tid]) + (double)red[2][tid]) + (double)red[3][tid];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (t == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // per-sample sums (6 per sample) and smoothness sums (5), fixed block order
+    for (int j = tid; j < 6 * a.B + 5; j += NT) {
+        double s = 0.0;
+        if (j < 6 * a.B) {
+            const int bb = j / 6, jj = j - bb * 6;
+            for (int c = 0; c < chunks; ++c) s += a.partials[((int64_t)bb * chunks + c) * NV + jj];
+        } else {
+            const int jj = 6 + (j - 6 * a.B);
+            for (int blk = 0; blk < (int)gridDim.x; ++blk) s += a.partials[(int64_t)blk * NV + jj];
+        }
+        scratch[j < NT ? j : 0] = s;  // (6B+5 <= NT enforced on the host)
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float total = 0.0f;
+        for (int d = 0; d < 2; ++d) {
+            float dir = 0.0f;
+            for (int bb = 0; bb < a.B; ++bb) {
+                const float sp = (float)scratch[6 * bb + 3 * d], sn = (float)scratch[6 * bb + 3 * d + 1];
+                const float nz = (float)scratch[6 * bb + 3 * d + 2];
+                float lb = sp + sn;
+                if (a.loss_scaling) lb = lb / nz;
+                float* ps = a.persample + ((int64_t)d * a.B + bb) * 4;
+                ps[0] = sp; ps[1] = sn; ps[2] = nz; ps[3] = lb;
+                dir += lb;
+            }
+            total += dir;
+        }
+        const int comps = a.overwrite_intermediate ? 4 : 5;
+        float sm = (float)scratch[6 * a.B + 0];
+        for (int j = 1; j < comps; ++j) sm += (float)scratch[6 * a.B + j];
+        sm = sm / (float)comps / (float)a.tf;
+        for (int j = 0; j < 5; ++j) a.smooth[j] = (float)scratch[6 * a.B + j];
+        a.smooth[5] = sm;
+        a.loss[0] = total + a.weight * sm;
+        __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Per pixel: dL/d(images) for both directions, and the smoothness part of dL/dflows
+// (plain stores: g_flows is fully written here; events add into it afterwards).
+__global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
+                                                        float* g_flows, int chunks) {
+    const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
+    const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
+    const int p = chunk * NT + tid;
+    if (p >= HWp) return;
+    const float g = g_loss[0];
+    const float T = (float)a.T;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
+        const float nz = ps[2], lb = ps[3];
+        const float gS = a.loss_scaling ? g / nz : g;
+        const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+        float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+        const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
+        const float dp = cp + 1e-9f, dn = cn + 1e-9f;
+        const float qp = tp / dp, qn = tn / dn;
+        const float Ap = qp / T, An = qn / T;
+        const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
+        float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
+        if (a.loss_scaling && !(cp + cn > 0.0f)) {
+            const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
+            gcp += gz;
+            gcn += gz;
+        }
+        gb[0] = gcp;
+        gb[img] = gcn;
+        gb[2 * img] = gqp / dp;
+        gb[3 * img] = gqn / dn;
+    }
+    // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
+    const int comps = a.overwrite_intermediate ? 4 : 5;
+    const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
+    const int h = p / a.W, w = p - h * a.W;
+    const bool sm = a.smoothing_mask != 0;
+    for (int t = 0; t < a.tf; ++t) {
+        const float* fx = a.flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+        const float* fy = fx + HWp;
+        const float* m = a.masks + ((int64_t)b * a.tf + t) * HWp;
+        float acc = 0.0f;
+        // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
+        auto pairgrad = [&](const float* fxa, const float* fya, const float* ma, int pa, const float* fxb,
+                            const float* fyb, const float* mb, int pb) {
+            const float dd = (fxa[pa] - fxb[pb]) + (fya[pa] - fyb[pb]);
+            const float c = charb(dd);
+            const float mk = sm ? ma[pa] * mb[pb] : 1.0f;
+            return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
+        };
+        if (w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + 1);
+        if (w >= 1) acc -= pairgrad(fx, fy, m, p - 1, fx, fy, m, p);
+        if (h + 1 < a.H) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W);
+        if (h >= 1) acc -= pairgrad(fx, fy, m, p - a.W, fx, fy, m, p);
+        if (h + 1 < a.H && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W + 1);
+        if (h >= 1 && w >= 1) acc -= pairgrad(fx, fy, m, p - a.W - 1, fx, fy, m, p);
+        if (h >= 1 && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p - a.W + 1);
+        if (h + 1 < a.H && w >= 1) acc -= pairgrad(fx, fy, m, p + a.W - 1, fx, fy, m, p);
+        if (!a.overwrite_intermediate) {
+            if (t + 1 < a.tf) {
+                const float* fx2 = fx + 2 * HWp;
+                acc += pairgrad(fx, fy, m, p, fx2, fx2 + HWp, m + HWp, p);
+            }
+            if (t >= 1) {
+                const float* fx0 = fx - 2 * HWp;
+                acc -= pairgrad(fx0, fx0 + HWp, m - HWp, p, fx, fy, m, p);
+            }
+        }
+        float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+        gf[p] = acc;
+        gf[HWp + p] = acc;
+    }
+}
+
+// Per event: gather dL/d(images) at the 4 corners of both warps, chain through the
+// bilinear weights to the warped position and the per-event flow, scatter into g_flows.
+__global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
+                                                      float* g_flows) {
+    const int64_t HWp = (int64_t)a.H * a.W;
+    const int64_t n = (int64_t)a.B * a.M;
+    const int64_t img = (int64_t)a.B * HWp;
+    for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
+        const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
+        const int k = pass_of(a.off, a.T, i);
+        const float* ev = a.events + e * 4;
+        const float ts = ev[0] + (float)k, y = ev[1], x = ev[2];
+        const int pix = (int)(y * (float)a.W + x);
+        const int kf = a.tf == 1 ? 0 : k;
+        const float* fl = a.flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+        const float fy = fl[HWp + pix], fx = fl[pix];
+        const float pm0 = a.pol[e * 2], pm1 = a.pol[e * 2 + 1];
+        float gfy = 0.0f, gfx = 0.0f;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            const float tref = d == 0 ? (float)a.T : 0.0f;
+            const float tsw = d == 0 ? ts : (float)a.T - ts;
+            Corner c[4];
+            float wy, wx;
+            warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+            const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
+            float gwy = 0.0f, gwx = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (!c[q].inb) continue;
+                const int id = c[q].idx;
+                const float gwt = (gb[id] * pm0 + gb[img + id] * pm1) +
+                                  (gb[2 * img + id] * (tsw * pm0) + gb[3 * img + id] * (tsw * pm1));
+                // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
+                const float gay = gwt * c[q].ax, gax = gwt * c[q].ay;
+                gwy += -(gay * relu_tie(1.0f - fabsf(c[q].dy))) * sgnf(c[q].dy);
+                gwx += -(gax * relu_tie(1.0f - fabsf(c[q].dx))) * sgnf(c[q].dx);
+            }
+            const float dt = tref - ts;
+            gfy += (gwy * a.flow_scaling) * dt;
+            gfx += (gwx * a.flow_scaling) * dt;
+        }
+        float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+        if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
+        if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
+    }
+}
+
+__global__ void k_iwe_corners(const float* __restrict__ events, const float* __restrict__ flow_ev, int B, int M,
+                              float tref, int H, int W, float s, int round_idx, int32_t* idx, float* wout) {
+    const int64_t n = (int64_t)B * M;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int b = (int)(e / M), i = (int)(e - (int64_t)b * M);
+        const float* ev = events + e * 4;
+        const float fy = flow_ev[e * 2], fx = flow_ev[e * 2 + 1];
+        if (round_idx) {
+            const float dt = tref - ev[0];
+            const float wy = ev[1] + (dt * fy) * s, wx = ev[2] + (dt * fx) * s;
+            const float cy = rintf(wy), cx = rintf(wx);
+            const bool inb = cy >= 0.0f && cy < (float)H && cx >= 0.0f && cx < (float)W;
+            const float m = inb ? 1.0f : 0.0f;
+            idx[(int64_t)b * M + i] = (int)((cy * m) * (float)W + cx * m);
+            wout[(int64_t)b * M + i] = 1.0f * m;
+        } else {
+            Corner c[4];
+            float wy, wx;
+            warp4(ev[0], ev[1], ev[2], fy, fx, tref, s, H, W, c, wy, wx);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                idx[(int64_t)b * 4 * M + (int64_t)q * M + i] = c[q].idx;
+                wout[(int64_t)b * 4 * M + (int64_t)q * M + i] = c[q].wt;
+            }
+        }
+    }
+}
+
+__global__ void k_iwe_interpolate(const int32_t* __restrict__ idx, const float* __restrict__ w,
+                                  const float* __restrict__ pol, int64_t pol_sb, int B, int K, int HW, float* img) {
+    const int64_t n = (int64_t)B * K;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int b = (int)(e / K), i = (int)(e - (int64_t)b * K);
+        float v = w[e];
+        if (pol) v = v * pol[(int64_t)b * pol_sb + i];
+        if (v != 0.0f) atomicAdd(img + (int64_t)b * HW + idx[e], v);
+    }
+}
+
+int grid_for(int64_t n, int per_block, int cap) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+int check_loss_args(const snnflow_iwe_loss_args* a) {
+    if (!a || a->B <= 0 || a->M < 0 || a->T <= 0 || a->T > 64 || a->H <= 0 || a->W <= 0 ||
+        !(a->tf == 1 || a->tf == a->T))
+        SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: bad shape");
+    if (!a->events || !a->pol || !a->flows || !a->masks || !a->images || !a->persample || !a->smooth || !a->loss ||
+        !a->partials || !a->counter)
+        SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: missing buffer");
+    if (6 * a->B + 5 > NT) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: batch too large (B <= 41)");
+    if (a->off[0] != 0 || a->off[a->T] != a->M) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: offsets must span [0, M]");
+    for (int k = 0; k < a->T; ++k)
+        if (a->off[k + 1] < a->off[k]) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: offsets must be non-decreasing");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int snnflow_iwe_scratch_floats(int B, int H, int W) { return 8 * B * H * W; }
+
+int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
+    if (int rc = check_loss_args(a)) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    const int64_t HWp = (int64_t)a->H * a->W;
+    hipError_t e = hipMemsetAsync(a->images, 0, sizeof(float) * 8 * a->B * HWp, s);
+    if (e != hipSuccess) SNN_FAIL((int)e, hipGetErrorString(e));
+    if (a->M > 0)
+        hipLaunchKernelGGL(k_iwe_scatter, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a);
+    const int chunks = (int)((HWp + NT - 1) / NT);
+    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows,
+                         void* stream) {
+    if (int rc = check_loss_args(a)) return rc;
+    if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
+    const hipStream_t s = (hipStream_t)stream;
+    const int64_t HWp = (int64_t)a->H * a->W;
+    const int chunks = (int)((HWp + NT - 1) / NT);
+    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows, chunks);
+    if (a->M > 0)
+        hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a, gimg,
+                           g_flows);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_iwe_corners(const float* events, const float* flow_ev, int B, int M, float tref, int H, int W,
+                        float flow_scaling, int round_idx, int32_t* idx, float* w, void* stream) {
+    if (!events || !flow_ev || !idx || !w || B <= 0 || M < 0 || H <= 0 || W <= 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "iwe_corners: bad args");
+    if (M == 0) return 0;
+    hipLaunchKernelGGL(k_iwe_corners, dim3(grid_for((int64_t)B * M, 256, 4096)), dim3(256), 0, (hipStream_t)stream,
+                       events, flow_ev, B, M, tref, H, W, flow_scaling, round_idx, idx, w);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_iwe_interpolate(const int32_t* idx, const float* w, const float* pol, int64_t pol_sb, int B, int K, int H,
+                            int W, float* img, void* stream) {
+    if (!idx || !w || !img || B <= 0 || K < 0 || H <= 0 || W <= 0) SNN_FAIL(SNNFLOW_E_ARG, "iwe_interpolate: bad args");
+    const hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(img, 0, sizeof(float) * (size_t)B * H * W, s);
+    if (e != hipSuccess) SNN_FAIL((int)e, hipGetErrorString(e));
+    if (K == 0) return 0;
+    hipLaunchKernelGGL(k_iwe_interpolate, dim3(grid_for((int64_t)B * K, 256, 4096)), dim3(256), 0, s, idx, w, pol,
+                       pol_sb, B, K, H * W, img);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

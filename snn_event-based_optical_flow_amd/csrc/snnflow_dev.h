@@ -1,0 +1,151 @@
+// Device-side building blocks shared by the snnflow HIP kernels (gfx950 / CDNA4).
+//
+// Numerics: the library is compiled with -ffp-contract=off so elementwise code
+// keeps the reference's separate multiply / add roundings; convolution
+// accumulations use explicit fmaf.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "snnflow.h"
+
+namespace snnflow {
+
+constexpr int TH = SNNFLOW_TILE_H;
+constexpr int TW = SNNFLOW_TILE_W;
+constexpr int NT = TH * TW;             // 256 threads = 4 waves, one output pixel each
+constexpr int HH = TH + 2;              // halo tile rows
+constexpr int HWD = TW + 2;             // halo tile cols
+constexpr int HN = HH * HWD;            // halo pixels (340)
+constexpr float kPiF = 3.14159265358979323846f;
+
+// LDS pixel stride (floats) for a C-channel pixel: conflict-free ds_read_b128 when
+// consecutive lanes read consecutive pixels (C=8 -> 12, 16 -> 20, 32 -> 36 dwords).
+template <int C> struct Pad { static constexpr int v = (C <= 4 || C % 4 != 0) ? C : C + 4; };
+
+// Channel-block width for vector LDS access of a C-channel pixel.
+template <int C> struct VecW { static constexpr int v = (C % 4 == 0) ? 4 : ((C % 2 == 0) ? 2 : 1); };
+
+struct Tile { int b, h0, w0; };
+
+__host__ __device__ inline int tiles_per_image(int H, int W) {
+    return ((H + TH - 1) / TH) * ((W + TW - 1) / TW);
+}
+
+// Block -> tile.  Blocks b and b+8 share an XCD under round-robin dispatch; give each
+// XCD group a contiguous range of tiles so neighbouring tiles (shared halo rows) hit
+// the same L2.  Bijective for any grid size.  Speed only, never correctness.
+__device__ inline Tile block_tile(int H, int W) {
+    const int nb = gridDim.x, bid = blockIdx.x;
+    const int q = nb / 8, r = nb % 8, x = bid % 8;
+    int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    const int tw = (W + TW - 1) / TW, th = (H + TH - 1) / TH;
+    Tile tl;
+    tl.w0 = (t % tw) * TW; t /= tw;
+    tl.h0 = (t % th) * TH;
+    tl.b = t / th;
+    return tl;
+}
+
+__device__ inline float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Per-channel LIF coefficients: I = y*alpha + shift (torch CPU BN transform order:
+// alpha = invstd*gamma, shift = bias - mean*alpha), beta clamped to [0,1].
+struct LifCoef { float alpha, shift, beta, theta; };
+
+__device__ inline LifCoef lif_coef(const snnflow_neuron& n, const float* stats, int C, int c) {
+    LifCoef k;
+    const float mean = stats[c], invstd = stats[C + c];
+    k.alpha = invstd * n.bn_weight[c];
+    k.shift = n.bn_bias[c] - mean * k.alpha;
+    k.beta = fminf(fmaxf(n.beta[c], 0.0f), 1.0f);
+    k.theta = n.threshold[c];
+    return k;
+}
+
+// snn.Leaky (0.9.4, restated: oracle/lif_ref.py LeakyRef), reset_delay=False.
+struct LifOut { float s, mout, v, mprime, I; };
+
+__device__ inline LifOut lif_step(float y, float m, const LifCoef& k, bool zero_reset) {
+    LifOut o;
+    o.I = y * k.alpha + k.shift;
+    const float r = (m - k.theta > 0.0f) ? 1.0f : 0.0f;
+    if (zero_reset) {
+        o.mprime = (1.0f - r) * m;
+        o.v = k.beta * o.mprime + o.I;
+    } else {
+        o.mprime = m;
+        o.v = (k.beta * m + o.I) - r * k.theta;
+    }
+    o.s = (o.v - k.theta > 0.0f) ? 1.0f : 0.0f;
+    const float dr = o.s - r;
+    o.mout = zero_reset ? o.v - dr * o.v : o.v - dr * k.theta;
+    return o;
+}
+
+// snntorch ATan surrogate (alpha = 2): alpha/2 / (1 + (pi/2*alpha*x)^2)
+__device__ inline float atan_sg(float x) {
+    const float u = kPiF * x;
+    return __frcp_rn(1.0f + u * u);
+}
+
+// ---------------------------------------------------------------------------
+// Deterministic grid-wide sum: every block contributes NV doubles; the last block
+// to arrive (agent-scope release/acquire ticket, MI355X guide G16) reduces all
+// contributions in fixed block order.  Returns true in the last block, with the
+// totals in `total` (LDS, NV doubles).  Leaves *counter == 0.
+// ---------------------------------------------------------------------------
+template <int NV>
+__device__ bool last_block_sum(const double* mine, double* __restrict__ partials, unsigned* counter,
+                               double* total) {
+    __shared__ double scratch[NT];
+    __shared__ int is_last;
+    const int tid = threadIdx.x, nb = gridDim.x;
+    for (int j = tid; j < NV; j += NT) partials[(size_t)blockIdx.x * NV + j] = mine[j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (t == (unsigned)(nb - 1));
+    }
+    __syncthreads();
+    if (!is_last) return false;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if constexpr (NV <= NT) {
+        constexpr int G = NT / NV;
+        const int j = tid % NV, g = tid / NV;
+        if (g < G) {
+            double s = 0.0;
+            for (int i = g; i < nb; i += G) s += partials[(size_t)i * NV + j];
+            scratch[g * NV + j] = s;
+        }
+        __syncthreads();
+        if (tid < NV) {
+            double s = 0.0;
+            for (int gg = 0; gg < G; ++gg) s += scratch[gg * NV + tid];
+            total[tid] = s;
+        }
+    } else {
+        for (int j = tid; j < NV; j += NT) {
+            double s = 0.0;
+            for (int i = 0; i < nb; ++i) s += partials[(size_t)i * NV + j];
+            total[j] = s;
+        }
+    }
+    if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return true;
+}
+
+}  // namespace snnflow

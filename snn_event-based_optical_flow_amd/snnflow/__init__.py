@@ -1,0 +1,13 @@
+"""snnflow -- MI355X-native (gfx950) LIFFireNet + event-warping hot path.
+
+Drop-in for the reference's ``models.model`` (LIFFireNet family), its spiking cells,
+``loss.flow.EventWarping`` and ``utils.iwe``; all compute runs in the HIP C-ABI library
+``libsnnflow.so`` (include/snnflow.h).  Importing fails loudly if the library is missing.
+"""
+from . import _lib  # noqa: F401  (loads libsnnflow.so or raises)
+from .cells import ConvLayer, Leaky, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
+from .loss import EventWarping
+from .model import LIFFireFlowNet, LIFFireFlowNet_short, LIFFireNet, LIFFireNet_short
+
+__all__ = ["LIFFireNet", "LIFFireNet_short", "LIFFireFlowNet", "LIFFireFlowNet_short", "SNNtorch_ConvLIF",
+           "SNNtorch_ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping"]

@@ -1,0 +1,180 @@
+"""ctypes binding of the snnflow C-ABI (include/snnflow.h).
+
+The HIP library is the product: there is no CPU fallback.  Importing this module
+fails loudly when libsnnflow.so is missing; calls fail loudly when there is no GPU.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SNNFLOW_LIB", os.path.join(_HERE, "libsnnflow.so"))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+
+TILE_H, TILE_W = 8, 32
+ABI_VERSION = 2
+
+
+class Neuron(ctypes.Structure):
+    _fields_ = [("bn_weight", P), ("bn_bias", P), ("running_mean", P), ("running_var", P),
+                ("num_batches_tracked", P), ("beta", P), ("threshold", P),
+                ("momentum", F64), ("eps", F64), ("bn_train", I32), ("zero_reset", I32)]
+
+
+class NeuronGrad(ctypes.Structure):
+    _fields_ = [("bn_weight", P), ("bn_bias", P), ("beta", P), ("threshold", P)]
+
+
+class ConvFwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32), ("lif_in", I32),
+                ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
+                ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron), ("prev_state", P),
+                ("wt_ff", P), ("wt_rec", P), ("s_prev", P), ("self", Neuron),
+                ("y", P), ("stats", P), ("partials", P), ("counter", P)]
+
+
+class LifFwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("c", I32),
+                ("y", P), ("mem", P), ("stats", P), ("n", Neuron), ("state", P),
+                ("pred_w", P), ("pred_b", P), ("flow", P)]
+
+
+class LifBwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("c", I32),
+                ("y", P), ("mem", P), ("stats", P), ("n", Neuron),
+                ("g_out", P), ("g_state", P), ("pred_w", P), ("flow", P), ("g_flow", P),
+                ("gflow_sb", I64), ("gflow_sc", I64),
+                ("g_cur", P), ("bstats", P), ("g_mem", P), ("ng", NeuronGrad), ("g_pred_w", P), ("g_pred_b", P),
+                ("accumulate", I32), ("partials", P), ("counter", P)]
+
+
+class LayerBwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
+                ("y", P), ("stats", P), ("g_cur", P), ("bstats", P), ("n", Neuron),
+                ("wt_bwd_ff", P), ("wt_bwd_rec", P), ("lif_in", I32),
+                ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
+                ("s_prev", P), ("slab_ff", P), ("slab_rec", P), ("accumulate", I32),
+                ("g_x", P), ("gxs_b", I64), ("gxs_c", I64), ("gxs_h", I64), ("gxs_w", I64),
+                ("g_state_prev", P), ("zero_mem_half", I32),
+                ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),
+                ("prev_g_state", P), ("prev_g_cur", P), ("prev_bstats", P), ("prev_ng", NeuronGrad),
+                ("prev_g_mem", P), ("partials", P), ("counter", P)]
+
+
+class SlabDesc(ctypes.Structure):
+    _fields_ = [("slab", P), ("out", P), ("elems", I32)]
+
+
+class IweLossArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("M", I32), ("T", I32), ("H", I32), ("W", I32), ("tf", I32),
+                ("events", P), ("pol", P), ("flows", P), ("masks", P), ("off", ctypes.c_int32 * 65),
+                ("flow_scaling", F32), ("weight", F32),
+                ("smoothing_mask", I32), ("overwrite_intermediate", I32), ("loss_scaling", I32),
+                ("images", P), ("persample", P), ("smooth", P), ("loss", P),
+                ("partials", P), ("counter", P)]
+
+
+EXPORTS = {
+    "snnflow_abi_version": (I32, []),
+    "snnflow_last_error": (ctypes.c_char_p, []),
+    "snnflow_conv_blocks": (I32, [I32, I32, I32]),
+    "snnflow_prep_weights": (I32, [P, I32, I32, P, P, P, P]),
+    "snnflow_conv_fwd": (I32, [ctypes.POINTER(ConvFwdArgs), P]),
+    "snnflow_lif_fwd": (I32, [ctypes.POINTER(LifFwdArgs), P]),
+    "snnflow_lif_bwd": (I32, [ctypes.POINTER(LifBwdArgs), P]),
+    "snnflow_layer_bwd": (I32, [ctypes.POINTER(LayerBwdArgs), P]),
+    "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),
+    "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
+    "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P]),
+    "snnflow_iwe_scratch_floats": (I32, [I32, I32, I32]),
+    "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
+    "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),
+    "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"snnflow HIP library not found at {LIB_PATH}; build it with "
+            "`make -C snn_event-based_optical_flow_amd/csrc` (or __graft_entry__.build()). "
+            "There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.snnflow_abi_version() != ABI_VERSION:
+        raise ImportError("snnflow ABI version mismatch; rebuild libsnnflow.so")
+    return lib
+
+
+lib = _load()
+
+
+class SnnflowError(RuntimeError):
+    pass
+
+
+def check(rc, what):
+    if rc != 0:
+        raise SnnflowError(f"{what} failed ({rc}): {lib.snnflow_last_error().decode(errors='replace')}")
+
+
+class KernelTimer:
+    """Brackets every C-ABI launch with HIP events on the launch stream (opt-in; used
+    by bench.py to time the dominant kernel live).  records: list of (name, start, end)."""
+
+    def __init__(self):
+        self.records = []
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, a, b in self.records:
+            ms = a.elapsed_time(b)
+            n, tot = out.get(name, (0, 0.0))
+            out[name] = (n + 1, tot + ms)
+        return {k: {"launches": n, "total_ms": tot, "avg_us": 1000.0 * tot / n} for k, (n, tot) in out.items()}
+
+
+TIMER = None
+
+
+def call(name, fn, *args):
+    """Launch one C-ABI entry point; raise with the library's message on failure."""
+    if TIMER is None:
+        check(fn(*args), name)
+        return
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    check(fn(*args), name)
+    b.record()
+    TIMER.records.append((name, a, b))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None):
+    if not torch.cuda.is_available():
+        raise SnnflowError("snnflow kernels need a HIP device (none visible); there is no CPU fallback")
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t, name):
+    if not t.is_cuda:
+        raise SnnflowError(f"{name} must be a HIP device tensor (got {t.device}); there is no CPU fallback")
+    if t.dtype != torch.float32:
+        raise SnnflowError(f"{name} must be float32 (got {t.dtype})")

@@ -1,0 +1,413 @@
+"""Drivers of the HIP C-ABI: the fused per-time-step LIFFireNet Function, the
+per-cell Function and their scratch workspaces.
+
+One time step of the network (reference ``models/model.py:135-207``: head, G1, R1a,
+R1b, G2, R2a, R2b, pred) is ONE autograd node here:
+
+  forward  (L+1 kernels)  conv(head) | LIF(l)+conv(l+1) ... | LIF(L-1)+pred
+  backward (L+1 kernels)  LIF(L-1)+pred bwd | BN-bwd+dgrad+wgrad(l)+LIF-bwd(l-1) ... | wgrad(head)
+
+States are the only tensors that cross time steps.  The spike halves of the
+recurrent cells' states carry gradients backward in time (the membrane half is
+detached, ``SNNtorch_spiking_submodules.py:554-556``).  Parameter gradients of all
+T steps of a truncated-BPTT window are accumulated on the device (weight
+gradients in per-block slabs, neuron/BN gradients in place) and returned once,
+by the first step of the window ("root"), so autograd performs no per-step
+gradient additions.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+_CONV_NV = 5  # partial doubles per channel (max over kernels: lif_bwd+pred = 5C + 2)
+
+
+def nhwc_state_strides(B, C, H, W):
+    """Strides of a [2,B,C,H,W] state whose storage is [2][B][H][W][C]."""
+    return (B * H * W * C, H * W * C, 1, W * C, C)
+
+
+def empty_state(B, C, H, W, device):
+    return torch.empty_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W), device=device, dtype=torch.float32)
+
+
+def as_nhwc_state(s):
+    """Any [2,B,C,H,W] state -> tensor with [2][B][H][W][C] storage (no copy if already)."""
+    two, B, C, H, W = s.shape
+    if s.stride() == nhwc_state_strides(B, C, H, W) and s.dtype == torch.float32:
+        return s
+    out = empty_state(B, C, H, W, s.device)
+    out.copy_(s)
+    return out
+
+
+def as_nhwc(t):
+    """[B,C,H,W] -> channels_last storage (no copy if already)."""
+    B, C, H, W = t.shape
+    if t.stride() == (H * W * C, 1, W * C, C) and t.dtype == torch.float32:
+        return t
+    return t.contiguous(memory_format=torch.channels_last).float()
+
+
+def neuron_struct(cell):
+    bn, lif = cell.bn, cell.lif
+    train = bn.training or not bn.track_running_stats
+    return _lib.Neuron(
+        ptr(bn.weight), ptr(bn.bias),
+        ptr(bn.running_mean) if bn.track_running_stats else None,
+        ptr(bn.running_var) if bn.track_running_stats else None,
+        ptr(bn.num_batches_tracked) if (bn.training and bn.track_running_stats) else None,
+        ptr(lif.beta), ptr(lif.threshold),
+        float(bn.momentum if bn.momentum is not None else 0.0), float(bn.eps),
+        1 if train else 0, 1 if cell.hard_reset else 0)
+
+
+class Workspace:
+    """Device scratch sized for one (B, H, W, C) problem; reused across steps."""
+
+    def __init__(self, B, H, W, C, layers, device):
+        self.key = (B, H, W, C, device)
+        self.B, self.H, self.W, self.C = B, H, W, C
+        self.nblk = lib.snnflow_conv_blocks(B, H, W)
+        self.partials = torch.empty(self.nblk * (_CONV_NV * C + 2), dtype=torch.float64, device=device)
+        self.counter = torch.zeros(16, dtype=torch.int32, device=device)
+        self.gcur = torch.empty(2, B, H, W, C, dtype=torch.float32, device=device)
+        self.bstats = torch.empty(max(layers, 1), 2, C, dtype=torch.float32, device=device)
+        self.slab_ff = []
+        self.slab_rec = []
+        self.device = device
+
+    def slabs(self, layer_shapes):
+        """layer_shapes: list of (cin, recurrent)."""
+        if len(self.slab_ff) != len(layer_shapes):
+            dev = self.device
+            self.slab_ff = [torch.empty(self.nblk, self.C * cin * 9, device=dev) for cin, _ in layer_shapes]
+            self.slab_rec = [torch.empty(self.nblk, self.C * self.C * 9, device=dev) if rec else None
+                             for _, rec in layer_shapes]
+        return self.slab_ff, self.slab_rec
+
+
+class PreppedWeights:
+    """Transposed conv weights [3][3][Cin][C] / [3][3][C][Cin] + in-place threshold clamp
+    (reference: ``threshold.data.clamp_(min=0.01)`` at every cell forward).  Cached
+    on parameter versions: recomputed after every optimizer step."""
+
+    def __init__(self):
+        self.key = None
+        self.fwd = {}
+        self.bwd = {}
+
+    def ensure(self, weights, thresholds, stream):
+        key = tuple((w.data_ptr(), w._version) for w in weights) + tuple((t.data_ptr(), t._version) for t in thresholds)
+        if key == self.key:
+            return
+        for i, w in enumerate(weights):
+            c, cin = w.shape[0], w.shape[1]
+            f = self.fwd.get(i)
+            if f is None or f.numel() != w.numel() or f.device != w.device:
+                self.fwd[i] = torch.empty(9 * cin * c, device=w.device)
+                self.bwd[i] = torch.empty(9 * cin * c, device=w.device)
+            _lib.call("prep_weights", lib.snnflow_prep_weights, ptr(w.detach().contiguous()), c, cin, ptr(self.fwd[i]), ptr(self.bwd[i]),
+                                           None, stream)
+        for t in thresholds:
+            _lib.call("threshold clamp", lib.snnflow_prep_weights, None, t.numel(), 1, None, None, ptr(t), stream)
+        self.key = key
+
+
+# ---------------------------------------------------------------------------
+# Fused time step of the LIFFireNet family
+# ---------------------------------------------------------------------------
+class FireNetEngine:
+    """Owns the cells' device-side bookkeeping for one model instance."""
+
+    def __init__(self, model):
+        self.cells = [getattr(model, name) for name, _ in model.layer_spec]
+        self.rec = [rec for _, rec in model.layer_spec]
+        self.pred = model.pred.conv2d
+        self.L = len(self.cells)
+        self.C = self.cells[0].hidden_size
+        self.ws = None
+        self.prep = PreppedWeights()
+        self.bwd_open = False
+        self.flat = None
+        self.flat_views = None
+
+    # parameter order = Function input order after the states
+    def param_list(self):
+        ps = []
+        for cell, rec in zip(self.cells, self.rec):
+            ps.append(cell.ff.weight)
+            if rec:
+                ps.append(cell.rec.weight)
+            ps += [cell.bn.weight, cell.bn.bias, cell.lif.beta, cell.lif.threshold]
+        ps += [self.pred.weight, self.pred.bias]
+        return ps
+
+    def workspace(self, B, H, W, device):
+        key = (B, H, W, self.C, device)
+        if self.ws is None or self.ws.key != key:
+            self.ws = Workspace(B, H, W, self.C, self.L, device)
+        self.ws.slabs([(c.input_size, r) for c, r in zip(self.cells, self.rec)])
+        return self.ws
+
+    def prep_weights(self, stream):
+        ws = []
+        for cell, rec in zip(self.cells, self.rec):
+            ws.append(cell.ff.weight)
+            if rec:
+                ws.append(cell.rec.weight)
+        self.prep.ensure(ws, [c.lif.threshold for c in self.cells], stream)
+        # map layer -> prepped buffers
+        fwd, bwd, i = [], [], 0
+        for rec in self.rec:
+            ff = (self.prep.fwd[i], self.prep.bwd[i])
+            i += 1
+            rc = (None, None)
+            if rec:
+                rc = (self.prep.fwd[i], self.prep.bwd[i])
+                i += 1
+            fwd.append((ff[0], rc[0]))
+            bwd.append((ff[1], rc[1]))
+        return fwd, bwd
+
+    def open_chain(self, device):
+        params = self.param_list()
+        total = sum(p.numel() for p in params)
+        self.flat = torch.empty(total, device=device)
+        views, off = [], 0
+        for p in params:
+            views.append(self.flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        self.flat_views = views
+        self.bwd_open = True
+
+    def grad_views(self):
+        """Per-layer gradient destinations inside the flat buffer."""
+        v = iter(self.flat_views)
+        layers = []
+        for rec in self.rec:
+            gff = next(v)
+            grec = next(v) if rec else None
+            gbw, gbb, gbeta, gth = next(v), next(v), next(v), next(v)
+            layers.append((gff, grec, _lib.NeuronGrad(ptr(gbw), ptr(gbb), ptr(gbeta), ptr(gth))))
+        gpw, gpb = next(v), next(v)
+        return layers, gpw, gpb
+
+
+def _x_strides(x):
+    return x.stride(0), x.stride(1), x.stride(2), x.stride(3)
+
+
+def _spk_half(state_nhwc):
+    """Spike half of a [2][B][H][W][C] state as (pointer, strides (b,c,h,w))."""
+    two, B, C, H, W = state_nhwc.shape
+    base = state_nhwc.data_ptr() + 4 * (B * H * W * C)
+    return base, (H * W * C, 1, W * C, C)
+
+
+class FireNetStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, eng, x, *rest):
+        L, C = eng.L, eng.C
+        prev = list(rest[:L])
+        B, cin0, H, W = x.shape
+        dev = x.device
+        _lib.require_device(x, "event tensor")
+        s = _lib.stream_ptr(dev)
+        ws = eng.workspace(B, H, W, dev)
+        wfwd, _ = eng.prep_weights(s)
+        cells = eng.cells
+
+        ys = torch.empty(L, B, H, W, C, device=dev)
+        stats = torch.empty(L, 2, C, device=dev)
+        states = [empty_state(B, C, H, W, dev) for _ in range(L)]
+        flow = torch.empty(B, 2, H, W, device=dev)
+
+        mem_in, s_prev, prev_nhwc = [], [], []
+        root = True
+        ext = [False] * L  # prev state requiring grad that this engine did not produce
+        for l in range(L):
+            p = prev[l]
+            if p is None:
+                cache = cells[l].lif.mem
+                mem_in.append(cache if (cache is not None and tuple(cache.shape) == (B, C, H, W)
+                                        and cache.device == dev) else None)
+                s_prev.append(None)
+                prev_nhwc.append(None)
+            else:
+                pn = as_nhwc_state(p)
+                prev_nhwc.append(pn)
+                mem_in.append(pn[0])
+                s_prev.append(pn[1] if eng.rec[l] else None)
+                ours = getattr(p.grad_fn, "eng", None) is eng
+                if eng.rec[l] and p.requires_grad and ours:
+                    root = False
+                ext[l] = p.requires_grad and not ours
+        neurons = [neuron_struct(c) for c in cells]
+        part, cnt = ptr(ws.partials), ptr(ws.counter)
+
+        # layer 0: conv(x) (+ BN statistics)
+        a = _lib.ConvFwdArgs()
+        a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin0, C, 0
+        a.x = ptr(x)
+        a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
+        a.wt_ff, a.wt_rec = ptr(wfwd[0][0]), ptr(wfwd[0][1])
+        a.s_prev = _ptr_nhwc_spk(s_prev[0])
+        a.self = neurons[0]
+        a.y, a.stats, a.partials, a.counter = ptr(ys[0]), ptr(stats[0]), part, cnt
+        _lib.call("conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
+        # layers 1..L-1: LIF(l-1) on the halo + conv(l)
+        for l in range(1, L):
+            a = _lib.ConvFwdArgs()
+            a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, C, C, 1
+            a.prev_y, a.prev_mem, a.prev_stats = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1])
+            a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
+            a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
+            a.s_prev = _ptr_t(s_prev[l])
+            a.self = neurons[l]
+            a.y, a.stats, a.partials, a.counter = ptr(ys[l]), ptr(stats[l]), part, cnt
+            _lib.call(f"conv_fwd[{l}]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
+        # LIF of the last layer + pred
+        f = _lib.LifFwdArgs()
+        f.B, f.H, f.W, f.c = B, H, W, C
+        f.y, f.mem, f.stats = ptr(ys[L - 1]), _ptr_t(mem_in[L - 1]), ptr(stats[L - 1])
+        f.n, f.state = neurons[L - 1], ptr(states[L - 1])
+        f.pred_w, f.pred_b, f.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), ptr(flow)
+        _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
+
+        for l in range(L):
+            cells[l].lif.mem = states[l][0].detach()
+
+        ctx.eng = eng
+        ctx.root = root
+        ctx.ext = ext
+        ctx.shape = (B, H, W, cin0)
+        ctx.has_prev = [p is not None for p in prev]
+        ctx.has_mem = [m is not None for m in mem_in]
+        saved = [x, ys, stats, flow] + states
+        saved += [m for m in mem_in if m is not None]
+        saved += [sp for sp in s_prev if sp is not None]
+        ctx.save_for_backward(*saved)
+        ctx.set_materialize_grads(False)
+        return (flow, *states)
+
+    @staticmethod
+    def backward(ctx, g_flow, *g_states):
+        eng = ctx.eng
+        L, C = eng.L, eng.C
+        B, H, W, cin0 = ctx.shape
+        saved = list(ctx.saved_tensors)
+        x, ys, stats, flow = saved[:4]
+        states = saved[4:4 + L]
+        rest = saved[4 + L:]
+        mem_in = []
+        for l in range(L):
+            mem_in.append(rest.pop(0) if ctx.has_mem[l] else None)
+        s_prev = []
+        for l in range(L):
+            s_prev.append(rest.pop(0) if (ctx.has_prev[l] and eng.rec[l]) else None)
+
+        dev = x.device
+        s = _lib.stream_ptr(dev)
+        ws = eng.workspace(B, H, W, dev)
+        _, wbwd = eng.prep_weights(s)
+        if not eng.bwd_open:
+            eng.open_chain(dev)
+            acc = 0
+        else:
+            acc = 1
+        glayers, gpw, gpb = eng.grad_views()
+        neurons = [neuron_struct(c) for c in eng.cells]
+        part, cnt = ptr(ws.partials), ptr(ws.counter)
+        slab_ff, slab_rec = ws.slab_ff, ws.slab_rec
+        gst = [as_nhwc_state(g) if g is not None else None for g in g_states]
+        # gradients of the previous states: the spike half of recurrent cells (rec dgrad);
+        # for states that did not come from this engine also the membrane half
+        # (v depends on the incoming membrane, SNNtorch_spiking_submodules.py:305 / snn.Leaky).
+        g_prev = [None] * L
+        for l in range(L):
+            if not (ctx.has_prev[l] and ctx.needs_input_grad[2 + l]):
+                continue
+            if ctx.ext[l]:
+                g_prev[l] = torch.zeros((2, B, C, H, W), device=dev).as_strided(
+                    (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
+            elif eng.rec[l]:
+                g_prev[l] = empty_state(B, C, H, W, dev)
+        gmem = [g_prev[l] if (g_prev[l] is not None and ctx.ext[l]) else None for l in range(L)]
+
+        # top: pred backward + LIF backward of layer L-1
+        top = L - 1
+        b = _lib.LifBwdArgs()
+        b.B, b.H, b.W, b.c = B, H, W, C
+        b.y, b.mem, b.stats, b.n = ptr(ys[top]), _ptr_t(mem_in[top]), ptr(stats[top]), neurons[top]
+        b.g_out = None
+        b.g_state = _ptr_t(gst[top])
+        b.pred_w, b.flow = ptr(eng.pred.weight), ptr(flow)
+        if g_flow is not None:
+            if g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32:
+                g_flow = g_flow.contiguous().float()
+            b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
+        b.g_cur, b.bstats = ptr(ws.gcur[top % 2]), ptr(ws.bstats[top])
+        b.g_mem = _ptr_t(gmem[top])
+        b.ng, b.g_pred_w, b.g_pred_b = glayers[top][2], ptr(gpw), ptr(gpb)
+        b.accumulate, b.partials, b.counter = acc, part, cnt
+        _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
+
+        gx = None
+        for l in range(L - 1, -1, -1):
+            a = _lib.LayerBwdArgs()
+            a.B, a.H, a.W, a.c = B, H, W, C
+            a.y, a.stats, a.g_cur, a.bstats, a.n = ptr(ys[l]), ptr(stats[l]), ptr(ws.gcur[l % 2]), ptr(ws.bstats[l]), neurons[l]
+            a.s_prev = _ptr_t(s_prev[l])
+            a.slab_ff, a.slab_rec, a.accumulate = ptr(slab_ff[l]), _ptr_t(slab_rec[l]), acc
+            a.partials, a.counter = part, cnt
+            if eng.rec[l]:
+                a.wt_bwd_rec = ptr(wbwd[l][1])
+                if g_prev[l] is not None:
+                    a.g_state_prev = ptr(g_prev[l])
+                    a.zero_mem_half = 0 if ctx.ext[l] else 1
+            if l > 0:
+                a.cin, a.lif_in = C, 1
+                a.wt_bwd_ff = ptr(wbwd[l][0])
+                a.x, (a.xs_b, a.xs_c, a.xs_h, a.xs_w) = _spk_half(states[l - 1])
+                a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
+                a.prev_g_state = _ptr_t(gst[l - 1])
+                a.prev_g_cur, a.prev_bstats, a.prev_ng = ptr(ws.gcur[(l - 1) % 2]), ptr(ws.bstats[l - 1]), glayers[l - 1][2]
+                a.prev_g_mem = _ptr_t(gmem[l - 1])
+            else:
+                a.cin, a.lif_in = cin0, 0
+                a.x = ptr(x)
+                a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
+                if ctx.needs_input_grad[1]:
+                    gx = torch.empty_like(x)
+                    a.wt_bwd_ff = ptr(wbwd[0][0])
+                    a.g_x = ptr(gx)
+                    a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
+            _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+
+        grads = [None] * len(eng.flat_views)
+        if ctx.root:
+            descs = []
+            for l in range(L):
+                gff, grec, _ = glayers[l]
+                descs.append(_lib.SlabDesc(ptr(slab_ff[l]), ptr(gff), gff.numel()))
+                if grec is not None:
+                    descs.append(_lib.SlabDesc(ptr(slab_rec[l]), ptr(grec), grec.numel()))
+            for i0 in range(0, len(descs), 16):
+                chunk = (_lib.SlabDesc * len(descs[i0:i0 + 16]))(*descs[i0:i0 + 16])
+                _lib.call("slab_reduce", lib.snnflow_slab_reduce, chunk, len(descs[i0:i0 + 16]), ws.nblk, s)
+            grads = list(eng.flat_views)
+            eng.bwd_open = False
+            eng.last_flat = eng.flat
+        return (None, gx, *g_prev, *grads)
+
+
+def _ptr_t(t):
+    return None if t is None else t.data_ptr()
+
+
+def _ptr_nhwc_spk(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,53 @@
+"""``utils/iwe.py`` API on the HIP kernels (forward only; the training path's
+gradients flow through the fused EventWarping kernels in loss.py).
+
+``get_interpolation`` returns float-valued flat indices [B, K*M, 1] and weights
+[B, K*M, 1] exactly like the reference (K = 4 bilinear corners, corner-major; K = 1
+with ``round_idx``); the integer corner computation is bit-exact with the reference
+(oracle/iwe_ref.py:warp_corners_np).
+"""
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr
+
+
+def get_interpolation(events, flow, tref, res, flow_scaling, round_idx=False):
+    """``utils/iwe.py:20-71`` (includes ``purge_unfeasible``, ``:4-17``)."""
+    _lib.require_device(events, "events")
+    ev = events.float().contiguous()
+    fl = flow.float().contiguous()
+    B, M = ev.shape[0], ev.shape[1]
+    K = 1 if round_idx else 4
+    idx = torch.empty(B, K * M, dtype=torch.int32, device=ev.device)
+    w = torch.empty(B, K * M, device=ev.device)
+    check(lib.snnflow_iwe_corners(ptr(ev), ptr(fl), B, M, float(tref), int(res[0]), int(res[1]),
+                                  float(flow_scaling), int(bool(round_idx)), ptr(idx), ptr(w),
+                                  _lib.stream_ptr(ev.device)), "iwe_corners")
+    return idx.float().unsqueeze(-1), w.unsqueeze(-1)
+
+
+def purge_unfeasible(x, res):
+    """``utils/iwe.py:4-17`` on [B, N, 2] (y, x) locations."""
+    bad = (x[:, :, 0:1] < 0) | (x[:, :, 0:1] >= res[0]) | (x[:, :, 1:2] < 0) | (x[:, :, 1:2] >= res[1])
+    mask = (~bad).to(x.dtype)
+    return x * mask, mask
+
+
+def interpolate(idx, weights, res, polarity_mask=None):
+    """``utils/iwe.py:74-93``: image of warped events [B, 1, H, W] (scatter-add)."""
+    B, K = idx.shape[0], idx.shape[1]
+    H, W = int(res[0]), int(res[1])
+    ii = idx.reshape(B, K).to(torch.int32).contiguous()
+    if not (bool((ii >= 0).all()) and bool((ii < H * W).all())):  # utils/iwe.py:87-89 (host sync, as there)
+        raise ValueError(f"Invalid idx values detected in interpolate: min={int(ii.min())}, max={int(ii.max())}")
+    ww = weights.reshape(B, K).float().contiguous()
+    pol = None
+    pol_sb = 0
+    if polarity_mask is not None:
+        pol = polarity_mask.reshape(B, K).float().contiguous()
+        pol_sb = K
+    img = torch.empty(B, 1, H, W, device=ww.device)
+    check(lib.snnflow_iwe_interpolate(ptr(ii), ptr(ww), ptr(pol), pol_sb, B, K, H, W, ptr(img),
+                                      _lib.stream_ptr(ww.device)), "iwe_interpolate")
+    return img

@@ -1,0 +1,164 @@
+"""The LIFFireNet family with the reference's module API (``models/model.py``).
+
+Same class names, constructor (``unet_kwargs`` dict of ``configs/train_SNN.yml``'s
+``model`` section), submodule names (head, G1, R1a, R1b, G2, R2a, R2b, pred),
+``states`` / ``reset_states`` / ``detach_states`` / ``mask`` / ``init_cropping`` and
+``forward(event_voxel, event_cnt, log, return_dict) -> {"flow": [B,2,H,W], "activity"}``.
+A forward call is one fused time step on the GPU (engine.FireNetStep).  If forward
+hooks are registered on a cell, the cells are called one by one instead (hooks see
+the reference's ``(spk, state)`` outputs).
+"""
+import copy
+
+import torch
+import torch.nn as nn
+
+from .cells import ConvLayer, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
+from .engine import FireNetEngine, FireNetStep
+
+
+class BaseModel(nn.Module):
+    """``models/base.py:10-31``."""
+
+    def __str__(self):
+        n = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        return super().__str__() + "\nTrainable parameters: {}".format(n)
+
+
+def copy_states(states):
+    """``models/model_util.py:96-102``: deepcopy a list of Nones, else clone."""
+    if states[0] is None:
+        return copy.deepcopy(states)
+    return [s.clone() if hasattr(s, "clone") else type(s)(t.clone() for t in s) for s in states]
+
+
+class _FireNetBase(BaseModel):
+    head_neuron = SNNtorch_ConvLIF
+    ff_neuron = SNNtorch_ConvLIF
+    rec_neuron = SNNtorch_ConvLIFRecurrent
+    residual = False
+    w_scale_pred = 0.01
+    # (cell name, uses rec_neuron)
+    layer_names = ()
+
+    def __init__(self, unet_kwargs):
+        super().__init__()
+        self.num_bins = unet_kwargs["num_bins"]
+        self.encoding = unet_kwargs["encoding"]
+        self.norm_input = unet_kwargs.get("norm_input", False)
+        self.mask = unet_kwargs["mask_output"]
+        self.exporting = unet_kwargs.get("exporting", False)
+        self.kwargs = [dict() for _ in range(self.num_recurrent_units)]
+        if isinstance(unet_kwargs.get("spiking_neuron"), dict):
+            for kw in self.kwargs:  # stored but, as in the reference, not passed to the cells
+                kw.update(unet_kwargs["spiking_neuron"])
+        C = unet_kwargs["base_num_channels"]
+        k = unet_kwargs["kernel_size"]
+        q = unet_kwargs.get("quantization", {})
+        tebn = unet_kwargs.get("tebn", {})
+        tebn = tebn.get("enabled", False) if isinstance(tebn, dict) else bool(tebn)
+        mpbn = unet_kwargs.get("mpbn", {})
+        mpbn = mpbn.get("enabled", False) if isinstance(mpbn, dict) else bool(mpbn)
+        spec = []
+        for i, (name, is_rec) in enumerate(self.layer_names):
+            cls = self.head_neuron if i == 0 else (self.rec_neuron if is_rec else self.ff_neuron)
+            cin = self.num_bins if i == 0 else C
+            setattr(self, name, cls(cin, C, k, quantization_config=q, tebn=tebn, mpbn=mpbn))
+            spec.append((name, cls is SNNtorch_ConvLIFRecurrent))
+        self.layer_spec = spec
+        self.pred = ConvLayer(C, out_channels=2, kernel_size=1, activation="tanh", w_scale=self.w_scale_pred,
+                              quantization_config=q)
+        self._engine = None
+        self.reset_states()
+
+    @property
+    def num_recurrent_units(self):
+        return len(self.layer_names)
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            object.__setattr__(self, "_engine", FireNetEngine(self))
+        return self._engine
+
+    @property
+    def states(self):
+        return copy_states(self._states)
+
+    @states.setter
+    def states(self, states):
+        self._states = states
+
+    def detach_states(self):
+        self.states = [s.detach() if s is not None else None for s in self.states]
+
+    def reset_states(self):
+        self._states = [None] * self.num_recurrent_units
+
+    def init_cropping(self, width, height):
+        pass
+
+    def _hooked(self):
+        mods = [getattr(self, n) for n, _ in self.layer_spec] + [self.pred]
+        return any(m._forward_hooks or m._forward_pre_hooks for m in mods)
+
+    def forward(self, event_voxel=None, event_cnt=None, log=False, return_dict=True):
+        if self.encoding == "voxel":
+            x = event_voxel
+        elif self.encoding == "cnt" and self.num_bins == 2:
+            x = event_cnt
+        else:
+            print("Model error: Incorrect input encoding.")
+            raise AttributeError
+        if self.norm_input:
+            nz = x != 0
+            mean, std = x[nz].mean(), x[nz].std()
+            x[nz] = (x[nz] - mean) / std
+        x = x.float()
+        if self._hooked():
+            h, outs = x, []
+            for i, (name, _) in enumerate(self.layer_spec):
+                h, self._states[i] = getattr(self, name)(h, self._states[i])
+                outs.append(h)
+            flow = self.pred(h)
+        else:
+            eng = self.engine
+            res = FireNetStep.apply(eng, x, *self._states, *eng.param_list())
+            flow, new_states = res[0], list(res[1:])
+            self._states = new_states
+            outs = [st[1] for st in new_states]
+        if not return_dict:
+            return flow
+        activity = None
+        if isinstance(log, bool) and log and not self.exporting:
+            names = ["0:input"] + [f"{i + 1}:{n}" for i, (n, _) in enumerate(self.layer_spec)]
+            names.append(f"{len(self.layer_spec) + 1}:pred")
+            activity = {n: t.detach().ne(0).float().mean().item() for n, t in zip(names, [x] + outs + [flow])}
+        return {"flow": [flow], "activity": activity}
+
+
+class LIFFireNet(_FireNetBase):
+    """``models/model.py:29-207``."""
+
+    layer_names = (("head", False), ("G1", True), ("R1a", False), ("R1b", False),
+                   ("G2", True), ("R2a", False), ("R2b", False))
+
+
+class LIFFireNet_short(_FireNetBase):
+    """``models/model.py:210-384`` (R1b and R2b removed)."""
+
+    layer_names = (("head", False), ("G1", True), ("R1a", False), ("G2", True), ("R2a", False))
+
+
+class LIFFireFlowNet(_FireNetBase):
+    """``models/model.py:387-554`` (feed-forward cells everywhere)."""
+
+    rec_neuron = SNNtorch_ConvLIF
+    layer_names = LIFFireNet.layer_names
+
+
+class LIFFireFlowNet_short(_FireNetBase):
+    """``models/model.py:557-720``."""
+
+    rec_neuron = SNNtorch_ConvLIF
+    layer_names = LIFFireNet_short.layer_names

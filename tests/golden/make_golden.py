@@ -123,12 +123,12 @@ def iwe_case(ref_iwe, out):
     np.savez_compressed(os.path.join(out, "iwe_case.npz"), **rec)
 
 
-def loss_case(ref_flow, out):
+def loss_case(ref_flow, out, overwrite=False, name="loss_case.npz"):
     """loss/flow.py EventWarping: value and dL/dflow over T windows."""
     gen = torch.Generator().manual_seed(12)
     H, W, B, N, T = 12, 20, 2, 96, 3
     config = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001,
-              "overwrite_intermediate": False}, "model": {"mask_output": True}}
+              "overwrite_intermediate": overwrite}, "model": {"mask_output": True}}
     lossf = ref_flow.EventWarping(config, "cpu")
     flows, rec = [], {"res": np.array([H, W]), "T": T}
     for t in range(T):
@@ -143,12 +143,15 @@ def loss_case(ref_flow, out):
         rec[f"mask_{t}"] = mask.numpy()
         rec[f"flow_{t}"] = f.detach().numpy().copy()
         lossf.event_flow_association([f], ev, pol, mask)
+    if overwrite:
+        lossf.overwrite_intermediate_flow([flows[-1]])
     loss = lossf()
     loss.backward()
     rec["loss"] = np.array(loss.item(), dtype=np.float32)
     for t in range(T):
-        rec[f"grad_{t}"] = flows[t].grad.numpy()
-    np.savez_compressed(os.path.join(out, "loss_case.npz"), **rec)
+        g = flows[t].grad
+        rec[f"grad_{t}"] = g.numpy() if g is not None else np.zeros_like(rec[f"flow_{t}"])
+    np.savez_compressed(os.path.join(out, name), **rec)
 
 
 def spiking_cells_case(ref_sub, out):
@@ -243,6 +246,7 @@ def main():
     torch.set_num_threads(1)
     iwe_case(ref_iwe, out)
     loss_case(ref_flow, out)
+    loss_case(ref_flow, out, overwrite=True, name="loss_case_overwrite.npz")
     spiking_cells_case(ref_sub_sp, out)
     convlayer_case(ref_sub, out)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 4)

@@ -1,0 +1,83 @@
+"""CPU-side checks of the C-ABI boundary (no GPU compute): the library loads, exports
+every entry point include/snnflow.h declares, the ctypes mirrors have the C layout
+(checked against gcc's sizeof/offsetof), and argument validation fails loudly before
+any device work."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "snnflow.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(snnflow_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from snnflow import _lib
+
+    names = _declared_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(_lib.lib, n), n
+        assert n in _lib.EXPORTS, f"{n} has no ctypes prototype"
+    assert _lib.lib.snnflow_abi_version() == _lib.ABI_VERSION
+
+
+def test_struct_layouts_match_c(tmp_path):
+    from snnflow import _lib
+
+    structs = {
+        "snnflow_neuron": _lib.Neuron, "snnflow_neuron_grad": _lib.NeuronGrad,
+        "snnflow_conv_fwd_args": _lib.ConvFwdArgs, "snnflow_lif_fwd_args": _lib.LifFwdArgs,
+        "snnflow_lif_bwd_args": _lib.LifBwdArgs, "snnflow_layer_bwd_args": _lib.LayerBwdArgs,
+        "snnflow_slab_desc": _lib.SlabDesc, "snnflow_iwe_loss_args": _lib.IweLossArgs,
+    }
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0;}")
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", str(c), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = dict(line.rsplit(" ", 1) for line in out if line)
+    for cname, py in structs.items():
+        assert int(got[f"{cname} size"]) == ctypes.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert int(got[f"{cname}.{fname}"]) == getattr(py, fname).offset, f"{cname}.{fname}"
+
+
+def test_argument_validation_without_gpu():
+    from snnflow import _lib
+
+    lib = _lib.lib
+    a = _lib.ConvFwdArgs()
+    assert lib.snnflow_conv_fwd(ctypes.byref(a), None) == -1
+    assert b"conv_fwd" in lib.snnflow_last_error()
+    a.B, a.H, a.W, a.c, a.cin = 1, 8, 8, 7, 2
+    a.wt_ff = a.y = a.stats = a.x = 1
+    assert lib.snnflow_conv_fwd(ctypes.byref(a), None) == -2  # no kernel for c=7
+    e = _lib.IweLossArgs()
+    assert lib.snnflow_iwe_loss_fwd(ctypes.byref(e), None) == -1
+    assert lib.snnflow_conv_blocks(8, 128, 128) == 8 * 16 * 4
+    assert lib.snnflow_slab_reduce(None, 1, 1, None) == -1
+
+
+def test_product_path_refuses_cpu_tensors():
+    import torch
+
+    import snnflow
+    from oracle import lif_ref
+
+    model = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8))
+    with pytest.raises(snnflow._lib.SnnflowError):
+        model(None, torch.zeros(1, 2, 16, 16))
