@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 2
+#define SNNFLOW_ABI_VERSION 3
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -61,56 +61,70 @@ typedef struct snnflow_neuron {
 int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* wt_bwd,
                          float* threshold, void* stream);
 
-/* ---- forward: [LIF of layer l on a halo tile] + conv3x3(layer l+1) + BN statistics
+/* Batch-statistics accumulators.  BatchNorm in train mode needs sums over (B,H,W)
+ * between the producing conv and the consuming LIF.  Each producer block adds its
+ * partial sums with fp64 atomics into an accumulator (one wave instruction per
+ * block); the next kernel in the chain derives the statistics in its prologue.  An
+ * accumulator must be zero when its producer starts: kernels zero (block 0) the
+ * accumulators named in `zero0`/`zero1` (`zero_n` doubles each), which the caller
+ * chooses among accumulators already consumed by an earlier kernel of the chain.
+ * fp64 accumulation makes the result independent of block order below fp32 resolution. */
+
+/* ---- forward: [LIF of layer l on a halo tile] + conv3x3(layer l+1) [+ BN batch sums]
  * Replaces, per time step, `lif(bn(...))` of layer l fused with `ff(input_)`
- * [+ `rec(prev_spk)`] of layer l+1 and the batch-stat part of its `bn`
+ * [+ `rec(prev_spk)`] of layer l+1 and the batch-sum part of its `bn`
  * (SNNtorch_spiking_submodules.py:289-305 and :521-550).
  * lif_in = 0: x is a strided tensor (e.g. event_cnt NCHW) with cin channels.
  * lif_in = 1: the input spikes are computed from the previous layer's pre-BN conv
- *             output prev_y (NHWC), its membrane prev_mem (NULL = zeros) and
- *             prev_stats [2][cin] (mean, invstd); prev_state [2][B][H][W][cin]
- *             receives (mem_out, spk) of the previous layer. */
+ *             output prev_y (NHWC), its membrane prev_mem (NULL = zeros) and its batch
+ *             sums prev_acc [2][cin] (train) or running stats (eval); block 0 writes
+ *             prev_stats [2][cin] (mean, invstd) and updates the running statistics;
+ *             prev_state [2][B][H][W][cin] receives (mem_out, spk) of the previous layer. */
 typedef struct snnflow_conv_fwd_args {
     int B, H, W, cin, c;
     int lif_in;
     const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* lif_in == 0 */
-    const float* prev_y; const float* prev_mem; const float* prev_stats;  /* lif_in == 1 */
+    const float* prev_y; const float* prev_mem;        /* lif_in == 1 */
+    const double* prev_acc; float* prev_stats;
     snnflow_neuron prev; float* prev_state;
     const float* wt_ff;         /* [3][3][cin][c]                      */
     const float* wt_rec;        /* [3][3][c][c] or NULL (feed-forward) */
     const float* s_prev;        /* NHWC [B][H][W][c] previous-step spikes; NULL = zeros */
-    snnflow_neuron self;        /* BN of this layer (running stats / train flag) */
     float* y;                   /* out NHWC [B][H][W][c] pre-BN current           */
-    float* stats;               /* out [2][c] (mean, invstd) for the LIF of this layer */
-    double* partials;           /* scratch >= snnflow_conv_blocks(B,H,W) * 2c doubles */
-    unsigned* counter;          /* scratch, zero on first use, left zero           */
+    double* acc;                /* += [2][c] (sum y, sum y^2); NULL = no batch sums (eval) */
+    double* zero0; double* zero1; int zero_n;
 } snnflow_conv_fwd_args;
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream);
 int snnflow_conv_blocks(int B, int H, int W);
 
-/* ---- forward: LIF of the last layer [+ pred ConvLayer(C->2,1x1,bias)+tanh]
+/* ---- forward: LIF of a layer [+ pred ConvLayer(C->2,1x1,bias)+tanh]
  * Replaces `lif(bn(.))` (SNNtorch_spiking_submodules.py:293-320) and
  * `pred` (models/submodules.py:96-113, models/model.py:182). */
 typedef struct snnflow_lif_fwd_args {
     int B, H, W, c;
-    const float* y; const float* mem; const float* stats;
+    const float* y; const float* mem;
+    const double* acc;          /* [2][c] batch sums (train) */
+    float* stats;               /* out [2][c] (mean, invstd) */
     snnflow_neuron n; float* state;
     const float* pred_w;        /* [2][c] or NULL (no pred) */
     const float* pred_b;        /* [2] */
     float* flow;                /* NCHW [B][2][H][W] */
+    double* zero0; double* zero1; int zero_n;
 } snnflow_lif_fwd_args;
 int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream);
 
-/* Gradient accumulators of one layer's neuron parameters (fp32, [C] each). */
+/* Gradient destinations of one layer's neuron parameters (fp32, [C] each). */
 typedef struct snnflow_neuron_grad {
     float* bn_weight; float* bn_bias; float* beta; float* threshold;
 } snnflow_neuron_grad;
 
+/* Number of doubles of a backward accumulator for c channels (3c LIF/BN sums + 2c+2 pred). */
+#define SNNFLOW_BWD_ACC(c) (5 * (c) + 2)
+
 /* ---- backward of the top layer: [pred backward] + LIF/ATan surrogate backward
  * g_s = g_out + g_state_spk + pred_w^T (g_flow * (1 - flow^2)); g_v = g_s * sg(v - theta).
- * Writes g_cur (= dL/d BN-output, NHWC) and bstats [2][c] (sum g, sum (y-mean) g)
- * for the BatchNorm backward, and accumulates (accumulate=1) or writes (0) the
- * neuron-parameter gradients (and pred gradients). */
+ * Writes g_cur (= dL/d BN-output, NHWC) [and g_mem = dL/d membrane input] and adds
+ * (sum g, sum (y-mean) g, sum g*m') [and the pred weight/bias sums] into acc. */
 typedef struct snnflow_lif_bwd_args {
     int B, H, W, c;
     const float* y; const float* mem; const float* stats; snnflow_neuron n;
@@ -118,40 +132,42 @@ typedef struct snnflow_lif_bwd_args {
     const float* g_state;       /* [2][B][H][W][c] grad of the state output or NULL */
     const float* pred_w; const float* flow; const float* g_flow;  /* pred or NULL    */
     int64_t gflow_sb, gflow_sc; /* element strides of g_flow (batch, channel); HW dense */
-    float* g_cur; float* bstats;
+    float* g_cur;
     float* g_mem;               /* NHWC grad of the membrane input (beta*(1-r)*g_v) or NULL */
-    snnflow_neuron_grad ng; float* g_pred_w; float* g_pred_b;
-    int accumulate;
-    double* partials; unsigned* counter;
+    double* acc;                /* += SNNFLOW_BWD_ACC(c) doubles */
+    double* zero0; double* zero1; int zero_n;
 } snnflow_lif_bwd_args;
 int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream);
 
 /* ---- backward of one layer: BN backward + conv dgrad/wgrad of layer l
  * [+ LIF backward of layer l-1 on the dgrad result] (the reverse of
- * snnflow_conv_fwd).  Weight gradients go to per-block slabs
- * (snnflow_conv_blocks() x c*cin*9 floats), written or accumulated across
- * time steps; snnflow_slab_reduce turns them into gradients. */
+ * snnflow_conv_fwd).  Block 0 turns acc_in into layer l's neuron-parameter
+ * gradients (and pred gradients when has_pred), written (accumulate=0) or added.
+ * Weight gradients go to per-block slabs (snnflow_conv_blocks() x c*cin*9 floats),
+ * written or accumulated across time steps; snnflow_slab_reduce sums them. */
 typedef struct snnflow_layer_bwd_args {
     int B, H, W, cin, c;
-    const float* y; const float* stats; const float* g_cur; const float* bstats;
-    snnflow_neuron n;           /* BN parameters of layer l */
+    const float* y; const float* stats; const float* g_cur;
+    const double* acc_in;       /* SNNFLOW_BWD_ACC(c) sums of layer l's LIF backward */
+    snnflow_neuron n;           /* BN / neuron parameters of layer l */
+    snnflow_neuron_grad ng;
+    int has_pred; float* g_pred_w; float* g_pred_b;
+    int accumulate;
     const float* wt_bwd_ff;     /* [3][3][c][cin]  (NULL: no input gradient)        */
     const float* wt_bwd_rec;    /* [3][3][c][c] or NULL                             */
-    /* input of layer l (for wgrad): strided x (lif_in=0) or prev layer spikes      */
     int lif_in;
-    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* input of layer l (wgrad)   */
     const float* s_prev;        /* NHWC previous-step spikes of layer l or NULL     */
-    float* slab_ff; float* slab_rec; int accumulate;
-    /* outputs */
+    float* slab_ff; float* slab_rec;
     float* g_x; int64_t gxs_b, gxs_c, gxs_h, gxs_w;   /* lif_in=0: input gradient (strided) or NULL */
     float* g_state_prev;        /* [2][B][H][W][c] grad of the previous state (rec) or NULL */
-    int zero_mem_half;          /* 1: Stage B also zero-fills the membrane half of g_state_prev */
+    int zero_mem_half;          /* 1: also zero-fill the membrane half of g_state_prev */
     /* lif_in = 1: LIF backward of layer l-1 */
     const float* prev_y; const float* prev_mem; const float* prev_stats; snnflow_neuron prev;
     const float* prev_g_state;  /* [2][B][H][W][cin] or NULL */
-    float* prev_g_cur; float* prev_bstats; snnflow_neuron_grad prev_ng;
-    float* prev_g_mem;          /* NHWC grad of layer l-1's membrane input or NULL */
-    double* partials; unsigned* counter;
+    float* prev_g_cur; float* prev_g_mem;
+    double* acc_out;            /* += SNNFLOW_BWD_ACC(cin) sums for layer l-1 */
+    double* zero0; double* zero1; int zero_n;
 } snnflow_layer_bwd_args;
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
 
@@ -173,17 +189,17 @@ typedef struct snnflow_iwe_loss_args {
     float flow_scaling, weight;
     int smoothing_mask, overwrite_intermediate, loss_scaling;
     float* images;              /* scratch [2 dir][4 img][B][H*W]: cnt+, cnt-, ts+, ts- */
+    double* acc;                /* scratch [6*B + 5] sums (zeroed by snnflow_iwe_loss_fwd) */
     float* persample;           /* scratch [2 dir][B][4]: S+, S-, nz, loss_b          */
     float* smooth;              /* scratch [8]                                         */
     float* loss;                /* out [1]                                             */
-    double* partials; unsigned* counter;
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
 /* g_loss: device scalar; g_flows out [B][T][2][H][W] (fully written). gimg scratch
  * like images. */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
                          float* g_flows, void* stream);
-int snnflow_iwe_scratch_floats(int B, int H, int W);
+int snnflow_iwe_scratch_floats(int B, int H, int W);  /* images floats; acc must directly follow */
 
 /* utils/iwe.py:20-71 get_interpolation (+ purge_unfeasible :4-17) for one pass:
  * idx out [B][K*M] int32 (corner-major, K=4 bilinear / 1 rounded), w out [B][K*M]. */

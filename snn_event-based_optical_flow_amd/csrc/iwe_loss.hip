@@ -66,6 +66,8 @@ __device__ inline float sgnf(float d) { return d > 0.0f ? 1.0f : (d < 0.0f ? -1.
 
 // images layout: [dir 2][img 4][B][HW], img = cnt+, cnt-, ts+, ts-
 __global__ __launch_bounds__(NT) void k_iwe_scatter(snnflow_iwe_loss_args a) {
+    if (blockIdx.x == 0)
+        for (int j = threadIdx.x; j < 6 * a.B + 5; j += NT) a.acc[j] = 0.0;
     const int64_t HWp = (int64_t)a.H * a.W;
     const int64_t n = (int64_t)a.B * a.M;
     const int64_t img = (int64_t)a.B * HWp;
@@ -137,13 +139,12 @@ __device__ inline SmoothTerms smooth_at(const snnflow_iwe_loss_args& a, int b, i
     return r;
 }
 
-// Per pixel: IWE loss terms for both directions + smoothness; last block finalises.
-// blocks: B * chunks (each block covers NT pixels of one sample).
+// Per pixel: IWE loss terms for both directions + smoothness, summed per block and
+// added (fp64 atomics) into acc[6*B + 5]: per sample {S+, S-, nz} x {fw, bw}, then the
+// five smoothness sums.  blocks: B * chunks (each block covers NT pixels of one sample).
 __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks) {
     constexpr int NV = 11;
     __shared__ float red[4][NV];
-    __shared__ double scratch[NT];
-    __shared__ int is_last;
     const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
@@ -176,61 +177,36 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
         if (lane == 0) red[wv][j] = s;
     }
     __syncthreads();
-    if (tid < NV)
-        a.partials[(int64_t)blockIdx.x * NV + tid] =
-            (((double)red[0][tid] + (double)red[1][tid]) + (double)red[2][tid]) + (double)red[3][tid];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = (t == gridDim.x - 1);
+    if (tid < NV) {
+        const double s = (((double)red[0][tid] + (double)red[1][tid]) + (double)red[2][tid]) + (double)red[3][tid];
+        atomicAdd(a.acc + (tid < 6 ? 6 * b + tid : 6 * a.B + (tid - 6)), s);
     }
-    __syncthreads();
-    if (!is_last) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    // per-sample sums (6 per sample) and smoothness sums (5), fixed block order
-    for (int j = tid; j < 6 * a.B + 5; j += NT) {
-        double s = 0.0;
-        if (j < 6 * a.B) {
-            const int bb = j / 6, jj = j - bb * 6;
-            for (int c = 0; c < chunks; ++c) s += a.partials[((int64_t)bb * chunks + c) * NV + jj];
-        } else {
-            const int jj = 6 + (j - 6 * a.B);
-            for (int blk = 0; blk < (int)gridDim.x; ++blk) s += a.partials[(int64_t)blk * NV + jj];
+}
+
+// loss = sum_b (S+ + S-)_fw / nz_fw + ... (loss/flow.py:219-261) + weight * smoothness.
+__global__ void k_iwe_finalize(snnflow_iwe_loss_args a) {
+    if (threadIdx.x != 0) return;
+    float total = 0.0f;
+    for (int d = 0; d < 2; ++d) {
+        float dir = 0.0f;
+        for (int bb = 0; bb < a.B; ++bb) {
+            const float sp = (float)a.acc[6 * bb + 3 * d], sn = (float)a.acc[6 * bb + 3 * d + 1];
+            const float nz = (float)a.acc[6 * bb + 3 * d + 2];
+            float lb = sp + sn;
+            if (a.loss_scaling) lb = lb / nz;
+            float* ps = a.persample + ((int64_t)d * a.B + bb) * 4;
+            ps[0] = sp; ps[1] = sn; ps[2] = nz; ps[3] = lb;
+            dir += lb;
         }
-        scratch[j < NT ? j : 0] = s;  // (6B+5 <= NT enforced on the host)
+        total += dir;
     }
-    __syncthreads();
-    if (tid == 0) {
-        float total = 0.0f;
-        for (int d = 0; d < 2; ++d) {
-            float dir = 0.0f;
-            for (int bb = 0; bb < a.B; ++bb) {
-                const float sp = (float)scratch[6 * bb + 3 * d], sn = (float)scratch[6 * bb + 3 * d + 1];
-                const float nz = (float)scratch[6 * bb + 3 * d + 2];
-                float lb = sp + sn;
-                if (a.loss_scaling) lb = lb / nz;
-                float* ps = a.persample + ((int64_t)d * a.B + bb) * 4;
-                ps[0] = sp; ps[1] = sn; ps[2] = nz; ps[3] = lb;
-                dir += lb;
-            }
-            total += dir;
-        }
-        const int comps = a.overwrite_intermediate ? 4 : 5;
-        float sm = (float)scratch[6 * a.B + 0];
-        for (int j = 1; j < comps; ++j) sm += (float)scratch[6 * a.B + j];
-        sm = sm / (float)comps / (float)a.tf;
-        for (int j = 0; j < 5; ++j) a.smooth[j] = (float)scratch[6 * a.B + j];
-        a.smooth[5] = sm;
-        a.loss[0] = total + a.weight * sm;
-        __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const int comps = a.overwrite_intermediate ? 4 : 5;
+    float sm = (float)a.acc[6 * a.B + 0];
+    for (int j = 1; j < comps; ++j) sm += (float)a.acc[6 * a.B + j];
+    sm = sm / (float)comps / (float)a.tf;
+    for (int j = 0; j < 5; ++j) a.smooth[j] = (float)a.acc[6 * a.B + j];
+    a.smooth[5] = sm;
+    a.loss[0] = total + a.weight * sm;
 }
 
 // Per pixel: dL/d(images) for both directions, and the smoothness part of dL/dflows
@@ -406,10 +382,9 @@ int check_loss_args(const snnflow_iwe_loss_args* a) {
     if (!a || a->B <= 0 || a->M < 0 || a->T <= 0 || a->T > 64 || a->H <= 0 || a->W <= 0 ||
         !(a->tf == 1 || a->tf == a->T))
         SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: bad shape");
-    if (!a->events || !a->pol || !a->flows || !a->masks || !a->images || !a->persample || !a->smooth || !a->loss ||
-        !a->partials || !a->counter)
+    if (!a->events || !a->pol || !a->flows || !a->masks || !a->images || !a->acc || !a->persample || !a->smooth ||
+        !a->loss)
         SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: missing buffer");
-    if (6 * a->B + 5 > NT) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: batch too large (B <= 41)");
     if (a->off[0] != 0 || a->off[a->T] != a->M) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: offsets must span [0, M]");
     for (int k = 0; k < a->T; ++k)
         if (a->off[k + 1] < a->off[k]) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: offsets must be non-decreasing");
@@ -428,10 +403,10 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     const int64_t HWp = (int64_t)a->H * a->W;
     hipError_t e = hipMemsetAsync(a->images, 0, sizeof(float) * 8 * a->B * HWp, s);
     if (e != hipSuccess) SNN_FAIL((int)e, hipGetErrorString(e));
-    if (a->M > 0)
-        hipLaunchKernelGGL(k_iwe_scatter, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a);
+    hipLaunchKernelGGL(k_iwe_scatter, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a);
     const int chunks = (int)((HWp + NT - 1) / NT);
     hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
+    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(64), 0, s, *a);
     SNN_CHECK_LAUNCH();
     return 0;
 }

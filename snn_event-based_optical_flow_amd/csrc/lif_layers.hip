@@ -92,7 +92,7 @@ __device__ inline void conv_acc(const float* tile, const float* __restrict__ wt,
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const float* xp = tile + ((ty + ky) * HWD + (tx + kx)) * P;
-            const float* wk = wt + (ky * 3 + kx) * CIN * C;
+            const cfloat_ptr wk = as_const(wt) + (ky * 3 + kx) * CIN * C;
 #pragma unroll(CIN <= 8 ? CIN : 1)
             for (int ci = 0; ci < CIN; ci += VW) {
                 float xs[VW];
@@ -125,7 +125,7 @@ __device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ w
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const float* gp = gtile + ((ty + 2 - ky) * HWD + (tx + 2 - kx)) * P;
-            const float* wk = wd + (ky * 3 + kx) * C * CIN;
+            const cfloat_ptr wk = as_const(wd) + (ky * 3 + kx) * C * CIN;
 #pragma unroll(C <= 8 ? C : 1)
             for (int co = 0; co < C; co += 4) {
                 const float4 v = *reinterpret_cast<const float4*>(gp + co);
@@ -226,49 +226,6 @@ __device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ s
     }
 }
 
-// Block-level sum of NV per-thread floats -> mine[NV] (double), fixed order.
-template <int NV>
-__device__ void block_partial(const float (&v)[NV], double* mine) {
-    __shared__ float red[4][NV];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-        const float s = wave_sum(v[j]);
-        if (lane == 0) red[wv][j] = s;
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < NV; j += NT)
-        mine[j] = (((double)red[0][j] + (double)red[1][j]) + (double)red[2][j]) + (double)red[3][j];
-    __syncthreads();
-}
-
-// BatchNorm batch statistics -> stats (mean, invstd) + running-stat update.
-__device__ void finalize_bn(const snnflow_neuron& n, const double* total, int C, double N, float* stats) {
-    const int c = threadIdx.x;
-    if (c < C) {
-        const double mean = total[c] / N;
-        double var = total[C + c] / N - mean * mean;
-        if (var < 0.0) var = 0.0;
-        stats[c] = (float)mean;
-        stats[C + c] = (float)(1.0 / sqrt(var + n.eps));
-        if (n.running_mean) {
-            const double unb = N > 1.0 ? var * N / (N - 1.0) : var;
-            n.running_mean[c] = (float)(n.momentum * mean + (1.0 - n.momentum) * (double)n.running_mean[c]);
-            n.running_var[c] = (float)(n.momentum * unb + (1.0 - n.momentum) * (double)n.running_var[c]);
-        }
-    }
-    if (c == 0 && n.num_batches_tracked) n.num_batches_tracked[0] += 1;
-}
-
-// Eval-mode statistics from running stats.
-__device__ void eval_stats(const snnflow_neuron& n, int C, float* stats) {
-    const int c = threadIdx.x;
-    if (c < C) {
-        stats[c] = n.running_mean[c];
-        stats[C + c] = (float)(1.0 / sqrt((double)n.running_var[c] + n.eps));
-    }
-}
-
 // dL/dm of the membrane input: v = beta*((1-r)*m) + I (zero reset) or beta*m + I - r*theta;
 // r = H(m - theta) is detached (snntorch mem_reset).
 __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_reset) {
@@ -278,16 +235,93 @@ __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_
     return gmp * (1.0f - r);
 }
 
-// LIF-backward finalize: bstats (sum g, sum (y-mean) g) and neuron-parameter grads.
-__device__ void finalize_lif_bwd(const snnflow_neuron& n, const float* stats, const double* total, int C,
-                                 float* bstats, const snnflow_neuron_grad& ng, int accumulate) {
+// Block-level sum of NV per-thread floats, then one fp64 atomic add per value into
+// acc (the block's partial; NV <= NT values issued by consecutive lanes).
+template <int NV>
+__device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
+    __shared__ float red[4][NV];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const float s = wave_sum(v[j]);
+        if (lane == 0) red[wv][j] = s;
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < NV; j += NT)
+        atomicAdd(acc + j, (((double)red[0][j] + (double)red[1][j]) + (double)red[2][j]) + (double)red[3][j]);
+}
+
+// Block 0 zeroes accumulators already consumed by an earlier kernel of the chain.
+__device__ inline void zero_consumed(double* z0, double* z1, int n) {
+    if (blockIdx.x != 0) return;
+    for (int j = threadIdx.x; j < n; j += NT) {
+        if (z0) z0[j] = 0.0;
+        if (z1) z1[j] = 0.0;
+    }
+}
+
+// BatchNorm statistics of channel c from batch sums (train) or running stats (eval):
+// mean = S/N, var = SS/N - mean^2 (biased), invstd = 1/sqrt(var + eps) in fp64.
+struct BnStat { float mean, invstd; double dmean, dvar; };
+
+__device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* acc, int C, int c, double N) {
+    BnStat st;
+    if (n.bn_train) {
+        st.dmean = acc[c] / N;
+        st.dvar = acc[C + c] / N - st.dmean * st.dmean;
+        if (st.dvar < 0.0) st.dvar = 0.0;
+        st.mean = (float)st.dmean;
+        st.invstd = (float)(1.0 / sqrt(st.dvar + n.eps));
+    } else {
+        st.dmean = n.running_mean[c];
+        st.dvar = n.running_var[c];
+        st.mean = n.running_mean[c];
+        st.invstd = (float)(1.0 / sqrt((double)n.running_var[c] + n.eps));
+    }
+    return st;
+}
+
+// Prologue of a LIF consumer: per-channel coefficients in LDS; block 0 also stores
+// (mean, invstd) for the backward pass and performs the running-stat update
+// (momentum, unbiased variance) and num_batches_tracked += 1 of torch's BatchNorm2d.
+__device__ void lif_prologue(const snnflow_neuron& n, const double* acc, int C, double N, float* stats_out,
+                             LifCoef* coef, float* mean_out) {
     const int c = threadIdx.x;
     if (c < C) {
-        const double gsum = total[c], dotp = total[C + c], gbm = total[2 * C + c];
-        bstats[c] = (float)gsum;
-        bstats[C + c] = (float)dotp;
-        const float invstd = stats[C + c];
-        const float gw = (float)(dotp * (double)invstd);
+        const BnStat st = bn_stat(n, acc, C, c, N);
+        LifCoef k;
+        k.alpha = st.invstd * n.bn_weight[c];
+        k.shift = n.bn_bias[c] - st.mean * k.alpha;
+        k.beta = fminf(fmaxf(n.beta[c], 0.0f), 1.0f);
+        k.theta = n.threshold[c];
+        coef[c] = k;
+        if (mean_out) mean_out[c] = st.mean;
+        if (blockIdx.x == 0) {
+            if (stats_out) {
+                stats_out[c] = st.mean;
+                stats_out[C + c] = st.invstd;
+            }
+            if (n.bn_train && n.running_mean) {
+                const double unb = N > 1.0 ? st.dvar * N / (N - 1.0) : st.dvar;
+                n.running_mean[c] = (float)(n.momentum * st.dmean + (1.0 - n.momentum) * (double)n.running_mean[c]);
+                n.running_var[c] = (float)(n.momentum * unb + (1.0 - n.momentum) * (double)n.running_var[c]);
+            }
+        }
+    }
+    if (c == 0 && blockIdx.x == 0 && n.bn_train && n.num_batches_tracked) n.num_batches_tracked[0] += 1;
+}
+
+// Layer-l gradients of (gamma, bn bias, beta, threshold) [and pred] from the LIF-backward
+// sums: gamma = dotp*invstd, bias = sum g, theta = -sum g, beta = sum g*m' (0 <= beta <= 1)
+// (torch batch_norm_cpu_backward; snntorch Leaky; clamp backward passes on [0,1]).
+__device__ void neuron_grads(const snnflow_neuron& n, const float* stats, const double* acc, int C,
+                             const snnflow_neuron_grad& ng, int accumulate, int has_pred, float* g_pred_w,
+                             float* g_pred_b) {
+    if (blockIdx.x != 0) return;
+    const int c = threadIdx.x;
+    if (c < C) {
+        const double gsum = acc[c], dotp = acc[C + c], gbm = acc[2 * C + c];
+        const float gw = (float)(dotp * (double)stats[C + c]);
         const float gb = (float)gsum;
         const float gth = -(float)gsum;
         const float be = n.beta[c];
@@ -296,6 +330,13 @@ __device__ void finalize_lif_bwd(const snnflow_neuron& n, const float* stats, co
             ng.bn_weight[c] += gw; ng.bn_bias[c] += gb; ng.threshold[c] += gth; ng.beta[c] += gbe;
         } else {
             ng.bn_weight[c] = gw; ng.bn_bias[c] = gb; ng.threshold[c] = gth; ng.beta[c] = gbe;
+        }
+    }
+    if (has_pred) {
+        for (int j = threadIdx.x; j < 2 * C + 2; j += NT) {
+            const float g = (float)acc[3 * C + j];
+            float* dst = (j < 2 * C) ? g_pred_w + j : g_pred_b + (j - 2 * C);
+            *dst = accumulate ? *dst + g : g;
         }
     }
 }
@@ -325,14 +366,14 @@ __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
     constexpr int PMAX = (REC && PC > PI_) ? PC : PI_;
     __shared__ __attribute__((aligned(16))) float tile[HN * PMAX];
     __shared__ LifCoef coef[LIF_IN ? CIN : 1];
-    __shared__ double mine[2 * C], total[2 * C];
 
     const int tid = threadIdx.x, ty = tid / TW, tx = tid - ty * TW;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
+    zero_consumed(a.zero0, a.zero1, a.zero_n);
 
     if constexpr (LIF_IN) {
-        if (tid < CIN) coef[tid] = lif_coef(a.prev, a.prev_stats, CIN, tid);
+        lif_prologue(a.prev, a.prev_acc, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
         __syncthreads();
         // LIF of the previous layer over the halo tile; interior pixels also write its state.
         const bool zr = a.prev.zero_reset != 0;
@@ -398,28 +439,24 @@ __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
         for (int co = 0; co < C; co += 4)
             *reinterpret_cast<float4*>(yp + co) = make_float4(y[co], y[co + 1], y[co + 2], y[co + 3]);
     }
-
-    if (!a.self.bn_train) {
-        if (blockIdx.x == 0) eval_stats(a.self, C, a.stats);
-        return;
-    }
-    float v[2 * C];
+    if (a.acc) {
+        float v[2 * C];
 #pragma unroll
-    for (int co = 0; co < C; ++co) {
-        const float yy = in ? y[co] : 0.0f;
-        v[co] = yy;
-        v[C + co] = yy * yy;
+        for (int co = 0; co < C; ++co) {
+            const float yy = in ? y[co] : 0.0f;
+            v[co] = yy;
+            v[C + co] = yy * yy;
+        }
+        block_atomic_sum<2 * C>(v, a.acc);
     }
-    block_partial<2 * C>(v, mine);
-    if (last_block_sum<2 * C>(mine, a.partials, a.counter, total))
-        finalize_bn(a.self, total, C, (double)a.B * H * W, a.stats);
 }
 
 template <int C, bool PRED>
 __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
     __shared__ LifCoef coef[C];
     const int tid = threadIdx.x;
-    if (tid < C) coef[tid] = lif_coef(a.n, a.stats, C, tid);
+    zero_consumed(a.zero0, a.zero1, a.zero_n);
+    lif_prologue(a.n, a.acc, C, (double)a.B * a.H * a.W, a.stats, coef, nullptr);
     __syncthreads();
     const bool zr = a.n.zero_reset != 0;
     const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane = npix * C;
@@ -455,8 +492,8 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
     constexpr int NV = 3 * C + (PRED ? 2 * C + 2 : 0);
     __shared__ LifCoef coef[C];
     __shared__ float meanv[C];
-    __shared__ double mine[NV], total[NV];
     const int tid = threadIdx.x;
+    zero_consumed(a.zero0, a.zero1, a.zero_n);
     if (tid < C) {
         coef[tid] = lif_coef(a.n, a.stats, C, tid);
         meanv[tid] = a.stats[tid];
@@ -515,17 +552,7 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
             v[5 * C + 1] += gpre[1];
         }
     }
-    block_partial<NV>(v, mine);
-    if (last_block_sum<NV>(mine, a.partials, a.counter, total)) {
-        finalize_lif_bwd(a.n, a.stats, total, C, a.bstats, a.ng, a.accumulate);
-        if constexpr (PRED) {
-            for (int j = tid; j < 2 * C + 2; j += NT) {
-                const float g = (float)total[3 * C + j];
-                float* dst = (j < 2 * C) ? a.g_pred_w + j : a.g_pred_b + (j - 2 * C);
-                *dst = a.accumulate ? *dst + g : g;
-            }
-        }
-    }
+    block_atomic_sum<NV>(v, a.acc);
 }
 
 template <int CIN, int C, bool LIF_IN, bool REC>
@@ -542,12 +569,14 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
     __shared__ LifCoef pcoef[LIF_IN ? CIN : 1];
     __shared__ float pmean[LIF_IN ? CIN : 1];
     constexpr int NVP = LIF_IN ? 3 * CIN : 1;
-    __shared__ double mine[NVP], total[NVP];
 
     const int tid = threadIdx.x, ty = tid / TW, tx = tid - ty * TW;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
-    const float nf = (float)((int64_t)a.B * H * W);
+    const double N = (double)a.B * H * W;
+    const float nf = (float)N;
+    zero_consumed(a.zero0, a.zero1, a.zero_n);
+    neuron_grads(a.n, a.stats, a.acc_in, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b);
 
     if (tid < C) {
         const float mean = a.stats[tid], inv = a.stats[C + tid];
@@ -556,8 +585,8 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
         bn_w[tid] = a.n.bn_weight[tid];
         if (a.n.bn_train) {
             // torch batch_norm_cpu_backward: k = dotp*invstd*invstd/n, grad_mean = sum/n
-            bn_k[tid] = a.bstats[C + tid] * inv * inv / nf;
-            bn_gm[tid] = a.bstats[tid] / nf;
+            bn_k[tid] = (float)a.acc_in[C + tid] * inv * inv / nf;
+            bn_gm[tid] = (float)(a.acc_in[tid] / N);
         } else {
             bn_k[tid] = 0.0f;
             bn_gm[tid] = 0.0f;
@@ -669,9 +698,7 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
                 v[2 * CIN + ci] = gv * o.mprime;
             }
         }
-        block_partial<NVP>(v, mine);
-        if (last_block_sum<NVP>(mine, a.partials, a.counter, total))
-            finalize_lif_bwd(a.prev, a.prev_stats, total, CIN, a.prev_bstats, a.prev_ng, a.accumulate);
+        block_atomic_sum<NVP>(v, a.acc_out);
     } else {
         if (a.g_x && a.wt_bwd_ff && in) {
             float* gb = a.g_x + (int64_t)tl.b * a.gxs_b + h * a.gxs_h + w * a.gxs_w;
@@ -781,11 +808,10 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
 }
 
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
-    if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || !a->wt_ff || !a->y || !a->stats)
+    if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || !a->wt_ff || !a->y)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: bad args");
-    if (a->lif_in ? (!a->prev_y || !a->prev_stats || !a->prev_state) : !a->x)
+    if (a->lif_in ? (!a->prev_y || !a->prev_state || (a->prev.bn_train && !a->prev_acc)) : !a->x)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: missing input");
-    if (a->self.bn_train && (!a->partials || !a->counter)) SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: missing scratch");
     const hipStream_t s = (hipStream_t)stream;
     switch (a->c) {
         case 4: return conv_fwd_c<4>(*a, s);
@@ -797,7 +823,7 @@ int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
 }
 
 int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
-    if (!a || !a->y || !a->stats || !a->state || a->B <= 0 || a->H <= 0 || a->W <= 0)
+    if (!a || !a->y || !a->state || a->B <= 0 || a->H <= 0 || a->W <= 0 || (a->n.bn_train && !a->acc))
         SNN_FAIL(SNNFLOW_E_ARG, "lif_fwd: bad args");
     if (a->pred_w && (!a->pred_b || !a->flow)) SNN_FAIL(SNNFLOW_E_ARG, "lif_fwd: pred needs bias and flow");
     const hipStream_t s = (hipStream_t)stream;
@@ -818,12 +844,9 @@ int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
 }
 
 int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
-    if (!a || !a->y || !a->stats || !a->g_cur || !a->bstats || !a->partials || !a->counter)
-        SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: bad args");
-    if (!a->ng.bn_weight || !a->ng.bn_bias || !a->ng.beta || !a->ng.threshold)
-        SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: missing parameter-gradient buffers");
+    if (!a || !a->y || !a->stats || !a->g_cur || !a->acc) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: bad args");
     const bool pred = a->pred_w != nullptr;
-    if (pred && (!a->flow || !a->g_pred_w || !a->g_pred_b)) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: pred needs flow and grads");
+    if (pred && !a->flow) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: pred needs flow");
     const hipStream_t s = (hipStream_t)stream;
     const dim3 grid(elem_grid((int64_t)a->B * a->H * a->W)), block(NT);
     switch (a->c) {
@@ -841,11 +864,13 @@ int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
 }
 
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
-    if (!a || !a->y || !a->stats || !a->g_cur || !a->bstats || !a->x || !a->slab_ff)
+    if (!a || !a->y || !a->stats || !a->g_cur || !a->acc_in || !a->x || !a->slab_ff)
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: bad args");
+    if (!a->ng.bn_weight || !a->ng.bn_bias || !a->ng.beta || !a->ng.threshold)
+        SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: missing parameter-gradient buffers");
+    if (a->has_pred && (!a->g_pred_w || !a->g_pred_b)) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: pred gradients");
     if (a->wt_bwd_rec && !a->slab_rec) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: recurrent layer needs slab_rec");
-    if (a->lif_in && (!a->wt_bwd_ff || !a->prev_y || !a->prev_stats || !a->prev_g_cur || !a->prev_bstats ||
-                      !a->partials || !a->counter || !a->prev_ng.bn_weight))
+    if (a->lif_in && (!a->wt_bwd_ff || !a->prev_y || !a->prev_stats || !a->prev_g_cur || !a->acc_out))
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: lif_in needs previous-layer buffers");
     const hipStream_t s = (hipStream_t)stream;
     switch (a->c) {

@@ -27,6 +27,12 @@ template <int C> struct Pad { static constexpr int v = (C <= 4 || C % 4 != 0) ? 
 // Channel-block width for vector LDS access of a C-channel pixel.
 template <int C> struct VecW { static constexpr int v = (C % 4 == 0) ? 4 : ((C % 2 == 0) ? 2 : 1); };
 
+// Weights are read with wave-uniform indices; reading them through the constant
+// address space (4) lets the compiler use scalar loads (s_load_dwordx8/x16) whose
+// results feed v_fma as SGPR operands, instead of one vector load per lane.
+typedef const __attribute__((address_space(4))) float* cfloat_ptr;
+__device__ inline cfloat_ptr as_const(const float* p) { return (cfloat_ptr)(p); }
+
 struct Tile { int b, h0, w0; };
 
 __host__ __device__ inline int tiles_per_image(int H, int W) {
@@ -92,60 +98,6 @@ __device__ inline LifOut lif_step(float y, float m, const LifCoef& k, bool zero_
 __device__ inline float atan_sg(float x) {
     const float u = kPiF * x;
     return __frcp_rn(1.0f + u * u);
-}
-
-// ---------------------------------------------------------------------------
-// Deterministic grid-wide sum: every block contributes NV doubles; the last block
-// to arrive (agent-scope release/acquire ticket, MI355X guide G16) reduces all
-// contributions in fixed block order.  Returns true in the last block, with the
-// totals in `total` (LDS, NV doubles).  Leaves *counter == 0.
-// ---------------------------------------------------------------------------
-template <int NV>
-__device__ bool last_block_sum(const double* mine, double* __restrict__ partials, unsigned* counter,
-                               double* total) {
-    __shared__ double scratch[NT];
-    __shared__ int is_last;
-    const int tid = threadIdx.x, nb = gridDim.x;
-    for (int j = tid; j < NV; j += NT) partials[(size_t)blockIdx.x * NV + j] = mine[j];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        is_last = (t == (unsigned)(nb - 1));
-    }
-    __syncthreads();
-    if (!is_last) return false;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if constexpr (NV <= NT) {
-        constexpr int G = NT / NV;
-        const int j = tid % NV, g = tid / NV;
-        if (g < G) {
-            double s = 0.0;
-            for (int i = g; i < nb; i += G) s += partials[(size_t)i * NV + j];
-            scratch[g * NV + j] = s;
-        }
-        __syncthreads();
-        if (tid < NV) {
-            double s = 0.0;
-            for (int gg = 0; gg < G; ++gg) s += scratch[gg * NV + tid];
-            total[tid] = s;
-        }
-    } else {
-        for (int j = tid; j < NV; j += NT) {
-            double s = 0.0;
-            for (int i = 0; i < nb; ++i) s += partials[(size_t)i * NV + j];
-            total[j] = s;
-        }
-    }
-    if (tid == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    return true;
 }
 
 }  // namespace snnflow

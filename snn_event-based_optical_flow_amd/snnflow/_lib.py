@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class Neuron(ctypes.Structure):
@@ -34,15 +34,17 @@ class NeuronGrad(ctypes.Structure):
 class ConvFwdArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32), ("lif_in", I32),
                 ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
-                ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron), ("prev_state", P),
-                ("wt_ff", P), ("wt_rec", P), ("s_prev", P), ("self", Neuron),
-                ("y", P), ("stats", P), ("partials", P), ("counter", P)]
+                ("prev_y", P), ("prev_mem", P), ("prev_acc", P), ("prev_stats", P),
+                ("prev", Neuron), ("prev_state", P),
+                ("wt_ff", P), ("wt_rec", P), ("s_prev", P),
+                ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32)]
 
 
 class LifFwdArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("c", I32),
-                ("y", P), ("mem", P), ("stats", P), ("n", Neuron), ("state", P),
-                ("pred_w", P), ("pred_b", P), ("flow", P)]
+                ("y", P), ("mem", P), ("acc", P), ("stats", P), ("n", Neuron), ("state", P),
+                ("pred_w", P), ("pred_b", P), ("flow", P),
+                ("zero0", P), ("zero1", P), ("zero_n", I32)]
 
 
 class LifBwdArgs(ctypes.Structure):
@@ -50,21 +52,26 @@ class LifBwdArgs(ctypes.Structure):
                 ("y", P), ("mem", P), ("stats", P), ("n", Neuron),
                 ("g_out", P), ("g_state", P), ("pred_w", P), ("flow", P), ("g_flow", P),
                 ("gflow_sb", I64), ("gflow_sc", I64),
-                ("g_cur", P), ("bstats", P), ("g_mem", P), ("ng", NeuronGrad), ("g_pred_w", P), ("g_pred_b", P),
-                ("accumulate", I32), ("partials", P), ("counter", P)]
+                ("g_cur", P), ("g_mem", P), ("acc", P),
+                ("zero0", P), ("zero1", P), ("zero_n", I32)]
 
 
 class LayerBwdArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
-                ("y", P), ("stats", P), ("g_cur", P), ("bstats", P), ("n", Neuron),
+                ("y", P), ("stats", P), ("g_cur", P), ("acc_in", P), ("n", Neuron), ("ng", NeuronGrad),
+                ("has_pred", I32), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32),
                 ("wt_bwd_ff", P), ("wt_bwd_rec", P), ("lif_in", I32),
                 ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
-                ("s_prev", P), ("slab_ff", P), ("slab_rec", P), ("accumulate", I32),
+                ("s_prev", P), ("slab_ff", P), ("slab_rec", P),
                 ("g_x", P), ("gxs_b", I64), ("gxs_c", I64), ("gxs_h", I64), ("gxs_w", I64),
                 ("g_state_prev", P), ("zero_mem_half", I32),
                 ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),
-                ("prev_g_state", P), ("prev_g_cur", P), ("prev_bstats", P), ("prev_ng", NeuronGrad),
-                ("prev_g_mem", P), ("partials", P), ("counter", P)]
+                ("prev_g_state", P), ("prev_g_cur", P), ("prev_g_mem", P), ("acc_out", P),
+                ("zero0", P), ("zero1", P), ("zero_n", I32)]
+
+
+def bwd_acc_len(c):
+    return 5 * c + 2
 
 
 class SlabDesc(ctypes.Structure):
@@ -76,8 +83,7 @@ class IweLossArgs(ctypes.Structure):
                 ("events", P), ("pol", P), ("flows", P), ("masks", P), ("off", ctypes.c_int32 * 65),
                 ("flow_scaling", F32), ("weight", F32),
                 ("smoothing_mask", I32), ("overwrite_intermediate", I32), ("loss_scaling", I32),
-                ("images", P), ("persample", P), ("smooth", P), ("loss", P),
-                ("partials", P), ("counter", P)]
+                ("images", P), ("acc", P), ("persample", P), ("smooth", P), ("loss", P)]
 
 
 EXPORTS = {

@@ -219,18 +219,19 @@ class CellFn(torch.autograd.Function):
         n = neuron_struct(cell)
         y = torch.empty(B, H, W, C, device=dev)
         stats = torch.empty(2, C, device=dev)
+        facc = ws.fwd_acc[0]
+        facc.zero_()
         a = _lib.ConvFwdArgs()
         a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin, C, 0
         a.x = ptr(x)
         a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
         a.wt_ff, a.wt_rec, a.s_prev = ptr(wff[0]), _ptr_t(wrec[0]), _ptr_t(sp)
-        a.self = n
-        a.y, a.stats, a.partials, a.counter = ptr(y), ptr(stats), ptr(ws.partials), ptr(ws.counter)
+        a.y, a.acc = ptr(y), (ptr(facc) if n.bn_train else None)
         _lib.call("conv_fwd", lib.snnflow_conv_fwd, ctypes.byref(a), s)
         state = empty_state(B, C, H, W, dev)
         f = _lib.LifFwdArgs()
         f.B, f.H, f.W, f.c = B, H, W, C
-        f.y, f.mem, f.stats, f.n, f.state = ptr(y), _ptr_t(mem), ptr(stats), n, ptr(state)
+        f.y, f.mem, f.acc, f.stats, f.n, f.state = ptr(y), _ptr_t(mem), ptr(facc), ptr(stats), n, ptr(state)
         _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
         cell.lif.mem = state[0].detach()
         spk = state[1].detach().clone()  # a separate output tensor (same values as state[1])
@@ -260,7 +261,8 @@ class CellFn(torch.autograd.Function):
         g_beta, g_th = torch.empty(C, device=dev), torch.empty(C, device=dev)
         ng = _lib.NeuronGrad(ptr(g_bw), ptr(g_bb), ptr(g_beta), ptr(g_th))
         g_cur = torch.empty(B, H, W, C, device=dev)
-        bstats = torch.empty(2, C, device=dev)
+        bacc = ws.bwd_acc[0]
+        bacc.zero_()
         b = _lib.LifBwdArgs()
         b.B, b.H, b.W, b.c = B, H, W, C
         b.y, b.mem, b.stats, b.n = ptr(y), _ptr_t(mem), ptr(stats), n
@@ -275,18 +277,18 @@ class CellFn(torch.autograd.Function):
             g_prev = torch.zeros((2, B, C, H, W), device=dev).as_strided(
                 (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
             b.g_mem = ptr(g_prev)
-        b.g_cur, b.bstats, b.ng, b.accumulate = ptr(g_cur), ptr(bstats), ng, 0
-        b.partials, b.counter = ptr(ws.partials), ptr(ws.counter)
+        b.g_cur, b.acc = ptr(g_cur), ptr(bacc)
         _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
 
         slab_ff = torch.empty(ws.nblk, C * cin * 9, device=dev)
         slab_rec = torch.empty(ws.nblk, C * C * 9, device=dev) if cell.recurrent else None
         a = _lib.LayerBwdArgs()
         a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin, C, 0
-        a.y, a.stats, a.g_cur, a.bstats, a.n = ptr(y), ptr(stats), ptr(g_cur), ptr(bstats), n
+        a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(y), ptr(stats), ptr(g_cur), ptr(bacc), n
+        a.ng, a.accumulate = ng, 0
         a.x = ptr(x)
         a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
-        a.s_prev, a.slab_ff, a.slab_rec, a.accumulate = _ptr_t(sp), ptr(slab_ff), _ptr_t(slab_rec), 0
+        a.s_prev, a.slab_ff, a.slab_rec = _ptr_t(sp), ptr(slab_ff), _ptr_t(slab_rec)
         gx = None
         if ctx.needs_input_grad[1]:
             gx = torch.empty_like(x)
@@ -296,7 +298,6 @@ class CellFn(torch.autograd.Function):
             a.wt_bwd_rec = ptr(ctx.wbwd[1])
             if g_prev is not None:
                 a.g_state_prev, a.zero_mem_half = ptr(g_prev), 0
-        a.partials, a.counter = ptr(ws.partials), ptr(ws.counter)
         _lib.call("layer_bwd", lib.snnflow_layer_bwd, ctypes.byref(a), s)
         g_wff = torch.empty_like(cell.ff.weight)
         descs = [_lib.SlabDesc(ptr(slab_ff), ptr(g_wff), g_wff.numel())]

@@ -22,7 +22,6 @@ import torch
 from . import _lib
 from ._lib import check, lib, ptr
 
-_CONV_NV = 5  # partial doubles per channel (max over kernels: lif_bwd+pred = 5C + 2)
 
 
 def nhwc_state_strides(B, C, H, W):
@@ -66,19 +65,26 @@ def neuron_struct(cell):
 
 
 class Workspace:
-    """Device scratch sized for one (B, H, W, C) problem; reused across steps."""
+    """Device scratch sized for one (B, H, W, C) problem; reused across steps.
+
+    fwd_acc[l] / bwd_acc[l]: fp64 batch-sum accumulators of layer l (BatchNorm forward
+    sums; LIF/BN backward sums + pred sums).  Zero when idle; each is re-zeroed by a
+    kernel that runs after its consumer (see FireNetStep)."""
 
     def __init__(self, B, H, W, C, layers, device):
         self.key = (B, H, W, C, device)
         self.B, self.H, self.W, self.C = B, H, W, C
         self.nblk = lib.snnflow_conv_blocks(B, H, W)
-        self.partials = torch.empty(self.nblk * (_CONV_NV * C + 2), dtype=torch.float64, device=device)
-        self.counter = torch.zeros(16, dtype=torch.int32, device=device)
+        self.fwd_acc = torch.zeros(max(layers, 1), 2 * C, dtype=torch.float64, device=device)
+        self.bwd_acc = torch.zeros(max(layers, 1), _lib.bwd_acc_len(C), dtype=torch.float64, device=device)
         self.gcur = torch.empty(2, B, H, W, C, dtype=torch.float32, device=device)
-        self.bstats = torch.empty(max(layers, 1), 2, C, dtype=torch.float32, device=device)
         self.slab_ff = []
         self.slab_rec = []
         self.device = device
+
+    def reset_acc(self):
+        self.fwd_acc.zero_()
+        self.bwd_acc.zero_()
 
     def slabs(self, layer_shapes):
         """layer_shapes: list of (cin, recurrent)."""
@@ -247,36 +253,45 @@ class FireNetStep(torch.autograd.Function):
                     root = False
                 ext[l] = p.requires_grad and not ours
         neurons = [neuron_struct(c) for c in cells]
-        part, cnt = ptr(ws.partials), ptr(ws.counter)
-
-        # layer 0: conv(x) (+ BN statistics)
-        a = _lib.ConvFwdArgs()
-        a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin0, C, 0
-        a.x = ptr(x)
-        a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
-        a.wt_ff, a.wt_rec = ptr(wfwd[0][0]), ptr(wfwd[0][1])
-        a.s_prev = _ptr_nhwc_spk(s_prev[0])
-        a.self = neurons[0]
-        a.y, a.stats, a.partials, a.counter = ptr(ys[0]), ptr(stats[0]), part, cnt
-        _lib.call("conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
-        # layers 1..L-1: LIF(l-1) on the halo + conv(l)
-        for l in range(1, L):
+        train = [c.bn.training or not c.bn.track_running_stats for c in cells]
+        facc = ws.fwd_acc
+        zn = 2 * C
+        try:
+            # K0: conv(head)  (zeroes fwd_acc[L-1], consumed by the previous step's last kernel)
             a = _lib.ConvFwdArgs()
-            a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, C, C, 1
-            a.prev_y, a.prev_mem, a.prev_stats = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1])
-            a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
-            a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
-            a.s_prev = _ptr_t(s_prev[l])
-            a.self = neurons[l]
-            a.y, a.stats, a.partials, a.counter = ptr(ys[l]), ptr(stats[l]), part, cnt
-            _lib.call(f"conv_fwd[{l}]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
-        # LIF of the last layer + pred
-        f = _lib.LifFwdArgs()
-        f.B, f.H, f.W, f.c = B, H, W, C
-        f.y, f.mem, f.stats = ptr(ys[L - 1]), _ptr_t(mem_in[L - 1]), ptr(stats[L - 1])
-        f.n, f.state = neurons[L - 1], ptr(states[L - 1])
-        f.pred_w, f.pred_b, f.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), ptr(flow)
-        _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
+            a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin0, C, 0
+            a.x = ptr(x)
+            a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
+            a.wt_ff, a.wt_rec = ptr(wfwd[0][0]), ptr(wfwd[0][1])
+            a.s_prev = _ptr_t(s_prev[0])
+            a.y, a.acc = ptr(ys[0]), (ptr(facc[0]) if train[0] else None)
+            a.zero0, a.zero_n = ptr(facc[L - 1]), zn
+            _lib.call("conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
+            # K_l: LIF(l-1) on the halo + conv(l)  (zeroes fwd_acc[l-2], consumed by K_{l-1})
+            for l in range(1, L):
+                a = _lib.ConvFwdArgs()
+                a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, C, C, 1
+                a.prev_y, a.prev_mem = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1])
+                a.prev_acc, a.prev_stats = ptr(facc[l - 1]), ptr(stats[l - 1])
+                a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
+                a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
+                a.s_prev = _ptr_t(s_prev[l])
+                a.y, a.acc = ptr(ys[l]), (ptr(facc[l]) if train[l] else None)
+                if l >= 2:
+                    a.zero0, a.zero_n = ptr(facc[l - 2]), zn
+                _lib.call(f"conv_fwd[{l}]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
+            # K_L: LIF of the last layer + pred  (zeroes fwd_acc[L-2])
+            f = _lib.LifFwdArgs()
+            f.B, f.H, f.W, f.c = B, H, W, C
+            f.y, f.mem, f.acc, f.stats = ptr(ys[L - 1]), _ptr_t(mem_in[L - 1]), ptr(facc[L - 1]), ptr(stats[L - 1])
+            f.n, f.state = neurons[L - 1], ptr(states[L - 1])
+            f.pred_w, f.pred_b, f.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), ptr(flow)
+            if L >= 2:
+                f.zero0, f.zero_n = ptr(facc[L - 2]), zn
+            _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
+        except Exception:
+            ws.reset_acc()
+            raise
 
         for l in range(L):
             cells[l].lif.mem = states[l][0].detach()
@@ -321,7 +336,8 @@ class FireNetStep(torch.autograd.Function):
             acc = 1
         glayers, gpw, gpb = eng.grad_views()
         neurons = [neuron_struct(c) for c in eng.cells]
-        part, cnt = ptr(ws.partials), ptr(ws.counter)
+        bacc = ws.bwd_acc
+        zn = bacc.shape[1]
         slab_ff, slab_rec = ws.slab_ff, ws.slab_rec
         gst = [as_nhwc_state(g) if g is not None else None for g in g_states]
         # gradients of the previous states: the spike half of recurrent cells (rec dgrad);
@@ -338,55 +354,62 @@ class FireNetStep(torch.autograd.Function):
                 g_prev[l] = empty_state(B, C, H, W, dev)
         gmem = [g_prev[l] if (g_prev[l] is not None and ctx.ext[l]) else None for l in range(L)]
 
-        # top: pred backward + LIF backward of layer L-1
-        top = L - 1
-        b = _lib.LifBwdArgs()
-        b.B, b.H, b.W, b.c = B, H, W, C
-        b.y, b.mem, b.stats, b.n = ptr(ys[top]), _ptr_t(mem_in[top]), ptr(stats[top]), neurons[top]
-        b.g_out = None
-        b.g_state = _ptr_t(gst[top])
-        b.pred_w, b.flow = ptr(eng.pred.weight), ptr(flow)
-        if g_flow is not None:
-            if g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32:
-                g_flow = g_flow.contiguous().float()
-            b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
-        b.g_cur, b.bstats = ptr(ws.gcur[top % 2]), ptr(ws.bstats[top])
-        b.g_mem = _ptr_t(gmem[top])
-        b.ng, b.g_pred_w, b.g_pred_b = glayers[top][2], ptr(gpw), ptr(gpb)
-        b.accumulate, b.partials, b.counter = acc, part, cnt
-        _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
+        try:
+            # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
+            top = L - 1
+            b = _lib.LifBwdArgs()
+            b.B, b.H, b.W, b.c = B, H, W, C
+            b.y, b.mem, b.stats, b.n = ptr(ys[top]), _ptr_t(mem_in[top]), ptr(stats[top]), neurons[top]
+            b.g_state = _ptr_t(gst[top])
+            b.pred_w, b.flow = ptr(eng.pred.weight), ptr(flow)
+            if g_flow is not None:
+                if g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32:
+                    g_flow = g_flow.contiguous().float()
+                b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
+            b.g_cur, b.g_mem = ptr(ws.gcur[top % 2]), _ptr_t(gmem[top])
+            b.acc = ptr(bacc[top])
+            b.zero0, b.zero_n = ptr(bacc[0]), zn
+            _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
 
-        gx = None
-        for l in range(L - 1, -1, -1):
-            a = _lib.LayerBwdArgs()
-            a.B, a.H, a.W, a.c = B, H, W, C
-            a.y, a.stats, a.g_cur, a.bstats, a.n = ptr(ys[l]), ptr(stats[l]), ptr(ws.gcur[l % 2]), ptr(ws.bstats[l]), neurons[l]
-            a.s_prev = _ptr_t(s_prev[l])
-            a.slab_ff, a.slab_rec, a.accumulate = ptr(slab_ff[l]), _ptr_t(slab_rec[l]), acc
-            a.partials, a.counter = part, cnt
-            if eng.rec[l]:
-                a.wt_bwd_rec = ptr(wbwd[l][1])
-                if g_prev[l] is not None:
-                    a.g_state_prev = ptr(g_prev[l])
-                    a.zero_mem_half = 0 if ctx.ext[l] else 1
-            if l > 0:
-                a.cin, a.lif_in = C, 1
-                a.wt_bwd_ff = ptr(wbwd[l][0])
-                a.x, (a.xs_b, a.xs_c, a.xs_h, a.xs_w) = _spk_half(states[l - 1])
-                a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
-                a.prev_g_state = _ptr_t(gst[l - 1])
-                a.prev_g_cur, a.prev_bstats, a.prev_ng = ptr(ws.gcur[(l - 1) % 2]), ptr(ws.bstats[l - 1]), glayers[l - 1][2]
-                a.prev_g_mem = _ptr_t(gmem[l - 1])
-            else:
-                a.cin, a.lif_in = cin0, 0
-                a.x = ptr(x)
-                a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
-                if ctx.needs_input_grad[1]:
-                    gx = torch.empty_like(x)
-                    a.wt_bwd_ff = ptr(wbwd[0][0])
-                    a.g_x = ptr(gx)
-                    a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
-            _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+            gx = None
+            for l in range(L - 1, -1, -1):
+                a = _lib.LayerBwdArgs()
+                a.B, a.H, a.W, a.c = B, H, W, C
+                a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(ys[l]), ptr(stats[l]), ptr(ws.gcur[l % 2]), ptr(bacc[l]), neurons[l]
+                a.ng, a.accumulate = glayers[l][2], acc
+                if l == L - 1:
+                    a.has_pred, a.g_pred_w, a.g_pred_b = 1, ptr(gpw), ptr(gpb)
+                a.s_prev = _ptr_t(s_prev[l])
+                a.slab_ff, a.slab_rec = ptr(slab_ff[l]), _ptr_t(slab_rec[l])
+                if l + 1 <= L - 1:
+                    a.zero0, a.zero_n = ptr(bacc[l + 1]), zn
+                if eng.rec[l]:
+                    a.wt_bwd_rec = ptr(wbwd[l][1])
+                    if g_prev[l] is not None:
+                        a.g_state_prev = ptr(g_prev[l])
+                        a.zero_mem_half = 0 if ctx.ext[l] else 1
+                if l > 0:
+                    a.cin, a.lif_in = C, 1
+                    a.wt_bwd_ff = ptr(wbwd[l][0])
+                    a.x, (a.xs_b, a.xs_c, a.xs_h, a.xs_w) = _spk_half(states[l - 1])
+                    a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
+                    a.prev_g_state = _ptr_t(gst[l - 1])
+                    a.prev_g_cur, a.prev_g_mem = ptr(ws.gcur[(l - 1) % 2]), _ptr_t(gmem[l - 1])
+                    a.acc_out = ptr(bacc[l - 1])
+                else:
+                    a.cin, a.lif_in = cin0, 0
+                    a.x = ptr(x)
+                    a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
+                    if ctx.needs_input_grad[1]:
+                        gx = torch.empty_like(x)
+                        a.wt_bwd_ff = ptr(wbwd[0][0])
+                        a.g_x = ptr(gx)
+                        a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
+                _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+        except Exception:
+            ws.reset_acc()
+            eng.bwd_open = False
+            raise
 
         grads = [None] * len(eng.flat_views)
         if ctx.root:

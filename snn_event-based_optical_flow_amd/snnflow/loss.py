@@ -23,9 +23,7 @@ class _Scratch:
     def get(self, B, H, W, device):
         key = (B, H, W, device)
         if self.key != key:
-            chunks = (H * W + 255) // 256
-            self.partials = torch.empty(B * chunks * 11 + 16, dtype=torch.float64, device=device)
-            self.counter = torch.zeros(4, dtype=torch.int32, device=device)
+            self.acc = torch.zeros(6 * B + 5, dtype=torch.float64, device=device)
             self.key = key
         return self
 
@@ -41,8 +39,7 @@ def _fill_args(meta, events, pol, masks, flows, images, persample, smooth, loss,
     a.smoothing_mask = 1 if meta["smoothing_mask"] else 0
     a.overwrite_intermediate = 1 if meta["overwrite_intermediate"] else 0
     a.loss_scaling = 1 if meta["loss_scaling"] else 0
-    a.images, a.persample, a.smooth, a.loss = ptr(images), ptr(persample), ptr(smooth), ptr(loss)
-    a.partials, a.counter = ptr(scr.partials), ptr(scr.counter)
+    a.images, a.acc, a.persample, a.smooth, a.loss = ptr(images), ptr(scr.acc), ptr(persample), ptr(smooth), ptr(loss)
     return a
 
 

@@ -1,0 +1,37 @@
+"""A few eager LIFFireNet train steps of the bench workload (for rocprofv3 --pmc passes)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "snn_event-based_optical_flow_amd")]
+import torch  # noqa: E402
+
+import snnflow  # noqa: E402
+from oracle import lif_ref  # noqa: E402
+from snnflow.synthetic import make_window  # noqa: E402
+
+
+def main(C=8, R=128, B=8, T=10, steps=3):
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=C)).to(dev).train()
+    cfg = {"loader": {"resolution": [R, R]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    lf = snnflow.EventWarping(cfg, dev)
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    wins = [make_window(B, 1000, R, R, gen, dev) for _ in range(T)]
+    for _ in range(steps):
+        lf.reset()
+        for w in wins:
+            out = model(w["event_voxel"], w["event_cnt"])
+            lf.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        lf().backward()
+        opt.step()
+        opt.zero_grad()
+        model.detach_states()
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main(*[int(a) for a in sys.argv[1:]])
