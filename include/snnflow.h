@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 3
+#define SNNFLOW_ABI_VERSION 5
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -61,14 +61,29 @@ typedef struct snnflow_neuron {
 int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* wt_bwd,
                          float* threshold, void* stream);
 
+/* All layers' weight preparation in one launch (one descriptor per conv weight and/or
+ * threshold vector; the fields mean what the snnflow_prep_weights arguments mean,
+ * thr_n = entries of `threshold` to clamp).  n <= SNNFLOW_MAX_BATCH. */
+typedef struct snnflow_prep_desc {
+    const float* w; int c, cin; float* wt_fwd; float* wt_bwd;
+    float* threshold; int thr_n;
+} snnflow_prep_desc;
+#define SNNFLOW_MAX_BATCH 16
+int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream);
+
 /* Batch-statistics accumulators.  BatchNorm in train mode needs sums over (B,H,W)
  * between the producing conv and the consuming LIF.  Each producer block adds its
- * partial sums with fp64 atomics into an accumulator (one wave instruction per
- * block); the next kernel in the chain derives the statistics in its prologue.  An
- * accumulator must be zero when its producer starts: kernels zero (block 0) the
- * accumulators named in `zero0`/`zero1` (`zero_n` doubles each), which the caller
- * chooses among accumulators already consumed by an earlier kernel of the chain.
- * fp64 accumulation makes the result independent of block order below fp32 resolution. */
+ * partial sums with fp64 atomics into one of SNNFLOW_ACC_SHARDS replicas of the
+ * accumulator (replica = block index mod shards: 512 blocks adding into one address
+ * serialise at the memory-side atomic unit); the next kernel in the chain sums the
+ * replicas in its prologue and derives the statistics.  An accumulator of n sums
+ * occupies SNNFLOW_ACC_LEN(n) doubles ([shard][SNNFLOW_ACC_STRIDE(n)]).  It must be
+ * zero when its producer starts: kernels zero the accumulators named in
+ * `zero0`/`zero1` (`zero_n` doubles each), which the caller chooses among
+ * accumulators already consumed by an earlier kernel of the chain. */
+#define SNNFLOW_ACC_SHARDS 32
+#define SNNFLOW_ACC_STRIDE(n) ((((n) + 15) / 16) * 16)
+#define SNNFLOW_ACC_LEN(n) (SNNFLOW_ACC_SHARDS * SNNFLOW_ACC_STRIDE(n))
 
 /* ---- forward: [LIF of layer l on a halo tile] + conv3x3(layer l+1) [+ BN batch sums]
  * Replaces, per time step, `lif(bn(...))` of layer l fused with `ff(input_)`
@@ -77,7 +92,7 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
  * lif_in = 0: x is a strided tensor (e.g. event_cnt NCHW) with cin channels.
  * lif_in = 1: the input spikes are computed from the previous layer's pre-BN conv
  *             output prev_y (NHWC), its membrane prev_mem (NULL = zeros) and its batch
- *             sums prev_acc [2][cin] (train) or running stats (eval); block 0 writes
+ *             sums prev_acc (SNNFLOW_ACC_LEN(2cin), train) or running stats (eval); block 0 writes
  *             prev_stats [2][cin] (mean, invstd) and updates the running statistics;
  *             prev_state [2][B][H][W][cin] receives (mem_out, spk) of the previous layer. */
 typedef struct snnflow_conv_fwd_args {
@@ -91,7 +106,7 @@ typedef struct snnflow_conv_fwd_args {
     const float* wt_rec;        /* [3][3][c][c] or NULL (feed-forward) */
     const float* s_prev;        /* NHWC [B][H][W][c] previous-step spikes; NULL = zeros */
     float* y;                   /* out NHWC [B][H][W][c] pre-BN current           */
-    double* acc;                /* += [2][c] (sum y, sum y^2); NULL = no batch sums (eval) */
+    double* acc;                /* += SNNFLOW_ACC_LEN(2c) (sum y, sum y^2); NULL = no batch sums (eval) */
     double* zero0; double* zero1; int zero_n;
 } snnflow_conv_fwd_args;
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream);
@@ -103,7 +118,7 @@ int snnflow_conv_blocks(int B, int H, int W);
 typedef struct snnflow_lif_fwd_args {
     int B, H, W, c;
     const float* y; const float* mem;
-    const double* acc;          /* [2][c] batch sums (train) */
+    const double* acc;          /* SNNFLOW_ACC_LEN(2c) batch sums (train) */
     float* stats;               /* out [2][c] (mean, invstd) */
     snnflow_neuron n; float* state;
     const float* pred_w;        /* [2][c] or NULL (no pred) */
@@ -119,7 +134,7 @@ typedef struct snnflow_neuron_grad {
 } snnflow_neuron_grad;
 
 /* Number of doubles of a backward accumulator for c channels (3c LIF/BN sums + 2c+2 pred). */
-#define SNNFLOW_BWD_ACC(c) (5 * (c) + 2)
+#define SNNFLOW_BWD_ACC(c) (5 * (c) + 2) /* sums per layer; storage SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC(c)) */
 
 /* ---- backward of the top layer: [pred backward] + LIF/ATan surrogate backward
  * g_s = g_out + g_state_spk + pred_w^T (g_flow * (1 - flow^2)); g_v = g_s * sg(v - theta).
@@ -134,7 +149,7 @@ typedef struct snnflow_lif_bwd_args {
     int64_t gflow_sb, gflow_sc; /* element strides of g_flow (batch, channel); HW dense */
     float* g_cur;
     float* g_mem;               /* NHWC grad of the membrane input (beta*(1-r)*g_v) or NULL */
-    double* acc;                /* += SNNFLOW_BWD_ACC(c) doubles */
+    double* acc;                /* += SNNFLOW_BWD_ACC(c) sums (storage SNNFLOW_ACC_LEN of it) */
     double* zero0; double* zero1; int zero_n;
 } snnflow_lif_bwd_args;
 int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream);

@@ -14,6 +14,13 @@
 
 #include "snnflow_dev.h"
 
+// Timing-attribution builds only (tools/kprobe.py): each set bit removes one stage,
+// results are then meaningless.  0 in every shipped build.
+#ifndef SNNFLOW_PROBE
+#define SNNFLOW_PROBE 0
+#endif
+#define PROBE_OFF(bit) ((SNNFLOW_PROBE & (bit)) != 0)
+
 using namespace snnflow;
 
 namespace {
@@ -37,7 +44,6 @@ namespace {
 // ---------------------------------------------------------------------------
 // LDS staging of a halo tile
 // ---------------------------------------------------------------------------
-__device__ inline bool in_image(int h, int w, int H, int W) { return h >= 0 && h < H && w >= 0 && w < W; }
 
 // Strided input (e.g. event_cnt NCHW, or an NHWC spike tensor) -> tile[p][ci]
 template <int CIN>
@@ -140,10 +146,21 @@ __device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ w
     }
 }
 
+// Opaque use of a register array: stops LLVM from sinking its computation into a
+// following conditional block (where the scalar-weight schedule no longer fits).
+template <int N>
+__device__ inline void pin(float (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
 // Per-block weight-gradient partial of one 3x3 conv:
 //   dW[co][ci][ky][kx] = sum_{tile pixels p} g[p][co] * x[p + (ky-1, kx-1)][ci]
 // G: LDS g tile (halo layout, C channels), X: LDS input halo tile (CIN channels).
 // Items (k, co-block of 4, ci-block of VW) x pixel groups; groups reduced in fixed order.
+// Each thread owns NO output slab entries (indices by slab_entry); with `accumulate`
+// their old values are prefetched at kernel start (slab_prefetch) so the read-modify-
+// write adds no memory round trip at the end.
 template <int CIN, int C>
 struct WgradShape {
     static constexpr int VW = VecW<CIN>::v;
@@ -151,15 +168,53 @@ struct WgradShape {
     static constexpr int Q = 9 * (C / 4) * NCB;
     static constexpr int GR = (Q >= NT) ? 1 : NT / Q;
     static constexpr int SCRATCH = (GR > 1) ? GR * Q * 4 * VW : 1;
+    static constexpr int NK = (Q * 4 * VW + NT - 1) / NT;  // outputs per thread (GR > 1)
+    static constexpr int NM = (Q + NT - 1) / NT;           // items per thread (GR == 1)
+    static constexpr int NO = (GR > 1) ? NK : NM * 4 * VW;
 };
 
+// Slab index of this thread's k-th output, or -1.
 template <int CIN, int C>
-__device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ slab, int accumulate, float* scratch) {
+__device__ inline int slab_entry(int k) {
+    using S = WgradShape<CIN, C>;
+    constexpr int VW = S::VW, Q = S::Q;
+    int qq, i, j;
+    if constexpr (S::GR > 1) {
+        const int e = threadIdx.x + k * NT;
+        if (e >= Q * 4 * VW) return -1;
+        qq = e / (4 * VW);
+        const int ij = e - qq * 4 * VW;
+        i = ij / VW;
+        j = ij - i * VW;
+    } else {
+        const int m = k / (4 * VW), ij = k - m * 4 * VW;
+        qq = threadIdx.x + m * NT;
+        if (qq >= Q) return -1;
+        i = ij / VW;
+        j = ij - i * VW;
+    }
+    const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
+    return ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
+}
+
+template <int CIN, int C>
+__device__ inline void slab_prefetch(const float* slab, int accumulate, float (&old)[WgradShape<CIN, C>::NO]) {
+#pragma unroll
+    for (int k = 0; k < WgradShape<CIN, C>::NO; ++k) {
+        const int idx = slab_entry<CIN, C>(k);
+        old[k] = (accumulate && idx >= 0) ? slab[idx] : 0.0f;
+    }
+}
+
+template <int CIN, int C>
+__device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ slab,
+                           const float (&old)[WgradShape<CIN, C>::NO], float* scratch) {
     using S = WgradShape<CIN, C>;
     constexpr int VW = S::VW, Q = S::Q, GR = S::GR, PC = Pad<C>::v, PX = Pad<CIN>::v;
     const int tid = threadIdx.x;
-    for (int q0 = 0; q0 < Q; q0 += (GR > 1 ? Q : NT)) {
-        const int q = (GR > 1) ? tid % Q : q0 + tid;
+#pragma unroll
+    for (int m = 0; m < (GR > 1 ? 1 : S::NM); ++m) {
+        const int q = (GR > 1) ? tid % Q : tid + m * NT;
         const int g = (GR > 1) ? tid / Q : 0;
         const bool active = (GR > 1) ? (g < GR) : (q < Q);
         float acc[4][VW];
@@ -167,12 +222,8 @@ __device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ s
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < VW; ++j) acc[i][j] = 0.f;
-        int kidx = 0, cob = 0, cib = 0;
         if (active) {
-            kidx = q % 9;
-            const int rest = q / 9;
-            cob = rest % (C / 4);
-            cib = rest / (C / 4);
+            const int kidx = q % 9, rest = q / 9, cob = rest % (C / 4), cib = rest / (C / 4);
             const int ky = kidx / 3, kx = kidx % 3;
             for (int p = g; p < NT; p += GR) {
                 const int ty = p / TW, tx = p - ty * TW;
@@ -203,13 +254,14 @@ __device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ s
                     for (int j = 0; j < VW; ++j) scratch[((g * Q + q) * 4 + i) * VW + j] = acc[i][j];
             }
             __syncthreads();
-            for (int e = tid; e < Q * 4 * VW; e += NT) {
-                float s = 0.f;
-                for (int gg = 0; gg < GR; ++gg) s += scratch[gg * Q * 4 * VW + e];
-                const int qq = e / (4 * VW), ij = e - qq * 4 * VW, i = ij / VW, j = ij - i * VW;
-                const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
-                const int widx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
-                slab[widx] = accumulate ? slab[widx] + s : s;
+#pragma unroll
+            for (int k = 0; k < S::NK; ++k) {
+                const int e = tid + k * NT;
+                if (e < Q * 4 * VW) {
+                    float sum = 0.f;
+                    for (int gg = 0; gg < GR; ++gg) sum += scratch[gg * Q * 4 * VW + e];
+                    slab[slab_entry<CIN, C>(k)] = old[k] + sum;
+                }
             }
             __syncthreads();
         } else {
@@ -218,8 +270,8 @@ __device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ s
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int j = 0; j < VW; ++j) {
-                        const int widx = ((cob * 4 + i) * CIN + cib * VW + j) * 9 + kidx;
-                        slab[widx] = accumulate ? slab[widx] + acc[i][j] : acc[i][j];
+                        const int k = m * 4 * VW + i * VW + j;
+                        slab[slab_entry<CIN, C>(k)] = old[k] + acc[i][j];
                     }
             }
         }
@@ -243,7 +295,7 @@ __device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const float s = wave_sum(v[j]);
+        const float s = wave_total(v[j]);
         if (lane == 0) red[wv][j] = s;
     }
     __syncthreads();
@@ -253,22 +305,55 @@ __device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
 
 // Block 0 zeroes accumulators already consumed by an earlier kernel of the chain.
 __device__ inline void zero_consumed(double* z0, double* z1, int n) {
-    if (blockIdx.x != 0) return;
-    for (int j = threadIdx.x; j < n; j += NT) {
+    for (int j = blockIdx.x * NT + threadIdx.x; j < n; j += gridDim.x * NT) {
         if (z0) z0[j] = 0.0;
         if (z1) z1[j] = 0.0;
     }
 }
 
-// BatchNorm statistics of channel c from batch sums (train) or running stats (eval):
-// mean = S/N, var = SS/N - mean^2 (biased), invstd = 1/sqrt(var + eps) in fp64.
+// Totals of the M sums of a sharded accumulator (n sums per replica, M <= n, M <= NT)
+// into LDS out[M]: TPJ = NT/M threads per sum each add a strided subset of the
+// replicas (all their loads in flight at once), then one LDS pass.  One global round
+// trip; called by every thread of the block (contains barriers).
+template <int M>
+__device__ void acc_gather(const double* acc, int n, double* out) {
+    static_assert(M >= 1 && M <= NT, "acc_gather: M sums");
+    constexpr int TPJ = NT / M;
+    constexpr int PER = (kAccShards + TPJ - 1) / TPJ;
+    __shared__ double red[TPJ * M];
+    const int tid = threadIdx.x, st = acc_stride(n);
+    if (tid < TPJ * M) {
+        const int j = tid % M, g = tid / M;
+        double v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int sh = g + k * TPJ;
+            v[k] = sh < kAccShards ? acc[sh * st + j] : 0.0;
+        }
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) sum += v[k];
+        red[g * M + j] = sum;
+    }
+    __syncthreads();
+    if (tid < M) {
+        double sum = 0.0;
+        for (int g = 0; g < TPJ; ++g) sum += red[g * M + tid];
+        out[tid] = sum;
+    }
+    __syncthreads();
+}
+
+// BatchNorm statistics of channel c from batch sums (train; sums[c] = S, sums[C+c] = SS)
+// or running stats (eval): mean = S/N, var = SS/N - mean^2 (biased),
+// invstd = 1/sqrt(var + eps) in fp64.
 struct BnStat { float mean, invstd; double dmean, dvar; };
 
-__device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* acc, int C, int c, double N) {
+__device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* sums, int C, int c, double N) {
     BnStat st;
     if (n.bn_train) {
-        st.dmean = acc[c] / N;
-        st.dvar = acc[C + c] / N - st.dmean * st.dmean;
+        st.dmean = sums[c] / N;
+        st.dvar = sums[C + c] / N - st.dmean * st.dmean;
         if (st.dvar < 0.0) st.dvar = 0.0;
         st.mean = (float)st.dmean;
         st.invstd = (float)(1.0 / sqrt(st.dvar + n.eps));
@@ -284,11 +369,14 @@ __device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* acc, int
 // Prologue of a LIF consumer: per-channel coefficients in LDS; block 0 also stores
 // (mean, invstd) for the backward pass and performs the running-stat update
 // (momentum, unbiased variance) and num_batches_tracked += 1 of torch's BatchNorm2d.
-__device__ void lif_prologue(const snnflow_neuron& n, const double* acc, int C, double N, float* stats_out,
+// `sums`: LDS totals from acc_gather (train mode only).
+__device__ void lif_prologue(const snnflow_neuron& n, const double* sums, int C, double N, float* stats_out,
                              LifCoef* coef, float* mean_out) {
     const int c = threadIdx.x;
     if (c < C) {
-        const BnStat st = bn_stat(n, acc, C, c, N);
+        const float rm = (blockIdx.x == 0 && n.bn_train && n.running_mean) ? n.running_mean[c] : 0.f;
+        const float rv = (blockIdx.x == 0 && n.bn_train && n.running_mean) ? n.running_var[c] : 0.f;
+        const BnStat st = bn_stat(n, sums, C, c, N);
         LifCoef k;
         k.alpha = st.invstd * n.bn_weight[c];
         k.shift = n.bn_bias[c] - st.mean * k.alpha;
@@ -303,8 +391,8 @@ __device__ void lif_prologue(const snnflow_neuron& n, const double* acc, int C, 
             }
             if (n.bn_train && n.running_mean) {
                 const double unb = N > 1.0 ? st.dvar * N / (N - 1.0) : st.dvar;
-                n.running_mean[c] = (float)(n.momentum * st.dmean + (1.0 - n.momentum) * (double)n.running_mean[c]);
-                n.running_var[c] = (float)(n.momentum * unb + (1.0 - n.momentum) * (double)n.running_var[c]);
+                n.running_mean[c] = (float)(n.momentum * st.dmean + (1.0 - n.momentum) * (double)rm);
+                n.running_var[c] = (float)(n.momentum * unb + (1.0 - n.momentum) * (double)rv);
             }
         }
     }
@@ -314,118 +402,181 @@ __device__ void lif_prologue(const snnflow_neuron& n, const double* acc, int C, 
 // Layer-l gradients of (gamma, bn bias, beta, threshold) [and pred] from the LIF-backward
 // sums: gamma = dotp*invstd, bias = sum g, theta = -sum g, beta = sum g*m' (0 <= beta <= 1)
 // (torch batch_norm_cpu_backward; snntorch Leaky; clamp backward passes on [0,1]).
-__device__ void neuron_grads(const snnflow_neuron& n, const float* stats, const double* acc, int C,
+__device__ void neuron_grads(const snnflow_neuron& n, const float* stats, const double* sums, int C,
                              const snnflow_neuron_grad& ng, int accumulate, int has_pred, float* g_pred_w,
                              float* g_pred_b) {
     if (blockIdx.x != 0) return;
+    // every load before any store: the destinations may alias as far as the compiler
+    // knows, and block 0's serial load->store chains would set the kernel's length
     const int c = threadIdx.x;
-    if (c < C) {
-        const double gsum = acc[c], dotp = acc[C + c], gbm = acc[2 * C + c];
-        const float gw = (float)(dotp * (double)stats[C + c]);
+    const bool ch = c < C;
+    const int cc = ch ? c : 0;
+    const double gsum = sums[cc], dotp = sums[C + cc], gbm = sums[2 * C + cc];
+    const float inv = stats[C + cc], be = n.beta[cc];
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
+    if (accumulate && ch) {
+        o0 = ng.bn_weight[c]; o1 = ng.bn_bias[c]; o2 = ng.threshold[c]; o3 = ng.beta[c];
+    }
+    const int j = threadIdx.x;
+    const bool pj = has_pred && j < 2 * C + 2;
+    float gp = 0.f, op = 0.f;
+    float* pdst = nullptr;
+    if (pj) {
+        gp = (float)sums[3 * C + j];
+        pdst = (j < 2 * C) ? g_pred_w + j : g_pred_b + (j - 2 * C);
+        if (accumulate) op = *pdst;
+    }
+    if (ch) {
+        const float gw = (float)(dotp * (double)inv);
         const float gb = (float)gsum;
         const float gth = -(float)gsum;
-        const float be = n.beta[c];
         const float gbe = (be >= 0.0f && be <= 1.0f) ? (float)gbm : 0.0f;
-        if (accumulate) {
-            ng.bn_weight[c] += gw; ng.bn_bias[c] += gb; ng.threshold[c] += gth; ng.beta[c] += gbe;
-        } else {
-            ng.bn_weight[c] = gw; ng.bn_bias[c] = gb; ng.threshold[c] = gth; ng.beta[c] = gbe;
-        }
+        ng.bn_weight[c] = o0 + gw;
+        ng.bn_bias[c] = o1 + gb;
+        ng.threshold[c] = o2 + gth;
+        ng.beta[c] = o3 + gbe;
     }
-    if (has_pred) {
-        for (int j = threadIdx.x; j < 2 * C + 2; j += NT) {
-            const float g = (float)acc[3 * C + j];
-            float* dst = (j < 2 * C) ? g_pred_w + j : g_pred_b + (j - 2 * C);
-            *dst = accumulate ? *dst + g : g;
-        }
-    }
+    if (pj) *pdst = op + gp;
 }
 
 // ---------------------------------------------------------------------------
 // Kernels
 // ---------------------------------------------------------------------------
-__global__ void k_prep_weights(const float* __restrict__ w, int c, int cin, float* __restrict__ wt_fwd,
-                               float* __restrict__ wt_bwd, float* thr) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    const int n = c * cin * 9;
-    if (w && e < n) {
-        const int k = e % 9, ci = (e / 9) % cin, co = e / (9 * cin);
-        const float v = w[e];
-        wt_fwd[(k * cin + ci) * c + co] = v;
-        wt_bwd[(k * c + co) * cin + ci] = v;
+// Up to 16 descriptors passed by value in the kernarg segment; blockIdx.y picks one
+// through constant-index selects (a dynamic index would copy the array to scratch).
+template <typename D>
+struct DescBatch {
+    D d[SNNFLOW_MAX_BATCH];
+    __device__ inline D pick(int k) const {
+        D r = d[0];
+#pragma unroll
+        for (int i = 1; i < SNNFLOW_MAX_BATCH; ++i)
+            if (k == i) r = d[i];
+        return r;
     }
-    if (thr && e < c) {
-        const float t = thr[e];
-        thr[e] = (t < 0.01f) ? 0.01f : t;
+};
+
+__global__ void k_prep_weights(DescBatch<snnflow_prep_desc> batch) {
+    const snnflow_prep_desc d = batch.pick(blockIdx.y);
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = d.c, cin = d.cin, n = c * cin * 9;
+    if (d.w && e < n) {
+        const int k = e % 9, ci = (e / 9) % cin, co = e / (9 * cin);
+        const float v = d.w[e];
+        d.wt_fwd[(k * cin + ci) * c + co] = v;
+        d.wt_bwd[(k * c + co) * cin + ci] = v;
+    }
+    if (d.threshold && e < d.thr_n) {
+        const float t = d.threshold[e];
+        d.threshold[e] = (t < 0.01f) ? 0.01f : t;
     }
 }
+
+// LIF of one float4 of channels [4q, 4q+4) (coefficients from LDS).
+struct Lif4 { float4 s, mout; };
+
+__device__ inline Lif4 lif_step4(const float4& y, const float4& m, const LifCoef* coef, bool zr) {
+    const LifOut o0 = lif_step(y.x, m.x, coef[0], zr);
+    const LifOut o1 = lif_step(y.y, m.y, coef[1], zr);
+    const LifOut o2 = lif_step(y.z, m.z, coef[2], zr);
+    const LifOut o3 = lif_step(y.w, m.w, coef[3], zr);
+    Lif4 r;
+    r.s = make_float4(o0.s, o1.s, o2.s, o3.s);
+    r.mout = make_float4(o0.mout, o1.mout, o2.mout, o3.mout);
+    return r;
+}
+
+__device__ inline void zero4(float4* r, int n) {
+    for (int i = 0; i < n; ++i) r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Register-prefetch budget: halo tiles of up to 16 channels are held in registers
+// (<= 6 float4 per thread each); wider layers stage straight into LDS.
+template <int CH>
+struct Prefetch { static constexpr bool on = (CH % 4 == 0) && Halo4<CH>::R <= 6; };
 
 template <int CIN, int C, bool LIF_IN, bool REC>
 __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
     constexpr int PI_ = Pad<CIN>::v, PC = Pad<C>::v;
-    constexpr int PMAX = (REC && PC > PI_) ? PC : PI_;
+    constexpr bool PF_REC = REC && Prefetch<C>::on;   // s_prev halo in registers + own LDS tile
+    constexpr int PMAX = (REC && !PF_REC && PC > PI_) ? PC : PI_;
     __shared__ __attribute__((aligned(16))) float tile[HN * PMAX];
+    __shared__ __attribute__((aligned(16))) float rtile[PF_REC ? HN * PC : 4];
     __shared__ LifCoef coef[LIF_IN ? CIN : 1];
 
     const int tid = threadIdx.x, ty = tid / TW, tx = tid - ty * TW;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
-    zero_consumed(a.zero0, a.zero1, a.zero_n);
+    const bool has_rec = REC && a.s_prev != nullptr;
 
+    // 1. issue every global load of the tile before any use
+    float4 rs[PF_REC ? Halo4<C>::R : 1];
+    if constexpr (PF_REC) {
+        if (has_rec) halo_load<C>(a.s_prev, tl, H, W, rs);
+    }
     if constexpr (LIF_IN) {
-        lif_prologue(a.prev, a.prev_acc, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
+        constexpr int R = Halo4<CIN>::R, Q = CIN / 4;
+        float4 ry[R], rm[R];
+        halo_load<CIN>(a.prev_y, tl, H, W, ry);
+        if (a.prev_mem) halo_load<CIN>(a.prev_mem, tl, H, W, rm);
+        else zero4(rm, R);
+        zero_consumed(a.zero0, a.zero1, a.zero_n);
+        __shared__ double sums[2 * CIN];
+        if (a.prev.bn_train) acc_gather<2 * CIN>(a.prev_acc, 2 * CIN, sums);
+        lif_prologue(a.prev, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
         __syncthreads();
-        // LIF of the previous layer over the halo tile; interior pixels also write its state.
+        // 2. LIF of the previous layer over the halo; interior pixels also write its state
         const bool zr = a.prev.zero_reset != 0;
-        const int64_t plane = (int64_t)a.B * H * W * CIN;
-        for (int p = tid; p < HN; p += NT) {
-            const int r = p / HWD, cc = p - r * HWD;
-            const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-            float* dst = tile + p * PI_;
-            if (in_image(h, w, H, W)) {
-                const int64_t pix = ((int64_t)tl.b * H + h) * W + w;
-                const bool interior = (r >= 1 && r <= TH && cc >= 1 && cc <= TW);
+        const int64_t plane4 = (int64_t)a.B * H * W * Q;
+        float4* st4 = reinterpret_cast<float4*>(a.prev_state);
 #pragma unroll
-                for (int ci = 0; ci < CIN; ci += 4) {
-                    const float4 yv = *reinterpret_cast<const float4*>(a.prev_y + pix * CIN + ci);
-                    const float4 mv = a.prev_mem ? *reinterpret_cast<const float4*>(a.prev_mem + pix * CIN + ci)
-                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-                    const LifOut o0 = lif_step(yv.x, mv.x, coef[ci + 0], zr);
-                    const LifOut o1 = lif_step(yv.y, mv.y, coef[ci + 1], zr);
-                    const LifOut o2 = lif_step(yv.z, mv.z, coef[ci + 2], zr);
-                    const LifOut o3 = lif_step(yv.w, mv.w, coef[ci + 3], zr);
-                    const float4 sv = make_float4(o0.s, o1.s, o2.s, o3.s);
-                    *reinterpret_cast<float4*>(dst + ci) = sv;
-                    if (interior) {
-                        *reinterpret_cast<float4*>(a.prev_state + pix * CIN + ci) =
-                            make_float4(o0.mout, o1.mout, o2.mout, o3.mout);
-                        *reinterpret_cast<float4*>(a.prev_state + plane + pix * CIN + ci) = sv;
+        for (int i = 0; i < R; ++i) {
+            const int e = tid + i * NT;
+            if (e < Halo4<CIN>::E) {
+                const int p = e / Q, q = e - p * Q;
+                const int r = p / HWD, cc = p - r * HWD;
+                const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+                float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (in_image(h, w, H, W)) {
+                    const Lif4 o = lif_step4(ry[i], rm[i], coef + 4 * q, zr);
+                    sv = o.s;
+                    if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
+                        const int64_t k = (((int64_t)tl.b * H + h) * W + w) * Q + q;
+                        st4[k] = o.mout;
+                        st4[plane4 + k] = o.s;
                     }
                 }
-            } else {
-#pragma unroll
-                for (int ci = 0; ci < CIN; ++ci) dst[ci] = 0.0f;
+                *reinterpret_cast<float4*>(tile + p * PI_ + 4 * q) = sv;
             }
         }
     } else {
+        zero_consumed(a.zero0, a.zero1, a.zero_n);
         stage_strided<CIN>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, tile);
+    }
+    if constexpr (PF_REC) {
+        if (has_rec) halo_store<C>(rtile, rs);
     }
     __syncthreads();
 
     float y[C];
 #pragma unroll
     for (int co = 0; co < C; ++co) y[co] = 0.0f;
-    conv_acc<CIN, C>(tile, a.wt_ff, ty, tx, y);
+    if (!PROBE_OFF(16)) conv_acc<CIN, C>(tile, a.wt_ff, ty, tx, y);
 
     if constexpr (REC) {
-        if (a.s_prev) {
-            __syncthreads();
-            stage_nhwc<C>(a.s_prev, tl, H, W, tile);
-            __syncthreads();
+        if (has_rec) {
+            const float* rt = tile;
+            if constexpr (PF_REC) {
+                rt = rtile;
+            } else {
+                __syncthreads();
+                stage_nhwc<C>(a.s_prev, tl, H, W, tile);
+                __syncthreads();
+            }
             float r[C];
 #pragma unroll
             for (int co = 0; co < C; ++co) r[co] = 0.0f;
-            conv_acc<C, C>(tile, a.wt_rec, ty, tx, r);
+            if (!PROBE_OFF(16)) conv_acc<C, C>(rt, a.wt_rec, ty, tx, r);
 #pragma unroll
             for (int co = 0; co < C; ++co) y[co] = y[co] + r[co];  // ff + rec (:540)
         }
@@ -447,52 +598,96 @@ __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
             v[co] = yy;
             v[C + co] = yy * yy;
         }
-        block_atomic_sum<2 * C>(v, a.acc);
+        if (!PROBE_OFF(4)) block_atomic_sum<2 * C>(v, acc_shard(a.acc, 2 * C));
     }
 }
 
+// LIF (+ 1x1 pred conv + tanh) over pixels: one thread per pixel, all C channels.
 template <int C, bool PRED>
 __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
+    constexpr int Q = C / 4;
     __shared__ LifCoef coef[C];
     const int tid = threadIdx.x;
+    const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
+    const int64_t p = (int64_t)blockIdx.x * NT + tid;
+    const bool act = p < npix;
+    const float4* y4 = reinterpret_cast<const float4*>(a.y);
+    const float4* m4 = reinterpret_cast<const float4*>(a.mem);
+    const int64_t pc = act ? p : npix - 1;  // unconditional 16-B loads
+    float4 yv[Q], mv[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        yv[q] = y4[pc * Q + q];
+        mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
+    }
     zero_consumed(a.zero0, a.zero1, a.zero_n);
-    lif_prologue(a.n, a.acc, C, (double)a.B * a.H * a.W, a.stats, coef, nullptr);
+    __shared__ double sums[2 * C];
+    if (a.n.bn_train) acc_gather<2 * C>(a.acc, 2 * C, sums);
+    lif_prologue(a.n, sums, C, (double)npix, a.stats, coef, nullptr);
     __syncthreads();
+    if (!act) return;
     const bool zr = a.n.zero_reset != 0;
-    const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane = npix * C;
-    for (int64_t p = (int64_t)blockIdx.x * NT + tid; p < npix; p += (int64_t)gridDim.x * NT) {
-        float s[C];
+    float4* st4 = reinterpret_cast<float4*>(a.state);
+    float s[C];
 #pragma unroll
-        for (int c = 0; c < C; c += 4) {
-            const float4 yv = *reinterpret_cast<const float4*>(a.y + p * C + c);
-            const float4 mv = a.mem ? *reinterpret_cast<const float4*>(a.mem + p * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-            const LifOut o0 = lif_step(yv.x, mv.x, coef[c + 0], zr);
-            const LifOut o1 = lif_step(yv.y, mv.y, coef[c + 1], zr);
-            const LifOut o2 = lif_step(yv.z, mv.z, coef[c + 2], zr);
-            const LifOut o3 = lif_step(yv.w, mv.w, coef[c + 3], zr);
-            s[c] = o0.s; s[c + 1] = o1.s; s[c + 2] = o2.s; s[c + 3] = o3.s;
-            *reinterpret_cast<float4*>(a.state + p * C + c) = make_float4(o0.mout, o1.mout, o2.mout, o3.mout);
-            *reinterpret_cast<float4*>(a.state + plane + p * C + c) = make_float4(o0.s, o1.s, o2.s, o3.s);
-        }
-        if constexpr (PRED) {
-            const int64_t b = p / HWp, hw = p - b * HWp;
+    for (int q = 0; q < Q; ++q) {
+        const Lif4 o = lif_step4(yv[q], mv[q], coef + 4 * q, zr);
+        st4[p * Q + q] = o.mout;
+        st4[plane4 + p * Q + q] = o.s;
+        s[4 * q] = o.s.x; s[4 * q + 1] = o.s.y; s[4 * q + 2] = o.s.z; s[4 * q + 3] = o.s.w;
+    }
+    if constexpr (PRED) {
+        const int64_t b = p / HWp, hw = p - b * HWp;
+        const cfloat_ptr pw = as_const(a.pred_w);
 #pragma unroll
-            for (int o = 0; o < 2; ++o) {
-                float acc = 0.0f;
+        for (int o = 0; o < 2; ++o) {
+            float acc = 0.0f;
 #pragma unroll
-                for (int c = 0; c < C; ++c) acc = fmaf(a.pred_w[o * C + c], s[c], acc);
-                a.flow[(b * 2 + o) * HWp + hw] = tanhf(acc + a.pred_b[o]);
-            }
+            for (int c = 0; c < C; ++c) acc = fmaf(pw[o * C + c], s[c], acc);
+            a.flow[(b * 2 + o) * HWp + hw] = tanhf(acc + a.pred_b[o]);
         }
     }
 }
 
+// Surrogate-gradient backward of the top LIF (+ pred): one thread per pixel; BN/neuron
+// sums into acc (block partials, fp64 atomics).
 template <int C, bool PRED>
 __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
-    constexpr int NV = 3 * C + (PRED ? 2 * C + 2 : 0);
+    constexpr int NV = 3 * C + (PRED ? 2 * C + 2 : 0), Q = C / 4;
     __shared__ LifCoef coef[C];
     __shared__ float meanv[C];
     const int tid = threadIdx.x;
+    const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
+    const int64_t p = (int64_t)blockIdx.x * NT + tid;
+    const bool act = p < npix;
+    const int64_t pc = act ? p : npix - 1;
+    const int64_t b = pc / HWp, hw = pc - b * HWp;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    // loads first
+    float4 yv[Q], mv[Q], gs[Q];
+    const float4* y4 = reinterpret_cast<const float4*>(a.y);
+    const float4* m4 = reinterpret_cast<const float4*>(a.mem);
+    const float4* go4 = reinterpret_cast<const float4*>(a.g_out);
+    const float4* gst4 = reinterpret_cast<const float4*>(a.g_state);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        yv[q] = y4[pc * Q + q];  // unconditional 16-B loads (clamped pixel)
+        mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
+        float4 g = ld4_or_zero(go4, y4, pc * Q + q);
+        const float4 t = ld4_or_zero(gst4 ? gst4 + plane4 : nullptr, y4, pc * Q + q);
+        if (gst4) g = make_float4(g.x + t.x, g.y + t.y, g.z + t.z, g.w + t.w);
+        gs[q] = g;
+    }
+    float fl[2] = {0.f, 0.f}, gf[2] = {0.f, 0.f};
+    if constexpr (PRED) {
+        if (a.g_flow) {
+#pragma unroll
+            for (int o = 0; o < 2; ++o) {
+                fl[o] = a.flow[(b * 2 + o) * HWp + hw];
+                gf[o] = a.g_flow[b * a.gflow_sb + o * a.gflow_sc + hw];
+            }
+        }
+    }
     zero_consumed(a.zero0, a.zero1, a.zero_n);
     if (tid < C) {
         coef[tid] = lif_coef(a.n, a.stats, C, tid);
@@ -500,59 +695,70 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
     }
     __syncthreads();
     const bool zr = a.n.zero_reset != 0;
-    const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane = npix * C;
     float v[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) v[j] = 0.0f;
-    for (int64_t p = (int64_t)blockIdx.x * NT + tid; p < npix; p += (int64_t)gridDim.x * NT) {
-        float gs[C];
+    float gpre[2] = {0.0f, 0.0f};
+    if constexpr (PRED) {
+        if (act && a.g_flow) {
 #pragma unroll
-        for (int c = 0; c < C; ++c) gs[c] = 0.0f;
-        if (a.g_out) {
-#pragma unroll
-            for (int c = 0; c < C; ++c) gs[c] = a.g_out[p * C + c];
+            for (int o = 0; o < 2; ++o) gpre[o] = gf[o] * (1.0f - fl[o] * fl[o]);  // tanh backward
         }
-        if (a.g_state) {
+    }
+    if (act) {
+        const cfloat_ptr pw = as_const(a.pred_w);
+        float4* gc4 = reinterpret_cast<float4*>(a.g_cur);
+        float4* gm4 = reinterpret_cast<float4*>(a.g_mem);
 #pragma unroll
-            for (int c = 0; c < C; ++c) gs[c] = gs[c] + a.g_state[plane + p * C + c];
-        }
-        float gpre[2] = {0.0f, 0.0f};
-        if constexpr (PRED) {
-            if (a.g_flow) {
-                const int64_t b = p / HWp, hw = p - b * HWp;
+        for (int q = 0; q < Q; ++q) {
+            const float yi[4] = {yv[q].x, yv[q].y, yv[q].z, yv[q].w};
+            const float mi[4] = {mv[q].x, mv[q].y, mv[q].z, mv[q].w};
+            const float gi[4] = {gs[q].x, gs[q].y, gs[q].z, gs[q].w};
+            float go[4], gmo[4];
 #pragma unroll
-                for (int o = 0; o < 2; ++o) {
-                    const float f = a.flow[(b * 2 + o) * HWp + hw];
-                    const float g = a.g_flow[b * a.gflow_sb + o * a.gflow_sc + hw];
-                    gpre[o] = g * (1.0f - f * f);  // tanh backward
+            for (int j = 0; j < 4; ++j) {
+                const int c = 4 * q + j;
+                float g = gi[j];
+                if constexpr (PRED) {
+                    if (a.g_flow) g = g + (pw[c] * gpre[0] + pw[C + c] * gpre[1]);
                 }
-#pragma unroll
-                for (int c = 0; c < C; ++c)
-                    gs[c] = gs[c] + (a.pred_w[c] * gpre[0] + a.pred_w[C + c] * gpre[1]);
+                const LifOut o = lif_step(yi[j], mi[j], coef[c], zr);
+                const float gv = atan_sg(o.v - coef[c].theta) * g;
+                go[j] = gv;
+                gmo[j] = mem_grad(gv, mi[j], coef[c], zr);
+                v[c] += gv;
+                v[C + c] += (yi[j] - meanv[c]) * gv;
+                v[2 * C + c] += gv * o.mprime;
+                if constexpr (PRED) {
+                    v[3 * C + c] += gpre[0] * o.s;
+                    v[4 * C + c] += gpre[1] * o.s;
+                }
             }
-        }
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const float yy = a.y[p * C + c];
-            const float mm = a.mem ? a.mem[p * C + c] : 0.0f;
-            const LifOut o = lif_step(yy, mm, coef[c], zr);
-            const float gv = atan_sg(o.v - coef[c].theta) * gs[c];
-            a.g_cur[p * C + c] = gv;
-            if (a.g_mem) a.g_mem[p * C + c] = mem_grad(gv, mm, coef[c], zr);
-            v[c] += gv;
-            v[C + c] += (yy - meanv[c]) * gv;
-            v[2 * C + c] += gv * o.mprime;
-            if constexpr (PRED) {
-                v[3 * C + c] += gpre[0] * o.s;
-                v[4 * C + c] += gpre[1] * o.s;
-            }
+            gc4[p * Q + q] = make_float4(go[0], go[1], go[2], go[3]);
+            if (gm4) gm4[p * Q + q] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
         }
         if constexpr (PRED) {
             v[5 * C] += gpre[0];
             v[5 * C + 1] += gpre[1];
         }
     }
-    block_atomic_sum<NV>(v, a.acc);
+    if (!PROBE_OFF(4)) block_atomic_sum<NV>(v, acc_shard(a.acc, SNNFLOW_BWD_ACC(C)));
+}
+
+// BatchNorm backward of one float4 of channels (torch batch_norm_cpu_backward, train):
+// dx = ((g - grad_mean) - (y - mean) * k) * invstd * gamma.
+struct BnBwdLds { float mean, inv, gm, k, w; };
+
+__device__ inline float4 bn_bwd4(const float4& g, const float4& y, const BnBwdLds* bp) {
+    const float gi[4] = {g.x, g.y, g.z, g.w}, yi[4] = {y.x, y.y, y.z, y.w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const BnBwdLds c = bp[j];
+        const float dx = (yi[j] - c.mean) * c.k;
+        o[j] = (((gi[j] - c.gm) - dx) * c.inv) * c.w;
+    }
+    return make_float4(o[0], o[1], o[2], o[3]);
 }
 
 template <int CIN, int C, bool LIF_IN, bool REC>
@@ -560,37 +766,89 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
     using WS = WgradShape<CIN, C>;
     using WR = WgradShape<C, C>;
     constexpr int PI_ = Pad<CIN>::v, PC = Pad<C>::v;
-    constexpr int PX = (REC && PC > PI_) ? PC : PI_;
+    constexpr bool PF = Prefetch<C>::on;                 // halo tiles held in registers
+    constexpr bool PFX = PF && Prefetch<CIN>::on;        // x halo prefetchable (dense NHWC)
+    constexpr bool SEP = REC && PF;                      // s_prev gets its own LDS tile
+    constexpr int PX = (REC && !SEP && PC > PI_) ? PC : PI_;
     constexpr int SCR = (WS::SCRATCH > WR::SCRATCH) ? WS::SCRATCH : WR::SCRATCH;
+    constexpr int NVP = LIF_IN ? 3 * CIN : 1;
+    constexpr int QI = CIN / 4 > 0 ? CIN / 4 : 1;
     __shared__ __attribute__((aligned(16))) float G[HN * PC];
     __shared__ __attribute__((aligned(16))) float X[HN * PX];
+    __shared__ __attribute__((aligned(16))) float S[SEP ? HN * PC : 4];
     __shared__ __attribute__((aligned(16))) float scratch[SCR];
-    __shared__ float bn_mean[C], bn_inv[C], bn_gm[C], bn_k[C], bn_w[C];
+    __shared__ BnBwdLds bnp[C];
     __shared__ LifCoef pcoef[LIF_IN ? CIN : 1];
     __shared__ float pmean[LIF_IN ? CIN : 1];
-    constexpr int NVP = LIF_IN ? 3 * CIN : 1;
 
     const int tid = threadIdx.x, ty = tid / TW, tx = tid - ty * TW;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
     const double N = (double)a.B * H * W;
     const float nf = (float)N;
-    zero_consumed(a.zero0, a.zero1, a.zero_n);
-    neuron_grads(a.n, a.stats, a.acc_in, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b);
+    const int h = tl.h0 + ty, w = tl.w0 + tx;
+    const bool in = (h < H) && (w < W);
+    const int64_t pix = ((int64_t)tl.b * H + h) * W + w;
+    const bool has_rec = REC && a.s_prev != nullptr;
+    bool dense = false;
+    if constexpr (CIN % 4 == 0)
+        dense = a.xs_c == 1 && a.xs_w == CIN && a.xs_h == (int64_t)W * CIN && a.xs_b == (int64_t)H * W * CIN;
+    float* slab_ff = a.slab_ff + (int64_t)blockIdx.x * (C * CIN * 9);
+    float* slab_rec = REC ? a.slab_rec + (int64_t)blockIdx.x * (C * C * 9) : nullptr;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
+    // 1. every global load of the kernel, issued up front (register prefetch)
+    float4 rg[PF ? Halo4<C>::R : 1], ry[PF ? Halo4<C>::R : 1];
+    float4 rx[PFX ? Halo4<CIN>::R : 1], rs[SEP ? Halo4<C>::R : 1];
+    float4 dy[LIF_IN ? QI : 1], dm[LIF_IN ? QI : 1], dg[LIF_IN ? QI : 1];
+    float oldff[WS::NO], oldrec[REC ? WR::NO : 1];
+    if constexpr (PF) {
+        halo_load<C>(a.g_cur, tl, H, W, rg);
+        halo_load<C>(a.y, tl, H, W, ry);
+    }
+    if constexpr (PFX) {
+        if (dense) halo_load<CIN>(a.x, tl, H, W, rx);
+    }
+    if constexpr (SEP) {
+        if (has_rec) halo_load<C>(a.s_prev, tl, H, W, rs);
+    }
+    if constexpr (LIF_IN) {
+        const int64_t plane4 = (int64_t)a.B * H * W * QI;
+        const float4* py4 = reinterpret_cast<const float4*>(a.prev_y);
+        const float4* pm4 = reinterpret_cast<const float4*>(a.prev_mem);
+        const float4* pg4 = reinterpret_cast<const float4*>(a.prev_g_state);
+        // unconditional 16-B loads (clamped pixel outside the image; results unused there)
+        const int64_t pc = ((int64_t)tl.b * H + (h < H ? h : H - 1)) * W + (w < W ? w : W - 1);
+#pragma unroll
+        for (int q = 0; q < QI; ++q) {
+            dy[q] = py4[pc * QI + q];
+            dm[q] = ld4_or_zero(pm4, py4, pc * QI + q);
+            dg[q] = ld4_or_zero(pg4 ? pg4 + plane4 : nullptr, py4, pc * QI + q);
+        }
+    }
+    slab_prefetch<CIN, C>(slab_ff, a.accumulate, oldff);
+    if constexpr (REC) slab_prefetch<C, C>(slab_rec, a.accumulate && has_rec, oldrec);
+
+    // 2. per-channel constants; block 0 finishes layer l's neuron gradients
+    zero_consumed(a.zero0, a.zero1, a.zero_n);
+    __shared__ double sums[SNNFLOW_BWD_ACC(C)];
+    acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
+    neuron_grads(a.n, a.stats, sums, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b);
     if (tid < C) {
         const float mean = a.stats[tid], inv = a.stats[C + tid];
-        bn_mean[tid] = mean;
-        bn_inv[tid] = inv;
-        bn_w[tid] = a.n.bn_weight[tid];
+        BnBwdLds c;
+        c.mean = mean;
+        c.inv = inv;
+        c.w = a.n.bn_weight[tid];
         if (a.n.bn_train) {
             // torch batch_norm_cpu_backward: k = dotp*invstd*invstd/n, grad_mean = sum/n
-            bn_k[tid] = (float)a.acc_in[C + tid] * inv * inv / nf;
-            bn_gm[tid] = (float)(a.acc_in[tid] / N);
+            c.k = (float)sums[C + tid] * inv * inv / nf;
+            c.gm = (float)(sums[tid] / N);
         } else {
-            bn_k[tid] = 0.0f;
-            bn_gm[tid] = 0.0f;
+            c.k = 0.0f;
+            c.gm = 0.0f;
         }
+        bnp[tid] = c;
     }
     if constexpr (LIF_IN) {
         if (tid < CIN) {
@@ -600,51 +858,62 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
     }
     __syncthreads();
 
-    // Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l)
-    for (int e = tid; e < HN * (C / 4); e += NT) {
-        const int p = e / (C / 4), q = e - p * (C / 4);
-        const int r = p / HWD, cc = p - r * HWD;
-        const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-        float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (in_image(h, w, H, W)) {
-            const int64_t off = (((int64_t)tl.b * H + h) * W + w) * C + 4 * q;
-            const float4 g = *reinterpret_cast<const float4*>(a.g_cur + off);
-            const float4 yv = *reinterpret_cast<const float4*>(a.y + off);
-            const float gi[4] = {g.x, g.y, g.z, g.w}, yi[4] = {yv.x, yv.y, yv.z, yv.w};
-            float o[4];
+    // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l);
+    //    input halos into X / S
+    if constexpr (PF) {
+        constexpr int Q = C / 4;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int c = 4 * q + j;
-                const float dx = (yi[j] - bn_mean[c]) * bn_k[c];
-                o[j] = (((gi[j] - bn_gm[c]) - dx) * bn_inv[c]) * bn_w[c];
+        for (int i = 0; i < Halo4<C>::R; ++i) {
+            const int e = tid + i * NT;
+            if (e < Halo4<C>::E) {
+                const int p = e / Q, q = e - p * Q;
+                const int r = p / HWD, cc = p - r * HWD;
+                const bool img = in_image(tl.h0 + r - 1, tl.w0 + cc - 1, H, W);
+                *reinterpret_cast<float4*>(G + p * PC + 4 * q) = img ? bn_bwd4(rg[i], ry[i], bnp + 4 * q) : z4;
             }
-            out = make_float4(o[0], o[1], o[2], o[3]);
         }
-        *reinterpret_cast<float4*>(G + p * PC + 4 * q) = out;
+    } else {
+        constexpr int Q = C / 4;
+        for (int e = tid; e < Halo4<C>::E; e += NT) {
+            const int p = e / Q, q = e - p * Q;
+            const int64_t k = halo_idx4<C>(e, tl, H, W);
+            float4 out = z4;
+            if (k >= 0)
+                out = bn_bwd4(reinterpret_cast<const float4*>(a.g_cur)[k], reinterpret_cast<const float4*>(a.y)[k],
+                              bnp + 4 * q);
+            *reinterpret_cast<float4*>(G + p * PC + 4 * q) = out;
+        }
+    }
+    if constexpr (PFX) {
+        if (dense) halo_store<CIN>(X, rx);
+    } else if constexpr (CIN % 4 == 0) {
+        if (dense) stage_nhwc<CIN>(a.x, tl, H, W, X);
+    }
+    if (!dense) stage_strided<CIN>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, X);
+    if constexpr (SEP) {
+        if (has_rec) halo_store<C>(S, rs);
     }
     __syncthreads();
 
-    const int h = tl.h0 + ty, w = tl.w0 + tx;
-    const bool in = (h < H) && (w < W);
-    const int64_t pix = ((int64_t)tl.b * H + h) * W + w;
-
-    // Stage B: input gradient (dgrad) of ff and rec convolutions
+    // 4. Stage B: input gradient (dgrad) of ff and rec convolutions
     float gx[CIN];
 #pragma unroll
     for (int ci = 0; ci < CIN; ++ci) gx[ci] = 0.0f;
-    if (a.wt_bwd_ff) dgrad_acc<C, CIN>(G, a.wt_bwd_ff, ty, tx, gx);
+    if (!PROBE_OFF(1) && a.wt_bwd_ff) dgrad_acc<C, CIN>(G, a.wt_bwd_ff, ty, tx, gx);
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (REC) {
         if (a.g_state_prev) {
             float gr[C];
 #pragma unroll
             for (int c = 0; c < C; ++c) gr[c] = 0.0f;
-            dgrad_acc<C, C>(G, a.wt_bwd_rec, ty, tx, gr);
+            if (!PROBE_OFF(1)) dgrad_acc<C, C>(G, a.wt_bwd_rec, ty, tx, gr);
+            pin(gr);  // keep the dgrad out of the `in` branch (sinking it there spills SGPRs)
             if (in) {
                 const int64_t plane = (int64_t)a.B * H * W * C;
 #pragma unroll
                 for (int c = 0; c < C; c += 4) {
                     if (a.zero_mem_half)
-                        *reinterpret_cast<float4*>(a.g_state_prev + pix * C + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+                        *reinterpret_cast<float4*>(a.g_state_prev + pix * C + c) = z4;
                     *reinterpret_cast<float4*>(a.g_state_prev + plane + pix * C + c) =
                         make_float4(gr[c], gr[c + 1], gr[c + 2], gr[c + 3]);
                 }
@@ -652,53 +921,38 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
         }
     }
 
-    // Stage C: weight gradients (per-block slabs)
-    const int64_t blk = blockIdx.x;
-    bool dense = false;
-    if constexpr (CIN % 4 == 0)
-        dense = a.xs_c == 1 && a.xs_w == CIN && a.xs_h == (int64_t)W * CIN && a.xs_b == (int64_t)H * W * CIN;
-    if constexpr (CIN % 4 == 0) {
-        if (dense) stage_nhwc<CIN>(a.x, tl, H, W, X);
-    }
-    if (!dense) stage_strided<CIN>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, X);
-    __syncthreads();
-    wgrad_tile<CIN, C>(G, X, a.slab_ff + blk * (C * CIN * 9), a.accumulate, scratch);
-    if constexpr (REC) {
-        float* slab = a.slab_rec + blk * (C * C * 9);
-        if (a.s_prev) {
-            __syncthreads();
-            stage_nhwc<C>(a.s_prev, tl, H, W, X);
-            __syncthreads();
-            wgrad_tile<C, C>(G, X, slab, a.accumulate, scratch);
-        } else if (!a.accumulate) {
-            for (int e = tid; e < C * C * 9; e += NT) slab[e] = 0.0f;
-        }
-    }
-
-    // Stage D: LIF backward of layer l-1 on the dgrad result, or the plain input gradient
+    // 5. Stage D: LIF backward of layer l-1 on the dgrad result, or the plain input gradient
+    //    (before the weight gradients so its stores drain behind them)
+    float vd[NVP];
+#pragma unroll
+    for (int j = 0; j < NVP; ++j) vd[j] = 0.0f;
     if constexpr (LIF_IN) {
-        float v[NVP];
-#pragma unroll
-        for (int j = 0; j < NVP; ++j) v[j] = 0.0f;
-        if (in) {
+        if (in && !PROBE_OFF(8)) {
             const bool zr = a.prev.zero_reset != 0;
-            const int64_t plane = (int64_t)a.B * H * W * CIN;
+            float4* gc4 = reinterpret_cast<float4*>(a.prev_g_cur);
+            float4* gm4 = reinterpret_cast<float4*>(a.prev_g_mem);
 #pragma unroll
-            for (int ci = 0; ci < CIN; ++ci) {
-                float gs = gx[ci];
-                if (a.prev_g_state) gs = gs + a.prev_g_state[plane + pix * CIN + ci];
-                const float yy = a.prev_y[pix * CIN + ci];
-                const float mm = a.prev_mem ? a.prev_mem[pix * CIN + ci] : 0.0f;
-                const LifOut o = lif_step(yy, mm, pcoef[ci], zr);
-                const float gv = atan_sg(o.v - pcoef[ci].theta) * gs;
-                a.prev_g_cur[pix * CIN + ci] = gv;
-                if (a.prev_g_mem) a.prev_g_mem[pix * CIN + ci] = mem_grad(gv, mm, pcoef[ci], zr);
-                v[ci] = gv;
-                v[CIN + ci] = (yy - pmean[ci]) * gv;
-                v[2 * CIN + ci] = gv * o.mprime;
+            for (int q = 0; q < QI; ++q) {
+                const float yi[4] = {dy[q].x, dy[q].y, dy[q].z, dy[q].w};
+                const float mi[4] = {dm[q].x, dm[q].y, dm[q].z, dm[q].w};
+                const float gi[4] = {dg[q].x, dg[q].y, dg[q].z, dg[q].w};
+                float go[4], gmo[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int ci = 4 * q + j;
+                    const float gs = gx[ci] + gi[j];
+                    const LifOut o = lif_step(yi[j], mi[j], pcoef[ci], zr);
+                    const float gv = atan_sg(o.v - pcoef[ci].theta) * gs;
+                    go[j] = gv;
+                    gmo[j] = mem_grad(gv, mi[j], pcoef[ci], zr);
+                    vd[ci] = gv;
+                    vd[CIN + ci] = (yi[j] - pmean[ci]) * gv;
+                    vd[2 * CIN + ci] = gv * o.mprime;
+                }
+                gc4[pix * QI + q] = make_float4(go[0], go[1], go[2], go[3]);
+                if (gm4) gm4[pix * QI + q] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
             }
         }
-        block_atomic_sum<NVP>(v, a.acc_out);
     } else {
         if (a.g_x && a.wt_bwd_ff && in) {
             float* gb = a.g_x + (int64_t)tl.b * a.gxs_b + h * a.gxs_h + w * a.gxs_w;
@@ -706,20 +960,60 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
             for (int ci = 0; ci < CIN; ++ci) gb[ci * a.gxs_c] = gx[ci];
         }
     }
+
+    // 6. Stage C: weight gradients (per-block slabs)
+    if (!PROBE_OFF(2)) wgrad_tile<CIN, C>(G, X, slab_ff, oldff, scratch);
+    if constexpr (REC) {
+        if (has_rec) {
+            const float* st = X;
+            if constexpr (SEP) {
+                st = S;
+            } else {
+                __syncthreads();
+                stage_nhwc<C>(a.s_prev, tl, H, W, X);
+                __syncthreads();
+            }
+            if (!PROBE_OFF(2)) wgrad_tile<C, C>(G, st, slab_rec, oldrec, scratch);
+        } else if (!a.accumulate) {
+            for (int e = tid; e < C * C * 9; e += NT) slab_rec[e] = 0.0f;
+        }
+    }
+    if constexpr (LIF_IN) {
+        if (!PROBE_OFF(4)) block_atomic_sum<NVP>(vd, acc_shard(a.acc_out, SNNFLOW_BWD_ACC(CIN)));
+    }
 }
 
-__global__ void k_slab_reduce(snnflow_slab_desc d0, snnflow_slab_desc d1, snnflow_slab_desc d2, snnflow_slab_desc d3,
-                              snnflow_slab_desc d4, snnflow_slab_desc d5, snnflow_slab_desc d6, snnflow_slab_desc d7,
-                              snnflow_slab_desc d8, snnflow_slab_desc d9, snnflow_slab_desc d10, snnflow_slab_desc d11,
-                              snnflow_slab_desc d12, snnflow_slab_desc d13, snnflow_slab_desc d14, snnflow_slab_desc d15,
-                              int nblk) {
-    const snnflow_slab_desc ds[16] = {d0, d1, d2, d3, d4, d5, d6, d7, d8, d9, d10, d11, d12, d13, d14, d15};
-    const snnflow_slab_desc d = ds[blockIdx.y];
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= d.elems) return;
-    double s = 0.0;
-    for (int b = 0; b < nblk; ++b) s += d.slab[(int64_t)b * d.elems + e];
-    d.out[e] = (float)s;
+// Sum of per-block weight-gradient slabs in fp64, fixed order: 64 elements x 16 slab
+// groups per 1024-thread block, 4 independent accumulators per thread.
+constexpr int SR_E = 64, SR_G = 16;
+
+__global__ __launch_bounds__(SR_E * SR_G) void k_slab_reduce(DescBatch<snnflow_slab_desc> batch, int nblk) {
+    __shared__ double part[SR_G][SR_E];
+    const snnflow_slab_desc d = batch.pick(blockIdx.y);
+    const int le = threadIdx.x % SR_E, g = threadIdx.x / SR_E;
+    const int e = blockIdx.x * SR_E + le;
+    if (blockIdx.x * SR_E >= d.elems) return;  // uniform per block
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if (e < d.elems) {
+        const float* src = d.slab + e;
+        const int64_t st = d.elems;
+        int b = g;
+        for (; b + 3 * SR_G < nblk; b += 4 * SR_G) {
+            s0 += src[(int64_t)b * st];
+            s1 += src[(int64_t)(b + SR_G) * st];
+            s2 += src[(int64_t)(b + 2 * SR_G) * st];
+            s3 += src[(int64_t)(b + 3 * SR_G) * st];
+        }
+        for (; b < nblk; b += SR_G) s0 += src[(int64_t)b * st];
+    }
+    part[g][le] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (g == 0 && e < d.elems) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < SR_G; ++k) s += part[k][le];
+        d.out[e] = (float)s;
+    }
 }
 
 __global__ void k_lif_export(const float* __restrict__ x, const float* __restrict__ mem, const float* __restrict__ beta,
@@ -796,15 +1090,30 @@ const char* snnflow_last_error(void) { return g_err.c_str(); }
 
 int snnflow_conv_blocks(int B, int H, int W) { return B * tiles_per_image(H, W); }
 
+int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream) {
+    if (!d || n <= 0 || n > SNNFLOW_MAX_BATCH) SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: bad count");
+    DescBatch<snnflow_prep_desc> batch = {};
+    int maxe = 1;
+    for (int i = 0; i < n; ++i) {
+        const snnflow_prep_desc& x = d[i];
+        if ((x.w && (x.c <= 0 || x.cin <= 0 || !x.wt_fwd || !x.wt_bwd)) || (!x.w && !x.threshold) ||
+            (x.threshold && x.thr_n <= 0))
+            SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: bad descriptor");
+        batch.d[i] = x;
+        if (x.w && x.c * x.cin * 9 > maxe) maxe = x.c * x.cin * 9;
+        if (x.threshold && x.thr_n > maxe) maxe = x.thr_n;
+    }
+    hipLaunchKernelGGL(k_prep_weights, dim3((maxe + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, batch);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
 int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* wt_bwd, float* threshold,
                          void* stream) {
     if (c <= 0 || cin <= 0 || (w && (!wt_fwd || !wt_bwd)) || (!w && !threshold))
         SNN_FAIL(SNNFLOW_E_ARG, "prep_weights: bad args");
-    const int n = c * cin * 9;
-    hipLaunchKernelGGL(k_prep_weights, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, w, c, cin, wt_fwd,
-                       wt_bwd, threshold);
-    SNN_CHECK_LAUNCH();
-    return 0;
+    snnflow_prep_desc d = {w, c, cin, wt_fwd, wt_bwd, threshold, c};
+    return snnflow_prep_weights_batch(&d, 1, stream);
 }
 
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
@@ -884,16 +1193,15 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
 
 int snnflow_slab_reduce(const snnflow_slab_desc* d, int n, int nblk, void* stream) {
     if (!d || n <= 0 || n > SNNFLOW_MAX_SLABS || nblk <= 0) SNN_FAIL(SNNFLOW_E_ARG, "slab_reduce: bad args");
-    snnflow_slab_desc ds[16] = {};
+    DescBatch<snnflow_slab_desc> batch = {};
     int maxe = 0;
     for (int i = 0; i < n; ++i) {
-        ds[i] = d[i];
+        batch.d[i] = d[i];
         if (!d[i].slab || !d[i].out || d[i].elems <= 0) SNN_FAIL(SNNFLOW_E_ARG, "slab_reduce: bad descriptor");
         maxe = d[i].elems > maxe ? d[i].elems : maxe;
     }
-    hipLaunchKernelGGL(k_slab_reduce, dim3((maxe + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, ds[0], ds[1],
-                       ds[2], ds[3], ds[4], ds[5], ds[6], ds[7], ds[8], ds[9], ds[10], ds[11], ds[12], ds[13], ds[14],
-                       ds[15], nblk);
+    hipLaunchKernelGGL(k_slab_reduce, dim3((maxe + SR_E - 1) / SR_E, n), dim3(SR_E * SR_G), 0, (hipStream_t)stream,
+                       batch, nblk);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -60,6 +60,89 @@ __device__ inline float wave_sum(float v) {
     return v;
 }
 
+// DPP lane exchange (GFX9 encodings): quad_perm [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E,
+// row_half_mirror = 0x141, row_mirror = 0x140.
+template <int CTRL>
+__device__ inline float dppf(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 64 lanes of a wave, result wave-uniform (all lanes must be active).
+// Rows of 16 reduce through DPP (no LDS traffic); the four row totals via readlane.
+__device__ inline float wave_total(float v) {
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    v += dppf<0x140>(v);
+    const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 0));
+    const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 16));
+    const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 32));
+    const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 48));
+    return ((r0 + r1) + r2) + r3;
+}
+
+// Sharded batch-sum accumulators (include/snnflow.h): [shard][acc_stride(n)] doubles.
+constexpr int kAccShards = SNNFLOW_ACC_SHARDS;
+__host__ __device__ constexpr int acc_stride(int n) { return SNNFLOW_ACC_STRIDE(n); }
+
+// This block's replica of an accumulator of n sums.
+__device__ inline double* acc_shard(double* acc, int n) { return acc + (blockIdx.x % kAccShards) * acc_stride(n); }
+
+// p[i] as one unconditional 16-B load, or zeros when p is NULL (the load then reads
+// fallback[i], which must be valid).  A `p ? p[i] : 0` select makes the compiler split
+// the load into four dword loads.
+__device__ inline float4 ld4_or_zero(const float4* p, const float4* fallback, int64_t i) {
+    const float4 t = (p ? p : fallback)[i];
+    return p ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ inline bool in_image(int h, int w, int H, int W) { return h >= 0 && h < H && w >= 0 && w < W; }
+
+// A C-channel NHWC halo tile as float4 elements e = pixel * (C/4) + quad, distributed
+// round-robin over the block's threads (element e -> thread e % NT, slot e / NT), so a
+// thread issues all R of its loads before using any (register prefetch).
+template <int CH>
+struct Halo4 {
+    static constexpr int Q = CH / 4;  // meaningful for CH % 4 == 0 only
+    static constexpr int E = HN * Q;
+    static constexpr int R = (E + NT - 1) / NT;
+};
+
+// float4 index of halo element e in an NHWC tensor with CH channels; -1 outside the tile/image.
+template <int CH>
+__device__ inline int64_t halo_idx4(int e, const Tile& tl, int H, int W) {
+    constexpr int Q = CH / 4;
+    if (e >= HN * Q) return -1;
+    const int p = e / Q, q = e - p * Q;
+    const int r = p / HWD, cc = p - r * HWD;
+    const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+    if (!in_image(h, w, H, W)) return -1;
+    return (((int64_t)tl.b * H + h) * W + w) * Q + q;
+}
+
+template <int CH>
+__device__ inline void halo_load(const float* __restrict__ src, const Tile& tl, int H, int W,
+                                 float4 (&r)[Halo4<CH>::R]) {
+#pragma unroll
+    for (int i = 0; i < Halo4<CH>::R; ++i) {
+        const int64_t k = halo_idx4<CH>(threadIdx.x + i * NT, tl, H, W);
+        r[i] = (k >= 0) ? reinterpret_cast<const float4*>(src)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+template <int CH>
+__device__ inline void halo_store(float* tile, const float4 (&r)[Halo4<CH>::R]) {
+    constexpr int Q = CH / 4;
+#pragma unroll
+    for (int i = 0; i < Halo4<CH>::R; ++i) {
+        const int e = threadIdx.x + i * NT;
+        if (e < Halo4<CH>::E) {
+            const int p = e / Q, q = e - p * Q;
+            *reinterpret_cast<float4*>(tile + p * Pad<CH>::v + 4 * q) = r[i];
+        }
+    }
+}
+
 // Per-channel LIF coefficients: I = y*alpha + shift (torch CPU BN transform order:
 // alpha = invstd*gamma, shift = bias - mean*alpha), beta clamped to [0,1].
 struct LifCoef { float alpha, shift, beta, theta; };

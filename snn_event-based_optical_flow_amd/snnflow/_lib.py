@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 3
+ABI_VERSION = 5
 
 
 class Neuron(ctypes.Structure):
@@ -70,12 +70,29 @@ class LayerBwdArgs(ctypes.Structure):
                 ("zero0", P), ("zero1", P), ("zero_n", I32)]
 
 
+ACC_SHARDS = 32  # SNNFLOW_ACC_SHARDS
+
+
 def bwd_acc_len(c):
+    """Sums per layer of the backward accumulator (SNNFLOW_BWD_ACC)."""
     return 5 * c + 2
+
+
+def acc_storage(n):
+    """Doubles occupied by a sharded accumulator of n sums (SNNFLOW_ACC_LEN)."""
+    return ACC_SHARDS * ((n + 15) // 16 * 16)
 
 
 class SlabDesc(ctypes.Structure):
     _fields_ = [("slab", P), ("out", P), ("elems", I32)]
+
+
+class PrepDesc(ctypes.Structure):
+    _fields_ = [("w", P), ("c", I32), ("cin", I32), ("wt_fwd", P), ("wt_bwd", P),
+                ("threshold", P), ("thr_n", I32)]
+
+
+MAX_BATCH = 16
 
 
 class IweLossArgs(ctypes.Structure):
@@ -91,6 +108,7 @@ EXPORTS = {
     "snnflow_last_error": (ctypes.c_char_p, []),
     "snnflow_conv_blocks": (I32, [I32, I32, I32]),
     "snnflow_prep_weights": (I32, [P, I32, I32, P, P, P, P]),
+    "snnflow_prep_weights_batch": (I32, [ctypes.POINTER(PrepDesc), I32, P]),
     "snnflow_conv_fwd": (I32, [ctypes.POINTER(ConvFwdArgs), P]),
     "snnflow_lif_fwd": (I32, [ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_lif_bwd": (I32, [ctypes.POINTER(LifBwdArgs), P]),

@@ -75,8 +75,9 @@ class Workspace:
         self.key = (B, H, W, C, device)
         self.B, self.H, self.W, self.C = B, H, W, C
         self.nblk = lib.snnflow_conv_blocks(B, H, W)
-        self.fwd_acc = torch.zeros(max(layers, 1), 2 * C, dtype=torch.float64, device=device)
-        self.bwd_acc = torch.zeros(max(layers, 1), _lib.bwd_acc_len(C), dtype=torch.float64, device=device)
+        self.fwd_acc = torch.zeros(max(layers, 1), _lib.acc_storage(2 * C), dtype=torch.float64, device=device)
+        self.bwd_acc = torch.zeros(max(layers, 1), _lib.acc_storage(_lib.bwd_acc_len(C)), dtype=torch.float64,
+                                   device=device)
         self.gcur = torch.empty(2, B, H, W, C, dtype=torch.float32, device=device)
         self.slab_ff = []
         self.slab_rec = []
@@ -98,29 +99,43 @@ class Workspace:
 
 class PreppedWeights:
     """Transposed conv weights [3][3][Cin][C] / [3][3][C][Cin] + in-place threshold clamp
-    (reference: ``threshold.data.clamp_(min=0.01)`` at every cell forward).  Cached
-    on parameter versions: recomputed after every optimizer step."""
+    (reference: ``threshold.data.clamp_(min=0.01)`` at every cell forward,
+    SNNtorch_spiking_submodules.py:284 / :516).
+
+    Refreshed by one batched launch at every forward call: parameter version counters
+    cannot key a cache (fused optimizers and ``.data`` writes update weights without
+    bumping them), and a hipGraph replay must re-read the weights anyway.  The
+    backward pass reuses the buffers of the last forward (same weights)."""
 
     def __init__(self):
-        self.key = None
         self.fwd = {}
         self.bwd = {}
 
-    def ensure(self, weights, thresholds, stream):
-        key = tuple((w.data_ptr(), w._version) for w in weights) + tuple((t.data_ptr(), t._version) for t in thresholds)
-        if key == self.key:
-            return
+    def ensure(self, weights, thresholds, stream, refresh=True):
+        fresh = False
         for i, w in enumerate(weights):
-            c, cin = w.shape[0], w.shape[1]
             f = self.fwd.get(i)
             if f is None or f.numel() != w.numel() or f.device != w.device:
-                self.fwd[i] = torch.empty(9 * cin * c, device=w.device)
-                self.bwd[i] = torch.empty(9 * cin * c, device=w.device)
-            _lib.call("prep_weights", lib.snnflow_prep_weights, ptr(w.detach().contiguous()), c, cin, ptr(self.fwd[i]), ptr(self.bwd[i]),
-                                           None, stream)
-        for t in thresholds:
-            _lib.call("threshold clamp", lib.snnflow_prep_weights, None, t.numel(), 1, None, None, ptr(t), stream)
-        self.key = key
+                self.fwd[i] = torch.empty(w.numel(), device=w.device)
+                self.bwd[i] = torch.empty(w.numel(), device=w.device)
+                fresh = True
+        if not (refresh or fresh):
+            return
+        descs = []
+        for i, w in enumerate(weights):
+            c, cin = w.shape[0], w.shape[1]
+            if not w.is_contiguous():
+                raise _lib.SnnflowError("conv weight must be contiguous")
+            descs.append(_lib.PrepDesc(ptr(w), c, cin, ptr(self.fwd[i]), ptr(self.bwd[i]), None, 0))
+        for i, t in enumerate(thresholds):  # ride along with the weight descriptors
+            if i < len(descs):
+                descs[i].threshold, descs[i].thr_n = ptr(t), t.numel()
+            else:
+                descs.append(_lib.PrepDesc(None, 0, 0, None, None, ptr(t), t.numel()))
+        for i0 in range(0, len(descs), _lib.MAX_BATCH):
+            chunk = descs[i0:i0 + _lib.MAX_BATCH]
+            _lib.call("prep_weights", lib.snnflow_prep_weights_batch, (_lib.PrepDesc * len(chunk))(*chunk),
+                      len(chunk), stream)
 
 
 # ---------------------------------------------------------------------------
@@ -159,13 +174,13 @@ class FireNetEngine:
         self.ws.slabs([(c.input_size, r) for c, r in zip(self.cells, self.rec)])
         return self.ws
 
-    def prep_weights(self, stream):
+    def prep_weights(self, stream, refresh=True):
         ws = []
         for cell, rec in zip(self.cells, self.rec):
             ws.append(cell.ff.weight)
             if rec:
                 ws.append(cell.rec.weight)
-        self.prep.ensure(ws, [c.lif.threshold for c in self.cells], stream)
+        self.prep.ensure(ws, [c.lif.threshold for c in self.cells], stream, refresh)
         # map layer -> prepped buffers
         fwd, bwd, i = [], [], 0
         for rec in self.rec:
@@ -183,11 +198,13 @@ class FireNetEngine:
         params = self.param_list()
         total = sum(p.numel() for p in params)
         self.flat = torch.empty(total, device=device)
-        views, off = [], 0
+        views, layout, off = [], [], 0
         for p in params:
             views.append(self.flat[off:off + p.numel()].view_as(p))
+            layout.append((off, p.numel(), p.shape))
             off += p.numel()
         self.flat_views = views
+        self.flat_layout = layout
         self.bwd_open = True
 
     def grad_views(self):
@@ -255,7 +272,7 @@ class FireNetStep(torch.autograd.Function):
         neurons = [neuron_struct(c) for c in cells]
         train = [c.bn.training or not c.bn.track_running_stats for c in cells]
         facc = ws.fwd_acc
-        zn = 2 * C
+        zn = facc.shape[1]
         try:
             # K0: conv(head)  (zeroes fwd_acc[L-1], consumed by the previous step's last kernel)
             a = _lib.ConvFwdArgs()
@@ -328,7 +345,7 @@ class FireNetStep(torch.autograd.Function):
         dev = x.device
         s = _lib.stream_ptr(dev)
         ws = eng.workspace(B, H, W, dev)
-        _, wbwd = eng.prep_weights(s)
+        _, wbwd = eng.prep_weights(s, refresh=False)
         if not eng.bwd_open:
             eng.open_chain(dev)
             acc = 0
@@ -411,7 +428,7 @@ class FireNetStep(torch.autograd.Function):
             eng.bwd_open = False
             raise
 
-        grads = [None] * len(eng.flat_views)
+        grads = [None] * len(eng.flat_layout)
         if ctx.root:
             descs = []
             for l in range(L):
@@ -422,7 +439,10 @@ class FireNetStep(torch.autograd.Function):
             for i0 in range(0, len(descs), 16):
                 chunk = (_lib.SlabDesc * len(descs[i0:i0 + 16]))(*descs[i0:i0 + 16])
                 _lib.call("slab_reduce", lib.snnflow_slab_reduce, chunk, len(descs[i0:i0 + 16]), ws.nblk, s)
-            grads = list(eng.flat_views)
+            # fresh views, no other reference: AccumulateGrad adopts them as .grad
+            # instead of copying (all gradients then live in one flat buffer)
+            grads = [eng.flat[o:o + n].view(shp) for o, n, shp in eng.flat_layout]
+            eng.flat_views = None
             eng.bwd_open = False
             eng.last_flat = eng.flat
         return (None, gx, *g_prev, *grads)

@@ -36,13 +36,17 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_neuron": _lib.Neuron, "snnflow_neuron_grad": _lib.NeuronGrad,
         "snnflow_conv_fwd_args": _lib.ConvFwdArgs, "snnflow_lif_fwd_args": _lib.LifFwdArgs,
         "snnflow_lif_bwd_args": _lib.LifBwdArgs, "snnflow_layer_bwd_args": _lib.LayerBwdArgs,
-        "snnflow_slab_desc": _lib.SlabDesc, "snnflow_iwe_loss_args": _lib.IweLossArgs,
+        "snnflow_slab_desc": _lib.SlabDesc, "snnflow_prep_desc": _lib.PrepDesc, "snnflow_iwe_loss_args": _lib.IweLossArgs,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
         for fname, _ in py._fields_:
             lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    for c_ in (4, 8, 16, 32):  # accumulator sizing macros vs the Python mirror
+        lines.append(f'printf("acc_fwd_{c_} %d\\n", SNNFLOW_ACC_LEN(2 * {c_}));')
+        lines.append(f'printf("acc_bwd_{c_} %d\\n", SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC({c_})));')
+    lines.append(f'printf("abi %d\\n", SNNFLOW_ABI_VERSION);')
     lines.append("return 0;}")
     c = tmp_path / "layout.c"
     c.write_text("\n".join(lines))
@@ -50,6 +54,10 @@ def test_struct_layouts_match_c(tmp_path):
     subprocess.run(["gcc", "-std=c11", str(c), "-o", str(exe)], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
     got = dict(line.rsplit(" ", 1) for line in out if line)
+    for c_ in (4, 8, 16, 32):
+        assert int(got[f"acc_fwd_{c_}"]) == _lib.acc_storage(2 * c_)
+        assert int(got[f"acc_bwd_{c_}"]) == _lib.acc_storage(_lib.bwd_acc_len(c_))
+    assert int(got["abi"]) == _lib.ABI_VERSION
     for cname, py in structs.items():
         assert int(got[f"{cname} size"]) == ctypes.sizeof(py), cname
         for fname, _ in py._fields_:

@@ -1,0 +1,102 @@
+"""Data-parallel path on CPU: world_size-2 gloo process group.
+
+Covers the sharding helpers, the flat-buffer detection used for the engine's
+gradient layout, the single-bucket SUM all-reduce (flat and packed paths) and the
+clip helper against torch.nn.utils.clip_grad_norm_.  The GPU ranks run the same
+code over RCCL (bench.py under torch.distributed.run)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from snnflow import dp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _params(rank, flat_layout):
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(8, 2, 3, 3)), torch.nn.Parameter(torch.randn(8)),
+          torch.nn.Parameter(torch.randn(2, 8, 1, 1))]
+    g = torch.Generator().manual_seed(100 + rank)
+    vals = [torch.randn(p.shape, generator=g) for p in ps]
+    if flat_layout:
+        flat = torch.cat([v.reshape(-1) for v in vals])
+        off = 0
+        for p in ps:
+            p.grad = flat[off:off + p.numel()].view(p.shape)
+            off += p.numel()
+    else:
+        for p, v in zip(ps, vals):
+            p.grad = v.clone()
+    return ps, vals
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        for flat_layout in (True, False):
+            ps, _ = _params(rank, flat_layout)
+            assert (dp.flat_grad_buffer(ps) is not None) == flat_layout
+            dp.GradAllReduce(ps)()
+            expect = [sum(_params(r, False)[1][i] for r in range(world)) for i in range(len(ps))]
+            out[flat_layout] = max(float((p.grad - e).abs().max()) for p, e in zip(ps, expect))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grad_allreduce_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in res:
+        assert out[True] < 1e-6 and out[False] < 1e-6, (rank, out)
+
+
+def test_shard_slots_partition():
+    slots = [list(dp.shard_slots(64, r, 8)) for r in range(8)]
+    assert sum(slots, []) == list(range(64))
+    assert all(len(s) == 8 for s in slots)
+    with pytest.raises(ValueError):
+        dp.shard_slots(10, 0, 4)
+    assert len({dp.stream_seed(1, r) for r in range(8)}) == 8
+
+
+def test_flat_buffer_detection_rejects_gaps_and_order():
+    flat = torch.arange(10.0)
+    a, b = torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(4))
+    a.grad, b.grad = flat[0:4], flat[4:8]
+    assert dp.flat_grad_buffer([a, b]) is not None
+    assert dp.flat_grad_buffer([b, a]) is None
+    b.grad = flat[5:9]
+    assert dp.flat_grad_buffer([a, b]) is None
+
+
+@pytest.mark.parametrize("flat_layout", [True, False])
+def test_clip_matches_torch(flat_layout):
+    ps, _ = _params(0, flat_layout)
+    ref, _ = _params(0, False)
+    for p in ps + ref:
+        p.grad.mul_(3.0)
+    n1 = dp.clip_grad_norm_(ps, 1.0)
+    n2 = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    assert abs(float(n1) - float(n2)) <= 1e-5 * float(n2)
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.grad, r.grad, rtol=1e-5, atol=1e-7)

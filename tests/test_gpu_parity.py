@@ -308,3 +308,55 @@ def test_lif_export_op(dev):
     np.testing.assert_array_equal(spk.cpu().numpy(), s_ref.numpy())
     np.testing.assert_array_equal(mo.cpu().numpy(), torch.where(s_ref > 0, torch.zeros_like(mp), mp).numpy())
     assert spk[0, 0, 0, 0].item() == 1.0
+
+
+def test_training_steps_fused_adam_vs_oracle(dev):
+    """Three optimizer steps (T=2 windows each, truncated BPTT) with torch's fused Adam,
+    which updates parameters without bumping their version counters: the engine must
+    re-read the weights at every forward.  Before every step the oracle is re-synced to
+    OUR parameters and states (Adam amplifies last-bit gradient differences of
+    near-zero gradients, so parameters are not compared across steps); flows, loss and
+    gradients of every step must then match."""
+    import snnflow
+    from oracle import iwe_ref, lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(3)
+    H = W = 32
+    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    model = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    ref = lif_ref.LIFFireNetRef(dict(kw), "LIFFireNet").train()
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2, fused=True)
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    ew = snnflow.EventWarping(cfg, dev)
+    rew = iwe_ref.EventWarpingRef([H, W], weight=0.001)
+    gen = torch.Generator(device=dev).manual_seed(11)
+    for step in range(3):
+        ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+        ref._states = [None if s is None else s.detach().cpu() for s in model._states]
+        for n, _ in model.layer_spec:
+            m = getattr(model, n).lif.mem
+            if m is not None:
+                getattr(ref, n).lif.mem = m.detach().cpu()
+        for t in range(2):
+            w = make_window(2, 400, H, W, gen, dev)
+            out = model(w["event_voxel"], w["event_cnt"])
+            rout = ref(None, w["event_cnt"].cpu())
+            np.testing.assert_allclose(out["flow"][0].detach().cpu().numpy(), rout["flow"][0].detach().numpy(),
+                                       rtol=1e-3, atol=1e-5, err_msg=f"step {step} window {t}")
+            ew.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            rew.event_flow_association(rout["flow"], w["event_list"].cpu(), w["event_list_pol_mask"].cpu(),
+                                       w["event_mask"].cpu())
+        loss, rloss = ew(), rew()
+        opt.zero_grad(set_to_none=True)
+        ref.zero_grad(set_to_none=True)
+        loss.backward()
+        rloss.backward()
+        np.testing.assert_allclose(loss.item(), rloss.item(), rtol=1e-4)
+        for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
+            assert _rel(a.grad.cpu().numpy(), b.grad.numpy()) < 2e-3, (step, n)
+        opt.step()
+        model.detach_states()
+        ew.reset()
+        rew.reset()
