@@ -105,10 +105,8 @@ def main():
     from snnflow.synthetic import make_window
 
     torch.manual_seed(0)  # configs/parser.py:92-96 (loader.seed = 0): identical init on every rank
-    kw = {"name": args.model, "encoding": "cnt", "round_encoding": False, "norm_input": False, "num_bins": 2,
-          "base_num_channels": args.channels, "kernel_size": 3, "activations": ["arctanspike", "arctanspike"],
-          "mask_output": True, "quantization": {"enabled": False}, "tebn": {"enabled": False},
-          "mpbn": {"enabled": False}, "spiking_neuron": {"leak": [0.0, 1.0], "thresh": [0.0, 0.8]}}
+    from snnflow.parser import train_snn_model_kwargs
+    kw = train_snn_model_kwargs(args.model, base_num_channels=args.channels)  # configs/train_SNN.yml
     model = getattr(snnflow, args.model)(kw).to(dev).train()
     R, B, T, N = args.res, args.batch, args.T, args.events
     cfg = {"loader": {"resolution": [R, R]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},

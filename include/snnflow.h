@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 5
+#define SNNFLOW_ABI_VERSION 6
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -154,12 +154,12 @@ typedef struct snnflow_lif_bwd_args {
 } snnflow_lif_bwd_args;
 int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream);
 
-/* ---- backward of one layer: BN backward + conv dgrad/wgrad of layer l
- * [+ LIF backward of layer l-1 on the dgrad result] (the reverse of
- * snnflow_conv_fwd).  Block 0 turns acc_in into layer l's neuron-parameter
- * gradients (and pred gradients when has_pred), written (accumulate=0) or added.
- * Weight gradients go to per-block slabs (snnflow_conv_blocks() x c*cin*9 floats),
- * written or accumulated across time steps; snnflow_slab_reduce sums them. */
+/* ---- backward of one layer on the critical path: BN backward + conv dgrad of layer l
+ * [+ LIF backward of layer l-1 on the dgrad result] (the reverse of snnflow_conv_fwd).
+ * Block 0 turns acc_in into layer l's neuron-parameter gradients (and pred gradients
+ * when has_pred), written (accumulate=0) or added, and stores the BatchNorm backward
+ * coefficients of this layer-step in bnc_out for the deferred weight gradient
+ * (snnflow_wgrad). */
 typedef struct snnflow_layer_bwd_args {
     int B, H, W, cin, c;
     const float* y; const float* stats; const float* g_cur;
@@ -168,12 +168,10 @@ typedef struct snnflow_layer_bwd_args {
     snnflow_neuron_grad ng;
     int has_pred; float* g_pred_w; float* g_pred_b;
     int accumulate;
+    float* bnc_out;             /* [2][c] (grad_mean, k) of layer l's BN backward */
     const float* wt_bwd_ff;     /* [3][3][c][cin]  (NULL: no input gradient)        */
     const float* wt_bwd_rec;    /* [3][3][c][c] or NULL                             */
     int lif_in;
-    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* input of layer l (wgrad)   */
-    const float* s_prev;        /* NHWC previous-step spikes of layer l or NULL     */
-    float* slab_ff; float* slab_rec;
     float* g_x; int64_t gxs_b, gxs_c, gxs_h, gxs_w;   /* lif_in=0: input gradient (strided) or NULL */
     float* g_state_prev;        /* [2][B][H][W][c] grad of the previous state (rec) or NULL */
     int zero_mem_half;          /* 1: also zero-fill the membrane half of g_state_prev */
@@ -185,6 +183,33 @@ typedef struct snnflow_layer_bwd_args {
     double* zero0; double* zero1; int zero_n;
 } snnflow_layer_bwd_args;
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
+
+/* ---- deferred weight gradients of one layer over many time steps ----------
+ * Nothing on the backward chain depends on dW, so the weight gradients of a layer
+ * are computed once per backward pass over all its time steps:
+ *   dW_ff[co][ci][k]  = sum_t sum_p G_t[p][co] x_t[p + k][ci]
+ *   dW_rec[co][ci][k] = sum_t sum_p G_t[p][co] s_prev_t[p + k][ci]
+ * with G_t = ((g_cur - grad_mean) - (y - mean) k) invstd gamma (BN backward, from the
+ * coefficients layer_bwd stored in bnc).  One block per tile accumulates over the
+ * steps in registers and writes (accumulate=0) or adds its per-block slab once;
+ * snnflow_slab_reduce sums the slabs.  Up to SNNFLOW_MAX_WGRAD_STEPS steps per call. */
+typedef struct snnflow_wgrad_step {
+    const float* g_cur;         /* NHWC [B][H][W][c] */
+    const float* y;             /* NHWC pre-BN conv output */
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* ff conv input (strided) */
+    const float* s_prev;        /* NHWC previous-step spikes (rec conv input) or NULL */
+    const float* stats;         /* [2][c] mean, invstd */
+    const float* bnc;           /* [2][c] grad_mean, k */
+} snnflow_wgrad_step;
+#define SNNFLOW_MAX_WGRAD_STEPS 32
+typedef struct snnflow_wgrad_args {
+    int B, H, W, cin, c, nsteps, accumulate, rec;
+    const float* bn_weight;     /* [c] gamma */
+    float* slab_ff;             /* snnflow_conv_blocks() x c*cin*9 */
+    float* slab_rec;            /* snnflow_conv_blocks() x c*c*9 (rec layers) */
+    snnflow_wgrad_step steps[SNNFLOW_MAX_WGRAD_STEPS];
+} snnflow_wgrad_args;
+int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream);
 
 /* Sums per-block weight-gradient slabs: out[i][e] = sum_b slab[i][b][e]. */
 typedef struct snnflow_slab_desc { const float* slab; float* out; int elems; } snnflow_slab_desc;

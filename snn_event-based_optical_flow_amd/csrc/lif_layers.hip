@@ -46,21 +46,21 @@ namespace {
 // ---------------------------------------------------------------------------
 
 // Strided input (e.g. event_cnt NCHW, or an NHWC spike tensor) -> tile[p][ci]
-template <int CIN>
+template <int CIN, int NTH = NT>
 __device__ void stage_strided(const float* __restrict__ x, int64_t sb, int64_t sc, int64_t sh, int64_t sw,
                               const Tile& tl, int H, int W, float* tile) {
     constexpr int P = Pad<CIN>::v;
     const int tid = threadIdx.x;
     const float* xb = x + (int64_t)tl.b * sb;
     if (sc == 1) {
-        for (int e = tid; e < HN * CIN; e += NT) {
+        for (int e = tid; e < HN * CIN; e += NTH) {
             const int p = e / CIN, ci = e - p * CIN;
             const int r = p / HWD, cc = p - r * HWD;
             const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
             tile[p * P + ci] = in_image(h, w, H, W) ? xb[h * sh + w * sw + ci] : 0.0f;
         }
     } else {
-        for (int e = tid; e < HN * CIN; e += NT) {
+        for (int e = tid; e < HN * CIN; e += NTH) {
             const int ci = e / HN, p = e - ci * HN;
             const int r = p / HWD, cc = p - r * HWD;
             const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
@@ -70,12 +70,12 @@ __device__ void stage_strided(const float* __restrict__ x, int64_t sb, int64_t s
 }
 
 // Contiguous NHWC [B][H][W][C] (C % 4 == 0) -> tile
-template <int C>
+template <int C, int NTH = NT>
 __device__ void stage_nhwc(const float* __restrict__ x, const Tile& tl, int H, int W, float* tile) {
     static_assert(C % 4 == 0, "vector staging");
     constexpr int P = Pad<C>::v, Q = C / 4;
     const int tid = threadIdx.x;
-    for (int e = tid; e < HN * Q; e += NT) {
+    for (int e = tid; e < HN * Q; e += NTH) {
         const int p = e / Q, q = e - p * Q;
         const int r = p / HWD, cc = p - r * HWD;
         const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
@@ -87,19 +87,22 @@ __device__ void stage_nhwc(const float* __restrict__ x, const Tile& tl, int H, i
 }
 
 // ---------------------------------------------------------------------------
-// 3x3 convolution of one output pixel (all C outputs) from an LDS halo tile.
-// wt: [3][3][CIN][C] (uniform -> scalar loads).  acc += sum_{ky,kx,ci} w * x.
+// 3x3 convolution of one output pixel (outputs [co0, co0+CO)) from an LDS halo tile.
+// wt: [3][3][CIN][C]; co0 must be wave-uniform (scalar weight loads).
+// acc += sum_{ky,kx,ci} w * x.
 // ---------------------------------------------------------------------------
-template <int CIN, int C>
-__device__ inline void conv_acc(const float* tile, const float* __restrict__ wt, int ty, int tx, float (&acc)[C]) {
+template <int CIN, int C, int CO = C>
+__device__ inline void conv_acc(const float* tile, const float* __restrict__ wt, int ty, int tx, int co0,
+                                float (&acc)[CO]) {
     constexpr int P = Pad<CIN>::v, VW = VecW<CIN>::v;
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const float* xp = tile + ((ty + ky) * HWD + (tx + kx)) * P;
-            const cfloat_ptr wk = as_const(wt) + (ky * 3 + kx) * CIN * C;
-#pragma unroll(CIN <= 8 ? CIN : 1)
+            const cfloat_ptr wk = as_const(wt) + (ky * 3 + kx) * CIN * C + co0;
+            constexpr int UR = CIN <= 8 ? CIN : 1;
+#pragma unroll UR
             for (int ci = 0; ci < CIN; ci += VW) {
                 float xs[VW];
                 if constexpr (VW == 4) {
@@ -114,32 +117,35 @@ __device__ inline void conv_acc(const float* tile, const float* __restrict__ wt,
 #pragma unroll
                 for (int j = 0; j < VW; ++j) {
 #pragma unroll
-                    for (int co = 0; co < C; ++co) acc[co] = fmaf(wk[(ci + j) * C + co], xs[j], acc[co]);
+                    for (int co = 0; co < CO; ++co) acc[co] = fmaf(wk[(ci + j) * C + co], xs[j], acc[co]);
                 }
             }
         }
     }
 }
 
-// Transposed 3x3 (input gradient) of one pixel from an LDS tile of output gradients.
-// wd: [3][3][C][CIN].  gx[ci] += sum_{ky,kx,co} w[co][ci][ky][kx] * g[h+1-ky][w+1-kx][co]
-template <int C, int CIN>
-__device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ wd, int ty, int tx, float (&gx)[CIN]) {
+// Transposed 3x3 (input gradient, inputs [ci0, ci0+CI)) of one pixel from an LDS tile of
+// output gradients.  wd: [3][3][C][CIN]; ci0 wave-uniform.
+// gx[ci] += sum_{ky,kx,co} w[co][ci][ky][kx] * g[h+1-ky][w+1-kx][co]
+template <int C, int CIN, int CI = CIN>
+__device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ wd, int ty, int tx, int ci0,
+                                 float (&gx)[CI]) {
     constexpr int P = Pad<C>::v;
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
             const float* gp = gtile + ((ty + 2 - ky) * HWD + (tx + 2 - kx)) * P;
-            const cfloat_ptr wk = as_const(wd) + (ky * 3 + kx) * C * CIN;
-#pragma unroll(C <= 8 ? C : 1)
+            const cfloat_ptr wk = as_const(wd) + (ky * 3 + kx) * C * CIN + ci0;
+            constexpr int UR = C <= 8 ? C : 1;
+#pragma unroll UR
             for (int co = 0; co < C; co += 4) {
                 const float4 v = *reinterpret_cast<const float4*>(gp + co);
                 const float gs[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
 #pragma unroll
-                    for (int ci = 0; ci < CIN; ++ci) gx[ci] = fmaf(wk[(co + j) * CIN + ci], gs[j], gx[ci]);
+                    for (int ci = 0; ci < CI; ++ci) gx[ci] = fmaf(wk[(co + j) * CIN + ci], gs[j], gx[ci]);
                 }
             }
         }
@@ -154,130 +160,6 @@ __device__ inline void pin(float (&v)[N]) {
     for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
 }
 
-// Per-block weight-gradient partial of one 3x3 conv:
-//   dW[co][ci][ky][kx] = sum_{tile pixels p} g[p][co] * x[p + (ky-1, kx-1)][ci]
-// G: LDS g tile (halo layout, C channels), X: LDS input halo tile (CIN channels).
-// Items (k, co-block of 4, ci-block of VW) x pixel groups; groups reduced in fixed order.
-// Each thread owns NO output slab entries (indices by slab_entry); with `accumulate`
-// their old values are prefetched at kernel start (slab_prefetch) so the read-modify-
-// write adds no memory round trip at the end.
-template <int CIN, int C>
-struct WgradShape {
-    static constexpr int VW = VecW<CIN>::v;
-    static constexpr int NCB = CIN / VW;
-    static constexpr int Q = 9 * (C / 4) * NCB;
-    static constexpr int GR = (Q >= NT) ? 1 : NT / Q;
-    static constexpr int SCRATCH = (GR > 1) ? GR * Q * 4 * VW : 1;
-    static constexpr int NK = (Q * 4 * VW + NT - 1) / NT;  // outputs per thread (GR > 1)
-    static constexpr int NM = (Q + NT - 1) / NT;           // items per thread (GR == 1)
-    static constexpr int NO = (GR > 1) ? NK : NM * 4 * VW;
-};
-
-// Slab index of this thread's k-th output, or -1.
-template <int CIN, int C>
-__device__ inline int slab_entry(int k) {
-    using S = WgradShape<CIN, C>;
-    constexpr int VW = S::VW, Q = S::Q;
-    int qq, i, j;
-    if constexpr (S::GR > 1) {
-        const int e = threadIdx.x + k * NT;
-        if (e >= Q * 4 * VW) return -1;
-        qq = e / (4 * VW);
-        const int ij = e - qq * 4 * VW;
-        i = ij / VW;
-        j = ij - i * VW;
-    } else {
-        const int m = k / (4 * VW), ij = k - m * 4 * VW;
-        qq = threadIdx.x + m * NT;
-        if (qq >= Q) return -1;
-        i = ij / VW;
-        j = ij - i * VW;
-    }
-    const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
-    return ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
-}
-
-template <int CIN, int C>
-__device__ inline void slab_prefetch(const float* slab, int accumulate, float (&old)[WgradShape<CIN, C>::NO]) {
-#pragma unroll
-    for (int k = 0; k < WgradShape<CIN, C>::NO; ++k) {
-        const int idx = slab_entry<CIN, C>(k);
-        old[k] = (accumulate && idx >= 0) ? slab[idx] : 0.0f;
-    }
-}
-
-template <int CIN, int C>
-__device__ void wgrad_tile(const float* G, const float* X, float* __restrict__ slab,
-                           const float (&old)[WgradShape<CIN, C>::NO], float* scratch) {
-    using S = WgradShape<CIN, C>;
-    constexpr int VW = S::VW, Q = S::Q, GR = S::GR, PC = Pad<C>::v, PX = Pad<CIN>::v;
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int m = 0; m < (GR > 1 ? 1 : S::NM); ++m) {
-        const int q = (GR > 1) ? tid % Q : tid + m * NT;
-        const int g = (GR > 1) ? tid / Q : 0;
-        const bool active = (GR > 1) ? (g < GR) : (q < Q);
-        float acc[4][VW];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < VW; ++j) acc[i][j] = 0.f;
-        if (active) {
-            const int kidx = q % 9, rest = q / 9, cob = rest % (C / 4), cib = rest / (C / 4);
-            const int ky = kidx / 3, kx = kidx % 3;
-            for (int p = g; p < NT; p += GR) {
-                const int ty = p / TW, tx = p - ty * TW;
-                const float4 gv4 = *reinterpret_cast<const float4*>(G + ((ty + 1) * HWD + tx + 1) * PC + cob * 4);
-                const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
-                const float* xp = X + ((ty + ky) * HWD + tx + kx) * PX + cib * VW;
-                float xv[VW];
-                if constexpr (VW == 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(xp);
-                    xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
-                } else if constexpr (VW == 2) {
-                    const float2 v = *reinterpret_cast<const float2*>(xp);
-                    xv[0] = v.x; xv[1] = v.y;
-                } else {
-                    xv[0] = xp[0];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) acc[i][j] = fmaf(gv[i], xv[j], acc[i][j]);
-            }
-        }
-        if constexpr (GR > 1) {
-            if (active) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) scratch[((g * Q + q) * 4 + i) * VW + j] = acc[i][j];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < S::NK; ++k) {
-                const int e = tid + k * NT;
-                if (e < Q * 4 * VW) {
-                    float sum = 0.f;
-                    for (int gg = 0; gg < GR; ++gg) sum += scratch[gg * Q * 4 * VW + e];
-                    slab[slab_entry<CIN, C>(k)] = old[k] + sum;
-                }
-            }
-            __syncthreads();
-        } else {
-            if (active) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) {
-                        const int k = m * 4 * VW + i * VW + j;
-                        slab[slab_entry<CIN, C>(k)] = old[k] + acc[i][j];
-                    }
-            }
-        }
-    }
-}
-
 // dL/dm of the membrane input: v = beta*((1-r)*m) + I (zero reset) or beta*m + I - r*theta;
 // r = H(m - theta) is detached (snntorch mem_reset).
 __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_reset) {
@@ -287,11 +169,13 @@ __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_
     return gmp * (1.0f - r);
 }
 
-// Block-level sum of NV per-thread floats, then one fp64 atomic add per value into
-// acc (the block's partial; NV <= NT values issued by consecutive lanes).
-template <int NV>
-__device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
-    __shared__ float red[4][NV];
+// Block-level sums of per-thread floats, then one fp64 atomic add per sum.  The block's
+// threads form PARTS groups of NT consecutive threads (whole waves); each group sums
+// its own NV values and dst(part, j) is the accumulator address of sum j of group part.
+template <int NV, int PARTS, typename Dst>
+__device__ void block_atomic_sum_parts(const float (&v)[NV], Dst dst) {
+    constexpr int WPP = NT / 64, NW = WPP * PARTS;
+    __shared__ float red[NW][NV];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
@@ -299,13 +183,24 @@ __device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
         if (lane == 0) red[wv][j] = s;
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < NV; j += NT)
-        atomicAdd(acc + j, (((double)red[0][j] + (double)red[1][j]) + (double)red[2][j]) + (double)red[3][j]);
+    for (int t = threadIdx.x; t < PARTS * NV; t += NT * PARTS) {
+        const int part = t / NV, j = t - part * NV;
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < WPP; ++w) s += (double)red[part * WPP + w][j];
+        atomicAdd(dst(part, j), s);
+    }
 }
 
-// Block 0 zeroes accumulators already consumed by an earlier kernel of the chain.
+template <int NV>
+__device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
+    block_atomic_sum_parts<NV, 1>(v, [acc](int, int j) { return acc + j; });
+}
+
+// Accumulators already consumed by an earlier kernel of the chain are zeroed here
+// (grid-stride over all threads of the launch).
 __device__ inline void zero_consumed(double* z0, double* z1, int n) {
-    for (int j = blockIdx.x * NT + threadIdx.x; j < n; j += gridDim.x * NT) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
         if (z0) z0[j] = 0.0;
         if (z1) z1[j] = 0.0;
     }
@@ -492,33 +387,44 @@ __device__ inline void zero4(float4* r, int n) {
 
 // Register-prefetch budget: halo tiles of up to 16 channels are held in registers
 // (<= 6 float4 per thread each); wider layers stage straight into LDS.
-template <int CH>
-struct Prefetch { static constexpr bool on = (CH % 4 == 0) && Halo4<CH>::R <= 6; };
+template <int CH, int NTH = NT>
+struct Prefetch { static constexpr bool on = (CH % 4 == 0) && Halo4<CH, NTH>::R <= 6; };
 
-template <int CIN, int C, bool LIF_IN, bool REC>
-__global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
+// Conv-layer kernels run SPLIT threads per output pixel (SPLIT groups of NT threads, whole
+// waves): group `part` owns output channels [part*C/SPLIT, ...) in the forward and input
+// channels [part*CIN/SPLIT, ...) in the backward.  SPLIT = 2 doubles the waves per SIMD
+// (the launch has only 2 blocks per CU at cfg2) so one wave's loads and barriers overlap
+// another's arithmetic.  The group index is wave-uniform (readfirstlane): weight
+// addresses stay scalar.
+__device__ inline int thread_part() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x / NT); }
+
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+__global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a) {
+    constexpr int NTB = NT * SPLIT, CO = C / SPLIT;
+    static_assert(CO % 4 == 0, "output channels per group: multiple of 4");
     constexpr int PI_ = Pad<CIN>::v, PC = Pad<C>::v;
-    constexpr bool PF_REC = REC && Prefetch<C>::on;   // s_prev halo in registers + own LDS tile
+    constexpr bool PF_REC = REC && Prefetch<C, NTB>::on;  // s_prev halo in registers + own LDS tile
     constexpr int PMAX = (REC && !PF_REC && PC > PI_) ? PC : PI_;
     __shared__ __attribute__((aligned(16))) float tile[HN * PMAX];
     __shared__ __attribute__((aligned(16))) float rtile[PF_REC ? HN * PC : 4];
     __shared__ LifCoef coef[LIF_IN ? CIN : 1];
 
-    const int tid = threadIdx.x, ty = tid / TW, tx = tid - ty * TW;
+    const int tid = threadIdx.x, pt = tid % NT, ty = pt / TW, tx = pt - ty * TW;
+    const int part = thread_part(), co0 = part * CO;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
     const bool has_rec = REC && a.s_prev != nullptr;
 
     // 1. issue every global load of the tile before any use
-    float4 rs[PF_REC ? Halo4<C>::R : 1];
+    float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
     if constexpr (PF_REC) {
-        if (has_rec) halo_load<C>(a.s_prev, tl, H, W, rs);
+        if (has_rec) halo_load<C, NTB>(a.s_prev, tl, H, W, rs);
     }
     if constexpr (LIF_IN) {
-        constexpr int R = Halo4<CIN>::R, Q = CIN / 4;
+        constexpr int R = Halo4<CIN, NTB>::R, Q = CIN / 4;
         float4 ry[R], rm[R];
-        halo_load<CIN>(a.prev_y, tl, H, W, ry);
-        if (a.prev_mem) halo_load<CIN>(a.prev_mem, tl, H, W, rm);
+        halo_load<CIN, NTB>(a.prev_y, tl, H, W, ry);
+        if (a.prev_mem) halo_load<CIN, NTB>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
         zero_consumed(a.zero0, a.zero1, a.zero_n);
         __shared__ double sums[2 * CIN];
@@ -531,8 +437,8 @@ __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
         float4* st4 = reinterpret_cast<float4*>(a.prev_state);
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            const int e = tid + i * NT;
-            if (e < Halo4<CIN>::E) {
+            const int e = tid + i * NTB;
+            if (e < Halo4<CIN, NTB>::E) {
                 const int p = e / Q, q = e - p * Q;
                 const int r = p / HWD, cc = p - r * HWD;
                 const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
@@ -551,17 +457,17 @@ __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
         }
     } else {
         zero_consumed(a.zero0, a.zero1, a.zero_n);
-        stage_strided<CIN>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, tile);
+        stage_strided<CIN, NTB>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, tile);
     }
     if constexpr (PF_REC) {
-        if (has_rec) halo_store<C>(rtile, rs);
+        if (has_rec) halo_store<C, NTB>(rtile, rs);
     }
     __syncthreads();
 
-    float y[C];
+    float y[CO];
 #pragma unroll
-    for (int co = 0; co < C; ++co) y[co] = 0.0f;
-    if (!PROBE_OFF(16)) conv_acc<CIN, C>(tile, a.wt_ff, ty, tx, y);
+    for (int co = 0; co < CO; ++co) y[co] = 0.0f;
+    if (!PROBE_OFF(16)) conv_acc<CIN, C, CO>(tile, a.wt_ff, ty, tx, co0, y);
 
     if constexpr (REC) {
         if (has_rec) {
@@ -570,35 +476,39 @@ __global__ __launch_bounds__(NT) void k_conv_fwd(snnflow_conv_fwd_args a) {
                 rt = rtile;
             } else {
                 __syncthreads();
-                stage_nhwc<C>(a.s_prev, tl, H, W, tile);
+                stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
                 __syncthreads();
             }
-            float r[C];
+            float r[CO];
 #pragma unroll
-            for (int co = 0; co < C; ++co) r[co] = 0.0f;
-            if (!PROBE_OFF(16)) conv_acc<C, C>(rt, a.wt_rec, ty, tx, r);
+            for (int co = 0; co < CO; ++co) r[co] = 0.0f;
+            if (!PROBE_OFF(16)) conv_acc<C, C, CO>(rt, a.wt_rec, ty, tx, co0, r);
 #pragma unroll
-            for (int co = 0; co < C; ++co) y[co] = y[co] + r[co];  // ff + rec (:540)
+            for (int co = 0; co < CO; ++co) y[co] = y[co] + r[co];  // ff + rec (:540)
         }
     }
 
     const int h = tl.h0 + ty, w = tl.w0 + tx;
     const bool in = (h < H) && (w < W);
     if (in) {
-        float* yp = a.y + (((int64_t)tl.b * H + h) * W + w) * C;
+        float* yp = a.y + (((int64_t)tl.b * H + h) * W + w) * C + co0;
 #pragma unroll
-        for (int co = 0; co < C; co += 4)
+        for (int co = 0; co < CO; co += 4)
             *reinterpret_cast<float4*>(yp + co) = make_float4(y[co], y[co + 1], y[co + 2], y[co + 3]);
     }
     if (a.acc) {
-        float v[2 * C];
+        float v[2 * CO];
 #pragma unroll
-        for (int co = 0; co < C; ++co) {
+        for (int co = 0; co < CO; ++co) {
             const float yy = in ? y[co] : 0.0f;
             v[co] = yy;
-            v[C + co] = yy * yy;
+            v[CO + co] = yy * yy;
         }
-        if (!PROBE_OFF(4)) block_atomic_sum<2 * C>(v, acc_shard(a.acc, 2 * C));
+        double* acc = acc_shard(a.acc, 2 * C);
+        if (!PROBE_OFF(4))
+            block_atomic_sum_parts<2 * CO, SPLIT>(v, [acc](int pp, int j) {
+                return acc + (j < CO ? pp * CO + j : C + pp * CO + (j - CO));
+            });
     }
 }
 
@@ -761,27 +671,23 @@ __device__ inline float4 bn_bwd4(const float4& g, const float4& y, const BnBwdLd
     return make_float4(o[0], o[1], o[2], o[3]);
 }
 
-template <int CIN, int C, bool LIF_IN, bool REC>
-__global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
-    using WS = WgradShape<CIN, C>;
-    using WR = WgradShape<C, C>;
-    constexpr int PI_ = Pad<CIN>::v, PC = Pad<C>::v;
-    constexpr bool PF = Prefetch<C>::on;                 // halo tiles held in registers
-    constexpr bool PFX = PF && Prefetch<CIN>::on;        // x halo prefetchable (dense NHWC)
-    constexpr bool SEP = REC && PF;                      // s_prev gets its own LDS tile
-    constexpr int PX = (REC && !SEP && PC > PI_) ? PC : PI_;
-    constexpr int SCR = (WS::SCRATCH > WR::SCRATCH) ? WS::SCRATCH : WR::SCRATCH;
-    constexpr int NVP = LIF_IN ? 3 * CIN : 1;
-    constexpr int QI = CIN / 4 > 0 ? CIN / 4 : 1;
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+__global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args a) {
+    constexpr int NTB = NT * SPLIT;
+    constexpr int CI = CIN / SPLIT, CR = C / SPLIT;  // input / recurrent channels per thread group
+    static_assert(CI * SPLIT == CIN && CR * SPLIT == C, "channel split");
+    static_assert(!LIF_IN || CI % 4 == 0, "LIF backward group: multiple of 4 channels");
+    constexpr int PC = Pad<C>::v;
+    constexpr bool PF = Prefetch<C, NTB>::on;  // g_cur / y halos held in registers
+    constexpr int NVP = LIF_IN ? 3 * CI : 1;
+    constexpr int QI = CI / 4 > 0 ? CI / 4 : 1;  // float4s of this group's channels
     __shared__ __attribute__((aligned(16))) float G[HN * PC];
-    __shared__ __attribute__((aligned(16))) float X[HN * PX];
-    __shared__ __attribute__((aligned(16))) float S[SEP ? HN * PC : 4];
-    __shared__ __attribute__((aligned(16))) float scratch[SCR];
     __shared__ BnBwdLds bnp[C];
     __shared__ LifCoef pcoef[LIF_IN ? CIN : 1];
     __shared__ float pmean[LIF_IN ? CIN : 1];
 
-    const int tid = threadIdx.x, ty = tid / TW, tx = tid - ty * TW;
+    const int tid = threadIdx.x, pt = tid % NT, ty = pt / TW, tx = pt - ty * TW;
+    const int part = thread_part(), ci0 = part * CI, cr0 = part * CR;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
     const double N = (double)a.B * H * W;
@@ -789,47 +695,34 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
     const int h = tl.h0 + ty, w = tl.w0 + tx;
     const bool in = (h < H) && (w < W);
     const int64_t pix = ((int64_t)tl.b * H + h) * W + w;
-    const bool has_rec = REC && a.s_prev != nullptr;
-    bool dense = false;
-    if constexpr (CIN % 4 == 0)
-        dense = a.xs_c == 1 && a.xs_w == CIN && a.xs_h == (int64_t)W * CIN && a.xs_b == (int64_t)H * W * CIN;
-    float* slab_ff = a.slab_ff + (int64_t)blockIdx.x * (C * CIN * 9);
-    float* slab_rec = REC ? a.slab_rec + (int64_t)blockIdx.x * (C * C * 9) : nullptr;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
     // 1. every global load of the kernel, issued up front (register prefetch)
-    float4 rg[PF ? Halo4<C>::R : 1], ry[PF ? Halo4<C>::R : 1];
-    float4 rx[PFX ? Halo4<CIN>::R : 1], rs[SEP ? Halo4<C>::R : 1];
+    float4 rg[PF ? Halo4<C, NTB>::R : 1], ry[PF ? Halo4<C, NTB>::R : 1];
     float4 dy[LIF_IN ? QI : 1], dm[LIF_IN ? QI : 1], dg[LIF_IN ? QI : 1];
-    float oldff[WS::NO], oldrec[REC ? WR::NO : 1];
     if constexpr (PF) {
-        halo_load<C>(a.g_cur, tl, H, W, rg);
-        halo_load<C>(a.y, tl, H, W, ry);
-    }
-    if constexpr (PFX) {
-        if (dense) halo_load<CIN>(a.x, tl, H, W, rx);
-    }
-    if constexpr (SEP) {
-        if (has_rec) halo_load<C>(a.s_prev, tl, H, W, rs);
+        halo_load<C, NTB>(a.g_cur, tl, H, W, rg);
+        halo_load<C, NTB>(a.y, tl, H, W, ry);
     }
     if constexpr (LIF_IN) {
-        const int64_t plane4 = (int64_t)a.B * H * W * QI;
+        constexpr int Q4 = CIN / 4;
+        const int64_t plane4 = (int64_t)a.B * H * W * Q4;
         const float4* py4 = reinterpret_cast<const float4*>(a.prev_y);
         const float4* pm4 = reinterpret_cast<const float4*>(a.prev_mem);
         const float4* pg4 = reinterpret_cast<const float4*>(a.prev_g_state);
         // unconditional 16-B loads (clamped pixel outside the image; results unused there)
         const int64_t pc = ((int64_t)tl.b * H + (h < H ? h : H - 1)) * W + (w < W ? w : W - 1);
+        const int64_t base = pc * Q4 + ci0 / 4;
 #pragma unroll
         for (int q = 0; q < QI; ++q) {
-            dy[q] = py4[pc * QI + q];
-            dm[q] = ld4_or_zero(pm4, py4, pc * QI + q);
-            dg[q] = ld4_or_zero(pg4 ? pg4 + plane4 : nullptr, py4, pc * QI + q);
+            dy[q] = py4[base + q];
+            dm[q] = ld4_or_zero(pm4, py4, base + q);
+            dg[q] = ld4_or_zero(pg4 ? pg4 + plane4 : nullptr, py4, base + q);
         }
     }
-    slab_prefetch<CIN, C>(slab_ff, a.accumulate, oldff);
-    if constexpr (REC) slab_prefetch<C, C>(slab_rec, a.accumulate && has_rec, oldrec);
 
-    // 2. per-channel constants; block 0 finishes layer l's neuron gradients
+    // 2. per-channel constants; block 0 finishes layer l's neuron gradients and stores the
+    //    BN backward coefficients for the deferred weight gradient
     zero_consumed(a.zero0, a.zero1, a.zero_n);
     __shared__ double sums[SNNFLOW_BWD_ACC(C)];
     acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
@@ -849,6 +742,10 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
             c.gm = 0.0f;
         }
         bnp[tid] = c;
+        if (blockIdx.x == 0 && a.bnc_out) {
+            a.bnc_out[tid] = c.gm;
+            a.bnc_out[C + tid] = c.k;
+        }
     }
     if constexpr (LIF_IN) {
         if (tid < CIN) {
@@ -858,14 +755,13 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
     }
     __syncthreads();
 
-    // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l);
-    //    input halos into X / S
+    // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l)
     if constexpr (PF) {
         constexpr int Q = C / 4;
 #pragma unroll
-        for (int i = 0; i < Halo4<C>::R; ++i) {
-            const int e = tid + i * NT;
-            if (e < Halo4<C>::E) {
+        for (int i = 0; i < Halo4<C, NTB>::R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < Halo4<C, NTB>::E) {
                 const int p = e / Q, q = e - p * Q;
                 const int r = p / HWD, cc = p - r * HWD;
                 const bool img = in_image(tl.h0 + r - 1, tl.w0 + cc - 1, H, W);
@@ -874,7 +770,7 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
         }
     } else {
         constexpr int Q = C / 4;
-        for (int e = tid; e < Halo4<C>::E; e += NT) {
+        for (int e = tid; e < Halo4<C>::E; e += NTB) {
             const int p = e / Q, q = e - p * Q;
             const int64_t k = halo_idx4<C>(e, tl, H, W);
             float4 out = z4;
@@ -884,53 +780,41 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
             *reinterpret_cast<float4*>(G + p * PC + 4 * q) = out;
         }
     }
-    if constexpr (PFX) {
-        if (dense) halo_store<CIN>(X, rx);
-    } else if constexpr (CIN % 4 == 0) {
-        if (dense) stage_nhwc<CIN>(a.x, tl, H, W, X);
-    }
-    if (!dense) stage_strided<CIN>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, X);
-    if constexpr (SEP) {
-        if (has_rec) halo_store<C>(S, rs);
-    }
     __syncthreads();
 
-    // 4. Stage B: input gradient (dgrad) of ff and rec convolutions
-    float gx[CIN];
+    // 4. Stage B: input gradient (dgrad) of ff and rec convolutions (this group's channels)
+    float gx[CI];
 #pragma unroll
-    for (int ci = 0; ci < CIN; ++ci) gx[ci] = 0.0f;
-    if (!PROBE_OFF(1) && a.wt_bwd_ff) dgrad_acc<C, CIN>(G, a.wt_bwd_ff, ty, tx, gx);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int ci = 0; ci < CI; ++ci) gx[ci] = 0.0f;
+    if (!PROBE_OFF(1) && a.wt_bwd_ff) dgrad_acc<C, CIN, CI>(G, a.wt_bwd_ff, ty, tx, ci0, gx);
     if constexpr (REC) {
         if (a.g_state_prev) {
-            float gr[C];
+            float gr[CR];
 #pragma unroll
-            for (int c = 0; c < C; ++c) gr[c] = 0.0f;
-            if (!PROBE_OFF(1)) dgrad_acc<C, C>(G, a.wt_bwd_rec, ty, tx, gr);
+            for (int c = 0; c < CR; ++c) gr[c] = 0.0f;
+            if (!PROBE_OFF(1)) dgrad_acc<C, C, CR>(G, a.wt_bwd_rec, ty, tx, cr0, gr);
             pin(gr);  // keep the dgrad out of the `in` branch (sinking it there spills SGPRs)
             if (in) {
                 const int64_t plane = (int64_t)a.B * H * W * C;
+                float* gsp = a.g_state_prev + pix * C + cr0;
 #pragma unroll
-                for (int c = 0; c < C; c += 4) {
-                    if (a.zero_mem_half)
-                        *reinterpret_cast<float4*>(a.g_state_prev + pix * C + c) = z4;
-                    *reinterpret_cast<float4*>(a.g_state_prev + plane + pix * C + c) =
-                        make_float4(gr[c], gr[c + 1], gr[c + 2], gr[c + 3]);
+                for (int c = 0; c < CR; c += 4) {
+                    if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp + c) = z4;
+                    *reinterpret_cast<float4*>(gsp + plane + c) = make_float4(gr[c], gr[c + 1], gr[c + 2], gr[c + 3]);
                 }
             }
         }
     }
 
     // 5. Stage D: LIF backward of layer l-1 on the dgrad result, or the plain input gradient
-    //    (before the weight gradients so its stores drain behind them)
-    float vd[NVP];
-#pragma unroll
-    for (int j = 0; j < NVP; ++j) vd[j] = 0.0f;
     if constexpr (LIF_IN) {
+        float vd[NVP];
+#pragma unroll
+        for (int j = 0; j < NVP; ++j) vd[j] = 0.0f;
         if (in && !PROBE_OFF(8)) {
             const bool zr = a.prev.zero_reset != 0;
-            float4* gc4 = reinterpret_cast<float4*>(a.prev_g_cur);
-            float4* gm4 = reinterpret_cast<float4*>(a.prev_g_mem);
+            float4* gc4 = reinterpret_cast<float4*>(a.prev_g_cur) + pix * (CIN / 4) + ci0 / 4;
+            float4* gm4 = a.prev_g_mem ? reinterpret_cast<float4*>(a.prev_g_mem) + pix * (CIN / 4) + ci0 / 4 : nullptr;
 #pragma unroll
             for (int q = 0; q < QI; ++q) {
                 const float yi[4] = {dy[q].x, dy[q].y, dy[q].z, dy[q].w};
@@ -939,48 +823,255 @@ __global__ __launch_bounds__(NT) void k_layer_bwd(snnflow_layer_bwd_args a) {
                 float go[4], gmo[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int ci = 4 * q + j;
-                    const float gs = gx[ci] + gi[j];
+                    const int cl = 4 * q + j, ci = ci0 + cl;
+                    const float gs = gx[cl] + gi[j];
                     const LifOut o = lif_step(yi[j], mi[j], pcoef[ci], zr);
                     const float gv = atan_sg(o.v - pcoef[ci].theta) * gs;
                     go[j] = gv;
                     gmo[j] = mem_grad(gv, mi[j], pcoef[ci], zr);
-                    vd[ci] = gv;
-                    vd[CIN + ci] = (yi[j] - pmean[ci]) * gv;
-                    vd[2 * CIN + ci] = gv * o.mprime;
+                    vd[cl] = gv;
+                    vd[CI + cl] = (yi[j] - pmean[ci]) * gv;
+                    vd[2 * CI + cl] = gv * o.mprime;
                 }
-                gc4[pix * QI + q] = make_float4(go[0], go[1], go[2], go[3]);
-                if (gm4) gm4[pix * QI + q] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
+                gc4[q] = make_float4(go[0], go[1], go[2], go[3]);
+                if (gm4) gm4[q] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
             }
         }
+        double* acc = acc_shard(a.acc_out, SNNFLOW_BWD_ACC(CIN));
+        if (!PROBE_OFF(4))
+            block_atomic_sum_parts<NVP, SPLIT>(vd, [acc](int pp, int j) {
+                const int k = j / CI, jj = j - k * CI;
+                return acc + k * CIN + pp * CI + jj;
+            });
     } else {
         if (a.g_x && a.wt_bwd_ff && in) {
             float* gb = a.g_x + (int64_t)tl.b * a.gxs_b + h * a.gxs_h + w * a.gxs_w;
 #pragma unroll
-            for (int ci = 0; ci < CIN; ++ci) gb[ci * a.gxs_c] = gx[ci];
+            for (int ci = 0; ci < CI; ++ci) gb[(ci0 + ci) * a.gxs_c] = gx[ci];
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Deferred weight gradients (snnflow_wgrad): one block per tile loops over the time
+// steps of one layer; the next step's loads are issued before the current step's
+// arithmetic (register double buffering); per-thread accumulators live across steps
+// and the block writes its slab once.
+// ---------------------------------------------------------------------------
+typedef const __attribute__((address_space(4))) snnflow_wgrad_args* cwgrad_ptr;
+
+// Accumulator set of one (conv, thread): item q (tap, co-block of 4, ci-block of VW) and
+// pixel group g of the tile, summed over the steps.  Threads [TOFF, TOFF+NTH) of the block
+// take part; items x groups fill them (groups reduced in fixed order by flush).
+template <int CIN, int C, int NTH, int TOFF>
+struct WAcc {
+    static constexpr int VW = VecW<CIN>::v;
+    static constexpr int Q = 9 * (C / 4) * (CIN / VW);
+    static constexpr int GR0 = (Q >= NTH) ? 1 : NTH / Q;
+    static constexpr int GR = GR0 > 16 ? 16 : GR0;
+    static constexpr int NM = (GR > 1) ? 1 : (Q + NTH - 1) / NTH;
+    static constexpr int SCRATCH = (GR > 1) ? GR * Q * 4 * VW : 1;
+    float acc[NM][4][VW];
+    __device__ void zero() {
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < VW; ++j) acc[m][i][j] = 0.f;
+    }
+    // Gi: interior G tile [NT][Pad<C>]; X: halo input tile [HN][Pad<CIN>]
+    __device__ void step(const float* Gi, const float* X) {
+        constexpr int PC = Pad<C>::v, PX = Pad<CIN>::v;
+        const int tid = (int)threadIdx.x - TOFF;
+        if (tid < 0 || tid >= NTH) return;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const int q = (GR > 1) ? tid % Q : tid + m * NTH;
+            const int g = (GR > 1) ? tid / Q : 0;
+            if ((GR > 1) ? (g >= GR) : (q >= Q)) continue;
+            const int kidx = q % 9, rest = q / 9, cob = rest % (C / 4), cib = rest / (C / 4);
+            const int ky = kidx / 3, kx = kidx % 3;
+#pragma unroll 4
+            for (int p = g; p < NT; p += GR) {
+                const int ty = p / TW, tx = p - ty * TW;
+                const float4 gv4 = *reinterpret_cast<const float4*>(Gi + p * PC + cob * 4);
+                const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
+                const float* xp = X + ((ty + ky) * HWD + tx + kx) * PX + cib * VW;
+                float xv[VW];
+                if constexpr (VW == 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(xp);
+                    xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
+                } else if constexpr (VW == 2) {
+                    const float2 v = *reinterpret_cast<const float2*>(xp);
+                    xv[0] = v.x; xv[1] = v.y;
+                } else {
+                    xv[0] = xp[0];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) acc[m][i][j] = fmaf(gv[i], xv[j], acc[m][i][j]);
+            }
+        }
+    }
+    // cross-group reduction in fixed order, then one write (or add) of the block's slab
+    __device__ void flush(float* __restrict__ slab, int accumulate, float* scratch) {
+        const int tid = (int)threadIdx.x - TOFF;
+        const bool mine = tid >= 0 && tid < NTH;
+        if constexpr (GR > 1) {
+            const int q = tid % Q, g = tid / Q;
+            if (mine && g < GR) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) scratch[((g * Q + q) * 4 + i) * VW + j] = acc[0][i][j];
+            }
+            __syncthreads();
+            for (int e = mine ? tid : Q * 4 * VW; e < Q * 4 * VW; e += NTH) {
+                float sum = 0.f;
+                for (int gg = 0; gg < GR; ++gg) sum += scratch[gg * Q * 4 * VW + e];
+                const int qq = e / (4 * VW), ij = e - qq * 4 * VW, i = ij / VW, j = ij - i * VW;
+                const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
+                const int idx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
+                slab[idx] = accumulate ? slab[idx] + sum : sum;
+            }
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const int q = tid + m * NTH;
+                if (!mine || q >= Q) continue;
+                const int kk = q % 9, rest = q / 9, cb = rest % (C / 4), ib = rest / (C / 4);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) {
+                        const int idx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
+                        slab[idx] = accumulate ? slab[idx] + acc[m][i][j] : acc[m][i][j];
+                    }
+            }
+        }
+    }
+};
+
+// own-pixel float4 elements of a C-channel NHWC tile, distributed over NTH threads
+template <int CH, int NTH>
+struct Own4 {
+    static constexpr int Q = CH / 4, E = NT * Q, R = (E + NTH - 1) / NTH;
+};
+
+template <int CIN, int C, bool REC, int SPLIT>
+__global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
+    constexpr int NTB = NT * SPLIT;
+    constexpr int PC = Pad<C>::v, PI_ = Pad<CIN>::v;
+    constexpr bool XV = CIN % 4 == 0;  // x may be dense NHWC (register prefetch)
+    // ff items on all threads; with a recurrent conv and SPLIT = 2 each conv gets one
+    // half of the block (one accumulator set per thread)
+    constexpr bool HALVES = REC && SPLIT == 2;
+    using AF = WAcc<CIN, C, HALVES ? NT : NTB, 0>;
+    using AR = WAcc<C, C, HALVES ? NT : NTB, HALVES ? NT : 0>;
+    using O = Own4<C, NTB>;
+    constexpr int RX = XV ? Halo4<CIN, NTB>::R : 1, RS = REC ? Halo4<C, NTB>::R : 1;
+    constexpr int SCR = (REC && AR::SCRATCH > AF::SCRATCH) ? AR::SCRATCH : AF::SCRATCH;
+    __shared__ __attribute__((aligned(16))) float Gi[NT * PC];
+    __shared__ __attribute__((aligned(16))) float X[HN * PI_];
+    __shared__ __attribute__((aligned(16))) float S[REC ? HN * PC : 4];
+    __shared__ __attribute__((aligned(16))) float scratch[SCR];
+    __shared__ BnBwdLds coef[SNNFLOW_MAX_WGRAD_STEPS][C];
+
+    // the step table stays in the kernarg segment (scalar loads; a dynamically indexed
+    // by-value copy would go to scratch)
+    const cwgrad_ptr ap = (cwgrad_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+    const int tid = threadIdx.x;
+    const int H = ap->H, W = ap->W, nsteps = ap->nsteps;
+    const Tile tl = block_tile(H, W);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    // per-step BN backward coefficients of every channel (one round trip for all steps)
+    for (int e = tid; e < nsteps * C; e += NTB) {
+        const int t = e / C, c = e - t * C;
+        const float* st = ap->steps[t].stats;
+        const float* bc = ap->steps[t].bnc;
+        BnBwdLds k;
+        k.mean = st[c];
+        k.inv = st[C + c];
+        k.gm = bc[c];
+        k.k = bc[C + c];
+        k.w = ap->bn_weight[c];
+        coef[t][c] = k;
     }
 
-    // 6. Stage C: weight gradients (per-block slabs)
-    if (!PROBE_OFF(2)) wgrad_tile<CIN, C>(G, X, slab_ff, oldff, scratch);
-    if constexpr (REC) {
-        if (has_rec) {
-            const float* st = X;
-            if constexpr (SEP) {
-                st = S;
-            } else {
-                __syncthreads();
-                stage_nhwc<C>(a.s_prev, tl, H, W, X);
-                __syncthreads();
-            }
-            if (!PROBE_OFF(2)) wgrad_tile<C, C>(G, st, slab_rec, oldrec, scratch);
-        } else if (!a.accumulate) {
-            for (int e = tid; e < C * C * 9; e += NT) slab_rec[e] = 0.0f;
+    float4 rg[O::R], ry[O::R], rx[RX], rs[RS];
+    bool dense = false, has_s = false;
+    auto issue = [&](int t) {  // loads of step t into registers
+        const float* g = ap->steps[t].g_cur;
+        const float* y = ap->steps[t].y;
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            const int p = e / O::Q, q = e - p * O::Q;
+            const int ty = p / TW, tx = p - ty * TW;
+            const int h = tl.h0 + ty, w = tl.w0 + tx;
+            const bool ok = e < O::E && h < H && w < W;
+            const int64_t k = ok ? (((int64_t)tl.b * H + h) * W + w) * O::Q + q : 0;
+            rg[i] = ok ? reinterpret_cast<const float4*>(g)[k] : z4;
+            ry[i] = ok ? reinterpret_cast<const float4*>(y)[k] : z4;
         }
+        const float* sx = ap->steps[t].x;
+        const float* sp = ap->steps[t].s_prev;
+        dense = false;
+        if constexpr (XV)
+            dense = ap->steps[t].xs_c == 1 && ap->steps[t].xs_w == CIN && ap->steps[t].xs_h == (int64_t)W * CIN &&
+                    ap->steps[t].xs_b == (int64_t)H * W * CIN;
+        if constexpr (XV) {
+            if (dense) halo_load<CIN, NTB>(sx, tl, H, W, rx);
+        }
+        has_s = REC && sp != nullptr;
+        if constexpr (REC) {
+            if (has_s) halo_load<C, NTB>(sp, tl, H, W, rs);
+        }
+    };
+
+    AF af;
+    AR ar;
+    af.zero();
+    if constexpr (REC) ar.zero();
+    issue(0);
+    __syncthreads();  // coef
+    for (int t = 0; t < nsteps; ++t) {
+        // stage step t: G on the tile interior, x and s_prev halos
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < O::E) {
+                const int p = e / O::Q, q = e - p * O::Q;
+                const int ty = p / TW, tx = p - ty * TW;
+                const bool img = tl.h0 + ty < H && tl.w0 + tx < W;  // G = 0 outside the image
+                *reinterpret_cast<float4*>(Gi + p * PC + 4 * q) = img ? bn_bwd4(rg[i], ry[i], &coef[t][4 * q]) : z4;
+            }
+        }
+        const bool dense_t = dense, has_s_t = has_s;
+        if constexpr (XV) {
+            if (dense_t) halo_store<CIN, NTB>(X, rx);
+        }
+        if (!dense_t)
+            stage_strided<CIN, NTB>(ap->steps[t].x, ap->steps[t].xs_b, ap->steps[t].xs_c, ap->steps[t].xs_h,
+                                    ap->steps[t].xs_w, tl, H, W, X);
+        if constexpr (REC) {
+            if (has_s_t) halo_store<C, NTB>(S, rs);
+        }
+        __syncthreads();
+        if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
+        af.step(Gi, X);
+        if constexpr (REC) {
+            if (has_s_t) ar.step(Gi, S);
+        }
+        __syncthreads();
     }
-    if constexpr (LIF_IN) {
-        if (!PROBE_OFF(4)) block_atomic_sum<NVP>(vd, acc_shard(a.acc_out, SNNFLOW_BWD_ACC(CIN)));
-    }
+    const int64_t blk = blockIdx.x;
+    af.flush(ap->slab_ff + blk * (C * CIN * 9), ap->accumulate, scratch);
+    if constexpr (REC) ar.flush(ap->slab_rec + blk * (C * C * 9), ap->accumulate, scratch);
 }
 
 // Sum of per-block weight-gradient slabs in fp64, fixed order: 64 elements x 16 slab
@@ -1034,20 +1125,21 @@ bool valid_c(int c) { return c == 4 || c == 8 || c == 16 || c == 32; }
 
 template <int C>
 int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
-    const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT);
+    constexpr int SP = (C == 8 || C == 16) ? 2 : 1;  // threads per output pixel (C=32: registers)
+    const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT * SP);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: lif_in requires cin == c");
-        if (a.wt_rec) hipLaunchKernelGGL((k_conv_fwd<C, C, true, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_conv_fwd<C, C, true, false>), grid, block, 0, s, a);
+        if (a.wt_rec) hipLaunchKernelGGL((k_conv_fwd<C, C, true, true, SP>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_conv_fwd<C, C, true, false, SP>), grid, block, 0, s, a);
     } else if (a.wt_rec) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: recurrent cell requires cin == c");
-        hipLaunchKernelGGL((k_conv_fwd<C, C, false, true>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((k_conv_fwd<C, C, false, true, SP>), grid, block, 0, s, a);
     } else {
-        if (a.cin == 1) hipLaunchKernelGGL((k_conv_fwd<1, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == 2) hipLaunchKernelGGL((k_conv_fwd<2, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == 4) hipLaunchKernelGGL((k_conv_fwd<4, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == 5) hipLaunchKernelGGL((k_conv_fwd<5, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == C) hipLaunchKernelGGL((k_conv_fwd<C, C, false, false>), grid, block, 0, s, a);
+        if (a.cin == 1) hipLaunchKernelGGL((k_conv_fwd<1, C, false, false, SP>), grid, block, 0, s, a);
+        else if (a.cin == 2) hipLaunchKernelGGL((k_conv_fwd<2, C, false, false, SP>), grid, block, 0, s, a);
+        else if (a.cin == 4) hipLaunchKernelGGL((k_conv_fwd<4, C, false, false, SP>), grid, block, 0, s, a);
+        else if (a.cin == 5) hipLaunchKernelGGL((k_conv_fwd<5, C, false, false, SP>), grid, block, 0, s, a);
+        else if (a.cin == C) hipLaunchKernelGGL((k_conv_fwd<C, C, false, false, SP>), grid, block, 0, s, a);
         else SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: unsupported cin");
     }
     SNN_CHECK_LAUNCH();
@@ -1056,20 +1148,21 @@ int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
 
 template <int C>
 int layer_bwd_c(const snnflow_layer_bwd_args& a, hipStream_t s) {
-    const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT);
+    constexpr int SP = (C == 8 || C == 16) ? 2 : 1;  // threads per pixel (C x C layers; the head keeps 1)
+    const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT * SP), block1(NT);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: lif_in requires cin == c");
-        if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_layer_bwd<C, C, true, false>), grid, block, 0, s, a);
+        if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true, SP>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_layer_bwd<C, C, true, false, SP>), grid, block, 0, s, a);
     } else if (a.wt_bwd_rec) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: recurrent cell requires cin == c");
-        hipLaunchKernelGGL((k_layer_bwd<C, C, false, true>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((k_layer_bwd<C, C, false, true, SP>), grid, block, 0, s, a);
     } else {
-        if (a.cin == 1) hipLaunchKernelGGL((k_layer_bwd<1, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == 2) hipLaunchKernelGGL((k_layer_bwd<2, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == 4) hipLaunchKernelGGL((k_layer_bwd<4, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == 5) hipLaunchKernelGGL((k_layer_bwd<5, C, false, false>), grid, block, 0, s, a);
-        else if (a.cin == C) hipLaunchKernelGGL((k_layer_bwd<C, C, false, false>), grid, block, 0, s, a);
+        if (a.cin == 1) hipLaunchKernelGGL((k_layer_bwd<1, C, false, false, 1>), grid, block1, 0, s, a);
+        else if (a.cin == 2) hipLaunchKernelGGL((k_layer_bwd<2, C, false, false, 1>), grid, block1, 0, s, a);
+        else if (a.cin == 4) hipLaunchKernelGGL((k_layer_bwd<4, C, false, false, 1>), grid, block1, 0, s, a);
+        else if (a.cin == 5) hipLaunchKernelGGL((k_layer_bwd<5, C, false, false, 1>), grid, block1, 0, s, a);
+        else if (a.cin == C) hipLaunchKernelGGL((k_layer_bwd<C, C, false, false, SP>), grid, block, 0, s, a);
         else SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: unsupported cin");
     }
     SNN_CHECK_LAUNCH();
@@ -1173,12 +1266,10 @@ int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
 }
 
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
-    if (!a || !a->y || !a->stats || !a->g_cur || !a->acc_in || !a->x || !a->slab_ff)
-        SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: bad args");
+    if (!a || !a->y || !a->stats || !a->g_cur || !a->acc_in) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: bad args");
     if (!a->ng.bn_weight || !a->ng.bn_bias || !a->ng.beta || !a->ng.threshold)
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: missing parameter-gradient buffers");
     if (a->has_pred && (!a->g_pred_w || !a->g_pred_b)) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: pred gradients");
-    if (a->wt_bwd_rec && !a->slab_rec) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: recurrent layer needs slab_rec");
     if (a->lif_in && (!a->wt_bwd_ff || !a->prev_y || !a->prev_stats || !a->prev_g_cur || !a->acc_out))
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: lif_in needs previous-layer buffers");
     const hipStream_t s = (hipStream_t)stream;
@@ -1189,6 +1280,45 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
         case 32: return layer_bwd_c<32>(*a, s);
         default: SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: c must be 4, 8, 16 or 32");
     }
+}
+
+int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
+    if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || a->nsteps <= 0 || a->nsteps > SNNFLOW_MAX_WGRAD_STEPS ||
+        !a->bn_weight || !a->slab_ff || (a->rec && !a->slab_rec))
+        SNN_FAIL(SNNFLOW_E_ARG, "wgrad: bad args");
+    for (int t = 0; t < a->nsteps; ++t) {
+        const snnflow_wgrad_step& st = a->steps[t];
+        if (!st.g_cur || !st.y || !st.x || !st.stats || !st.bnc) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: incomplete step");
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(snnflow_conv_blocks(a->B, a->H, a->W));
+    const int c = a->c, cin = a->cin;
+    if (!valid_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: c must be 4, 8, 16 or 32");
+#define WG_LAUNCH(CI_, CC_, REC_)                                                                          \
+    do {                                                                                                   \
+        constexpr int SP_ = (CC_ == 8 || CC_ == 16) ? 2 : 1;                                               \
+        hipLaunchKernelGGL((k_wgrad<CI_, CC_, REC_, SP_>), grid, dim3(NT * SP_), 0, s, *a);               \
+    } while (0)
+#define WG_CASE(CC_)                                                                                       \
+    case CC_:                                                                                              \
+        if (a->rec) {                                                                                      \
+            if (cin != CC_) SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: recurrent layer requires cin == c");      \
+            WG_LAUNCH(CC_, CC_, true);                                                                     \
+        } else if (cin == CC_) WG_LAUNCH(CC_, CC_, false);                                                 \
+        else if (cin == 1) WG_LAUNCH(1, CC_, false);                                                       \
+        else if (cin == 2) WG_LAUNCH(2, CC_, false);                                                       \
+        else if (cin == 4) WG_LAUNCH(4, CC_, false);                                                       \
+        else if (cin == 5) WG_LAUNCH(5, CC_, false);                                                       \
+        else SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: unsupported cin");                                       \
+        break;
+    switch (c) {
+        WG_CASE(4) WG_CASE(8) WG_CASE(16) WG_CASE(32)
+        default: break;
+    }
+#undef WG_CASE
+#undef WG_LAUNCH
+    SNN_CHECK_LAUNCH();
+    return 0;
 }
 
 int snnflow_slab_reduce(const snnflow_slab_desc* d, int n, int nblk, void* stream) {

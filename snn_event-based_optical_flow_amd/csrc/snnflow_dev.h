@@ -99,13 +99,13 @@ __device__ inline float4 ld4_or_zero(const float4* p, const float4* fallback, in
 __device__ inline bool in_image(int h, int w, int H, int W) { return h >= 0 && h < H && w >= 0 && w < W; }
 
 // A C-channel NHWC halo tile as float4 elements e = pixel * (C/4) + quad, distributed
-// round-robin over the block's threads (element e -> thread e % NT, slot e / NT), so a
-// thread issues all R of its loads before using any (register prefetch).
-template <int CH>
+// round-robin over the block's NTH threads (element e -> thread e % NTH, slot e / NTH),
+// so a thread issues all R of its loads before using any (register prefetch).
+template <int CH, int NTH = NT>
 struct Halo4 {
     static constexpr int Q = CH / 4;  // meaningful for CH % 4 == 0 only
     static constexpr int E = HN * Q;
-    static constexpr int R = (E + NT - 1) / NT;
+    static constexpr int R = (E + NTH - 1) / NTH;
 };
 
 // float4 index of halo element e in an NHWC tensor with CH channels; -1 outside the tile/image.
@@ -120,23 +120,23 @@ __device__ inline int64_t halo_idx4(int e, const Tile& tl, int H, int W) {
     return (((int64_t)tl.b * H + h) * W + w) * Q + q;
 }
 
-template <int CH>
+template <int CH, int NTH = NT>
 __device__ inline void halo_load(const float* __restrict__ src, const Tile& tl, int H, int W,
-                                 float4 (&r)[Halo4<CH>::R]) {
+                                 float4 (&r)[Halo4<CH, NTH>::R]) {
 #pragma unroll
-    for (int i = 0; i < Halo4<CH>::R; ++i) {
-        const int64_t k = halo_idx4<CH>(threadIdx.x + i * NT, tl, H, W);
+    for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
+        const int64_t k = halo_idx4<CH>(threadIdx.x + i * NTH, tl, H, W);
         r[i] = (k >= 0) ? reinterpret_cast<const float4*>(src)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
 
-template <int CH>
-__device__ inline void halo_store(float* tile, const float4 (&r)[Halo4<CH>::R]) {
+template <int CH, int NTH = NT>
+__device__ inline void halo_store(float* tile, const float4 (&r)[Halo4<CH, NTH>::R]) {
     constexpr int Q = CH / 4;
 #pragma unroll
-    for (int i = 0; i < Halo4<CH>::R; ++i) {
-        const int e = threadIdx.x + i * NT;
-        if (e < Halo4<CH>::E) {
+    for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
+        const int e = threadIdx.x + i * NTH;
+        if (e < Halo4<CH, NTH>::E) {
             const int p = e / Q, q = e - p * Q;
             *reinterpret_cast<float4*>(tile + p * Pad<CH>::v + 4 * q) = r[i];
         }

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class Neuron(ctypes.Structure):
@@ -60,14 +60,26 @@ class LayerBwdArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
                 ("y", P), ("stats", P), ("g_cur", P), ("acc_in", P), ("n", Neuron), ("ng", NeuronGrad),
                 ("has_pred", I32), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32),
-                ("wt_bwd_ff", P), ("wt_bwd_rec", P), ("lif_in", I32),
-                ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
-                ("s_prev", P), ("slab_ff", P), ("slab_rec", P),
+                ("bnc_out", P), ("wt_bwd_ff", P), ("wt_bwd_rec", P), ("lif_in", I32),
                 ("g_x", P), ("gxs_b", I64), ("gxs_c", I64), ("gxs_h", I64), ("gxs_w", I64),
                 ("g_state_prev", P), ("zero_mem_half", I32),
                 ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),
                 ("prev_g_state", P), ("prev_g_cur", P), ("prev_g_mem", P), ("acc_out", P),
                 ("zero0", P), ("zero1", P), ("zero_n", I32)]
+
+
+MAX_WGRAD_STEPS = 32
+
+
+class WgradStep(ctypes.Structure):
+    _fields_ = [("g_cur", P), ("y", P), ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
+                ("s_prev", P), ("stats", P), ("bnc", P)]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32), ("nsteps", I32),
+                ("accumulate", I32), ("rec", I32), ("bn_weight", P), ("slab_ff", P), ("slab_rec", P),
+                ("steps", WgradStep * MAX_WGRAD_STEPS)]
 
 
 ACC_SHARDS = 32  # SNNFLOW_ACC_SHARDS
@@ -113,6 +125,7 @@ EXPORTS = {
     "snnflow_lif_fwd": (I32, [ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_lif_bwd": (I32, [ctypes.POINTER(LifBwdArgs), P]),
     "snnflow_layer_bwd": (I32, [ctypes.POINTER(LayerBwdArgs), P]),
+    "snnflow_wgrad": (I32, [ctypes.POINTER(WgradArgs), P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
     "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P]),

@@ -282,13 +282,11 @@ class CellFn(torch.autograd.Function):
 
         slab_ff = torch.empty(ws.nblk, C * cin * 9, device=dev)
         slab_rec = torch.empty(ws.nblk, C * C * 9, device=dev) if cell.recurrent else None
+        bnc = torch.empty(2, C, device=dev)
         a = _lib.LayerBwdArgs()
         a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin, C, 0
         a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(y), ptr(stats), ptr(g_cur), ptr(bacc), n
-        a.ng, a.accumulate = ng, 0
-        a.x = ptr(x)
-        a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
-        a.s_prev, a.slab_ff, a.slab_rec = _ptr_t(sp), ptr(slab_ff), _ptr_t(slab_rec)
+        a.ng, a.accumulate, a.bnc_out = ng, 0, ptr(bnc)
         gx = None
         if ctx.needs_input_grad[1]:
             gx = torch.empty_like(x)
@@ -299,6 +297,19 @@ class CellFn(torch.autograd.Function):
             if g_prev is not None:
                 a.g_state_prev, a.zero_mem_half = ptr(g_prev), 0
         _lib.call("layer_bwd", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+        # weight gradients of this single step (snnflow_wgrad with one step)
+        slab_ff = torch.empty(ws.nblk, C * cin * 9, device=dev)
+        slab_rec = torch.empty(ws.nblk, C * C * 9, device=dev) if cell.recurrent else None
+        wa = _lib.WgradArgs()
+        wa.B, wa.H, wa.W, wa.cin, wa.c, wa.nsteps, wa.accumulate = B, H, W, cin, C, 1, 0
+        wa.rec = 1 if cell.recurrent else 0
+        wa.bn_weight, wa.slab_ff, wa.slab_rec = ptr(cell.bn.weight), ptr(slab_ff), _ptr_t(slab_rec)
+        st = wa.steps[0]
+        st.g_cur, st.y, st.stats, st.bnc = ptr(g_cur), ptr(y), ptr(stats), ptr(bnc)
+        st.x = ptr(x)
+        st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
+        st.s_prev = _ptr_t(sp) if cell.recurrent else None
+        _lib.call("wgrad", lib.snnflow_wgrad, ctypes.byref(wa), s)
         g_wff = torch.empty_like(cell.ff.weight)
         descs = [_lib.SlabDesc(ptr(slab_ff), ptr(g_wff), g_wff.numel())]
         g_wrec = None

@@ -78,7 +78,6 @@ class Workspace:
         self.fwd_acc = torch.zeros(max(layers, 1), _lib.acc_storage(2 * C), dtype=torch.float64, device=device)
         self.bwd_acc = torch.zeros(max(layers, 1), _lib.acc_storage(_lib.bwd_acc_len(C)), dtype=torch.float64,
                                    device=device)
-        self.gcur = torch.empty(2, B, H, W, C, dtype=torch.float32, device=device)
         self.slab_ff = []
         self.slab_rec = []
         self.device = device
@@ -155,6 +154,7 @@ class FireNetEngine:
         self.bwd_open = False
         self.flat = None
         self.flat_views = None
+        self.pending = []   # per-step tensors of the open backward chain (deferred wgrad)
 
     # parameter order = Function input order after the states
     def param_list(self):
@@ -206,6 +206,43 @@ class FireNetEngine:
         self.flat_views = views
         self.flat_layout = layout
         self.bwd_open = True
+
+    def flush_weight_grads(self, B, H, W, cin0, ws, glayers, stream):
+        """Deferred weight gradients of every layer over all pending time steps (one
+        snnflow_wgrad launch per layer and <= 32 steps), then the slab reduction into the
+        flat gradient buffer (x, s_prev, y, stats saved per step)."""
+        L, C = self.L, self.C
+        steps = self.pending
+        self.pending = []
+        for l in range(L):
+            rec = self.rec[l]
+            for i0 in range(0, len(steps), _lib.MAX_WGRAD_STEPS):
+                chunk = steps[i0:i0 + _lib.MAX_WGRAD_STEPS]
+                a = _lib.WgradArgs()
+                a.B, a.H, a.W, a.c = B, H, W, C
+                a.cin = cin0 if l == 0 else C
+                a.nsteps, a.accumulate, a.rec = len(chunk), 1 if i0 else 0, 1 if rec else 0
+                a.bn_weight = ptr(self.cells[l].bn.weight)
+                a.slab_ff, a.slab_rec = ptr(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
+                for k, (gcur, bnc, ys, stats, x, states, s_prev) in enumerate(chunk):
+                    st = a.steps[k]
+                    st.g_cur, st.y, st.stats, st.bnc = ptr(gcur[l]), ptr(ys[l]), ptr(stats[l]), ptr(bnc[l])
+                    if l == 0:
+                        st.x = ptr(x)
+                        st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
+                    else:
+                        st.x, (st.xs_b, st.xs_c, st.xs_h, st.xs_w) = _spk_half(states[l - 1])
+                    st.s_prev = _ptr_t(s_prev[l]) if rec else None
+                _lib.call(f"wgrad[{l}]", lib.snnflow_wgrad, ctypes.byref(a), stream)
+        descs = []
+        for l in range(L):
+            gff, grec, _ = glayers[l]
+            descs.append(_lib.SlabDesc(ptr(ws.slab_ff[l]), ptr(gff), gff.numel()))
+            if grec is not None:
+                descs.append(_lib.SlabDesc(ptr(ws.slab_rec[l]), ptr(grec), grec.numel()))
+        for i0 in range(0, len(descs), 16):
+            chunk = (_lib.SlabDesc * len(descs[i0:i0 + 16]))(*descs[i0:i0 + 16])
+            _lib.call("slab_reduce", lib.snnflow_slab_reduce, chunk, len(descs[i0:i0 + 16]), ws.nblk, stream)
 
     def grad_views(self):
         """Per-layer gradient destinations inside the flat buffer."""
@@ -355,7 +392,6 @@ class FireNetStep(torch.autograd.Function):
         neurons = [neuron_struct(c) for c in eng.cells]
         bacc = ws.bwd_acc
         zn = bacc.shape[1]
-        slab_ff, slab_rec = ws.slab_ff, ws.slab_rec
         gst = [as_nhwc_state(g) if g is not None else None for g in g_states]
         # gradients of the previous states: the spike half of recurrent cells (rec dgrad);
         # for states that did not come from this engine also the membrane half
@@ -371,6 +407,9 @@ class FireNetStep(torch.autograd.Function):
                 g_prev[l] = empty_state(B, C, H, W, dev)
         gmem = [g_prev[l] if (g_prev[l] is not None and ctx.ext[l]) else None for l in range(L)]
 
+        # per-step buffers kept until the deferred weight gradients run (root step)
+        gcur = torch.empty(L, B, H, W, C, device=dev)   # dL/d BN-output of every layer
+        bnc = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
         try:
             # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
             top = L - 1
@@ -383,7 +422,7 @@ class FireNetStep(torch.autograd.Function):
                 if g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32:
                     g_flow = g_flow.contiguous().float()
                 b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
-            b.g_cur, b.g_mem = ptr(ws.gcur[top % 2]), _ptr_t(gmem[top])
+            b.g_cur, b.g_mem = ptr(gcur[top]), _ptr_t(gmem[top])
             b.acc = ptr(bacc[top])
             b.zero0, b.zero_n = ptr(bacc[0]), zn
             _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
@@ -392,12 +431,10 @@ class FireNetStep(torch.autograd.Function):
             for l in range(L - 1, -1, -1):
                 a = _lib.LayerBwdArgs()
                 a.B, a.H, a.W, a.c = B, H, W, C
-                a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(ys[l]), ptr(stats[l]), ptr(ws.gcur[l % 2]), ptr(bacc[l]), neurons[l]
-                a.ng, a.accumulate = glayers[l][2], acc
+                a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(ys[l]), ptr(stats[l]), ptr(gcur[l]), ptr(bacc[l]), neurons[l]
+                a.ng, a.accumulate, a.bnc_out = glayers[l][2], acc, ptr(bnc[l])
                 if l == L - 1:
                     a.has_pred, a.g_pred_w, a.g_pred_b = 1, ptr(gpw), ptr(gpb)
-                a.s_prev = _ptr_t(s_prev[l])
-                a.slab_ff, a.slab_rec = ptr(slab_ff[l]), _ptr_t(slab_rec[l])
                 if l + 1 <= L - 1:
                     a.zero0, a.zero_n = ptr(bacc[l + 1]), zn
                 if eng.rec[l]:
@@ -408,37 +445,29 @@ class FireNetStep(torch.autograd.Function):
                 if l > 0:
                     a.cin, a.lif_in = C, 1
                     a.wt_bwd_ff = ptr(wbwd[l][0])
-                    a.x, (a.xs_b, a.xs_c, a.xs_h, a.xs_w) = _spk_half(states[l - 1])
                     a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
                     a.prev_g_state = _ptr_t(gst[l - 1])
-                    a.prev_g_cur, a.prev_g_mem = ptr(ws.gcur[(l - 1) % 2]), _ptr_t(gmem[l - 1])
+                    a.prev_g_cur, a.prev_g_mem = ptr(gcur[l - 1]), _ptr_t(gmem[l - 1])
                     a.acc_out = ptr(bacc[l - 1])
                 else:
                     a.cin, a.lif_in = cin0, 0
-                    a.x = ptr(x)
-                    a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
                     if ctx.needs_input_grad[1]:
                         gx = torch.empty_like(x)
                         a.wt_bwd_ff = ptr(wbwd[0][0])
                         a.g_x = ptr(gx)
                         a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
                 _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+            eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev))
+            if ctx.root:
+                eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s)
         except Exception:
             ws.reset_acc()
             eng.bwd_open = False
+            eng.pending = []
             raise
 
         grads = [None] * len(eng.flat_layout)
         if ctx.root:
-            descs = []
-            for l in range(L):
-                gff, grec, _ = glayers[l]
-                descs.append(_lib.SlabDesc(ptr(slab_ff[l]), ptr(gff), gff.numel()))
-                if grec is not None:
-                    descs.append(_lib.SlabDesc(ptr(slab_rec[l]), ptr(grec), grec.numel()))
-            for i0 in range(0, len(descs), 16):
-                chunk = (_lib.SlabDesc * len(descs[i0:i0 + 16]))(*descs[i0:i0 + 16])
-                _lib.call("slab_reduce", lib.snnflow_slab_reduce, chunk, len(descs[i0:i0 + 16]), ws.nblk, s)
             # fresh views, no other reference: AccumulateGrad adopts them as .grad
             # instead of copying (all gradients then live in one flat buffer)
             grads = [eng.flat[o:o + n].view(shp) for o, n, shp in eng.flat_layout]

@@ -26,10 +26,8 @@ def main():
     C, R, B, T, N = 8, 128, 8, 10, 1000
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    kw = {"name": "LIFFireNet", "encoding": "cnt", "round_encoding": False, "norm_input": False, "num_bins": 2,
-          "base_num_channels": C, "kernel_size": 3, "activations": ["arctanspike", "arctanspike"],
-          "mask_output": True, "quantization": {"enabled": False}, "tebn": {"enabled": False},
-          "mpbn": {"enabled": False}, "spiking_neuron": {"leak": [0.0, 1.0], "thresh": [0.0, 0.8]}}
+    from snnflow.parser import train_snn_model_kwargs
+    kw = train_snn_model_kwargs(base_num_channels=C)
     model = snnflow.LIFFireNet(kw).to(dev).train()
     cfg = {"loader": {"resolution": [R, R]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
            "model": {"mask_output": True}}

@@ -7,14 +7,14 @@ sys.path[:0] = [REPO, os.path.join(REPO, "snn_event-based_optical_flow_amd")]
 import torch  # noqa: E402
 
 import snnflow  # noqa: E402
-from oracle import lif_ref  # noqa: E402
+from snnflow.parser import train_snn_model_kwargs  # noqa: E402
 from snnflow.synthetic import make_window  # noqa: E402
 
 
 def main(C=8, R=128, B=8, T=10, steps=3):
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
-    model = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=C)).to(dev).train()
+    model = snnflow.LIFFireNet(train_snn_model_kwargs(base_num_channels=C)).to(dev).train()
     cfg = {"loader": {"resolution": [R, R]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
            "model": {"mask_output": True}}
     lf = snnflow.EventWarping(cfg, dev)
