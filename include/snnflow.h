@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 6
+#define SNNFLOW_ABI_VERSION 7
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -198,18 +198,69 @@ typedef struct snnflow_wgrad_step {
     const float* y;             /* NHWC pre-BN conv output */
     const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* ff conv input (strided) */
     const float* s_prev;        /* NHWC previous-step spikes (rec conv input) or NULL */
-    const float* stats;         /* [2][c] mean, invstd */
-    const float* bnc;           /* [2][c] grad_mean, k */
+    const float* stats;         /* [2][c] mean, invstd; NULL: no BatchNorm (G = g_cur, ConvLIF) */
+    const float* bnc;           /* [2][c] grad_mean, k (ignored without stats) */
 } snnflow_wgrad_step;
 #define SNNFLOW_MAX_WGRAD_STEPS 32
 typedef struct snnflow_wgrad_args {
     int B, H, W, cin, c, nsteps, accumulate, rec;
-    const float* bn_weight;     /* [c] gamma */
+    const float* bn_weight;     /* [c] gamma (ignored without stats) */
     float* slab_ff;             /* snnflow_conv_blocks() x c*cin*9 */
     float* slab_rec;            /* snnflow_conv_blocks() x c*c*9 (rec layers) */
     snnflow_wgrad_step steps[SNNFLOW_MAX_WGRAD_STEPS];
 } snnflow_wgrad_args;
 int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream);
+
+/* ---- U-Net neuron flavour: ConvLIF / ConvLIFRecurrent ----------------------
+ * models/spiking_submodules.py:121-151 (ConvLIF, stride 1), :265-300 (ConvLIFRecurrent):
+ *   I = conv_ff(x) [+ conv_rec(z_prev)];  leak = sigmoid(leak_raw);  th = clamp_min(thresh, 0.01)
+ *   hard: v_out = v*leak*(1 - z) + (1 - leak)*I    soft: v_out = v*leak + (1 - leak)*I - z*th
+ *   z_out = (v_out - th > 0); backward of the spike: g / (1 + width*(v_out - th)^2) (ArctanSpike,
+ *   models/spiking_util.py:82-109); z (reset) detached, v not (BPTT through the membrane).
+ * No normalisation; weights prepared by snnflow_prep_weights.  The weight gradients come from
+ * snnflow_wgrad with stats = NULL (G = g_current). */
+typedef struct snnflow_convlif_params {
+    const float* leak;          /* [c] raw leak parameter */
+    const float* thresh;        /* [c] raw threshold */
+    float act_width;
+    int hard_reset;
+} snnflow_convlif_params;
+
+typedef struct snnflow_convlif_fwd_args {
+    int B, H, W, cin, c;
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;   /* input (strided) */
+    const float* prev_state;    /* [2][B][H][W][c] (v, z) or NULL (zeros) */
+    const float* wt_ff;         /* [3][3][cin][c] */
+    const float* wt_rec;        /* [3][3][c][c] (ConvLIFRecurrent) or NULL */
+    snnflow_convlif_params p;
+    const float* residual; int64_t rs_b, rs_c, rs_h, rs_w;   /* added to the spikes, or NULL */
+    float* out;                 /* NHWC z_out + residual */
+    float* state;               /* [2][B][H][W][c] (v_out, z_out) */
+    float* current;             /* NHWC I, saved for the backward pass */
+} snnflow_convlif_fwd_args;
+int snnflow_convlif_fwd(const snnflow_convlif_fwd_args* a, void* stream);
+
+typedef struct snnflow_convlif_bwd_args {
+    int B, H, W, cin, c;
+    const float* g_out; int64_t gs_b, gs_c, gs_h, gs_w;   /* grad of out (strided) or NULL */
+    const float* g_state;       /* [2][B][H][W][c] grad of (v_out, z_out) or NULL */
+    const float* state;         /* the forward's state output */
+    const float* prev_state;    /* [2][B][H][W][c] or NULL */
+    const float* current;       /* the forward's current */
+    const float* wt_bwd_ff;     /* [3][3][c][cin] or NULL (no input gradient) */
+    const float* wt_bwd_rec;    /* [3][3][c][c] or NULL */
+    snnflow_convlif_params p;
+    float* g_x; int64_t gxs_b, gxs_c, gxs_h, gxs_w;   /* or NULL */
+    float* g_prev;              /* [2][B][H][W][c] grad of prev_state or NULL */
+    float* g_current;           /* NHWC dL/dI (input of snnflow_wgrad) */
+    double* acc;                /* += SNNFLOW_ACC_LEN(2c): sum dL/dth, sum dL/dleak (must start zeroed) */
+} snnflow_convlif_bwd_args;
+int snnflow_convlif_bwd(const snnflow_convlif_bwd_args* a, void* stream);
+
+/* Parameter gradients from the backward sums: g_thresh = sum * (thresh >= 0.01) (clamp_min),
+ * g_leak = sum * s * (1 - s), s = sigmoid(leak) (written, or added when accumulate). */
+int snnflow_convlif_param_grads(const double* acc, const float* leak, const float* thresh, int c, int accumulate,
+                                float* g_leak, float* g_thresh, void* stream);
 
 /* Sums per-block weight-gradient slabs: out[i][e] = sum_b slab[i][b][e]. */
 typedef struct snnflow_slab_desc { const float* slab; float* out; int elems; } snnflow_slab_desc;

@@ -13,6 +13,7 @@
 #include <string>
 
 #include "snnflow_dev.h"
+#include "snnflow_tile.h"
 
 // Timing-attribution builds only (tools/kprobe.py): each set bit removes one stage,
 // results are then meaningless.  0 in every shipped build.
@@ -41,125 +42,6 @@ int snnflow_set_error(int code, const char* msg) {
 
 namespace {
 
-// ---------------------------------------------------------------------------
-// LDS staging of a halo tile
-// ---------------------------------------------------------------------------
-
-// Strided input (e.g. event_cnt NCHW, or an NHWC spike tensor) -> tile[p][ci]
-template <int CIN, int NTH = NT>
-__device__ void stage_strided(const float* __restrict__ x, int64_t sb, int64_t sc, int64_t sh, int64_t sw,
-                              const Tile& tl, int H, int W, float* tile) {
-    constexpr int P = Pad<CIN>::v;
-    const int tid = threadIdx.x;
-    const float* xb = x + (int64_t)tl.b * sb;
-    if (sc == 1) {
-        for (int e = tid; e < HN * CIN; e += NTH) {
-            const int p = e / CIN, ci = e - p * CIN;
-            const int r = p / HWD, cc = p - r * HWD;
-            const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-            tile[p * P + ci] = in_image(h, w, H, W) ? xb[h * sh + w * sw + ci] : 0.0f;
-        }
-    } else {
-        for (int e = tid; e < HN * CIN; e += NTH) {
-            const int ci = e / HN, p = e - ci * HN;
-            const int r = p / HWD, cc = p - r * HWD;
-            const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-            tile[p * P + ci] = in_image(h, w, H, W) ? xb[ci * sc + h * sh + w * sw] : 0.0f;
-        }
-    }
-}
-
-// Contiguous NHWC [B][H][W][C] (C % 4 == 0) -> tile
-template <int C, int NTH = NT>
-__device__ void stage_nhwc(const float* __restrict__ x, const Tile& tl, int H, int W, float* tile) {
-    static_assert(C % 4 == 0, "vector staging");
-    constexpr int P = Pad<C>::v, Q = C / 4;
-    const int tid = threadIdx.x;
-    for (int e = tid; e < HN * Q; e += NTH) {
-        const int p = e / Q, q = e - p * Q;
-        const int r = p / HWD, cc = p - r * HWD;
-        const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (in_image(h, w, H, W))
-            v = *reinterpret_cast<const float4*>(x + (((int64_t)tl.b * H + h) * W + w) * C + 4 * q);
-        *reinterpret_cast<float4*>(tile + p * P + 4 * q) = v;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// 3x3 convolution of one output pixel (outputs [co0, co0+CO)) from an LDS halo tile.
-// wt: [3][3][CIN][C]; co0 must be wave-uniform (scalar weight loads).
-// acc += sum_{ky,kx,ci} w * x.
-// ---------------------------------------------------------------------------
-template <int CIN, int C, int CO = C>
-__device__ inline void conv_acc(const float* tile, const float* __restrict__ wt, int ty, int tx, int co0,
-                                float (&acc)[CO]) {
-    constexpr int P = Pad<CIN>::v, VW = VecW<CIN>::v;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const float* xp = tile + ((ty + ky) * HWD + (tx + kx)) * P;
-            const cfloat_ptr wk = as_const(wt) + (ky * 3 + kx) * CIN * C + co0;
-            constexpr int UR = CIN <= 8 ? CIN : 1;
-#pragma unroll UR
-            for (int ci = 0; ci < CIN; ci += VW) {
-                float xs[VW];
-                if constexpr (VW == 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(xp + ci);
-                    xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
-                } else if constexpr (VW == 2) {
-                    const float2 v = *reinterpret_cast<const float2*>(xp + ci);
-                    xs[0] = v.x; xs[1] = v.y;
-                } else {
-                    xs[0] = xp[ci];
-                }
-#pragma unroll
-                for (int j = 0; j < VW; ++j) {
-#pragma unroll
-                    for (int co = 0; co < CO; ++co) acc[co] = fmaf(wk[(ci + j) * C + co], xs[j], acc[co]);
-                }
-            }
-        }
-    }
-}
-
-// Transposed 3x3 (input gradient, inputs [ci0, ci0+CI)) of one pixel from an LDS tile of
-// output gradients.  wd: [3][3][C][CIN]; ci0 wave-uniform.
-// gx[ci] += sum_{ky,kx,co} w[co][ci][ky][kx] * g[h+1-ky][w+1-kx][co]
-template <int C, int CIN, int CI = CIN>
-__device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ wd, int ty, int tx, int ci0,
-                                 float (&gx)[CI]) {
-    constexpr int P = Pad<C>::v;
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
-            const float* gp = gtile + ((ty + 2 - ky) * HWD + (tx + 2 - kx)) * P;
-            const cfloat_ptr wk = as_const(wd) + (ky * 3 + kx) * C * CIN + ci0;
-            constexpr int UR = C <= 8 ? C : 1;
-#pragma unroll UR
-            for (int co = 0; co < C; co += 4) {
-                const float4 v = *reinterpret_cast<const float4*>(gp + co);
-                const float gs[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                    for (int ci = 0; ci < CI; ++ci) gx[ci] = fmaf(wk[(co + j) * CIN + ci], gs[j], gx[ci]);
-                }
-            }
-        }
-    }
-}
-
-// Opaque use of a register array: stops LLVM from sinking its computation into a
-// following conditional block (where the scalar-weight schedule no longer fits).
-template <int N>
-__device__ inline void pin(float (&v)[N]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
-}
-
 // dL/dm of the membrane input: v = beta*((1-r)*m) + I (zero reset) or beta*m + I - r*theta;
 // r = H(m - theta) is detached (snntorch mem_reset).
 __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_reset) {
@@ -169,74 +51,26 @@ __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_
     return gmp * (1.0f - r);
 }
 
-// Block-level sums of per-thread floats, then one fp64 atomic add per sum.  The block's
-// threads form PARTS groups of NT consecutive threads (whole waves); each group sums
-// its own NV values and dst(part, j) is the accumulator address of sum j of group part.
-template <int NV, int PARTS, typename Dst>
-__device__ void block_atomic_sum_parts(const float (&v)[NV], Dst dst) {
-    constexpr int WPP = NT / 64, NW = WPP * PARTS;
-    __shared__ float red[NW][NV];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-        const float s = wave_total(v[j]);
-        if (lane == 0) red[wv][j] = s;
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < PARTS * NV; t += NT * PARTS) {
-        const int part = t / NV, j = t - part * NV;
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < WPP; ++w) s += (double)red[part * WPP + w][j];
-        atomicAdd(dst(part, j), s);
-    }
-}
+// Per-channel neuron / BatchNorm parameters of one layer, loaded by threads c < C at
+// kernel start, before the barrier-separated prologue: their round trip then overlaps
+// the halo loads instead of following the batch-sum gather.
+struct NeuronRegs { float w, b, beta, theta, rm, rv; };
 
-template <int NV>
-__device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
-    block_atomic_sum_parts<NV, 1>(v, [acc](int, int j) { return acc + j; });
-}
-
-// Accumulators already consumed by an earlier kernel of the chain are zeroed here
-// (grid-stride over all threads of the launch).
-__device__ inline void zero_consumed(double* z0, double* z1, int n) {
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        if (z0) z0[j] = 0.0;
-        if (z1) z1[j] = 0.0;
-    }
-}
-
-// Totals of the M sums of a sharded accumulator (n sums per replica, M <= n, M <= NT)
-// into LDS out[M]: TPJ = NT/M threads per sum each add a strided subset of the
-// replicas (all their loads in flight at once), then one LDS pass.  One global round
-// trip; called by every thread of the block (contains barriers).
-template <int M>
-__device__ void acc_gather(const double* acc, int n, double* out) {
-    static_assert(M >= 1 && M <= NT, "acc_gather: M sums");
-    constexpr int TPJ = NT / M;
-    constexpr int PER = (kAccShards + TPJ - 1) / TPJ;
-    __shared__ double red[TPJ * M];
-    const int tid = threadIdx.x, st = acc_stride(n);
-    if (tid < TPJ * M) {
-        const int j = tid % M, g = tid / M;
-        double v[PER];
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int sh = g + k * TPJ;
-            v[k] = sh < kAccShards ? acc[sh * st + j] : 0.0;
+__device__ inline NeuronRegs load_neuron(const snnflow_neuron& n, int C) {
+    NeuronRegs r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int c = threadIdx.x;
+    if (c < C) {
+        r.w = n.bn_weight[c];
+        r.b = n.bn_bias[c];
+        r.beta = n.beta[c];
+        r.theta = n.threshold[c];
+        // running statistics: every block in eval mode, block 0 (the updater) in train mode
+        if (n.running_mean && (!n.bn_train || blockIdx.x == 0)) {
+            r.rm = n.running_mean[c];
+            r.rv = n.running_var[c];
         }
-        double sum = 0.0;
-#pragma unroll
-        for (int k = 0; k < PER; ++k) sum += v[k];
-        red[g * M + j] = sum;
     }
-    __syncthreads();
-    if (tid < M) {
-        double sum = 0.0;
-        for (int g = 0; g < TPJ; ++g) sum += red[g * M + tid];
-        out[tid] = sum;
-    }
-    __syncthreads();
+    return r;
 }
 
 // BatchNorm statistics of channel c from batch sums (train; sums[c] = S, sums[C+c] = SS)
@@ -244,7 +78,8 @@ __device__ void acc_gather(const double* acc, int n, double* out) {
 // invstd = 1/sqrt(var + eps) in fp64.
 struct BnStat { float mean, invstd; double dmean, dvar; };
 
-__device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* sums, int C, int c, double N) {
+__device__ inline BnStat bn_stat(const snnflow_neuron& n, const NeuronRegs& r, const double* sums, int C, int c,
+                                 double N) {
     BnStat st;
     if (n.bn_train) {
         st.dmean = sums[c] / N;
@@ -253,10 +88,10 @@ __device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* sums, in
         st.mean = (float)st.dmean;
         st.invstd = (float)(1.0 / sqrt(st.dvar + n.eps));
     } else {
-        st.dmean = n.running_mean[c];
-        st.dvar = n.running_var[c];
-        st.mean = n.running_mean[c];
-        st.invstd = (float)(1.0 / sqrt((double)n.running_var[c] + n.eps));
+        st.dmean = r.rm;
+        st.dvar = r.rv;
+        st.mean = r.rm;
+        st.invstd = (float)(1.0 / sqrt((double)r.rv + n.eps));
     }
     return st;
 }
@@ -264,19 +99,17 @@ __device__ inline BnStat bn_stat(const snnflow_neuron& n, const double* sums, in
 // Prologue of a LIF consumer: per-channel coefficients in LDS; block 0 also stores
 // (mean, invstd) for the backward pass and performs the running-stat update
 // (momentum, unbiased variance) and num_batches_tracked += 1 of torch's BatchNorm2d.
-// `sums`: LDS totals from acc_gather (train mode only).
-__device__ void lif_prologue(const snnflow_neuron& n, const double* sums, int C, double N, float* stats_out,
-                             LifCoef* coef, float* mean_out) {
+// `sums`: LDS totals from acc_gather (train mode only); r: load_neuron of this thread.
+__device__ void lif_prologue(const snnflow_neuron& n, const NeuronRegs& r, const double* sums, int C, double N,
+                             float* stats_out, LifCoef* coef, float* mean_out) {
     const int c = threadIdx.x;
     if (c < C) {
-        const float rm = (blockIdx.x == 0 && n.bn_train && n.running_mean) ? n.running_mean[c] : 0.f;
-        const float rv = (blockIdx.x == 0 && n.bn_train && n.running_mean) ? n.running_var[c] : 0.f;
-        const BnStat st = bn_stat(n, sums, C, c, N);
+        const BnStat st = bn_stat(n, r, sums, C, c, N);
         LifCoef k;
-        k.alpha = st.invstd * n.bn_weight[c];
-        k.shift = n.bn_bias[c] - st.mean * k.alpha;
-        k.beta = fminf(fmaxf(n.beta[c], 0.0f), 1.0f);
-        k.theta = n.threshold[c];
+        k.alpha = st.invstd * r.w;
+        k.shift = r.b - st.mean * k.alpha;
+        k.beta = fminf(fmaxf(r.beta, 0.0f), 1.0f);
+        k.theta = r.theta;
         coef[c] = k;
         if (mean_out) mean_out[c] = st.mean;
         if (blockIdx.x == 0) {
@@ -286,8 +119,8 @@ __device__ void lif_prologue(const snnflow_neuron& n, const double* sums, int C,
             }
             if (n.bn_train && n.running_mean) {
                 const double unb = N > 1.0 ? st.dvar * N / (N - 1.0) : st.dvar;
-                n.running_mean[c] = (float)(n.momentum * st.dmean + (1.0 - n.momentum) * (double)rm);
-                n.running_var[c] = (float)(n.momentum * unb + (1.0 - n.momentum) * (double)rv);
+                n.running_mean[c] = (float)(n.momentum * st.dmean + (1.0 - n.momentum) * (double)r.rm);
+                n.running_var[c] = (float)(n.momentum * unb + (1.0 - n.momentum) * (double)r.rv);
             }
         }
     }
@@ -297,41 +130,47 @@ __device__ void lif_prologue(const snnflow_neuron& n, const double* sums, int C,
 // Layer-l gradients of (gamma, bn bias, beta, threshold) [and pred] from the LIF-backward
 // sums: gamma = dotp*invstd, bias = sum g, theta = -sum g, beta = sum g*m' (0 <= beta <= 1)
 // (torch batch_norm_cpu_backward; snntorch Leaky; clamp backward passes on [0,1]).
-__device__ void neuron_grads(const snnflow_neuron& n, const float* stats, const double* sums, int C,
-                             const snnflow_neuron_grad& ng, int accumulate, int has_pred, float* g_pred_w,
-                             float* g_pred_b) {
-    if (blockIdx.x != 0) return;
-    // every load before any store: the destinations may alias as far as the compiler
-    // knows, and block 0's serial load->store chains would set the kernel's length
+// Block 0's inputs of neuron_grads other than the sums, loaded at kernel start (every
+// load before any store: the destinations may alias as far as the compiler knows, and
+// block 0's serial load->store chains would set the kernel's length).
+struct NeuronGradRegs { float inv, be, o0, o1, o2, o3, op; };
+
+__device__ inline NeuronGradRegs load_neuron_grad(const snnflow_neuron& n, const float* stats, int C,
+                                                  const snnflow_neuron_grad& ng, int accumulate, int has_pred,
+                                                  float* g_pred_w, float* g_pred_b) {
+    NeuronGradRegs r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (blockIdx.x != 0) return r;
     const int c = threadIdx.x;
-    const bool ch = c < C;
-    const int cc = ch ? c : 0;
-    const double gsum = sums[cc], dotp = sums[C + cc], gbm = sums[2 * C + cc];
-    const float inv = stats[C + cc], be = n.beta[cc];
-    float o0 = 0.f, o1 = 0.f, o2 = 0.f, o3 = 0.f;
-    if (accumulate && ch) {
-        o0 = ng.bn_weight[c]; o1 = ng.bn_bias[c]; o2 = ng.threshold[c]; o3 = ng.beta[c];
+    if (c < C) {
+        r.inv = stats[C + c];
+        r.be = n.beta[c];
+        if (accumulate) {
+            r.o0 = ng.bn_weight[c]; r.o1 = ng.bn_bias[c]; r.o2 = ng.threshold[c]; r.o3 = ng.beta[c];
+        }
     }
-    const int j = threadIdx.x;
-    const bool pj = has_pred && j < 2 * C + 2;
-    float gp = 0.f, op = 0.f;
-    float* pdst = nullptr;
-    if (pj) {
-        gp = (float)sums[3 * C + j];
-        pdst = (j < 2 * C) ? g_pred_w + j : g_pred_b + (j - 2 * C);
-        if (accumulate) op = *pdst;
-    }
-    if (ch) {
-        const float gw = (float)(dotp * (double)inv);
+    if (has_pred && accumulate && c < 2 * C + 2) r.op = (c < 2 * C) ? g_pred_w[c] : g_pred_b[c - 2 * C];
+    return r;
+}
+
+__device__ void neuron_grads(const NeuronGradRegs& r, const double* sums, int C, const snnflow_neuron_grad& ng,
+                             int has_pred, float* g_pred_w, float* g_pred_b) {
+    if (blockIdx.x != 0) return;
+    const int c = threadIdx.x;
+    if (c < C) {
+        const double gsum = sums[c], dotp = sums[C + c], gbm = sums[2 * C + c];
+        const float gw = (float)(dotp * (double)r.inv);
         const float gb = (float)gsum;
         const float gth = -(float)gsum;
-        const float gbe = (be >= 0.0f && be <= 1.0f) ? (float)gbm : 0.0f;
-        ng.bn_weight[c] = o0 + gw;
-        ng.bn_bias[c] = o1 + gb;
-        ng.threshold[c] = o2 + gth;
-        ng.beta[c] = o3 + gbe;
+        const float gbe = (r.be >= 0.0f && r.be <= 1.0f) ? (float)gbm : 0.0f;
+        ng.bn_weight[c] = r.o0 + gw;
+        ng.bn_bias[c] = r.o1 + gb;
+        ng.threshold[c] = r.o2 + gth;
+        ng.beta[c] = r.o3 + gbe;
     }
-    if (pj) *pdst = op + gp;
+    if (has_pred && c < 2 * C + 2) {
+        float* dst = (c < 2 * C) ? g_pred_w + c : g_pred_b + (c - 2 * C);
+        *dst = r.op + (float)sums[3 * C + c];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -381,23 +220,6 @@ __device__ inline Lif4 lif_step4(const float4& y, const float4& m, const LifCoef
     return r;
 }
 
-__device__ inline void zero4(float4* r, int n) {
-    for (int i = 0; i < n; ++i) r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-}
-
-// Register-prefetch budget: halo tiles of up to 16 channels are held in registers
-// (<= 6 float4 per thread each); wider layers stage straight into LDS.
-template <int CH, int NTH = NT>
-struct Prefetch { static constexpr bool on = (CH % 4 == 0) && Halo4<CH, NTH>::R <= 6; };
-
-// Conv-layer kernels run SPLIT threads per output pixel (SPLIT groups of NT threads, whole
-// waves): group `part` owns output channels [part*C/SPLIT, ...) in the forward and input
-// channels [part*CIN/SPLIT, ...) in the backward.  SPLIT = 2 doubles the waves per SIMD
-// (the launch has only 2 blocks per CU at cfg2) so one wave's loads and barriers overlap
-// another's arithmetic.  The group index is wave-uniform (readfirstlane): weight
-// addresses stay scalar.
-__device__ inline int thread_part() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x / NT); }
-
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
 __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a) {
     constexpr int NTB = NT * SPLIT, CO = C / SPLIT;
@@ -426,10 +248,11 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         halo_load<CIN, NTB>(a.prev_y, tl, H, W, ry);
         if (a.prev_mem) halo_load<CIN, NTB>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
+        const NeuronRegs nr = load_neuron(a.prev, CIN);
         zero_consumed(a.zero0, a.zero1, a.zero_n);
         __shared__ double sums[2 * CIN];
         if (a.prev.bn_train) acc_gather<2 * CIN>(a.prev_acc, 2 * CIN, sums);
-        lif_prologue(a.prev, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
+        lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
         __syncthreads();
         // 2. LIF of the previous layer over the halo; interior pixels also write its state
         const bool zr = a.prev.zero_reset != 0;
@@ -530,10 +353,11 @@ __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
         yv[q] = y4[pc * Q + q];
         mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
     }
+    const NeuronRegs nr = load_neuron(a.n, C);
     zero_consumed(a.zero0, a.zero1, a.zero_n);
     __shared__ double sums[2 * C];
     if (a.n.bn_train) acc_gather<2 * C>(a.acc, 2 * C, sums);
-    lif_prologue(a.n, sums, C, (double)npix, a.stats, coef, nullptr);
+    lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr);
     __syncthreads();
     if (!act) return;
     const bool zr = a.n.zero_reset != 0;
@@ -721,18 +545,36 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
         }
     }
 
+    // per-channel parameters (their round trip overlaps the halo loads)
+    float st_mean = 0.f, st_inv = 0.f, gamma = 0.f;
+    if (tid < C) {
+        st_mean = a.stats[tid];
+        st_inv = a.stats[C + tid];
+        gamma = a.n.bn_weight[tid];
+    }
+    const NeuronGradRegs ngr =
+        load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b);
+    LifCoef pk = {0.f, 0.f, 0.f, 0.f};
+    float pmu = 0.f;
+    if constexpr (LIF_IN) {
+        if (tid < CIN) {
+            pk = lif_coef(a.prev, a.prev_stats, CIN, tid);
+            pmu = a.prev_stats[tid];
+        }
+    }
+
     // 2. per-channel constants; block 0 finishes layer l's neuron gradients and stores the
     //    BN backward coefficients for the deferred weight gradient
     zero_consumed(a.zero0, a.zero1, a.zero_n);
     __shared__ double sums[SNNFLOW_BWD_ACC(C)];
     acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
-    neuron_grads(a.n, a.stats, sums, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b);
+    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b);
     if (tid < C) {
-        const float mean = a.stats[tid], inv = a.stats[C + tid];
+        const float mean = st_mean, inv = st_inv;
         BnBwdLds c;
         c.mean = mean;
         c.inv = inv;
-        c.w = a.n.bn_weight[tid];
+        c.w = gamma;
         if (a.n.bn_train) {
             // torch batch_norm_cpu_backward: k = dotp*invstd*invstd/n, grad_mean = sum/n
             c.k = (float)sums[C + tid] * inv * inv / nf;
@@ -749,8 +591,8 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     }
     if constexpr (LIF_IN) {
         if (tid < CIN) {
-            pcoef[tid] = lif_coef(a.prev, a.prev_stats, CIN, tid);
-            pmean[tid] = a.prev_stats[tid];
+            pcoef[tid] = pk;
+            pmean[tid] = pmu;
         }
     }
     __syncthreads();
@@ -993,12 +835,14 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
         const int t = e / C, c = e - t * C;
         const float* st = ap->steps[t].stats;
         const float* bc = ap->steps[t].bnc;
-        BnBwdLds k;
-        k.mean = st[c];
-        k.inv = st[C + c];
-        k.gm = bc[c];
-        k.k = bc[C + c];
-        k.w = ap->bn_weight[c];
+        BnBwdLds k = {0.f, 1.f, 0.f, 0.f, 1.f};  // no BatchNorm: G = g_cur
+        if (st) {
+            k.mean = st[c];
+            k.inv = st[C + c];
+            k.gm = bc[c];
+            k.k = bc[C + c];
+            k.w = ap->bn_weight[c];
+        }
         coef[t][c] = k;
     }
 
@@ -1284,11 +1128,12 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
 
 int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
     if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || a->nsteps <= 0 || a->nsteps > SNNFLOW_MAX_WGRAD_STEPS ||
-        !a->bn_weight || !a->slab_ff || (a->rec && !a->slab_rec))
+        !a->slab_ff || (a->rec && !a->slab_rec))
         SNN_FAIL(SNNFLOW_E_ARG, "wgrad: bad args");
     for (int t = 0; t < a->nsteps; ++t) {
         const snnflow_wgrad_step& st = a->steps[t];
-        if (!st.g_cur || !st.y || !st.x || !st.stats || !st.bnc) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: incomplete step");
+        if (!st.g_cur || !st.y || !st.x || (st.stats && !st.bnc)) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: incomplete step");
+        if (st.stats && !a->bn_weight) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: BatchNorm step needs bn_weight");
     }
     const hipStream_t s = (hipStream_t)stream;
     const dim3 grid(snnflow_conv_blocks(a->B, a->H, a->W));
@@ -1307,6 +1152,7 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
         } else if (cin == CC_) WG_LAUNCH(CC_, CC_, false);                                                 \
         else if (cin == 1) WG_LAUNCH(1, CC_, false);                                                       \
         else if (cin == 2) WG_LAUNCH(2, CC_, false);                                                       \
+        else if (cin == 3) WG_LAUNCH(3, CC_, false);                                                       \
         else if (cin == 4) WG_LAUNCH(4, CC_, false);                                                       \
         else if (cin == 5) WG_LAUNCH(5, CC_, false);                                                       \
         else SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: unsupported cin");                                       \

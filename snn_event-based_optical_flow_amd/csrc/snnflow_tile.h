@@ -1,0 +1,217 @@
+// Shared tile machinery of the conv-layer kernels (LIFFireNet cells, ConvLIF cells):
+// halo staging, 3x3 conv / transposed conv of one pixel from LDS, block reductions into
+// sharded fp64 accumulators.  Device code only; included by the .hip translation units.
+#pragma once
+
+#include "snnflow_dev.h"
+
+namespace snnflow {
+
+// ---------------------------------------------------------------------------
+// LDS staging of a halo tile
+// ---------------------------------------------------------------------------
+
+// Strided input (e.g. event_cnt NCHW, or an NHWC spike tensor) -> tile[p][ci]
+template <int CIN, int NTH = NT>
+__device__ void stage_strided(const float* __restrict__ x, int64_t sb, int64_t sc, int64_t sh, int64_t sw,
+                              const Tile& tl, int H, int W, float* tile) {
+    constexpr int P = Pad<CIN>::v;
+    const int tid = threadIdx.x;
+    const float* xb = x + (int64_t)tl.b * sb;
+    if (sc == 1) {
+        for (int e = tid; e < HN * CIN; e += NTH) {
+            const int p = e / CIN, ci = e - p * CIN;
+            const int r = p / HWD, cc = p - r * HWD;
+            const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+            tile[p * P + ci] = in_image(h, w, H, W) ? xb[h * sh + w * sw + ci] : 0.0f;
+        }
+    } else {
+        for (int e = tid; e < HN * CIN; e += NTH) {
+            const int ci = e / HN, p = e - ci * HN;
+            const int r = p / HWD, cc = p - r * HWD;
+            const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+            tile[p * P + ci] = in_image(h, w, H, W) ? xb[ci * sc + h * sh + w * sw] : 0.0f;
+        }
+    }
+}
+
+// Contiguous NHWC [B][H][W][C] (C % 4 == 0) -> tile
+template <int C, int NTH = NT>
+__device__ void stage_nhwc(const float* __restrict__ x, const Tile& tl, int H, int W, float* tile) {
+    static_assert(C % 4 == 0, "vector staging");
+    constexpr int P = Pad<C>::v, Q = C / 4;
+    const int tid = threadIdx.x;
+    for (int e = tid; e < HN * Q; e += NTH) {
+        const int p = e / Q, q = e - p * Q;
+        const int r = p / HWD, cc = p - r * HWD;
+        const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (in_image(h, w, H, W))
+            v = *reinterpret_cast<const float4*>(x + (((int64_t)tl.b * H + h) * W + w) * C + 4 * q);
+        *reinterpret_cast<float4*>(tile + p * P + 4 * q) = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 3x3 convolution of one output pixel (outputs [co0, co0+CO)) from an LDS halo tile.
+// wt: [3][3][CIN][C]; co0 must be wave-uniform (scalar weight loads).
+// acc += sum_{ky,kx,ci} w * x.
+// ---------------------------------------------------------------------------
+template <int CIN, int C, int CO = C>
+__device__ inline void conv_acc(const float* tile, const float* __restrict__ wt, int ty, int tx, int co0,
+                                float (&acc)[CO]) {
+    constexpr int P = Pad<CIN>::v, VW = VecW<CIN>::v;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const float* xp = tile + ((ty + ky) * HWD + (tx + kx)) * P;
+            const cfloat_ptr wk = as_const(wt) + (ky * 3 + kx) * CIN * C + co0;
+            constexpr int UR = CIN <= 8 ? CIN : 1;
+#pragma unroll UR
+            for (int ci = 0; ci < CIN; ci += VW) {
+                float xs[VW];
+                if constexpr (VW == 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(xp + ci);
+                    xs[0] = v.x; xs[1] = v.y; xs[2] = v.z; xs[3] = v.w;
+                } else if constexpr (VW == 2) {
+                    const float2 v = *reinterpret_cast<const float2*>(xp + ci);
+                    xs[0] = v.x; xs[1] = v.y;
+                } else {
+                    xs[0] = xp[ci];
+                }
+#pragma unroll
+                for (int j = 0; j < VW; ++j) {
+#pragma unroll
+                    for (int co = 0; co < CO; ++co) acc[co] = fmaf(wk[(ci + j) * C + co], xs[j], acc[co]);
+                }
+            }
+        }
+    }
+}
+
+// Transposed 3x3 (input gradient, inputs [ci0, ci0+CI)) of one pixel from an LDS tile of
+// output gradients.  wd: [3][3][C][CIN]; ci0 wave-uniform.
+// gx[ci] += sum_{ky,kx,co} w[co][ci][ky][kx] * g[h+1-ky][w+1-kx][co]
+template <int C, int CIN, int CI = CIN>
+__device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ wd, int ty, int tx, int ci0,
+                                 float (&gx)[CI]) {
+    constexpr int P = Pad<C>::v;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+            const float* gp = gtile + ((ty + 2 - ky) * HWD + (tx + 2 - kx)) * P;
+            const cfloat_ptr wk = as_const(wd) + (ky * 3 + kx) * C * CIN + ci0;
+            constexpr int UR = C <= 8 ? C : 1;
+#pragma unroll UR
+            for (int co = 0; co < C; co += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(gp + co);
+                const float gs[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+#pragma unroll
+                    for (int ci = 0; ci < CI; ++ci) gx[ci] = fmaf(wk[(co + j) * CIN + ci], gs[j], gx[ci]);
+                }
+            }
+        }
+    }
+}
+
+// Opaque use of a register array: stops LLVM from sinking its computation into a
+// following conditional block (where the scalar-weight schedule no longer fits).
+template <int N>
+__device__ inline void pin(float (&v)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+// Block-level sums of per-thread floats, then one fp64 atomic add per sum.  The block's
+// threads form PARTS groups of NT consecutive threads (whole waves); each group sums
+// its own NV values and dst(part, j) is the accumulator address of sum j of group part.
+template <int NV, int PARTS, typename Dst>
+__device__ void block_atomic_sum_parts(const float (&v)[NV], Dst dst) {
+    constexpr int WPP = NT / 64, NW = WPP * PARTS;
+    __shared__ float red[NW][NV];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const float s = wave_total(v[j]);
+        if (lane == 0) red[wv][j] = s;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < PARTS * NV; t += NT * PARTS) {
+        const int part = t / NV, j = t - part * NV;
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < WPP; ++w) s += (double)red[part * WPP + w][j];
+        atomicAdd(dst(part, j), s);
+    }
+}
+
+template <int NV>
+__device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
+    block_atomic_sum_parts<NV, 1>(v, [acc](int, int j) { return acc + j; });
+}
+
+// Accumulators already consumed by an earlier kernel of the chain are zeroed here
+// (grid-stride over all threads of the launch).
+__device__ inline void zero_consumed(double* z0, double* z1, int n) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        if (z0) z0[j] = 0.0;
+        if (z1) z1[j] = 0.0;
+    }
+}
+
+// Totals of the M sums of a sharded accumulator (n sums per replica, M <= n, M <= NT)
+// into LDS out[M]: TPJ = NT/M threads per sum each add a strided subset of the
+// replicas (all their loads in flight at once), then one LDS pass.  One global round
+// trip; called by every thread of the block (contains barriers).
+template <int M>
+__device__ void acc_gather(const double* acc, int n, double* out) {
+    static_assert(M >= 1 && M <= NT, "acc_gather: M sums");
+    constexpr int TPJ = NT / M;
+    constexpr int PER = (kAccShards + TPJ - 1) / TPJ;
+    __shared__ double red[TPJ * M];
+    const int tid = threadIdx.x, st = acc_stride(n);
+    if (tid < TPJ * M) {
+        const int j = tid % M, g = tid / M;
+        double v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int sh = g + k * TPJ;
+            v[k] = sh < kAccShards ? acc[sh * st + j] : 0.0;
+        }
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) sum += v[k];
+        red[g * M + j] = sum;
+    }
+    __syncthreads();
+    if (tid < M) {
+        double sum = 0.0;
+        for (int g = 0; g < TPJ; ++g) sum += red[g * M + tid];
+        out[tid] = sum;
+    }
+    __syncthreads();
+}
+
+__device__ inline void zero4(float4* r, int n) {
+    for (int i = 0; i < n; ++i) r[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// Register-prefetch budget: halo tiles of up to 16 channels are held in registers
+// (<= 6 float4 per thread each); wider layers stage straight into LDS.
+template <int CH, int NTH = NT>
+struct Prefetch { static constexpr bool on = (CH % 4 == 0) && Halo4<CH, NTH>::R <= 6; };
+
+// Conv-layer kernels run SPLIT threads per output pixel (SPLIT groups of NT threads, whole
+// waves): group `part` owns output channels [part*C/SPLIT, ...) in the forward and input
+// channels [part*CIN/SPLIT, ...) in the backward.  SPLIT = 2 doubles the waves per SIMD
+// (the launch has only 2 blocks per CU at cfg2) so one wave's loads and barriers overlap
+// another's arithmetic.  The group index is wave-uniform (readfirstlane): weight
+// addresses stay scalar.
+__device__ inline int thread_part() { return __builtin_amdgcn_readfirstlane((int)threadIdx.x / NT); }
+
+
+}  // namespace snnflow

@@ -6,8 +6,9 @@ Drop-in for the reference's ``models.model`` (LIFFireNet family), its spiking ce
 """
 from . import _lib  # noqa: F401  (loads libsnnflow.so or raises)
 from .cells import ConvLayer, Leaky, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
+from .convlif import ConvLIF, ConvLIFRecurrent
 from .loss import EventWarping
 from .model import LIFFireFlowNet, LIFFireFlowNet_short, LIFFireNet, LIFFireNet_short
 
 __all__ = ["LIFFireNet", "LIFFireNet_short", "LIFFireFlowNet", "LIFFireFlowNet_short", "SNNtorch_ConvLIF",
-           "SNNtorch_ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping"]
+           "SNNtorch_ConvLIFRecurrent", "ConvLIF", "ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping"]

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class Neuron(ctypes.Structure):
@@ -82,6 +82,27 @@ class WgradArgs(ctypes.Structure):
                 ("steps", WgradStep * MAX_WGRAD_STEPS)]
 
 
+class ConvLifParams(ctypes.Structure):
+    _fields_ = [("leak", P), ("thresh", P), ("act_width", F32), ("hard_reset", I32)]
+
+
+class ConvLifFwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
+                ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
+                ("prev_state", P), ("wt_ff", P), ("wt_rec", P), ("p", ConvLifParams),
+                ("residual", P), ("rs_b", I64), ("rs_c", I64), ("rs_h", I64), ("rs_w", I64),
+                ("out", P), ("state", P), ("current", P)]
+
+
+class ConvLifBwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
+                ("g_out", P), ("gs_b", I64), ("gs_c", I64), ("gs_h", I64), ("gs_w", I64),
+                ("g_state", P), ("state", P), ("prev_state", P), ("current", P),
+                ("wt_bwd_ff", P), ("wt_bwd_rec", P), ("p", ConvLifParams),
+                ("g_x", P), ("gxs_b", I64), ("gxs_c", I64), ("gxs_h", I64), ("gxs_w", I64),
+                ("g_prev", P), ("g_current", P), ("acc", P)]
+
+
 ACC_SHARDS = 32  # SNNFLOW_ACC_SHARDS
 
 
@@ -126,6 +147,9 @@ EXPORTS = {
     "snnflow_lif_bwd": (I32, [ctypes.POINTER(LifBwdArgs), P]),
     "snnflow_layer_bwd": (I32, [ctypes.POINTER(LayerBwdArgs), P]),
     "snnflow_wgrad": (I32, [ctypes.POINTER(WgradArgs), P]),
+    "snnflow_convlif_fwd": (I32, [ctypes.POINTER(ConvLifFwdArgs), P]),
+    "snnflow_convlif_bwd": (I32, [ctypes.POINTER(ConvLifBwdArgs), P]),
+    "snnflow_convlif_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
     "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P]),

@@ -101,16 +101,22 @@ class PreppedWeights:
     (reference: ``threshold.data.clamp_(min=0.01)`` at every cell forward,
     SNNtorch_spiking_submodules.py:284 / :516).
 
-    Refreshed by one batched launch at every forward call: parameter version counters
-    cannot key a cache (fused optimizers and ``.data`` writes update weights without
-    bumping them), and a hipGraph replay must re-read the weights anyway.  The
-    backward pass reuses the buffers of the last forward (same weights)."""
+    Refreshed by one batched launch at the first forward after a completed backward
+    pass (the optimizer step sits between them) and whenever a parameter's version
+    counter moved (load_state_dict, in-place edits through autograd-visible ops).  Version
+    counters alone cannot key the cache: fused optimizers update weights without bumping
+    them.  The backward pass reuses the buffers of the last forward (same weights)."""
 
     def __init__(self):
         self.fwd = {}
         self.bwd = {}
+        self.key = None
 
     def ensure(self, weights, thresholds, stream, refresh=True):
+        key = tuple((w.data_ptr(), w._version) for w in weights) + tuple((t.data_ptr(), t._version) for t in thresholds)
+        if key != self.key:
+            refresh = True
+        self.key = key
         fresh = False
         for i, w in enumerate(weights):
             f = self.fwd.get(i)
@@ -155,6 +161,7 @@ class FireNetEngine:
         self.flat = None
         self.flat_views = None
         self.pending = []   # per-step tensors of the open backward chain (deferred wgrad)
+        self.prep_stale = True  # re-prepare weights at the next forward (set after each backward)
 
     # parameter order = Function input order after the states
     def param_list(self):
@@ -278,7 +285,8 @@ class FireNetStep(torch.autograd.Function):
         _lib.require_device(x, "event tensor")
         s = _lib.stream_ptr(dev)
         ws = eng.workspace(B, H, W, dev)
-        wfwd, _ = eng.prep_weights(s)
+        wfwd, _ = eng.prep_weights(s, refresh=eng.prep_stale)
+        eng.prep_stale = False
         cells = eng.cells
 
         ys = torch.empty(L, B, H, W, C, device=dev)
@@ -464,6 +472,7 @@ class FireNetStep(torch.autograd.Function):
             ws.reset_acc()
             eng.bwd_open = False
             eng.pending = []
+            eng.prep_stale = True
             raise
 
         grads = [None] * len(eng.flat_layout)
@@ -474,6 +483,7 @@ class FireNetStep(torch.autograd.Function):
             eng.flat_views = None
             eng.bwd_open = False
             eng.last_flat = eng.flat
+            eng.prep_stale = True
         return (None, gx, *g_prev, *grads)
 
 

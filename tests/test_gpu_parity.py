@@ -360,3 +360,84 @@ def test_training_steps_fused_adam_vs_oracle(dev):
         model.detach_states()
         ew.reset()
         rew.reset()
+
+
+# ---------------------------------------------------------------------------
+# U-Net neuron flavour: ConvLIF / ConvLIFRecurrent (models/spiking_submodules.py)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("tag", ["ff", "rec"])
+def test_convlif_vs_golden(golden, dev, tag):
+    """Reference-generated fixture: 3 steps, loss = sum z*linspace + 0.3*sum v each step
+    (tests/golden/make_golden.py:spiking_cells_case); spikes, last membrane and every
+    parameter gradient (BPTT through the membrane)."""
+    import snnflow
+
+    g = golden("spiking_cells_case.npz")
+    cls = snnflow.ConvLIF if tag == "ff" else snnflow.ConvLIFRecurrent
+    cell = cls(3, 4, 3, leak=(0.0, 1.0), thresh=(0.8, 0.1)).to(dev)
+    cell.load_state_dict({k[len(tag) + 3:]: torch.from_numpy(v).to(dev) for k, v in g.items()
+                          if k.startswith(f"{tag}.p.")})
+    state, loss = None, 0
+    for t in range(3):
+        x = torch.from_numpy(g[f"{tag}.x_{t}"]).to(dev)
+        z, state = cell(x, state)
+        np.testing.assert_array_equal(z.detach().cpu().numpy(), g[f"{tag}.z_{t}"])
+        lin = torch.linspace(-1, 1, z.numel(), device=dev).view_as(z)
+        loss = loss + (z * lin).sum() + 0.3 * state[0].sum()
+    np.testing.assert_allclose(state[0].detach().cpu().numpy(), g[f"{tag}.v_last"], rtol=1e-5, atol=1e-6)
+    loss.backward()
+    for n, p in cell.named_parameters():
+        ref = g[f"{tag}.g.{n}"]
+        assert _rel(p.grad.cpu().numpy(), ref) < 1e-4, (n, _rel(p.grad.cpu().numpy(), ref))
+
+
+@pytest.mark.parametrize("recurrent", [False, True])
+@pytest.mark.parametrize("C,cin,hard", [(8, 8, True), (8, 2, False), (16, 16, True), (32, 32, False)])
+def test_convlif_vs_oracle_random(dev, recurrent, C, cin, hard):
+    """Random cells and inputs, 3 steps with a residual on the ff cell: outputs, states and
+    gradients of inputs, initial state and parameters against the oracle (steps run
+    teacher-forced on OUR spikes/state so a near-threshold flip cannot cascade)."""
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(21 + C)
+    B, H, W, T = 2, 20, 37, 3
+    if recurrent:
+        cell = snnflow.ConvLIFRecurrent(cin, C, 3, leak=(0.0, 1.0), thresh=(0.5, 0.2), hard_reset=hard).to(dev)
+    else:
+        cell = snnflow.ConvLIF(cin, C, 3, leak=(0.0, 1.0), thresh=(0.5, 0.2), hard_reset=hard).to(dev)
+    ref = lif_ref.SpikingCellRef(cin, C, 3, recurrent=recurrent, hard_reset=hard)
+    ref.load_state_dict({k: v.cpu() for k, v in cell.state_dict().items()})
+    gen = torch.Generator().manual_seed(5)
+    s0 = torch.randn(2, B, C, H, W, generator=gen) * 0.5
+    s0[1] = (s0[1] > 0).float()
+    state_d = s0.to(dev).requires_grad_(True)
+    state_c = s0.clone().requires_grad_(True)
+    for t in range(T):
+        x = (torch.rand(B, cin, H, W, generator=gen) < 0.5).float()
+        xd, xc = x.to(dev).requires_grad_(True), x.clone().requires_grad_(True)
+        res = torch.randn(B, C, H, W, generator=gen) if not recurrent else None
+        if recurrent:
+            zd, sd = cell(xd, state_d)
+            zc, sc = ref(xc, state_c)
+        else:
+            zd, sd = cell(xd, state_d, res.to(dev))
+            zc, sc = ref(xc, state_c, res)
+        v = sc[0].detach()
+        th = ref.thresh.detach().clamp_min(0.01)
+        assert _spike_mismatch_ok(sd[1].detach().cpu(), sc[1].detach(), v, th), t
+        np.testing.assert_allclose(sd[0].detach().cpu().numpy(), sc[0].detach().numpy(), rtol=1e-5, atol=1e-5)
+        wz = torch.randn(B, C, H, W, generator=gen)
+        wv = torch.randn(B, C, H, W, generator=gen)
+        ((zd * wz.to(dev)).sum() + (sd[0] * wv.to(dev)).sum()).backward()
+        ((zc * wz).sum() + (sc[0] * wv).sum()).backward()
+        if (sd[1].detach().cpu() == sc[1].detach()).all():
+            assert _rel(xd.grad.cpu().numpy(), xc.grad.numpy()) < 1e-4, t
+            assert _rel(state_d.grad.cpu().numpy(), state_c.grad.numpy()) < 1e-4, t
+            for (n, p), (_, q) in zip(cell.named_parameters(), ref.named_parameters()):
+                assert _rel(p.grad.cpu().numpy(), q.grad.numpy()) < 1e-4, (t, n)
+        cell.zero_grad()
+        ref.zero_grad()
+        # next step from OUR state (teacher forcing), fresh leaves
+        state_d = sd.detach().clone().requires_grad_(True)
+        state_c = sd.detach().cpu().clone().requires_grad_(True)
