@@ -1144,17 +1144,19 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
         constexpr int SP_ = (CC_ == 8 || CC_ == 16) ? 2 : 1;                                               \
         hipLaunchKernelGGL((k_wgrad<CI_, CC_, REC_, SP_>), grid, dim3(NT * SP_), 0, s, *a);               \
     } while (0)
+#define WG_PICK(CI_, CC_)                                                                                  \
+    do {                                                                                                   \
+        if (a->rec) WG_LAUNCH(CI_, CC_, true);                                                             \
+        else WG_LAUNCH(CI_, CC_, false);                                                                   \
+    } while (0)
 #define WG_CASE(CC_)                                                                                       \
     case CC_:                                                                                              \
-        if (a->rec) {                                                                                      \
-            if (cin != CC_) SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: recurrent layer requires cin == c");      \
-            WG_LAUNCH(CC_, CC_, true);                                                                     \
-        } else if (cin == CC_) WG_LAUNCH(CC_, CC_, false);                                                 \
-        else if (cin == 1) WG_LAUNCH(1, CC_, false);                                                       \
-        else if (cin == 2) WG_LAUNCH(2, CC_, false);                                                       \
-        else if (cin == 3) WG_LAUNCH(3, CC_, false);                                                       \
-        else if (cin == 4) WG_LAUNCH(4, CC_, false);                                                       \
-        else if (cin == 5) WG_LAUNCH(5, CC_, false);                                                       \
+        if (cin == CC_) WG_PICK(CC_, CC_);                                                                 \
+        else if (cin == 1) WG_PICK(1, CC_);                                                                \
+        else if (cin == 2) WG_PICK(2, CC_);                                                                \
+        else if (cin == 3) WG_PICK(3, CC_);                                                                \
+        else if (cin == 4) WG_PICK(4, CC_);                                                                \
+        else if (cin == 5) WG_PICK(5, CC_);                                                                \
         else SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: unsupported cin");                                       \
         break;
     switch (c) {
@@ -1162,6 +1164,7 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
         default: break;
     }
 #undef WG_CASE
+#undef WG_PICK
 #undef WG_LAUNCH
     SNN_CHECK_LAUNCH();
     return 0;
