@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 7
+#define SNNFLOW_ABI_VERSION 8
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -261,6 +261,26 @@ int snnflow_convlif_bwd(const snnflow_convlif_bwd_args* a, void* stream);
  * g_leak = sum * s * (1 - s), s = sigmoid(leak) (written, or added when accumulate). */
 int snnflow_convlif_param_grads(const double* acc, const float* leak, const float* thresh, int c, int accumulate,
                                 float* g_leak, float* g_thresh, void* stream);
+
+/* ---- on-device event encodings (dataloader/encodings.py:30-85, dataloader/base.py) ----
+ * Event e of sample b has fields ts/ys/xs/ps at base + b*batch_stride + e*ev_stride
+ * (ev_stride 4 for an event list [B][N][4] (ts, y, x, p), 1 for separate arrays).
+ * Pixel = (long)y * W + (long)x (truncation, as .long()); events outside the sensor are
+ * skipped (the reference's index_put_ would raise).  Outputs (any may be NULL) are fully
+ * written:
+ *   cnt      [B][2][H][W]   events_to_channels: += p*p into channel 0 (p >= 0) / 1 (p <= 0)
+ *   voxel    [B][bins][H][W] events_to_voxel: t = ts*(bins-1) [rounded half-even], += p*max(0, 1-|t-k|)
+ *   image    [B][H][W]      events_to_image(ps, accumulate) (accumulate=0: last write wins)
+ *   mask     [B][1][H][W]   events_to_image(|p|, accumulate=False)  (create_mask_encoding)
+ *   pol_mask [B][N][2]      create_polarity_mask: (p<0 ? 0 : p, -(p>0 ? 0 : p)) */
+typedef struct snnflow_encode_args {
+    int B, N, H, W;
+    const float* ts; const float* ys; const float* xs; const float* ps;
+    int64_t ev_stride, batch_stride;
+    int num_bins, round_ts, accumulate;
+    float* cnt; float* voxel; float* image; float* mask; float* pol_mask;
+} snnflow_encode_args;
+int snnflow_encode_events(const snnflow_encode_args* a, void* stream);
 
 /* Sums per-block weight-gradient slabs: out[i][e] = sum_b slab[i][b][e]. */
 typedef struct snnflow_slab_desc { const float* slab; float* out; int elems; } snnflow_slab_desc;

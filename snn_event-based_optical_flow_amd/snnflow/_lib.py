@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class Neuron(ctypes.Structure):
@@ -103,6 +103,12 @@ class ConvLifBwdArgs(ctypes.Structure):
                 ("g_prev", P), ("g_current", P), ("acc", P)]
 
 
+class EncodeArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("N", I32), ("H", I32), ("W", I32), ("ts", P), ("ys", P), ("xs", P), ("ps", P),
+                ("ev_stride", I64), ("batch_stride", I64), ("num_bins", I32), ("round_ts", I32),
+                ("accumulate", I32), ("cnt", P), ("voxel", P), ("image", P), ("mask", P), ("pol_mask", P)]
+
+
 ACC_SHARDS = 32  # SNNFLOW_ACC_SHARDS
 
 
@@ -148,6 +154,7 @@ EXPORTS = {
     "snnflow_layer_bwd": (I32, [ctypes.POINTER(LayerBwdArgs), P]),
     "snnflow_wgrad": (I32, [ctypes.POINTER(WgradArgs), P]),
     "snnflow_convlif_fwd": (I32, [ctypes.POINTER(ConvLifFwdArgs), P]),
+    "snnflow_encode_events": (I32, [ctypes.POINTER(EncodeArgs), P]),
     "snnflow_convlif_bwd": (I32, [ctypes.POINTER(ConvLifBwdArgs), P]),
     "snnflow_convlif_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),

@@ -232,10 +232,53 @@ def convlayer_case(ref_sub, out):
                         gw=layer.conv2d.weight.grad.numpy(), gb=layer.conv2d.bias.grad.numpy())
 
 
+def encodings_case(ref_enc, ref_base, out):
+    """dataloader/encodings.py events_to_image / events_to_voxel / events_to_channels and
+    dataloader/base.py create_mask_encoding / create_polarity_mask on a window with
+    repeated pixels, both polarities and ts at bin edges."""
+    gen = torch.Generator().manual_seed(31)
+    H, W, N = 13, 17, 600
+    xs = torch.randint(0, W, (N,), generator=gen).float()
+    ys = torch.randint(0, H, (N,), generator=gen).float()
+    ts = torch.sort(torch.rand(N, generator=gen)).values
+    ts[:5] = torch.tensor([0.0, 0.25, 0.5, 0.75, 1.0])
+    ps = (torch.rand(N, generator=gen) < 0.5).float() * 2 - 1
+    rec = {"xs": xs.numpy(), "ys": ys.numpy(), "ts": ts.numpy(), "ps": ps.numpy(), "res": np.array([H, W])}
+    rec["cnt"] = ref_enc.events_to_channels(xs, ys, ps, sensor_size=(H, W)).numpy()
+    rec["image_acc"] = ref_enc.events_to_image(xs, ys, ps, sensor_size=(H, W)).numpy()
+    for nb in (2, 5):
+        for rnd in (False, True):
+            rec[f"voxel_{nb}_{int(rnd)}"] = ref_enc.events_to_voxel(xs, ys, ts, ps, nb, sensor_size=(H, W),
+                                                                    round_ts=rnd).numpy()
+    loader = ref_base.BaseDataLoader.__new__(ref_base.BaseDataLoader)
+    loader.resolution = (H, W)
+    rec["mask"] = ref_base.BaseDataLoader.create_mask_encoding(loader, xs, ys, ps).numpy()
+    rec["pol_mask"] = ref_base.BaseDataLoader.create_polarity_mask(ps).numpy()
+    np.savez_compressed(os.path.join(out, "encodings_case.npz"), **rec)
+
+
+def import_dataloader(ref_root):
+    """dataloader/__init__.py imports h5py (absent): register the package without running
+    it, then import the two pure-torch modules."""
+    pkg = types.ModuleType("dataloader")
+    pkg.__path__ = [os.path.join(ref_root, "dataloader")]
+    sys.modules["dataloader"] = pkg
+    import dataloader.base as ref_base
+    import dataloader.encodings as ref_enc
+    return ref_enc, ref_base
+
+
 def main():
-    ref_root = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    args = [a for a in sys.argv[1:] if not a.startswith("--only=")]
+    only = [a[len("--only="):] for a in sys.argv[1:] if a.startswith("--only=")]
+    ref_root = args[0] if args else "/root/reference"
     install_stubs()
     sys.path.insert(0, ref_root)
+    if only == ["encodings"]:
+        ref_enc, ref_base = import_dataloader(ref_root)
+        encodings_case(ref_enc, ref_base, HERE)
+        print("encodings fixture written")
+        return
     import loss.flow as ref_flow
     import models.model as ref_model
     import models.spiking_submodules as ref_sub_sp
@@ -251,6 +294,8 @@ def main():
     convlayer_case(ref_sub, out)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 4)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet_short", 4)
+    ref_enc, ref_base = import_dataloader(ref_root)
+    encodings_case(ref_enc, ref_base, out)
     print("golden fixtures written to", out)
 
 

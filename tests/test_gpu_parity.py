@@ -441,3 +441,51 @@ def test_convlif_vs_oracle_random(dev, recurrent, C, cin, hard):
         # next step from OUR state (teacher forcing), fresh leaves
         state_d = sd.detach().clone().requires_grad_(True)
         state_c = sd.detach().cpu().clone().requires_grad_(True)
+
+
+# ---------------------------------------------------------------------------
+# On-device event encodings (dataloader/encodings.py, dataloader/base.py)
+# ---------------------------------------------------------------------------
+def test_encodings_vs_golden(golden, dev):
+    """Counts, masks and polarity masks bit-exact; voxel grids exact with rounded
+    timestamps (0/1 weights) and within fp32 summation-order error otherwise."""
+    from snnflow import encodings as E
+
+    g = golden("encodings_case.npz")
+    xs, ys, ts, ps = (torch.from_numpy(g[k]).to(dev) for k in ("xs", "ys", "ts", "ps"))
+    res = tuple(int(v) for v in g["res"])
+    np.testing.assert_array_equal(E.events_to_channels(xs, ys, ps, res).cpu().numpy(), g["cnt"])
+    np.testing.assert_array_equal(E.events_to_image(xs, ys, ps, res).cpu().numpy(), g["image_acc"])
+    for nb in (2, 5):
+        for rnd in (0, 1):
+            v = E.events_to_voxel(xs, ys, ts, ps, nb, res, bool(rnd)).cpu().numpy()
+            if rnd:
+                np.testing.assert_array_equal(v, g[f"voxel_{nb}_{rnd}"])
+            else:
+                np.testing.assert_allclose(v, g[f"voxel_{nb}_{rnd}"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_array_equal(E.create_mask_encoding(xs, ys, ps, res).cpu().numpy(), g["mask"])
+    np.testing.assert_array_equal(E.create_polarity_mask(ps).cpu().numpy(), g["pol_mask"])
+
+
+def test_encode_batch_vs_oracle(dev):
+    """One launch for a whole batch (B=4, 128x128, 3000 events each, duplicates) against the
+    per-sample oracle; and the synthetic loader's own counts."""
+    from oracle import encodings_ref as E
+    from snnflow import encodings
+    from snnflow.synthetic import make_window
+
+    gen = torch.Generator(device=dev).manual_seed(7)
+    w = make_window(4, 3000, 128, 128, gen, dev)
+    out = encodings.encode_batch(w["event_list"], (128, 128), num_bins=5, round_ts=False)
+    ev = w["event_list"].cpu()
+    for b in range(4):
+        ts, ys, xs, ps = ev[b, :, 0], ev[b, :, 1], ev[b, :, 2], ev[b, :, 3]
+        np.testing.assert_array_equal(out["event_cnt"][b].cpu().numpy(),
+                                      E.events_to_channels(xs, ys, ps, (128, 128)).numpy())
+        np.testing.assert_allclose(out["event_voxel"][b].cpu().numpy(),
+                                   E.events_to_voxel(xs, ys, ts, ps, 5, (128, 128)).numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(out["event_mask"][b].cpu().numpy(),
+                                      E.create_mask_encoding(xs, ys, ps, (128, 128)).numpy())
+        np.testing.assert_array_equal(out["event_list_pol_mask"][b].cpu().numpy(),
+                                      E.create_polarity_mask(ps).t().numpy())
+    np.testing.assert_array_equal(out["event_cnt"].cpu().numpy(), w["event_cnt"].cpu().numpy())
