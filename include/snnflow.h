@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 8
+#define SNNFLOW_ABI_VERSION 9
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -320,6 +320,31 @@ int snnflow_iwe_corners(const float* events, const float* flow_ev, int B, int M,
 /* utils/iwe.py:74-93 interpolate: img[b][idx] += w * pol (img zeroed by the call). */
 int snnflow_iwe_interpolate(const int32_t* idx, const float* w, const float* pol, int64_t pol_sb,
                             int B, int K, int H, int W, float* img, void* stream);
+
+/* ---- evaluation path (eval_flow.py:220-282, utils/iwe.py:96-150, loss/flow.py:597-649) ----
+ * deblur_events / compute_pol_iwe: per event gather the flow at its pixel ((long)(y*W + x)),
+ * warp to tref, round half-even (round_idx) or take the 4 bilinear corners, purge
+ * out-of-sensor locations, and scatter weight * mask into nimg images of out
+ * [B][nimg][H][W] (fully written).  Mask of image k: pol[e*pol_stride + k], or 1 when pol
+ * is NULL (nimg = 1 only). */
+int snnflow_pol_iwe(const float* events, const float* flow, const float* pol, int64_t pol_stride, int nimg, int B,
+                    int N, int H, int W, float tref, float flow_scaling, int round_idx, float* out, void* stream);
+
+/* AEE: flow' = (flow * flow_scaling) * dt_ratio[b]; error = |flow' - gt|_2 per pixel;
+ * valid = event_mask && gt != (0,0); AEE[b] = sum(error*valid) / (sum(valid) + 1e-9);
+ * outliers = (error*valid > 3) && (error*valid > 0.05*|flow'|*valid), counted over the
+ * whole batch; percent[b] = outliers / (sum(valid)[b] + 1e-9) (loss/flow.py:609-649). */
+typedef struct snnflow_aee_args {
+    int B, H, W;
+    const float* flow;          /* [B][2][H][W] network flow (before scaling) */
+    const float* gtflow;        /* [B][2][H][W] */
+    const float* event_mask;    /* [B][H][W] event mask of the last window */
+    const float* dt_ratio;      /* [B] dt_gt / dt_input */
+    float flow_scaling;
+    double* acc;                /* scratch [2B + 1], zeroed by the call */
+    float* aee; float* percent; /* out [B] */
+} snnflow_aee_args;
+int snnflow_aee(const snnflow_aee_args* a, void* stream);
 
 /* HIP twin of the export op SNN_implementation::LIF (ONNX_LIF_operator/src/lif_op.cpp:8-56):
  * m' = beta[c]*mem + x; spk = m' >= thr[c]; mem_out = spk ? 0 : m'  (NCHW). */

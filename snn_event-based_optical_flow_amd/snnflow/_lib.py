@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class Neuron(ctypes.Structure):
@@ -109,6 +109,11 @@ class EncodeArgs(ctypes.Structure):
                 ("accumulate", I32), ("cnt", P), ("voxel", P), ("image", P), ("mask", P), ("pol_mask", P)]
 
 
+class AeeArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("flow", P), ("gtflow", P), ("event_mask", P),
+                ("dt_ratio", P), ("flow_scaling", F32), ("acc", P), ("aee", P), ("percent", P)]
+
+
 ACC_SHARDS = 32  # SNNFLOW_ACC_SHARDS
 
 
@@ -155,6 +160,8 @@ EXPORTS = {
     "snnflow_wgrad": (I32, [ctypes.POINTER(WgradArgs), P]),
     "snnflow_convlif_fwd": (I32, [ctypes.POINTER(ConvLifFwdArgs), P]),
     "snnflow_encode_events": (I32, [ctypes.POINTER(EncodeArgs), P]),
+    "snnflow_pol_iwe": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
+    "snnflow_aee": (I32, [ctypes.POINTER(AeeArgs), P]),
     "snnflow_convlif_bwd": (I32, [ctypes.POINTER(ConvLifBwdArgs), P]),
     "snnflow_convlif_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),

@@ -51,3 +51,37 @@ def interpolate(idx, weights, res, polarity_mask=None):
     check(lib.snnflow_iwe_interpolate(ptr(ii), ptr(ww), ptr(pol), pol_sb, B, K, H, W, ptr(img),
                                       _lib.stream_ptr(ww.device)), "iwe_interpolate")
     return img
+
+
+def _pol_iwe(flow, event_list, res, masks, flow_scaling, round_idx, tref=1.0):
+    _lib.require_device(event_list, "event_list")
+    ev = event_list.float().contiguous()
+    fl = flow.float().contiguous()
+    B, N = ev.shape[0], ev.shape[1]
+    H, W = int(res[0]), int(res[1])
+    if fl.shape[2] * fl.shape[3] != H * W:
+        raise ValueError("flow map and resolution disagree")
+    pol, stride, nimg = None, 0, 1
+    if masks is not None:
+        pol = torch.cat([m.reshape(B, N, 1).float() for m in masks], dim=2).contiguous()
+        stride, nimg = pol.shape[2], pol.shape[2]
+    out = torch.empty(B, nimg, H, W, device=ev.device)
+    check(lib.snnflow_pol_iwe(ptr(ev), ptr(fl), ptr(pol), stride, nimg, B, N, H, W, float(tref), float(flow_scaling),
+                              int(bool(round_idx)), ptr(out), _lib.stream_ptr(ev.device)), "pol_iwe")
+    return out
+
+
+def deblur_events(flow, event_list, res, flow_scaling=128, round_idx=True, polarity_mask=None):
+    """``utils/iwe.py:96-131``: image of the events warped to t=1 by the flow map [B,1,H,W]."""
+    return _pol_iwe(flow, event_list, res, None if polarity_mask is None else [polarity_mask], flow_scaling,
+                    round_idx)
+
+
+def compute_pol_iwe(flow, event_list, res, pos_mask, neg_mask, flow_scaling=128, round_idx=True):
+    """``utils/iwe.py:134-150``: per-polarity images of warped events [B,2,H,W] (one launch)."""
+    return _pol_iwe(flow, event_list, res, [pos_mask, neg_mask], flow_scaling, round_idx)
+
+
+def upsample_flow(flow, target_height, target_width):
+    """``utils/iwe.py:153-171``: nearest-neighbour upsampling of a flow map."""
+    return torch.nn.functional.interpolate(flow, size=(target_height, target_width), mode="nearest")

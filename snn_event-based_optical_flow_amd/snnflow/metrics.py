@@ -1,0 +1,111 @@
+"""Validation metrics with the reference's API (``loss/flow.py:306-649``: BaseValidationLoss,
+AEE), the evaluation counterpart of the training loss.
+
+``AEE.forward`` runs the HIP kernels of csrc/eval.hip (per-pixel endpoint error,
+validity, outliers, per-sample reduction).  The association bookkeeping is the
+reference's (last flow map, event masks, ground truth, time scaling).  Error heatmap
+accumulation for visualisation (``accumulate_error_heatmap`` and friends) is not part of
+this path; ``get_error_map`` returns None.
+
+Difference, documented: the reference multiplies the flow by ``dt_gt / dt_input`` with
+plain broadcasting, which is only per-sample for a batch of one; here the ratio is applied
+per sample for any batch size (identical for B = 1 and for scalar dt).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import lib, ptr
+from .iwe import compute_pol_iwe
+
+
+class BaseValidationLoss(torch.nn.Module):
+    """``loss/flow.py:306-475`` bookkeeping."""
+
+    def __init__(self, config, device, flow_scaling=128):
+        super().__init__()
+        self.res = config["loader"]["resolution"]
+        self.flow_scaling = flow_scaling
+        self.overwrite_intermediate = config["loss"].get("overwrite_intermediate", False)
+        self.device = device
+        self.reset()
+
+    def reset(self):
+        self._passes = 0
+        self._event_list = None
+        self._pol_mask_list = None
+        self._flow_map = None
+        self._event_mask = None
+        self._gtflow = None
+
+    @property
+    def num_events(self):
+        return 0 if self._event_list is None else self._event_list.shape[1]
+
+    def event_flow_association(self, flow_list, inputs):
+        event_list = inputs["event_list"].to(self.device)
+        pol_mask = inputs["event_list_pol_mask"].to(self.device)
+        event_mask = inputs["event_mask"].to(self.device)
+        gtflow = inputs["gtflow"].to(self.device) if "gtflow" in inputs else None
+        flow = flow_list[-1]
+        if self._event_list is None:
+            self._event_list = event_list
+            self._pol_mask_list = pol_mask
+            self._event_mask = event_mask
+            self._flow_map = []
+        else:
+            event_list = event_list.clone()
+            event_list[:, :, 0:1] += self._passes
+            self._event_list = torch.cat([self._event_list, event_list], dim=1)
+            self._pol_mask_list = torch.cat([self._pol_mask_list, pol_mask], dim=1)
+            self._event_mask = torch.cat([self._event_mask, event_mask], dim=1)
+        self._flow_map.append(flow.reshape(flow.shape[0], 2, self.res[0], self.res[1]))
+        self._gtflow = gtflow
+        self._dt_input = inputs["dt_input"]
+        self._dt_gt = inputs["dt_gt"]
+        self._passes += 1
+
+    def overwrite_intermediate_flow(self, flow_list):
+        flow = flow_list[-1]
+        self._flow_map = [flow.reshape(flow.shape[0], 2, self.res[0], self.res[1])]
+        m = torch.sum(self._event_mask, dim=1, keepdim=True)
+        m[m > 1] = 1
+        self._event_mask = m
+
+    def get_error_map(self):
+        return None
+
+    def compute_window_iwe(self, round_idx=True):
+        """Per-polarity image of all window events warped with their window's flow (``:476-487``);
+        uses the last flow map for every event (the reference's per-event flow list)."""
+        pol = self._pol_mask_list
+        return compute_pol_iwe(self._flow_map[-1], self._event_list, self.res, pol[:, :, 0:1], pol[:, :, 1:2],
+                               flow_scaling=self.flow_scaling, round_idx=round_idx)
+
+
+class AEE(BaseValidationLoss):
+    """``loss/flow.py:597-649``: average endpoint error and outlier percentage per sample."""
+
+    @property
+    def num_events(self):
+        return float("inf")
+
+    def forward(self):
+        flow = self._flow_map[-1].float().contiguous()
+        B, _, H, W = flow.shape
+        gt = self._gtflow.float().contiguous()
+        mask = self._event_mask[:, -1, :, :].float().contiguous()
+        ratio = torch.as_tensor(self._dt_gt, dtype=torch.float32, device=flow.device) / torch.as_tensor(
+            self._dt_input, dtype=torch.float32, device=flow.device)
+        ratio = ratio.reshape(-1).expand(B).contiguous() if ratio.numel() == 1 else ratio.reshape(B).contiguous()
+        acc = torch.empty(2 * B + 1, dtype=torch.float64, device=flow.device)
+        aee = torch.empty(B, device=flow.device)
+        pct = torch.empty(B, device=flow.device)
+        a = _lib.AeeArgs()
+        a.B, a.H, a.W = B, H, W
+        a.flow, a.gtflow, a.event_mask, a.dt_ratio = ptr(flow), ptr(gt), ptr(mask), ptr(ratio)
+        a.flow_scaling = float(self.flow_scaling)
+        a.acc, a.aee, a.percent = ptr(acc), ptr(aee), ptr(pct)
+        _lib.call("aee", lib.snnflow_aee, ctypes.byref(a), _lib.stream_ptr(flow.device))
+        return aee, pct

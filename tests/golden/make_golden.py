@@ -257,6 +257,40 @@ def encodings_case(ref_enc, ref_base, out):
     np.savez_compressed(os.path.join(out, "encodings_case.npz"), **rec)
 
 
+def eval_case(ref_flow, ref_iwe, out):
+    """loss/flow.py AEE (B=1 with tensor dt, B=2 with scalar dt) and utils/iwe.py
+    compute_pol_iwe (rounded and bilinear) / deblur_events on synthetic windows."""
+    gen = torch.Generator().manual_seed(41)
+    H, W, N = 20, 24, 400
+    rec = {"res": np.array([H, W])}
+    for B in (1, 2):
+        flow = (torch.rand(B, 2, H, W, generator=gen) - 0.5) * 0.1
+        gt = (torch.rand(B, 2, H, W, generator=gen) - 0.5) * 12
+        gt[:, :, :3, :] = 0.0  # invalid ground truth rows
+        mask = (torch.rand(B, 1, H, W, generator=gen) < 0.6).float()
+        ys = torch.randint(0, H, (B, N), generator=gen).float()
+        xs = torch.randint(0, W, (B, N), generator=gen).float()
+        ts = torch.sort(torch.rand(B, N, generator=gen), dim=1).values
+        ps = (torch.rand(B, N, generator=gen) < 0.5).float() * 2 - 1
+        ev = torch.stack([ts, ys, xs, ps], dim=2)
+        pol = torch.stack([(ps > 0).float(), (ps < 0).float()], dim=2)
+        dt_in, dt_gt = (torch.tensor([0.5]), torch.tensor([1.25])) if B == 1 else (torch.tensor(0.5), torch.tensor(0.8))
+        cfg = {"loader": {"resolution": [H, W]}, "loss": {"overwrite_intermediate": False}}
+        aee = ref_flow.AEE(cfg, "cpu", flow_scaling=128)
+        aee.event_flow_association([flow], {"event_list": ev, "event_list_pol_mask": pol, "event_mask": mask,
+                                            "gtflow": gt, "dt_input": dt_in, "dt_gt": dt_gt})
+        v, pct = aee()
+        rec.update({f"b{B}_flow": flow.numpy(), f"b{B}_gt": gt.numpy(), f"b{B}_mask": mask.numpy(),
+                    f"b{B}_ev": ev.numpy(), f"b{B}_pol": pol.numpy(), f"b{B}_dt_in": dt_in.numpy(),
+                    f"b{B}_dt_gt": dt_gt.numpy(), f"b{B}_aee": v.numpy(), f"b{B}_pct": pct.numpy()})
+        for rnd in (True, False):
+            iwe = ref_iwe.compute_pol_iwe(flow, ev, [H, W], pol[:, :, 0:1], pol[:, :, 1:2], flow_scaling=128,
+                                          round_idx=rnd)
+            rec[f"b{B}_poliwe_{int(rnd)}"] = iwe.numpy()
+        rec[f"b{B}_deblur"] = ref_iwe.deblur_events(flow, ev, [H, W], flow_scaling=128, round_idx=True).numpy()
+    np.savez_compressed(os.path.join(out, "eval_case.npz"), **rec)
+
+
 def import_dataloader(ref_root):
     """dataloader/__init__.py imports h5py (absent): register the package without running
     it, then import the two pure-torch modules."""
@@ -279,6 +313,12 @@ def main():
         encodings_case(ref_enc, ref_base, HERE)
         print("encodings fixture written")
         return
+    if only == ["eval"]:
+        import loss.flow as ref_flow
+        import utils.iwe as ref_iwe
+        eval_case(ref_flow, ref_iwe, HERE)
+        print("eval fixture written")
+        return
     import loss.flow as ref_flow
     import models.model as ref_model
     import models.spiking_submodules as ref_sub_sp
@@ -296,6 +336,7 @@ def main():
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet_short", 4)
     ref_enc, ref_base = import_dataloader(ref_root)
     encodings_case(ref_enc, ref_base, out)
+    eval_case(ref_flow, ref_iwe, out)
     print("golden fixtures written to", out)
 
 

@@ -37,7 +37,7 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_conv_fwd_args": _lib.ConvFwdArgs, "snnflow_lif_fwd_args": _lib.LifFwdArgs,
         "snnflow_lif_bwd_args": _lib.LifBwdArgs, "snnflow_layer_bwd_args": _lib.LayerBwdArgs,
         "snnflow_slab_desc": _lib.SlabDesc, "snnflow_prep_desc": _lib.PrepDesc,
-        "snnflow_wgrad_step": _lib.WgradStep, "snnflow_encode_args": _lib.EncodeArgs, "snnflow_convlif_params": _lib.ConvLifParams,
+        "snnflow_wgrad_step": _lib.WgradStep, "snnflow_aee_args": _lib.AeeArgs, "snnflow_encode_args": _lib.EncodeArgs, "snnflow_convlif_params": _lib.ConvLifParams,
         "snnflow_convlif_fwd_args": _lib.ConvLifFwdArgs, "snnflow_convlif_bwd_args": _lib.ConvLifBwdArgs, "snnflow_wgrad_args": _lib.WgradArgs, "snnflow_iwe_loss_args": _lib.IweLossArgs,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]

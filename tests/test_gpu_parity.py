@@ -489,3 +489,36 @@ def test_encode_batch_vs_oracle(dev):
         np.testing.assert_array_equal(out["event_list_pol_mask"][b].cpu().numpy(),
                                       E.create_polarity_mask(ps).t().numpy())
     np.testing.assert_array_equal(out["event_cnt"].cpu().numpy(), w["event_cnt"].cpu().numpy())
+
+
+# ---------------------------------------------------------------------------
+# Evaluation path (utils/iwe.py deblur / compute_pol_iwe, loss/flow.py AEE)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("B", [1, 2])
+def test_eval_vs_golden(golden, dev, B):
+    """Rounded IWEs bit-exact (integer counts), bilinear IWEs within fp32 atomic-order error,
+    AEE and outlier percentage within 1e-5 relative (north_star: AEE within 1e-4)."""
+    import snnflow
+    from snnflow import iwe
+
+    g = golden("eval_case.npz")
+    H, W = (int(v) for v in g["res"])
+    t = {k: torch.from_numpy(g[f"b{B}_{k}"]).to(dev) for k in ("flow", "gt", "mask", "ev", "pol")}
+    for rnd in (1, 0):
+        out = iwe.compute_pol_iwe(t["flow"], t["ev"], [H, W], t["pol"][:, :, 0:1], t["pol"][:, :, 1:2],
+                                  flow_scaling=128, round_idx=bool(rnd)).cpu().numpy()
+        if rnd:
+            np.testing.assert_array_equal(out, g[f"b{B}_poliwe_{rnd}"])
+        else:
+            np.testing.assert_allclose(out, g[f"b{B}_poliwe_{rnd}"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(iwe.deblur_events(t["flow"], t["ev"], [H, W], flow_scaling=128).cpu().numpy(),
+                                  g[f"b{B}_deblur"])
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"overwrite_intermediate": False}}
+    m = snnflow.AEE(cfg, dev, flow_scaling=128)
+    m.event_flow_association([t["flow"]], {"event_list": t["ev"], "event_list_pol_mask": t["pol"],
+                                           "event_mask": t["mask"], "gtflow": t["gt"],
+                                           "dt_input": torch.from_numpy(g[f"b{B}_dt_in"]),
+                                           "dt_gt": torch.from_numpy(g[f"b{B}_dt_gt"])})
+    aee, pct = m()
+    np.testing.assert_allclose(aee.cpu().numpy(), g[f"b{B}_aee"], rtol=1e-5)
+    np.testing.assert_allclose(pct.cpu().numpy(), g[f"b{B}_pct"], rtol=1e-6)
