@@ -19,7 +19,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kernel_class(name):
-    m = re.search(r"k_(conv_fwd|layer_bwd)<(\d+), (\d+), (true|false), (true|false)>", name)
+    m = re.search(r"k_(conv_fwd|layer_bwd)<(\d+), (\d+), (true|false), (true|false)(, \d+)?>", name)
     if m:
         kind, cin, rec = m.group(1), int(m.group(2)), m.group(5) == "true"
         lif_in = m.group(4) == "true"
@@ -57,6 +57,20 @@ def find(root, counter):
     return None
 
 
+def all_counters(root):
+    """Per-kernel-class averages of every counter found under root (one dict per class)."""
+    out = collections.defaultdict(dict)
+    for path in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        names = set()
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                names.add(r["Counter_Name"])
+        for n in names:
+            for k, v in per_kernel(path, n).items():
+                out[k][n] = round(v, 1)
+    return out
+
+
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "gpurun_out", "pmc")
     key = sys.argv[2] if len(sys.argv) > 2 else "C8_R128_B8"
@@ -74,6 +88,11 @@ def main():
     with open(path, "w") as f:
         json.dump(d, f, indent=1, sort_keys=True)
     print(json.dumps(res, indent=1))
+    if len(sys.argv) > 3:  # full per-class counter summary for profiles/
+        with open(sys.argv[3], "w") as f:
+            json.dump({"note": "rocprofv3 --pmc per-dispatch averages per kernel class (tools/pmc.sh passes); "
+                               "FETCH_SIZE/WRITE_SIZE in KB as reported", "workload": key,
+                       "kernels": all_counters(root)}, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
