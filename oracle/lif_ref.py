@@ -291,3 +291,18 @@ def make_unet_kwargs(base_num_channels=8, num_bins=2, encoding="cnt", mask_outpu
         "spiking_neuron": {"leak": [0.0, 1.0], "thresh": [0.0, 0.8], "learn_leak": True,
                            "learn_thresh": True, "hard_reset": True},
     }
+
+
+# ---------------------------------------------------------------------------
+# Export op
+# ---------------------------------------------------------------------------
+def lif_export_ref(x, mem, beta, threshold):
+    """``SNN_implementation::LIF`` (``ONNX_LIF_operator/src/lif_op.cpp:8-55``), restated:
+    per element of NCHW, ``m' = beta[c]*mem + x`` (two roundings, :41), spike on
+    ``m' >= threshold[c]`` (:42, note ``>=`` and no beta clamp, unlike snntorch), reset
+    to exactly 0 else keep ``m'`` (:43-48).  Pinned against the op itself
+    (``oracle/_ref/lif_op.so``, fixture ``tests/golden/lif_export_case.npz``)."""
+    C = x.shape[1]
+    mp = beta.view(1, C, 1, 1) * mem + x
+    spk = (mp >= threshold.view(1, C, 1, 1)).to(x.dtype)
+    return spk, torch.where(spk > 0, torch.zeros_like(mp), mp)

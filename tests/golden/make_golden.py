@@ -291,6 +291,29 @@ def eval_case(ref_flow, ref_iwe, out):
     np.savez_compressed(os.path.join(out, "eval_case.npz"), **rec)
 
 
+def lif_export_case(out):
+    """SNN_implementation::LIF (ONNX_LIF_operator/src/lif_op.cpp:8-55), the reference's own
+    compiled CPU op built from its source by oracle/Makefile into oracle/_ref/lif_op.so.
+    Ties of m' == threshold are planted (the op spikes on >=)."""
+    so = os.path.join(REPO, "oracle", "_ref", "lif_op.so")
+    if not os.path.exists(so):
+        raise SystemExit("build oracle/_ref first: make -C oracle")
+    torch.ops.load_library(so)
+    gen = torch.Generator().manual_seed(11)
+    N, C, H, W = 3, 5, 7, 9
+    x = torch.randn(N, C, H, W, generator=gen)
+    mem = torch.randn(N, C, H, W, generator=gen)
+    beta = torch.rand(C, generator=gen) * 1.2 - 0.1  # no clamp in the op: include beta < 0, > 1
+    thr = torch.rand(C, generator=gen)
+    x[0, :, 0, 0] = thr - 0.5 * mem[0, :, 0, 0]
+    beta[:] = torch.where(torch.arange(C) == 0, torch.tensor(0.5), beta)
+    x[0, 0, 0, 0] = thr[0] - 0.5 * mem[0, 0, 0, 0]  # exact tie only where the products are exact
+    mem[1, 0, 0, 0], x[1, 0, 0, 0] = 0.0, thr[0]      # m' == thr exactly -> spike
+    spk, mo = torch.ops.SNN_implementation.LIF(x, mem, beta, thr)
+    np.savez_compressed(os.path.join(out, "lif_export_case.npz"), x=x.numpy(), mem=mem.numpy(), beta=beta.numpy(),
+                        threshold=thr.numpy(), spk=spk.numpy(), mem_out=mo.numpy())
+
+
 def import_dataloader(ref_root):
     """dataloader/__init__.py imports h5py (absent): register the package without running
     it, then import the two pure-torch modules."""
@@ -312,6 +335,10 @@ def main():
         ref_enc, ref_base = import_dataloader(ref_root)
         encodings_case(ref_enc, ref_base, HERE)
         print("encodings fixture written")
+        return
+    if only == ["lif_export"]:
+        lif_export_case(HERE)
+        print("lif_export fixture written")
         return
     if only == ["eval"]:
         import loss.flow as ref_flow
@@ -337,6 +364,7 @@ def main():
     ref_enc, ref_base = import_dataloader(ref_root)
     encodings_case(ref_enc, ref_base, out)
     eval_case(ref_flow, ref_iwe, out)
+    lif_export_case(out)
     print("golden fixtures written to", out)
 
 

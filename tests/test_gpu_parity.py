@@ -310,6 +310,38 @@ def test_lif_export_op(dev):
     assert spk[0, 0, 0, 0].item() == 1.0
 
 
+def test_lif_export_op_vs_reference_op(golden, dev):
+    """snnflow_lif_export bit-exact against the reference's own compiled CPU op
+    (ONNX_LIF_operator/src/lif_op.cpp via oracle/_ref/lif_op.so): its committed fixture,
+    and the .so itself on fresh random inputs when it was shipped with the tree."""
+    import os
+
+    from snnflow import _lib
+    from snnflow._lib import lib, ptr
+
+    def run(x, m, b, th):
+        N, C, H, W = x.shape
+        xd, md, bd, td = (t.contiguous().to(dev) for t in (x, m, b, th))
+        spk, mo = torch.empty_like(xd), torch.empty_like(xd)
+        _lib.check(lib.snnflow_lif_export(ptr(xd), ptr(md), ptr(bd), ptr(td), N, C, H * W, ptr(spk), ptr(mo),
+                                          _lib.stream_ptr(dev)), "lif_export")
+        return spk.cpu(), mo.cpu()
+
+    g = golden("lif_export_case.npz")
+    spk, mo = run(*(torch.from_numpy(g[k]) for k in ("x", "mem", "beta", "threshold")))
+    np.testing.assert_array_equal(spk.numpy(), g["spk"])
+    np.testing.assert_array_equal(mo.numpy(), g["mem_out"])
+    so = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "lif_op.so")
+    if os.path.exists(so):
+        torch.ops.load_library(so)
+        gen = torch.Generator().manual_seed(7)
+        x, m = torch.randn(4, 16, 33, 17, generator=gen), torch.randn(4, 16, 33, 17, generator=gen)
+        b, th = torch.rand(16, generator=gen), torch.rand(16, generator=gen)
+        rs, rm = torch.ops.SNN_implementation.LIF(x, m, b, th)
+        s2, m2 = run(x, m, b, th)
+        assert torch.equal(rs, s2) and torch.equal(rm, m2)
+
+
 def test_training_steps_fused_adam_vs_oracle(dev):
     """Three optimizer steps (T=2 windows each, truncated BPTT) with torch's fused Adam,
     which updates parameters without bumping their version counters: the engine must
