@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 9
+#define SNNFLOW_ABI_VERSION 10
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -104,6 +104,9 @@ typedef struct snnflow_conv_fwd_args {
     snnflow_neuron prev; float* prev_state;
     const float* wt_ff;         /* [3][3][cin][c]                      */
     const float* wt_rec;        /* [3][3][c][c] or NULL (feed-forward) */
+    /* the same weights in the backward layout ([3][3][c][cin], [3][3][c][c]): the matrix-core
+     * (MFMA) B operand of the cin == c kernels, required there (wt_rec_t iff wt_rec) */
+    const float* wt_ff_t; const float* wt_rec_t;
     const float* s_prev;        /* NHWC [B][H][W][c] previous-step spikes; NULL = zeros */
     float* y;                   /* out NHWC [B][H][W][c] pre-BN current           */
     double* acc;                /* += SNNFLOW_ACC_LEN(2c) (sum y, sum y^2); NULL = no batch sums (eval) */
@@ -171,6 +174,9 @@ typedef struct snnflow_layer_bwd_args {
     float* bnc_out;             /* [2][c] (grad_mean, k) of layer l's BN backward */
     const float* wt_bwd_ff;     /* [3][3][c][cin]  (NULL: no input gradient)        */
     const float* wt_bwd_rec;    /* [3][3][c][c] or NULL                             */
+    /* the same weights in the forward layout ([3][3][cin][c], [3][3][c][c]): MFMA B operand of
+     * the input-gradient convs of the cin == c kernels, required there with their wt_bwd_* */
+    const float* wt_fwd_ff; const float* wt_fwd_rec;
     int lif_in;
     float* g_x; int64_t gxs_b, gxs_c, gxs_h, gxs_w;   /* lif_in=0: input gradient (strided) or NULL */
     float* g_state_prev;        /* [2][B][H][W][c] grad of the previous state (rec) or NULL */

@@ -22,6 +22,25 @@
 #endif
 #define PROBE_OFF(bit) ((SNNFLOW_PROBE & (bit)) != 0)
 
+// Phase-timestamp builds only (tools/ktrace.py, `make trace`): thread 0 of every block
+// records the 100 MHz wall clock at phase boundaries of the C x C layer kernels.
+// 0 in every shipped build.
+#ifndef SNNFLOW_SP32
+#define SNNFLOW_SP32 2  // threads per pixel of the C = 32 conv-layer kernels
+#endif
+#ifndef SNNFLOW_TRACE
+#define SNNFLOW_TRACE 0
+#endif
+#if SNNFLOW_TRACE
+__device__ unsigned long long g_trace[4][4096][8];
+#define TRACE_AT(on, kind, k)                                                                  \
+    do {                                                                                      \
+        if ((on) && threadIdx.x == 0 && blockIdx.x < 4096) g_trace[kind][blockIdx.x][k] = wall_clock64(); \
+    } while (0)
+#else
+#define TRACE_AT(on, kind, k) do { } while (0)
+#endif
+
 using namespace snnflow;
 
 namespace {
@@ -206,6 +225,10 @@ __global__ void k_prep_weights(DescBatch<snnflow_prep_desc> batch) {
     }
 }
 
+// The C x C conv layers (C = 8, 16, 32) run their convolutions on the matrix cores.
+template <int CIN, int C>
+constexpr bool kMfma = CIN == C && C % 8 == 0;
+
 // LIF of one float4 of channels [4q, 4q+4) (coefficients from LDS).
 struct Lif4 { float4 s, mout; };
 
@@ -236,6 +259,9 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W);
     const bool has_rec = REC && a.s_prev != nullptr;
+    [[maybe_unused]] constexpr bool TR = LIF_IN && CIN == C;
+    [[maybe_unused]] constexpr int TK = REC ? 1 : 0;
+    TRACE_AT(TR, TK, 0);
 
     // 1. issue every global load of the tile before any use
     float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
@@ -254,6 +280,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         if (a.prev.bn_train) acc_gather<2 * CIN>(a.prev_acc, 2 * CIN, sums);
         lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
         __syncthreads();
+        TRACE_AT(TR, TK, 1);
         // 2. LIF of the previous layer over the halo; interior pixels also write its state
         const bool zr = a.prev.zero_reset != 0;
         const int64_t plane4 = (int64_t)a.B * H * W * Q;
@@ -286,31 +313,68 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         if (has_rec) halo_store<C, NTB>(rtile, rs);
     }
     __syncthreads();
+    TRACE_AT(TR, TK, 2);
 
     float y[CO];
-#pragma unroll
-    for (int co = 0; co < CO; ++co) y[co] = 0.0f;
-    if (!PROBE_OFF(16)) conv_acc<CIN, C, CO>(tile, a.wt_ff, ty, tx, co0, y);
-
-    if constexpr (REC) {
-        if (has_rec) {
-            const float* rt = tile;
-            if constexpr (PF_REC) {
-                rt = rtile;
-            } else {
-                __syncthreads();
-                stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
-                __syncthreads();
+    if constexpr (kMfma<CIN, C>) {
+        // matrix-core implicit GEMM over the whole tile (weights in the [tap][c][cin] layout);
+        // the sums come back through LDS, aliasing `tile`, in this thread's pixel/channel order
+        constexpr int NW = NTB / 64;
+        MfmaAcc<C, C, NW> af, ar;
+        af.zero();
+        if (!PROBE_OFF(16)) mfma_conv3x3<C, C, false, NW>(tile, a.wt_ff_t, af);
+        bool rec_on = false;
+        if constexpr (REC) {
+            if (has_rec) {
+                rec_on = true;
+                const float* rt = tile;
+                if constexpr (PF_REC) {
+                    rt = rtile;
+                } else {
+                    __syncthreads();
+                    stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    __syncthreads();
+                }
+                ar.zero();
+                if (!PROBE_OFF(16)) mfma_conv3x3<C, C, false, NW>(rt, a.wt_rec_t, ar);
             }
-            float r[CO];
+        }
+        __syncthreads();
+        if (rec_on) mfma_store<true>(af, ar, tile);  // ff + rec (:540)
+        else mfma_store<false>(af, ar, tile);
+        __syncthreads();
+        const float* yl = tile + pt * PC + co0;
 #pragma unroll
-            for (int co = 0; co < CO; ++co) r[co] = 0.0f;
-            if (!PROBE_OFF(16)) conv_acc<C, C, CO>(rt, a.wt_rec, ty, tx, co0, r);
+        for (int co = 0; co < CO; co += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(yl + co);
+            y[co] = v.x; y[co + 1] = v.y; y[co + 2] = v.z; y[co + 3] = v.w;
+        }
+    } else {
 #pragma unroll
-            for (int co = 0; co < CO; ++co) y[co] = y[co] + r[co];  // ff + rec (:540)
+        for (int co = 0; co < CO; ++co) y[co] = 0.0f;
+        if (!PROBE_OFF(16)) conv_acc<CIN, C, CO>(tile, a.wt_ff, ty, tx, co0, y);
+
+        if constexpr (REC) {
+            if (has_rec) {
+                const float* rt = tile;
+                if constexpr (PF_REC) {
+                    rt = rtile;
+                } else {
+                    __syncthreads();
+                    stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    __syncthreads();
+                }
+                float r[CO];
+#pragma unroll
+                for (int co = 0; co < CO; ++co) r[co] = 0.0f;
+                if (!PROBE_OFF(16)) conv_acc<C, C, CO>(rt, a.wt_rec, ty, tx, co0, r);
+#pragma unroll
+                for (int co = 0; co < CO; ++co) y[co] = y[co] + r[co];  // ff + rec (:540)
+            }
         }
     }
 
+    TRACE_AT(TR, TK, 3);
     const int h = tl.h0 + ty, w = tl.w0 + tx;
     const bool in = (h < H) && (w < W);
     if (in) {
@@ -333,6 +397,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
                 return acc + (j < CO ? pp * CO + j : C + pp * CO + (j - CO));
             });
     }
+    TRACE_AT(TR, TK, 4);
 }
 
 // LIF (+ 1x1 pred conv + tanh) over pixels: one thread per pixel, all C channels.
@@ -396,7 +461,6 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
     const bool act = p < npix;
     const int64_t pc = act ? p : npix - 1;
     const int64_t b = pc / HWp, hw = pc - b * HWp;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
     // loads first
     float4 yv[Q], mv[Q], gs[Q];
     const float4* y4 = reinterpret_cast<const float4*>(a.y);
@@ -520,6 +584,9 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     const bool in = (h < H) && (w < W);
     const int64_t pix = ((int64_t)tl.b * H + h) * W + w;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    [[maybe_unused]] constexpr bool TR = LIF_IN && CIN == C;
+    [[maybe_unused]] constexpr int TK = REC ? 3 : 2;
+    TRACE_AT(TR, TK, 0);
 
     // 1. every global load of the kernel, issued up front (register prefetch)
     float4 rg[PF ? Halo4<C, NTB>::R : 1], ry[PF ? Halo4<C, NTB>::R : 1];
@@ -596,6 +663,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
         }
     }
     __syncthreads();
+    TRACE_AT(TR, TK, 1);
 
     // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l)
     if constexpr (PF) {
@@ -623,31 +691,78 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
         }
     }
     __syncthreads();
+    TRACE_AT(TR, TK, 2);
 
     // 4. Stage B: input gradient (dgrad) of ff and rec convolutions (this group's channels)
     float gx[CI];
 #pragma unroll
     for (int ci = 0; ci < CI; ++ci) gx[ci] = 0.0f;
-    if (!PROBE_OFF(1) && a.wt_bwd_ff) dgrad_acc<C, CIN, CI>(G, a.wt_bwd_ff, ty, tx, ci0, gx);
-    if constexpr (REC) {
-        if (a.g_state_prev) {
-            float gr[CR];
+    if constexpr (kMfma<CIN, C>) {
+        // matrix-core transposed convs over the whole tile (weights in the [tap][cin][c]
+        // layout); results come back through LDS aliasing G, one conv at a time
+        constexpr int NW = NTB / 64;
+        const bool do_x = a.wt_bwd_ff != nullptr;
+        const bool do_r = REC && a.g_state_prev != nullptr;
+        MfmaAcc<C, CIN, NW> ax;
+        MfmaAcc<C, C, NW> arr;
+        if (do_x) {
+            ax.zero();
+            if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, a.wt_fwd_ff, ax);
+        }
+        if constexpr (REC) {
+            if (do_r) {
+                arr.zero();
+                if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, a.wt_fwd_rec, arr);
+            }
+        }
+        __syncthreads();
+        if (do_x) {
+            mfma_store<false>(ax, ax, G);
+            __syncthreads();
+            const float* gl = G + pt * Pad<CIN>::v + ci0;
 #pragma unroll
-            for (int c = 0; c < CR; ++c) gr[c] = 0.0f;
-            if (!PROBE_OFF(1)) dgrad_acc<C, C, CR>(G, a.wt_bwd_rec, ty, tx, cr0, gr);
-            pin(gr);  // keep the dgrad out of the `in` branch (sinking it there spills SGPRs)
-            if (in) {
-                const int64_t plane = (int64_t)a.B * H * W * C;
-                float* gsp = a.g_state_prev + pix * C + cr0;
+            for (int ci = 0; ci < CI; ++ci) gx[ci] = gl[ci];
+        }
+        if constexpr (REC) {
+            if (do_r) {
+                __syncthreads();
+                mfma_store<false>(arr, arr, G);
+                __syncthreads();
+                if (in) {
+                    const float* rl = G + pt * PC + cr0;
+                    const int64_t plane = (int64_t)a.B * H * W * C;
+                    float* gsp = a.g_state_prev + pix * C + cr0;
 #pragma unroll
-                for (int c = 0; c < CR; c += 4) {
-                    if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp + c) = z4;
-                    *reinterpret_cast<float4*>(gsp + plane + c) = make_float4(gr[c], gr[c + 1], gr[c + 2], gr[c + 3]);
+                    for (int c = 0; c < CR; c += 4) {
+                        if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp + c) = z4;
+                        *reinterpret_cast<float4*>(gsp + plane + c) = *reinterpret_cast<const float4*>(rl + c);
+                    }
+                }
+            }
+        }
+    } else {
+        if (!PROBE_OFF(1) && a.wt_bwd_ff) dgrad_acc<C, CIN, CI>(G, a.wt_bwd_ff, ty, tx, ci0, gx);
+        if constexpr (REC) {
+            if (a.g_state_prev) {
+                float gr[CR];
+#pragma unroll
+                for (int c = 0; c < CR; ++c) gr[c] = 0.0f;
+                if (!PROBE_OFF(1)) dgrad_acc<C, C, CR>(G, a.wt_bwd_rec, ty, tx, cr0, gr);
+                pin(gr);  // keep the dgrad out of the `in` branch (sinking it there spills SGPRs)
+                if (in) {
+                    const int64_t plane = (int64_t)a.B * H * W * C;
+                    float* gsp = a.g_state_prev + pix * C + cr0;
+#pragma unroll
+                    for (int c = 0; c < CR; c += 4) {
+                        if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp + c) = z4;
+                        *reinterpret_cast<float4*>(gsp + plane + c) = make_float4(gr[c], gr[c + 1], gr[c + 2], gr[c + 3]);
+                    }
                 }
             }
         }
     }
 
+    TRACE_AT(TR, TK, 3);
     // 5. Stage D: LIF backward of layer l-1 on the dgrad result, or the plain input gradient
     if constexpr (LIF_IN) {
         float vd[NVP];
@@ -679,12 +794,14 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
                 if (gm4) gm4[q] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
             }
         }
+        TRACE_AT(TR, TK, 4);
         double* acc = acc_shard(a.acc_out, SNNFLOW_BWD_ACC(CIN));
         if (!PROBE_OFF(4))
             block_atomic_sum_parts<NVP, SPLIT>(vd, [acc](int pp, int j) {
                 const int k = j / CI, jj = j - k * CI;
                 return acc + k * CIN + pp * CI + jj;
             });
+        TRACE_AT(TR, TK, 5);
     } else {
         if (a.g_x && a.wt_bwd_ff && in) {
             float* gb = a.g_x + (int64_t)tl.b * a.gxs_b + h * a.gxs_h + w * a.gxs_w;
@@ -969,7 +1086,7 @@ bool valid_c(int c) { return c == 4 || c == 8 || c == 16 || c == 32; }
 
 template <int C>
 int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
-    constexpr int SP = (C == 8 || C == 16) ? 2 : 1;  // threads per output pixel (C=32: registers)
+    constexpr int SP = (C == 8 || C == 16 || (C == 32 && SNNFLOW_SP32 == 2)) ? 2 : 1;  // threads per output pixel
     const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT * SP);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: lif_in requires cin == c");
@@ -992,7 +1109,7 @@ int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
 
 template <int C>
 int layer_bwd_c(const snnflow_layer_bwd_args& a, hipStream_t s) {
-    constexpr int SP = (C == 8 || C == 16) ? 2 : 1;  // threads per pixel (C x C layers; the head keeps 1)
+    constexpr int SP = (C == 8 || C == 16 || (C == 32 && SNNFLOW_SP32 == 2)) ? 2 : 1;  // threads per pixel (C x C layers; the head keeps 1)
     const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT * SP), block1(NT);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: lif_in requires cin == c");
@@ -1023,6 +1140,13 @@ int elem_grid(int64_t n) {
 extern "C" {
 
 int snnflow_abi_version(void) { return SNNFLOW_ABI_VERSION; }
+
+#if SNNFLOW_TRACE
+int snnflow_trace_copy(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_trace), bytes < sizeof(g_trace) ? bytes : sizeof(g_trace), 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif
 const char* snnflow_last_error(void) { return g_err.c_str(); }
 
 int snnflow_conv_blocks(int B, int H, int W) { return B * tiles_per_image(H, W); }
@@ -1056,6 +1180,8 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
     if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || !a->wt_ff || !a->y)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: bad args");
+    if (a->cin == a->c && a->c % 8 == 0 && (!a->wt_ff_t || (a->wt_rec && !a->wt_rec_t)))
+        SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: cin == c needs the backward-layout weights wt_ff_t / wt_rec_t");
     if (a->lif_in ? (!a->prev_y || !a->prev_state || (a->prev.bn_train && !a->prev_acc)) : !a->x)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: missing input");
     const hipStream_t s = (hipStream_t)stream;
@@ -1116,6 +1242,9 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
     if (a->has_pred && (!a->g_pred_w || !a->g_pred_b)) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: pred gradients");
     if (a->lif_in && (!a->wt_bwd_ff || !a->prev_y || !a->prev_stats || !a->prev_g_cur || !a->acc_out))
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: lif_in needs previous-layer buffers");
+    if (a->cin == a->c && a->c % 8 == 0 &&
+        ((a->wt_bwd_ff && !a->wt_fwd_ff) || (a->wt_bwd_rec && a->g_state_prev && !a->wt_fwd_rec)))
+        SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: cin == c needs the forward-layout weights wt_fwd_ff / wt_fwd_rec");
     const hipStream_t s = (hipStream_t)stream;
     switch (a->c) {
         case 4: return layer_bwd_c<4>(*a, s);

@@ -118,6 +118,138 @@ __device__ inline void dgrad_acc(const float* gtile, const float* __restrict__ w
     }
 }
 
+// ---------------------------------------------------------------------------
+// Implicit-GEMM 3x3 convolution of a block's NT output pixels on the matrix cores
+// (v_mfma_f32_16x16x4_f32: f32 operands, f32 accumulation, bit-for-bit a k-ordered fmaf
+// chain -- the same arithmetic as the vector path, in a different summation order).
+//
+//   out[p][n] = sum_{tap, k} src[halo(p, tap)][k] * wB[tap][n][k]
+//
+// M = pixels: 16 M-tiles of 16 consecutive pixels of one tile row (TW = 32), split over
+// the block's NW waves.  N = output channels in 16-wide tiles (NOUT = 8 pads with zero
+// weights).  K = 9 taps x KIN channels; in the MFMA of step j of a 16-channel block, lane
+// group g = lane >> 4 supplies channel 16 kb + E g + j for both operands (a permutation of
+// k, so each lane reads E consecutive channels with one LDS / global vector load).
+// src: LDS halo tile [HN][Pad<KIN>]; wB: global, [9][NOUT][KIN] (k fastest).
+// FLIP = false: halo(p, tap) = p + (ky, kx) (forward conv); true: p + (2 - ky, 2 - kx)
+// (input gradient of the conv: wB then holds the forward weights in [tap][cin][c] order).
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int KIN, int NOUT>
+struct MfmaGeo {
+    static_assert(KIN % 4 == 0 && (KIN < 16 || KIN % 16 == 0), "MFMA conv: KIN in {4, 8, 16, 32, ...}");
+    static constexpr int E = KIN >= 16 ? 4 : KIN / 4;    // channels per lane per 16-channel block
+    static constexpr int NKB = KIN >= 16 ? KIN / 16 : 1;  // 16-channel blocks of K per tap
+    static constexpr int NNT = (NOUT + 15) / 16;          // 16-wide output-channel tiles
+    static constexpr int BPT = NNT * NKB * E;             // B operand floats per lane per tap
+};
+
+template <int E>
+__device__ inline void ld_vec(const float* p, float* v) {
+    if constexpr (E == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else if constexpr (E == 2) {
+        const float2 t = *reinterpret_cast<const float2*>(p);
+        v[0] = t.x; v[1] = t.y;
+    } else {
+        v[0] = p[0];
+    }
+}
+
+// B fragments of one tap (zeros for padded output channels n >= NOUT).
+template <int KIN, int NOUT>
+__device__ inline void mfma_load_b(const float* __restrict__ wB, int tap, float (&b)[MfmaGeo<KIN, NOUT>::BPT]) {
+    using G = MfmaGeo<KIN, NOUT>;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int nt = 0; nt < G::NNT; ++nt) {
+        const int n = nt * 16 + m;
+        const bool ok = n < NOUT;
+        const float* p = wB + (int64_t)(tap * NOUT + (ok ? n : 0)) * KIN + g * G::E;
+#pragma unroll
+        for (int kb = 0; kb < G::NKB; ++kb) {
+            float v[G::E];
+            ld_vec<G::E>(p + kb * 16, v);
+#pragma unroll
+            for (int j = 0; j < G::E; ++j) b[(nt * G::NKB + kb) * G::E + j] = ok ? v[j] : 0.0f;
+        }
+    }
+}
+
+template <int KIN, int NOUT, int NW>
+struct MfmaAcc {
+    static constexpr int MT = 16 / NW;  // M-tiles per wave
+    f32x4 v[MT][MfmaGeo<KIN, NOUT>::NNT];
+    __device__ inline void zero() {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < MfmaGeo<KIN, NOUT>::NNT; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+};
+
+template <int KIN, int NOUT, bool FLIP, int NW>
+__device__ void mfma_conv3x3(const float* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW>& acc) {
+    using G = MfmaGeo<KIN, NOUT>;
+    static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
+    constexpr int P = Pad<KIN>::v, MT = 16 / NW;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    float bc[G::BPT], bn[G::BPT];
+    mfma_load_b<KIN, NOUT>(wB, 0, bc);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+        if (tap + 1 < 9) mfma_load_b<KIN, NOUT>(wB, tap + 1, bn);  // next tap's weights in flight
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+        const int oy = FLIP ? 2 - ky : ky, ox = FLIP ? 2 - kx : kx;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int T = wv * MT + mt, row = T >> 1, c0 = (T & 1) * 16;
+            const float* ap = src + ((row + oy) * HWD + c0 + m + ox) * P + g * G::E;
+#pragma unroll
+            for (int kb = 0; kb < G::NKB; ++kb) {
+                float a[G::E];
+                ld_vec<G::E>(ap + kb * 16, a);
+#pragma unroll
+                for (int j = 0; j < G::E; ++j)
+#pragma unroll
+                    for (int nt = 0; nt < G::NNT; ++nt)
+                        acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bc[(nt * G::NKB + kb) * G::E + j],
+                                                                             acc.v[mt][nt], 0, 0, 0);
+            }
+        }
+        if (tap + 1 < 9) {
+#pragma unroll
+            for (int i = 0; i < G::BPT; ++i) bc[i] = bn[i];
+        }
+    }
+}
+
+// Accumulators (C/D layout: lane holds pixels 4g..4g+3 of its M-tile, channel n = lane & 15)
+// [+ a second set added element-wise when SUM: ff + rec] -> LDS out[NT][Pad<NOUT>].
+template <bool SUM, int KIN, int NOUT, int NW, int KIN2>
+__device__ void mfma_store(const MfmaAcc<KIN, NOUT, NW>& acc, const MfmaAcc<KIN2, NOUT, NW>& acc2, float* out) {
+    constexpr int PO = Pad<NOUT>::v, MT = 16 / NW, NNT = MfmaGeo<KIN, NOUT>::NNT;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+        const int T = wv * MT + mt, row = T >> 1, c0 = (T & 1) * 16;
+#pragma unroll
+        for (int nt = 0; nt < NNT; ++nt) {
+            const int n = nt * 16 + m;
+            if (n < NOUT) {
+                f32x4 v = acc.v[mt][nt];
+                if constexpr (SUM) v = v + acc2.v[mt][nt];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) out[(row * TW + c0 + g * 4 + r) * PO + n] = v[r];
+            }
+        }
+    }
+}
+
 // Opaque use of a register array: stops LLVM from sinking its computation into a
 // following conditional block (where the scalar-weight schedule no longer fits).
 template <int N>

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class Neuron(ctypes.Structure):
@@ -36,7 +36,7 @@ class ConvFwdArgs(ctypes.Structure):
                 ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
                 ("prev_y", P), ("prev_mem", P), ("prev_acc", P), ("prev_stats", P),
                 ("prev", Neuron), ("prev_state", P),
-                ("wt_ff", P), ("wt_rec", P), ("s_prev", P),
+                ("wt_ff", P), ("wt_rec", P), ("wt_ff_t", P), ("wt_rec_t", P), ("s_prev", P),
                 ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32)]
 
 
@@ -60,7 +60,8 @@ class LayerBwdArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
                 ("y", P), ("stats", P), ("g_cur", P), ("acc_in", P), ("n", Neuron), ("ng", NeuronGrad),
                 ("has_pred", I32), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32),
-                ("bnc_out", P), ("wt_bwd_ff", P), ("wt_bwd_rec", P), ("lif_in", I32),
+                ("bnc_out", P), ("wt_bwd_ff", P), ("wt_bwd_rec", P),
+                ("wt_fwd_ff", P), ("wt_fwd_rec", P), ("lif_in", I32),
                 ("g_x", P), ("gxs_b", I64), ("gxs_c", I64), ("gxs_h", I64), ("gxs_w", I64),
                 ("g_state_prev", P), ("zero_mem_half", I32),
                 ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),

@@ -226,6 +226,7 @@ class CellFn(torch.autograd.Function):
         a.x = ptr(x)
         a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
         a.wt_ff, a.wt_rec, a.s_prev = ptr(wff[0]), _ptr_t(wrec[0]), _ptr_t(sp)
+        a.wt_ff_t, a.wt_rec_t = ptr(wff[1]), _ptr_t(wrec[1])
         a.y, a.acc = ptr(y), (ptr(facc) if n.bn_train else None)
         _lib.call("conv_fwd", lib.snnflow_conv_fwd, ctypes.byref(a), s)
         state = empty_state(B, C, H, W, dev)
@@ -239,6 +240,7 @@ class CellFn(torch.autograd.Function):
         ctx.has_mem, ctx.has_sp = mem is not None, sp is not None
         ctx.has_prev = prev_state is not None
         ctx.wbwd = (wff[1], wrec[1])
+        ctx.wfwd = (wff[0], wrec[0])
         ctx.save_for_backward(x, y, stats, *(t for t in (mem, sp) if t is not None))
         ctx.set_materialize_grads(False)
         return spk, state
@@ -290,10 +292,10 @@ class CellFn(torch.autograd.Function):
         gx = None
         if ctx.needs_input_grad[1]:
             gx = torch.empty_like(x)
-            a.wt_bwd_ff, a.g_x = ptr(ctx.wbwd[0]), ptr(gx)
+            a.wt_bwd_ff, a.wt_fwd_ff, a.g_x = ptr(ctx.wbwd[0]), ptr(ctx.wfwd[0]), ptr(gx)
             a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
         if cell.recurrent:
-            a.wt_bwd_rec = ptr(ctx.wbwd[1])
+            a.wt_bwd_rec, a.wt_fwd_rec = ptr(ctx.wbwd[1]), ptr(ctx.wfwd[1])
             if g_prev is not None:
                 a.g_state_prev, a.zero_mem_half = ptr(g_prev), 0
         _lib.call("layer_bwd", lib.snnflow_layer_bwd, ctypes.byref(a), s)

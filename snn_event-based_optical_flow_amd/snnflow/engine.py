@@ -285,7 +285,7 @@ class FireNetStep(torch.autograd.Function):
         _lib.require_device(x, "event tensor")
         s = _lib.stream_ptr(dev)
         ws = eng.workspace(B, H, W, dev)
-        wfwd, _ = eng.prep_weights(s, refresh=eng.prep_stale)
+        wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale)
         eng.prep_stale = False
         cells = eng.cells
 
@@ -325,6 +325,7 @@ class FireNetStep(torch.autograd.Function):
             a.x = ptr(x)
             a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
             a.wt_ff, a.wt_rec = ptr(wfwd[0][0]), ptr(wfwd[0][1])
+            a.wt_ff_t, a.wt_rec_t = ptr(wbwd[0][0]), ptr(wbwd[0][1])
             a.s_prev = _ptr_t(s_prev[0])
             a.y, a.acc = ptr(ys[0]), (ptr(facc[0]) if train[0] else None)
             a.zero0, a.zero_n = ptr(facc[L - 1]), zn
@@ -337,6 +338,7 @@ class FireNetStep(torch.autograd.Function):
                 a.prev_acc, a.prev_stats = ptr(facc[l - 1]), ptr(stats[l - 1])
                 a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
                 a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
+                a.wt_ff_t, a.wt_rec_t = ptr(wbwd[l][0]), ptr(wbwd[l][1])  # MFMA B operand layout
                 a.s_prev = _ptr_t(s_prev[l])
                 a.y, a.acc = ptr(ys[l]), (ptr(facc[l]) if train[l] else None)
                 if l >= 2:
@@ -390,7 +392,7 @@ class FireNetStep(torch.autograd.Function):
         dev = x.device
         s = _lib.stream_ptr(dev)
         ws = eng.workspace(B, H, W, dev)
-        _, wbwd = eng.prep_weights(s, refresh=False)
+        wfwd, wbwd = eng.prep_weights(s, refresh=False)
         if not eng.bwd_open:
             eng.open_chain(dev)
             acc = 0
@@ -446,13 +448,13 @@ class FireNetStep(torch.autograd.Function):
                 if l + 1 <= L - 1:
                     a.zero0, a.zero_n = ptr(bacc[l + 1]), zn
                 if eng.rec[l]:
-                    a.wt_bwd_rec = ptr(wbwd[l][1])
+                    a.wt_bwd_rec, a.wt_fwd_rec = ptr(wbwd[l][1]), ptr(wfwd[l][1])
                     if g_prev[l] is not None:
                         a.g_state_prev = ptr(g_prev[l])
                         a.zero_mem_half = 0 if ctx.ext[l] else 1
                 if l > 0:
                     a.cin, a.lif_in = C, 1
-                    a.wt_bwd_ff = ptr(wbwd[l][0])
+                    a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[l][0]), ptr(wfwd[l][0])
                     a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
                     a.prev_g_state = _ptr_t(gst[l - 1])
                     a.prev_g_cur, a.prev_g_mem = ptr(gcur[l - 1]), _ptr_t(gmem[l - 1])
@@ -461,7 +463,7 @@ class FireNetStep(torch.autograd.Function):
                     a.cin, a.lif_in = cin0, 0
                     if ctx.needs_input_grad[1]:
                         gx = torch.empty_like(x)
-                        a.wt_bwd_ff = ptr(wbwd[0][0])
+                        a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[0][0]), ptr(wfwd[0][0])
                         a.g_x = ptr(gx)
                         a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
                 _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)

@@ -137,7 +137,7 @@ def _spike_mismatch_ok(ours, ref, v, theta, tol=1e-4):
 
 
 @pytest.mark.parametrize("recurrent", [False, True])
-@pytest.mark.parametrize("C", [8, 32])
+@pytest.mark.parametrize("C", [8, 16, 32])
 def test_cell_teacher_forced(dev, recurrent, C):
     import snnflow
     from oracle import lif_ref
@@ -213,7 +213,7 @@ def test_liffirenet_short_vs_golden(golden, dev):
     _run_golden_firenet(golden("liffirenet_short_case.npz"), "LIFFireNet_short", dev)
 
 
-@pytest.mark.parametrize("C", [8, 32])
+@pytest.mark.parametrize("C", [8, 16, 32])
 def test_liffirenet_layerwise_teacher_forced_128(dev, C):
     """Every layer of the fused time step at the benchmark size (128x128, B=2, 3 steps),
     teacher-forced layer by layer: the oracle cell gets OUR previous layer's spikes and
