@@ -914,6 +914,79 @@ struct WAcc {
     }
 };
 
+// Matrix-core weight gradient of one block (C >= 16, CIN % 16 == 0): per tap,
+//   dW_tap[co][ci] += sum_p G[p][co] * X[halo(p, tap)][ci]
+// as v_mfma_f32_16x16x4_f32 with M = co (A = G^T from the interior tile), N = ci (B from the
+// halo tile), K = 4 tile pixels per MFMA (lane group g takes pixel 4s + g).  The 9 x (C/16) x
+// (CIN/16) output tiles of the ff conv [+ the 9 x (C/16)^2 of the recurrent conv] are dealt
+// round-robin to the block's NW waves; accumulators live across all time steps.
+template <int CIN, int C, bool REC, int NW>
+struct WgradMfma {
+    static constexpr int MTc = C / 16, NTF = CIN / 16, NTR = C / 16;
+    static constexpr int NFF = 9 * MTc * NTF, NREC = REC ? 9 * MTc * NTR : 0, NTOT = NFF + NREC;
+    static constexpr int J = (NTOT + NW - 1) / NW;
+    static_assert(C % 16 == 0 && CIN % 16 == 0, "MFMA wgrad: 16-channel tiles");
+    f32x4 acc[J];
+    // wave-uniform tile decode
+    int off[J], mt[J], nt[J], tap[J];
+    bool rec[J], live[J];
+    __device__ void init() {
+        const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int i = wv + NW * j;
+            live[j] = i < NTOT;
+            rec[j] = i >= NFF;
+            const int ii = rec[j] ? i - NFF : i, ntx = rec[j] ? NTR : NTF;
+            tap[j] = live[j] ? ii / (MTc * ntx) : 0;
+            const int rem = ii - tap[j] * (MTc * ntx);
+            mt[j] = live[j] ? rem / ntx : 0;
+            nt[j] = live[j] ? rem - mt[j] * ntx : 0;
+            off[j] = (tap[j] / 3) * HWD + (tap[j] % 3);
+        }
+    }
+    // Gi: interior G tile [NT][Pad<C>]; X: halo input [HN][Pad<CIN>]; S: halo s_prev [HN][Pad<C>]
+    __device__ void step(const float* Gi, const float* X, const float* S, bool has_s) {
+        constexpr int PC = Pad<C>::v, PX = Pad<CIN>::v;
+        const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+#pragma unroll 2
+        for (int s = 0; s < NT / 4; ++s) {
+            const int p = 4 * s + g, ty = p / TW, tx = p - ty * TW;
+            const int hb = ty * HWD + tx;
+            float a[MTc];
+#pragma unroll
+            for (int q = 0; q < MTc; ++q) a[q] = Gi[p * PC + q * 16 + m];
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                if (!live[j] || (rec[j] && !has_s)) continue;
+                float av = a[0];
+#pragma unroll
+                for (int q = 1; q < MTc; ++q)
+                    if (mt[j] == q) av = a[q];
+                const float b = rec[j] ? S[(hb + off[j]) * PC + nt[j] * 16 + m] : X[(hb + off[j]) * PX + nt[j] * 16 + m];
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b, acc[j], 0, 0, 0);
+            }
+        }
+    }
+    // C/D layout: rows co = 16 mt + 4 g + r, column ci = 16 nt + (lane & 15); slab [co][ci][tap]
+    __device__ void flush(float* __restrict__ slab_ff, float* __restrict__ slab_rec, int accumulate) {
+        const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            if (!live[j] || (rec[j] && !slab_rec)) continue;
+            const int ci = nt[j] * 16 + m, cin = rec[j] ? C : CIN;
+            float* base = rec[j] ? slab_rec : slab_ff;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = mt[j] * 16 + g * 4 + r;
+                float* d = base + ((int64_t)co * cin + ci) * 9 + tap[j];
+                *d = accumulate ? *d + acc[j][r] : acc[j][r];
+            }
+        }
+    }
+};
+
 // own-pixel float4 elements of a C-channel NHWC tile, distributed over NTH threads
 template <int CH, int NTH>
 struct Own4 {
@@ -930,9 +1003,10 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
     constexpr bool HALVES = REC && SPLIT == 2;
     using AF = WAcc<CIN, C, HALVES ? NT : NTB, 0>;
     using AR = WAcc<C, C, HALVES ? NT : NTB, HALVES ? NT : 0>;
+    constexpr bool MF = C >= 16 && CIN % 16 == 0;  // matrix-core path (WgradMfma)
     using O = Own4<C, NTB>;
     constexpr int RX = XV ? Halo4<CIN, NTB>::R : 1, RS = REC ? Halo4<C, NTB>::R : 1;
-    constexpr int SCR = (REC && AR::SCRATCH > AF::SCRATCH) ? AR::SCRATCH : AF::SCRATCH;
+    constexpr int SCR = MF ? 4 : ((REC && AR::SCRATCH > AF::SCRATCH) ? AR::SCRATCH : AF::SCRATCH);
     __shared__ __attribute__((aligned(16))) float Gi[NT * PC];
     __shared__ __attribute__((aligned(16))) float X[HN * PI_];
     __shared__ __attribute__((aligned(16))) float S[REC ? HN * PC : 4];
@@ -996,8 +1070,13 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
 
     AF af;
     AR ar;
-    af.zero();
-    if constexpr (REC) ar.zero();
+    WgradMfma<(MF ? CIN : 16), (MF ? C : 16), REC, NTB / 64> am;
+    if constexpr (MF) {
+        am.init();
+    } else {
+        af.zero();
+        if constexpr (REC) ar.zero();
+    }
     issue(0);
     __syncthreads();  // coef
     for (int t = 0; t < nsteps; ++t) {
@@ -1024,15 +1103,23 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
         }
         __syncthreads();
         if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
-        af.step(Gi, X);
-        if constexpr (REC) {
-            if (has_s_t) ar.step(Gi, S);
+        if constexpr (MF) {
+            am.step(Gi, X, S, has_s_t);
+        } else {
+            af.step(Gi, X);
+            if constexpr (REC) {
+                if (has_s_t) ar.step(Gi, S);
+            }
         }
         __syncthreads();
     }
     const int64_t blk = blockIdx.x;
-    af.flush(ap->slab_ff + blk * (C * CIN * 9), ap->accumulate, scratch);
-    if constexpr (REC) ar.flush(ap->slab_rec + blk * (C * C * 9), ap->accumulate, scratch);
+    if constexpr (MF) {
+        am.flush(ap->slab_ff + blk * (C * CIN * 9), REC ? ap->slab_rec + blk * (C * C * 9) : nullptr, ap->accumulate);
+    } else {
+        af.flush(ap->slab_ff + blk * (C * CIN * 9), ap->accumulate, scratch);
+        if constexpr (REC) ar.flush(ap->slab_rec + blk * (C * C * 9), ap->accumulate, scratch);
+    }
 }
 
 // Sum of per-block weight-gradient slabs in fp64, fixed order: 64 elements x 16 slab
@@ -1270,7 +1357,7 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
     if (!valid_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: c must be 4, 8, 16 or 32");
 #define WG_LAUNCH(CI_, CC_, REC_)                                                                          \
     do {                                                                                                   \
-        constexpr int SP_ = (CC_ == 8 || CC_ == 16) ? 2 : 1;                                               \
+        constexpr int SP_ = (CC_ == 8 || CC_ == 16 || (CC_ == 32 && CI_ % 16 == 0)) ? 2 : 1;              \
         hipLaunchKernelGGL((k_wgrad<CI_, CC_, REC_, SP_>), grid, dim3(NT * SP_), 0, s, *a);               \
     } while (0)
 #define WG_PICK(CI_, CC_)                                                                                  \
