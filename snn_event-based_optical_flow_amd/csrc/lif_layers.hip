@@ -922,10 +922,10 @@ struct WAcc {
 // round-robin to the block's NW waves; accumulators live across all time steps.
 template <int CIN, int C, bool REC, int NW>
 struct WgradMfma {
-    static constexpr int MTc = C / 16, NTF = CIN / 16, NTR = C / 16;
+    static constexpr int MTc = (C + 15) / 16, NTF = (CIN + 15) / 16, NTR = (C + 15) / 16;
     static constexpr int NFF = 9 * MTc * NTF, NREC = REC ? 9 * MTc * NTR : 0, NTOT = NFF + NREC;
     static constexpr int J = (NTOT + NW - 1) / NW;
-    static_assert(C % 16 == 0 && CIN % 16 == 0, "MFMA wgrad: 16-channel tiles");
+    static_assert(C % 8 == 0 && CIN % 8 == 0, "MFMA wgrad: 8-channel multiples (C = 8 pads the 16-wide tiles)");
     f32x4 acc[J];
     // wave-uniform tile decode
     int off[J], mt[J], nt[J], tap[J];
@@ -956,7 +956,7 @@ struct WgradMfma {
             const int hb = ty * HWD + tx;
             float a[MTc];
 #pragma unroll
-            for (int q = 0; q < MTc; ++q) a[q] = Gi[p * PC + q * 16 + m];
+            for (int q = 0; q < MTc; ++q) a[q] = (q * 16 + m < C) ? Gi[p * PC + q * 16 + m] : 0.0f;
 #pragma unroll
             for (int j = 0; j < J; ++j) {
                 if (!live[j] || (rec[j] && !has_s)) continue;
@@ -964,7 +964,13 @@ struct WgradMfma {
 #pragma unroll
                 for (int q = 1; q < MTc; ++q)
                     if (mt[j] == q) av = a[q];
-                const float b = rec[j] ? S[(hb + off[j]) * PC + nt[j] * 16 + m] : X[(hb + off[j]) * PX + nt[j] * 16 + m];
+                const int n = nt[j] * 16 + m;
+                float b = 0.0f;  // padded columns: zero (their outputs are not stored)
+                if (rec[j]) {
+                    if (n < C) b = S[(hb + off[j]) * PC + n];
+                } else if (n < CIN) {
+                    b = X[(hb + off[j]) * PX + n];
+                }
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, b, acc[j], 0, 0, 0);
             }
         }
@@ -976,10 +982,12 @@ struct WgradMfma {
         for (int j = 0; j < J; ++j) {
             if (!live[j] || (rec[j] && !slab_rec)) continue;
             const int ci = nt[j] * 16 + m, cin = rec[j] ? C : CIN;
+            if (ci >= cin) continue;
             float* base = rec[j] ? slab_rec : slab_ff;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int co = mt[j] * 16 + g * 4 + r;
+                if (co >= C) continue;
                 float* d = base + ((int64_t)co * cin + ci) * 9 + tap[j];
                 *d = accumulate ? *d + acc[j][r] : acc[j][r];
             }
@@ -1003,7 +1011,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
     constexpr bool HALVES = REC && SPLIT == 2;
     using AF = WAcc<CIN, C, HALVES ? NT : NTB, 0>;
     using AR = WAcc<C, C, HALVES ? NT : NTB, HALVES ? NT : 0>;
-    constexpr bool MF = C >= 16 && CIN % 16 == 0;  // matrix-core path (WgradMfma)
+    constexpr bool MF = C >= 16 && CIN % 16 == 0;  // matrix-core path (WgradMfma; at C = 8 the vector path is faster)
     using O = Own4<C, NTB>;
     constexpr int RX = XV ? Halo4<CIN, NTB>::R : 1, RS = REC ? Halo4<C, NTB>::R : 1;
     constexpr int SCR = MF ? 4 : ((REC && AR::SCRATCH > AF::SCRATCH) ? AR::SCRATCH : AF::SCRATCH);
@@ -1070,7 +1078,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
 
     AF af;
     AR ar;
-    WgradMfma<(MF ? CIN : 16), (MF ? C : 16), REC, NTB / 64> am;
+    WgradMfma<(MF ? CIN : 8), (MF ? C : 8), REC, NTB / 64> am;
     if constexpr (MF) {
         am.init();
     } else {

@@ -214,35 +214,34 @@ class FireNetEngine:
         self.flat_layout = layout
         self.bwd_open = True
 
-    def flush_weight_grads(self, B, H, W, cin0, ws, glayers, stream):
-        """Deferred weight gradients of every layer over all pending time steps (one
-        snnflow_wgrad launch per layer and <= 32 steps), then the slab reduction into the
-        flat gradient buffer (x, s_prev, y, stats saved per step)."""
-        L, C = self.L, self.C
-        steps = self.pending
-        self.pending = []
-        for l in range(L):
-            rec = self.rec[l]
-            for i0 in range(0, len(steps), _lib.MAX_WGRAD_STEPS):
-                chunk = steps[i0:i0 + _lib.MAX_WGRAD_STEPS]
-                a = _lib.WgradArgs()
-                a.B, a.H, a.W, a.c = B, H, W, C
-                a.cin = cin0 if l == 0 else C
-                a.nsteps, a.accumulate, a.rec = len(chunk), 1 if i0 else 0, 1 if rec else 0
-                a.bn_weight = ptr(self.cells[l].bn.weight)
-                a.slab_ff, a.slab_rec = ptr(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
-                for k, (gcur, bnc, ys, stats, x, states, s_prev) in enumerate(chunk):
-                    st = a.steps[k]
-                    st.g_cur, st.y, st.stats, st.bnc = ptr(gcur[l]), ptr(ys[l]), ptr(stats[l]), ptr(bnc[l])
-                    if l == 0:
-                        st.x = ptr(x)
-                        st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
-                    else:
-                        st.x, (st.xs_b, st.xs_c, st.xs_h, st.xs_w) = _spk_half(states[l - 1])
-                    st.s_prev = _ptr_t(s_prev[l]) if rec else None
-                _lib.call(f"wgrad[{l}]", lib.snnflow_wgrad, ctypes.byref(a), stream)
+    def launch_wgrad(self, l, B, H, W, cin0, ws, stream):
+        """Deferred weight gradients of layer l over all pending time steps (one snnflow_wgrad
+        launch per <= 32 steps) into the layer's per-block slabs (x,
+        s_prev, y, stats saved per step)."""
+        C, rec, steps = self.C, self.rec[l], self.pending
+        for i0 in range(0, len(steps), _lib.MAX_WGRAD_STEPS):
+            chunk = steps[i0:i0 + _lib.MAX_WGRAD_STEPS]
+            a = _lib.WgradArgs()
+            a.B, a.H, a.W, a.c = B, H, W, C
+            a.cin = cin0 if l == 0 else C
+            a.nsteps, a.accumulate, a.rec = len(chunk), 1 if i0 else 0, 1 if rec else 0
+            a.bn_weight = ptr(self.cells[l].bn.weight)
+            a.slab_ff, a.slab_rec = ptr(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
+            for k, (gcur, bnc, ys, stats, x, states, s_prev) in enumerate(chunk):
+                st = a.steps[k]
+                st.g_cur, st.y, st.stats, st.bnc = ptr(gcur[l]), ptr(ys[l]), ptr(stats[l]), ptr(bnc[l])
+                if l == 0:
+                    st.x = ptr(x)
+                    st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
+                else:
+                    st.x, (st.xs_b, st.xs_c, st.xs_h, st.xs_w) = _spk_half(states[l - 1])
+                st.s_prev = _ptr_t(s_prev[l]) if rec else None
+            _lib.call(f"wgrad[{l}]", lib.snnflow_wgrad, ctypes.byref(a), stream)
+
+    def launch_slab_reduce(self, ws, glayers, stream):
+        """Fixed-order fp64 sum of every layer's per-block slabs into the flat gradient buffer."""
         descs = []
-        for l in range(L):
+        for l in range(self.L):
             gff, grec, _ = glayers[l]
             descs.append(_lib.SlabDesc(ptr(ws.slab_ff[l]), ptr(gff), gff.numel()))
             if grec is not None:
@@ -250,6 +249,13 @@ class FireNetEngine:
         for i0 in range(0, len(descs), 16):
             chunk = (_lib.SlabDesc * len(descs[i0:i0 + 16]))(*descs[i0:i0 + 16])
             _lib.call("slab_reduce", lib.snnflow_slab_reduce, chunk, len(descs[i0:i0 + 16]), ws.nblk, stream)
+
+    def flush_weight_grads(self, B, H, W, cin0, ws, glayers, stream):
+        """All deferred weight gradients on `stream` (serial form of the root step's tail)."""
+        for l in range(self.L):
+            self.launch_wgrad(l, B, H, W, cin0, ws, stream)
+        self.launch_slab_reduce(ws, glayers, stream)
+        self.pending = []
 
     def grad_views(self):
         """Per-layer gradient destinations inside the flat buffer."""
@@ -420,6 +426,10 @@ class FireNetStep(torch.autograd.Function):
         # per-step buffers kept until the deferred weight gradients run (root step)
         gcur = torch.empty(L, B, H, W, C, device=dev)   # dL/d BN-output of every layer
         bnc = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
+        eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev))
+        # (the deferred weight gradients stay on this stream after the chain: a side stream
+        # overlapping them with the root step's chain measured slower under graph replay,
+        # 2.48 -> 2.72 ms per cfg2 train step)
         try:
             # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
             top = L - 1
@@ -467,7 +477,6 @@ class FireNetStep(torch.autograd.Function):
                         a.g_x = ptr(gx)
                         a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
                 _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
-            eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev))
             if ctx.root:
                 eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s)
         except Exception:
