@@ -145,8 +145,7 @@ def main():
         nonlocal state_bufs
         if state_bufs is None:
             state_bufs = [s.detach().clone() for s in model._states]
-        for dst, s in zip(state_bufs, model._states):
-            dst.copy_(s.detach())
+        torch._foreach_copy_(state_bufs, [s.detach() for s in model._states])  # one multi-tensor launch
         model._states = list(state_bufs)
 
     def step_eager():

@@ -96,6 +96,25 @@ __device__ inline float4 ld4_or_zero(const float4* p, const float4* fallback, in
     return p ? t : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// Output stores of the layer kernels (states, pre-BN currents, gradients): write-through
+// (sc1 buffer stores) so the kernel does not end with megabytes of dirty L2 lines to write
+// back at the boundary (MI355X_MICROARCH.md price list, row 'boundary').  0: plain stores.
+#ifndef SNNFLOW_WT_STORES
+#define SNNFLOW_WT_STORES 0  // measured: sc1 stores cost 2.48 -> 3.32 ms per cfg2 step (the next kernel loses its L2 hits)
+#endif
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline void st_out4(float4* base, int64_t i, const float4& v) {
+#if SNNFLOW_WT_STORES
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+    const i32x4 d = {__builtin_bit_cast(int, v.x), __builtin_bit_cast(int, v.y), __builtin_bit_cast(int, v.z),
+                     __builtin_bit_cast(int, v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(d, r, (int)(i * 16), 0, 16);  // aux 16 = sc1
+#else
+    base[i] = v;
+#endif
+}
+
 __device__ inline bool in_image(int h, int w, int H, int W) { return h >= 0 && h < H && w >= 0 && w < W; }
 
 // A C-channel NHWC halo tile as float4 elements e = pixel * (C/4) + quad, distributed
