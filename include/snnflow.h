@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 10
+#define SNNFLOW_ABI_VERSION 11
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -294,29 +294,39 @@ typedef struct snnflow_slab_desc { const float* slab; float* out; int elems; } s
 int snnflow_slab_reduce(const snnflow_slab_desc* d, int n, int nblk, void* stream);
 
 /* ---- event warping / contrast-maximisation loss (loss/flow.py:178-303) ----
- * events [B][M][4] (ts,y,x,p) with per-window offsets (pass k owns events
- * [off[k], off[k+1]) of every sample; its timestamps are ts + k, flow.py:92),
- * pol [B][M][2], flows [B][T][2][H][W] (NCHW per window), masks [B][T][H][W]. */
+ * Window k's events are the concatenated index range [off[k], off[k+1]) of every sample
+ * (flow.py:58-121); its timestamps are ts + k (flow.py:92).  Each window's tensors are
+ * passed by pointer (tables below), so nothing is concatenated on the device. */
+#define SNNFLOW_MAX_WINDOWS 64
 typedef struct snnflow_iwe_loss_args {
     int B, M, T, H, W;
     int tf;                     /* flow/mask windows: T, or 1 when overwrite_intermediate
                                    (all events use the last flow; loss/flow.py:123-150) */
-    const float* events; const float* pol; const float* flows; const float* masks;
-    int32_t off[65];            /* pass offsets off[0..T] (T <= 64), by value */
+    /* per event window k < T (N_k = off[k+1] - off[k] events per sample, M = sum N_k):
+     * events [B][N_k][4] (ts, y, x, p) and polarity masks [B][N_k][2] -- the tensors
+     * event_flow_association recorded, read in place (no concatenation) */
+    const float* events[SNNFLOW_MAX_WINDOWS]; const float* pol[SNNFLOW_MAX_WINDOWS];
+    /* per flow window t < tf: flow [B][2][H][W] and event mask [B][H][W] */
+    const float* flows[SNNFLOW_MAX_WINDOWS]; const float* masks[SNNFLOW_MAX_WINDOWS];
+    int32_t off[SNNFLOW_MAX_WINDOWS + 1];  /* pass offsets off[0..T], by value */
     float flow_scaling, weight;
     int smoothing_mask, overwrite_intermediate, loss_scaling;
-    float* images;              /* scratch [2 dir][4 img][B][H*W]: cnt+, cnt-, ts+, ts- */
-    double* acc;                /* scratch [6*B + 5] sums (zeroed by snnflow_iwe_loss_fwd) */
+    float* images;              /* scratch snnflow_iwe_scratch_floats(B, H, W): per-split partial
+                                   IWEs; after the forward its first [2 dir][4 img][B][H*W]
+                                   (cnt+, cnt-, ts+, ts-) hold the totals the backward reads */
+    double* acc;                /* scratch snnflow_iwe_acc_doubles(B, H, W, tf): per-block partial
+                                   sums, reduced in a fixed order (deterministic loss) */
     float* persample;           /* scratch [2 dir][B][4]: S+, S-, nz, loss_b          */
     float* smooth;              /* scratch [8]                                         */
     float* loss;                /* out [1]                                             */
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
-/* g_loss: device scalar; g_flows out [B][T][2][H][W] (fully written). gimg scratch
- * like images. */
+/* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch
+ * [2][4][B][H*W]. */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
                          float* g_flows, void* stream);
-int snnflow_iwe_scratch_floats(int B, int H, int W);  /* images floats; acc must directly follow */
+int snnflow_iwe_acc_doubles(int B, int H, int W, int tf);
+int snnflow_iwe_scratch_floats(int B, int H, int W);  /* floats of the images scratch */
 
 /* utils/iwe.py:20-71 get_interpolation (+ purge_unfeasible :4-17) for one pass:
  * idx out [B][K*M] int32 (corner-major, K=4 bilinear / 1 rounded), w out [B][K*M]. */

@@ -34,47 +34,78 @@ __device__ inline int pass_of(const int32_t* off, int T, int i) {
 __device__ inline float relu_tie(float z) { return z > 0.0f ? 1.0f : (z == 0.0f ? 0.5f : 0.0f); }
 __device__ inline float sgnf(float d) { return d > 0.0f ? 1.0f : (d < 0.0f ? -1.0f : 0.0f); }
 
-// images layout: [dir 2][img 4][B][HW], img = cnt+, cnt-, ts+, ts-
-__global__ __launch_bounds__(NT) void k_iwe_scatter(snnflow_iwe_loss_args a) {
-    if (blockIdx.x == 0)
-        for (int j = threadIdx.x; j < 6 * a.B + 5; j += NT) a.acc[j] = 0.0;
-    const int64_t HWp = (int64_t)a.H * a.W;
-    const int64_t n = (int64_t)a.B * a.M;
-    const int64_t img = (int64_t)a.B * HWp;
-    for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
-        const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
-        const int k = pass_of(a.off, a.T, i);
-        const float* ev = a.events + e * 4;
-        const float ts = ev[0] + (float)k, y = ev[1], x = ev[2];
+// Event e = (sample b, concatenated index i) of window k: its 4 floats and 2 pol floats.
+struct EventRef { const float* ev; const float* pol; int k; };
+
+__device__ inline EventRef event_ref(const snnflow_iwe_loss_args& a, int b, int i) {
+    const int k = pass_of(a.off, a.T, i);
+    const int64_t nk = a.off[k + 1] - a.off[k], j = (int64_t)b * nk + (i - a.off[k]);
+    EventRef r;
+    r.ev = a.events[k] + j * 4;
+    r.pol = a.pol[k] + j * 2;
+    r.k = k;
+    return r;
+}
+
+__device__ inline const float* flow_of(const snnflow_iwe_loss_args& a, int b, int t) {
+    return a.flows[t] + (int64_t)b * 2 * a.H * a.W;
+}
+__device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, int t) {
+    return a.masks[t] + (int64_t)b * a.H * a.W;
+}
+
+// IWE splat with LDS-privatised images.  One block per (sample, warp direction, band of
+// SPLAT_BAND pixels) owns the four images (cnt+, cnt-, ts+, ts-) of its band in LDS, scans
+// every event of its sample, adds the bilinear corners that fall into the band with LDS
+// atomics, then writes the band once (no memset, no global atomics).
+// images layout: [dir 2][img 4][B][HW].
+// Events of a sample are dealt to SPLAT_SPLIT blocks per band; each writes its own partial
+// image set (images + split * 8*B*HW), summed in fixed order by k_iwe_loss.
+constexpr int SPLAT_NT = 1024, SPLAT_BAND = 4096, SPLAT_SPLIT = 4;
+
+__global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands) {
+    __shared__ float img[4][SPLAT_BAND];
+    const int tid = threadIdx.x;
+    const int split = blockIdx.x % SPLAT_SPLIT, rest = blockIdx.x / SPLAT_SPLIT;
+    const int band = rest % nbands, d = (rest / nbands) % 2, b = rest / (2 * nbands);
+    const int64_t HWp = (int64_t)a.H * a.W, imgsz = (int64_t)a.B * HWp;
+    const int p0 = band * SPLAT_BAND;
+    const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
+    for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&img[0][0])[j] = 0.0f;
+    __syncthreads();
+    const float tref = d == 0 ? (float)a.T : 0.0f;
+    for (int i = split * SPLAT_NT + tid; i < a.M; i += SPLAT_SPLIT * SPLAT_NT) {
+        const EventRef r = event_ref(a, b, i);
+        const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
+        const float pm0 = r.pol[0], pm1 = r.pol[1];
         const int pix = (int)(y * (float)a.W + x);
-        const int kf = a.tf == 1 ? 0 : k;
-        const float* fl = a.flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+        const float* fl = flow_of(a, b, a.tf == 1 ? 0 : r.k);
         const float fy = fl[HWp + pix], fx = fl[pix];
-        const float pm0 = a.pol[e * 2], pm1 = a.pol[e * 2 + 1];
+        const float tsw = d == 0 ? ts : (float)a.T - ts;
+        Corner c[4];
+        float wy, wx;
+        warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            const float tref = d == 0 ? (float)a.T : 0.0f;
-            const float tsw = d == 0 ? ts : (float)a.T - ts;
-            Corner c[4];
-            float wy, wx;
-            warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
-            float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float wt = c[q].wt;
-                if (wt == 0.0f) continue;
-                const float wts = wt * tsw;
-                if (pm0 != 0.0f) {
-                    atomicAdd(base + c[q].idx, wt * pm0);
-                    atomicAdd(base + 2 * img + c[q].idx, wts * pm0);
-                }
-                if (pm1 != 0.0f) {
-                    atomicAdd(base + img + c[q].idx, wt * pm1);
-                    atomicAdd(base + 3 * img + c[q].idx, wts * pm1);
-                }
+        for (int q = 0; q < 4; ++q) {
+            const float wt = c[q].wt;
+            const int li = c[q].idx - p0;
+            if (wt == 0.0f || li < 0 || li >= np) continue;
+            const float wts = wt * tsw;
+            if (pm0 != 0.0f) {
+                atomicAdd(&img[0][li], wt * pm0);
+                atomicAdd(&img[2][li], wts * pm0);
+            }
+            if (pm1 != 0.0f) {
+                atomicAdd(&img[1][li], wt * pm1);
+                atomicAdd(&img[3][li], wts * pm1);
             }
         }
     }
+    __syncthreads();
+    float* out = a.images + (int64_t)split * 8 * imgsz + (int64_t)d * 4 * imgsz + (int64_t)b * HWp + p0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        for (int j = tid; j < np; j += SPLAT_NT) out[(int64_t)q * imgsz + j] = img[q][j];
 }
 
 // Smoothness terms where pixel (h,w) of window t is the first element 'a' of the pair.
@@ -84,9 +115,9 @@ __device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
 
 __device__ inline SmoothTerms smooth_at(const snnflow_iwe_loss_args& a, int b, int t, int h, int w) {
     const int64_t HWp = (int64_t)a.H * a.W;
-    const float* fx = a.flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+    const float* fx = flow_of(a, b, t);
     const float* fy = fx + HWp;
-    const float* m = a.masks + ((int64_t)b * a.tf + t) * HWp;
+    const float* m = mask_of(a, b, t);
     const int p = h * a.W + w;
     SmoothTerms r;
     const bool sm = a.smoothing_mask != 0;
@@ -101,67 +132,119 @@ __device__ inline SmoothTerms smooth_at(const snnflow_iwe_loss_args& a, int b, i
     r.v[3] = (h >= 1 && w + 1 < a.W) ? term(p - a.W + 1, fx, fy, m) : 0.0f;         // dxdy_ur
     r.v[4] = 0.0f;                                                                  // dt
     if (t + 1 < a.tf && !a.overwrite_intermediate) {
-        const float* fx2 = fx + 2 * HWp;
-        const float* fy2 = fx2 + HWp;
-        const float* m2 = m + HWp;
-        r.v[4] = term(p, fx2, fy2, m2);
+        const float* fx2 = flow_of(a, b, t + 1);
+        r.v[4] = term(p, fx2, fx2 + HWp, mask_of(a, b, t + 1));
     }
     return r;
 }
 
-// Per pixel: IWE loss terms for both directions + smoothness, summed per block and
-// added (fp64 atomics) into acc[6*B + 5]: per sample {S+, S-, nz} x {fw, bw}, then the
-// five smoothness sums.  blocks: B * chunks (each block covers NT pixels of one sample).
+// Per (sample, window t, chunk of NT pixels): IWE loss terms of both directions (t == 0
+// blocks) + the smoothness terms of window t, reduced per block and stored as one row of
+// partial sums acc[block][LOSS_NV] (no atomics; k_iwe_finalize sums rows in fixed order).
+// Row: {S+, S-, nz} x {fw, bw}, then the five smoothness sums.
+constexpr int LOSS_NV = 11;
+
 __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks) {
-    constexpr int NV = 11;
-    __shared__ float red[4][NV];
-    const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
+    __shared__ float red[NT / 64][LOSS_NV];
+    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, t = (blockIdx.x / chunks) % a.tf,
+              b = blockIdx.x / (chunks * a.tf);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
-    float v[NV];
+    float v[LOSS_NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) v[j] = 0.0f;
+    for (int j = 0; j < LOSS_NV; ++j) v[j] = 0.0f;
     if (p < HWp) {
-        const float T = (float)a.T;
+        if (t == 0) {
+            const float T = (float)a.T;
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-            const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
-            const float A = (tp / (cp + 1e-9f)) / T;
-            const float Bv = (tn / (cn + 1e-9f)) / T;
-            v[3 * d + 0] = A * A;
-            v[3 * d + 1] = Bv * Bv;
-            v[3 * d + 2] = (cp + cn > 0.0f) ? 1.0f : 0.0f;
+            for (int d = 0; d < 2; ++d) {
+                // sum the splat's partial images (fixed order) and keep the total in partial 0
+                float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+                float q4[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    float v0 = base[q * img];
+#pragma unroll
+                    for (int sp = 1; sp < SPLAT_SPLIT; ++sp) v0 += base[(int64_t)sp * 8 * img + q * img];
+                    q4[q] = v0;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) base[q * img] = q4[q];
+                const float cp = q4[0], cn = q4[1], tp = q4[2], tn = q4[3];
+                const float A = (tp / (cp + 1e-9f)) / T;
+                const float Bv = (tn / (cn + 1e-9f)) / T;
+                v[3 * d + 0] = A * A;
+                v[3 * d + 1] = Bv * Bv;
+                v[3 * d + 2] = (cp + cn > 0.0f) ? 1.0f : 0.0f;
+            }
         }
         const int h = p / a.W, w = p - h * a.W;
-        for (int t = 0; t < a.tf; ++t) {
-            const SmoothTerms s = smooth_at(a, b, t, h, w);
+        const SmoothTerms sm = smooth_at(a, b, t, h, w);
 #pragma unroll
-            for (int j = 0; j < 5; ++j) v[6 + j] += s.v[j];
-        }
+        for (int j = 0; j < 5; ++j) v[6 + j] = sm.v[j];
     }
     const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-        const float s = wave_sum(v[j]);
+    for (int j = 0; j < LOSS_NV; ++j) {
+        const float s = wave_total(v[j]);
         if (lane == 0) red[wv][j] = s;
     }
     __syncthreads();
-    if (tid < NV) {
-        const double s = (((double)red[0][tid] + (double)red[1][tid]) + (double)red[2][tid]) + (double)red[3][tid];
-        atomicAdd(a.acc + (tid < 6 ? 6 * b + tid : 6 * a.B + (tid - 6)), s);
+    if (tid < LOSS_NV) {
+        double s = 0.0;
+#pragma unroll
+        for (int w2 = 0; w2 < NT / 64; ++w2) s += (double)red[w2][tid];
+        a.acc[(int64_t)blockIdx.x * LOSS_NV + tid] = s;
     }
 }
 
-// loss = sum_b (S+ + S-)_fw / nz_fw + ... (loss/flow.py:219-261) + weight * smoothness.
-__global__ void k_iwe_finalize(snnflow_iwe_loss_args a) {
+// Fixed-order fp64 reduction of the partial rows, then loss = sum_b (S+ + S-)_fw / nz_fw
+// + ... (loss/flow.py:219-261) + weight * smoothness.  One block: wave w reduces the rows
+// of samples w, w + 16, ... (all 11 columns), then the smoothness sums add up over samples.
+constexpr int FIN_NT = 1024;
+
+__global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int chunks) {
+    __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
+    __shared__ double smp[64][5];          // per-sample smoothness sums
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int rows_b = chunks * a.tf;
+    // wave w reduces samples w, w + 16, ...: lane-strided rows, all 11 columns at once
+    for (int b = wv; b < a.B; b += FIN_NT / 64) {
+        double s[LOSS_NV];
+#pragma unroll
+        for (int j = 0; j < LOSS_NV; ++j) s[j] = 0.0;
+        const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
+#pragma unroll 4
+        for (int c = lane; c < rows_b; c += 64) {
+#pragma unroll
+            for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
+        }
+#pragma unroll
+        for (int j = 0; j < LOSS_NV; ++j) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) s[j] += __shfl_xor(s[j], off, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) outv[6 * b + j] = s[j];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) smp[b][j] = s[6 + j];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        double t = 0.0;
+        for (int b = 0; b < a.B; ++b) t += smp[b][threadIdx.x];
+        outv[6 * a.B + threadIdx.x] = t;
+    }
+    __syncthreads();
     if (threadIdx.x != 0) return;
     float total = 0.0f;
     for (int d = 0; d < 2; ++d) {
         float dir = 0.0f;
         for (int bb = 0; bb < a.B; ++bb) {
-            const float sp = (float)a.acc[6 * bb + 3 * d], sn = (float)a.acc[6 * bb + 3 * d + 1];
-            const float nz = (float)a.acc[6 * bb + 3 * d + 2];
+            const float sp = (float)outv[6 * bb + 3 * d], sn = (float)outv[6 * bb + 3 * d + 1];
+            const float nz = (float)outv[6 * bb + 3 * d + 2];
             float lb = sp + sn;
             if (a.loss_scaling) lb = lb / nz;
             float* ps = a.persample + ((int64_t)d * a.B + bb) * 4;
@@ -171,87 +254,89 @@ __global__ void k_iwe_finalize(snnflow_iwe_loss_args a) {
         total += dir;
     }
     const int comps = a.overwrite_intermediate ? 4 : 5;
-    float sm = (float)a.acc[6 * a.B + 0];
-    for (int j = 1; j < comps; ++j) sm += (float)a.acc[6 * a.B + j];
+    float sm = (float)outv[6 * a.B + 0];
+    for (int j = 1; j < comps; ++j) sm += (float)outv[6 * a.B + j];
     sm = sm / (float)comps / (float)a.tf;
-    for (int j = 0; j < 5; ++j) a.smooth[j] = (float)a.acc[6 * a.B + j];
+    for (int j = 0; j < 5; ++j) a.smooth[j] = (float)outv[6 * a.B + j];
     a.smooth[5] = sm;
     a.loss[0] = total + a.weight * sm;
 }
 
-// Per pixel: dL/d(images) for both directions, and the smoothness part of dL/dflows
-// (plain stores: g_flows is fully written here; events add into it afterwards).
+// Per (sample, window t, pixel): dL/d(images) for both directions (t == 0 blocks) and the
+// smoothness part of dL/dflow_t (plain stores: g_flows is fully written here; the events
+// add into it afterwards).
 __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
                                                         float* g_flows, int chunks) {
-    const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
+    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, t = (blockIdx.x / chunks) % a.tf,
+              b = blockIdx.x / (chunks * a.tf);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
     if (p >= HWp) return;
     const float g = g_loss[0];
-    const float T = (float)a.T;
+    if (t == 0) {
+        const float T = (float)a.T;
 #pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
-        const float nz = ps[2], lb = ps[3];
-        const float gS = a.loss_scaling ? g / nz : g;
-        const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-        float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-        const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
-        const float dp = cp + 1e-9f, dn = cn + 1e-9f;
-        const float qp = tp / dp, qn = tn / dn;
-        const float Ap = qp / T, An = qn / T;
-        const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
-        float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
-        if (a.loss_scaling && !(cp + cn > 0.0f)) {
-            const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
-            gcp += gz;
-            gcn += gz;
+        for (int d = 0; d < 2; ++d) {
+            const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
+            const float nz = ps[2], lb = ps[3];
+            const float gS = a.loss_scaling ? g / nz : g;
+            const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+            float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+            const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
+            const float dp = cp + 1e-9f, dn = cn + 1e-9f;
+            const float qp = tp / dp, qn = tn / dn;
+            const float Ap = qp / T, An = qn / T;
+            const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
+            float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
+            if (a.loss_scaling && !(cp + cn > 0.0f)) {
+                const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
+                gcp += gz;
+                gcn += gz;
+            }
+            gb[0] = gcp;
+            gb[img] = gcn;
+            gb[2 * img] = gqp / dp;
+            gb[3 * img] = gqn / dn;
         }
-        gb[0] = gcp;
-        gb[img] = gcn;
-        gb[2 * img] = gqp / dp;
-        gb[3 * img] = gqn / dn;
     }
     // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
     const int comps = a.overwrite_intermediate ? 4 : 5;
     const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
     const int h = p / a.W, w = p - h * a.W;
     const bool sm = a.smoothing_mask != 0;
-    for (int t = 0; t < a.tf; ++t) {
-        const float* fx = a.flows + (((int64_t)b * a.tf + t) * 2) * HWp;
-        const float* fy = fx + HWp;
-        const float* m = a.masks + ((int64_t)b * a.tf + t) * HWp;
-        float acc = 0.0f;
-        // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
-        auto pairgrad = [&](const float* fxa, const float* fya, const float* ma, int pa, const float* fxb,
-                            const float* fyb, const float* mb, int pb) {
-            const float dd = (fxa[pa] - fxb[pb]) + (fya[pa] - fyb[pb]);
-            const float c = charb(dd);
-            const float mk = sm ? ma[pa] * mb[pb] : 1.0f;
-            return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
-        };
-        if (w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + 1);
-        if (w >= 1) acc -= pairgrad(fx, fy, m, p - 1, fx, fy, m, p);
-        if (h + 1 < a.H) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W);
-        if (h >= 1) acc -= pairgrad(fx, fy, m, p - a.W, fx, fy, m, p);
-        if (h + 1 < a.H && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W + 1);
-        if (h >= 1 && w >= 1) acc -= pairgrad(fx, fy, m, p - a.W - 1, fx, fy, m, p);
-        if (h >= 1 && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p - a.W + 1);
-        if (h + 1 < a.H && w >= 1) acc -= pairgrad(fx, fy, m, p + a.W - 1, fx, fy, m, p);
-        if (!a.overwrite_intermediate) {
-            if (t + 1 < a.tf) {
-                const float* fx2 = fx + 2 * HWp;
-                acc += pairgrad(fx, fy, m, p, fx2, fx2 + HWp, m + HWp, p);
-            }
-            if (t >= 1) {
-                const float* fx0 = fx - 2 * HWp;
-                acc -= pairgrad(fx0, fx0 + HWp, m - HWp, p, fx, fy, m, p);
-            }
+    const float* fx = flow_of(a, b, t);
+    const float* fy = fx + HWp;
+    const float* m = mask_of(a, b, t);
+    float acc = 0.0f;
+    // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
+    auto pairgrad = [&](const float* fxa, const float* fya, const float* ma, int pa, const float* fxb,
+                        const float* fyb, const float* mb, int pb) {
+        const float dd = (fxa[pa] - fxb[pb]) + (fya[pa] - fyb[pb]);
+        const float c = charb(dd);
+        const float mk = sm ? ma[pa] * mb[pb] : 1.0f;
+        return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
+    };
+    if (w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + 1);
+    if (w >= 1) acc -= pairgrad(fx, fy, m, p - 1, fx, fy, m, p);
+    if (h + 1 < a.H) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W);
+    if (h >= 1) acc -= pairgrad(fx, fy, m, p - a.W, fx, fy, m, p);
+    if (h + 1 < a.H && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W + 1);
+    if (h >= 1 && w >= 1) acc -= pairgrad(fx, fy, m, p - a.W - 1, fx, fy, m, p);
+    if (h >= 1 && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p - a.W + 1);
+    if (h + 1 < a.H && w >= 1) acc -= pairgrad(fx, fy, m, p + a.W - 1, fx, fy, m, p);
+    if (!a.overwrite_intermediate) {
+        if (t + 1 < a.tf) {
+            const float* fx2 = flow_of(a, b, t + 1);
+            acc += pairgrad(fx, fy, m, p, fx2, fx2 + HWp, mask_of(a, b, t + 1), p);
         }
-        float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
-        gf[p] = acc;
-        gf[HWp + p] = acc;
+        if (t >= 1) {
+            const float* fx0 = flow_of(a, b, t - 1);
+            acc -= pairgrad(fx0, fx0 + HWp, mask_of(a, b, t - 1), p, fx, fy, m, p);
+        }
     }
+    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+    gf[p] = acc;
+    gf[HWp + p] = acc;
 }
 
 // Per event: gather dL/d(images) at the 4 corners of both warps, chain through the
@@ -263,14 +348,13 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
     const int64_t img = (int64_t)a.B * HWp;
     for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
         const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
-        const int k = pass_of(a.off, a.T, i);
-        const float* ev = a.events + e * 4;
-        const float ts = ev[0] + (float)k, y = ev[1], x = ev[2];
+        const EventRef r = event_ref(a, b, i);
+        const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
         const int pix = (int)(y * (float)a.W + x);
-        const int kf = a.tf == 1 ? 0 : k;
-        const float* fl = a.flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+        const int kf = a.tf == 1 ? 0 : r.k;
+        const float* fl = flow_of(a, b, kf);
         const float fy = fl[HWp + pix], fx = fl[pix];
-        const float pm0 = a.pol[e * 2], pm1 = a.pol[e * 2 + 1];
+        const float pm0 = r.pol[0], pm1 = r.pol[1];
         float gfy = 0.0f, gfx = 0.0f;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
@@ -349,12 +433,15 @@ int grid_for(int64_t n, int per_block, int cap) {
 }
 
 int check_loss_args(const snnflow_iwe_loss_args* a) {
-    if (!a || a->B <= 0 || a->M < 0 || a->T <= 0 || a->T > 64 || a->H <= 0 || a->W <= 0 ||
-        !(a->tf == 1 || a->tf == a->T))
-        SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: bad shape");
-    if (!a->events || !a->pol || !a->flows || !a->masks || !a->images || !a->acc || !a->persample || !a->smooth ||
-        !a->loss)
+    if (!a || a->B <= 0 || a->B > 64 || a->M < 0 || a->T <= 0 || a->T > SNNFLOW_MAX_WINDOWS || a->H <= 0 ||
+        a->W <= 0 || !(a->tf == 1 || a->tf == a->T))
+        SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: bad shape (B <= 64, T <= 64, tf in {1, T})");
+    if (!a->images || !a->acc || !a->persample || !a->smooth || !a->loss)
         SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: missing buffer");
+    for (int k = 0; k < a->T; ++k)
+        if (!a->events[k] || !a->pol[k]) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: missing event window");
+    for (int t = 0; t < a->tf; ++t)
+        if (!a->flows[t] || !a->masks[t]) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: missing flow / mask window");
     if (a->off[0] != 0 || a->off[a->T] != a->M) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: offsets must span [0, M]");
     for (int k = 0; k < a->T; ++k)
         if (a->off[k + 1] < a->off[k]) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: offsets must be non-decreasing");
@@ -365,18 +452,22 @@ int check_loss_args(const snnflow_iwe_loss_args* a) {
 
 extern "C" {
 
-int snnflow_iwe_scratch_floats(int B, int H, int W) { return 8 * B * H * W; }
+int snnflow_iwe_scratch_floats(int B, int H, int W) { return SPLAT_SPLIT * 8 * B * H * W; }
+
+int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
+    const int64_t chunks = ((int64_t)H * W + NT - 1) / NT;
+    return (int)((int64_t)B * tf * chunks * LOSS_NV);
+}
 
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     if (int rc = check_loss_args(a)) return rc;
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
-    hipError_t e = hipMemsetAsync(a->images, 0, sizeof(float) * 8 * a->B * HWp, s);
-    if (e != hipSuccess) SNN_FAIL((int)e, hipGetErrorString(e));
-    hipLaunchKernelGGL(k_iwe_scatter, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a);
+    const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
+    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands * SPLAT_SPLIT), dim3(SPLAT_NT), 0, s, *a, nbands);
     const int chunks = (int)((HWp + NT - 1) / NT);
-    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
-    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(64), 0, s, *a);
+    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * a->tf * chunks), dim3(NT), 0, s, *a, chunks);
+    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, chunks);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -388,7 +479,8 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
     const int chunks = (int)((HWp + NT - 1) / NT);
-    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows, chunks);
+    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * a->tf * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
+                       chunks);
     if (a->M > 0)
         hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a, gimg,
                            g_flows);

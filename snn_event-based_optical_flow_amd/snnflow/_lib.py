@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class Neuron(ctypes.Structure):
@@ -140,9 +140,13 @@ class PrepDesc(ctypes.Structure):
 MAX_BATCH = 16
 
 
+MAX_WINDOWS = 64
+
+
 class IweLossArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("M", I32), ("T", I32), ("H", I32), ("W", I32), ("tf", I32),
-                ("events", P), ("pol", P), ("flows", P), ("masks", P), ("off", ctypes.c_int32 * 65),
+                ("events", P * MAX_WINDOWS), ("pol", P * MAX_WINDOWS), ("flows", P * MAX_WINDOWS),
+                ("masks", P * MAX_WINDOWS), ("off", ctypes.c_int32 * (MAX_WINDOWS + 1)),
                 ("flow_scaling", F32), ("weight", F32),
                 ("smoothing_mask", I32), ("overwrite_intermediate", I32), ("loss_scaling", I32),
                 ("images", P), ("acc", P), ("persample", P), ("smooth", P), ("loss", P)]
@@ -169,6 +173,7 @@ EXPORTS = {
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
     "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P]),
     "snnflow_iwe_scratch_floats": (I32, [I32, I32, I32]),
+    "snnflow_iwe_acc_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
     "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),

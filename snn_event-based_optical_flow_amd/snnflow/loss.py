@@ -1,12 +1,14 @@
 """Contrast-maximisation loss with the reference's ``EventWarping`` API
 (``loss/flow.py:28-303``) running on the HIP IWE kernels (csrc/iwe_loss.hip).
 
-``event_flow_association`` only records the per-window tensors; ``forward`` runs
-two kernels (warp + bilinear splat of all events of all windows into the 8 IWEs
--- forward/backward warp x {count, timestamp} x polarity -- then per-pixel loss
-terms, Charbonnier smoothness and the batch reduction); its backward runs two
-more (per-pixel image gradients + smoothness gradient, then per-event gradient
-gathered from the 4 corners of both warps and scattered onto the flow maps).
+``event_flow_association`` only records the per-window tensors, which the kernels read
+in place through per-window pointer tables (nothing is concatenated).  ``forward`` runs
+three kernels: the warp + bilinear splat of every event into the 8 IWEs (forward/backward
+warp x {count, timestamp} x polarity) with LDS-privatised image bands; per (pixel,
+window) loss and Charbonnier smoothness terms reduced to per-block rows; a fixed-order
+fp64 reduction of the rows into the loss.  The backward runs two more: per (pixel,
+window) image and smoothness gradients, then the per-event gradient gathered from the 4
+corners of both warps and scattered onto the flow maps.
 """
 import ctypes
 
@@ -20,19 +22,26 @@ class _Scratch:
     def __init__(self):
         self.key = None
 
-    def get(self, B, H, W, device):
-        key = (B, H, W, device)
+    def get(self, B, H, W, tf, device):
+        key = (B, H, W, tf, device)
         if self.key != key:
-            self.acc = torch.zeros(6 * B + 5, dtype=torch.float64, device=device)
+            self.acc = torch.empty(lib.snnflow_iwe_acc_doubles(B, H, W, tf), dtype=torch.float64, device=device)
+            self.dummy = torch.zeros(8, device=device)  # pointer for empty event windows (never read)
             self.key = key
         return self
 
 
-def _fill_args(meta, events, pol, masks, flows, images, persample, smooth, loss, scr):
+def _fill_args(meta, windows, flows, images, persample, smooth, loss, scr):
+    """windows: (events [B,N_k,4], pols [B,N_k,2], masks [B,1,H,W]) per window, read in place."""
+    evs, pols, masks = windows
     a = _lib.IweLossArgs()
-    B, M = events.shape[0], events.shape[1]
-    a.B, a.M, a.T, a.H, a.W, a.tf = B, M, meta["T"], meta["H"], meta["W"], flows.shape[1]
-    a.events, a.pol, a.flows, a.masks = ptr(events), ptr(pol), ptr(flows), ptr(masks)
+    B = evs[0].shape[0]
+    a.B, a.M, a.T, a.H, a.W, a.tf = B, meta["off"][-1], meta["T"], meta["H"], meta["W"], len(flows)
+    for k, (e, p) in enumerate(zip(evs, pols)):
+        a.events[k] = ptr(e) if e.numel() else ptr(scr.dummy)
+        a.pol[k] = ptr(p) if p.numel() else ptr(scr.dummy)
+    for t, (f, m) in enumerate(zip(flows, masks)):
+        a.flows[t], a.masks[t] = ptr(f), ptr(m)
     for i, o in enumerate(meta["off"]):
         a.off[i] = o
     a.flow_scaling, a.weight = float(meta["flow_scaling"]), float(meta["weight"])
@@ -45,35 +54,41 @@ def _fill_args(meta, events, pol, masks, flows, images, persample, smooth, loss,
 
 class EventWarpingFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, meta, scr, events, pol, masks, *flows):
-        dev = events.device
+    def forward(ctx, meta, scr, windows, *flows):
+        evs = windows[0]
+        dev = evs[0].device
         s = _lib.stream_ptr(dev)
-        flows_all = torch.stack([f.float() for f in flows], dim=1).contiguous()  # [B, Tf, 2, H, W]
-        B, H, W = events.shape[0], meta["H"], meta["W"]
-        scr = scr.get(B, H, W, dev)
-        images = torch.empty(8 * B * H * W, device=dev)
+        if len(evs) > _lib.MAX_WINDOWS:
+            raise _lib.SnnflowError(f"EventWarping: at most {_lib.MAX_WINDOWS} windows per loss")
+        flows_c = [f.float().contiguous() for f in flows]  # [B, 2, H, W] each, no copy when already so
+        for f in flows_c:
+            _lib.require_device(f, "flow")
+        B, H, W = evs[0].shape[0], meta["H"], meta["W"]
+        scr = scr.get(B, H, W, len(flows_c), dev)
+        images = torch.empty(lib.snnflow_iwe_scratch_floats(B, H, W), device=dev)
         persample = torch.empty(2 * B * 4, device=dev)
         smooth = torch.empty(8, device=dev)
         loss = torch.empty((), device=dev)
-        a = _fill_args(meta, events, pol, masks, flows_all, images, persample, smooth, loss, scr)
+        a = _fill_args(meta, windows, flows_c, images, persample, smooth, loss, scr)
         _lib.call("iwe_loss_fwd", lib.snnflow_iwe_loss_fwd, ctypes.byref(a), s)
-        ctx.meta, ctx.scr = meta, scr
-        ctx.save_for_backward(events, pol, masks, flows_all, images, persample, smooth)
-        ctx.nflows = len(flows)
+        ctx.meta, ctx.scr, ctx.windows = meta, scr, windows
+        ctx.save_for_backward(images, persample, smooth, *flows_c)
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        events, pol, masks, flows_all, images, persample, smooth = ctx.saved_tensors
-        dev = events.device
+        images, persample, smooth = ctx.saved_tensors[:3]
+        flows_c = list(ctx.saved_tensors[3:])
+        dev = images.device
         s = _lib.stream_ptr(dev)
         loss = torch.empty((), device=dev)
-        a = _fill_args(ctx.meta, events, pol, masks, flows_all, images, persample, smooth, loss, ctx.scr)
+        a = _fill_args(ctx.meta, ctx.windows, flows_c, images, persample, smooth, loss, ctx.scr)
         g = g.contiguous().float()
-        gimg = torch.empty_like(images)
-        g_flows = torch.empty_like(flows_all)
+        B, H, W = flows_c[0].shape[0], ctx.meta["H"], ctx.meta["W"]
+        gimg = torch.empty(8 * B * H * W, device=dev)
+        g_flows = torch.empty(B, len(flows_c), 2, H, W, device=dev)
         _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), s)
-        return (None, None, None, None, None, *g_flows.unbind(1))
+        return (None, None, None, *g_flows.unbind(1))
 
 
 class EventWarping(torch.nn.Module):
@@ -130,27 +145,27 @@ class EventWarping(torch.nn.Module):
 
     def forward(self):
         T = self._passes
-        events = torch.cat(self._events, dim=1)
-        pol = torch.cat(self._pols, dim=1)
         off = [0]
         for e in self._events:
             off.append(off[-1] + e.shape[1])
         H, W = int(self.res[0]), int(self.res[1])
         nflow = len(self._flows[0])
-        if self.overwrite_intermediate and self._final_flow is not None:
-            masks = self._overwritten_mask().reshape(events.shape[0], 1, H, W).contiguous()
+        overwrite = self.overwrite_intermediate and self._final_flow is not None
+        if overwrite:
+            masks = [self._overwritten_mask().reshape(-1, 1, H, W).contiguous()]
         else:
-            masks = torch.cat(self._masks, dim=1).reshape(events.shape[0], T, H, W).contiguous()
+            masks = [m.reshape(-1, 1, H, W).contiguous() for m in self._masks]
         meta = {"T": T, "H": H, "W": W, "off": off, "flow_scaling": self.flow_scaling, "weight": self.weight,
                 "smoothing_mask": self.smoothing_mask, "overwrite_intermediate": self.overwrite_intermediate,
                 "loss_scaling": self.loss_scaling}
+        windows = (list(self._events), list(self._pols), masks)
         losses = []
         for i in range(nflow):
-            if self.overwrite_intermediate and self._final_flow is not None:
+            if overwrite:
                 flows = [self._final_flow[i]]
             else:
                 flows = [fl[i] for fl in self._flows]
-            losses.append(EventWarpingFn.apply(meta, self._scratch, events, pol, masks, *flows))
+            losses.append(EventWarpingFn.apply(meta, self._scratch, windows, *flows))
         if nflow == 1:
             return losses[0]  # loss /= len(flow_list) with one flow map is the identity
         return sum(losses) / nflow
