@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 11
+#define SNNFLOW_ABI_VERSION 12
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -361,6 +361,41 @@ typedef struct snnflow_aee_args {
     float* aee; float* percent; /* out [B] */
 } snnflow_aee_args;
 int snnflow_aee(const snnflow_aee_args* a, void* stream);
+
+/* Every flow-vs-ground-truth metric of loss/flow.py in one pass over the pixels
+ * (flow' = flow*flow_scaling*dt_ratio[b], valid = event_mask && gt != (0,0)):
+ *   out[b][SNNFLOW_M_AEE], [_AEE_PCT]   AEE (:597-649): same as snnflow_aee
+ *   [_NEE], [_NEE_PCT]    NEE (:651-701): |f'-g| / (min(|f'|,|g|) + 0.01); outliers
+ *                         (masked error > 0.5) counted over the whole batch
+ *   [_AAE], [_AAE_PCT]    AAE (:703-762): acos(clamp((|f'||g|) / (f'.g + 0.01))) (the
+ *                         reference's formula); outliers (> pi/6) per sample
+ *   [_NAAE]               NAAE (:764-820): acos(clamp(f'.g / (|f'||g| + 1e-9))) / (|f'| + 1e-9)
+ *   [_AE_OF_MEANS]        AE_ofMeans (:822-883): angle between the masked means
+ *   [_AAE_WEIGHTED]       AAE_Weighted (:885-909): sum(ang*|f'|) over ALL pixels /
+ *                         (sum(|f'|*valid) + 1e-9) (the reference does not mask the numerator)
+ *   [_AAE_FILTERED]       AAE_Filtered (:911-937): mean ang over valid && |f'| >= mag_threshold
+ * Per-pixel terms are reduced per block into rows (scratch snnflow_flow_metrics_rows
+ * doubles) and summed in a fixed order: deterministic. */
+#define SNNFLOW_M_AEE 0
+#define SNNFLOW_M_AEE_PCT 1
+#define SNNFLOW_M_NEE 2
+#define SNNFLOW_M_NEE_PCT 3
+#define SNNFLOW_M_AAE 4
+#define SNNFLOW_M_AAE_PCT 5
+#define SNNFLOW_M_NAAE 6
+#define SNNFLOW_M_AE_OF_MEANS 7
+#define SNNFLOW_M_AAE_WEIGHTED 8
+#define SNNFLOW_M_AAE_FILTERED 9
+#define SNNFLOW_NUM_METRICS 10
+typedef struct snnflow_flow_metrics_args {
+    int B, H, W;
+    const float* flow; const float* gtflow; const float* event_mask; const float* dt_ratio;
+    float flow_scaling, mag_threshold;
+    double* rows;               /* scratch snnflow_flow_metrics_rows(B, H, W) doubles */
+    float* out;                 /* out [B][SNNFLOW_NUM_METRICS] */
+} snnflow_flow_metrics_args;
+int snnflow_flow_metrics(const snnflow_flow_metrics_args* a, void* stream);
+int snnflow_flow_metrics_rows(int B, int H, int W);
 
 /* HIP twin of the export op SNN_implementation::LIF (ONNX_LIF_operator/src/lif_op.cpp:8-56):
  * m' = beta[c]*mem + x; spk = m' >= thr[c]; mem_out = spk ? 0 : m'  (NCHW). */

@@ -103,6 +103,127 @@ __global__ void k_aee_finalize(snnflow_aee_args a) {
     a.percent[b] = (float)a.acc[2 * a.B] / (nvalid + 1e-9f);
 }
 
+// All flow metrics (snnflow.h, snnflow_flow_metrics): one row of FM_NV per-block sums per
+// (sample, chunk of NT pixels):
+//   0 nvalid  1 aee  2 aee outliers  3 nee  4 nee outliers  5 aae  6 aae outliers  7 naae
+//   8..11 masked sums of f'x, f'y, gx, gy   12 ang*|f'| (all pixels)  13 |f'|*valid
+//   14 ang * (valid && |f'| >= thr)  15 (valid && |f'| >= thr)
+constexpr int FM_NV = 16;
+constexpr float kClampLo = -1.0f + 1e-5f, kClampHi = 1.0f - 1e-5f;
+
+__global__ __launch_bounds__(NT) void k_flow_metrics(snnflow_flow_metrics_args a, int chunks) {
+    __shared__ float red[NT / 64][FM_NV];
+    const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
+    const int64_t HWp = (int64_t)a.H * a.W;
+    const int64_t p = (int64_t)chunk * NT + tid;
+    float v[FM_NV];
+#pragma unroll
+    for (int j = 0; j < FM_NV; ++j) v[j] = 0.0f;
+    if (p < HWp) {
+        const float r = a.dt_ratio[b];
+        const float* f = a.flow + (int64_t)b * 2 * HWp + p;
+        const float* g = a.gtflow + (int64_t)b * 2 * HWp + p;
+        const float fx = (f[0] * a.flow_scaling) * r, fy = (f[HWp] * a.flow_scaling) * r;
+        const float gx = g[0], gy = g[HWp];
+        const float fn = sqrtf(fx * fx + fy * fy), gn = sqrtf(gx * gx + gy * gy);
+        const float dx = fx - gx, dy = fy - gy;
+        const float e = sqrtf(dx * dx + dy * dy);
+        const bool valid = a.event_mask[(int64_t)b * HWp + p] != 0.0f && !(gx == 0.0f && gy == 0.0f);
+        const float mk = valid ? 1.0f : 0.0f;
+        const float dot = fx * gx + fy * gy;
+        // AEE (:609-649)
+        const float ae = e * mk;
+        v[0] = mk;
+        v[1] = ae;
+        v[2] = (ae > 3.0f && ae > 0.05f * (fn * mk)) ? 1.0f : 0.0f;
+        // NEE (:663-701)
+        const float ne = (e / (fminf(fn, gn) + 0.01f)) * mk;
+        v[3] = ne;
+        v[4] = ne > 0.5f ? 1.0f : 0.0f;
+        // AAE (:715-762), the reference's cosine formula
+        const float aa = acosf(fminf(fmaxf((fn * gn) / (dot + 0.01f), kClampLo), kClampHi)) * mk;
+        v[5] = aa;
+        v[6] = aa > (float)(3.14159265358979323846 / 6.0) ? 1.0f : 0.0f;
+        // angular error with the normalised cosine (NAAE, AAE_Weighted, AAE_Filtered)
+        const float ang = acosf(fminf(fmaxf(dot / (fn * gn + 1e-9f), kClampLo), kClampHi));
+        v[7] = (ang / (fn + 1e-9f)) * mk;
+        // AE_ofMeans (:835-883)
+        v[8] = fx * mk;
+        v[9] = fy * mk;
+        v[10] = gx * mk;
+        v[11] = gy * mk;
+        // AAE_Weighted (:888-909): numerator over every pixel
+        v[12] = ang * fn;
+        v[13] = fn * mk;
+        // AAE_Filtered (:917-937)
+        const float mf = (valid && fn >= a.mag_threshold) ? 1.0f : 0.0f;
+        v[14] = ang * mf;
+        v[15] = mf;
+    }
+    const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+    for (int j = 0; j < FM_NV; ++j) {
+        const float s = wave_total(v[j]);
+        if (lane == 0) red[wv][j] = s;
+    }
+    __syncthreads();
+    if (tid < FM_NV) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) t += (double)red[w][tid];
+        a.rows[(int64_t)blockIdx.x * FM_NV + tid] = t;
+    }
+}
+
+// Fixed-order reduction of the rows: wave w owns samples w, w + 4, ...; then the metrics.
+__global__ __launch_bounds__(NT) void k_flow_metrics_finalize(snnflow_flow_metrics_args a, int chunks) {
+    __shared__ double sums[NT][FM_NV];  // B <= NT (host check)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int b = wv; b < a.B; b += NT / 64) {
+        double s[FM_NV];
+#pragma unroll
+        for (int j = 0; j < FM_NV; ++j) s[j] = 0.0;
+        const double* r = a.rows + (int64_t)b * chunks * FM_NV;
+#pragma unroll 2
+        for (int c = lane; c < chunks; c += 64) {
+#pragma unroll
+            for (int j = 0; j < FM_NV; ++j) s[j] += r[(int64_t)c * FM_NV + j];
+        }
+#pragma unroll
+        for (int j = 0; j < FM_NV; ++j) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) s[j] += __shfl_xor(s[j], off, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < FM_NV; ++j) sums[b][j] = s[j];
+        }
+    }
+    __syncthreads();
+    const int b = threadIdx.x;
+    if (b >= a.B) return;
+    double aee_out = 0.0, nee_out = 0.0;  // the reference counts these over the whole batch
+    for (int bb = 0; bb < a.B; ++bb) {
+        aee_out += sums[bb][2];
+        nee_out += sums[bb][4];
+    }
+    const double* s = sums[b];
+    const float nv = (float)s[0], den = nv + 1e-9f;
+    float* o = a.out + (int64_t)b * SNNFLOW_NUM_METRICS;
+    o[SNNFLOW_M_AEE] = (float)s[1] / den;
+    o[SNNFLOW_M_AEE_PCT] = (float)aee_out / den;
+    o[SNNFLOW_M_NEE] = (float)s[3] / den;
+    o[SNNFLOW_M_NEE_PCT] = (float)nee_out / den;
+    o[SNNFLOW_M_AAE] = (float)s[5] / den;
+    o[SNNFLOW_M_AAE_PCT] = (float)s[6] / den;
+    o[SNNFLOW_M_NAAE] = (float)s[7] / den;
+    const float mfx = (float)s[8] / den, mfy = (float)s[9] / den, mgx = (float)s[10] / den, mgy = (float)s[11] / den;
+    const float mfn = sqrtf(mfx * mfx + mfy * mfy), mgn = sqrtf(mgx * mgx + mgy * mgy);
+    o[SNNFLOW_M_AE_OF_MEANS] = acosf(fminf(fmaxf((mfx * mgx + mfy * mgy) / (mfn * mgn + 1e-9f), kClampLo), kClampHi));
+    o[SNNFLOW_M_AAE_WEIGHTED] = (float)s[12] / ((float)s[13] + 1e-9f);
+    o[SNNFLOW_M_AAE_FILTERED] = (float)s[14] / ((float)s[15] + 1e-9f);
+}
+
 __global__ void k_zero_f64(double* p, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
 }
@@ -138,6 +259,22 @@ int snnflow_aee(const snnflow_aee_args* a, void* stream) {
     const int chunks = (int)(((int64_t)a->H * a->W + NT - 1) / NT);
     hipLaunchKernelGGL(k_aee, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
     hipLaunchKernelGGL(k_aee_finalize, dim3(1), dim3(NT), 0, s, *a);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_flow_metrics_rows(int B, int H, int W) {
+    return (int)((int64_t)B * (((int64_t)H * W + NT - 1) / NT) * FM_NV);
+}
+
+int snnflow_flow_metrics(const snnflow_flow_metrics_args* a, void* stream) {
+    if (!a || a->B <= 0 || a->B > NT || a->H <= 0 || a->W <= 0 || !a->flow || !a->gtflow || !a->event_mask ||
+        !a->dt_ratio || !a->rows || !a->out)
+        SNN_FAIL(SNNFLOW_E_ARG, "flow_metrics: bad args");
+    const hipStream_t s = (hipStream_t)stream;
+    const int chunks = (int)(((int64_t)a->H * a->W + NT - 1) / NT);
+    hipLaunchKernelGGL(k_flow_metrics, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
+    hipLaunchKernelGGL(k_flow_metrics_finalize, dim3(1), dim3(NT), 0, s, *a, chunks);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -9,8 +9,9 @@ from .cells import ConvLayer, Leaky, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
 from .convlif import ConvLIF, ConvLIFRecurrent
 from . import encodings  # noqa: F401  (on-device event encodings)
 from .loss import EventWarping
-from .metrics import AEE
+from .metrics import AAE, AAE_Filtered, AAE_Weighted, AE_ofMeans, AEE, NAAE, NEE
 from .model import LIFFireFlowNet, LIFFireFlowNet_short, LIFFireNet, LIFFireNet_short
 
 __all__ = ["LIFFireNet", "LIFFireNet_short", "LIFFireFlowNet", "LIFFireFlowNet_short", "SNNtorch_ConvLIF",
-           "SNNtorch_ConvLIFRecurrent", "ConvLIF", "ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping", "AEE"]
+           "SNNtorch_ConvLIFRecurrent", "ConvLIF", "ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping", "AEE",
+           "NEE", "AAE", "NAAE", "AE_ofMeans", "AAE_Weighted", "AAE_Filtered"]

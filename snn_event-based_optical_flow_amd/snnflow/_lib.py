@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class Neuron(ctypes.Structure):
@@ -115,6 +115,15 @@ class AeeArgs(ctypes.Structure):
                 ("dt_ratio", P), ("flow_scaling", F32), ("acc", P), ("aee", P), ("percent", P)]
 
 
+class FlowMetricsArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("flow", P), ("gtflow", P), ("event_mask", P),
+                ("dt_ratio", P), ("flow_scaling", F32), ("mag_threshold", F32), ("rows", P), ("out", P)]
+
+
+# SNNFLOW_M_* output columns of snnflow_flow_metrics
+METRICS = ("aee", "aee_pct", "nee", "nee_pct", "aae", "aae_pct", "naae", "ae_of_means", "aae_weighted",
+           "aae_filtered")
+
 ACC_SHARDS = 32  # SNNFLOW_ACC_SHARDS
 
 
@@ -167,6 +176,8 @@ EXPORTS = {
     "snnflow_encode_events": (I32, [ctypes.POINTER(EncodeArgs), P]),
     "snnflow_pol_iwe": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
     "snnflow_aee": (I32, [ctypes.POINTER(AeeArgs), P]),
+    "snnflow_flow_metrics": (I32, [ctypes.POINTER(FlowMetricsArgs), P]),
+    "snnflow_flow_metrics_rows": (I32, [I32, I32, I32]),
     "snnflow_convlif_bwd": (I32, [ctypes.POINTER(ConvLifBwdArgs), P]),
     "snnflow_convlif_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),

@@ -1,8 +1,13 @@
-"""Validation metrics with the reference's API (``loss/flow.py:306-649``: BaseValidationLoss,
-AEE), the evaluation counterpart of the training loss.
+"""Validation metrics with the reference's API (``loss/flow.py:306-937``: BaseValidationLoss,
+AEE, NEE, AAE, NAAE, AE_ofMeans, AAE_Weighted, AAE_Filtered), the evaluation counterpart of
+the training loss.
 
 ``AEE.forward`` runs the HIP kernels of csrc/eval.hip (per-pixel endpoint error,
-validity, outliers, per-sample reduction).  The association bookkeeping is the
+validity, outliers, per-sample reduction); the other metrics share one pass
+(``snnflow_flow_metrics``: every per-pixel term of every metric, per-block rows, a
+fixed-order reduction), each class returning its own columns with the reference's
+formulas and quirks (AAE's inverted cosine, batch-total outlier counts of AEE/NEE,
+the unmasked numerator of AAE_Weighted).  The association bookkeeping is the
 reference's (last flow map, event masks, ground truth, time scaling).  Error heatmap
 accumulation for visualisation (``accumulate_error_heatmap`` and friends) is not part of
 this path; ``get_error_map`` returns None.
@@ -109,3 +114,90 @@ class AEE(BaseValidationLoss):
         a.acc, a.aee, a.percent = ptr(acc), ptr(aee), ptr(pct)
         _lib.call("aee", lib.snnflow_aee, ctypes.byref(a), _lib.stream_ptr(flow.device))
         return aee, pct
+
+
+def _flow_metrics(m, mag_threshold=0.5):
+    """All SNNFLOW_M_* columns for the current association state of metric object m."""
+    flow = m._flow_map[-1].float().contiguous()
+    B, _, H, W = flow.shape
+    gt = m._gtflow.float().contiguous()
+    mask = m._event_mask[:, -1, :, :].float().contiguous()
+    ratio = torch.as_tensor(m._dt_gt, dtype=torch.float32, device=flow.device) / torch.as_tensor(
+        m._dt_input, dtype=torch.float32, device=flow.device)
+    ratio = ratio.reshape(-1).expand(B).contiguous() if ratio.numel() == 1 else ratio.reshape(B).contiguous()
+    rows = torch.empty(lib.snnflow_flow_metrics_rows(B, H, W), dtype=torch.float64, device=flow.device)
+    out = torch.empty(B, len(_lib.METRICS), device=flow.device)
+    a = _lib.FlowMetricsArgs()
+    a.B, a.H, a.W = B, H, W
+    a.flow, a.gtflow, a.event_mask, a.dt_ratio = ptr(flow), ptr(gt), ptr(mask), ptr(ratio)
+    a.flow_scaling, a.mag_threshold = float(m.flow_scaling), float(mag_threshold)
+    a.rows, a.out = ptr(rows), ptr(out)
+    _lib.call("flow_metrics", lib.snnflow_flow_metrics, ctypes.byref(a), _lib.stream_ptr(flow.device))
+    return {k: out[:, i] for i, k in enumerate(_lib.METRICS)}
+
+
+class NEE(BaseValidationLoss):
+    """``loss/flow.py:651-701``: normalised endpoint error |f-g| / (min(|f|,|g|) + 0.01) and
+    the share of outliers (> 0.5), the latter counted over the whole batch as the reference does."""
+
+    @property
+    def num_events(self):
+        return float("inf")
+
+    def forward(self):
+        r = _flow_metrics(self)
+        return r["nee"], r["nee_pct"]
+
+
+class AAE(BaseValidationLoss):
+    """``loss/flow.py:703-762``: angular error with the reference's cosine
+    (|f||g| / (f.g + 0.01), clamped) and the per-sample share of errors above pi/6."""
+
+    @property
+    def num_events(self):
+        return float("inf")
+
+    def forward(self):
+        r = _flow_metrics(self)
+        return r["aae"], r["aae_pct"]
+
+
+class NAAE(BaseValidationLoss):
+    """``loss/flow.py:764-820``: angular error divided by the predicted flow magnitude."""
+
+    @property
+    def num_events(self):
+        return float("inf")
+
+    def forward(self):
+        return _flow_metrics(self)["naae"]
+
+
+class AE_ofMeans(BaseValidationLoss):
+    """``loss/flow.py:822-883``: angle between the masked mean flow and mean ground truth."""
+
+    @property
+    def num_events(self):
+        return float("inf")
+
+    def forward(self):
+        return _flow_metrics(self)["ae_of_means"]
+
+
+class AAE_Weighted(BaseValidationLoss):
+    """``loss/flow.py:885-909``: magnitude-weighted angular error (numerator over all pixels,
+    as in the reference)."""
+
+    def forward(self):
+        return _flow_metrics(self)["aae_weighted"]
+
+
+class AAE_Filtered(BaseValidationLoss):
+    """``loss/flow.py:911-937``: angular error over valid pixels with |f| >= mag_threshold."""
+
+    def __init__(self, config, device, flow_scaling=128, mag_threshold=0.5):
+        super().__init__(config, device, flow_scaling)
+        self.mag_threshold = mag_threshold
+
+    def forward(self):
+        return _flow_metrics(self, self.mag_threshold)["aae_filtered"]

@@ -280,6 +280,19 @@ def eval_case(ref_flow, ref_iwe, out):
         aee.event_flow_association([flow], {"event_list": ev, "event_list_pol_mask": pol, "event_mask": mask,
                                             "gtflow": gt, "dt_input": dt_in, "dt_gt": dt_gt})
         v, pct = aee()
+        # the other flow metrics of loss/flow.py on the same association (no randomness drawn)
+        for name in ("NEE", "AAE", "NAAE", "AE_ofMeans", "AAE_Weighted", "AAE_Filtered"):
+            mobj = getattr(ref_flow, name)(cfg, "cpu", flow_scaling=128)
+            mobj.event_flow_association([flow], {"event_list": ev, "event_list_pol_mask": pol, "event_mask": mask,
+                                                 "gtflow": gt, "dt_input": dt_in, "dt_gt": dt_gt})
+            try:
+                res = mobj()
+            except RuntimeError as err:  # NEE broadcasts [B,H,W] / [B,1,H,W]: the reference raises for B > 1
+                print(f"reference {name} fails for B={B}: {err}")
+                continue
+            res = res if isinstance(res, tuple) else (res,)
+            for j, r in enumerate(res):
+                rec[f"b{B}_{name}_{j}"] = r.detach().reshape(-1).numpy()
         rec.update({f"b{B}_flow": flow.numpy(), f"b{B}_gt": gt.numpy(), f"b{B}_mask": mask.numpy(),
                     f"b{B}_ev": ev.numpy(), f"b{B}_pol": pol.numpy(), f"b{B}_dt_in": dt_in.numpy(),
                     f"b{B}_dt_gt": dt_gt.numpy(), f"b{B}_aee": v.numpy(), f"b{B}_pct": pct.numpy()})

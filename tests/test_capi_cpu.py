@@ -39,6 +39,7 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_slab_desc": _lib.SlabDesc, "snnflow_prep_desc": _lib.PrepDesc,
         "snnflow_wgrad_step": _lib.WgradStep, "snnflow_aee_args": _lib.AeeArgs, "snnflow_encode_args": _lib.EncodeArgs, "snnflow_convlif_params": _lib.ConvLifParams,
         "snnflow_convlif_fwd_args": _lib.ConvLifFwdArgs, "snnflow_convlif_bwd_args": _lib.ConvLifBwdArgs, "snnflow_wgrad_args": _lib.WgradArgs, "snnflow_iwe_loss_args": _lib.IweLossArgs,
+        "snnflow_flow_metrics_args": _lib.FlowMetricsArgs,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
