@@ -7,7 +7,7 @@ Drop-in for the reference's ``models.model`` (LIFFireNet family), its spiking ce
 from . import _lib  # noqa: F401  (loads libsnnflow.so or raises)
 from .cells import ConvLayer, Leaky, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
 from .convlif import ConvLIF, ConvLIFRecurrent
-from . import encodings  # noqa: F401  (on-device event encodings)
+from . import checkpoint, encodings  # noqa: F401  (checkpoint interchange, on-device event encodings)
 from .loss import EventWarping
 from .metrics import AAE, AAE_Filtered, AAE_Weighted, AE_ofMeans, AEE, NAAE, NEE
 from .model import LIFFireFlowNet, LIFFireFlowNet_short, LIFFireNet, LIFFireNet_short
