@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=3, help="distinct synthetic batches cycled in HBM")
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsals)")
     return p.parse_args()
 
 
@@ -93,10 +94,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("SNNFLOW_SHARE_GPU") == "1":  # rehearsal: several ranks on one device (gloo)
+        local = local % torch.cuda.device_count()
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(args.dist_backend, init_method="env://")
     dev = torch.device("cuda", local)
 
     import snnflow
