@@ -228,6 +228,9 @@ __global__ void k_prep_weights(DescBatch<snnflow_prep_desc> batch) {
 // The C x C conv layers (C = 8, 16, 32) run their convolutions on the matrix cores.
 template <int CIN, int C>
 constexpr bool kMfma = CIN == C && C % 8 == 0;
+// ... with their weights staged in LDS up to C = 16 (C = 32: 36 KB per conv, read from L2)
+template <int CIN, int C>
+constexpr bool kWlds = kMfma<CIN, C> && C <= 16;
 
 // LIF of one float4 of channels [4q, 4q+4) (coefficients from LDS).
 struct Lif4 { float4 s, mout; };
@@ -263,7 +266,17 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
     [[maybe_unused]] constexpr int TK = REC ? 1 : 0;
     TRACE_AT(TR, TK, 0);
 
-    // 1. issue every global load of the tile before any use
+    // 1. issue every global load of the tile before any use (weights for LDS first)
+    constexpr bool WL = kWlds<CIN, C>;
+    __shared__ __attribute__((aligned(16))) float wl_ff[WL ? 9 * C * C : 4];
+    __shared__ __attribute__((aligned(16))) float wl_rec[WL && REC ? 9 * C * C : 4];
+    WStage<WL ? 9 * C * C : 1, NTB> sw_ff, sw_rec;
+    if constexpr (WL) {
+        sw_ff.load(a.wt_ff_t);
+        if constexpr (REC) {
+            if (has_rec) sw_rec.load(a.wt_rec_t);
+        }
+    }
     float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
     if constexpr (PF_REC) {
         if (has_rec) halo_load<C, NTB>(a.s_prev, tl, H, W, rs);
@@ -275,11 +288,13 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         if (a.prev_mem) halo_load<CIN, NTB>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
         const NeuronRegs nr = load_neuron(a.prev, CIN);
-        zero_consumed(a.zero0, a.zero1, a.zero_n);
         __shared__ double sums[2 * CIN];
         if (a.prev.bn_train) acc_gather<2 * CIN>(a.prev_acc, 2 * CIN, sums);
         lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
         __syncthreads();
+        // (stores issued after the gather: CDNA's vmcnt counts stores, so zeroing before the
+        // gather made its wait include the store acknowledgements)
+        zero_consumed(a.zero0, a.zero1, a.zero_n);
         TRACE_AT(TR, TK, 1);
         // 2. LIF of the previous layer over the halo; interior pixels also write its state
         const bool zr = a.prev.zero_reset != 0;
@@ -306,11 +321,26 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
             }
         }
     } else {
-        zero_consumed(a.zero0, a.zero1, a.zero_n);
         stage_strided<CIN, NTB>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, tile);
+        zero_consumed(a.zero0, a.zero1, a.zero_n);
     }
+    if constexpr (WL) {
+        sw_ff.store(wl_ff);
+        if constexpr (REC) {
+            if (has_rec) sw_rec.store(wl_rec);
+        }
+    }
+    // previous-step spikes exact in bf16 (0/1; always so on the engine path) -> bf16 MFMA
+    bool rec_bf = false;
     if constexpr (PF_REC) {
-        if (has_rec) halo_store<C, NTB>(rtile, rs);
+        if (has_rec) {
+            halo_store<C, NTB>(rtile, rs);
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < Halo4<C, NTB>::R; ++i)
+                ok = ok && exact_bf16(rs[i].x) && exact_bf16(rs[i].y) && exact_bf16(rs[i].z) && exact_bf16(rs[i].w);
+            rec_bf = __syncthreads_and(ok) != 0;
+        }
     }
     __syncthreads();
     TRACE_AT(TR, TK, 2);
@@ -322,7 +352,11 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         constexpr int NW = NTB / 64;
         MfmaAcc<C, C, NW> af, ar;
         af.zero();
-        if (!PROBE_OFF(16)) mfma_conv3x3<C, C, false, NW>(tile, a.wt_ff_t, af);
+        if (!PROBE_OFF(16)) {
+            const float* wf = WL ? wl_ff : a.wt_ff_t;
+            if constexpr (LIF_IN) mfma_conv3x3_bf3<C, C, NW>(tile, wf, af);  // spikes of layer l-1
+            else mfma_conv3x3<C, C, false, NW>(tile, wf, af);
+        }
         bool rec_on = false;
         if constexpr (REC) {
             if (has_rec) {
@@ -336,7 +370,11 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
                     __syncthreads();
                 }
                 ar.zero();
-                if (!PROBE_OFF(16)) mfma_conv3x3<C, C, false, NW>(rt, a.wt_rec_t, ar);
+                if (!PROBE_OFF(16)) {
+                    const float* wr = WL ? wl_rec : a.wt_rec_t;
+                    if (rec_bf) mfma_conv3x3_bf3<C, C, NW>(rt, wr, ar);
+                    else mfma_conv3x3<C, C, false, NW>(rt, wr, ar);
+                }
             }
         }
         __syncthreads();
@@ -419,11 +457,11 @@ __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
         mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
     }
     const NeuronRegs nr = load_neuron(a.n, C);
-    zero_consumed(a.zero0, a.zero1, a.zero_n);
     __shared__ double sums[2 * C];
     if (a.n.bn_train) acc_gather<2 * C>(a.acc, 2 * C, sums);
     lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr);
     __syncthreads();
+    zero_consumed(a.zero0, a.zero1, a.zero_n);  // after the gather (vmcnt counts stores)
     if (!act) return;
     const bool zr = a.n.zero_reset != 0;
     float4* st4 = reinterpret_cast<float4*>(a.state);
@@ -486,7 +524,6 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
             }
         }
     }
-    zero_consumed(a.zero0, a.zero1, a.zero_n);
     if (tid < C) {
         coef[tid] = lif_coef(a.n, a.stats, C, tid);
         meanv[tid] = a.stats[tid];
@@ -541,6 +578,7 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
         }
     }
     if (!PROBE_OFF(4)) block_atomic_sum<NV>(v, acc_shard(a.acc, SNNFLOW_BWD_ACC(C)));
+    zero_consumed(a.zero0, a.zero1, a.zero_n);  // last: no load waits behind these stores
 }
 
 // BatchNorm backward of one float4 of channels (torch batch_norm_cpu_backward, train):
@@ -588,7 +626,17 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     [[maybe_unused]] constexpr int TK = REC ? 3 : 2;
     TRACE_AT(TR, TK, 0);
 
-    // 1. every global load of the kernel, issued up front (register prefetch)
+    // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS)
+    constexpr bool WL = kWlds<CIN, C>;
+    __shared__ __attribute__((aligned(16))) float wl_x[WL ? 9 * C * C : 4];
+    __shared__ __attribute__((aligned(16))) float wl_r[WL && REC ? 9 * C * C : 4];
+    WStage<WL ? 9 * C * C : 1, NTB> sw_x, sw_r;
+    if constexpr (WL) {
+        if (a.wt_bwd_ff) sw_x.load(a.wt_fwd_ff);
+        if constexpr (REC) {
+            if (a.g_state_prev) sw_r.load(a.wt_fwd_rec);
+        }
+    }
     float4 rg[PF ? Halo4<C, NTB>::R : 1], ry[PF ? Halo4<C, NTB>::R : 1];
     float4 dy[LIF_IN ? QI : 1], dm[LIF_IN ? QI : 1], dg[LIF_IN ? QI : 1];
     if constexpr (PF) {
@@ -632,7 +680,6 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
 
     // 2. per-channel constants; block 0 finishes layer l's neuron gradients and stores the
     //    BN backward coefficients for the deferred weight gradient
-    zero_consumed(a.zero0, a.zero1, a.zero_n);
     __shared__ double sums[SNNFLOW_BWD_ACC(C)];
     acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
     neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b);
@@ -664,6 +711,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     }
     __syncthreads();
     TRACE_AT(TR, TK, 1);
+    zero_consumed(a.zero0, a.zero1, a.zero_n);  // after the gather (vmcnt counts stores)
 
     // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l)
     if constexpr (PF) {
@@ -690,6 +738,12 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
             *reinterpret_cast<float4*>(G + p * PC + 4 * q) = out;
         }
     }
+    if constexpr (WL) {
+        if (a.wt_bwd_ff) sw_x.store(wl_x);
+        if constexpr (REC) {
+            if (a.g_state_prev) sw_r.store(wl_r);
+        }
+    }
     __syncthreads();
     TRACE_AT(TR, TK, 2);
 
@@ -707,12 +761,12 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
         MfmaAcc<C, C, NW> arr;
         if (do_x) {
             ax.zero();
-            if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, a.wt_fwd_ff, ax);
+            if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, WL ? wl_x : a.wt_fwd_ff, ax);
         }
         if constexpr (REC) {
             if (do_r) {
                 arr.zero();
-                if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, a.wt_fwd_rec, arr);
+                if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, WL ? wl_r : a.wt_fwd_rec, arr);
             }
         }
         __syncthreads();

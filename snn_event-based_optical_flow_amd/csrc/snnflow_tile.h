@@ -227,6 +227,143 @@ __device__ void mfma_conv3x3(const float* src, const float* __restrict__ wB, Mfm
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same implicit GEMM on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16, 16x the f32
+// rate) for inputs that are exact in bf16 -- spikes (0/1) -- with the f32 weights split
+// w = hi + mid + lo into three bf16 parts (round-to-nearest; the residuals are exact in
+// f32, so the parts carry all 24 mantissa bits).  Every product x*part is exact in f32 and
+// accumulates in f32: the result equals the f32 conv up to summation order.
+// K = (tap, channel) in chunks of 32: lane group g = lane >> 4 supplies 8 consecutive
+// channels of one tap (A: 8 floats of its pixel from LDS; B: 8 weights [tap][n][c0..c0+7]).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int KIN, int NOUT>
+struct Bf3Geo {
+    static_assert(KIN % 8 == 0 && (KIN <= 32 ? 32 % KIN == 0 : KIN % 32 == 0), "bf16 conv: KIN 8, 16, 32, 64..");
+    static constexpr int GPT = KIN / 8;                   // lane groups per tap
+    static constexpr int TPI = GPT >= 4 ? 1 : 4 / GPT;    // taps per instruction
+    static constexpr int IPT = GPT >= 4 ? GPT / 4 : 1;    // instructions per tap
+    static constexpr int NI = ((9 + TPI - 1) / TPI) * IPT;  // K chunks of 32
+    static constexpr int NNT = (NOUT + 15) / 16;
+};
+
+// tap and first channel of lane group g in K chunk i (tap >= 9: padding)
+template <int KIN>
+__device__ inline void bf3_k(int i, int g, int& tap, int& c0) {
+    using G = Bf3Geo<KIN, 16>;
+    if constexpr (G::GPT >= 4) {
+        tap = i / G::IPT;
+        c0 = ((i % G::IPT) * 4 + g) * 8;
+    } else {
+        tap = i * G::TPI + g / G::GPT;
+        c0 = (g % G::GPT) * 8;
+    }
+}
+
+__device__ inline bool exact_bf16(float v) { return v == (float)(__bf16)v; }
+
+template <int KIN, int NOUT>
+__device__ inline void bf3_load_b(const float* __restrict__ wB, int i, float (&w)[Bf3Geo<KIN, NOUT>::NNT][8]) {
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    int tap, c0;
+    bf3_k<KIN>(i, g, tap, c0);
+#pragma unroll
+    for (int nt = 0; nt < Bf3Geo<KIN, NOUT>::NNT; ++nt) {
+        const int n = nt * 16 + m;
+        if (tap < 9 && n < NOUT) {
+            const float* p = wB + (int64_t)(tap * NOUT + n) * KIN + c0;
+            const float4 u = *reinterpret_cast<const float4*>(p), v = *reinterpret_cast<const float4*>(p + 4);
+            w[nt][0] = u.x; w[nt][1] = u.y; w[nt][2] = u.z; w[nt][3] = u.w;
+            w[nt][4] = v.x; w[nt][5] = v.y; w[nt][6] = v.z; w[nt][7] = v.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) w[nt][j] = 0.0f;
+        }
+    }
+}
+
+template <int KIN, int NOUT, int NW>
+__device__ void mfma_conv3x3_bf3(const float* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW>& acc) {
+    using G = Bf3Geo<KIN, NOUT>;
+    static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
+    static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
+    constexpr int P = Pad<KIN>::v, MT = 16 / NW;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    float wc[G::NNT][8], wn[G::NNT][8];
+    bf3_load_b<KIN, NOUT>(wB, 0, wc);
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+        if (i + 1 < G::NI) bf3_load_b<KIN, NOUT>(wB, i + 1, wn);  // next chunk's weights in flight
+        bf16x8 bh[G::NNT], bm[G::NNT], bl[G::NNT];
+#pragma unroll
+        for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float w = wc[nt][j];
+                const __bf16 h = (__bf16)w;
+                const float r1 = w - (float)h;
+                const __bf16 md = (__bf16)r1;
+                bh[nt][j] = h;
+                bm[nt][j] = md;
+                bl[nt][j] = (__bf16)(r1 - (float)md);
+            }
+        int tap, c0;
+        bf3_k<KIN>(i, g, tap, c0);
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            bf16x8 a;
+            if (tap < 9) {
+                const float* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
+                const float4 u = *reinterpret_cast<const float4*>(ap), v = *reinterpret_cast<const float4*>(ap + 4);
+                a[0] = (__bf16)u.x; a[1] = (__bf16)u.y; a[2] = (__bf16)u.z; a[3] = (__bf16)u.w;
+                a[4] = (__bf16)v.x; a[5] = (__bf16)v.y; a[6] = (__bf16)v.z; a[7] = (__bf16)v.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
+            }
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt) {
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl[nt], acc.v[mt][nt], 0, 0, 0);
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[nt], acc.v[mt][nt], 0, 0, 0);
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[nt], acc.v[mt][nt], 0, 0, 0);
+            }
+        }
+        if (i + 1 < G::NI) {
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) wc[nt][j] = wn[nt][j];
+        }
+    }
+}
+
+// A weight tensor of N floats staged into LDS by the whole block: the loads are issued into
+// registers at kernel start (load) and written to LDS before a later barrier (store), so
+// the matrix-core loops read their B operands from LDS and never wait on global memory.
+template <int N, int NTH>
+struct WStage {
+    static constexpr int R = (N + NTH - 1) / NTH;
+    float r[R];
+    __device__ inline void load(const float* __restrict__ w) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = (int)threadIdx.x + i * NTH;
+            r[i] = (e < N) ? w[e] : 0.0f;
+        }
+    }
+    __device__ inline void store(float* lds) const {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = (int)threadIdx.x + i * NTH;
+            if (e < N) lds[e] = r[i];
+        }
+    }
+};
+
 // Accumulators (C/D layout: lane holds pixels 4g..4g+3 of its M-tile, channel n = lane & 15)
 // [+ a second set added element-wise when SUM: ff + rec] -> LDS out[NT][Pad<NOUT>].
 template <bool SUM, int KIN, int NOUT, int NW, int KIN2>
