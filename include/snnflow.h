@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 12
+#define SNNFLOW_ABI_VERSION 13
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -210,6 +210,8 @@ typedef struct snnflow_wgrad_step {
 #define SNNFLOW_MAX_WGRAD_STEPS 32
 typedef struct snnflow_wgrad_args {
     int B, H, W, cin, c, nsteps, accumulate, rec;
+    int exact_inputs;           /* 1: every x and s_prev value is exact in bf16 (spikes):
+                                   cin == c layers then run on the bf16 matrix cores */
     const float* bn_weight;     /* [c] gamma (ignored without stats) */
     float* slab_ff;             /* snnflow_conv_blocks() x c*cin*9 */
     float* slab_rec;            /* snnflow_conv_blocks() x c*c*9 (rec layers) */

@@ -1004,7 +1004,7 @@ struct WgradMfma {
     __device__ void step(const float* Gi, const float* X, const float* S, bool has_s) {
         constexpr int PC = Pad<C>::v, PX = Pad<CIN>::v;
         const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
-#pragma unroll 2
+#pragma unroll 8
         for (int s = 0; s < NT / 4; ++s) {
             const int p = 4 * s + g, ty = p / TW, tx = p - ty * TW;
             const int hb = ty * HWD + tx;
@@ -1181,6 +1181,260 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
     } else {
         af.flush(ap->slab_ff + blk * (C * CIN * 9), ap->accumulate, scratch);
         if constexpr (REC) ar.flush(ap->slab_rec + blk * (C * C * 9), ap->accumulate, scratch);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradients of the C x C layers on the bf16 matrix cores (snnflow_wgrad with
+// exact_inputs: the conv inputs -- spikes -- are exact in bf16).  Per tap,
+//   dW_tap[co][ci] = sum_p G[p][co] * X[p + tap][ci]
+// as v_mfma_f32_16x16x32_bf16 with M = co (A = G^T split into three bf16 parts, so the
+// products are the exact f32 products), N = ci (B = X, exact), K = the 32 pixels of one tile
+// row (lane group g: pixels 8g..8g+7).  LDS holds G^T [C][260] f32 and X^T / S^T
+// [C][10][40] bf16 (channel-major, padded: conflict-free 16-B reads); one 12-element read
+// of a halo row gives the B operands of all three kx taps by register shifts.  The output
+// tiles (src, ci-tile, ky) x (kx, co-tile) are split over TG wave groups, the 8 tile rows
+// over RG = 8 / TG row groups; row groups are summed through LDS in a fixed order at the
+// end (deterministic), then one slab write per block.
+// ---------------------------------------------------------------------------
+template <int C, bool REC>
+struct WbGeo {
+    static constexpr int MTc = (C + 15) / 16, NTc = (C + 15) / 16;
+    static constexpr int BROWS = (REC ? 2 : 1) * NTc * 3;  // (src, ci-tile, ky)
+    static constexpr int TPB = 3 * MTc;                     // tiles per B-row: (kx, co-tile)
+    static constexpr int NTOT = BROWS * TPB;
+    static constexpr int TG = NTOT <= 18 ? 1 : (NTOT <= 36 ? 2 : 4);
+    static constexpr int RG = 8 / TG;
+    static constexpr int BRW = BROWS / TG;                  // B-rows per wave
+    static constexpr int TPW = BRW * TPB;                   // accumulator tiles per wave
+    static_assert(BROWS % TG == 0, "B-rows split evenly over the wave groups");
+    static constexpr int GS = NT + 4;                       // G^T channel stride (floats)
+    static constexpr int XS = 10 * 40 + 8;                  // X^T channel stride (bf16)
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int C, bool REC>
+__global__ __launch_bounds__(NT * 2) void k_wgrad_bf(snnflow_wgrad_args) {
+    using Gm = WbGeo<C, REC>;
+    constexpr int NTB = NT * 2, NW = NTB / 64, Q = C / 4;
+    constexpr int RX = Halo4<C, NTB>::R;
+    using O = Own4<C, NTB>;
+    static_assert(NW == 8, "8 waves");
+    __shared__ __attribute__((aligned(16))) float Gt[C * Gm::GS];
+    __shared__ __attribute__((aligned(16))) unsigned short Xt[C * Gm::XS];
+    __shared__ __attribute__((aligned(16))) unsigned short St[REC ? C * Gm::XS : 8];
+    __shared__ BnBwdLds coef[SNNFLOW_MAX_WGRAD_STEPS][C];
+
+    const cwgrad_ptr ap = (cwgrad_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+    const int tid = threadIdx.x, lane = tid & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), tg = wv % Gm::TG, rg = wv / Gm::TG;
+    const int H = ap->H, W = ap->W, nsteps = ap->nsteps;
+    const Tile tl = block_tile(H, W);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    for (int e = tid; e < nsteps * C; e += NTB) {
+        const int t = e / C, c = e - t * C;
+        const float* st = ap->steps[t].stats;
+        const float* bc = ap->steps[t].bnc;
+        BnBwdLds k = {0.f, 1.f, 0.f, 0.f, 1.f};
+        if (st) {
+            k.mean = st[c];
+            k.inv = st[C + c];
+            k.gm = bc[c];
+            k.k = bc[C + c];
+            k.w = ap->bn_weight[c];
+        }
+        coef[t][c] = k;
+    }
+
+    float4 rg4[O::R], ry4[O::R], rx[RX], rs[REC ? RX : 1];
+    bool dense = false, has_s = false;
+    auto issue = [&](int t) {
+        const float* gp = ap->steps[t].g_cur;
+        const float* yp = ap->steps[t].y;
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            const int p = e / Q, q = e - p * Q;
+            const int ty = p / TW, tx = p - ty * TW;
+            const int h = tl.h0 + ty, w = tl.w0 + tx;
+            const bool ok = e < O::E && h < H && w < W;
+            const int64_t k = ok ? (((int64_t)tl.b * H + h) * W + w) * Q + q : 0;
+            rg4[i] = ok ? reinterpret_cast<const float4*>(gp)[k] : z4;
+            ry4[i] = ok ? reinterpret_cast<const float4*>(yp)[k] : z4;
+        }
+        const auto& sp = ap->steps[t];
+        dense = sp.xs_c == 1 && sp.xs_w == C && sp.xs_h == (int64_t)W * C && sp.xs_b == (int64_t)H * W * C;
+        if (dense) halo_load<C, NTB>(sp.x, tl, H, W, rx);
+        has_s = REC && sp.s_prev != nullptr;
+        if constexpr (REC) {
+            if (has_s) halo_load<C, NTB>(sp.s_prev, tl, H, W, rs);
+        }
+    };
+    // halo float4 element (pixel p, quad q) -> 4 bf16 of the channel-major tile
+    auto put_halo = [&](unsigned short* T, int e, const float4& v) {
+        const int p = e / Q, q = e - p * Q;
+        const int hr = p / HWD, hc = p - hr * HWD;
+        unsigned short* d = T + (4 * q) * Gm::XS + hr * 40 + hc;
+        d[0] = __builtin_bit_cast(unsigned short, (__bf16)v.x);
+        d[Gm::XS] = __builtin_bit_cast(unsigned short, (__bf16)v.y);
+        d[2 * Gm::XS] = __builtin_bit_cast(unsigned short, (__bf16)v.z);
+        d[3 * Gm::XS] = __builtin_bit_cast(unsigned short, (__bf16)v.w);
+    };
+
+    f32x4 acc[Gm::TPW];
+#pragma unroll
+    for (int j = 0; j < Gm::TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    issue(0);
+    __syncthreads();  // coef
+    for (int t = 0; t < nsteps; ++t) {
+        // stage step t: G^T (BN backward of g_cur, zero outside the image), X^T, S^T
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < O::E) {
+                const int p = e / Q, q = e - p * Q;
+                const int ty = p / TW, tx = p - ty * TW;
+                const bool img = tl.h0 + ty < H && tl.w0 + tx < W;
+                const float4 gv = img ? bn_bwd4(rg4[i], ry4[i], &coef[t][4 * q]) : z4;
+                float* d = Gt + (4 * q) * Gm::GS + p;
+                d[0] = gv.x;
+                d[Gm::GS] = gv.y;
+                d[2 * Gm::GS] = gv.z;
+                d[3 * Gm::GS] = gv.w;
+            }
+        }
+        const bool dense_t = dense, has_s_t = has_s;
+        if (dense_t) {
+#pragma unroll
+            for (int i = 0; i < RX; ++i) {
+                const int e = tid + i * NTB;
+                if (e < Halo4<C, NTB>::E) put_halo(Xt, e, rx[i]);
+            }
+        } else {  // strided input: element-wise gather (not the engine's path)
+            const auto& sp = ap->steps[t];
+            for (int e = tid; e < HN * C; e += NTB) {
+                const int p = e / C, c = e - p * C;
+                const int hr = p / HWD, hc = p - hr * HWD;
+                const int h = tl.h0 + hr - 1, w = tl.w0 + hc - 1;
+                const float v = in_image(h, w, H, W) ? sp.x[tl.b * sp.xs_b + c * sp.xs_c + h * sp.xs_h + w * sp.xs_w] : 0.f;
+                Xt[c * Gm::XS + hr * 40 + hc] = __builtin_bit_cast(unsigned short, (__bf16)v);
+            }
+        }
+        if constexpr (REC) {
+            if (has_s_t) {
+#pragma unroll
+                for (int i = 0; i < RX; ++i) {
+                    const int e = tid + i * NTB;
+                    if (e < Halo4<C, NTB>::E) put_halo(St, e, rs[i]);
+                }
+            }
+        }
+        __syncthreads();
+        if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
+
+        // compute: this wave's tile rows r = rg, rg + RG, ...
+#pragma unroll
+        for (int rr = 0; rr < Gm::TG; ++rr) {
+            const int r = rg + rr * Gm::RG;
+            bf16x8 ah[Gm::MTc], am[Gm::MTc], al[Gm::MTc];
+#pragma unroll
+            for (int mt = 0; mt < Gm::MTc; ++mt) {
+                const int co = mt * 16 + m;
+                float a8[8];
+                if (co < C) {
+                    const float* src = Gt + co * Gm::GS + r * TW + 8 * g;
+                    const float4 u = *reinterpret_cast<const float4*>(src), v = *reinterpret_cast<const float4*>(src + 4);
+                    a8[0] = u.x; a8[1] = u.y; a8[2] = u.z; a8[3] = u.w; a8[4] = v.x; a8[5] = v.y; a8[6] = v.z; a8[7] = v.w;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) a8[j] = 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const __bf16 h = (__bf16)a8[j];
+                    const float r1 = a8[j] - (float)h;
+                    const __bf16 md = (__bf16)r1;
+                    ah[mt][j] = h;
+                    am[mt][j] = md;
+                    al[mt][j] = (__bf16)(r1 - (float)md);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < Gm::BRW; ++k) {
+                const int br = tg * Gm::BRW + k;  // (src, ci-tile, ky), ky fastest
+                const int ky = br % 3, nt = (br / 3) % Gm::NTc, src = br / (3 * Gm::NTc);
+                if (src == 1 && !has_s_t) continue;
+                const int ci = nt * 16 + m;
+                unsigned int w6[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+                if (ci < C) {
+                    const unsigned short* T = (src == 0 ? Xt : St) + ci * Gm::XS + (r + ky) * 40 + 8 * g;
+                    const u32x4 u = *reinterpret_cast<const u32x4*>(T);
+                    const uint2 v = *reinterpret_cast<const uint2*>(T + 8);
+                    w6[0] = u.x; w6[1] = u.y; w6[2] = u.z; w6[3] = u.w; w6[4] = v.x; w6[5] = v.y;
+                }
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    u32x4 bw;
+                    if (kx == 0) bw = u32x4{w6[0], w6[1], w6[2], w6[3]};
+                    else if (kx == 2) bw = u32x4{w6[1], w6[2], w6[3], w6[4]};
+                    else bw = u32x4{__builtin_amdgcn_alignbit(w6[1], w6[0], 16), __builtin_amdgcn_alignbit(w6[2], w6[1], 16),
+                                    __builtin_amdgcn_alignbit(w6[3], w6[2], 16), __builtin_amdgcn_alignbit(w6[4], w6[3], 16)};
+                    const bf16x8 b = __builtin_bit_cast(bf16x8, bw);
+#pragma unroll
+                    for (int mt = 0; mt < Gm::MTc; ++mt) {
+                        f32x4& d = acc[k * Gm::TPB + kx * Gm::MTc + mt];
+                        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[mt], b, d, 0, 0, 0);
+                        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am[mt], b, d, 0, 0, 0);
+                        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[mt], b, d, 0, 0, 0);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // row groups 1..RG-1 add into row group 0 through LDS (fixed order), aliasing Gt/Xt/St
+    float* red = Gt;  // [TG][TPW][64][4] floats
+#pragma unroll 1
+    for (int q = 1; q < Gm::RG; ++q) {
+        if (rg == q) {
+#pragma unroll
+            for (int j = 0; j < Gm::TPW; ++j)
+                *reinterpret_cast<f32x4*>(red + ((tg * Gm::TPW + j) * 64 + lane) * 4) = acc[j];
+        }
+        __syncthreads();
+        if (rg == 0) {
+#pragma unroll
+            for (int j = 0; j < Gm::TPW; ++j) acc[j] = acc[j] + *reinterpret_cast<const f32x4*>(red + ((tg * Gm::TPW + j) * 64 + lane) * 4);
+        }
+        __syncthreads();
+    }
+    if (rg != 0) return;
+    const int64_t blk = blockIdx.x;
+    const int accumulate = ap->accumulate;
+#pragma unroll
+    for (int k = 0; k < Gm::BRW; ++k) {
+        const int br = tg * Gm::BRW + k;
+        const int ky = br % 3, nt = (br / 3) % Gm::NTc, src = br / (3 * Gm::NTc);
+        float* slab = (src == 0 ? ap->slab_ff : ap->slab_rec) + blk * (C * C * 9);
+        const int ci = nt * 16 + m;
+        if (ci >= C) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+            for (int mt = 0; mt < Gm::MTc; ++mt) {
+                const f32x4 v = acc[k * Gm::TPB + kx * Gm::MTc + mt];
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int co = mt * 16 + 4 * g + r4;
+                    if (co >= C) continue;
+                    float* d = slab + ((int64_t)co * C + ci) * 9 + ky * 3 + kx;
+                    *d = accumulate ? *d + v[r4] : v[r4];
+                }
+            }
     }
 }
 
@@ -1437,6 +1691,21 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
         else if (cin == 5) WG_PICK(5, CC_);                                                                \
         else SNN_FAIL(SNNFLOW_E_CHANNELS, "wgrad: unsupported cin");                                       \
         break;
+    if (a->exact_inputs && cin == c && (c == 8 || c == 16 || c == 32)) {
+        const dim3 blk(NT * 2);
+        if (c == 8) {
+            if (a->rec) hipLaunchKernelGGL((k_wgrad_bf<8, true>), grid, blk, 0, s, *a);
+            else hipLaunchKernelGGL((k_wgrad_bf<8, false>), grid, blk, 0, s, *a);
+        } else if (c == 16) {
+            if (a->rec) hipLaunchKernelGGL((k_wgrad_bf<16, true>), grid, blk, 0, s, *a);
+            else hipLaunchKernelGGL((k_wgrad_bf<16, false>), grid, blk, 0, s, *a);
+        } else {
+            if (a->rec) hipLaunchKernelGGL((k_wgrad_bf<32, true>), grid, blk, 0, s, *a);
+            else hipLaunchKernelGGL((k_wgrad_bf<32, false>), grid, blk, 0, s, *a);
+        }
+        SNN_CHECK_LAUNCH();
+        return 0;
+    }
     switch (c) {
         WG_CASE(4) WG_CASE(8) WG_CASE(16) WG_CASE(32)
         default: break;

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class Neuron(ctypes.Structure):
@@ -79,7 +79,8 @@ class WgradStep(ctypes.Structure):
 
 class WgradArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32), ("nsteps", I32),
-                ("accumulate", I32), ("rec", I32), ("bn_weight", P), ("slab_ff", P), ("slab_rec", P),
+                ("accumulate", I32), ("rec", I32), ("exact_inputs", I32), ("bn_weight", P), ("slab_ff", P),
+                ("slab_rec", P),
                 ("steps", WgradStep * MAX_WGRAD_STEPS)]
 
 

@@ -225,6 +225,8 @@ class FireNetEngine:
             a.B, a.H, a.W, a.c = B, H, W, C
             a.cin = cin0 if l == 0 else C
             a.nsteps, a.accumulate, a.rec = len(chunk), 1 if i0 else 0, 1 if rec else 0
+            # layers >= 1: x and s_prev are spikes of this engine (0/1, exact in bf16)
+            a.exact_inputs = 1 if l > 0 else 0
             a.bn_weight = ptr(self.cells[l].bn.weight)
             a.slab_ff, a.slab_rec = ptr(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
             for k, (gcur, bnc, ys, stats, x, states, s_prev) in enumerate(chunk):
