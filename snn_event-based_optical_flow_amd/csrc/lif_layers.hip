@@ -1203,7 +1203,8 @@ struct WbGeo {
     static constexpr int BROWS = (REC ? 2 : 1) * NTc * 3;  // (src, ci-tile, ky)
     static constexpr int TPB = 3 * MTc;                     // tiles per B-row: (kx, co-tile)
     static constexpr int NTOT = BROWS * TPB;
-    static constexpr int TG = NTOT <= 18 ? 1 : (NTOT <= 36 ? 2 : 4);
+    // wave groups over the tiles: <= 9 accumulator tiles per wave up to C = 16, 18 at C = 32
+    static constexpr int TG = C <= 16 ? (REC ? 2 : 1) : (REC ? 4 : 2);
     static constexpr int RG = 8 / TG;
     static constexpr int BRW = BROWS / TG;                  // B-rows per wave
     static constexpr int TPW = BRW * TPB;                   // accumulator tiles per wave
