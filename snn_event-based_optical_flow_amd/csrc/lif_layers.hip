@@ -313,8 +313,9 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
                     sv = o.s;
                     if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
                         const int64_t k = (((int64_t)tl.b * H + h) * W + w) * Q + q;
-                        st4[k] = o.mout;
-                        st4[plane4 + k] = o.s;
+                        // write-through: read again only at the next time step (measured -1 us per launch)
+                        st_state4(st4, k, o.mout);
+                        st_state4(st4, plane4 + k, o.s);
                     }
                 }
                 *reinterpret_cast<float4*>(tile + p * PI_ + 4 * q) = sv;
@@ -469,7 +470,7 @@ __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const Lif4 o = lif_step4(yv[q], mv[q], coef + 4 * q, zr);
-        st4[p * Q + q] = o.mout;
+        st4[p * Q + q] = o.mout;  // plain: write-through measured slower in this streaming kernel
         st4[plane4 + p * Q + q] = o.s;
         s[4 * q] = o.s.x; s[4 * q + 1] = o.s.y; s[4 * q + 2] = o.s.z; s[4 * q + 3] = o.s.w;
     }
