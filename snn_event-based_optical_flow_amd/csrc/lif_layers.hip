@@ -11,6 +11,7 @@
 // 8x32 pixel tile; halo rows are recomputed by neighbouring blocks (never stored).
 #include <cmath>
 #include <string>
+#include <type_traits>
 
 #include "snnflow_dev.h"
 #include "snnflow_tile.h"
@@ -296,31 +297,40 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         // gather made its wait include the store acknowledgements)
         zero_consumed(a.zero0, a.zero1, a.zero_n);
         TRACE_AT(TR, TK, 1);
-        // 2. LIF of the previous layer over the halo; interior pixels also write its state
-        const bool zr = a.prev.zero_reset != 0;
+        // 2. LIF of the previous layer over the halo; interior pixels also write its state.
+        //    Element e = tid + i*NTB has channel quad e % Q = tid % Q (NTB % Q == 0): the four
+        //    coefficients come out of LDS once, and the reset flavour is a loop version.
+        static_assert(NTB % Q == 0, "constant channel quad per thread");
         const int64_t plane4 = (int64_t)a.B * H * W * Q;
         float4* st4 = reinterpret_cast<float4*>(a.prev_state);
+        const int qt = tid % Q;
+        const LifCoef kc[4] = {coef[4 * qt], coef[4 * qt + 1], coef[4 * qt + 2], coef[4 * qt + 3]};
+        auto halo_lif = [&](auto zr_c) {
+            constexpr bool ZR = decltype(zr_c)::value;
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
-            const int e = tid + i * NTB;
-            if (e < Halo4<CIN, NTB>::E) {
-                const int p = e / Q, q = e - p * Q;
-                const int r = p / HWD, cc = p - r * HWD;
-                const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-                float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (in_image(h, w, H, W)) {
-                    const Lif4 o = lif_step4(ry[i], rm[i], coef + 4 * q, zr);
-                    sv = o.s;
-                    if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
-                        const int64_t k = (((int64_t)tl.b * H + h) * W + w) * Q + q;
-                        // write-through: read again only at the next time step (measured -1 us per launch)
-                        st_state4(st4, k, o.mout);
-                        st_state4(st4, plane4 + k, o.s);
+            for (int i = 0; i < R; ++i) {
+                const int e = tid + i * NTB;
+                if (e < Halo4<CIN, NTB>::E) {
+                    const int p = e / Q;
+                    const int r = p / HWD, cc = p - r * HWD;
+                    const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+                    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (in_image(h, w, H, W)) {
+                        const Lif4 o = lif_step4(ry[i], rm[i], kc, ZR);
+                        sv = o.s;
+                        if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
+                            const int64_t k = (((int64_t)tl.b * H + h) * W + w) * Q + qt;
+                            // write-through: read again only at the next time step (measured -1 us per launch)
+                            st_state4(st4, k, o.mout);
+                            st_state4(st4, plane4 + k, o.s);
+                        }
                     }
+                    *reinterpret_cast<float4*>(tile + p * PI_ + 4 * qt) = sv;
                 }
-                *reinterpret_cast<float4*>(tile + p * PI_ + 4 * q) = sv;
             }
-        }
+        };
+        if (a.prev.zero_reset) halo_lif(std::true_type{});
+        else halo_lif(std::false_type{});
     } else {
         stage_strided<CIN, NTB>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, tile);
         zero_consumed(a.zero0, a.zero1, a.zero_n);
@@ -717,14 +727,17 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l)
     if constexpr (PF) {
         constexpr int Q = C / 4;
+        static_assert(NTB % Q == 0, "constant channel quad per thread");
+        const int qt = tid % Q;
+        const BnBwdLds kb[4] = {bnp[4 * qt], bnp[4 * qt + 1], bnp[4 * qt + 2], bnp[4 * qt + 3]};
 #pragma unroll
         for (int i = 0; i < Halo4<C, NTB>::R; ++i) {
             const int e = tid + i * NTB;
             if (e < Halo4<C, NTB>::E) {
-                const int p = e / Q, q = e - p * Q;
+                const int p = e / Q;
                 const int r = p / HWD, cc = p - r * HWD;
                 const bool img = in_image(tl.h0 + r - 1, tl.w0 + cc - 1, H, W);
-                *reinterpret_cast<float4*>(G + p * PC + 4 * q) = img ? bn_bwd4(rg[i], ry[i], bnp + 4 * q) : z4;
+                *reinterpret_cast<float4*>(G + p * PC + 4 * qt) = img ? bn_bwd4(rg[i], ry[i], kb) : z4;
             }
         }
     } else {
