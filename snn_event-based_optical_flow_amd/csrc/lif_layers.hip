@@ -1114,6 +1114,9 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
     }
 
     float4 rg[O::R], ry[O::R], rx[RX], rs[RS];
+    // narrow strided inputs (the head's NCHW event counts): element-wise register prefetch
+    constexpr int RXS = XV ? 1 : (HN * CIN + NTB - 1) / NTB;
+    float rxs[RXS];
     bool dense = false, has_s = false;
     auto issue = [&](int t) {  // loads of step t into registers
         const float* g = ap->steps[t].g_cur;
@@ -1137,6 +1140,17 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
                     ap->steps[t].xs_b == (int64_t)H * W * CIN;
         if constexpr (XV) {
             if (dense) halo_load<CIN, NTB>(sx, tl, H, W, rx);
+        } else {
+            const auto& st = ap->steps[t];
+            const float* xb = sx + (int64_t)tl.b * st.xs_b;
+#pragma unroll
+            for (int i = 0; i < RXS; ++i) {
+                const int e = tid + i * NTB;
+                const int ci = e / HN, p = e - ci * HN;  // channel-major: plane reads coalesce
+                const int r = p / HWD, cc = p - r * HWD;
+                const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+                rxs[i] = (e < HN * CIN && in_image(h, w, H, W)) ? xb[ci * st.xs_c + h * st.xs_h + w * st.xs_w] : 0.0f;
+            }
         }
         has_s = REC && sp != nullptr;
         if constexpr (REC) {
@@ -1171,9 +1185,19 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
         if constexpr (XV) {
             if (dense_t) halo_store<CIN, NTB>(X, rx);
         }
-        if (!dense_t)
+        if constexpr (!XV) {
+#pragma unroll
+            for (int i = 0; i < RXS; ++i) {
+                const int e = tid + i * NTB;
+                if (e < HN * CIN) {
+                    const int ci = e / HN, p = e - ci * HN;
+                    X[p * PI_ + ci] = rxs[i];
+                }
+            }
+        } else if (!dense_t) {
             stage_strided<CIN, NTB>(ap->steps[t].x, ap->steps[t].xs_b, ap->steps[t].xs_c, ap->steps[t].xs_h,
                                     ap->steps[t].xs_w, tl, H, W, X);
+        }
         if constexpr (REC) {
             if (has_s_t) halo_store<C, NTB>(S, rs);
         }
