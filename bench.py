@@ -129,6 +129,7 @@ def main():
 
     # persistent state buffers: detach_states() == copy into them (the reference clones)
     state_bufs = None
+    state_flat = None
 
     def fwd_bwd():
         loss_fn.reset()
@@ -145,10 +146,22 @@ def main():
     def update():
         dp.clip_grad_norm_(params, 1.0)
         opt.step()
-        nonlocal state_bufs
+        nonlocal state_bufs, state_flat
         if state_bufs is None:
-            state_bufs = [s.detach().clone() for s in model._states]
-        torch._foreach_copy_(state_bufs, [s.detach() for s in model._states])  # one multi-tensor launch
+            src = _flat_span(model._states)
+            if src is not None:  # persistent buffers with the same back-to-back layout
+                state_flat = src.clone()
+                base = src.data_ptr()
+                state_bufs = [torch.empty(0, device=dev).set_(state_flat.untyped_storage(),
+                                                              (s.data_ptr() - base) // 4, s.shape, s.stride())
+                              for s in model._states]
+            else:
+                state_bufs = [s.detach().clone() for s in model._states]
+        src = _flat_span(model._states)
+        if src is not None and state_flat is not None:
+            state_flat.copy_(src)  # the engine's states are back to back: one contiguous copy
+        else:
+            torch._foreach_copy_(state_bufs, [s.detach() for s in model._states])
         model._states = list(state_bufs)
 
     def step_eager():
@@ -262,6 +275,23 @@ def main():
 
 
 _KEYS = ("event_cnt", "event_list", "event_list_pol_mask", "event_mask")
+
+
+def _flat_span(tensors):
+    """1-D view over the storage range of `tensors` if they are fp32 views laid back to back
+    in one storage (each exactly covering its numel), else None."""
+    if not tensors or any(t is None for t in tensors):
+        return None
+    st = tensors[0].untyped_storage()
+    off = tensors[0].storage_offset()
+    base = off
+    for t in tensors:
+        if t.untyped_storage().data_ptr() != st.data_ptr() or t.storage_offset() != off or t.dtype != torch.float32:
+            return None
+        off += t.numel()
+    flat = torch.empty(0, device=tensors[0].device)
+    flat.set_(st, base, (off - base,), (1,))
+    return flat
 
 
 def _pack(windows):

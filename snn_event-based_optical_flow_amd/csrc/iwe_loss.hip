@@ -144,16 +144,22 @@ __device__ inline SmoothTerms smooth_at(const snnflow_iwe_loss_args& a, int b, i
 // Row: {S+, S-, nz} x {fw, bw}, then the five smoothness sums.
 constexpr int LOSS_NV = 11;
 
-__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks) {
+// Each block covers LOSS_CPB chunks of NT pixels of one (sample, window): one partial row
+// per LOSS_CPB * NT pixels keeps the fixed-order reduction in k_iwe_finalize short.
+constexpr int LOSS_CPB = 4;
+
+__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int groups) {
     __shared__ float red[NT / 64][LOSS_NV];
-    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, t = (blockIdx.x / chunks) % a.tf,
-              b = blockIdx.x / (chunks * a.tf);
+    const int tid = threadIdx.x, grp = blockIdx.x % groups, t = (blockIdx.x / groups) % a.tf,
+              b = blockIdx.x / (groups * a.tf);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
-    const int p = chunk * NT + tid;
     float v[LOSS_NV];
 #pragma unroll
     for (int j = 0; j < LOSS_NV; ++j) v[j] = 0.0f;
-    if (p < HWp) {
+#pragma unroll
+    for (int cc = 0; cc < LOSS_CPB; ++cc) {
+        const int p = (grp * LOSS_CPB + cc) * NT + tid;
+        if (p >= HWp) break;
         if (t == 0) {
             const float T = (float)a.T;
 #pragma unroll
@@ -173,15 +179,15 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
                 const float cp = q4[0], cn = q4[1], tp = q4[2], tn = q4[3];
                 const float A = (tp / (cp + 1e-9f)) / T;
                 const float Bv = (tn / (cn + 1e-9f)) / T;
-                v[3 * d + 0] = A * A;
-                v[3 * d + 1] = Bv * Bv;
-                v[3 * d + 2] = (cp + cn > 0.0f) ? 1.0f : 0.0f;
+                v[3 * d + 0] += A * A;
+                v[3 * d + 1] += Bv * Bv;
+                v[3 * d + 2] += (cp + cn > 0.0f) ? 1.0f : 0.0f;
             }
         }
         const int h = p / a.W, w = p - h * a.W;
         const SmoothTerms sm = smooth_at(a, b, t, h, w);
 #pragma unroll
-        for (int j = 0; j < 5; ++j) v[6 + j] = sm.v[j];
+        for (int j = 0; j < 5; ++j) v[6 + j] += sm.v[j];
     }
     const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
@@ -203,11 +209,11 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
 // of samples w, w + 16, ... (all 11 columns), then the smoothness sums add up over samples.
 constexpr int FIN_NT = 1024;
 
-__global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int chunks) {
+__global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int groups) {
     __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
     __shared__ double smp[64][5];          // per-sample smoothness sums
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int rows_b = chunks * a.tf;
+    const int rows_b = groups * a.tf;
     // wave w reduces samples w, w + 16, ...: lane-strided rows, all 11 columns at once
     for (int b = wv; b < a.B; b += FIN_NT / 64) {
         double s[LOSS_NV];
@@ -455,8 +461,8 @@ extern "C" {
 int snnflow_iwe_scratch_floats(int B, int H, int W) { return SPLAT_SPLIT * 8 * B * H * W; }
 
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
-    const int64_t chunks = ((int64_t)H * W + NT - 1) / NT;
-    return (int)((int64_t)B * tf * chunks * LOSS_NV);
+    const int64_t groups = ((int64_t)H * W + LOSS_CPB * NT - 1) / (LOSS_CPB * NT);
+    return (int)((int64_t)B * tf * groups * LOSS_NV);
 }
 
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
@@ -465,9 +471,9 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     const int64_t HWp = (int64_t)a->H * a->W;
     const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
     hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands * SPLAT_SPLIT), dim3(SPLAT_NT), 0, s, *a, nbands);
-    const int chunks = (int)((HWp + NT - 1) / NT);
-    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * a->tf * chunks), dim3(NT), 0, s, *a, chunks);
-    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, chunks);
+    const int groups = (int)((HWp + LOSS_CPB * NT - 1) / (LOSS_CPB * NT));
+    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * a->tf * groups), dim3(NT), 0, s, *a, groups);
+    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, groups);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -299,7 +299,12 @@ class FireNetStep(torch.autograd.Function):
 
         ys = torch.empty(L, B, H, W, C, device=dev)
         stats = torch.empty(L, 2, C, device=dev)
-        states = [empty_state(B, C, H, W, dev) for _ in range(L)]
+        # all L states of the step in one allocation, back to back (a state hand-over, e.g. the
+        # bench's graph-replay detach, is then a single contiguous copy)
+        n1 = 2 * B * H * W * C
+        st_all = torch.empty(L * n1, device=dev)
+        states = [st_all[l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
+                  for l in range(L)]
         flow = torch.empty(B, 2, H, W, device=dev)
 
         mem_in, s_prev, prev_nhwc = [], [], []
