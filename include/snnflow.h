@@ -404,6 +404,10 @@ int snnflow_flow_metrics_rows(int B, int H, int W);
 int snnflow_lif_export(const float* x, const float* mem, const float* beta, const float* thr,
                        int N, int C, int HW, float* spk, float* mem_out, void* stream);
 
+/* clip_grad_norm_ (train_flow.py:265-266) over one flat gradient buffer of n floats, in place:
+ * total = ||g||_2, g *= min(max_norm / (total + eps), 1); total_out (device, may be NULL). */
+int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float* total_out, void* stream);
+
 const char* snnflow_last_error(void);
 int snnflow_abi_version(void);
 

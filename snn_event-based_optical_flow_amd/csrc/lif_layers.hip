@@ -1510,6 +1510,37 @@ __global__ __launch_bounds__(SR_E * SR_G) void k_slab_reduce(DescBatch<snnflow_s
     }
 }
 
+// torch.nn.utils.clip_grad_norm_ over the engine's flat gradient buffer in one block:
+// total = ||g||_2 (fp64 accumulation, fixed order), coef = min(max_norm / (total + eps), 1),
+// g *= coef (train_flow.py:265-266).
+constexpr int CLIP_NT = 1024;
+
+__global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n, float max_norm, float eps,
+                                                          float* total_out) {
+    __shared__ double part[CLIP_NT / 64];
+    __shared__ float coef_s;
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < n; i += CLIP_NT) {
+        const double v = g[i];
+        s += v * v;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < CLIP_NT / 64; ++w) t += part[w];
+        const float total = (float)sqrt(t);
+        float c = max_norm / (total + eps);
+        coef_s = c < 1.0f ? c : 1.0f;
+        if (total_out) total_out[0] = total;
+    }
+    __syncthreads();
+    const float c = coef_s;
+    for (int64_t i = threadIdx.x; i < n; i += CLIP_NT) g[i] = g[i] * c;
+}
+
 __global__ void k_lif_export(const float* __restrict__ x, const float* __restrict__ mem, const float* __restrict__ beta,
                              const float* __restrict__ thr, int64_t total, int C, int HW, float* spk, float* mout) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1767,6 +1798,13 @@ int snnflow_slab_reduce(const snnflow_slab_desc* d, int n, int nblk, void* strea
     }
     hipLaunchKernelGGL(k_slab_reduce, dim3((maxe + SR_E - 1) / SR_E, n), dim3(SR_E * SR_G), 0, (hipStream_t)stream,
                        batch, nblk);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float* total_out, void* stream) {
+    if (!g || n < 0) SNN_FAIL(SNNFLOW_E_ARG, "clip_grad_norm: bad args");
+    hipLaunchKernelGGL(k_clip_grad_norm, dim3(1), dim3(CLIP_NT), 0, (hipStream_t)stream, g, n, max_norm, eps, total_out);
     SNN_CHECK_LAUNCH();
     return 0;
 }

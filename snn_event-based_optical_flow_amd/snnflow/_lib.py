@@ -189,6 +189,7 @@ EXPORTS = {
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
     "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
+    "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
 }
 
 

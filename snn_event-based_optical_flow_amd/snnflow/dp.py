@@ -84,7 +84,14 @@ def clip_grad_norm_(params, max_norm, eps=1e-6):
     flat = flat_grad_buffer(params)
     if flat is None:
         return torch.nn.utils.clip_grad_norm_(params, max_norm)
-    total = torch.linalg.vector_norm(flat, 2.0)
+    if flat.is_cuda and flat.dtype == torch.float32:
+        # one HIP launch: norm (fp64 accumulation) + scale in place
+        from . import _lib
+        total = torch.empty((), device=flat.device)
+        _lib.call("clip_grad_norm", _lib.lib.snnflow_clip_grad_norm, flat.data_ptr(), flat.numel(), float(max_norm),
+                  float(eps), total.data_ptr(), _lib.stream_ptr(flat.device))
+        return total
+    total = torch.linalg.vector_norm(flat, 2.0)  # host tensors (gloo tests): same math in torch
     coef = torch.clamp(max_norm / (total + eps), max=1.0)
     flat.mul_(coef)
     return total

@@ -613,3 +613,30 @@ def test_flow_metrics_vs_oracle_random(dev):
     ref = flow_metrics_ref(flow, gt, mask, dt_in, dt_gt, 128, 0.5)
     for k in _lib.METRICS:
         np.testing.assert_allclose(ours[k].cpu().numpy(), ref[k].numpy(), rtol=2e-5, atol=1e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("scale", [1e-3, 10.0])
+def test_clip_grad_norm_flat_vs_torch(dev, scale):
+    """snnflow_clip_grad_norm (one launch over the engine's flat gradient buffer) against
+    torch.nn.utils.clip_grad_norm_ on the same gradients (no clipping / clipping)."""
+    from snnflow import dp
+
+    gen = torch.Generator().manual_seed(9)
+    shapes = [(8, 2, 3, 3), (8,), (8, 8, 3, 3), (2, 8, 1, 1), (2,)]
+    vals = [torch.randn(s, generator=gen) * scale for s in shapes]
+    flat = torch.cat([v.reshape(-1) for v in vals]).to(dev)
+    ps, ref = [], []
+    off = 0
+    for v in vals:
+        p = torch.nn.Parameter(torch.zeros_like(v, device=dev))
+        p.grad = flat[off:off + v.numel()].view(v.shape)
+        off += v.numel()
+        ps.append(p)
+        q = torch.nn.Parameter(torch.zeros_like(v))
+        q.grad = v.clone()
+        ref.append(q)
+    total = dp.clip_grad_norm_(ps, 1.0)
+    rtotal = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    np.testing.assert_allclose(total.item(), rtotal.item(), rtol=1e-5)
+    for p, q in zip(ps, ref):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), q.grad.numpy(), rtol=1e-5, atol=1e-8)
