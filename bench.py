@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--events", type=int, default=1000, help="events per window (data.window)")
     p.add_argument("--model", default="LIFFireNet")
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--per-step", action="store_true",
+                   help="T model() calls (FireNetStep) instead of model.forward_sequence (wavefront launches)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=3, help="distinct synthetic batches cycled in HBM")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsals)")
@@ -72,6 +74,17 @@ def algorithmic_bytes(name, C, P, cin0):
     if name.startswith("layer_bwd"):
         return f * (3 * C + 2 * C + C)
     return None
+
+
+def slot_pass_bytes(kind, C, P, cin0, T, layer_spec):
+    """Algorithmic bytes of all T x (L+1) layer-steps of a forward (fwd_slot) or backward
+    (bwd_slot) pass: the per-kernel formulas of algorithmic_bytes, summed."""
+    rec = [r for _, r in layer_spec]
+    if kind == "fwd_slot":
+        names = ["conv_fwd[0]"] + ["conv_fwd_rec" if r else "conv_fwd" for r in rec[1:]] + ["lif_fwd"]
+    else:
+        names = ["lif_bwd"] + ["layer_bwd_rec" if r else "layer_bwd" for r in rec[1:]] + ["layer_bwd_head"]
+    return T * sum(algorithmic_bytes(n, C, P, cin0) for n in names)
 
 
 def classify(name, rec_layers):
@@ -133,10 +146,13 @@ def main():
 
     def fwd_bwd():
         loss_fn.reset()
+        if args.per_step:
+            outs = [model(w["event_voxel"], w["event_cnt"]) for w in static]
+        else:  # the same T steps, kernels issued as wavefront launches (C = 8; else per step)
+            outs = model.forward_sequence([w["event_voxel"] for w in static], [w["event_cnt"] for w in static])
         for t in range(T):
             w = static[t]
-            out = model(w["event_voxel"], w["event_cnt"])
-            loss_fn.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            loss_fn.event_flow_association(outs[t]["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
         loss = loss_fn()
         loss.backward()
         return loss
@@ -246,6 +262,8 @@ def main():
     n_dom, tot_dom = classes[dominant]
     avg_us = 1000.0 * tot_dom / n_dom
     abytes = algorithmic_bytes(dominant, args.channels, P, 2)
+    if dominant in ("fwd_slot", "bwd_slot"):  # wavefront launches: the pass's layer-step bytes / its launches
+        abytes = slot_pass_bytes(dominant, args.channels, P, 2, T, model.layer_spec) / n_dom
     achieved = abytes / (avg_us * 1e-6) / 1e9 if abytes else None
     kernels = {k: {"launches": n, "avg_us": round(1000.0 * t / n, 2), "share": round(t / sum(x[1] for x in classes.values()), 3)}
                for k, (n, t) in sorted(classes.items(), key=lambda kv: -kv[1][1])}
@@ -266,7 +284,8 @@ def main():
             "config": {"workload": f"{args.model} train step: T={T} x {N}-event windows, {R}x{R}, "
                                    f"batch {B}/GPU, base_num_channels {args.channels}, EventWarping + Adam",
                        "global_batch": B * world, "parallelism": f"dp{world}",
-                       "hip_graph": not args.no_graph},
+                       "hip_graph": not args.no_graph,
+                       "launch_order": "per-step" if args.per_step else "wavefront"},
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 13
+#define SNNFLOW_ABI_VERSION 14
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -189,6 +189,26 @@ typedef struct snnflow_layer_bwd_args {
     double* zero0; double* zero1; int zero_n;
 } snnflow_layer_bwd_args;
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
+
+/* ---- wavefront launches (ABI 14) -------------------------------------------
+ * Up to SNNFLOW_MAX_SLOT_TASKS mutually independent layer-steps of one model in ONE launch.
+ * A single layer-step launch is latency-bound (load -> LIF -> conv -> store chain of one
+ * block per tile); the (layer, step) grid of a T-step sequence instead runs as 2(T-1)+L+1
+ * launches of about (L+1)/2 layer-steps each (task (l, t) in launch l + 2t; snnflow/engine.py
+ * FireNetSequence).  Each task means exactly what the single-task call with the same
+ * arguments means; the caller guarantees that no task reads what another task of the same
+ * launch writes.  Forward: conv tasks (snnflow_conv_fwd) + at most one LIF(+pred) task
+ * (snnflow_lif_fwd); backward: layer tasks (snnflow_layer_bwd) + at most one top-LIF task
+ * (snnflow_lif_bwd).  All tasks of a launch share c and B, H, W.
+ * snnflow_slot_supported(c, cin0): 1 if both slot kernels take every task of a model with
+ * c channels and a cin0-channel input (c = 8; cin0 2 or 4), else 0 (C = 16 / 32: one
+ * layer-step already fills the chip). */
+#define SNNFLOW_MAX_SLOT_TASKS 4
+int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow_lif_fwd_args* lif,
+                     void* stream);
+int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnflow_lif_bwd_args* lif,
+                     void* stream);
+int snnflow_slot_supported(int c, int cin0);
 
 /* ---- deferred weight gradients of one layer over many time steps ----------
  * Nothing on the backward chain depends on dW, so the weight gradients of a layer

@@ -76,7 +76,7 @@ __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_
 // the halo loads instead of following the batch-sum gather.
 struct NeuronRegs { float w, b, beta, theta, rm, rv; };
 
-__device__ inline NeuronRegs load_neuron(const snnflow_neuron& n, int C) {
+__device__ inline NeuronRegs load_neuron(const snnflow_neuron& n, int C, bool lead) {
     NeuronRegs r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int c = threadIdx.x;
     if (c < C) {
@@ -85,7 +85,7 @@ __device__ inline NeuronRegs load_neuron(const snnflow_neuron& n, int C) {
         r.beta = n.beta[c];
         r.theta = n.threshold[c];
         // running statistics: every block in eval mode, block 0 (the updater) in train mode
-        if (n.running_mean && (!n.bn_train || blockIdx.x == 0)) {
+        if (n.running_mean && (!n.bn_train || lead)) {
             r.rm = n.running_mean[c];
             r.rv = n.running_var[c];
         }
@@ -121,7 +121,7 @@ __device__ inline BnStat bn_stat(const snnflow_neuron& n, const NeuronRegs& r, c
 // (momentum, unbiased variance) and num_batches_tracked += 1 of torch's BatchNorm2d.
 // `sums`: LDS totals from acc_gather (train mode only); r: load_neuron of this thread.
 __device__ void lif_prologue(const snnflow_neuron& n, const NeuronRegs& r, const double* sums, int C, double N,
-                             float* stats_out, LifCoef* coef, float* mean_out) {
+                             float* stats_out, LifCoef* coef, float* mean_out, bool lead) {
     const int c = threadIdx.x;
     if (c < C) {
         const BnStat st = bn_stat(n, r, sums, C, c, N);
@@ -132,7 +132,7 @@ __device__ void lif_prologue(const snnflow_neuron& n, const NeuronRegs& r, const
         k.theta = r.theta;
         coef[c] = k;
         if (mean_out) mean_out[c] = st.mean;
-        if (blockIdx.x == 0) {
+        if (lead) {
             if (stats_out) {
                 stats_out[c] = st.mean;
                 stats_out[C + c] = st.invstd;
@@ -144,7 +144,7 @@ __device__ void lif_prologue(const snnflow_neuron& n, const NeuronRegs& r, const
             }
         }
     }
-    if (c == 0 && blockIdx.x == 0 && n.bn_train && n.num_batches_tracked) n.num_batches_tracked[0] += 1;
+    if (c == 0 && lead && n.bn_train && n.num_batches_tracked) n.num_batches_tracked[0] += 1;
 }
 
 // Layer-l gradients of (gamma, bn bias, beta, threshold) [and pred] from the LIF-backward
@@ -157,9 +157,9 @@ struct NeuronGradRegs { float inv, be, o0, o1, o2, o3, op; };
 
 __device__ inline NeuronGradRegs load_neuron_grad(const snnflow_neuron& n, const float* stats, int C,
                                                   const snnflow_neuron_grad& ng, int accumulate, int has_pred,
-                                                  float* g_pred_w, float* g_pred_b) {
+                                                  float* g_pred_w, float* g_pred_b, bool lead) {
     NeuronGradRegs r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (blockIdx.x != 0) return r;
+    if (!lead) return r;
     const int c = threadIdx.x;
     if (c < C) {
         r.inv = stats[C + c];
@@ -173,8 +173,8 @@ __device__ inline NeuronGradRegs load_neuron_grad(const snnflow_neuron& n, const
 }
 
 __device__ void neuron_grads(const NeuronGradRegs& r, const double* sums, int C, const snnflow_neuron_grad& ng,
-                             int has_pred, float* g_pred_w, float* g_pred_b) {
-    if (blockIdx.x != 0) return;
+                             int has_pred, float* g_pred_w, float* g_pred_b, bool lead) {
+    if (!lead) return;
     const int c = threadIdx.x;
     if (c < C) {
         const double gsum = sums[c], dotp = sums[C + c], gbm = sums[2 * C + c];
@@ -247,30 +247,44 @@ __device__ inline Lif4 lif_step4(const float4& y, const float4& m, const LifCoef
     return r;
 }
 
+// LDS of one conv_fwd block (floats, 16-B aligned parts): halo tile, [s_prev halo tile],
+// [weights of the ff / rec convs].  Carved out of one pool so that a wavefront launch can
+// run several variants over the same allocation.
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
-__global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a) {
+struct ConvFwdLds {
+    static constexpr int NTB = NT * SPLIT, PI_ = Pad<CIN>::v, PC = Pad<C>::v;
+    static constexpr bool PF_REC = REC && Prefetch<C, NTB>::on;  // s_prev halo in registers + own LDS tile
+    static constexpr int PMAX = (REC && !PF_REC && PC > PI_) ? PC : PI_;
+    static constexpr bool WL = kWlds<CIN, C>;
+    static constexpr int TILE = (HN * PMAX + 3) / 4 * 4, RTILE = PF_REC ? HN * PC : 0;
+    static constexpr int WFF = WL ? 9 * C * C : 0, WREC = (WL && REC) ? 9 * C * C : 0;
+    static constexpr int FLOATS = TILE + RTILE + WFF + WREC;
+};
+
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+__device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, float* lds) {
+    using L = ConvFwdLds<CIN, C, LIF_IN, REC, SPLIT>;
     constexpr int NTB = NT * SPLIT, CO = C / SPLIT;
     static_assert(CO % 4 == 0, "output channels per group: multiple of 4");
-    constexpr int PI_ = Pad<CIN>::v, PC = Pad<C>::v;
-    constexpr bool PF_REC = REC && Prefetch<C, NTB>::on;  // s_prev halo in registers + own LDS tile
-    constexpr int PMAX = (REC && !PF_REC && PC > PI_) ? PC : PI_;
-    __shared__ __attribute__((aligned(16))) float tile[HN * PMAX];
-    __shared__ __attribute__((aligned(16))) float rtile[PF_REC ? HN * PC : 4];
+    constexpr int PI_ = L::PI_, PC = L::PC;
+    constexpr bool PF_REC = L::PF_REC;
+    float* tile = lds;
+    [[maybe_unused]] float* rtile = lds + L::TILE;
+    [[maybe_unused]] float* wl_ff = rtile + L::RTILE;
+    [[maybe_unused]] float* wl_rec = wl_ff + L::WFF;
     __shared__ LifCoef coef[LIF_IN ? CIN : 1];
 
     const int tid = threadIdx.x, pt = tid % NT, ty = pt / TW, tx = pt - ty * TW;
     const int part = thread_part(), co0 = part * CO;
     const int H = a.H, W = a.W;
-    const Tile tl = block_tile(H, W);
+    const Tile tl = block_tile(H, W, g);
     const bool has_rec = REC && a.s_prev != nullptr;
     [[maybe_unused]] constexpr bool TR = LIF_IN && CIN == C;
     [[maybe_unused]] constexpr int TK = REC ? 1 : 0;
     TRACE_AT(TR, TK, 0);
 
     // 1. issue every global load of the tile before any use (weights for LDS first)
-    constexpr bool WL = kWlds<CIN, C>;
-    __shared__ __attribute__((aligned(16))) float wl_ff[WL ? 9 * C * C : 4];
-    __shared__ __attribute__((aligned(16))) float wl_rec[WL && REC ? 9 * C * C : 4];
+    constexpr bool WL = L::WL;
     WStage<WL ? 9 * C * C : 1, NTB> sw_ff, sw_rec;
     if constexpr (WL) {
         sw_ff.load(a.wt_ff_t);
@@ -288,14 +302,14 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         halo_load<CIN, NTB>(a.prev_y, tl, H, W, ry);
         if (a.prev_mem) halo_load<CIN, NTB>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
-        const NeuronRegs nr = load_neuron(a.prev, CIN);
+        const NeuronRegs nr = load_neuron(a.prev, CIN, g.bid == 0);
         __shared__ double sums[2 * CIN];
         if (a.prev.bn_train) acc_gather<2 * CIN>(a.prev_acc, 2 * CIN, sums);
-        lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr);
+        lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr, g.bid == 0);
         __syncthreads();
         // (stores issued after the gather: CDNA's vmcnt counts stores, so zeroing before the
         // gather made its wait include the store acknowledgements)
-        zero_consumed(a.zero0, a.zero1, a.zero_n);
+        zero_consumed(a.zero0, a.zero1, a.zero_n, g);
         TRACE_AT(TR, TK, 1);
         // 2. LIF of the previous layer over the halo; interior pixels also write its state.
         //    Element e = tid + i*NTB has channel quad e % Q = tid % Q (NTB % Q == 0): the four
@@ -333,7 +347,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
         else halo_lif(std::false_type{});
     } else {
         stage_strided<CIN, NTB>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, tile);
-        zero_consumed(a.zero0, a.zero1, a.zero_n);
+        zero_consumed(a.zero0, a.zero1, a.zero_n, g);
     }
     if constexpr (WL) {
         sw_ff.store(wl_ff);
@@ -440,7 +454,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
             v[co] = yy;
             v[CO + co] = yy * yy;
         }
-        double* acc = acc_shard(a.acc, 2 * C);
+        double* acc = acc_shard(a.acc, 2 * C, g.bid);
         if (!PROBE_OFF(4))
             block_atomic_sum_parts<2 * CO, SPLIT>(v, [acc](int pp, int j) {
                 return acc + (j < CO ? pp * CO + j : C + pp * CO + (j - CO));
@@ -449,14 +463,21 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
     TRACE_AT(TR, TK, 4);
 }
 
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+__global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a) {
+    __shared__ __attribute__((aligned(16))) float pool[ConvFwdLds<CIN, C, LIF_IN, REC, SPLIT>::FLOATS];
+    conv_fwd_body<CIN, C, LIF_IN, REC, SPLIT>(a, hw_grid(), pool);
+}
+
 // LIF (+ 1x1 pred conv + tanh) over pixels: one thread per pixel, all C channels.
-template <int C, bool PRED>
-__global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
+// NTH threads (= pixels) per block: NT for its own launch, NT * 2 inside a wavefront launch.
+template <int C, bool PRED, int NTH>
+__device__ void lif_fwd_body(const snnflow_lif_fwd_args& a, const Grid g) {
     constexpr int Q = C / 4;
     __shared__ LifCoef coef[C];
     const int tid = threadIdx.x;
     const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
-    const int64_t p = (int64_t)blockIdx.x * NT + tid;
+    const int64_t p = (int64_t)g.bid * NTH + tid;
     const bool act = p < npix;
     const float4* y4 = reinterpret_cast<const float4*>(a.y);
     const float4* m4 = reinterpret_cast<const float4*>(a.mem);
@@ -467,12 +488,12 @@ __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
         yv[q] = y4[pc * Q + q];
         mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
     }
-    const NeuronRegs nr = load_neuron(a.n, C);
+    const NeuronRegs nr = load_neuron(a.n, C, g.bid == 0);
     __shared__ double sums[2 * C];
     if (a.n.bn_train) acc_gather<2 * C>(a.acc, 2 * C, sums);
-    lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr);
+    lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr, g.bid == 0);
     __syncthreads();
-    zero_consumed(a.zero0, a.zero1, a.zero_n);  // after the gather (vmcnt counts stores)
+    zero_consumed(a.zero0, a.zero1, a.zero_n, g);  // after the gather (vmcnt counts stores)
     if (!act) return;
     const bool zr = a.n.zero_reset != 0;
     float4* st4 = reinterpret_cast<float4*>(a.state);
@@ -497,16 +518,22 @@ __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
     }
 }
 
+template <int C, bool PRED>
+__global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
+    lif_fwd_body<C, PRED, NT>(a, hw_grid());
+}
+
 // Surrogate-gradient backward of the top LIF (+ pred): one thread per pixel; BN/neuron
 // sums into acc (block partials, fp64 atomics).
-template <int C, bool PRED>
-__global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
+template <int C, bool PRED, int NTH>
+__device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
     constexpr int NV = 3 * C + (PRED ? 2 * C + 2 : 0), Q = C / 4;
+    static_assert(NTH % NT == 0, "whole 256-thread parts");
     __shared__ LifCoef coef[C];
     __shared__ float meanv[C];
     const int tid = threadIdx.x;
     const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
-    const int64_t p = (int64_t)blockIdx.x * NT + tid;
+    const int64_t p = (int64_t)g.bid * NTH + tid;
     const bool act = p < npix;
     const int64_t pc = act ? p : npix - 1;
     const int64_t b = pc / HWp, hw = pc - b * HWp;
@@ -588,8 +615,14 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
             v[5 * C + 1] += gpre[1];
         }
     }
-    if (!PROBE_OFF(4)) block_atomic_sum<NV>(v, acc_shard(a.acc, SNNFLOW_BWD_ACC(C)));
-    zero_consumed(a.zero0, a.zero1, a.zero_n);  // last: no load waits behind these stores
+    double* acc = acc_shard(a.acc, SNNFLOW_BWD_ACC(C), g.bid);
+    if (!PROBE_OFF(4)) block_atomic_sum_parts<NV, NTH / NT>(v, [acc](int, int j) { return acc + j; });
+    zero_consumed(a.zero0, a.zero1, a.zero_n, g);  // last: no load waits behind these stores
+}
+
+template <int C, bool PRED>
+__global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
+    lif_bwd_body<C, PRED, NT>(a, hw_grid());
 }
 
 // BatchNorm backward of one float4 of channels (torch batch_norm_cpu_backward, train):
@@ -609,7 +642,15 @@ __device__ inline float4 bn_bwd4(const float4& g, const float4& y, const BnBwdLd
 }
 
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
-__global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args a) {
+struct LayerBwdLds {
+    static constexpr bool WL = kWlds<CIN, C>;
+    static constexpr int G = HN * Pad<C>::v, WX = WL ? 9 * C * C : 0, WR = (WL && REC) ? 9 * C * C : 0;
+    static constexpr int FLOATS = G + WX + WR;
+};
+
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+__device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, float* lds) {
+    using LB = LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT>;
     constexpr int NTB = NT * SPLIT;
     constexpr int CI = CIN / SPLIT, CR = C / SPLIT;  // input / recurrent channels per thread group
     static_assert(CI * SPLIT == CIN && CR * SPLIT == C, "channel split");
@@ -618,7 +659,9 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     constexpr bool PF = Prefetch<C, NTB>::on;  // g_cur / y halos held in registers
     constexpr int NVP = LIF_IN ? 3 * CI : 1;
     constexpr int QI = CI / 4 > 0 ? CI / 4 : 1;  // float4s of this group's channels
-    __shared__ __attribute__((aligned(16))) float G[HN * PC];
+    float* G = lds;
+    [[maybe_unused]] float* wl_x = lds + LB::G;
+    [[maybe_unused]] float* wl_r = wl_x + LB::WX;
     __shared__ BnBwdLds bnp[C];
     __shared__ LifCoef pcoef[LIF_IN ? CIN : 1];
     __shared__ float pmean[LIF_IN ? CIN : 1];
@@ -626,7 +669,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     const int tid = threadIdx.x, pt = tid % NT, ty = pt / TW, tx = pt - ty * TW;
     const int part = thread_part(), ci0 = part * CI, cr0 = part * CR;
     const int H = a.H, W = a.W;
-    const Tile tl = block_tile(H, W);
+    const Tile tl = block_tile(H, W, g);
     const double N = (double)a.B * H * W;
     const float nf = (float)N;
     const int h = tl.h0 + ty, w = tl.w0 + tx;
@@ -638,9 +681,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     TRACE_AT(TR, TK, 0);
 
     // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS)
-    constexpr bool WL = kWlds<CIN, C>;
-    __shared__ __attribute__((aligned(16))) float wl_x[WL ? 9 * C * C : 4];
-    __shared__ __attribute__((aligned(16))) float wl_r[WL && REC ? 9 * C * C : 4];
+    constexpr bool WL = LB::WL;
     WStage<WL ? 9 * C * C : 1, NTB> sw_x, sw_r;
     if constexpr (WL) {
         if (a.wt_bwd_ff) sw_x.load(a.wt_fwd_ff);
@@ -679,7 +720,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
         gamma = a.n.bn_weight[tid];
     }
     const NeuronGradRegs ngr =
-        load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b);
+        load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
     LifCoef pk = {0.f, 0.f, 0.f, 0.f};
     float pmu = 0.f;
     if constexpr (LIF_IN) {
@@ -693,7 +734,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     //    BN backward coefficients for the deferred weight gradient
     __shared__ double sums[SNNFLOW_BWD_ACC(C)];
     acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
-    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b);
+    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
     if (tid < C) {
         const float mean = st_mean, inv = st_inv;
         BnBwdLds c;
@@ -709,7 +750,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
             c.gm = 0.0f;
         }
         bnp[tid] = c;
-        if (blockIdx.x == 0 && a.bnc_out) {
+        if (g.bid == 0 && a.bnc_out) {
             a.bnc_out[tid] = c.gm;
             a.bnc_out[C + tid] = c.k;
         }
@@ -722,7 +763,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
     }
     __syncthreads();
     TRACE_AT(TR, TK, 1);
-    zero_consumed(a.zero0, a.zero1, a.zero_n);  // after the gather (vmcnt counts stores)
+    zero_consumed(a.zero0, a.zero1, a.zero_n, g);  // after the gather (vmcnt counts stores)
 
     // 3. Stage A: BN backward on the halo -> G = dL/dy (pre-BN conv output of layer l)
     if constexpr (PF) {
@@ -863,7 +904,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
             }
         }
         TRACE_AT(TR, TK, 4);
-        double* acc = acc_shard(a.acc_out, SNNFLOW_BWD_ACC(CIN));
+        double* acc = acc_shard(a.acc_out, SNNFLOW_BWD_ACC(CIN), g.bid);
         if (!PROBE_OFF(4))
             block_atomic_sum_parts<NVP, SPLIT>(vd, [acc](int pp, int j) {
                 const int k = j / CI, jj = j - k * CI;
@@ -877,6 +918,12 @@ __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args
             for (int ci = 0; ci < CI; ++ci) gb[(ci0 + ci) * a.gxs_c] = gx[ci];
         }
     }
+}
+
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+__global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args a) {
+    __shared__ __attribute__((aligned(16))) float pool[LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT>::FLOATS];
+    layer_bwd_body<CIN, C, LIF_IN, REC, SPLIT>(a, hw_grid(), pool);
 }
 
 // ---------------------------------------------------------------------------
@@ -1553,6 +1600,146 @@ __global__ void k_lif_export(const float* __restrict__ x, const float* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Wavefront launches (snnflow_fwd_slot / snnflow_bwd_slot): the blocks of one launch are
+// split into per-task ranges (each a multiple of 8 blocks, so a task's block -> tile map
+// keeps its XCD grouping); every block runs the body of its task's kernel variant on its
+// own range (Grid), out of one LDS pool sized for the largest variant.
+// ---------------------------------------------------------------------------
+constexpr int kSlotTasks = SNNFLOW_MAX_SLOT_TASKS;
+enum SlotKind : int {
+    SK_HEAD1, SK_HEAD2, SK_HEAD4, SK_HEAD5,  // conv of a cin-channel input (no LIF)
+    SK_PLAIN, SK_PLAIN_REC,                  // conv of a C-channel input (no LIF) [+ rec]
+    SK_LIF, SK_LIF_REC,                      // LIF(l-1) on the halo + conv(l) [+ rec]
+    SK_TOP, SK_TOP_PRED                      // LIF of the last layer [+ pred]
+};
+
+struct FwdSlotParams {
+    snnflow_conv_fwd_args conv[kSlotTasks];
+    snnflow_lif_fwd_args lif;
+    int kind[kSlotTasks], blk0[kSlotTasks], nblk[kSlotTasks];
+    int ntask;
+};
+struct BwdSlotParams {
+    snnflow_layer_bwd_args layer[kSlotTasks];
+    snnflow_lif_bwd_args lif;
+    int kind[kSlotTasks], blk0[kSlotTasks], nblk[kSlotTasks];
+    int ntask;
+};
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <int C>
+struct SlotLds {
+    static constexpr int FWD = cmax(cmax(cmax(ConvFwdLds<1, C, false, false, 2>::FLOATS, ConvFwdLds<2, C, false, false, 2>::FLOATS),
+                                         cmax(ConvFwdLds<4, C, false, false, 2>::FLOATS, ConvFwdLds<5, C, false, false, 2>::FLOATS)),
+                                    cmax(cmax(ConvFwdLds<C, C, false, false, 2>::FLOATS, ConvFwdLds<C, C, false, true, 2>::FLOATS),
+                                         cmax(ConvFwdLds<C, C, true, false, 2>::FLOATS, ConvFwdLds<C, C, true, true, 2>::FLOATS)));
+    static constexpr int BWD = cmax(cmax(LayerBwdLds<2, C, false, false, 2>::FLOATS, LayerBwdLds<4, C, false, false, 2>::FLOATS),
+                                    cmax(cmax(LayerBwdLds<C, C, false, false, 2>::FLOATS, LayerBwdLds<C, C, false, true, 2>::FLOATS),
+                                         cmax(LayerBwdLds<C, C, true, false, 2>::FLOATS, LayerBwdLds<C, C, true, true, 2>::FLOATS)));
+};
+
+// A by-value copy of a kernarg-resident struct (dword loads from the constant address
+// space: scalar loads; the fields a body never reads are dead and vanish).
+template <typename T>
+__device__ inline T kernarg_copy(const __attribute__((address_space(4))) T* p) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized struct");
+    T r;
+    const __attribute__((address_space(4))) int* src = (const __attribute__((address_space(4))) int*)p;
+    int* dst = reinterpret_cast<int*>(&r);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) dst[i] = src[i];
+    return r;
+}
+
+// Task of this block (block ranges ascending; ntask <= kSlotTasks) and its Grid.
+template <typename P>
+__device__ inline int slot_task(const __attribute__((address_space(4))) P* pp, Grid& g) {
+    const int bid = blockIdx.x, nt = pp->ntask;
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < kSlotTasks; ++i)
+        if (i < nt && bid >= pp->blk0[i]) k = i;
+    g.bid = bid - pp->blk0[k];
+    g.nb = pp->nblk[k];
+    return k;
+}
+
+template <int C>
+__global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
+    typedef const __attribute__((address_space(4))) FwdSlotParams* cptr;
+    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+    Grid g;
+    const int k = slot_task(pp, g);
+    if (g.bid >= g.nb) return;  // padding block of a range
+    __shared__ __attribute__((aligned(16))) float pool[SlotLds<C>::FWD];
+    switch (pp->kind[k]) {
+#define FWD_CONV(KIND, ...)                                   \
+    case KIND: {                                              \
+        const snnflow_conv_fwd_args a = kernarg_copy(&pp->conv[k]);          \
+        conv_fwd_body<__VA_ARGS__>(a, g, pool);               \
+        break;                                                \
+    }
+        FWD_CONV(SK_HEAD1, 1, C, false, false, 2)
+        FWD_CONV(SK_HEAD2, 2, C, false, false, 2)
+        FWD_CONV(SK_HEAD4, 4, C, false, false, 2)
+        FWD_CONV(SK_HEAD5, 5, C, false, false, 2)
+        FWD_CONV(SK_PLAIN, C, C, false, false, 2)
+        FWD_CONV(SK_PLAIN_REC, C, C, false, true, 2)
+        FWD_CONV(SK_LIF, C, C, true, false, 2)
+        FWD_CONV(SK_LIF_REC, C, C, true, true, 2)
+#undef FWD_CONV
+        case SK_TOP: {
+            const snnflow_lif_fwd_args a = kernarg_copy(&pp->lif);
+            lif_fwd_body<C, false, NT * 2>(a, g);
+            break;
+        }
+        case SK_TOP_PRED: {
+            const snnflow_lif_fwd_args a = kernarg_copy(&pp->lif);
+            lif_fwd_body<C, true, NT * 2>(a, g);
+            break;
+        }
+        default: break;
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(NT * 2) void k_bwd_slot(BwdSlotParams) {
+    typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
+    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+    Grid g;
+    const int k = slot_task(pp, g);
+    if (g.bid >= g.nb) return;
+    __shared__ __attribute__((aligned(16))) float pool[SlotLds<C>::BWD];
+    switch (pp->kind[k]) {
+#define BWD_LAYER(KIND, ...)                                  \
+    case KIND: {                                              \
+        const snnflow_layer_bwd_args a = kernarg_copy(&pp->layer[k]);        \
+        layer_bwd_body<__VA_ARGS__>(a, g, pool);              \
+        break;                                                \
+    }
+        BWD_LAYER(SK_HEAD2, 2, C, false, false, 2)
+        BWD_LAYER(SK_HEAD4, 4, C, false, false, 2)
+        BWD_LAYER(SK_PLAIN, C, C, false, false, 2)
+        BWD_LAYER(SK_PLAIN_REC, C, C, false, true, 2)
+        BWD_LAYER(SK_LIF, C, C, true, false, 2)
+        BWD_LAYER(SK_LIF_REC, C, C, true, true, 2)
+#undef BWD_LAYER
+        case SK_TOP: {
+            const snnflow_lif_bwd_args a = kernarg_copy(&pp->lif);
+            lif_bwd_body<C, false, NT * 2>(a, g);
+            break;
+        }
+        case SK_TOP_PRED: {
+            const snnflow_lif_bwd_args a = kernarg_copy(&pp->lif);
+            lif_bwd_body<C, true, NT * 2>(a, g);
+            break;
+        }
+        default: break;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host dispatch
 // ---------------------------------------------------------------------------
 bool valid_c(int c) { return c == 4 || c == 8 || c == 16 || c == 32; }
@@ -1650,13 +1837,18 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
     return snnflow_prep_weights_batch(&d, 1, stream);
 }
 
-int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
+static int conv_fwd_check(const snnflow_conv_fwd_args* a) {
     if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || !a->wt_ff || !a->y)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: bad args");
     if (a->cin == a->c && a->c % 8 == 0 && (!a->wt_ff_t || (a->wt_rec && !a->wt_rec_t)))
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: cin == c needs the backward-layout weights wt_ff_t / wt_rec_t");
     if (a->lif_in ? (!a->prev_y || !a->prev_state || (a->prev.bn_train && !a->prev_acc)) : !a->x)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: missing input");
+    return 0;
+}
+
+int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
+    if (const int e = conv_fwd_check(a)) return e;
     const hipStream_t s = (hipStream_t)stream;
     switch (a->c) {
         case 4: return conv_fwd_c<4>(*a, s);
@@ -1667,10 +1859,15 @@ int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream) {
     }
 }
 
-int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
+static int lif_fwd_check(const snnflow_lif_fwd_args* a) {
     if (!a || !a->y || !a->state || a->B <= 0 || a->H <= 0 || a->W <= 0 || (a->n.bn_train && !a->acc))
         SNN_FAIL(SNNFLOW_E_ARG, "lif_fwd: bad args");
     if (a->pred_w && (!a->pred_b || !a->flow)) SNN_FAIL(SNNFLOW_E_ARG, "lif_fwd: pred needs bias and flow");
+    return 0;
+}
+
+int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
+    if (const int e = lif_fwd_check(a)) return e;
     const hipStream_t s = (hipStream_t)stream;
     const dim3 grid(elem_grid((int64_t)a->B * a->H * a->W)), block(NT);
     const bool pred = a->pred_w != nullptr;
@@ -1688,10 +1885,15 @@ int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
     return 0;
 }
 
-int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
+static int lif_bwd_check(const snnflow_lif_bwd_args* a) {
     if (!a || !a->y || !a->stats || !a->g_cur || !a->acc) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: bad args");
+    if (a->pred_w && !a->flow) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: pred needs flow");
+    return 0;
+}
+
+int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
+    if (const int e = lif_bwd_check(a)) return e;
     const bool pred = a->pred_w != nullptr;
-    if (pred && !a->flow) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: pred needs flow");
     const hipStream_t s = (hipStream_t)stream;
     const dim3 grid(elem_grid((int64_t)a->B * a->H * a->W)), block(NT);
     switch (a->c) {
@@ -1708,7 +1910,7 @@ int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
     return 0;
 }
 
-int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
+static int layer_bwd_check(const snnflow_layer_bwd_args* a) {
     if (!a || !a->y || !a->stats || !a->g_cur || !a->acc_in) SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: bad args");
     if (!a->ng.bn_weight || !a->ng.bn_bias || !a->ng.beta || !a->ng.threshold)
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: missing parameter-gradient buffers");
@@ -1718,6 +1920,11 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
     if (a->cin == a->c && a->c % 8 == 0 &&
         ((a->wt_bwd_ff && !a->wt_fwd_ff) || (a->wt_bwd_rec && a->g_state_prev && !a->wt_fwd_rec)))
         SNN_FAIL(SNNFLOW_E_ARG, "layer_bwd: cin == c needs the forward-layout weights wt_fwd_ff / wt_fwd_rec");
+    return 0;
+}
+
+int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
+    if (const int e = layer_bwd_check(a)) return e;
     const hipStream_t s = (hipStream_t)stream;
     switch (a->c) {
         case 4: return layer_bwd_c<4>(*a, s);
@@ -1726,6 +1933,113 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
         case 32: return layer_bwd_c<32>(*a, s);
         default: SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: c must be 4, 8, 16 or 32");
     }
+}
+
+// C = 8 only: one layer-step of C = 16 / 32 already fills the chip for a launch (and the
+// merged variants would spill registers there).
+static bool slot_c(int c) { return c == 8; }
+
+int snnflow_slot_supported(int c, int cin0) { return slot_c(c) && (cin0 == 2 || cin0 == 4) ? 1 : 0; }
+
+// Block ranges of the tasks: each a multiple of 8 blocks (XCD grouping of block_tile).
+static int slot_ranges(const int* nblk, int n, int* blk0) {
+    int b = 0;
+    for (int i = 0; i < n; ++i) {
+        blk0[i] = b;
+        b += (nblk[i] + 7) / 8 * 8;
+    }
+    return b;
+}
+
+int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow_lif_fwd_args* lif, void* stream) {
+    const int nt = nconv + (lif ? 1 : 0);
+    if (nconv < 0 || nt <= 0 || nt > kSlotTasks || (nconv && !conv)) SNN_FAIL(SNNFLOW_E_ARG, "fwd_slot: task count");
+    FwdSlotParams p = {};
+    const int c = nconv ? conv[0].c : lif->c;
+    const int B = nconv ? conv[0].B : lif->B, H = nconv ? conv[0].H : lif->H, W = nconv ? conv[0].W : lif->W;
+    if (!slot_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c must be 8");
+    for (int i = 0; i < nconv; ++i) {
+        const snnflow_conv_fwd_args& a = conv[i];
+        if (const int e = conv_fwd_check(&a)) return e;
+        if (a.c != c || a.B != B || a.H != H || a.W != W) SNN_FAIL(SNNFLOW_E_ARG, "fwd_slot: tasks of different shapes");
+        int kind;
+        if (a.lif_in) {
+            if (a.cin != c) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: lif_in requires cin == c");
+            kind = a.wt_rec ? SK_LIF_REC : SK_LIF;
+        } else if (a.wt_rec) {
+            if (a.cin != c) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: recurrent cell requires cin == c");
+            kind = SK_PLAIN_REC;
+        } else if (a.cin == c) {
+            kind = SK_PLAIN;
+        } else if (a.cin == 1 || a.cin == 2 || a.cin == 4 || a.cin == 5) {
+            kind = a.cin == 1 ? SK_HEAD1 : a.cin == 2 ? SK_HEAD2 : a.cin == 4 ? SK_HEAD4 : SK_HEAD5;
+        } else {
+            SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: unsupported cin");
+        }
+        p.conv[i] = a;
+        p.kind[i] = kind;
+        p.nblk[i] = snnflow_conv_blocks(B, H, W);
+    }
+    if (lif) {
+        if (const int e = lif_fwd_check(lif)) return e;
+        if (lif->c != c || lif->B != B || lif->H != H || lif->W != W)
+            SNN_FAIL(SNNFLOW_E_ARG, "fwd_slot: tasks of different shapes");
+        p.lif = *lif;
+        p.kind[nconv] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
+        p.nblk[nconv] = (int)(((int64_t)B * H * W + 2 * NT - 1) / (2 * NT));
+    }
+    p.ntask = nt;
+    const int nb = slot_ranges(p.nblk, nt, p.blk0);
+    const hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_fwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnflow_lif_bwd_args* lif,
+                     void* stream) {
+    const int nt = nlayer + (lif ? 1 : 0);
+    if (nlayer < 0 || nt <= 0 || nt > kSlotTasks || (nlayer && !layer)) SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: task count");
+    BwdSlotParams p = {};
+    const int c = nlayer ? layer[0].c : lif->c;
+    const int B = nlayer ? layer[0].B : lif->B, H = nlayer ? layer[0].H : lif->H, W = nlayer ? layer[0].W : lif->W;
+    if (!slot_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c must be 8");
+    for (int i = 0; i < nlayer; ++i) {
+        const snnflow_layer_bwd_args& a = layer[i];
+        if (const int e = layer_bwd_check(&a)) return e;
+        if (a.c != c || a.B != B || a.H != H || a.W != W) SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: tasks of different shapes");
+        int kind;
+        if (a.lif_in) {
+            if (a.cin != c) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: lif_in requires cin == c");
+            kind = a.wt_bwd_rec ? SK_LIF_REC : SK_LIF;
+        } else if (a.wt_bwd_rec) {
+            if (a.cin != c) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: recurrent cell requires cin == c");
+            kind = SK_PLAIN_REC;
+        } else if (a.cin == c) {
+            kind = SK_PLAIN;
+        } else if (a.cin == 2 || a.cin == 4) {
+            kind = a.cin == 2 ? SK_HEAD2 : SK_HEAD4;
+        } else {
+            SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: unsupported cin (2, 4 or c)");
+        }
+        p.layer[i] = a;
+        p.kind[i] = kind;
+        p.nblk[i] = snnflow_conv_blocks(B, H, W);
+    }
+    if (lif) {
+        if (const int e = lif_bwd_check(lif)) return e;
+        if (lif->c != c || lif->B != B || lif->H != H || lif->W != W)
+            SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: tasks of different shapes");
+        p.lif = *lif;
+        p.kind[nlayer] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
+        p.nblk[nlayer] = (int)(((int64_t)B * H * W + 2 * NT - 1) / (2 * NT));
+    }
+    p.ntask = nt;
+    const int nb = slot_ranges(p.nblk, nt, p.blk0);
+    const hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_bwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    SNN_CHECK_LAUNCH();
+    return 0;
 }
 
 int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {

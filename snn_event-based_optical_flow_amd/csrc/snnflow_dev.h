@@ -42,8 +42,13 @@ __host__ __device__ inline int tiles_per_image(int H, int W) {
 // Block -> tile.  Blocks b and b+8 share an XCD under round-robin dispatch; give each
 // XCD group a contiguous range of tiles so neighbouring tiles (shared halo rows) hit
 // the same L2.  Bijective for any grid size.  Speed only, never correctness.
-__device__ inline Tile block_tile(int H, int W) {
-    const int nb = gridDim.x, bid = blockIdx.x;
+// A kernel body's view of its grid: the hardware grid for a plain launch, or one task's
+// range of blocks inside a wavefront launch (several independent layer-steps per launch).
+struct Grid { int bid, nb; };
+__device__ inline Grid hw_grid() { return Grid{(int)blockIdx.x, (int)gridDim.x}; }
+
+__device__ inline Tile block_tile(int H, int W, const Grid& g) {
+    const int nb = g.nb, bid = g.bid;
     const int q = nb / 8, r = nb % 8, x = bid % 8;
     int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
     const int tw = (W + TW - 1) / TW, th = (H + TH - 1) / TH;
@@ -53,6 +58,7 @@ __device__ inline Tile block_tile(int H, int W) {
     tl.b = t / th;
     return tl;
 }
+__device__ inline Tile block_tile(int H, int W) { return block_tile(H, W, hw_grid()); }
 
 __device__ inline float wave_sum(float v) {
 #pragma unroll
@@ -86,7 +92,8 @@ constexpr int kAccShards = SNNFLOW_ACC_SHARDS;
 __host__ __device__ constexpr int acc_stride(int n) { return SNNFLOW_ACC_STRIDE(n); }
 
 // This block's replica of an accumulator of n sums.
-__device__ inline double* acc_shard(double* acc, int n) { return acc + (blockIdx.x % kAccShards) * acc_stride(n); }
+__device__ inline double* acc_shard(double* acc, int n, int bid) { return acc + (bid % kAccShards) * acc_stride(n); }
+__device__ inline double* acc_shard(double* acc, int n) { return acc_shard(acc, n, (int)blockIdx.x); }
 
 // p[i] as one unconditional 16-B load, or zeros when p is NULL (the load then reads
 // fallback[i], which must be valid).  A `p ? p[i] : 0` select makes the compiler split

@@ -425,12 +425,13 @@ __device__ void block_atomic_sum(const float (&v)[NV], double* acc) {
 
 // Accumulators already consumed by an earlier kernel of the chain are zeroed here
 // (grid-stride over all threads of the launch).
-__device__ inline void zero_consumed(double* z0, double* z1, int n) {
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+__device__ inline void zero_consumed(double* z0, double* z1, int n, const Grid& g) {
+    for (int j = g.bid * (int)blockDim.x + threadIdx.x; j < n; j += g.nb * (int)blockDim.x) {
         if (z0) z0[j] = 0.0;
         if (z1) z1[j] = 0.0;
     }
 }
+__device__ inline void zero_consumed(double* z0, double* z1, int n) { zero_consumed(z0, z1, n, hw_grid()); }
 
 // Totals of the M sums of a sharded accumulator (n sums per replica, M <= n, M <= NT)
 // into LDS out[M]: TPJ = NT/M threads per sum each add a strided subset of the

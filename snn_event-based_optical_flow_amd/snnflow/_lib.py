@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 
 class Neuron(ctypes.Structure):
@@ -190,7 +190,11 @@ EXPORTS = {
     "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
+    "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
+    "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),
+    "snnflow_slot_supported": (I32, [I32, I32]),
 }
+MAX_SLOT_TASKS = 4
 
 
 def _load():

@@ -163,6 +163,10 @@ class FireNetEngine:
         self.pending = []   # per-step tensors of the open backward chain (deferred wgrad)
         self.prep_stale = True  # re-prepare weights at the next forward (set after each backward)
 
+    def sequence_ok(self, cin0):
+        """True if FireNetSequence's wavefront launches take this model (C = 8, cin0 2 or 4)."""
+        return bool(lib.snnflow_slot_supported(self.C, cin0))
+
     # parameter order = Function input order after the states
     def param_list(self):
         ps = []
@@ -283,6 +287,90 @@ def _spk_half(state_nhwc):
     return base, (H * W * C, 1, W * C, C)
 
 
+
+# ---------------------------------------------------------------------------
+# Kernel arguments of one time step (shared by the per-step and the sequence Functions)
+# ---------------------------------------------------------------------------
+def _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, facc, neurons, train, wfwd, wbwd):
+    """Forward kernel K_l (l < L) of one step: conv(head) for l == 0, else LIF(l-1) on the
+    halo + conv(l).  facc[l]: layer l's BatchNorm batch-sum accumulator."""
+    a = _lib.ConvFwdArgs()
+    a.B, a.H, a.W, a.c = B, H, W, eng.C
+    if l == 0:
+        a.cin, a.lif_in = cin0, 0
+        a.x = ptr(x)
+        a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
+    else:
+        a.cin, a.lif_in = eng.C, 1
+        a.prev_y, a.prev_mem = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1])
+        a.prev_acc, a.prev_stats = ptr(facc[l - 1]), ptr(stats[l - 1])
+        a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
+    a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
+    a.wt_ff_t, a.wt_rec_t = ptr(wbwd[l][0]), ptr(wbwd[l][1])  # MFMA B operand layout
+    a.s_prev = _ptr_t(s_prev[l])
+    a.y, a.acc = ptr(ys[l]), (ptr(facc[l]) if train[l] else None)
+    return a
+
+
+def _fwd_top_args(eng, B, H, W, ys, stats, states, mem_in, facc, neurons, flow):
+    """Forward kernel K_L of one step: LIF of the last layer + pred."""
+    L = eng.L
+    f = _lib.LifFwdArgs()
+    f.B, f.H, f.W, f.c = B, H, W, eng.C
+    f.y, f.mem, f.acc, f.stats = ptr(ys[L - 1]), _ptr_t(mem_in[L - 1]), ptr(facc[L - 1]), ptr(stats[L - 1])
+    f.n, f.state = neurons[L - 1], ptr(states[L - 1])
+    f.pred_w, f.pred_b, f.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), ptr(flow)
+    return f
+
+
+def _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, gcur, gmem, bacc):
+    """Backward kernel of the top of one step: pred backward + LIF backward of layer L-1.
+    g_flow: dL/dflow with unit W and channel-plane strides, or None."""
+    top = eng.L - 1
+    b = _lib.LifBwdArgs()
+    b.B, b.H, b.W, b.c = B, H, W, eng.C
+    b.y, b.mem, b.stats, b.n = ptr(ys[top]), _ptr_t(mem_in[top]), ptr(stats[top]), neurons[top]
+    b.g_state = _ptr_t(gst[top])
+    b.pred_w, b.flow = ptr(eng.pred.weight), ptr(flow)
+    if g_flow is not None:
+        b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
+    b.g_cur, b.g_mem = ptr(gcur[top]), _ptr_t(gmem[top])
+    b.acc = ptr(bacc[top])
+    return b
+
+
+def _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur, gmem, bacc, bnc, glayers, gpw, gpb,
+                    acc, wfwd, wbwd, g_prev, ext, gx):
+    """Backward kernel of layer l of one step: BN backward + dgrad of layer l's convs
+    [+ LIF backward of layer l-1]; gx: input gradient of the head (l == 0) or None."""
+    C, L = eng.C, eng.L
+    a = _lib.LayerBwdArgs()
+    a.B, a.H, a.W, a.c = B, H, W, C
+    a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(ys[l]), ptr(stats[l]), ptr(gcur[l]), ptr(bacc[l]), neurons[l]
+    a.ng, a.accumulate, a.bnc_out = glayers[l][2], acc, ptr(bnc[l])
+    if l == L - 1:
+        a.has_pred, a.g_pred_w, a.g_pred_b = 1, ptr(gpw), ptr(gpb)
+    if eng.rec[l]:
+        a.wt_bwd_rec, a.wt_fwd_rec = ptr(wbwd[l][1]), ptr(wfwd[l][1])
+        if g_prev[l] is not None:
+            a.g_state_prev = ptr(g_prev[l])
+            a.zero_mem_half = 0 if ext[l] else 1
+    if l > 0:
+        a.cin, a.lif_in = C, 1
+        a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[l][0]), ptr(wfwd[l][0])
+        a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
+        a.prev_g_state = _ptr_t(gst[l - 1])
+        a.prev_g_cur, a.prev_g_mem = ptr(gcur[l - 1]), _ptr_t(gmem[l - 1])
+        a.acc_out = ptr(bacc[l - 1])
+    else:
+        a.cin, a.lif_in = cin0, 0
+        if gx is not None:
+            a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[0][0]), ptr(wfwd[0][0])
+            a.g_x = ptr(gx)
+            a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
+    return a
+
+
 class FireNetStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, eng, x, *rest):
@@ -333,36 +421,17 @@ class FireNetStep(torch.autograd.Function):
         zn = facc.shape[1]
         try:
             # K0: conv(head)  (zeroes fwd_acc[L-1], consumed by the previous step's last kernel)
-            a = _lib.ConvFwdArgs()
-            a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, cin0, C, 0
-            a.x = ptr(x)
-            a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
-            a.wt_ff, a.wt_rec = ptr(wfwd[0][0]), ptr(wfwd[0][1])
-            a.wt_ff_t, a.wt_rec_t = ptr(wbwd[0][0]), ptr(wbwd[0][1])
-            a.s_prev = _ptr_t(s_prev[0])
-            a.y, a.acc = ptr(ys[0]), (ptr(facc[0]) if train[0] else None)
-            a.zero0, a.zero_n = ptr(facc[L - 1]), zn
-            _lib.call("conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
             # K_l: LIF(l-1) on the halo + conv(l)  (zeroes fwd_acc[l-2], consumed by K_{l-1})
-            for l in range(1, L):
-                a = _lib.ConvFwdArgs()
-                a.B, a.H, a.W, a.cin, a.c, a.lif_in = B, H, W, C, C, 1
-                a.prev_y, a.prev_mem = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1])
-                a.prev_acc, a.prev_stats = ptr(facc[l - 1]), ptr(stats[l - 1])
-                a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
-                a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
-                a.wt_ff_t, a.wt_rec_t = ptr(wbwd[l][0]), ptr(wbwd[l][1])  # MFMA B operand layout
-                a.s_prev = _ptr_t(s_prev[l])
-                a.y, a.acc = ptr(ys[l]), (ptr(facc[l]) if train[l] else None)
-                if l >= 2:
+            for l in range(L):
+                a = _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, facc, neurons,
+                                   train, wfwd, wbwd)
+                if l == 0:
+                    a.zero0, a.zero_n = ptr(facc[L - 1]), zn
+                elif l >= 2:
                     a.zero0, a.zero_n = ptr(facc[l - 2]), zn
-                _lib.call(f"conv_fwd[{l}]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
+                _lib.call(f"conv_fwd[{l}]" if l else "conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
             # K_L: LIF of the last layer + pred  (zeroes fwd_acc[L-2])
-            f = _lib.LifFwdArgs()
-            f.B, f.H, f.W, f.c = B, H, W, C
-            f.y, f.mem, f.acc, f.stats = ptr(ys[L - 1]), _ptr_t(mem_in[L - 1]), ptr(facc[L - 1]), ptr(stats[L - 1])
-            f.n, f.state = neurons[L - 1], ptr(states[L - 1])
-            f.pred_w, f.pred_b, f.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), ptr(flow)
+            f = _fwd_top_args(eng, B, H, W, ys, stats, states, mem_in, facc, neurons, flow)
             if L >= 2:
                 f.zero0, f.zero_n = ptr(facc[L - 2]), zn
             _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
@@ -439,50 +508,20 @@ class FireNetStep(torch.autograd.Function):
         # 2.48 -> 2.72 ms per cfg2 train step)
         try:
             # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
-            top = L - 1
-            b = _lib.LifBwdArgs()
-            b.B, b.H, b.W, b.c = B, H, W, C
-            b.y, b.mem, b.stats, b.n = ptr(ys[top]), _ptr_t(mem_in[top]), ptr(stats[top]), neurons[top]
-            b.g_state = _ptr_t(gst[top])
-            b.pred_w, b.flow = ptr(eng.pred.weight), ptr(flow)
-            if g_flow is not None:
-                if g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32:
-                    g_flow = g_flow.contiguous().float()
-                b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
-            b.g_cur, b.g_mem = ptr(gcur[top]), _ptr_t(gmem[top])
-            b.acc = ptr(bacc[top])
+            if g_flow is not None and (g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32):
+                g_flow = g_flow.contiguous().float()
+            b = _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, gcur, gmem, bacc)
             b.zero0, b.zero_n = ptr(bacc[0]), zn
             _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
 
             gx = None
+            if ctx.needs_input_grad[1]:
+                gx = torch.empty_like(x)
             for l in range(L - 1, -1, -1):
-                a = _lib.LayerBwdArgs()
-                a.B, a.H, a.W, a.c = B, H, W, C
-                a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(ys[l]), ptr(stats[l]), ptr(gcur[l]), ptr(bacc[l]), neurons[l]
-                a.ng, a.accumulate, a.bnc_out = glayers[l][2], acc, ptr(bnc[l])
-                if l == L - 1:
-                    a.has_pred, a.g_pred_w, a.g_pred_b = 1, ptr(gpw), ptr(gpb)
+                a = _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur, gmem, bacc, bnc,
+                                    glayers, gpw, gpb, acc, wfwd, wbwd, g_prev, ctx.ext, gx)
                 if l + 1 <= L - 1:
                     a.zero0, a.zero_n = ptr(bacc[l + 1]), zn
-                if eng.rec[l]:
-                    a.wt_bwd_rec, a.wt_fwd_rec = ptr(wbwd[l][1]), ptr(wfwd[l][1])
-                    if g_prev[l] is not None:
-                        a.g_state_prev = ptr(g_prev[l])
-                        a.zero_mem_half = 0 if ctx.ext[l] else 1
-                if l > 0:
-                    a.cin, a.lif_in = C, 1
-                    a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[l][0]), ptr(wfwd[l][0])
-                    a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
-                    a.prev_g_state = _ptr_t(gst[l - 1])
-                    a.prev_g_cur, a.prev_g_mem = ptr(gcur[l - 1]), _ptr_t(gmem[l - 1])
-                    a.acc_out = ptr(bacc[l - 1])
-                else:
-                    a.cin, a.lif_in = cin0, 0
-                    if ctx.needs_input_grad[1]:
-                        gx = torch.empty_like(x)
-                        a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[0][0]), ptr(wfwd[0][0])
-                        a.g_x = ptr(gx)
-                        a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
                 _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
             if ctx.root:
                 eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s)
@@ -511,3 +550,210 @@ def _ptr_t(t):
 
 def _ptr_nhwc_spk(t):
     return None if t is None else t.data_ptr()
+
+
+# ---------------------------------------------------------------------------
+# A whole truncated-BPTT window in one autograd node, launched in wavefront order
+# ---------------------------------------------------------------------------
+def wavefront_slots(T, K):
+    """Launch order of a (kernel k < K, step t < T) grid whose task (k, t) reads the outputs of
+    (k-1, t), (k, t-1) and (k+1, t-1) (the spikes of a recurrent layer come out of the next
+    kernel of the previous step): task (k, t) runs in launch k + 2t, so every launch holds
+    mutually independent tasks and follows all of its inputs' launches.
+    Returns [[(k, t), ...] per launch]."""
+    slots = [[] for _ in range(K + 2 * (T - 1))]
+    for t in range(T):
+        for k in range(K):
+            slots[k + 2 * t].append((k, t))
+    return slots
+
+
+class FireNetSequence(torch.autograd.Function):
+    """T fused time steps of the network as one autograd node (``forward_sequence``).
+
+    Same arithmetic per (layer, step) as T FireNetStep calls; the L+1 kernels of every step are
+    issued as wavefront launches (``wavefront_slots``, ``snnflow_fwd_slot`` /
+    ``snnflow_bwd_slot``) that each run up to four independent layer-steps: a single
+    layer-step of C = 8 at 128x128 occupies the chip for one latency-bound block round, so
+    the (L+1) x T launches of the per-step path are replaced by 2(T-1)+L+1.  Batch-sum
+    accumulators are per (step, layer) and zeroed once per call.  Inputs: eng, T, x_0..x_{T-1},
+    initial states (L), parameters; outputs: flow_0..flow_{T-1}, final states (L)."""
+
+    @staticmethod
+    def forward(ctx, eng, T, *rest):
+        L, C = eng.L, eng.C
+        xs = list(rest[:T])
+        prev = list(rest[T:T + L])
+        B, cin0, H, W = xs[0].shape
+        dev = xs[0].device
+        for x in xs:
+            _lib.require_device(x, "event tensor")
+            if tuple(x.shape) != (B, cin0, H, W):
+                raise _lib.SnnflowError("forward_sequence: every step's input must have the same shape")
+        s = _lib.stream_ptr(dev)
+        ws = eng.workspace(B, H, W, dev)
+        wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale)
+        eng.prep_stale = False
+        cells = eng.cells
+
+        ys = torch.empty(T, L, B, H, W, C, device=dev)
+        stats = torch.empty(T, L, 2, C, device=dev)
+        n1 = 2 * B * H * W * C
+        st_all = torch.empty(T, L * n1, device=dev)
+        states = [[st_all[t, l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
+                   for l in range(L)] for t in range(T)]
+        flows = [torch.empty(B, 2, H, W, device=dev) for _ in range(T)]
+        facc = torch.zeros(T, L, _lib.acc_storage(2 * C), dtype=torch.float64, device=dev)
+
+        # step 0 reads the initial states (as FireNetStep); step t > 0 the states of step t-1
+        mem0, sprev0 = [], []
+        root = True
+        ext = [False] * L
+        for l in range(L):
+            p = prev[l]
+            if p is None:
+                cache = cells[l].lif.mem
+                mem0.append(cache if (cache is not None and tuple(cache.shape) == (B, C, H, W)
+                                      and cache.device == dev) else None)
+                sprev0.append(None)
+            else:
+                pn = as_nhwc_state(p)
+                mem0.append(pn[0])
+                sprev0.append(pn[1] if eng.rec[l] else None)
+                ours = getattr(p.grad_fn, "eng", None) is eng
+                if eng.rec[l] and p.requires_grad and ours:
+                    root = False
+                ext[l] = p.requires_grad and not ours
+        mem_in = [mem0] + [[states[t - 1][l][0] for l in range(L)] for t in range(1, T)]
+        s_prev = [sprev0] + [[states[t - 1][l][1] if eng.rec[l] else None for l in range(L)] for t in range(1, T)]
+        neurons = [neuron_struct(c) for c in cells]
+        train = [c.bn.training or not c.bn.track_running_stats for c in cells]
+
+        for tasks in wavefront_slots(T, L + 1):
+            convs, top = [], None
+            for k, t in tasks:
+                if k < L:
+                    convs.append(_fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
+                                                s_prev[t], facc[t], neurons, train, wfwd, wbwd))
+                else:
+                    top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons, flows[t])
+            arr = (_lib.ConvFwdArgs * max(len(convs), 1))(*convs)
+            _lib.call("fwd_slot", lib.snnflow_fwd_slot, arr, len(convs), ctypes.byref(top) if top is not None else None, s)
+
+        for l in range(L):
+            cells[l].lif.mem = states[T - 1][l][0].detach()
+
+        ctx.eng = eng
+        ctx.T = T
+        ctx.root = root
+        ctx.ext = ext
+        ctx.shape = (B, H, W, cin0)
+        ctx.has_prev = [p is not None for p in prev]
+        ctx.has_mem = [m is not None for m in mem0]
+        saved = xs + flows + [ys, stats, st_all]
+        saved += [m for m in mem0 if m is not None]
+        saved += [sp for sp in sprev0 if sp is not None]
+        ctx.save_for_backward(*saved)
+        ctx.set_materialize_grads(False)
+        return (*flows, *states[T - 1])
+
+    @staticmethod
+    def backward(ctx, *grads):
+        eng, T = ctx.eng, ctx.T
+        L, C = eng.L, eng.C
+        B, H, W, cin0 = ctx.shape
+        g_flows, g_final = list(grads[:T]), list(grads[T:T + L])
+        saved = list(ctx.saved_tensors)
+        xs, flows = saved[:T], saved[T:2 * T]
+        ys, stats, st_all = saved[2 * T:2 * T + 3]
+        rest = saved[2 * T + 3:]
+        n1 = 2 * B * H * W * C
+        states = [[st_all[t, l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
+                   for l in range(L)] for t in range(T)]
+        mem0 = [rest.pop(0) if ctx.has_mem[l] else None for l in range(L)]
+        sprev0 = [rest.pop(0) if (ctx.has_prev[l] and eng.rec[l]) else None for l in range(L)]
+        mem_in = [mem0] + [[states[t - 1][l][0] for l in range(L)] for t in range(1, T)]
+        s_prev = [sprev0] + [[states[t - 1][l][1] if eng.rec[l] else None for l in range(L)] for t in range(1, T)]
+
+        dev = xs[0].device
+        s = _lib.stream_ptr(dev)
+        eng.workspace(B, H, W, dev)
+        ws = eng.ws
+        wfwd, wbwd = eng.prep_weights(s, refresh=False)
+        fresh = not eng.bwd_open
+        if fresh:
+            eng.open_chain(dev)
+        glayers, gpw, gpb = eng.grad_views()
+        neurons = [neuron_struct(c) for c in eng.cells]
+        bacc = torch.zeros(T, L, _lib.acc_storage(_lib.bwd_acc_len(C)), dtype=torch.float64, device=dev)
+        gcur = torch.empty(T, L, B, H, W, C, device=dev)
+        bnc = torch.empty(T, L, 2, C, device=dev)
+
+        # gradients flowing into the states of step t: from the caller for the last step, from
+        # step t+1's recurrent dgrad (spike half; membrane half zero-filled) for the others
+        g_into = [None] * T   # g_into[t][l]: dL/d state_t[l]
+        g_into[T - 1] = [as_nhwc_state(g) if g is not None else None for g in g_final]
+        g_out = [None] * T    # g_out[t][l]: dL/d (state input of step t)[l], written by step t's backward
+        for t in range(T - 1, 0, -1):
+            g_out[t] = [empty_state(B, C, H, W, dev) if eng.rec[l] else None for l in range(L)]
+            g_into[t - 1] = g_out[t]
+        g0 = [None] * L
+        for l in range(L):
+            if not (ctx.has_prev[l] and ctx.needs_input_grad[2 + T + l]):
+                continue
+            if ctx.ext[l]:
+                g0[l] = torch.zeros((2, B, C, H, W), device=dev).as_strided(
+                    (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
+            elif eng.rec[l]:
+                g0[l] = empty_state(B, C, H, W, dev)
+        g_out[0] = g0
+        ext = [[False] * L] * T
+        ext[0] = ctx.ext
+        gmem = [[None] * L for _ in range(T)]
+        gmem[0] = [g0[l] if (g0[l] is not None and ctx.ext[l]) else None for l in range(L)]
+        gxs = [torch.empty_like(xs[t]) if ctx.needs_input_grad[2 + t] else None for t in range(T)]
+        gfl = []
+        for g in g_flows:
+            if g is not None and (g.stride(3) != 1 or g.stride(2) != W or g.dtype != torch.float32):
+                g = g.contiguous().float()
+            gfl.append(g)
+
+        # the deferred weight gradients see the steps in the per-step path's order (last first)
+        for t in range(T - 1, -1, -1):
+            eng.pending.append((gcur[t], bnc[t], ys[t], stats[t], xs[t], states[t], s_prev[t]))
+        try:
+            # backward kernel j of step t: j = 0 top (pred + LIF of layer L-1), j >= 1 layer L-j;
+            # in reversed time tau = T-1-t the dependencies have the forward's shape
+            for tasks in wavefront_slots(T, L + 1):
+                layers, top = [], None
+                for j, tau in tasks:
+                    t = T - 1 - tau
+                    acc = 0 if (fresh and t == T - 1) else 1
+                    if j == 0:
+                        top = _bwd_top_args(eng, B, H, W, ys[t], stats[t], mem_in[t], neurons, g_into[t], gfl[t],
+                                            flows[t], gcur[t], gmem[t], bacc[t])
+                    else:
+                        l = L - j
+                        layers.append(_bwd_layer_args(eng, l, B, H, W, cin0, ys[t], stats[t], mem_in[t], neurons,
+                                                      g_into[t], gcur[t], gmem[t], bacc[t], bnc[t], glayers, gpw, gpb,
+                                                      acc, wfwd, wbwd, g_out[t], ext[t], gxs[t] if l == 0 else None))
+                arr = (_lib.LayerBwdArgs * max(len(layers), 1))(*layers)
+                _lib.call("bwd_slot", lib.snnflow_bwd_slot, arr, len(layers),
+                          ctypes.byref(top) if top is not None else None, s)
+            if ctx.root:
+                eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s)
+        except Exception:
+            ws.reset_acc()
+            eng.bwd_open = False
+            eng.pending = []
+            eng.prep_stale = True
+            raise
+
+        pgrads = [None] * len(eng.flat_layout)
+        if ctx.root:
+            pgrads = [eng.flat[o:o + n].view(shp) for o, n, shp in eng.flat_layout]
+            eng.flat_views = None
+            eng.bwd_open = False
+            eng.last_flat = eng.flat
+            eng.prep_stale = True
+        return (None, None, *gxs, *g0, *pgrads)

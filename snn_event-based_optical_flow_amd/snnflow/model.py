@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 
 from .cells import ConvLayer, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
-from .engine import FireNetEngine, FireNetStep
+from .engine import FireNetEngine, FireNetSequence, FireNetStep
 
 
 class BaseModel(nn.Module):
@@ -102,7 +102,7 @@ class _FireNetBase(BaseModel):
         mods = [getattr(self, n) for n, _ in self.layer_spec] + [self.pred]
         return any(m._forward_hooks or m._forward_pre_hooks for m in mods)
 
-    def forward(self, event_voxel=None, event_cnt=None, log=False, return_dict=True):
+    def _input(self, event_voxel, event_cnt):
         if self.encoding == "voxel":
             x = event_voxel
         elif self.encoding == "cnt" and self.num_bins == 2:
@@ -114,7 +114,36 @@ class _FireNetBase(BaseModel):
             nz = x != 0
             mean, std = x[nz].mean(), x[nz].std()
             x[nz] = (x[nz] - mean) / std
-        x = x.float()
+        return x.float()
+
+    def forward_sequence(self, event_voxels=None, event_cnts=None, log=False):
+        """T consecutive time steps in one call (not in the reference; its training loop calls
+        ``forward`` once per window, ``train_flow.py:232-279``).  Same results, states and
+        ``lif.mem`` caches as T ``forward`` calls -- returns their T result dicts -- with the
+        steps' kernels issued as wavefront launches (engine.FireNetSequence).  Falls back to T
+        ``forward`` calls where those launches do not apply (hooks, ``log``, C != 8)."""
+        seq = event_voxels if self.encoding == "voxel" else event_cnts
+        T = len(seq)
+        none = [None] * T
+        pairs = list(zip(event_voxels if event_voxels is not None else none, event_cnts if event_cnts is not None else none))
+        if T == 0:
+            return []
+        xs = [self._input(v, c) for v, c in pairs]
+        eng = self.engine
+        if T == 1 or log or self._hooked() or not xs[0].is_cuda or not eng.sequence_ok(xs[0].shape[1]):
+            outs = []
+            for x in xs:  # already encoded / normalised: feed through the per-step path
+                outs.append(self._step(x, log))
+            return outs
+        res = FireNetSequence.apply(eng, T, *xs, *self._states, *eng.param_list())
+        self._states = list(res[T:])
+        return [{"flow": [f], "activity": None} for f in res[:T]]
+
+    def forward(self, event_voxel=None, event_cnt=None, log=False, return_dict=True):
+        out = self._step(self._input(event_voxel, event_cnt), log)
+        return out if return_dict else out["flow"][0]
+
+    def _step(self, x, log):
         if self._hooked():
             h, outs = x, []
             for i, (name, _) in enumerate(self.layer_spec):
@@ -127,8 +156,6 @@ class _FireNetBase(BaseModel):
             flow, new_states = res[0], list(res[1:])
             self._states = new_states
             outs = [st[1] for st in new_states]
-        if not return_dict:
-            return flow
         activity = None
         if isinstance(log, bool) and log and not self.exporting:
             names = ["0:input"] + [f"{i + 1}:{n}" for i, (n, _) in enumerate(self.layer_spec)]

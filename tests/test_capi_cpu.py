@@ -92,3 +92,25 @@ def test_product_path_refuses_cpu_tensors():
     model = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8))
     with pytest.raises(snnflow._lib.SnnflowError):
         model(None, torch.zeros(1, 2, 16, 16))
+
+
+def test_wavefront_slots_respect_dependencies():
+    """Every (kernel k, step t) task appears once; its inputs (k-1, t), (k, t-1), (k+1, t-1)
+    run in strictly earlier launches; a launch never holds more than SNNFLOW_MAX_SLOT_TASKS."""
+    from snnflow import _lib
+    from snnflow.engine import wavefront_slots
+
+    for T in (1, 2, 5, 10):
+        for K in (6, 8):
+            slots = wavefront_slots(T, K)
+            where = {}
+            for i, tasks in enumerate(slots):
+                assert 0 < len(tasks) <= _lib.MAX_SLOT_TASKS
+                for task in tasks:
+                    assert task not in where
+                    where[task] = i
+            assert len(where) == T * K
+            for (k, t), i in where.items():
+                for dep in ((k - 1, t), (k, t - 1), (k + 1, t - 1)):
+                    if dep in where:
+                        assert where[dep] < i, (T, K, k, t, dep)

@@ -682,3 +682,102 @@ def test_event_warping_bands_and_empty_windows_vs_oracle(dev, H, W, Ns):
             assert gd is None or float(gd.abs().max()) == 0.0
             continue
         assert _rel(gd.cpu().numpy(), gc.numpy()) < 1e-4, t
+
+
+# ---------------------------------------------------------------------------
+# Wavefront sequence path (forward_sequence) against the per-step path
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("H,W,T", [(64, 64, 5), (40, 72, 3)])
+def test_forward_sequence_matches_per_step(dev, H, W, T):
+    """T steps through model.forward_sequence (wavefront launches, FireNetSequence) against T
+    model.forward calls (FireNetStep) of an identical copy: flows, loss, every parameter
+    gradient, final states, lif.mem caches and BatchNorm running statistics, over two
+    truncated-BPTT windows (the second starts from the first's detached states).  The
+    per-(layer, step) arithmetic is the same code; only fp64 batch-sum atomics may add in
+    another order, so the tolerances are near-exact."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(5)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    ea, eb = snnflow.EventWarping(cfg, dev), snnflow.EventWarping(cfg, dev)
+    gen = torch.Generator(device=dev).manual_seed(13)
+    for it in range(2):
+        wins = [make_window(2, 300, H, W, gen, dev) for _ in range(T)]
+        fa = [ma(w["event_voxel"], w["event_cnt"])["flow"][0] for w in wins]
+        outs = mb.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+        assert len(outs) == T
+        for t, w in enumerate(wins):
+            ea.event_flow_association([fa[t]], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            eb.event_flow_association(outs[t]["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            np.testing.assert_allclose(outs[t]["flow"][0].detach().cpu().numpy(), fa[t].detach().cpu().numpy(),
+                                       rtol=1e-5, atol=1e-7, err_msg=f"flow it {it} t {t}")
+        la, lb = ea(), eb()
+        ma.zero_grad(set_to_none=True)
+        mb.zero_grad(set_to_none=True)
+        la.backward()
+        lb.backward()
+        np.testing.assert_allclose(lb.item(), la.item(), rtol=1e-6)
+        for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
+            assert _rel(b.grad.cpu().numpy(), a.grad.cpu().numpy()) < 1e-5, (it, n)
+        for sa, sb in zip(ma.states, mb.states):
+            np.testing.assert_allclose(sb.detach().cpu().numpy(), sa.detach().cpu().numpy(), rtol=1e-5, atol=1e-6)
+        for (n, a), (_, b) in zip(ma.named_buffers(), mb.named_buffers()):
+            np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=1e-7, err_msg=n)
+        for n, _ in ma.layer_spec:
+            np.testing.assert_allclose(getattr(mb, n).lif.mem.cpu().numpy(), getattr(ma, n).lif.mem.cpu().numpy(),
+                                       rtol=1e-5, atol=1e-6)
+        ma.detach_states()
+        mb.detach_states()
+        ea.reset()
+        eb.reset()
+
+
+def test_forward_sequence_input_and_state_grads(dev):
+    """Gradients into the sequence's inputs and into initial states that did not come from the
+    engine (the 'external state' path) match the per-step path."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(6)
+    H = W = 32
+    T, B, C = 3, 2, 8
+    kw = lif_ref.make_unet_kwargs(base_num_channels=C)
+    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    gen = torch.Generator(device=dev).manual_seed(2)
+    xs = [(torch.rand(B, 2, H, W, generator=gen, device=dev) < 0.2).float() * 3 for _ in range(T)]
+    st0 = [(torch.rand(2, B, C, H, W, generator=gen, device=dev) * 0.8) for _ in range(7)]
+    for s in st0:
+        s[1] = (s[1] > 0.5).float()
+    wts = [torch.randn(B, 2, H, W, generator=gen, device=dev) for _ in range(T)]
+    res = {}
+    for tag, m in (("step", ma), ("seq", mb)):
+        xg = [x.clone().requires_grad_(True) for x in xs]
+        sg = [s.clone().requires_grad_(True) for s in st0]
+        m.states = sg
+        if tag == "step":
+            flows = [m(None, x)["flow"][0] for x in xg]
+        else:
+            flows = [o["flow"][0] for o in m.forward_sequence(None, xg)]
+        loss = sum((f * w).sum() for f, w in zip(flows, wts))
+        loss.backward()
+        res[tag] = ([x.grad.cpu().numpy() for x in xg], [None if s.grad is None else s.grad.cpu().numpy() for s in sg],
+                    [p.grad.cpu().numpy() for p in m.parameters()])
+    for a, b in zip(res["step"][0], res["seq"][0]):
+        assert _rel(b, a) < 1e-5
+    for a, b in zip(res["step"][1], res["seq"][1]):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert _rel(b, a) < 1e-5
+    for a, b in zip(res["step"][2], res["seq"][2]):
+        assert _rel(b, a) < 1e-5

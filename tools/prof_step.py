@@ -23,8 +23,11 @@ def main(C=8, R=128, B=8, T=10, steps=3):
     wins = [make_window(B, 1000, R, R, gen, dev) for _ in range(T)]
     for _ in range(steps):
         lf.reset()
-        for w in wins:
-            out = model(w["event_voxel"], w["event_cnt"])
+        if os.environ.get("SNNFLOW_PER_STEP") == "1":
+            outs = [model(w["event_voxel"], w["event_cnt"]) for w in wins]
+        else:  # as bench.py: wavefront launches
+            outs = model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+        for w, out in zip(wins, outs):
             lf.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
         lf().backward()
         opt.step()
