@@ -247,6 +247,11 @@ __device__ inline Lif4 lif_step4(const float4& y, const float4& m, const LifCoef
     return r;
 }
 
+template <bool F, int C, int NTB>
+struct FragFloats { static constexpr int v = 0; };
+template <int C, int NTB>
+struct FragFloats<true, C, NTB> { static constexpr int v = (FragStage<C, C, NTB>::HALFS / 2 + 3) / 4 * 4; };
+
 // LDS of one conv_fwd block (floats, 16-B aligned parts): halo tile, [s_prev halo tile],
 // [weights of the ff / rec convs].  Carved out of one pool so that a wavefront launch can
 // run several variants over the same allocation.
@@ -255,10 +260,19 @@ struct ConvFwdLds {
     static constexpr int NTB = NT * SPLIT, PI_ = Pad<CIN>::v, PC = Pad<C>::v;
     static constexpr bool PF_REC = REC && Prefetch<C, NTB>::on;  // s_prev halo in registers + own LDS tile
     static constexpr int PMAX = (REC && !PF_REC && PC > PI_) ? PC : PI_;
-    static constexpr bool WL = kWlds<CIN, C>;
-    static constexpr int TILE = (HN * PMAX + 3) / 4 * 4, RTILE = PF_REC ? HN * PC : 0;
-    static constexpr int WFF = WL ? 9 * C * C : 0, WREC = (WL && REC) ? 9 * C * C : 0;
-    static constexpr int FLOATS = TILE + RTILE + WFF + WREC;
+    // C = 8 spike convs: B operand pre-split into bf16 fragments once per block (FragStage);
+    // otherwise f32 weights in LDS up to C = 16 (kWlds)
+    static constexpr bool FRAG = LIF_IN && kMfma<CIN, C> && C == 8;
+    static constexpr bool WL = kWlds<CIN, C> && !FRAG;
+    static constexpr int FRAGF = FragFloats<FRAG, C, NTB>::v;
+    // FRAG: the LIF spikes of the halo as a bf16 tile [HN][C] (exact 0/1); the output
+    // staging after the convs (mfma_store, f32 [NT][PC]) reuses the pool from its start
+    static constexpr int TILE = FRAG ? (HN * C / 2 + 3) / 4 * 4 : (HN * PMAX + 3) / 4 * 4;
+    static constexpr int RTILE = PF_REC ? HN * PC : 0;
+    static constexpr int WFF = WL ? 9 * C * C : FRAGF, WREC = REC ? (WL ? 9 * C * C : FRAGF) : 0;
+    static constexpr int BODY = TILE + RTILE + WFF + WREC;
+    static constexpr int FLOATS = (FRAG && BODY < NT * PC) ? NT * PC : BODY;
+    static_assert(!FRAG || !REC || PF_REC, "bf16 spike tile: s_prev needs its own tile");
 };
 
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
@@ -284,12 +298,19 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     TRACE_AT(TR, TK, 0);
 
     // 1. issue every global load of the tile before any use (weights for LDS first)
-    constexpr bool WL = L::WL;
+    constexpr bool WL = L::WL, FRAG = L::FRAG;
     WStage<WL ? 9 * C * C : 1, NTB> sw_ff, sw_rec;
+    FragStage<FRAG ? C : 8, FRAG ? C : 8, FRAG ? NTB : 64> fs_ff, fs_rec;
     if constexpr (WL) {
         sw_ff.load(a.wt_ff_t);
         if constexpr (REC) {
             if (has_rec) sw_rec.load(a.wt_rec_t);
+        }
+    }
+    if constexpr (FRAG) {
+        fs_ff.load(a.wt_ff_t);
+        if constexpr (REC) {
+            if (has_rec) fs_rec.load(a.wt_rec_t);
         }
     }
     float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
@@ -339,7 +360,13 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                             st_state4(st4, plane4 + k, o.s);
                         }
                     }
-                    *reinterpret_cast<float4*>(tile + p * PI_ + 4 * qt) = sv;
+                    if constexpr (L::FRAG) {
+                        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                        const bf16x4 sb = {(__bf16)sv.x, (__bf16)sv.y, (__bf16)sv.z, (__bf16)sv.w};
+                        *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(tile) + p * CIN + 4 * qt) = sb;
+                    } else {
+                        *reinterpret_cast<float4*>(tile + p * PI_ + 4 * qt) = sv;
+                    }
                 }
             }
         };
@@ -353,6 +380,12 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         sw_ff.store(wl_ff);
         if constexpr (REC) {
             if (has_rec) sw_rec.store(wl_rec);
+        }
+    }
+    if constexpr (FRAG) {
+        fs_ff.store(reinterpret_cast<__bf16*>(wl_ff));
+        if constexpr (REC) {
+            if (has_rec) fs_rec.store(reinterpret_cast<__bf16*>(wl_rec));
         }
     }
     // previous-step spikes exact in bf16 (0/1; always so on the engine path) -> bf16 MFMA
@@ -379,7 +412,9 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         af.zero();
         if (!PROBE_OFF(16)) {
             const float* wf = WL ? wl_ff : a.wt_ff_t;
-            if constexpr (LIF_IN) mfma_conv3x3_bf3<C, C, NW>(tile, wf, af);  // spikes of layer l-1
+            if constexpr (FRAG)
+                mfma_conv3x3_bf3f<C, C, NW>(reinterpret_cast<const __bf16*>(tile), reinterpret_cast<const __bf16*>(wl_ff), af);
+            else if constexpr (LIF_IN) mfma_conv3x3_bf3<C, C, NW>(tile, wf, af);  // spikes of layer l-1
             else mfma_conv3x3<C, C, false, NW>(tile, wf, af);
         }
         bool rec_on = false;
@@ -397,8 +432,13 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                 ar.zero();
                 if (!PROBE_OFF(16)) {
                     const float* wr = WL ? wl_rec : a.wt_rec_t;
-                    if (rec_bf) mfma_conv3x3_bf3<C, C, NW>(rt, wr, ar);
-                    else mfma_conv3x3<C, C, false, NW>(rt, wr, ar);
+                    if constexpr (FRAG) {
+                        if (rec_bf) mfma_conv3x3_bf3f<C, C, NW>(rt, reinterpret_cast<const __bf16*>(wl_rec), ar);
+                        else mfma_conv3x3<C, C, false, NW>(rt, a.wt_rec_t, ar);  // non-binary s_prev
+                    } else {
+                        if (rec_bf) mfma_conv3x3_bf3<C, C, NW>(rt, wr, ar);
+                        else mfma_conv3x3<C, C, false, NW>(rt, wr, ar);
+                    }
                 }
             }
         }
@@ -1606,6 +1646,7 @@ __global__ void k_lif_export(const float* __restrict__ x, const float* __restric
 // own range (Grid), out of one LDS pool sized for the largest variant.
 // ---------------------------------------------------------------------------
 constexpr int kSlotTasks = SNNFLOW_MAX_SLOT_TASKS;
+
 enum SlotKind : int {
     SK_HEAD1, SK_HEAD2, SK_HEAD4, SK_HEAD5,  // conv of a cin-channel input (no LIF)
     SK_PLAIN, SK_PLAIN_REC,                  // conv of a C-channel input (no LIF) [+ rec]

@@ -3,6 +3,8 @@
 // sharded fp64 accumulators.  Device code only; included by the .hip translation units.
 #pragma once
 
+#include <type_traits>
+
 #include "snnflow_dev.h"
 
 namespace snnflow {
@@ -337,6 +339,101 @@ __device__ void mfma_conv3x3_bf3(const float* src, const float* __restrict__ wB,
             for (int nt = 0; nt < G::NNT; ++nt)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) wc[nt][j] = wn[nt][j];
+        }
+    }
+}
+
+// The B operand of mfma_conv3x3_bf3 split ONCE per block: weights [tap][NOUT][KIN] (f32,
+// global) -> LDS fragments [chunk i][n-tile][part hi/mid/lo][lane][8] bf16, exactly what a
+// lane feeds v_mfma_f32_16x16x32_bf16 (same round-to-nearest split as the in-loop form, so
+// results are bit-identical).  load() issues the global reads at kernel start; store()
+// splits and writes before a later barrier.
+template <int KIN, int NOUT, int NTH>
+struct FragStage {
+    using G = Bf3Geo<KIN, NOUT>;
+    static constexpr int E = G::NI * G::NNT * 64 * 8;  // elements per part
+    static constexpr int R = (E + NTH - 1) / NTH;
+    static constexpr int HALFS = 3 * E;                // bf16 entries in LDS
+    float r[R];
+    __device__ inline void load(const float* __restrict__ wB) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = (int)threadIdx.x + i * NTH;
+            const int j = e & 7, lane = (e >> 3) & 63, rest = e >> 9;
+            const int nt = rest % G::NNT, ch = rest / G::NNT, n = nt * 16 + (lane & 15);
+            int tap, c0;
+            bf3_k<KIN>(ch, lane >> 4, tap, c0);
+            r[i] = (e < E && tap < 9 && n < NOUT) ? wB[(tap * NOUT + n) * KIN + c0 + j] : 0.0f;
+        }
+    }
+    __device__ inline void store(__bf16* lds) const {
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = (int)threadIdx.x + i * NTH;
+            if (e < E) {
+                const int low = e & 511, frag = e >> 9;  // (lane, j) and (chunk, n-tile)
+                const float w = r[i];
+                const __bf16 h = (__bf16)w;
+                const float r1 = w - (float)h;
+                const __bf16 md = (__bf16)r1;
+                __bf16* f = lds + frag * 3 * 512 + low;
+                f[0] = h;
+                f[512] = md;
+                f[1024] = (__bf16)(r1 - (float)md);
+            }
+        }
+    }
+};
+
+// mfma_conv3x3_bf3 with the B operand from FragStage fragments in LDS (no per-wave split).
+// A from an f32 halo tile [HN][Pad<KIN>], or (AT = __bf16) from a bf16 tile [HN][KIN] of
+// exact values (spikes): one 16-B LDS read is the lane's A operand.
+template <int KIN, int NOUT, int NW, typename AT = float>
+__device__ void mfma_conv3x3_bf3f(const AT* src, const __bf16* frag, MfmaAcc<KIN, NOUT, NW>& acc) {
+    using G = Bf3Geo<KIN, NOUT>;
+    static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
+    static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
+    constexpr bool ABF = std::is_same<AT, __bf16>::value;
+    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = 16 / NW;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const bf16x8* fv = reinterpret_cast<const bf16x8*>(frag);
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+        bf16x8 bh[G::NNT], bm[G::NNT], bl[G::NNT];
+#pragma unroll
+        for (int nt = 0; nt < G::NNT; ++nt) {
+            const bf16x8* f = fv + (i * G::NNT + nt) * 3 * 64 + lane;
+            bh[nt] = f[0];
+            bm[nt] = f[64];
+            bl[nt] = f[128];
+        }
+        int tap, c0;
+        bf3_k<KIN>(i, g, tap, c0);
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            bf16x8 a;
+            if (tap < 9) {
+                const AT* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
+                if constexpr (ABF) {
+                    a = *reinterpret_cast<const bf16x8*>(ap);
+                } else {
+                    const float4 u = *reinterpret_cast<const float4*>(ap), v = *reinterpret_cast<const float4*>(ap + 4);
+                    a[0] = (__bf16)u.x; a[1] = (__bf16)u.y; a[2] = (__bf16)u.z; a[3] = (__bf16)u.w;
+                    a[4] = (__bf16)v.x; a[5] = (__bf16)v.y; a[6] = (__bf16)v.z; a[7] = (__bf16)v.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
+            }
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt) {
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl[nt], acc.v[mt][nt], 0, 0, 0);
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[nt], acc.v[mt][nt], 0, 0, 0);
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[nt], acc.v[mt][nt], 0, 0, 0);
+            }
         }
     }
 }
