@@ -30,19 +30,22 @@ def stream_seed(seed, rank):
 
 
 def flat_grad_buffer(params):
-    """If every p.grad is a contiguous view laid out back to back (in order) in one
-    storage -- the layout FireNetEngine hands to AccumulateGrad -- return one 1-D
-    tensor over that range, else None."""
+    """If the p.grad are contiguous views that tile one range of one storage exactly (in any
+    order: FireNetEngine's buffer follows its own parameter order, not the module's
+    registration order) -- the layout FireNetEngine hands to AccumulateGrad -- return one
+    1-D tensor over that range, else None."""
     grads = [p.grad for p in params]
     if not grads or any(g is None or not g.is_contiguous() for g in grads):
         return None
     st = grads[0].untyped_storage()
-    base = grads[0].storage_offset()
-    off = base
-    for g in grads:
-        if g.untyped_storage().data_ptr() != st.data_ptr() or g.storage_offset() != off or g.dtype != grads[0].dtype:
+    if any(g.untyped_storage().data_ptr() != st.data_ptr() or g.dtype != grads[0].dtype for g in grads):
+        return None
+    spans = sorted((g.storage_offset(), g.numel()) for g in grads)
+    base = off = spans[0][0]
+    for o, n in spans:
+        if o != off:
             return None
-        off += g.numel()
+        off += n
     flat = torch.empty(0, dtype=grads[0].dtype, device=grads[0].device)
     flat.set_(st, base, (off - base,), (1,))
     return flat

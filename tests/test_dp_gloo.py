@@ -79,13 +79,20 @@ def test_shard_slots_partition():
     assert len({dp.stream_seed(1, r) for r in range(8)}) == 8
 
 
-def test_flat_buffer_detection_rejects_gaps_and_order():
+def test_flat_buffer_detection_any_order_rejects_gaps_and_overlaps():
+    """The engine's flat buffer follows its own parameter order, not the module's
+    registration order: any order that tiles one range exactly is accepted."""
     flat = torch.arange(10.0)
     a, b = torch.nn.Parameter(torch.zeros(4)), torch.nn.Parameter(torch.zeros(4))
     a.grad, b.grad = flat[0:4], flat[4:8]
-    assert dp.flat_grad_buffer([a, b]) is not None
-    assert dp.flat_grad_buffer([b, a]) is None
-    b.grad = flat[5:9]
+    f = dp.flat_grad_buffer([a, b])
+    assert f is not None and f.numel() == 8 and f.data_ptr() == flat.data_ptr()
+    assert dp.flat_grad_buffer([b, a]) is not None
+    b.grad = flat[5:9]   # gap
+    assert dp.flat_grad_buffer([a, b]) is None
+    b.grad = flat[3:7]   # overlap
+    assert dp.flat_grad_buffer([a, b]) is None
+    b.grad = torch.zeros(4)  # other storage
     assert dp.flat_grad_buffer([a, b]) is None
 
 
