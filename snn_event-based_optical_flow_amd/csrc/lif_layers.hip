@@ -683,9 +683,14 @@ __device__ inline float4 bn_bwd4(const float4& g, const float4& y, const BnBwdLd
 
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
 struct LayerBwdLds {
-    static constexpr bool WL = kWlds<CIN, C>;
-    static constexpr int G = HN * Pad<C>::v, WX = WL ? 9 * C * C : 0, WR = (WL && REC) ? 9 * C * C : 0;
+    // C = 8 input gradients: gradient tile and weights split into bf16 parts (mfma_dgrad_bf6)
+    static constexpr bool BF6 = kMfma<CIN, C> && C == 8;
+    static constexpr bool WL = kWlds<CIN, C> && !BF6;
+    static constexpr int FR = FragFloats<BF6, C, NT * SPLIT>::v;
+    static constexpr int G = BF6 ? (3 * HN * C / 2 + 3) / 4 * 4 : HN * Pad<C>::v;
+    static constexpr int WX = WL ? 9 * C * C : FR, WR = REC ? (WL ? 9 * C * C : FR) : 0;
     static constexpr int FLOATS = G + WX + WR;
+    static_assert(!BF6 || G >= NT * Pad<CIN>::v, "output staging aliases the gradient tile");
 };
 
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
@@ -721,12 +726,20 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     TRACE_AT(TR, TK, 0);
 
     // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS)
-    constexpr bool WL = LB::WL;
+    constexpr bool WL = LB::WL, BF6 = LB::BF6;
     WStage<WL ? 9 * C * C : 1, NTB> sw_x, sw_r;
+    FragStage<BF6 ? C : 8, BF6 ? CIN : 8, BF6 ? NTB : 64> fs_x, fs_r;
+    static_assert(!BF6 || PF, "bf16 gradient tile: register-prefetched halo");
     if constexpr (WL) {
         if (a.wt_bwd_ff) sw_x.load(a.wt_fwd_ff);
         if constexpr (REC) {
             if (a.g_state_prev) sw_r.load(a.wt_fwd_rec);
+        }
+    }
+    if constexpr (BF6) {
+        if (a.wt_bwd_ff) fs_x.load(a.wt_fwd_ff);
+        if constexpr (REC) {
+            if (a.g_state_prev) fs_r.load(a.wt_fwd_rec);
         }
     }
     float4 rg[PF ? Halo4<C, NTB>::R : 1], ry[PF ? Halo4<C, NTB>::R : 1];
@@ -818,7 +831,9 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                 const int p = e / Q;
                 const int r = p / HWD, cc = p - r * HWD;
                 const bool img = in_image(tl.h0 + r - 1, tl.w0 + cc - 1, H, W);
-                *reinterpret_cast<float4*>(G + p * PC + 4 * qt) = img ? bn_bwd4(rg[i], ry[i], kb) : z4;
+                const float4 gv = img ? bn_bwd4(rg[i], ry[i], kb) : z4;
+                if constexpr (BF6) split3_store4(reinterpret_cast<__bf16*>(G) + p * C + 4 * qt, HN * C, gv);
+                else *reinterpret_cast<float4*>(G + p * PC + 4 * qt) = gv;
             }
         }
     } else {
@@ -839,6 +854,12 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (a.g_state_prev) sw_r.store(wl_r);
         }
     }
+    if constexpr (BF6) {
+        if (a.wt_bwd_ff) fs_x.store(reinterpret_cast<__bf16*>(wl_x));
+        if constexpr (REC) {
+            if (a.g_state_prev) fs_r.store(reinterpret_cast<__bf16*>(wl_r));
+        }
+    }
     __syncthreads();
     TRACE_AT(TR, TK, 2);
 
@@ -854,14 +875,23 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         const bool do_r = REC && a.g_state_prev != nullptr;
         MfmaAcc<C, CIN, NW> ax;
         MfmaAcc<C, C, NW> arr;
+        const __bf16* g3 = reinterpret_cast<const __bf16*>(G);
         if (do_x) {
             ax.zero();
-            if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, WL ? wl_x : a.wt_fwd_ff, ax);
+            if constexpr (BF6) {
+                if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, CIN, NW>(g3, reinterpret_cast<const __bf16*>(wl_x), ax);
+            } else {
+                if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, WL ? wl_x : a.wt_fwd_ff, ax);
+            }
         }
         if constexpr (REC) {
             if (do_r) {
                 arr.zero();
-                if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, WL ? wl_r : a.wt_fwd_rec, arr);
+                if constexpr (BF6) {
+                    if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, C, NW>(g3, reinterpret_cast<const __bf16*>(wl_r), arr);
+                } else {
+                    if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, WL ? wl_r : a.wt_fwd_rec, arr);
+                }
             }
         }
         __syncthreads();
@@ -1744,8 +1774,11 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
     }
 }
 
+#ifndef SNNFLOW_BWD_SLOT_WAVES
+#define SNNFLOW_BWD_SLOT_WAVES 6  // min waves per SIMD: 3 blocks per CU (measured: 2 per CU is 15 % slower)
+#endif
 template <int C>
-__global__ __launch_bounds__(NT * 2) void k_bwd_slot(BwdSlotParams) {
+__global__ __launch_bounds__(NT * 2, SNNFLOW_BWD_SLOT_WAVES) void k_bwd_slot(BwdSlotParams) {
     typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
     const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
     Grid g;

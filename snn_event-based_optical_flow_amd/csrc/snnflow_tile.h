@@ -438,6 +438,82 @@ __device__ void mfma_conv3x3_bf3f(const AT* src, const __bf16* frag, MfmaAcc<KIN
     }
 }
 
+// The transposed 3x3 conv (input gradient: A = dL/dy at the flipped tap offset, as
+// mfma_conv3x3<..., FLIP = true>) with BOTH operands split into three bf16 parts: A from a
+// three-part bf16 tile [3][HN][KIN] (src3, hi / mid / lo of the f32 gradient), B from FragStage
+// fragments.  Six products per K chunk (mid*mid, lo*hi, hi*lo, mid*hi, hi*mid, hi*hi, small
+// to large; the dropped ones are below 2^-24 relative), each on v_mfma_f32_16x16x32_bf16 at
+// 16 cycles against 8 x 32 for the same K on the f32 matrix cores; f32 accumulation.
+template <int KIN, int NOUT, int NW>
+__device__ void mfma_dgrad_bf6(const __bf16* src3, const __bf16* frag, MfmaAcc<KIN, NOUT, NW>& acc) {
+    using G = Bf3Geo<KIN, NOUT>;
+    static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
+    static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
+    constexpr int MT = 16 / NW, PART = HN * KIN;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const bf16x8* fv = reinterpret_cast<const bf16x8*>(frag);
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+        bf16x8 bh[G::NNT], bm[G::NNT], bl[G::NNT];
+#pragma unroll
+        for (int nt = 0; nt < G::NNT; ++nt) {
+            const bf16x8* f = fv + (i * G::NNT + nt) * 3 * 64 + lane;
+            bh[nt] = f[0];
+            bm[nt] = f[64];
+            bl[nt] = f[128];
+        }
+        int tap, c0;
+        bf3_k<KIN>(i, g, tap, c0);
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+        const int oy = 2 - ky, ox = 2 - kx;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            bf16x8 ah, am, al;
+            if (tap < 9) {
+                const __bf16* ap = src3 + ((row + oy) * HWD + cb + m + ox) * KIN + c0;
+                ah = *reinterpret_cast<const bf16x8*>(ap);
+                am = *reinterpret_cast<const bf16x8*>(ap + PART);
+                al = *reinterpret_cast<const bf16x8*>(ap + 2 * PART);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ah[j] = am[j] = al[j] = (__bf16)0.0f;
+            }
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt) {
+                f32x4 c = acc.v[mt][nt];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm[nt], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[nt], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[nt], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh[nt], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm[nt], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[nt], c, 0, 0, 0);
+                acc.v[mt][nt] = c;
+            }
+        }
+    }
+}
+
+// hi / mid / lo bf16 parts of four floats into three bf16 tiles (part stride `part`).
+__device__ inline void split3_store4(__bf16* d, int part, const float4& v) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    bf16x4 h, md, lo;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const __bf16 a = (__bf16)x[j];
+        const float r1 = x[j] - (float)a;
+        const __bf16 b = (__bf16)r1;
+        h[j] = a;
+        md[j] = b;
+        lo[j] = (__bf16)(r1 - (float)b);
+    }
+    *reinterpret_cast<bf16x4*>(d) = h;
+    *reinterpret_cast<bf16x4*>(d + part) = md;
+    *reinterpret_cast<bf16x4*>(d + 2 * part) = lo;
+}
+
 // A weight tensor of N floats staged into LDS by the whole block: the loads are issued into
 // registers at kernel start (load) and written to LDS before a later barrier (store), so
 // the matrix-core loops read their B operands from LDS and never wait on global memory.
