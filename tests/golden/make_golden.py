@@ -179,7 +179,7 @@ def spiking_cells_case(ref_sub, out):
     np.savez_compressed(os.path.join(out, "spiking_cells_case.npz"), **rec)
 
 
-def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4):
+def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4, fname=None):
     """models/model.py LIFFireNet (reference wiring, conv, BN, states) with the
     restated Leaky; T forwards + EventWarping + backward, train mode."""
     sys.path.insert(0, REPO)
@@ -216,7 +216,7 @@ def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4):
         rec[f"g.{n}"] = p.grad.numpy()
     for k, v in model.state_dict().items():
         rec[f"p1.{k}"] = v.numpy().copy()
-    np.savez_compressed(os.path.join(out, f"{name.lower()}_case.npz"), **rec)
+    np.savez_compressed(os.path.join(out, fname or f"{name.lower()}_case.npz"), **rec)
 
 
 def convlayer_case(ref_sub, out):
@@ -353,6 +353,13 @@ def main():
         lif_export_case(HERE)
         print("lif_export fixture written")
         return
+    if only == ["liffirenet_c8"]:  # C = 8 (the width of the wavefront launches)
+        import loss.flow as ref_flow
+        import models.model as ref_model
+        torch.set_num_threads(1)
+        liffirenet_case(ref_model, ref_flow, HERE, "LIFFireNet", 8, "liffirenet_c8_case.npz")
+        print("liffirenet_c8 fixture written")
+        return
     if only == ["eval"]:
         import loss.flow as ref_flow
         import utils.iwe as ref_iwe
@@ -374,6 +381,7 @@ def main():
     convlayer_case(ref_sub, out)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 4)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet_short", 4)
+    liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 8, "liffirenet_c8_case.npz")
     ref_enc, ref_base = import_dataloader(ref_root)
     encodings_case(ref_enc, ref_base, out)
     eval_case(ref_flow, ref_iwe, out)

@@ -175,7 +175,9 @@ def test_cell_teacher_forced(dev, recurrent, C):
             assert _rel(pd.grad.cpu().numpy(), pc.grad.numpy()) < 1e-3
 
 
-def _run_golden_firenet(g, name, dev):
+def _run_golden_firenet(g, name, dev, seq=False):
+    """seq: the T windows through model.forward_sequence (wavefront launches; only the final
+    step's states are observable there) instead of T model() calls."""
     import snnflow
     from oracle import lif_ref
 
@@ -186,13 +188,16 @@ def _run_golden_firenet(g, name, dev):
     cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
            "model": {"mask_output": True}}
     ew = snnflow.EventWarping(cfg, dev)
+    cnts = [torch.from_numpy(g[f"cnt_{t}"]).to(dev) for t in range(T)]
+    outs = model.forward_sequence(None, cnts) if seq else None
     for t in range(T):
-        out = model(None, torch.from_numpy(g[f"cnt_{t}"]).to(dev))
+        out = outs[t] if seq else model(None, cnts[t])
         np.testing.assert_allclose(out["flow"][0].detach().cpu().numpy(), g[f"flow_{t}"], rtol=1e-4, atol=1e-6)
-        for i, s in enumerate(model._states):
-            ref_s = g[f"state_{t}_{i}"]
-            np.testing.assert_array_equal(s[1].detach().cpu().numpy(), ref_s[1])  # spikes
-            np.testing.assert_allclose(s[0].detach().cpu().numpy(), ref_s[0], rtol=1e-4, atol=1e-5)
+        if not seq or t == T - 1:
+            for i, s in enumerate(model._states):
+                ref_s = g[f"state_{t}_{i}"]
+                np.testing.assert_array_equal(s[1].detach().cpu().numpy(), ref_s[1])  # spikes
+                np.testing.assert_allclose(s[0].detach().cpu().numpy(), ref_s[0], rtol=1e-4, atol=1e-5)
         ew.event_flow_association(out["flow"], torch.from_numpy(g[f"events_{t}"]).to(dev),
                                   torch.from_numpy(g[f"pol_{t}"]).to(dev), torch.from_numpy(g[f"mask_{t}"]).to(dev))
     loss = ew()
@@ -211,6 +216,19 @@ def test_liffirenet_vs_golden(golden, dev):
 
 def test_liffirenet_short_vs_golden(golden, dev):
     _run_golden_firenet(golden("liffirenet_short_case.npz"), "LIFFireNet_short", dev)
+
+
+def test_liffirenet_c8_vs_golden(golden, dev):
+    _run_golden_firenet(golden("liffirenet_c8_case.npz"), "LIFFireNet", dev)
+
+
+@pytest.mark.parametrize("case,name", [("liffirenet_c8_case.npz", "LIFFireNet"),
+                                       ("liffirenet_case.npz", "LIFFireNet"),
+                                       ("liffirenet_short_case.npz", "LIFFireNet_short")])
+def test_forward_sequence_vs_golden(golden, dev, case, name):
+    """The reference-generated fixtures through forward_sequence: the wavefront launches at C = 8,
+    the per-step fallback at C = 4."""
+    _run_golden_firenet(golden(case), name, dev, seq=True)
 
 
 @pytest.mark.parametrize("C", [8, 16, 32])
