@@ -262,17 +262,18 @@ struct ConvFwdLds {
     static constexpr int PMAX = (REC && !PF_REC && PC > PI_) ? PC : PI_;
     // C = 8 spike convs: B operand pre-split into bf16 fragments once per block (FragStage);
     // otherwise f32 weights in LDS up to C = 16 (kWlds)
-    static constexpr bool FRAG = LIF_IN && kMfma<CIN, C> && C == 8;
+    static constexpr bool BT = LIF_IN && kMfma<CIN, C>;  // LIF spikes of the halo as a bf16 tile
+    static constexpr bool FRAG = BT && C == 8;
     static constexpr bool WL = kWlds<CIN, C> && !FRAG;
     static constexpr int FRAGF = FragFloats<FRAG, C, NTB>::v;
-    // FRAG: the LIF spikes of the halo as a bf16 tile [HN][C] (exact 0/1); the output
-    // staging after the convs (mfma_store, f32 [NT][PC]) reuses the pool from its start
-    static constexpr int TILE = FRAG ? (HN * C / 2 + 3) / 4 * 4 : (HN * PMAX + 3) / 4 * 4;
+    // BT: the halo spikes as a bf16 tile [HN][C] (exact 0/1, a lane's MFMA A operand in one 16-B
+    // read); the output staging after the convs (mfma_store, f32 [NT][PC]) reuses the pool
+    static constexpr int TILE = BT ? (HN * C / 2 + 3) / 4 * 4 : (HN * PMAX + 3) / 4 * 4;
     static constexpr int RTILE = PF_REC ? HN * PC : 0;
     static constexpr int WFF = WL ? 9 * C * C : FRAGF, WREC = REC ? (WL ? 9 * C * C : FRAGF) : 0;
     static constexpr int BODY = TILE + RTILE + WFF + WREC;
-    static constexpr int FLOATS = (FRAG && BODY < NT * PC) ? NT * PC : BODY;
-    static_assert(!FRAG || !REC || PF_REC, "bf16 spike tile: s_prev needs its own tile");
+    static constexpr int FLOATS = (BT && BODY < NT * PC) ? NT * PC : BODY;
+    static_assert(!BT || !REC || PF_REC, "bf16 spike tile: s_prev needs its own tile");
 };
 
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
@@ -360,7 +361,7 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                             st_state4(st4, plane4 + k, o.s);
                         }
                     }
-                    if constexpr (L::FRAG) {
+                    if constexpr (L::BT) {
                         typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
                         const bf16x4 sb = {(__bf16)sv.x, (__bf16)sv.y, (__bf16)sv.z, (__bf16)sv.w};
                         *reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(tile) + p * CIN + 4 * qt) = sb;
@@ -414,7 +415,8 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
             const float* wf = WL ? wl_ff : a.wt_ff_t;
             if constexpr (FRAG)
                 mfma_conv3x3_bf3f<C, C, NW>(reinterpret_cast<const __bf16*>(tile), reinterpret_cast<const __bf16*>(wl_ff), af);
-            else if constexpr (LIF_IN) mfma_conv3x3_bf3<C, C, NW>(tile, wf, af);  // spikes of layer l-1
+            else if constexpr (L::BT)  // spikes of layer l-1
+                mfma_conv3x3_bf3<C, C, NW, __bf16>(reinterpret_cast<const __bf16*>(tile), wf, af);
             else mfma_conv3x3<C, C, false, NW>(tile, wf, af);
         }
         bool rec_on = false;

@@ -285,12 +285,13 @@ __device__ inline void bf3_load_b(const float* __restrict__ wB, int i, float (&w
     }
 }
 
-template <int KIN, int NOUT, int NW>
-__device__ void mfma_conv3x3_bf3(const float* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW>& acc) {
+template <int KIN, int NOUT, int NW, typename AT = float>
+__device__ void mfma_conv3x3_bf3(const AT* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW>& acc) {
     using G = Bf3Geo<KIN, NOUT>;
     static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
     static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
-    constexpr int P = Pad<KIN>::v, MT = 16 / NW;
+    constexpr bool ABF = std::is_same<AT, __bf16>::value;  // A: bf16 tile [HN][KIN] of exact values
+    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = 16 / NW;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     float wc[G::NNT][8], wn[G::NNT][8];
@@ -319,10 +320,14 @@ __device__ void mfma_conv3x3_bf3(const float* src, const float* __restrict__ wB,
             const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
             bf16x8 a;
             if (tap < 9) {
-                const float* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
-                const float4 u = *reinterpret_cast<const float4*>(ap), v = *reinterpret_cast<const float4*>(ap + 4);
-                a[0] = (__bf16)u.x; a[1] = (__bf16)u.y; a[2] = (__bf16)u.z; a[3] = (__bf16)u.w;
-                a[4] = (__bf16)v.x; a[5] = (__bf16)v.y; a[6] = (__bf16)v.z; a[7] = (__bf16)v.w;
+                const AT* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
+                if constexpr (ABF) {
+                    a = *reinterpret_cast<const bf16x8*>(ap);
+                } else {
+                    const float4 u = *reinterpret_cast<const float4*>(ap), v = *reinterpret_cast<const float4*>(ap + 4);
+                    a[0] = (__bf16)u.x; a[1] = (__bf16)u.y; a[2] = (__bf16)u.z; a[3] = (__bf16)u.w;
+                    a[4] = (__bf16)v.x; a[5] = (__bf16)v.y; a[6] = (__bf16)v.z; a[7] = (__bf16)v.w;
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
