@@ -1843,10 +1843,18 @@ int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
     return 0;
 }
 
+// Blocks of a layer_bwd launch: a layer without any per-pixel output (the head when its input
+// needs no gradient and it has no recurrent state gradient to produce) only finishes its neuron
+// gradients and BN-backward coefficients, which block 0 does: one block.
+int layer_bwd_blocks(const snnflow_layer_bwd_args& a) {
+    const bool pixels = a.lif_in || (a.g_x && a.wt_bwd_ff) || (a.wt_bwd_rec && a.g_state_prev);
+    return pixels ? snnflow_conv_blocks(a.B, a.H, a.W) : 1;
+}
+
 template <int C>
 int layer_bwd_c(const snnflow_layer_bwd_args& a, hipStream_t s) {
     constexpr int SP = (C == 8 || C == 16 || (C == 32 && SNNFLOW_SP32 == 2)) ? 2 : 1;  // threads per pixel (C x C layers; the head keeps 1)
-    const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT * SP), block1(NT);
+    const dim3 grid(layer_bwd_blocks(a)), block(NT * SP), block1(NT);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: lif_in requires cin == c");
         if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true, SP>), grid, block, 0, s, a);
@@ -2100,7 +2108,7 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         }
         p.layer[i] = a;
         p.kind[i] = kind;
-        p.nblk[i] = snnflow_conv_blocks(B, H, W);
+        p.nblk[i] = layer_bwd_blocks(a);
     }
     if (lif) {
         if (const int e = lif_bwd_check(lif)) return e;

@@ -799,3 +799,37 @@ def test_forward_sequence_input_and_state_grads(dev):
             assert _rel(b, a) < 1e-5
     for a, b in zip(res["step"][2], res["seq"][2]):
         assert _rel(b, a) < 1e-5
+
+
+def test_forward_sequence_eval_mode_and_fallbacks(dev):
+    """Eval mode (running statistics, no running-stat update) through the wavefront launches
+    matches per-step eval; T = 1 and log=True take the per-step path with the same results."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(8)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    wins = [make_window(2, 300, 48, 64, gen, dev) for _ in range(4)]
+    for w in wins[:2]:  # populate running statistics and the lif.mem caches
+        ma(w["event_voxel"], w["event_cnt"])
+    ma.eval()
+    ma.detach_states()
+    mb = copy.deepcopy(ma)
+    rm = ma.G1.bn.running_mean.clone()
+    with torch.no_grad():
+        fa = [ma(w["event_voxel"], w["event_cnt"])["flow"][0] for w in wins]
+        fb = [o["flow"][0] for o in mb.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])]
+    assert torch.equal(mb.G1.bn.running_mean, rm)
+    for a, b in zip(fa, fb):
+        np.testing.assert_allclose(b.cpu().numpy(), a.cpu().numpy(), rtol=1e-5, atol=1e-7)
+    for sa, sb in zip(ma.states, mb.states):
+        np.testing.assert_allclose(sb.cpu().numpy(), sa.cpu().numpy(), rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        one = mb.forward_sequence(None, [wins[0]["event_cnt"]])
+        logged = mb.forward_sequence(None, [w["event_cnt"] for w in wins[:2]], log=True)
+    assert len(one) == 1 and len(logged) == 2 and logged[0]["activity"] is not None
