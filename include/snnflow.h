@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 14
+#define SNNFLOW_ABI_VERSION 15
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -67,7 +67,14 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
 typedef struct snnflow_prep_desc {
     const float* w; int c, cin; float* wt_fwd; float* wt_bwd;
     float* threshold; int thr_n;
+    /* ABI 15, optional (NULL = skip; cin == c, c % 8 == 0): the weights split into three bf16
+     * parts (hi + mid + lo == w exactly) in the matrix-core operand order of the kernels --
+     * frag_fwd for the forward conv (snnflow_conv_fwd_args.wf_ff / wf_rec), frag_bwd for the
+     * input-gradient conv (snnflow_layer_bwd_args.wd_ff / wd_rec); snnflow_frag_halfs(c, cin)
+     * bf16 values (uint16 bit patterns) each */
+    uint16_t* frag_fwd; uint16_t* frag_bwd;
 } snnflow_prep_desc;
+int snnflow_frag_halfs(int c, int cin);
 #define SNNFLOW_MAX_BATCH 16
 int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream);
 
@@ -111,6 +118,9 @@ typedef struct snnflow_conv_fwd_args {
     float* y;                   /* out NHWC [B][H][W][c] pre-BN current           */
     double* acc;                /* += SNNFLOW_ACC_LEN(2c) (sum y, sum y^2); NULL = no batch sums (eval) */
     double* zero0; double* zero1; int zero_n;
+    /* ABI 15, optional: bf16 fragments of wt_ff_t / wt_rec_t (snnflow_prep_desc.frag_fwd) for the
+     * spike convs of the cin == c kernels at c = 16, 32 (else split in the kernel) */
+    const uint16_t* wf_ff; const uint16_t* wf_rec;
 } snnflow_conv_fwd_args;
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream);
 int snnflow_conv_blocks(int B, int H, int W);
@@ -187,6 +197,9 @@ typedef struct snnflow_layer_bwd_args {
     float* prev_g_cur; float* prev_g_mem;
     double* acc_out;            /* += SNNFLOW_BWD_ACC(cin) sums for layer l-1 */
     double* zero0; double* zero1; int zero_n;
+    /* ABI 15, optional: bf16 fragments of wt_fwd_ff / wt_fwd_rec (snnflow_prep_desc.frag_bwd)
+     * for the input-gradient convs of the cin == c kernels at c = 16, 32 (else f32 matrix cores) */
+    const uint16_t* wd_ff; const uint16_t* wd_rec;
 } snnflow_layer_bwd_args;
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
 

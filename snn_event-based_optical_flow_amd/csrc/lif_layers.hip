@@ -210,6 +210,52 @@ struct DescBatch {
     }
 };
 
+// Matrix-core operand geometry of a KIN x NOUT 3x3 conv at run time (Bf3Geo / bf3_k).
+struct FragGeo {
+    int gpt, tpi, ipt, ni, nnt;
+    __host__ __device__ FragGeo(int kin, int nout) {
+        gpt = kin / 8;
+        tpi = gpt >= 4 ? 1 : 4 / gpt;
+        ipt = gpt >= 4 ? gpt / 4 : 1;
+        ni = ((9 + tpi - 1) / tpi) * ipt;
+        nnt = (nout + 15) / 16;
+    }
+    __host__ __device__ int halfs() const { return ni * nnt * 3 * 512; }
+    __device__ void k(int i, int g, int& tap, int& c0) const {
+        if (gpt >= 4) {
+            tap = i / ipt;
+            c0 = ((i % ipt) * 4 + g) * 8;
+        } else {
+            tap = i * tpi + g / gpt;
+            c0 = (g % gpt) * 8;
+        }
+    }
+};
+
+// Fragment element e (chunk, n-tile, lane, j) of a KIN x NOUT conv: the three bf16 parts of
+// W(tap, n, k = c0 + j) at frag[((chunk * nnt + nt) * 3 + part) * 512 + lane * 8 + j]
+// (FragStage's layout, in global memory).  fwd: n = co, k = ci; !fwd (input gradient): n = ci, k = co.
+__device__ inline void prep_frag(const snnflow_prep_desc& d, int e, bool fwd) {
+    const int c = d.c, cin = d.cin;
+    const FragGeo G(fwd ? cin : c, fwd ? c : cin);
+    if (e >= G.ni * G.nnt * 512) return;
+    const int j = e & 7, lane = (e >> 3) & 63, rest = e >> 9;
+    const int nt = rest % G.nnt, ch = rest / G.nnt, n = nt * 16 + (lane & 15);
+    int tap, c0;
+    G.k(ch, lane >> 4, tap, c0);
+    const int kk = c0 + j, nout = fwd ? c : cin;
+    float w = 0.0f;
+    if (tap < 9 && n < nout) w = fwd ? d.w[(n * cin + kk) * 9 + tap] : d.w[(kk * cin + n) * 9 + tap];
+    const __bf16 h = (__bf16)w;
+    const float r1 = w - (float)h;
+    const __bf16 md = (__bf16)r1;
+    const __bf16 lo = (__bf16)(r1 - (float)md);
+    uint16_t* f = (fwd ? d.frag_fwd : d.frag_bwd) + (rest * 3) * 512 + (e & 511);
+    f[0] = __builtin_bit_cast(uint16_t, h);
+    f[512] = __builtin_bit_cast(uint16_t, md);
+    f[1024] = __builtin_bit_cast(uint16_t, lo);
+}
+
 __global__ void k_prep_weights(DescBatch<snnflow_prep_desc> batch) {
     const snnflow_prep_desc d = batch.pick(blockIdx.y);
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -220,6 +266,8 @@ __global__ void k_prep_weights(DescBatch<snnflow_prep_desc> batch) {
         d.wt_fwd[(k * cin + ci) * c + co] = v;
         d.wt_bwd[(k * c + co) * cin + ci] = v;
     }
+    if (d.w && d.frag_fwd) prep_frag(d, e, true);
+    if (d.w && d.frag_bwd) prep_frag(d, e, false);
     if (d.threshold && e < d.thr_n) {
         const float t = d.threshold[e];
         d.threshold[e] = (t < 0.01f) ? 0.01f : t;
@@ -415,8 +463,11 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
             const float* wf = WL ? wl_ff : a.wt_ff_t;
             if constexpr (FRAG)
                 mfma_conv3x3_bf3f<C, C, NW>(reinterpret_cast<const __bf16*>(tile), reinterpret_cast<const __bf16*>(wl_ff), af);
-            else if constexpr (L::BT)  // spikes of layer l-1
-                mfma_conv3x3_bf3<C, C, NW, __bf16>(reinterpret_cast<const __bf16*>(tile), wf, af);
+            else if constexpr (L::BT) {  // spikes of layer l-1
+                const __bf16* tb = reinterpret_cast<const __bf16*>(tile);
+                if (a.wf_ff) mfma_conv3x3_bf3g<C, C, NW, __bf16>(tb, reinterpret_cast<const __bf16*>(a.wf_ff), af);
+                else mfma_conv3x3_bf3<C, C, NW, __bf16>(tb, wf, af);
+            }
             else mfma_conv3x3<C, C, false, NW>(tile, wf, af);
         }
         bool rec_on = false;
@@ -438,7 +489,8 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                         if (rec_bf) mfma_conv3x3_bf3f<C, C, NW>(rt, reinterpret_cast<const __bf16*>(wl_rec), ar);
                         else mfma_conv3x3<C, C, false, NW>(rt, a.wt_rec_t, ar);  // non-binary s_prev
                     } else {
-                        if (rec_bf) mfma_conv3x3_bf3<C, C, NW>(rt, wr, ar);
+                        if (rec_bf && a.wf_rec) mfma_conv3x3_bf3g<C, C, NW>(rt, reinterpret_cast<const __bf16*>(a.wf_rec), ar);
+                        else if (rec_bf) mfma_conv3x3_bf3<C, C, NW>(rt, wr, ar);
                         else mfma_conv3x3<C, C, false, NW>(rt, wr, ar);
                     }
                 }
@@ -1895,6 +1947,11 @@ const char* snnflow_last_error(void) { return g_err.c_str(); }
 
 int snnflow_conv_blocks(int B, int H, int W) { return B * tiles_per_image(H, W); }
 
+int snnflow_frag_halfs(int c, int cin) {
+    if (cin != c || c <= 0 || c % 8 != 0 || c > 64) return 0;
+    return FragGeo(c, c).halfs();
+}
+
 int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream) {
     if (!d || n <= 0 || n > SNNFLOW_MAX_BATCH) SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: bad count");
     DescBatch<snnflow_prep_desc> batch = {};
@@ -1904,8 +1961,14 @@ int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream) 
         if ((x.w && (x.c <= 0 || x.cin <= 0 || !x.wt_fwd || !x.wt_bwd)) || (!x.w && !x.threshold) ||
             (x.threshold && x.thr_n <= 0))
             SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: bad descriptor");
+        if ((x.frag_fwd || x.frag_bwd) && (!x.w || snnflow_frag_halfs(x.c, x.cin) == 0))
+            SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: fragments need cin == c, c % 8 == 0");
         batch.d[i] = x;
         if (x.w && x.c * x.cin * 9 > maxe) maxe = x.c * x.cin * 9;
+        if (x.frag_fwd || x.frag_bwd) {
+            const int fe = snnflow_frag_halfs(x.c, x.cin) / 3;
+            if (fe > maxe) maxe = fe;
+        }
         if (x.threshold && x.thr_n > maxe) maxe = x.thr_n;
     }
     hipLaunchKernelGGL(k_prep_weights, dim3((maxe + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, batch);
@@ -1917,7 +1980,7 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
                          void* stream) {
     if (c <= 0 || cin <= 0 || (w && (!wt_fwd || !wt_bwd)) || (!w && !threshold))
         SNN_FAIL(SNNFLOW_E_ARG, "prep_weights: bad args");
-    snnflow_prep_desc d = {w, c, cin, wt_fwd, wt_bwd, threshold, c};
+    snnflow_prep_desc d = {w, c, cin, wt_fwd, wt_bwd, threshold, c, nullptr, nullptr};
     return snnflow_prep_weights_batch(&d, 1, stream);
 }
 

@@ -443,6 +443,68 @@ __device__ void mfma_conv3x3_bf3f(const AT* src, const __bf16* frag, MfmaAcc<KIN
     }
 }
 
+// mfma_conv3x3_bf3f with the fragments in global memory (snnflow_prep_desc.frag_fwd, L2-resident:
+// every block reads the same few KB), the next chunk's fragments in flight during this chunk's
+// products.  C = 16 / 32, where the fragments do not fit beside the tiles in LDS.
+template <int KIN, int NOUT, int NW, typename AT = float>
+__device__ void mfma_conv3x3_bf3g(const AT* src, const __bf16* __restrict__ frag, MfmaAcc<KIN, NOUT, NW>& acc) {
+    using G = Bf3Geo<KIN, NOUT>;
+    static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
+    static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
+    constexpr bool ABF = std::is_same<AT, __bf16>::value;
+    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = 16 / NW;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const bf16x8* fv = reinterpret_cast<const bf16x8*>(frag) + lane;
+    bf16x8 cur[G::NNT][3], nxt[G::NNT][3];
+#pragma unroll
+    for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cur[nt][q] = fv[(nt * 3 + q) * 64];
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+        if (i + 1 < G::NI) {
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + nt) * 3 + q) * 64];
+        }
+        int tap, c0;
+        bf3_k<KIN>(i, g, tap, c0);
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            bf16x8 a;
+            if (tap < 9) {
+                const AT* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
+                if constexpr (ABF) {
+                    a = *reinterpret_cast<const bf16x8*>(ap);
+                } else {
+                    const float4 u = *reinterpret_cast<const float4*>(ap), v = *reinterpret_cast<const float4*>(ap + 4);
+                    a[0] = (__bf16)u.x; a[1] = (__bf16)u.y; a[2] = (__bf16)u.z; a[3] = (__bf16)u.w;
+                    a[4] = (__bf16)v.x; a[5] = (__bf16)v.y; a[6] = (__bf16)v.z; a[7] = (__bf16)v.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
+            }
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt) {
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[nt][2], acc.v[mt][nt], 0, 0, 0);
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[nt][1], acc.v[mt][nt], 0, 0, 0);
+                acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[nt][0], acc.v[mt][nt], 0, 0, 0);
+            }
+        }
+        if (i + 1 < G::NI) {
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) cur[nt][q] = nxt[nt][q];
+        }
+    }
+}
+
 // The transposed 3x3 conv (input gradient: A = dL/dy at the flipped tap offset, as
 // mfma_conv3x3<..., FLIP = true>) with BOTH operands split into three bf16 parts: A from a
 // three-part bf16 tile [3][HN][KIN] (src3, hi / mid / lo of the f32 gradient), B from FragStage

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 
 class Neuron(ctypes.Structure):
@@ -37,7 +37,8 @@ class ConvFwdArgs(ctypes.Structure):
                 ("prev_y", P), ("prev_mem", P), ("prev_acc", P), ("prev_stats", P),
                 ("prev", Neuron), ("prev_state", P),
                 ("wt_ff", P), ("wt_rec", P), ("wt_ff_t", P), ("wt_rec_t", P), ("s_prev", P),
-                ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32)]
+                ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32),
+                ("wf_ff", P), ("wf_rec", P)]
 
 
 class LifFwdArgs(ctypes.Structure):
@@ -66,7 +67,7 @@ class LayerBwdArgs(ctypes.Structure):
                 ("g_state_prev", P), ("zero_mem_half", I32),
                 ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),
                 ("prev_g_state", P), ("prev_g_cur", P), ("prev_g_mem", P), ("acc_out", P),
-                ("zero0", P), ("zero1", P), ("zero_n", I32)]
+                ("zero0", P), ("zero1", P), ("zero_n", I32), ("wd_ff", P), ("wd_rec", P)]
 
 
 MAX_WGRAD_STEPS = 32
@@ -144,7 +145,7 @@ class SlabDesc(ctypes.Structure):
 
 class PrepDesc(ctypes.Structure):
     _fields_ = [("w", P), ("c", I32), ("cin", I32), ("wt_fwd", P), ("wt_bwd", P),
-                ("threshold", P), ("thr_n", I32)]
+                ("threshold", P), ("thr_n", I32), ("frag_fwd", P), ("frag_bwd", P)]
 
 
 MAX_BATCH = 16
@@ -193,6 +194,7 @@ EXPORTS = {
     "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),
     "snnflow_slot_supported": (I32, [I32, I32]),
+    "snnflow_frag_halfs": (I32, [I32, I32]),
 }
 MAX_SLOT_TASKS = 4
 

@@ -110,6 +110,7 @@ class PreppedWeights:
     def __init__(self):
         self.fwd = {}
         self.bwd = {}
+        self.frag = {}   # i -> uint16 [snnflow_frag_halfs] forward-conv bf16 fragments (C = 16, 32) or None
         self.key = None
 
     def ensure(self, weights, thresholds, stream, refresh=True):
@@ -123,6 +124,9 @@ class PreppedWeights:
             if f is None or f.numel() != w.numel() or f.device != w.device:
                 self.fwd[i] = torch.empty(w.numel(), device=w.device)
                 self.bwd[i] = torch.empty(w.numel(), device=w.device)
+                c, cin = w.shape[0], w.shape[1]
+                nf = lib.snnflow_frag_halfs(c, cin) if c >= 16 else 0  # C = 8 splits in LDS
+                self.frag[i] = torch.empty(nf, dtype=torch.int16, device=w.device) if nf else None
                 fresh = True
         if not (refresh or fresh):
             return
@@ -131,7 +135,8 @@ class PreppedWeights:
             c, cin = w.shape[0], w.shape[1]
             if not w.is_contiguous():
                 raise _lib.SnnflowError("conv weight must be contiguous")
-            descs.append(_lib.PrepDesc(ptr(w), c, cin, ptr(self.fwd[i]), ptr(self.bwd[i]), None, 0))
+            descs.append(_lib.PrepDesc(ptr(w), c, cin, ptr(self.fwd[i]), ptr(self.bwd[i]), None, 0,
+                                       _ptr_t(self.frag.get(i)), None))
         for i, t in enumerate(thresholds):  # ride along with the weight descriptors
             if i < len(descs):
                 descs[i].threshold, descs[i].thr_n = ptr(t), t.numel()
@@ -193,16 +198,18 @@ class FireNetEngine:
                 ws.append(cell.rec.weight)
         self.prep.ensure(ws, [c.lif.threshold for c in self.cells], stream, refresh)
         # map layer -> prepped buffers
-        fwd, bwd, i = [], [], 0
+        fwd, bwd, frag, i = [], [], [], 0
         for rec in self.rec:
-            ff = (self.prep.fwd[i], self.prep.bwd[i])
+            ff = (self.prep.fwd[i], self.prep.bwd[i], self.prep.frag.get(i))
             i += 1
-            rc = (None, None)
+            rc = (None, None, None)
             if rec:
-                rc = (self.prep.fwd[i], self.prep.bwd[i])
+                rc = (self.prep.fwd[i], self.prep.bwd[i], self.prep.frag.get(i))
                 i += 1
             fwd.append((ff[0], rc[0]))
             bwd.append((ff[1], rc[1]))
+            frag.append((ff[2], rc[2]))
+        self.frags = frag
         return fwd, bwd
 
     def open_chain(self, device):
@@ -309,6 +316,9 @@ def _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, 
     a.wt_ff_t, a.wt_rec_t = ptr(wbwd[l][0]), ptr(wbwd[l][1])  # MFMA B operand layout
     a.s_prev = _ptr_t(s_prev[l])
     a.y, a.acc = ptr(ys[l]), (ptr(facc[l]) if train[l] else None)
+    fr = getattr(eng, "frags", None)
+    if fr is not None:  # pre-split bf16 fragments of the spike convs (C = 16, 32)
+        a.wf_ff, a.wf_rec = _ptr_t(fr[l][0]), _ptr_t(fr[l][1])
     return a
 
 
