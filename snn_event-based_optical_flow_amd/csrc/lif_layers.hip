@@ -1690,8 +1690,17 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
                                                           float* total_out) {
     __shared__ double part[CLIP_NT / 64];
     __shared__ float coef_s;
+    // 8 loads in flight per thread (one block: the vector is small, ~5e3..1e5 floats)
     double s = 0.0;
-    for (int64_t i = threadIdx.x; i < n; i += CLIP_NT) {
+    int64_t i = threadIdx.x;
+    for (; i + 7 * CLIP_NT < n; i += 8 * CLIP_NT) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = g[i + k * CLIP_NT];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += (double)v[k] * (double)v[k];
+    }
+    for (; i < n; i += CLIP_NT) {
         const double v = g[i];
         s += v * v;
     }
@@ -1709,7 +1718,15 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
     }
     __syncthreads();
     const float c = coef_s;
-    for (int64_t i = threadIdx.x; i < n; i += CLIP_NT) g[i] = g[i] * c;
+    int64_t j = threadIdx.x;
+    for (; j + 7 * CLIP_NT < n; j += 8 * CLIP_NT) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = g[j + k * CLIP_NT];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[j + k * CLIP_NT] = v[k] * c;
+    }
+    for (; j < n; j += CLIP_NT) g[j] = g[j] * c;
 }
 
 __global__ void k_lif_export(const float* __restrict__ x, const float* __restrict__ mem, const float* __restrict__ beta,
@@ -1874,7 +1891,7 @@ bool valid_c(int c) { return c == 4 || c == 8 || c == 16 || c == 32; }
 
 template <int C>
 int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
-    constexpr int SP = (C == 8 || C == 16 || (C == 32 && SNNFLOW_SP32 == 2)) ? 2 : 1;  // threads per output pixel
+    constexpr int SP = C == 32 ? SNNFLOW_SP32 : ((C == 8 || C == 16) ? 2 : 1);  // threads per output pixel
     const dim3 grid(snnflow_conv_blocks(a.B, a.H, a.W)), block(NT * SP);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: lif_in requires cin == c");
@@ -1905,7 +1922,7 @@ int layer_bwd_blocks(const snnflow_layer_bwd_args& a) {
 
 template <int C>
 int layer_bwd_c(const snnflow_layer_bwd_args& a, hipStream_t s) {
-    constexpr int SP = (C == 8 || C == 16 || (C == 32 && SNNFLOW_SP32 == 2)) ? 2 : 1;  // threads per pixel (C x C layers; the head keeps 1)
+    constexpr int SP = C == 32 ? SNNFLOW_SP32 : ((C == 8 || C == 16) ? 2 : 1);  // threads per pixel (C x C layers; the head keeps 1)
     const dim3 grid(layer_bwd_blocks(a)), block(NT * SP), block1(NT);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: lif_in requires cin == c");
