@@ -735,21 +735,22 @@ __device__ inline float4 bn_bwd4(const float4& g, const float4& y, const BnBwdLd
     return make_float4(o[0], o[1], o[2], o[3]);
 }
 
-template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false>
 struct LayerBwdLds {
-    // C = 8 input gradients: gradient tile and weights split into bf16 parts (mfma_dgrad_bf6)
-    static constexpr bool BF6 = kMfma<CIN, C> && C == 8;
+    // input gradients with the gradient tile and weights split into bf16 parts (mfma_dgrad_bf6):
+    // C = 8 with the weight fragments staged in LDS, C = 16 / 32 (BFG) read from global memory
+    static constexpr bool BF6 = kMfma<CIN, C> && (C == 8 || BFG);
     static constexpr bool WL = kWlds<CIN, C> && !BF6;
-    static constexpr int FR = FragFloats<BF6, C, NT * SPLIT>::v;
+    static constexpr int FR = FragFloats<BF6 && C == 8, C, NT * SPLIT>::v;
     static constexpr int G = BF6 ? (3 * HN * C / 2 + 3) / 4 * 4 : HN * Pad<C>::v;
     static constexpr int WX = WL ? 9 * C * C : FR, WR = REC ? (WL ? 9 * C * C : FR) : 0;
     static constexpr int FLOATS = G + WX + WR;
     static_assert(!BF6 || G >= NT * Pad<CIN>::v, "output staging aliases the gradient tile");
 };
 
-template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false>
 __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, float* lds) {
-    using LB = LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT>;
+    using LB = LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT, BFG>;
     constexpr int NTB = NT * SPLIT;
     constexpr int CI = CIN / SPLIT, CR = C / SPLIT;  // input / recurrent channels per thread group
     static_assert(CI * SPLIT == CIN && CR * SPLIT == C, "channel split");
@@ -780,9 +781,9 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     TRACE_AT(TR, TK, 0);
 
     // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS)
-    constexpr bool WL = LB::WL, BF6 = LB::BF6;
+    constexpr bool WL = LB::WL, BF6 = LB::BF6, FLDS = BF6 && C == 8;  // FLDS: fragments in LDS
     WStage<WL ? 9 * C * C : 1, NTB> sw_x, sw_r;
-    FragStage<BF6 ? C : 8, BF6 ? CIN : 8, BF6 ? NTB : 64> fs_x, fs_r;
+    FragStage<FLDS ? C : 8, FLDS ? CIN : 8, FLDS ? NTB : 64> fs_x, fs_r;
     static_assert(!BF6 || PF, "bf16 gradient tile: register-prefetched halo");
     if constexpr (WL) {
         if (a.wt_bwd_ff) sw_x.load(a.wt_fwd_ff);
@@ -790,7 +791,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (a.g_state_prev) sw_r.load(a.wt_fwd_rec);
         }
     }
-    if constexpr (BF6) {
+    if constexpr (FLDS) {
         if (a.wt_bwd_ff) fs_x.load(a.wt_fwd_ff);
         if constexpr (REC) {
             if (a.g_state_prev) fs_r.load(a.wt_fwd_rec);
@@ -908,7 +909,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (a.g_state_prev) sw_r.store(wl_r);
         }
     }
-    if constexpr (BF6) {
+    if constexpr (FLDS) {
         if (a.wt_bwd_ff) fs_x.store(reinterpret_cast<__bf16*>(wl_x));
         if constexpr (REC) {
             if (a.g_state_prev) fs_r.store(reinterpret_cast<__bf16*>(wl_r));
@@ -932,8 +933,10 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         const __bf16* g3 = reinterpret_cast<const __bf16*>(G);
         if (do_x) {
             ax.zero();
-            if constexpr (BF6) {
+            if constexpr (FLDS) {
                 if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, CIN, NW>(g3, reinterpret_cast<const __bf16*>(wl_x), ax);
+            } else if constexpr (BF6) {
+                if (!PROBE_OFF(1)) mfma_dgrad_bf6g<C, CIN, NW>(g3, reinterpret_cast<const __bf16*>(a.wd_ff), ax);
             } else {
                 if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, WL ? wl_x : a.wt_fwd_ff, ax);
             }
@@ -941,8 +944,10 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         if constexpr (REC) {
             if (do_r) {
                 arr.zero();
-                if constexpr (BF6) {
+                if constexpr (FLDS) {
                     if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, C, NW>(g3, reinterpret_cast<const __bf16*>(wl_r), arr);
+                } else if constexpr (BF6) {
+                    if (!PROBE_OFF(1)) mfma_dgrad_bf6g<C, C, NW>(g3, reinterpret_cast<const __bf16*>(a.wd_rec), arr);
                 } else {
                     if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, WL ? wl_r : a.wt_fwd_rec, arr);
                 }
@@ -1044,10 +1049,10 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     }
 }
 
-template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false>
 __global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args a) {
-    __shared__ __attribute__((aligned(16))) float pool[LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT>::FLOATS];
-    layer_bwd_body<CIN, C, LIF_IN, REC, SPLIT>(a, hw_grid(), pool);
+    __shared__ __attribute__((aligned(16))) float pool[LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT, BFG>::FLOATS];
+    layer_bwd_body<CIN, C, LIF_IN, REC, SPLIT, BFG>(a, hw_grid(), pool);
 }
 
 // ---------------------------------------------------------------------------
@@ -1926,7 +1931,12 @@ int layer_bwd_c(const snnflow_layer_bwd_args& a, hipStream_t s) {
     const dim3 grid(layer_bwd_blocks(a)), block(NT * SP), block1(NT);
     if (a.lif_in) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: lif_in requires cin == c");
-        if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true, SP>), grid, block, 0, s, a);
+        // C = 16 / 32 with pre-split fragments of every conv it transposes: bf16 input gradients
+        const bool bfg = C >= 16 && a.wd_ff && (!a.wt_bwd_rec || !a.g_state_prev || a.wd_rec);
+        if (bfg) {
+            if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true, SP, C >= 16>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_layer_bwd<C, C, true, false, SP, C >= 16>), grid, block, 0, s, a);
+        } else if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true, SP>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_layer_bwd<C, C, true, false, SP>), grid, block, 0, s, a);
     } else if (a.wt_bwd_rec) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: recurrent cell requires cin == c");

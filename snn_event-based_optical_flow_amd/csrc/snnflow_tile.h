@@ -562,6 +562,68 @@ __device__ void mfma_dgrad_bf6(const __bf16* src3, const __bf16* frag, MfmaAcc<K
     }
 }
 
+// mfma_dgrad_bf6 with the weight fragments in global memory (snnflow_prep_desc.frag_bwd,
+// L2-resident), the next chunk's in flight during this chunk's products (C = 16 / 32).
+template <int KIN, int NOUT, int NW>
+__device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ frag, MfmaAcc<KIN, NOUT, NW>& acc) {
+    using G = Bf3Geo<KIN, NOUT>;
+    static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
+    static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
+    constexpr int MT = 16 / NW, PART = HN * KIN;
+    const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const bf16x8* fv = reinterpret_cast<const bf16x8*>(frag) + lane;
+    bf16x8 cur[G::NNT][3], nxt[G::NNT][3];
+#pragma unroll
+    for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) cur[nt][q] = fv[(nt * 3 + q) * 64];
+#pragma unroll
+    for (int i = 0; i < G::NI; ++i) {
+        if (i + 1 < G::NI) {
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + nt) * 3 + q) * 64];
+        }
+        int tap, c0;
+        bf3_k<KIN>(i, g, tap, c0);
+        const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+        const int oy = 2 - ky, ox = 2 - kx;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            bf16x8 ah, am, al;
+            if (tap < 9) {
+                const __bf16* ap = src3 + ((row + oy) * HWD + cb + m + ox) * KIN + c0;
+                ah = *reinterpret_cast<const bf16x8*>(ap);
+                am = *reinterpret_cast<const bf16x8*>(ap + PART);
+                al = *reinterpret_cast<const bf16x8*>(ap + 2 * PART);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ah[j] = am[j] = al[j] = (__bf16)0.0f;
+            }
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt) {
+                f32x4 c = acc.v[mt][nt];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, cur[nt][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, cur[nt][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, cur[nt][2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, cur[nt][0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, cur[nt][1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, cur[nt][0], c, 0, 0, 0);
+                acc.v[mt][nt] = c;
+            }
+        }
+        if (i + 1 < G::NI) {
+#pragma unroll
+            for (int nt = 0; nt < G::NNT; ++nt)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) cur[nt][q] = nxt[nt][q];
+        }
+    }
+}
+
 // hi / mid / lo bf16 parts of four floats into three bf16 tiles (part stride `part`).
 __device__ inline void split3_store4(__bf16* d, int part, const float4& v) {
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

@@ -111,6 +111,7 @@ class PreppedWeights:
         self.fwd = {}
         self.bwd = {}
         self.frag = {}   # i -> uint16 [snnflow_frag_halfs] forward-conv bf16 fragments (C = 16, 32) or None
+        self.fragb = {}  # i -> the same for the input-gradient conv
         self.key = None
 
     def ensure(self, weights, thresholds, stream, refresh=True):
@@ -127,6 +128,7 @@ class PreppedWeights:
                 c, cin = w.shape[0], w.shape[1]
                 nf = lib.snnflow_frag_halfs(c, cin) if c >= 16 else 0  # C = 8 splits in LDS
                 self.frag[i] = torch.empty(nf, dtype=torch.int16, device=w.device) if nf else None
+                self.fragb[i] = torch.empty(nf, dtype=torch.int16, device=w.device) if nf else None
                 fresh = True
         if not (refresh or fresh):
             return
@@ -136,7 +138,7 @@ class PreppedWeights:
             if not w.is_contiguous():
                 raise _lib.SnnflowError("conv weight must be contiguous")
             descs.append(_lib.PrepDesc(ptr(w), c, cin, ptr(self.fwd[i]), ptr(self.bwd[i]), None, 0,
-                                       _ptr_t(self.frag.get(i)), None))
+                                       _ptr_t(self.frag.get(i)), _ptr_t(self.fragb.get(i))))
         for i, t in enumerate(thresholds):  # ride along with the weight descriptors
             if i < len(descs):
                 descs[i].threshold, descs[i].thr_n = ptr(t), t.numel()
@@ -198,18 +200,19 @@ class FireNetEngine:
                 ws.append(cell.rec.weight)
         self.prep.ensure(ws, [c.lif.threshold for c in self.cells], stream, refresh)
         # map layer -> prepped buffers
-        fwd, bwd, frag, i = [], [], [], 0
+        fwd, bwd, frag, fragb, i = [], [], [], [], 0
         for rec in self.rec:
-            ff = (self.prep.fwd[i], self.prep.bwd[i], self.prep.frag.get(i))
+            ff = (self.prep.fwd[i], self.prep.bwd[i], self.prep.frag.get(i), self.prep.fragb.get(i))
             i += 1
-            rc = (None, None, None)
+            rc = (None, None, None, None)
             if rec:
-                rc = (self.prep.fwd[i], self.prep.bwd[i], self.prep.frag.get(i))
+                rc = (self.prep.fwd[i], self.prep.bwd[i], self.prep.frag.get(i), self.prep.fragb.get(i))
                 i += 1
             fwd.append((ff[0], rc[0]))
             bwd.append((ff[1], rc[1]))
             frag.append((ff[2], rc[2]))
-        self.frags = frag
+            fragb.append((ff[3], rc[3]))
+        self.frags, self.fragsb = frag, fragb
         return fwd, bwd
 
     def open_chain(self, device):
@@ -365,6 +368,9 @@ def _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur
         if g_prev[l] is not None:
             a.g_state_prev = ptr(g_prev[l])
             a.zero_mem_half = 0 if ext[l] else 1
+    fb = getattr(eng, "fragsb", None)
+    if fb is not None:  # pre-split bf16 fragments of the input-gradient convs (C = 16, 32)
+        a.wd_ff, a.wd_rec = _ptr_t(fb[l][0]), _ptr_t(fb[l][1])
     if l > 0:
         a.cin, a.lif_in = C, 1
         a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[l][0]), ptr(wfwd[l][0])

@@ -833,3 +833,41 @@ def test_forward_sequence_eval_mode_and_fallbacks(dev):
         one = mb.forward_sequence(None, [wins[0]["event_cnt"]])
         logged = mb.forward_sequence(None, [w["event_cnt"] for w in wins[:2]], log=True)
     assert len(one) == 1 and len(logged) == 2 and logged[0]["activity"] is not None
+
+
+@pytest.mark.parametrize("C", [16, 32])
+def test_engine_gradients_wide_vs_oracle(dev, C):
+    """C = 16 / 32 through the engine (pre-split weight fragments from the prep kernel: forward
+    spike convs and the bf16 six-product input gradients read them from L2) against the oracle:
+    flows, loss and every parameter gradient of a T = 2 window."""
+    import snnflow
+    from oracle import iwe_ref, lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(12)
+    H = W = 32
+    kw = lif_ref.make_unet_kwargs(base_num_channels=C)
+    model = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    ref = lif_ref.LIFFireNetRef(dict(kw), "LIFFireNet").train()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    ew = snnflow.EventWarping(cfg, dev)
+    rew = iwe_ref.EventWarpingRef([H, W], weight=0.001)
+    gen = torch.Generator(device=dev).manual_seed(17)
+    for t in range(2):
+        w = make_window(2, 400, H, W, gen, dev)
+        out = model(w["event_voxel"], w["event_cnt"])
+        rout = ref(None, w["event_cnt"].cpu())
+        np.testing.assert_allclose(out["flow"][0].detach().cpu().numpy(), rout["flow"][0].detach().numpy(),
+                                   rtol=1e-3, atol=1e-5)
+        ew.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        rew.event_flow_association(rout["flow"], w["event_list"].cpu(), w["event_list_pol_mask"].cpu(),
+                                   w["event_mask"].cpu())
+    loss, rloss = ew(), rew()
+    loss.backward()
+    rloss.backward()
+    np.testing.assert_allclose(loss.item(), rloss.item(), rtol=1e-4)
+    assert model.engine.prep.frag.get(1) is not None  # the fragment path ran
+    for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
+        assert _rel(a.grad.cpu().numpy(), b.grad.numpy()) < 2e-3, n
