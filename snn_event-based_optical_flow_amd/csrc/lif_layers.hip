@@ -29,6 +29,9 @@
 #ifndef SNNFLOW_SP32
 #define SNNFLOW_SP32 2  // threads per pixel of the C = 32 conv-layer kernels
 #endif
+#ifndef SNNFLOW_L32_WAVES
+#define SNNFLOW_L32_WAVES 4  // min waves per SIMD of the C = 32 LIF-fed backward kernels
+#endif
 #ifndef SNNFLOW_TRACE
 #define SNNFLOW_TRACE 0
 #endif
@@ -803,22 +806,28 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         halo_load<C, NTB>(a.g_cur, tl, H, W, rg);
         halo_load<C, NTB>(a.y, tl, H, W, ry);
     }
-    if constexpr (LIF_IN) {
-        constexpr int Q4 = CIN / 4;
-        const int64_t plane4 = (int64_t)a.B * H * W * Q4;
-        const float4* py4 = reinterpret_cast<const float4*>(a.prev_y);
-        const float4* pm4 = reinterpret_cast<const float4*>(a.prev_mem);
-        const float4* pg4 = reinterpret_cast<const float4*>(a.prev_g_state);
-        // unconditional 16-B loads (clamped pixel outside the image; results unused there)
-        const int64_t pc = ((int64_t)tl.b * H + (h < H ? h : H - 1)) * W + (w < W ? w : W - 1);
-        const int64_t base = pc * Q4 + ci0 / 4;
+    // layer l-1's inputs of the LIF backward at this thread's pixel; C = 32 loads them only after
+    // the input-gradient convs (48 registers fewer across the matrix-core loop)
+    constexpr bool LATE_D = C >= 32;
+    auto load_prev = [&]() {
+        if constexpr (LIF_IN) {
+            constexpr int Q4 = CIN / 4;
+            const int64_t plane4 = (int64_t)a.B * H * W * Q4;
+            const float4* py4 = reinterpret_cast<const float4*>(a.prev_y);
+            const float4* pm4 = reinterpret_cast<const float4*>(a.prev_mem);
+            const float4* pg4 = reinterpret_cast<const float4*>(a.prev_g_state);
+            // unconditional 16-B loads (clamped pixel outside the image; results unused there)
+            const int64_t pc = ((int64_t)tl.b * H + (h < H ? h : H - 1)) * W + (w < W ? w : W - 1);
+            const int64_t base = pc * Q4 + ci0 / 4;
 #pragma unroll
-        for (int q = 0; q < QI; ++q) {
-            dy[q] = py4[base + q];
-            dm[q] = ld4_or_zero(pm4, py4, base + q);
-            dg[q] = ld4_or_zero(pg4 ? pg4 + plane4 : nullptr, py4, base + q);
+            for (int q = 0; q < QI; ++q) {
+                dy[q] = py4[base + q];
+                dm[q] = ld4_or_zero(pm4, py4, base + q);
+                dg[q] = ld4_or_zero(pg4 ? pg4 + plane4 : nullptr, py4, base + q);
+            }
         }
-    }
+    };
+    if constexpr (!LATE_D) load_prev();
 
     // per-channel parameters (their round trip overlaps the halo loads)
     float st_mean = 0.f, st_inv = 0.f, gamma = 0.f;
@@ -953,6 +962,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                 }
             }
         }
+        if constexpr (LATE_D) load_prev();
         __syncthreads();
         if (do_x) {
             mfma_store<false>(ax, ax, G);
@@ -1049,8 +1059,11 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     }
 }
 
+// C = 32 LIF-fed layers: two blocks per CU (<= 128 registers) once the LIF-backward inputs are
+// loaded after the input-gradient convs (LATE_D)
 template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false>
-__global__ __launch_bounds__(NT * SPLIT) void k_layer_bwd(snnflow_layer_bwd_args a) {
+__global__ __launch_bounds__(NT * SPLIT, (C == 32 && LIF_IN && SPLIT == 2) ? SNNFLOW_L32_WAVES : 1)
+void k_layer_bwd(snnflow_layer_bwd_args a) {
     __shared__ __attribute__((aligned(16))) float pool[LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT, BFG>::FLOATS];
     layer_bwd_body<CIN, C, LIF_IN, REC, SPLIT, BFG>(a, hw_grid(), pool);
 }
