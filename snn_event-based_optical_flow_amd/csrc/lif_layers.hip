@@ -460,7 +460,8 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         // matrix-core implicit GEMM over the whole tile (weights in the [tap][c][cin] layout);
         // the sums come back through LDS, aliasing `tile`, in this thread's pixel/channel order
         constexpr int NW = NTB / 64;
-        MfmaAcc<C, C, NW> af, ar;
+        constexpr int NG = C >= 32 ? 2 : 1;  // C = 32: waves split the output channels too
+        MfmaAcc<C, C, NW, NG> af, ar;
         af.zero();
         if (!PROBE_OFF(16)) {
             const float* wf = WL ? wl_ff : a.wt_ff_t;
@@ -468,10 +469,10 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                 mfma_conv3x3_bf3f<C, C, NW>(reinterpret_cast<const __bf16*>(tile), reinterpret_cast<const __bf16*>(wl_ff), af);
             else if constexpr (L::BT) {  // spikes of layer l-1
                 const __bf16* tb = reinterpret_cast<const __bf16*>(tile);
-                if (a.wf_ff) mfma_conv3x3_bf3g<C, C, NW, __bf16>(tb, reinterpret_cast<const __bf16*>(a.wf_ff), af);
-                else mfma_conv3x3_bf3<C, C, NW, __bf16>(tb, wf, af);
+                if (a.wf_ff) mfma_conv3x3_bf3g<C, C, NW, __bf16, NG>(tb, reinterpret_cast<const __bf16*>(a.wf_ff), af);
+                else mfma_conv3x3_bf3<C, C, NW, __bf16, NG>(tb, wf, af);
             }
-            else mfma_conv3x3<C, C, false, NW>(tile, wf, af);
+            else mfma_conv3x3<C, C, false, NW, NG>(tile, wf, af);
         }
         bool rec_on = false;
         if constexpr (REC) {
@@ -492,9 +493,10 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                         if (rec_bf) mfma_conv3x3_bf3f<C, C, NW>(rt, reinterpret_cast<const __bf16*>(wl_rec), ar);
                         else mfma_conv3x3<C, C, false, NW>(rt, a.wt_rec_t, ar);  // non-binary s_prev
                     } else {
-                        if (rec_bf && a.wf_rec) mfma_conv3x3_bf3g<C, C, NW>(rt, reinterpret_cast<const __bf16*>(a.wf_rec), ar);
-                        else if (rec_bf) mfma_conv3x3_bf3<C, C, NW>(rt, wr, ar);
-                        else mfma_conv3x3<C, C, false, NW>(rt, wr, ar);
+                        if (rec_bf && a.wf_rec)
+                            mfma_conv3x3_bf3g<C, C, NW, float, NG>(rt, reinterpret_cast<const __bf16*>(a.wf_rec), ar);
+                        else if (rec_bf) mfma_conv3x3_bf3<C, C, NW, float, NG>(rt, wr, ar);
+                        else mfma_conv3x3<C, C, false, NW, NG>(rt, wr, ar);
                     }
                 }
             }
@@ -937,17 +939,18 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         constexpr int NW = NTB / 64;
         const bool do_x = a.wt_bwd_ff != nullptr;
         const bool do_r = REC && a.g_state_prev != nullptr;
-        MfmaAcc<C, CIN, NW> ax;
-        MfmaAcc<C, C, NW> arr;
+        constexpr int NG = (C >= 32 && BF6) ? 2 : 1;  // C = 32: waves split the output channels too
+        MfmaAcc<C, CIN, NW, NG> ax;
+        MfmaAcc<C, C, NW, NG> arr;
         const __bf16* g3 = reinterpret_cast<const __bf16*>(G);
         if (do_x) {
             ax.zero();
             if constexpr (FLDS) {
                 if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, CIN, NW>(g3, reinterpret_cast<const __bf16*>(wl_x), ax);
             } else if constexpr (BF6) {
-                if (!PROBE_OFF(1)) mfma_dgrad_bf6g<C, CIN, NW>(g3, reinterpret_cast<const __bf16*>(a.wd_ff), ax);
+                if (!PROBE_OFF(1)) mfma_dgrad_bf6g<C, CIN, NW, NG>(g3, reinterpret_cast<const __bf16*>(a.wd_ff), ax);
             } else {
-                if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW>(G, WL ? wl_x : a.wt_fwd_ff, ax);
+                if (!PROBE_OFF(1)) mfma_conv3x3<C, CIN, true, NW, NG>(G, WL ? wl_x : a.wt_fwd_ff, ax);
             }
         }
         if constexpr (REC) {
@@ -956,9 +959,9 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                 if constexpr (FLDS) {
                     if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, C, NW>(g3, reinterpret_cast<const __bf16*>(wl_r), arr);
                 } else if constexpr (BF6) {
-                    if (!PROBE_OFF(1)) mfma_dgrad_bf6g<C, C, NW>(g3, reinterpret_cast<const __bf16*>(a.wd_rec), arr);
+                    if (!PROBE_OFF(1)) mfma_dgrad_bf6g<C, C, NW, NG>(g3, reinterpret_cast<const __bf16*>(a.wd_rec), arr);
                 } else {
-                    if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW>(G, WL ? wl_r : a.wt_fwd_rec, arr);
+                    if (!PROBE_OFF(1)) mfma_conv3x3<C, C, true, NW, NG>(G, WL ? wl_r : a.wt_fwd_rec, arr);
                 }
             }
         }

@@ -160,14 +160,15 @@ __device__ inline void ld_vec(const float* p, float* v) {
     }
 }
 
-// B fragments of one tap (zeros for padded output channels n >= NOUT).
-template <int KIN, int NOUT>
-__device__ inline void mfma_load_b(const float* __restrict__ wB, int tap, float (&b)[MfmaGeo<KIN, NOUT>::BPT]) {
+// B fragments of one tap for n-tiles [ntb, ntb + WNT) (zeros for padded channels n >= NOUT).
+template <int KIN, int NOUT, int WNT = MfmaGeo<KIN, NOUT>::NNT>
+__device__ inline void mfma_load_b(const float* __restrict__ wB, int tap, int ntb,
+                                   float (&b)[WNT * MfmaGeo<KIN, NOUT>::NKB * MfmaGeo<KIN, NOUT>::E]) {
     using G = MfmaGeo<KIN, NOUT>;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
 #pragma unroll
-    for (int nt = 0; nt < G::NNT; ++nt) {
-        const int n = nt * 16 + m;
+    for (int nt = 0; nt < WNT; ++nt) {
+        const int n = (ntb + nt) * 16 + m;
         const bool ok = n < NOUT;
         const float* p = wB + (int64_t)(tap * NOUT + (ok ? n : 0)) * KIN + g * G::E;
 #pragma unroll
@@ -180,35 +181,46 @@ __device__ inline void mfma_load_b(const float* __restrict__ wB, int tap, float 
     }
 }
 
-template <int KIN, int NOUT, int NW>
+// Accumulators of one wave.  The 16 M-tiles x NNT N-tiles of a block are split over its NW
+// waves in NG n-groups: wave wv owns M-tiles [mt0, mt0 + MT) and N-tiles [nt0, nt0 + WNT).
+// NG = 1: every wave all N-tiles (fewest A reads); NG = 2 at C = 32: half the B operand per
+// wave (the weight fragments every wave streams from L2 halve).
+template <int KIN, int NOUT, int NW, int NG = 1>
 struct MfmaAcc {
-    static constexpr int MT = 16 / NW;  // M-tiles per wave
-    f32x4 v[MT][MfmaGeo<KIN, NOUT>::NNT];
+    static constexpr int NNT = MfmaGeo<KIN, NOUT>::NNT;
+    static_assert(NNT % NG == 0 && NW % NG == 0 && (16 * NG) % NW == 0, "wave tiling");
+    static constexpr int MT = 16 * NG / NW;  // M-tiles per wave
+    static constexpr int WNT = NNT / NG;     // N-tiles per wave
+    f32x4 v[MT][WNT];
+    __device__ static inline int mt0(int wv) { return (wv / NG) * MT; }
+    __device__ static inline int nt0(int wv) { return (wv % NG) * WNT; }
     __device__ inline void zero() {
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
-            for (int j = 0; j < MfmaGeo<KIN, NOUT>::NNT; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < WNT; ++j) v[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 };
 
-template <int KIN, int NOUT, bool FLIP, int NW>
-__device__ void mfma_conv3x3(const float* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW>& acc) {
+template <int KIN, int NOUT, bool FLIP, int NW, int NG = 1>
+__device__ void mfma_conv3x3(const float* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW, NG>& acc) {
     using G = MfmaGeo<KIN, NOUT>;
+    using A = MfmaAcc<KIN, NOUT, NW, NG>;
     static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
-    constexpr int P = Pad<KIN>::v, MT = 16 / NW;
+    constexpr int P = Pad<KIN>::v, MT = A::MT, WNT = A::WNT, BPW = WNT * G::NKB * G::E;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    float bc[G::BPT], bn[G::BPT];
-    mfma_load_b<KIN, NOUT>(wB, 0, bc);
+    const int mtb = A::mt0(wv), ntb = A::nt0(wv);
+    float bc[BPW], bn[BPW];
+    mfma_load_b<KIN, NOUT, WNT>(wB, 0, ntb, bc);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-        if (tap + 1 < 9) mfma_load_b<KIN, NOUT>(wB, tap + 1, bn);  // next tap's weights in flight
+        if (tap + 1 < 9) mfma_load_b<KIN, NOUT, WNT>(wB, tap + 1, ntb, bn);  // next tap's weights in flight
         const int ky = tap / 3, kx = tap - 3 * (tap / 3);
         const int oy = FLIP ? 2 - ky : ky, ox = FLIP ? 2 - kx : kx;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const int T = wv * MT + mt, row = T >> 1, c0 = (T & 1) * 16;
+            const int T = mtb + mt, row = T >> 1, c0 = (T & 1) * 16;
             const float* ap = src + ((row + oy) * HWD + c0 + m + ox) * P + g * G::E;
 #pragma unroll
             for (int kb = 0; kb < G::NKB; ++kb) {
@@ -217,14 +229,14 @@ __device__ void mfma_conv3x3(const float* src, const float* __restrict__ wB, Mfm
 #pragma unroll
                 for (int j = 0; j < G::E; ++j)
 #pragma unroll
-                    for (int nt = 0; nt < G::NNT; ++nt)
+                    for (int nt = 0; nt < WNT; ++nt)
                         acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], bc[(nt * G::NKB + kb) * G::E + j],
                                                                              acc.v[mt][nt], 0, 0, 0);
             }
         }
         if (tap + 1 < 9) {
 #pragma unroll
-            for (int i = 0; i < G::BPT; ++i) bc[i] = bn[i];
+            for (int i = 0; i < BPW; ++i) bc[i] = bn[i];
         }
     }
 }
@@ -265,14 +277,14 @@ __device__ inline void bf3_k(int i, int g, int& tap, int& c0) {
 
 __device__ inline bool exact_bf16(float v) { return v == (float)(__bf16)v; }
 
-template <int KIN, int NOUT>
-__device__ inline void bf3_load_b(const float* __restrict__ wB, int i, float (&w)[Bf3Geo<KIN, NOUT>::NNT][8]) {
+template <int KIN, int NOUT, int WNT = Bf3Geo<KIN, NOUT>::NNT>
+__device__ inline void bf3_load_b(const float* __restrict__ wB, int i, int ntb, float (&w)[WNT][8]) {
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     int tap, c0;
     bf3_k<KIN>(i, g, tap, c0);
 #pragma unroll
-    for (int nt = 0; nt < Bf3Geo<KIN, NOUT>::NNT; ++nt) {
-        const int n = nt * 16 + m;
+    for (int nt = 0; nt < WNT; ++nt) {
+        const int n = (ntb + nt) * 16 + m;
         if (tap < 9 && n < NOUT) {
             const float* p = wB + (int64_t)(tap * NOUT + n) * KIN + c0;
             const float4 u = *reinterpret_cast<const float4*>(p), v = *reinterpret_cast<const float4*>(p + 4);
@@ -285,23 +297,25 @@ __device__ inline void bf3_load_b(const float* __restrict__ wB, int i, float (&w
     }
 }
 
-template <int KIN, int NOUT, int NW, typename AT = float>
-__device__ void mfma_conv3x3_bf3(const AT* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW>& acc) {
+template <int KIN, int NOUT, int NW, typename AT = float, int NG = 1>
+__device__ void mfma_conv3x3_bf3(const AT* src, const float* __restrict__ wB, MfmaAcc<KIN, NOUT, NW, NG>& acc) {
     using G = Bf3Geo<KIN, NOUT>;
+    using A = MfmaAcc<KIN, NOUT, NW, NG>;
     static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
     static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
     constexpr bool ABF = std::is_same<AT, __bf16>::value;  // A: bf16 tile [HN][KIN] of exact values
-    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = 16 / NW;
+    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = A::MT, WNT = A::WNT;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    float wc[G::NNT][8], wn[G::NNT][8];
-    bf3_load_b<KIN, NOUT>(wB, 0, wc);
+    const int mtb = A::mt0(wv), ntb = A::nt0(wv);
+    float wc[WNT][8], wn[WNT][8];
+    bf3_load_b<KIN, NOUT, WNT>(wB, 0, ntb, wc);
 #pragma unroll
     for (int i = 0; i < G::NI; ++i) {
-        if (i + 1 < G::NI) bf3_load_b<KIN, NOUT>(wB, i + 1, wn);  // next chunk's weights in flight
-        bf16x8 bh[G::NNT], bm[G::NNT], bl[G::NNT];
+        if (i + 1 < G::NI) bf3_load_b<KIN, NOUT, WNT>(wB, i + 1, ntb, wn);  // next chunk's weights in flight
+        bf16x8 bh[WNT], bm[WNT], bl[WNT];
 #pragma unroll
-        for (int nt = 0; nt < G::NNT; ++nt)
+        for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const float w = wc[nt][j];
@@ -317,7 +331,7 @@ __device__ void mfma_conv3x3_bf3(const AT* src, const float* __restrict__ wB, Mf
         const int ky = tap / 3, kx = tap - 3 * (tap / 3);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            const int T = mtb + mt, row = T >> 1, cb = (T & 1) * 16;
             bf16x8 a;
             if (tap < 9) {
                 const AT* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
@@ -333,7 +347,7 @@ __device__ void mfma_conv3x3_bf3(const AT* src, const float* __restrict__ wB, Mf
                 for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
             }
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt) {
+            for (int nt = 0; nt < WNT; ++nt) {
                 acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl[nt], acc.v[mt][nt], 0, 0, 0);
                 acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bm[nt], acc.v[mt][nt], 0, 0, 0);
                 acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bh[nt], acc.v[mt][nt], 0, 0, 0);
@@ -341,7 +355,7 @@ __device__ void mfma_conv3x3_bf3(const AT* src, const float* __restrict__ wB, Mf
         }
         if (i + 1 < G::NI) {
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt)
+            for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) wc[nt][j] = wn[nt][j];
         }
@@ -446,35 +460,37 @@ __device__ void mfma_conv3x3_bf3f(const AT* src, const __bf16* frag, MfmaAcc<KIN
 // mfma_conv3x3_bf3f with the fragments in global memory (snnflow_prep_desc.frag_fwd, L2-resident:
 // every block reads the same few KB), the next chunk's fragments in flight during this chunk's
 // products.  C = 16 / 32, where the fragments do not fit beside the tiles in LDS.
-template <int KIN, int NOUT, int NW, typename AT = float>
-__device__ void mfma_conv3x3_bf3g(const AT* src, const __bf16* __restrict__ frag, MfmaAcc<KIN, NOUT, NW>& acc) {
+template <int KIN, int NOUT, int NW, typename AT = float, int NG = 1>
+__device__ void mfma_conv3x3_bf3g(const AT* src, const __bf16* __restrict__ frag, MfmaAcc<KIN, NOUT, NW, NG>& acc) {
     using G = Bf3Geo<KIN, NOUT>;
+    using A = MfmaAcc<KIN, NOUT, NW, NG>;
     static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
     static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
     constexpr bool ABF = std::is_same<AT, __bf16>::value;
-    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = 16 / NW;
+    constexpr int P = ABF ? KIN : Pad<KIN>::v, MT = A::MT, WNT = A::WNT;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int mtb = A::mt0(wv), ntb = A::nt0(wv);
     const bf16x8* fv = reinterpret_cast<const bf16x8*>(frag) + lane;
-    bf16x8 cur[G::NNT][3], nxt[G::NNT][3];
+    bf16x8 cur[WNT][3], nxt[WNT][3];
 #pragma unroll
-    for (int nt = 0; nt < G::NNT; ++nt)
+    for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) cur[nt][q] = fv[(nt * 3 + q) * 64];
+        for (int q = 0; q < 3; ++q) cur[nt][q] = fv[((ntb + nt) * 3 + q) * 64];
 #pragma unroll
     for (int i = 0; i < G::NI; ++i) {
         if (i + 1 < G::NI) {
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt)
+            for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + nt) * 3 + q) * 64];
+                for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + ntb + nt) * 3 + q) * 64];
         }
         int tap, c0;
         bf3_k<KIN>(i, g, tap, c0);
         const int ky = tap / 3, kx = tap - 3 * (tap / 3);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            const int T = mtb + mt, row = T >> 1, cb = (T & 1) * 16;
             bf16x8 a;
             if (tap < 9) {
                 const AT* ap = src + ((row + ky) * HWD + cb + m + kx) * P + c0;
@@ -490,7 +506,7 @@ __device__ void mfma_conv3x3_bf3g(const AT* src, const __bf16* __restrict__ frag
                 for (int j = 0; j < 8; ++j) a[j] = (__bf16)0.0f;
             }
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt) {
+            for (int nt = 0; nt < WNT; ++nt) {
                 acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[nt][2], acc.v[mt][nt], 0, 0, 0);
                 acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[nt][1], acc.v[mt][nt], 0, 0, 0);
                 acc.v[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, cur[nt][0], acc.v[mt][nt], 0, 0, 0);
@@ -498,7 +514,7 @@ __device__ void mfma_conv3x3_bf3g(const AT* src, const __bf16* __restrict__ frag
         }
         if (i + 1 < G::NI) {
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt)
+            for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
                 for (int q = 0; q < 3; ++q) cur[nt][q] = nxt[nt][q];
         }
@@ -564,27 +580,29 @@ __device__ void mfma_dgrad_bf6(const __bf16* src3, const __bf16* frag, MfmaAcc<K
 
 // mfma_dgrad_bf6 with the weight fragments in global memory (snnflow_prep_desc.frag_bwd,
 // L2-resident), the next chunk's in flight during this chunk's products (C = 16 / 32).
-template <int KIN, int NOUT, int NW>
-__device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ frag, MfmaAcc<KIN, NOUT, NW>& acc) {
+template <int KIN, int NOUT, int NW, int NG = 1>
+__device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ frag, MfmaAcc<KIN, NOUT, NW, NG>& acc) {
     using G = Bf3Geo<KIN, NOUT>;
+    using A = MfmaAcc<KIN, NOUT, NW, NG>;
     static_assert(NT == 256 && TW == 32 && 16 % NW == 0, "MFMA conv: 8x32 tiles, NW | 16");
     static_assert(G::NNT == MfmaGeo<KIN, NOUT>::NNT, "accumulator tiling");
-    constexpr int MT = 16 / NW, PART = HN * KIN;
+    constexpr int MT = A::MT, WNT = A::WNT, PART = HN * KIN;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int mtb = A::mt0(wv), ntb = A::nt0(wv);
     const bf16x8* fv = reinterpret_cast<const bf16x8*>(frag) + lane;
-    bf16x8 cur[G::NNT][3], nxt[G::NNT][3];
+    bf16x8 cur[WNT][3], nxt[WNT][3];
 #pragma unroll
-    for (int nt = 0; nt < G::NNT; ++nt)
+    for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) cur[nt][q] = fv[(nt * 3 + q) * 64];
+        for (int q = 0; q < 3; ++q) cur[nt][q] = fv[((ntb + nt) * 3 + q) * 64];
 #pragma unroll
     for (int i = 0; i < G::NI; ++i) {
         if (i + 1 < G::NI) {
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt)
+            for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + nt) * 3 + q) * 64];
+                for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + ntb + nt) * 3 + q) * 64];
         }
         int tap, c0;
         bf3_k<KIN>(i, g, tap, c0);
@@ -592,7 +610,7 @@ __device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ f
         const int oy = 2 - ky, ox = 2 - kx;
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const int T = wv * MT + mt, row = T >> 1, cb = (T & 1) * 16;
+            const int T = mtb + mt, row = T >> 1, cb = (T & 1) * 16;
             bf16x8 ah, am, al;
             if (tap < 9) {
                 const __bf16* ap = src3 + ((row + oy) * HWD + cb + m + ox) * KIN + c0;
@@ -604,7 +622,7 @@ __device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ f
                 for (int j = 0; j < 8; ++j) ah[j] = am[j] = al[j] = (__bf16)0.0f;
             }
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt) {
+            for (int nt = 0; nt < WNT; ++nt) {
                 f32x4 c = acc.v[mt][nt];
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, cur[nt][1], c, 0, 0, 0);
                 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, cur[nt][0], c, 0, 0, 0);
@@ -617,7 +635,7 @@ __device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ f
         }
         if (i + 1 < G::NI) {
 #pragma unroll
-            for (int nt = 0; nt < G::NNT; ++nt)
+            for (int nt = 0; nt < WNT; ++nt)
 #pragma unroll
                 for (int q = 0; q < 3; ++q) cur[nt][q] = nxt[nt][q];
         }
@@ -668,17 +686,19 @@ struct WStage {
 
 // Accumulators (C/D layout: lane holds pixels 4g..4g+3 of its M-tile, channel n = lane & 15)
 // [+ a second set added element-wise when SUM: ff + rec] -> LDS out[NT][Pad<NOUT>].
-template <bool SUM, int KIN, int NOUT, int NW, int KIN2>
-__device__ void mfma_store(const MfmaAcc<KIN, NOUT, NW>& acc, const MfmaAcc<KIN2, NOUT, NW>& acc2, float* out) {
-    constexpr int PO = Pad<NOUT>::v, MT = 16 / NW, NNT = MfmaGeo<KIN, NOUT>::NNT;
+template <bool SUM, int KIN, int NOUT, int NW, int KIN2, int NG>
+__device__ void mfma_store(const MfmaAcc<KIN, NOUT, NW, NG>& acc, const MfmaAcc<KIN2, NOUT, NW, NG>& acc2, float* out) {
+    using A = MfmaAcc<KIN, NOUT, NW, NG>;
+    constexpr int PO = Pad<NOUT>::v, MT = A::MT, WNT = A::WNT;
     const int lane = threadIdx.x & 63, m = lane & 15, g = lane >> 4;
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int mtb = A::mt0(wv), ntb = A::nt0(wv);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-        const int T = wv * MT + mt, row = T >> 1, c0 = (T & 1) * 16;
+        const int T = mtb + mt, row = T >> 1, c0 = (T & 1) * 16;
 #pragma unroll
-        for (int nt = 0; nt < NNT; ++nt) {
-            const int n = nt * 16 + m;
+        for (int nt = 0; nt < WNT; ++nt) {
+            const int n = (ntb + nt) * 16 + m;
             if (n < NOUT) {
                 f32x4 v = acc.v[mt][nt];
                 if constexpr (SUM) v = v + acc2.v[mt][nt];
