@@ -871,3 +871,37 @@ def test_engine_gradients_wide_vs_oracle(dev, C):
     assert model.engine.prep.frag.get(1) is not None  # the fragment path ran
     for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
         assert _rel(a.grad.cpu().numpy(), b.grad.numpy()) < 2e-3, n
+
+
+def test_forward_sequence_chained_without_detach(dev):
+    """Two forward_sequence calls whose states are not detached in between (one BPTT window of
+    2T steps): the second call's backward must hand its state gradients to the first (non-root
+    node, deferred weight gradients flushed once by the first) -- against 2T model() calls."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(21)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    H = W = 48
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    ea, eb = snnflow.EventWarping(cfg, dev), snnflow.EventWarping(cfg, dev)
+    gen = torch.Generator(device=dev).manual_seed(22)
+    wins = [make_window(2, 300, H, W, gen, dev) for _ in range(6)]
+    fa = [ma(w["event_voxel"], w["event_cnt"])["flow"][0] for w in wins]
+    outs = (mb.forward_sequence([w["event_voxel"] for w in wins[:3]], [w["event_cnt"] for w in wins[:3]]) +
+            mb.forward_sequence([w["event_voxel"] for w in wins[3:]], [w["event_cnt"] for w in wins[3:]]))
+    for t, w in enumerate(wins):
+        ea.event_flow_association([fa[t]], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        eb.event_flow_association(outs[t]["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+    la, lb = ea(), eb()
+    la.backward()
+    lb.backward()
+    np.testing.assert_allclose(lb.item(), la.item(), rtol=1e-6)
+    for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
+        assert _rel(b.grad.cpu().numpy(), a.grad.cpu().numpy()) < 1e-5, n
