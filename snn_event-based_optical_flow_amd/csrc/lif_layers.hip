@@ -349,7 +349,12 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     [[maybe_unused]] constexpr int TK = REC ? 1 : 0;
     TRACE_AT(TR, TK, 0);
 
-    // 1. issue every global load of the tile before any use (weights for LDS first)
+    // 1. issue every global load of the tile before any use: the BN-sum replicas first (their
+    //    reduction and the coefficients then overlap the halo loads), weights for LDS next
+    AccGather<LIF_IN ? 2 * CIN : 1> gat;
+    if constexpr (LIF_IN) {
+        if (a.prev.bn_train) acc_gather_load<2 * CIN>(a.prev_acc, 2 * CIN, gat);
+    }
     constexpr bool WL = L::WL, FRAG = L::FRAG;
     WStage<WL ? 9 * C * C : 1, NTB> sw_ff, sw_rec;
     FragStage<FRAG ? C : 8, FRAG ? C : 8, FRAG ? NTB : 64> fs_ff, fs_rec;
@@ -377,7 +382,7 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         else zero4(rm, R);
         const NeuronRegs nr = load_neuron(a.prev, CIN, g.bid == 0);
         __shared__ double sums[2 * CIN];
-        if (a.prev.bn_train) acc_gather<2 * CIN>(a.prev_acc, 2 * CIN, sums);
+        if (a.prev.bn_train) acc_gather_reduce<2 * CIN>(gat, sums);
         lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr, g.bid == 0);
         __syncthreads();
         // (stores issued after the gather: CDNA's vmcnt counts stores, so zeroing before the
@@ -785,7 +790,12 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     [[maybe_unused]] constexpr int TK = REC ? 3 : 2;
     TRACE_AT(TR, TK, 0);
 
-    // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS)
+    // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS);
+    //    the BN-sum replicas first, so that their reduction overlaps the halo loads
+    //    (C <= 16; at C = 32 the 12 extra live registers spill: gathered in place there)
+    constexpr bool EARLY_G = C <= 16;
+    AccGather<SNNFLOW_BWD_ACC(C)> gat;
+    if constexpr (EARLY_G) acc_gather_load<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), gat);
     constexpr bool WL = LB::WL, BF6 = LB::BF6, FLDS = BF6 && C == 8;  // FLDS: fragments in LDS
     WStage<WL ? 9 * C * C : 1, NTB> sw_x, sw_r;
     FragStage<FLDS ? C : 8, FLDS ? CIN : 8, FLDS ? NTB : 64> fs_x, fs_r;
@@ -852,7 +862,8 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     // 2. per-channel constants; block 0 finishes layer l's neuron gradients and stores the
     //    BN backward coefficients for the deferred weight gradient
     __shared__ double sums[SNNFLOW_BWD_ACC(C)];
-    acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
+    if constexpr (EARLY_G) acc_gather_reduce<SNNFLOW_BWD_ACC(C)>(gat, sums);
+    else acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
     neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
     if (tid < C) {
         const float mean = st_mean, inv = st_inv;

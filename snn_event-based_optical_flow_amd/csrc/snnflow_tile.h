@@ -759,6 +759,51 @@ __device__ inline void zero_consumed(double* z0, double* z1, int n) { zero_consu
 // into LDS out[M]: TPJ = NT/M threads per sum each add a strided subset of the
 // replicas (all their loads in flight at once), then one LDS pass.  One global round
 // trip; called by every thread of the block (contains barriers).
+// Split form: acc_gather_load issues the replica loads into registers (call it before the
+// kernel's other loads, so that the coefficient math after acc_gather_reduce overlaps their
+// latency instead of waiting behind them: vmcnt retires loads in order).
+template <int M>
+struct AccGather {
+    static_assert(M >= 1 && M <= NT, "acc_gather: M sums");
+    static constexpr int TPJ = NT / M;
+    static constexpr int PER = (kAccShards + TPJ - 1) / TPJ;
+    double v[PER];
+};
+
+template <int M>
+__device__ inline void acc_gather_load(const double* acc, int n, AccGather<M>& r) {
+    using A = AccGather<M>;
+    const int tid = threadIdx.x, st = acc_stride(n);
+    const int j = tid % M, g = tid / M;
+#pragma unroll
+    for (int k = 0; k < A::PER; ++k) {
+        const int sh = g + k * A::TPJ;
+        r.v[k] = (tid < A::TPJ * M && sh < kAccShards) ? acc[sh * st + j] : 0.0;
+    }
+}
+
+template <int M>
+__device__ void acc_gather_reduce(const AccGather<M>& r, double* out) {
+    using A = AccGather<M>;
+    constexpr int TPJ = A::TPJ, PER = A::PER;
+    __shared__ double red[TPJ * M];
+    const int tid = threadIdx.x;
+    if (tid < TPJ * M) {
+        const int j = tid % M, g = tid / M;
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) sum += r.v[k];
+        red[g * M + j] = sum;
+    }
+    __syncthreads();
+    if (tid < M) {
+        double sum = 0.0;
+        for (int g = 0; g < TPJ; ++g) sum += red[g * M + tid];
+        out[tid] = sum;
+    }
+    __syncthreads();
+}
+
 template <int M>
 __device__ void acc_gather(const double* acc, int n, double* out) {
     static_assert(M >= 1 && M <= NT, "acc_gather: M sums");
