@@ -352,8 +352,10 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     // 1. issue every global load of the tile before any use: the BN-sum replicas first (their
     //    reduction and the coefficients then overlap the halo loads), weights for LDS next
     AccGather<LIF_IN ? 2 * CIN : 1> gat;
+    NeuronRegs nr = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (LIF_IN) {
         if (a.prev.bn_train) acc_gather_load<2 * CIN>(a.prev_acc, 2 * CIN, gat);
+        nr = load_neuron(a.prev, CIN, g.bid == 0);
     }
     constexpr bool WL = L::WL, FRAG = L::FRAG;
     WStage<WL ? 9 * C * C : 1, NTB> sw_ff, sw_rec;
@@ -380,7 +382,6 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         halo_load<CIN, NTB>(a.prev_y, tl, H, W, ry);
         if (a.prev_mem) halo_load<CIN, NTB>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
-        const NeuronRegs nr = load_neuron(a.prev, CIN, g.bid == 0);
         __shared__ double sums[2 * CIN];
         if (a.prev.bn_train) acc_gather_reduce<2 * CIN>(gat, sums);
         lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr, g.bid == 0);
@@ -796,6 +797,24 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     constexpr bool EARLY_G = C <= 16;
     AccGather<SNNFLOW_BWD_ACC(C)> gat;
     if constexpr (EARLY_G) acc_gather_load<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), gat);
+    // per-channel parameters, also ahead of the halo loads
+    float st_mean = 0.f, st_inv = 0.f, gamma = 0.f;
+    if (tid < C) {
+        st_mean = a.stats[tid];
+        st_inv = a.stats[C + tid];
+        gamma = a.n.bn_weight[tid];
+    }
+    const NeuronGradRegs ngr =
+        load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
+    LifCoef pk = {0.f, 0.f, 0.f, 0.f};
+    float pmu = 0.f;
+    if constexpr (LIF_IN) {
+        if (tid < CIN) {
+            pk = lif_coef(a.prev, a.prev_stats, CIN, tid);
+            pmu = a.prev_stats[tid];
+        }
+    }
+
     constexpr bool WL = LB::WL, BF6 = LB::BF6, FLDS = BF6 && C == 8;  // FLDS: fragments in LDS
     WStage<WL ? 9 * C * C : 1, NTB> sw_x, sw_r;
     FragStage<FLDS ? C : 8, FLDS ? CIN : 8, FLDS ? NTB : 64> fs_x, fs_r;
@@ -841,23 +860,6 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     };
     if constexpr (!LATE_D) load_prev();
 
-    // per-channel parameters (their round trip overlaps the halo loads)
-    float st_mean = 0.f, st_inv = 0.f, gamma = 0.f;
-    if (tid < C) {
-        st_mean = a.stats[tid];
-        st_inv = a.stats[C + tid];
-        gamma = a.n.bn_weight[tid];
-    }
-    const NeuronGradRegs ngr =
-        load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
-    LifCoef pk = {0.f, 0.f, 0.f, 0.f};
-    float pmu = 0.f;
-    if constexpr (LIF_IN) {
-        if (tid < CIN) {
-            pk = lif_coef(a.prev, a.prev_stats, CIN, tid);
-            pmu = a.prev_stats[tid];
-        }
-    }
 
     // 2. per-channel constants; block 0 finishes layer l's neuron gradients and stores the
     //    BN backward coefficients for the deferred weight gradient
