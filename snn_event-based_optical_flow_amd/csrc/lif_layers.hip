@@ -587,15 +587,18 @@ __device__ void lif_fwd_body(const snnflow_lif_fwd_args& a, const Grid g) {
     const float4* y4 = reinterpret_cast<const float4*>(a.y);
     const float4* m4 = reinterpret_cast<const float4*>(a.mem);
     const int64_t pc = act ? p : npix - 1;  // unconditional 16-B loads
+    // BN-sum replicas and per-channel parameters first: their math then overlaps the pixel loads
+    AccGather<2 * C> gat;
+    if (a.n.bn_train) acc_gather_load<2 * C>(a.acc, 2 * C, gat);
+    const NeuronRegs nr = load_neuron(a.n, C, g.bid == 0);
     float4 yv[Q], mv[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         yv[q] = y4[pc * Q + q];
         mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
     }
-    const NeuronRegs nr = load_neuron(a.n, C, g.bid == 0);
     __shared__ double sums[2 * C];
-    if (a.n.bn_train) acc_gather<2 * C>(a.acc, 2 * C, sums);
+    if (a.n.bn_train) acc_gather_reduce<2 * C>(gat, sums);
     lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr, g.bid == 0);
     __syncthreads();
     zero_consumed(a.zero0, a.zero1, a.zero_n, g);  // after the gather (vmcnt counts stores)
@@ -642,7 +645,13 @@ __device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
     const bool act = p < npix;
     const int64_t pc = act ? p : npix - 1;
     const int64_t b = pc / HWp, hw = pc - b * HWp;
-    // loads first
+    // per-channel coefficients first (their loads then do not wait behind the pixel loads)
+    LifCoef kc = {0.f, 0.f, 0.f, 0.f};
+    float mu = 0.f;
+    if (tid < C) {
+        kc = lif_coef(a.n, a.stats, C, tid);
+        mu = a.stats[tid];
+    }
     float4 yv[Q], mv[Q], gs[Q];
     const float4* y4 = reinterpret_cast<const float4*>(a.y);
     const float4* m4 = reinterpret_cast<const float4*>(a.mem);
@@ -668,8 +677,8 @@ __device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
         }
     }
     if (tid < C) {
-        coef[tid] = lif_coef(a.n, a.stats, C, tid);
-        meanv[tid] = a.stats[tid];
+        coef[tid] = kc;
+        meanv[tid] = mu;
     }
     __syncthreads();
     const bool zr = a.n.zero_reset != 0;
