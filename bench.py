@@ -82,8 +82,8 @@ def slot_pass_bytes(kind, C, P, cin0, T, layer_spec):
     rec = [r for _, r in layer_spec]
     if kind == "fwd_slot":
         names = ["conv_fwd[0]"] + ["conv_fwd_rec" if r else "conv_fwd" for r in rec[1:]] + ["lif_fwd"]
-    else:
-        names = ["lif_bwd"] + ["layer_bwd_rec" if r else "layer_bwd" for r in rec[1:]] + ["layer_bwd_head"]
+    else:  # the head's backward reads no pixels without an input gradient (one block: neuron grads only)
+        names = ["lif_bwd"] + ["layer_bwd_rec" if r else "layer_bwd" for r in rec[1:]]
     return T * sum(algorithmic_bytes(n, C, P, cin0) for n in names)
 
 
