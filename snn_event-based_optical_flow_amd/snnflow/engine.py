@@ -723,8 +723,7 @@ class FireNetSequence(torch.autograd.Function):
             elif eng.rec[l]:
                 g0[l] = empty_state(B, C, H, W, dev)
         g_out[0] = g0
-        ext = [[False] * L] * T
-        ext[0] = ctx.ext
+        ext = [list(ctx.ext)] + [[False] * L for _ in range(T - 1)]  # only step 0 sees external states
         gmem = [[None] * L for _ in range(T)]
         gmem[0] = [g0[l] if (g0[l] is not None and ctx.ext[l]) else None for l in range(L)]
         gxs = [torch.empty_like(xs[t]) if ctx.needs_input_grad[2 + t] else None for t in range(T)]
