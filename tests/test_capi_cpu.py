@@ -114,3 +114,33 @@ def test_wavefront_slots_respect_dependencies():
                 for dep in ((k - 1, t), (k, t - 1), (k + 1, t - 1)):
                     if dep in where:
                         assert where[dep] < i, (T, K, k, t, dep)
+
+
+def test_slot_and_fragment_entry_points_validate_without_gpu():
+    """snnflow_fwd_slot / snnflow_bwd_slot refuse bad task lists before any launch; the
+    fragment size query matches the kernels' operand geometry (chunks x n-tiles x 3 x 512)."""
+    from snnflow import _lib
+
+    lib = _lib.lib
+    assert lib.snnflow_slot_supported(8, 2) == 1 and lib.snnflow_slot_supported(32, 2) == 0
+    assert lib.snnflow_slot_supported(8, 5) == 0
+    conv = (_lib.ConvFwdArgs * 5)()
+    assert lib.snnflow_fwd_slot(conv, 5, None, None) == -1          # more than 4 tasks
+    assert lib.snnflow_fwd_slot(conv, 0, None, None) == -1          # no task
+    for i in range(2):
+        c = conv[i]
+        c.B, c.H, c.W, c.c, c.cin, c.lif_in = 1, 8, 8, 8, 2, 0
+        c.wt_ff = c.y = c.x = 1
+    conv[1].H = 16
+    assert lib.snnflow_fwd_slot(conv, 2, None, None) == -1          # tasks of different shapes
+    assert b"shapes" in lib.snnflow_last_error()
+    conv[0].c = conv[1].c = 16
+    assert lib.snnflow_fwd_slot(conv, 1, None, None) == -2          # c != 8
+    layer = (_lib.LayerBwdArgs * 1)()
+    assert lib.snnflow_bwd_slot(layer, 1, None, None) == -2         # c = 0
+    layer[0].c = 8
+    assert lib.snnflow_bwd_slot(layer, 1, None, None) == -1         # missing buffers
+    assert lib.snnflow_frag_halfs(8, 8) == 3 * 1 * 3 * 512          # 3 K chunks (4 taps each)
+    assert lib.snnflow_frag_halfs(16, 16) == 5 * 1 * 3 * 512
+    assert lib.snnflow_frag_halfs(32, 32) == 9 * 2 * 3 * 512
+    assert lib.snnflow_frag_halfs(32, 2) == 0 and lib.snnflow_frag_halfs(12, 12) == 0
