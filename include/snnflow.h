@@ -441,6 +441,14 @@ int snnflow_lif_export(const float* x, const float* mem, const float* beta, cons
  * total = ||g||_2, g *= min(max_norm / (total + eps), 1); total_out (device, may be NULL). */
 int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float* total_out, void* stream);
 
+/* Activity log of LIFFireNet.forward(log=True) (models/model.py:188-205: per tensor
+ * `l.detach().ne(0).float().mean()`): counts[i] = number of non-zero elements (NaN counts, -0 does
+ * not) of the i-th dense fp32 region ptrs[i][0 .. sizes[i]).  ptrs/sizes are host arrays of n <=
+ * SNNFLOW_MAX_COUNT_TENSORS entries; counts is a device array of n uint64, overwritten.  Exact
+ * integer counts (wavefront ballots + popcount, integer atomics): order-independent. */
+#define SNNFLOW_MAX_COUNT_TENSORS 16
+int snnflow_count_nonzero(const float* const* ptrs, const int64_t* sizes, int n, uint64_t* counts, void* stream);
+
 const char* snnflow_last_error(void);
 int snnflow_abi_version(void);
 

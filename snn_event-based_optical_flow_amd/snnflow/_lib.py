@@ -191,12 +191,14 @@ EXPORTS = {
     "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
+    "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),
     "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),
     "snnflow_slot_supported": (I32, [I32, I32]),
     "snnflow_frag_halfs": (I32, [I32, I32]),
 }
 MAX_SLOT_TASKS = 4
+MAX_COUNT_TENSORS = 16
 
 
 def _load():

@@ -9,10 +9,13 @@ hooks are registered on a cell, the cells are called one by one instead (hooks s
 the reference's ``(spk, state)`` outputs).
 """
 import copy
+import ctypes
 
+import numpy as np
 import torch
 import torch.nn as nn
 
+from . import _lib
 from .cells import ConvLayer, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
 from .engine import FireNetEngine, FireNetSequence, FireNetStep
 
@@ -30,6 +33,40 @@ def copy_states(states):
     if states[0] is None:
         return copy.deepcopy(states)
     return [s.clone() if hasattr(s, "clone") else type(s)(t.clone() for t in s) for s in states]
+
+
+def _dense(t):
+    """True when t's elements fill one contiguous memory span (any dimension order)."""
+    dims = sorted((st, n) for st, n in zip(t.stride(), t.shape) if n > 1)
+    expect = 1
+    for st, n in dims:
+        if st != expect:
+            return False
+        expect *= n
+    return True
+
+
+def activity_log(names, tensors):
+    """``models/model.py:188-205``: ``{name: l.detach().ne(0).float().mean().item()}`` for every
+    layer output of the step, as ONE ``snnflow_count_nonzero`` launch (wavefront ballots) and one
+    read-back instead of a reduction and a host sync per tensor.  The counts are exact; the mean
+    is the fp32 quotient count / numel, as torch's fp32 mean of 0/1 values below 2**24."""
+    ts = [t.detach() for t in tensors]
+    ts = [t if _dense(t) else t.contiguous() for t in ts]
+    for t, n in zip(ts, names):
+        _lib.require_device(t, n)
+    counts = torch.empty(len(ts), dtype=torch.int64, device=ts[0].device)
+    res = {}
+    for i0 in range(0, len(ts), _lib.MAX_COUNT_TENSORS):
+        chunk = ts[i0:i0 + _lib.MAX_COUNT_TENSORS]
+        ptrs = (ctypes.c_void_p * len(chunk))(*[t.data_ptr() for t in chunk])
+        sizes = (ctypes.c_int64 * len(chunk))(*[t.numel() for t in chunk])
+        _lib.call("count_nonzero", _lib.lib.snnflow_count_nonzero, ptrs, sizes, len(chunk),
+                  counts[i0:].data_ptr(), _lib.stream_ptr(ts[0].device))
+    host = counts.cpu().numpy()
+    for n, t, c in zip(names, ts, host):
+        res[n] = float(np.float32(c) / np.float32(t.numel())) if t.numel() else float("nan")
+    return res
 
 
 class _FireNetBase(BaseModel):
@@ -160,7 +197,7 @@ class _FireNetBase(BaseModel):
         if isinstance(log, bool) and log and not self.exporting:
             names = ["0:input"] + [f"{i + 1}:{n}" for i, (n, _) in enumerate(self.layer_spec)]
             names.append(f"{len(self.layer_spec) + 1}:pred")
-            activity = {n: t.detach().ne(0).float().mean().item() for n, t in zip(names, [x] + outs + [flow])}
+            activity = activity_log(names, [x] + outs + [flow])
         return {"flow": [flow], "activity": activity}
 
 

@@ -81,6 +81,12 @@ def test_argument_validation_without_gpu():
     assert lib.snnflow_iwe_loss_fwd(ctypes.byref(e), None) == -1
     assert lib.snnflow_conv_blocks(8, 128, 128) == 8 * 16 * 4
     assert lib.snnflow_slab_reduce(None, 1, 1, None) == -1
+    ptrs, sizes = (ctypes.c_void_p * 17)(), (ctypes.c_int64 * 17)()
+    assert lib.snnflow_count_nonzero(ptrs, sizes, 0, 1, None) == -1    # no tensor
+    assert lib.snnflow_count_nonzero(ptrs, sizes, 17, 1, None) == -1   # > SNNFLOW_MAX_COUNT_TENSORS
+    sizes[0] = 4
+    assert lib.snnflow_count_nonzero(ptrs, sizes, 1, 1, None) == -1    # NULL data, non-empty
+    assert b"count_nonzero" in lib.snnflow_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

@@ -905,3 +905,55 @@ def test_forward_sequence_chained_without_detach(dev):
     np.testing.assert_allclose(lb.item(), la.item(), rtol=1e-6)
     for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
         assert _rel(b.grad.cpu().numpy(), a.grad.cpu().numpy()) < 1e-5, n
+
+
+# ---------------------------------------------------------------------------
+# Activity log (models/model.py:188-205)
+# ---------------------------------------------------------------------------
+def test_count_nonzero_exact_on_edge_cases(dev):
+    """snnflow_count_nonzero against torch's count: ragged sizes (not multiples of 4 or of a
+    block), an unaligned start, -0.0 (not counted), NaN and inf (counted), empty and all-zero
+    regions, a permuted dense view (the [2,B,C,H,W] state over NHWC memory) -- exact against the
+    CPU reduction (fp32 sum / numel; torch's HIP mean multiplies by 1/numel and can differ by
+    one ulp)."""
+    from snnflow.model import activity_log
+
+    g = torch.Generator(device=dev).manual_seed(5)
+    base = (torch.rand(1 << 20, generator=g, device=dev) < 0.3).float()
+    special = torch.tensor([0.0, -0.0, float("nan"), float("inf"), -1e-38, 1e-45], device=dev)
+    nhwc = (torch.rand(2, 3, 17, 19, 8, generator=g, device=dev) < 0.5).float()
+    tensors = [base, base[:1], base[:3], base[:5], base[1:100003], base[3:], special,
+               torch.zeros(777, device=dev), torch.empty(0, device=dev),
+               nhwc.permute(0, 1, 4, 2, 3)[1], (torch.rand(4, 2, 33, 65, generator=g, device=dev) - 0.5)]
+    names = [str(i) for i in range(len(tensors))]
+    got = activity_log(names, tensors)
+    for n, t in zip(names, tensors):
+        want = t.cpu().ne(0).float().mean().item()
+        if t.numel() == 0:
+            assert np.isnan(got[n]) and np.isnan(want)
+        else:
+            assert got[n] == want, (n, got[n], want)
+    assert got["6"] == float(np.float32(4) / np.float32(6))  # subnormals count, as on the CPU
+
+
+def test_liffirenet_log_activity_matches_torch_reduction(dev):
+    """forward(log=True) returns the reference's activity dict (names and values) for every
+    layer output, equal to `l.detach().ne(0).float().mean().item()` on the same tensors (CPU
+    reduction, the reference's platform)."""
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(2)
+    m = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8)).to(dev).train()
+    gen = torch.Generator(device=dev).manual_seed(4)
+    names = ["0:input", "1:head", "2:G1", "3:R1a", "4:R1b", "5:G2", "6:R2a", "7:R2b", "8:pred"]
+    for _ in range(3):
+        w = make_window(2, 500, 48, 64, gen, dev)
+        out = m(w["event_voxel"], w["event_cnt"], log=True)
+        act = out["activity"]
+        assert list(act) == names
+        tensors = [w["event_cnt"]] + [s[1] for s in m.states] + [out["flow"][0]]
+        for n, t in zip(names, tensors):
+            assert act[n] == t.detach().cpu().ne(0).float().mean().item(), n
+        assert 0.0 < act["0:input"] < 1.0 and act["8:pred"] > 0.0
