@@ -168,6 +168,8 @@ class FireNetEngine:
         self.flat = None
         self.flat_views = None
         self.pending = []   # per-step tensors of the open backward chain (deferred wgrad)
+        self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
+        self.seq_states = None
         self.prep_stale = True  # re-prepare weights at the next forward (set after each backward)
 
     def sequence_ok(self, cin0):
@@ -658,6 +660,8 @@ class FireNetSequence(torch.autograd.Function):
 
         for l in range(L):
             cells[l].lif.mem = states[T - 1][l][0].detach()
+        # per-step states for the caller's activity log (forward_sequence(log=True)); views only
+        eng.seq_states = [[st.detach() for st in sts] for sts in states] if eng.keep_seq_states else None
 
         ctx.eng = eng
         ctx.T = T

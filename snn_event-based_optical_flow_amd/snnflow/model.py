@@ -157,8 +157,9 @@ class _FireNetBase(BaseModel):
         """T consecutive time steps in one call (not in the reference; its training loop calls
         ``forward`` once per window, ``train_flow.py:232-279``).  Same results, states and
         ``lif.mem`` caches as T ``forward`` calls -- returns their T result dicts -- with the
-        steps' kernels issued as wavefront launches (engine.FireNetSequence).  Falls back to T
-        ``forward`` calls where those launches do not apply (hooks, ``log``, C != 8)."""
+        steps' kernels issued as wavefront launches (engine.FireNetSequence).  With ``log`` the T
+        activity dicts come from one count launch per 16 tensors and one read-back.  Falls back to
+        T ``forward`` calls where those launches do not apply (hooks, C != 8)."""
         seq = event_voxels if self.encoding == "voxel" else event_cnts
         T = len(seq)
         none = [None] * T
@@ -167,14 +168,32 @@ class _FireNetBase(BaseModel):
             return []
         xs = [self._input(v, c) for v, c in pairs]
         eng = self.engine
-        if T == 1 or log or self._hooked() or not xs[0].is_cuda or not eng.sequence_ok(xs[0].shape[1]):
+        if T == 1 or self._hooked() or not xs[0].is_cuda or not eng.sequence_ok(xs[0].shape[1]):
             outs = []
             for x in xs:  # already encoded / normalised: feed through the per-step path
                 outs.append(self._step(x, log))
             return outs
-        res = FireNetSequence.apply(eng, T, *xs, *self._states, *eng.param_list())
+        logging = isinstance(log, bool) and log and not self.exporting
+        eng.keep_seq_states = logging
+        try:
+            res = FireNetSequence.apply(eng, T, *xs, *self._states, *eng.param_list())
+        finally:
+            eng.keep_seq_states = False
         self._states = list(res[T:])
-        return [{"flow": [f], "activity": None} for f in res[:T]]
+        outs = [{"flow": [f], "activity": None} for f in res[:T]]
+        if logging:
+            names = self._activity_names()
+            sts, eng.seq_states = eng.seq_states, None
+            tensors = [[x] + [st[1] for st in sts[t]] + [res[t]] for t, x in enumerate(xs)]
+            keyed = [f"{t}/{n}" for t in range(T) for n in names]
+            act = activity_log(keyed, [u for ts in tensors for u in ts])
+            for t in range(T):
+                outs[t]["activity"] = {n: act[f"{t}/{n}"] for n in names}
+        return outs
+
+    def _activity_names(self):
+        names = ["0:input"] + [f"{i + 1}:{n}" for i, (n, _) in enumerate(self.layer_spec)]
+        return names + [f"{len(self.layer_spec) + 1}:pred"]
 
     def forward(self, event_voxel=None, event_cnt=None, log=False, return_dict=True):
         out = self._step(self._input(event_voxel, event_cnt), log)
@@ -195,9 +214,7 @@ class _FireNetBase(BaseModel):
             outs = [st[1] for st in new_states]
         activity = None
         if isinstance(log, bool) and log and not self.exporting:
-            names = ["0:input"] + [f"{i + 1}:{n}" for i, (n, _) in enumerate(self.layer_spec)]
-            names.append(f"{len(self.layer_spec) + 1}:pred")
-            activity = activity_log(names, [x] + outs + [flow])
+            activity = activity_log(self._activity_names(), [x] + outs + [flow])
         return {"flow": [flow], "activity": activity}
 
 

@@ -957,3 +957,32 @@ def test_liffirenet_log_activity_matches_torch_reduction(dev):
         for n, t in zip(names, tensors):
             assert act[n] == t.detach().cpu().ne(0).float().mean().item(), n
         assert 0.0 < act["0:input"] < 1.0 and act["8:pred"] > 0.0
+
+
+def test_forward_sequence_log_activity(dev):
+    """forward_sequence(log=True) keeps the wavefront launches and returns every step's activity
+    dict: the last step equal to the CPU reduction of its returned tensors, every step within a
+    few spike flips (1e-4) of T per-step forward(log=True) calls on a copy of the model."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(6)
+    ma = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    gen = torch.Generator(device=dev).manual_seed(9)
+    wins = [make_window(2, 400, 48, 64, gen, dev) for _ in range(4)]
+    with torch.no_grad():
+        seq = mb.forward_sequence(None, [w["event_cnt"] for w in wins], log=True)
+        per = [ma(None, w["event_cnt"], log=True) for w in wins]
+    assert mb.engine.seq_states is None and not mb.engine.keep_seq_states
+    names = list(per[0]["activity"])
+    last = [wins[-1]["event_cnt"]] + [s[1] for s in mb.states] + [seq[-1]["flow"][0]]
+    for n, t in zip(names, last):
+        assert seq[-1]["activity"][n] == t.detach().cpu().ne(0).float().mean().item(), n
+    for a, b in zip(per, seq):
+        assert list(b["activity"]) == names
+        for n in names:
+            assert abs(a["activity"][n] - b["activity"][n]) <= 1e-4, n
