@@ -150,3 +150,41 @@ def test_slot_and_fragment_entry_points_validate_without_gpu():
     assert lib.snnflow_frag_halfs(16, 16) == 5 * 1 * 3 * 512
     assert lib.snnflow_frag_halfs(32, 32) == 9 * 2 * 3 * 512
     assert lib.snnflow_frag_halfs(32, 2) == 0 and lib.snnflow_frag_halfs(12, 12) == 0
+
+
+_EXPORT_OP_PROBE = r"""
+import os, sys, torch
+sys.path.insert(0, os.path.join({repo!r}, "snn_event-based_optical_flow_amd"))
+so = os.path.join({repo!r}, "oracle", "_ref", "lif_op.so")
+if {ref_first} and os.path.exists(so):
+    torch.ops.load_library(so)
+from snnflow.export_op import register_lif_op
+op = register_lif_op()
+assert register_lif_op() is op
+assert torch._C._dispatch_has_kernel_for_dispatch_key("SNN_implementation::LIF", "CUDA")
+x = torch.empty(2, 3, 4, 5, device="meta")
+s, m = op(x, x, torch.empty(3, device="meta"), torch.empty(3, device="meta"))
+assert s.shape == x.shape and m.shape == x.shape and s.device.type == "meta"
+xc = torch.ones(1, 2, 2, 2)
+try:
+    s, m = op(xc, torch.zeros_like(xc), torch.ones(2), torch.ones(2))
+    print("cpu", int(s.sum().item()))
+except NotImplementedError:
+    print("cpu refused")
+"""
+
+
+@pytest.mark.parametrize("ref_first", [False, True])
+def test_export_op_registration(ref_first):
+    """snnflow.export_op registers the HIP kernel of torch.ops.SNN_implementation.LIF (the
+    reference's op, ONNX_LIF_operator/src/lif_op.cpp:70-82): schema + Meta when the reference
+    library is absent (host tensors refused: no CPU fallback), only the HIP kernel beside the
+    reference's CPU/Meta kernels when its library was loaded first.  Fresh interpreter each:
+    an op registry is per process."""
+    import sys
+
+    code = _EXPORT_OP_PROBE.format(repo=REPO, ref_first=ref_first)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    ref_loaded = ref_first and os.path.exists(os.path.join(REPO, "oracle", "_ref", "lif_op.so"))
+    assert out.stdout.strip().splitlines()[-1] == ("cpu 8" if ref_loaded else "cpu refused")

@@ -986,3 +986,27 @@ def test_forward_sequence_log_activity(dev):
         assert list(b["activity"]) == names
         for n in names:
             assert abs(a["activity"][n] - b["activity"][n]) <= 1e-4, n
+
+
+def test_export_op_dispatches_to_hip(golden, dev):
+    """torch.ops.SNN_implementation.LIF on device tensors runs snnflow_lif_export (registered by
+    snnflow.export_op): bit-exact against the reference op's fixture; beside the reference's CPU
+    kernel when its library is loaded (test_lif_export_op_vs_reference_op loads it first)."""
+    from snnflow.export_op import register_lif_op
+
+    op = register_lif_op()
+    g = golden("lif_export_case.npz")
+    args = [torch.from_numpy(g[k]) for k in ("x", "mem", "beta", "threshold")]
+    spk, mo = op(*(a.to(dev) for a in args))
+    assert spk.device.type == "cuda"
+    np.testing.assert_array_equal(spk.cpu().numpy(), g["spk"])
+    np.testing.assert_array_equal(mo.cpu().numpy(), g["mem_out"])
+    gen = torch.Generator().manual_seed(11)
+    x, m = torch.randn(3, 8, 20, 24, generator=gen), torch.randn(3, 8, 20, 24, generator=gen)
+    b, th = torch.rand(8, 1, 1, generator=gen), torch.rand(8, 1, 1, generator=gen)  # [C,1,1] as the cells hold them
+    s2, m2 = op(x.to(dev), m.to(dev), b.to(dev), th.to(dev))
+    if torch._C._dispatch_has_kernel_for_dispatch_key("SNN_implementation::LIF", "CPU"):
+        rs, rm = op(x, m, b, th)
+        assert torch.equal(rs, s2.cpu()) and torch.equal(rm, m2.cpu())
+    with pytest.raises(RuntimeError):
+        op(x.to(dev), m[:, :4].to(dev), b.to(dev), th.to(dev))
