@@ -188,3 +188,17 @@ def test_export_op_registration(ref_first):
     assert out.returncode == 0, out.stderr[-2000:]
     ref_loaded = ref_first and os.path.exists(os.path.join(REPO, "oracle", "_ref", "lif_op.so"))
     assert out.stdout.strip().splitlines()[-1] == ("cpu 8" if ref_loaded else "cpu refused")
+
+
+def test_activity_dense_regions():
+    """The activity log hands a tensor to snnflow_count_nonzero as one memory span only when
+    its elements fill that span in some dimension order (else it is made contiguous first)."""
+    import torch
+
+    from snnflow.model import _dense
+
+    x = torch.zeros(2, 3, 5, 4)
+    assert _dense(x) and _dense(x.permute(0, 2, 3, 1)) and _dense(x[1]) and _dense(torch.zeros(0))
+    st = torch.zeros(2, 4, 6, 7, 8).permute(0, 1, 4, 2, 3)  # [2,B,C,H,W] state over NHWC memory
+    assert _dense(st) and _dense(st[1])
+    assert not _dense(x[:, :2]) and not _dense(x[..., ::2]) and not _dense(x.expand(2, 3, 5, 4)[:, :, :1].expand(2, 3, 5, 4))
