@@ -705,8 +705,10 @@ def test_event_warping_bands_and_empty_windows_vs_oracle(dev, H, W, Ns):
 # ---------------------------------------------------------------------------
 # Wavefront sequence path (forward_sequence) against the per-step path
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("H,W,T", [(64, 64, 5), (40, 72, 3)])
-def test_forward_sequence_matches_per_step(dev, H, W, T):
+@pytest.mark.parametrize("H,W,T,name", [(64, 64, 5, "LIFFireNet"), (40, 72, 3, "LIFFireNet"),
+                                         (64, 64, 5, "LIFFireNet_short"), (48, 64, 4, "LIFFireFlowNet"),
+                                         (40, 56, 3, "LIFFireFlowNet_short")])
+def test_forward_sequence_matches_per_step(dev, H, W, T, name):
     """T steps through model.forward_sequence (wavefront launches, FireNetSequence) against T
     model.forward calls (FireNetStep) of an identical copy: flows, loss, every parameter
     gradient, final states, lif.mem caches and BatchNorm running statistics, over two
@@ -721,7 +723,7 @@ def test_forward_sequence_matches_per_step(dev, H, W, T):
 
     torch.manual_seed(5)
     kw = lif_ref.make_unet_kwargs(base_num_channels=8)
-    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    ma = getattr(snnflow, name)(dict(kw)).to(dev).train()
     mb = copy.deepcopy(ma)
     cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
            "model": {"mask_output": True}}
