@@ -709,6 +709,23 @@ def test_event_warping_bands_and_empty_windows_vs_oracle(dev, H, W, Ns):
                                          (64, 64, 5, "LIFFireNet_short"), (48, 64, 4, "LIFFireFlowNet"),
                                          (40, 56, 3, "LIFFireFlowNet_short")])
 def test_forward_sequence_matches_per_step(dev, H, W, T, name):
+    _check_sequence_vs_per_step(dev, H, W, T, name, B=2, N=300, iters=2)
+
+
+@pytest.mark.parametrize("H,B", [(128, 8), (256, 4)])
+def test_forward_sequence_matches_per_step_full_size(dev, H, B):
+    """BASELINE cfg2 (128x128, B=8) and cfg3 (256x256, B=4) at full size, T=10 windows of 1000
+    events, C=8: the bench's wavefront train step against the reference loop's per-step calls
+    (size-independent property: two launch orders of the same arithmetic agree near-exactly),
+    plus spikes exactly 0/1 and every gradient finite."""
+    mb = _check_sequence_vs_per_step(dev, H, H, 10, "LIFFireNet", B=B, N=1000, iters=1)
+    for st in mb.states:
+        s = st[1].detach()
+        assert torch.equal(s, (s > 0.5).float())
+    assert all(torch.isfinite(p.grad).all() for p in mb.parameters())
+
+
+def _check_sequence_vs_per_step(dev, H, W, T, name, B, N, iters):
     """T steps through model.forward_sequence (wavefront launches, FireNetSequence) against T
     model.forward calls (FireNetStep) of an identical copy: flows, loss, every parameter
     gradient, final states, lif.mem caches and BatchNorm running statistics, over two
@@ -729,8 +746,8 @@ def test_forward_sequence_matches_per_step(dev, H, W, T, name):
            "model": {"mask_output": True}}
     ea, eb = snnflow.EventWarping(cfg, dev), snnflow.EventWarping(cfg, dev)
     gen = torch.Generator(device=dev).manual_seed(13)
-    for it in range(2):
-        wins = [make_window(2, 300, H, W, gen, dev) for _ in range(T)]
+    for it in range(iters):
+        wins = [make_window(B, N, H, W, gen, dev) for _ in range(T)]
         fa = [ma(w["event_voxel"], w["event_cnt"])["flow"][0] for w in wins]
         outs = mb.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
         assert len(outs) == T
@@ -758,6 +775,7 @@ def test_forward_sequence_matches_per_step(dev, H, W, T, name):
         mb.detach_states()
         ea.reset()
         eb.reset()
+    return mb
 
 
 def test_forward_sequence_input_and_state_grads(dev):
