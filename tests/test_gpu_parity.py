@@ -1030,3 +1030,29 @@ def test_export_op_dispatches_to_hip(golden, dev):
         assert torch.equal(rs, s2.cpu()) and torch.equal(rm, m2.cpu())
     with pytest.raises(RuntimeError):
         op(x.to(dev), m[:, :4].to(dev), b.to(dev), th.to(dev))
+
+
+def test_log_activity_with_forward_hooks(dev):
+    """With a forward hook on a cell (analyze_voltage_dynamics.py:80-96 style) the cells run one by
+    one; the activity log of that path equals the fused path's on an identical copy."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(3)
+    ma = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8)).to(dev).eval()
+    mb = copy.deepcopy(ma)
+    seen = []
+    mb.G1.register_forward_hook(lambda m, i, o: seen.append(o[0].detach().ne(0).float().mean().item()))
+    gen = torch.Generator(device=dev).manual_seed(12)
+    with torch.no_grad():
+        for _ in range(2):
+            w = make_window(2, 500, 40, 48, gen, dev)
+            a = ma(None, w["event_cnt"], log=True)["activity"]
+            b = mb(None, w["event_cnt"], log=True)["activity"]
+            assert list(a) == list(b)
+            for n in a:
+                assert abs(a[n] - b[n]) <= 1e-4, n
+    assert len(seen) == 2
