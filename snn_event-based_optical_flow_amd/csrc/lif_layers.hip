@@ -29,6 +29,12 @@
 #ifndef SNNFLOW_SP32
 #define SNNFLOW_SP32 2  // threads per pixel of the C = 32 conv-layer kernels
 #endif
+#ifndef SNNFLOW_LATE_D_REC8
+#define SNNFLOW_LATE_D_REC8 1  // C = 8 recurrent backward: LIF-backward inputs after the convs (no spill at 80 VGPRs)
+#endif
+#ifndef SNNFLOW_EARLY_G_REC8
+#define SNNFLOW_EARLY_G_REC8 1  // C = 8 recurrent backward: BN-sum replicas ahead of the halo loads
+#endif
 #ifndef SNNFLOW_L32_WAVES
 #define SNNFLOW_L32_WAVES 4  // min waves per SIMD of the C = 32 LIF-fed backward kernels
 #endif
@@ -803,7 +809,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     // 1. every global load of the kernel, issued up front (register prefetch; weights for LDS);
     //    the BN-sum replicas first, so that their reduction overlaps the halo loads
     //    (C <= 16; at C = 32 the 12 extra live registers spill: gathered in place there)
-    constexpr bool EARLY_G = C <= 16;
+    constexpr bool EARLY_G = C <= 16 && !(REC && C == 8 && !SNNFLOW_EARLY_G_REC8);
     AccGather<SNNFLOW_BWD_ACC(C)> gat;
     if constexpr (EARLY_G) acc_gather_load<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), gat);
     // per-channel parameters, also ahead of the halo loads
@@ -848,7 +854,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     }
     // layer l-1's inputs of the LIF backward at this thread's pixel; C = 32 loads them only after
     // the input-gradient convs (48 registers fewer across the matrix-core loop)
-    constexpr bool LATE_D = C >= 32;
+    constexpr bool LATE_D = C >= 32 || (REC && C == 8 && SNNFLOW_LATE_D_REC8);
     auto load_prev = [&]() {
         if constexpr (LIF_IN) {
             constexpr int Q4 = CIN / 4;
