@@ -32,6 +32,9 @@
 #ifndef SNNFLOW_LATE_D_REC8
 #define SNNFLOW_LATE_D_REC8 1  // C = 8 recurrent backward: LIF-backward inputs after the convs (no spill at 80 VGPRs)
 #endif
+#ifndef SNNFLOW_LATE_D_FF8
+#define SNNFLOW_LATE_D_FF8 1  // C = 8 feed-forward LIF-fed backward: the same (A/B: 1.57-1.585 vs 1.593-1.595 ms)
+#endif
 #ifndef SNNFLOW_EARLY_G_REC8
 #define SNNFLOW_EARLY_G_REC8 1  // C = 8 recurrent backward: BN-sum replicas ahead of the halo loads
 #endif
@@ -854,7 +857,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     }
     // layer l-1's inputs of the LIF backward at this thread's pixel; C = 32 loads them only after
     // the input-gradient convs (48 registers fewer across the matrix-core loop)
-    constexpr bool LATE_D = C >= 32 || (REC && C == 8 && SNNFLOW_LATE_D_REC8);
+    constexpr bool LATE_D = C >= 32 || (C == 8 && (REC ? SNNFLOW_LATE_D_REC8 : SNNFLOW_LATE_D_FF8));
     auto load_prev = [&]() {
         if constexpr (LIF_IN) {
             constexpr int Q4 = CIN / 4;
