@@ -361,7 +361,7 @@ def _pmc_traffic(kernel, args):
 def cpu_baseline(args, windows):
     """The CPU oracle (pure-PyTorch restatement of the reference path, same op sequence)
     timed on this host: one full train step of the same workload after one warm-up
-    step (bounded sample: 2 train steps)."""
+    step, then whole train steps until ~10 s of CPU work (bounded sample, >= 1 step)."""
     from oracle import iwe_ref, lif_ref
 
     threads = len(os.sched_getaffinity(0))
