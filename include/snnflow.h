@@ -371,6 +371,14 @@ int snnflow_iwe_corners(const float* events, const float* flow_ev, int B, int M,
 /* utils/iwe.py:74-93 interpolate: img[b][idx] += w * pol (img zeroed by the call). */
 int snnflow_iwe_interpolate(const int32_t* idx, const float* w, const float* pol, int64_t pol_sb,
                             int B, int K, int H, int W, float* img, void* stream);
+/* Autograd of the two above (the reference's weights carry gradient, utils/iwe.py:59, 65, 91):
+ * corners_bwd: g_w [B][4*M] (corner-major, bilinear only) -> g_flow_ev [B][M][2] (y, x), overwritten;
+ * interpolate_bwd: g_img [B][H*W] -> g_w [B][K] = g_img[b][idx] * pol, overwritten. */
+int snnflow_iwe_corners_bwd(const float* events, const float* flow_ev, int B, int M, float tref,
+                            int H, int W, float flow_scaling, const float* g_w, float* g_flow_ev,
+                            void* stream);
+int snnflow_iwe_interpolate_bwd(const int32_t* idx, const float* pol, int64_t pol_sb, int B, int K,
+                                int H, int W, const float* g_img, float* g_w, void* stream);
 
 /* ---- evaluation path (eval_flow.py:220-282, utils/iwe.py:96-150, loss/flow.py:597-649) ----
  * deblur_events / compute_pol_iwe: per event gather the flow at its pixel ((long)(y*W + x)),

@@ -431,6 +431,45 @@ __global__ void k_iwe_interpolate(const int32_t* __restrict__ idx, const float* 
     }
 }
 
+// Backward of get_interpolation (utils/iwe.py:37-65) w.r.t. the per-event flow: the gradients
+// of the 4 corner weights [B][4][M] -> dL/dflow_ev [B][M][2] (y, x).  weights = prod(max(0,
+// 1 - |w - c|), -1) * mask, w = pos + ((tref - ts) * f) * s: the same chain as k_iwe_bwd_event.
+__global__ void k_iwe_corners_bwd(const float* __restrict__ events, const float* __restrict__ flow_ev, int B, int M,
+                                  float tref, int H, int W, float s, const float* __restrict__ g_w,
+                                  float* __restrict__ g_flow_ev) {
+    const int64_t n = (int64_t)B * M;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int b = (int)(e / M), i = (int)(e - (int64_t)b * M);
+        const float* ev = events + e * 4;
+        Corner c[4];
+        float wy, wx;
+        warp4(ev[0], ev[1], ev[2], flow_ev[e * 2], flow_ev[e * 2 + 1], tref, s, H, W, c, wy, wx);
+        float gwy = 0.0f, gwx = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float gwt = c[q].inb ? g_w[(int64_t)b * 4 * M + (int64_t)q * M + i] : 0.0f;
+            const float gay = gwt * c[q].ax, gax = gwt * c[q].ay;
+            gwy += -(gay * relu_tie(1.0f - fabsf(c[q].dy))) * sgnf(c[q].dy);
+            gwx += -(gax * relu_tie(1.0f - fabsf(c[q].dx))) * sgnf(c[q].dx);
+        }
+        const float dt = tref - ev[0];
+        g_flow_ev[e * 2] = (gwy * s) * dt;
+        g_flow_ev[e * 2 + 1] = (gwx * s) * dt;
+    }
+}
+
+// Backward of interpolate (utils/iwe.py:84-92): scatter_add_ backward is a gather,
+// dL/dweights[e] = dL/dimg[b, idx[e]] * polarity_mask[e].
+__global__ void k_iwe_interpolate_bwd(const int32_t* __restrict__ idx, const float* __restrict__ pol, int64_t pol_sb,
+                                      int B, int K, int HW, const float* __restrict__ g_img, float* __restrict__ g_w) {
+    const int64_t n = (int64_t)B * K;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int b = (int)(e / K), i = (int)(e - (int64_t)b * K);
+        const float g = g_img[(int64_t)b * HW + idx[e]];
+        g_w[e] = pol ? g * pol[(int64_t)b * pol_sb + i] : g;
+    }
+}
+
 int grid_for(int64_t n, int per_block, int cap) {
     int64_t g = (n + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -514,6 +553,28 @@ int snnflow_iwe_interpolate(const int32_t* idx, const float* w, const float* pol
     if (K == 0) return 0;
     hipLaunchKernelGGL(k_iwe_interpolate, dim3(grid_for((int64_t)B * K, 256, 4096)), dim3(256), 0, s, idx, w, pol,
                        pol_sb, B, K, H * W, img);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_iwe_corners_bwd(const float* events, const float* flow_ev, int B, int M, float tref, int H, int W,
+                            float flow_scaling, const float* g_w, float* g_flow_ev, void* stream) {
+    if (!events || !flow_ev || !g_w || !g_flow_ev || B <= 0 || M < 0 || H <= 0 || W <= 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "iwe_corners_bwd: bad args");
+    if (M == 0) return 0;
+    hipLaunchKernelGGL(k_iwe_corners_bwd, dim3(grid_for((int64_t)B * M, 256, 4096)), dim3(256), 0,
+                       (hipStream_t)stream, events, flow_ev, B, M, tref, H, W, flow_scaling, g_w, g_flow_ev);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_iwe_interpolate_bwd(const int32_t* idx, const float* pol, int64_t pol_sb, int B, int K, int H, int W,
+                                const float* g_img, float* g_w, void* stream) {
+    if (!idx || !g_img || !g_w || B <= 0 || K < 0 || H <= 0 || W <= 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "iwe_interpolate_bwd: bad args");
+    if (K == 0) return 0;
+    hipLaunchKernelGGL(k_iwe_interpolate_bwd, dim3(grid_for((int64_t)B * K, 256, 4096)), dim3(256), 0,
+                       (hipStream_t)stream, idx, pol, pol_sb, B, K, H * W, g_img, g_w);
     SNN_CHECK_LAUNCH();
     return 0;
 }

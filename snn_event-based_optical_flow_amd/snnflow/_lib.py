@@ -189,6 +189,8 @@ EXPORTS = {
     "snnflow_iwe_acc_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
     "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),
+    "snnflow_iwe_corners_bwd": (I32, [P, P, I32, I32, F32, I32, I32, F32, P, P, P]),
+    "snnflow_iwe_interpolate_bwd": (I32, [P, P, I64, I32, I32, I32, I32, P, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
     "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),

@@ -169,6 +169,7 @@ class FireNetEngine:
         self.flat_views = None
         self.pending = []   # per-step tensors of the open backward chain (deferred wgrad)
         self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
+        self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
         self.seq_states = None
         self.prep_stale = True  # re-prepare weights at the next forward (set after each backward)
 
@@ -563,10 +564,6 @@ class FireNetStep(torch.autograd.Function):
 
 
 def _ptr_t(t):
-    return None if t is None else t.data_ptr()
-
-
-def _ptr_nhwc_spk(t):
     return None if t is None else t.data_ptr()
 
 

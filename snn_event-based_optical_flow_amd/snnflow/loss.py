@@ -119,9 +119,12 @@ class EventWarping(torch.nn.Module):
 
     @property
     def event_mask(self):
+        """``loss/flow.py:170-176``: with ``overwrite_intermediate`` the stacked [B,T,H,W] masks
+        of the window, collapsed to [B,1,H,W] once ``overwrite_intermediate_flow`` ran
+        (``:151-152``); otherwise the mask of the last pass."""
         m = torch.cat(self._masks, dim=1)
         if self.overwrite_intermediate:
-            return self._overwritten_mask()
+            return self._overwritten_mask() if self._final_flow is not None else m
         return m[:, -1:, :, :]
 
     def event_flow_association(self, flow_list, event_list, pol_mask, event_mask):

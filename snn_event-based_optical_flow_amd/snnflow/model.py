@@ -174,7 +174,7 @@ class _FireNetBase(BaseModel):
                 outs.append(self._step(x, log))
             return outs
         logging = isinstance(log, bool) and log and not self.exporting
-        eng.keep_seq_states = logging
+        eng.keep_seq_states = logging or eng.capture_states
         try:
             res = FireNetSequence.apply(eng, T, *xs, *self._states, *eng.param_list())
         finally:

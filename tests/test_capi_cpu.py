@@ -202,3 +202,31 @@ def test_activity_dense_regions():
     st = torch.zeros(2, 4, 6, 7, 8).permute(0, 1, 4, 2, 3)  # [2,B,C,H,W] state over NHWC memory
     assert _dense(st) and _dense(st[1])
     assert not _dense(x[:, :2]) and not _dense(x[..., ::2]) and not _dense(x.expand(2, 3, 5, 4)[:, :, :1].expand(2, 3, 5, 4))
+
+
+def test_event_warping_event_mask_shapes():
+    """loss/flow.py:170-176: with overwrite_intermediate the property returns the stacked
+    [B,T,H,W] masks until overwrite_intermediate_flow() collapses them to [B,1,H,W]; without it,
+    the mask of the last pass.  (Bookkeeping only: no kernel runs.)"""
+    import torch
+
+    import snnflow
+
+    B, T, H, W = 2, 3, 6, 7
+    for overwrite in (False, True):
+        cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001,
+                                                          "overwrite_intermediate": overwrite},
+               "model": {"mask_output": True}}
+        ew = snnflow.EventWarping(cfg, "cpu")
+        masks = [(torch.rand(B, 1, H, W) < 0.5).float() for _ in range(T)]
+        flows = [torch.zeros(B, 2, H, W) for _ in range(T)]
+        for t in range(T):
+            ew.event_flow_association([flows[t]], torch.zeros(B, 4, 4), torch.zeros(B, 4, 2), masks[t])
+        if overwrite:
+            assert tuple(ew.event_mask.shape) == (B, T, H, W)
+            assert torch.equal(ew.event_mask, torch.cat(masks, 1))
+            ew.overwrite_intermediate_flow([flows[-1]])
+            want = torch.cat(masks, 1).sum(1, keepdim=True).clamp(max=1)
+            assert torch.equal(ew.event_mask, want)
+        else:
+            assert torch.equal(ew.event_mask, masks[-1])

@@ -14,10 +14,26 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+# Parameter-gradient bounds (relative L2) where the spikes agree; ~2x the worst case measured on
+# MI355X (printed by _grad_check; DESIGN.md section 3 lists the figures).
+GOLDEN_GRAD_TOL = 4e-6   # vs the reference-generated fixtures (fp32 CPU, oneDNN summation order);
+                         # measured worst 1.5e-6 (head.lif.threshold, C=8)
+ORACLE_GRAD_TOL = 1e-5   # vs the CPU oracle on fresh inputs; measured worst 4.4e-6 (cell C=8 recurrent, ff.weight)
+
 
 def _rel(a, b):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+
+
+def _grad_check(tag, pairs, tol):
+    """Relative-L2 error of every (name, ours, reference) gradient: printed (the measured figures
+    behind the tolerances), then asserted against tol."""
+    errs = {n: _rel(a, b) for n, a, b in pairs}
+    worst = max(errs.items(), key=lambda kv: kv[1])
+    print(f"\n[{tag}] grad rel-L2 worst {worst[0]} {worst[1]:.2e}: " + ", ".join(f"{k}={v:.1e}" for k, v in errs.items()))
+    for n, v in errs.items():
+        assert v < tol, (tag, n, v)
 
 
 def _sd(rec, prefix, dev):
@@ -168,11 +184,12 @@ def test_cell_teacher_forced(dev, recurrent, C):
     (spk * wgt.to(dev)).sum().backward()
     (rspk * wgt).sum().backward()
     if (spk.detach().cpu() == rspk.detach()).all():
-        for (n, p), (_, q) in zip(cell.named_parameters(), ref.named_parameters()):
-            assert _rel(p.grad.cpu().numpy(), q.grad.numpy()) < 1e-3, n
-        assert _rel(xd.grad.cpu().numpy(), xc.grad.numpy()) < 1e-3
+        pairs = [(n, p.grad.cpu().numpy(), q.grad.numpy())
+                 for (n, p), (_, q) in zip(cell.named_parameters(), ref.named_parameters())]
+        pairs.append(("input", xd.grad.cpu().numpy(), xc.grad.numpy()))
         if recurrent:
-            assert _rel(pd.grad.cpu().numpy(), pc.grad.numpy()) < 1e-3
+            pairs.append(("prev_state", pd.grad.cpu().numpy(), pc.grad.numpy()))
+        _grad_check(f"cell C={C} rec={recurrent}", pairs, ORACLE_GRAD_TOL)
 
 
 def _run_golden_firenet(g, name, dev, seq=False):
@@ -205,7 +222,8 @@ def _run_golden_firenet(g, name, dev, seq=False):
     np.testing.assert_allclose(loss.item(), g["loss"], rtol=1e-4)
     for n, p in model.named_parameters():
         assert p.grad is not None, n
-        assert _rel(p.grad.cpu().numpy(), g[f"g.{n}"]) < 2e-3, n
+    _grad_check(f"golden {name} C={C} seq={seq}", [(n, p.grad.cpu().numpy(), g[f"g.{n}"])
+                                                   for n, p in model.named_parameters()], GOLDEN_GRAD_TOL)
     for k, v in model.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), g[f"p1.{k}"], rtol=1e-5, atol=1e-6, err_msg=k)
 
@@ -404,8 +422,9 @@ def test_training_steps_fused_adam_vs_oracle(dev):
         loss.backward()
         rloss.backward()
         np.testing.assert_allclose(loss.item(), rloss.item(), rtol=1e-4)
-        for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
-            assert _rel(a.grad.cpu().numpy(), b.grad.numpy()) < 2e-3, (step, n)
+        _grad_check(f"fused adam step {step}", [(n, a.grad.cpu().numpy(), b.grad.numpy()) for (n, a), (_, b)
+                                                 in zip(model.named_parameters(), ref.named_parameters())],
+                    ORACLE_GRAD_TOL)
         opt.step()
         model.detach_states()
         ew.reset()
@@ -889,8 +908,8 @@ def test_engine_gradients_wide_vs_oracle(dev, C):
     rloss.backward()
     np.testing.assert_allclose(loss.item(), rloss.item(), rtol=1e-4)
     assert model.engine.prep.frag.get(1) is not None  # the fragment path ran
-    for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
-        assert _rel(a.grad.cpu().numpy(), b.grad.numpy()) < 2e-3, n
+    _grad_check(f"engine C={C}", [(n, a.grad.cpu().numpy(), b.grad.numpy()) for (n, a), (_, b)
+                                   in zip(model.named_parameters(), ref.named_parameters())], ORACLE_GRAD_TOL)
 
 
 def test_forward_sequence_chained_without_detach(dev):
