@@ -457,6 +457,141 @@ int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float
 #define SNNFLOW_MAX_COUNT_TENSORS 16
 int snnflow_count_nonzero(const float* const* ptrs, const int64_t* sizes, int n, uint64_t* counts, void* stream);
 
+/* ---- Spiking U-Net: SpikingRecEVFlowNet (models/model.py:723-858) =
+ *      SpikingMultiResUNetRecurrent (models/unet.py:414-461) of ConvLIF / ConvLIFRecurrent cells
+ *      (models/spiking_submodules.py:29-300) in SpikingRecurrentConvLayer (:303-346),
+ *      SpikingResidualBlock (:349-385) and SpikingUpsampleConvLayer (:388-417) blocks.
+ *
+ * Every convolution is an implicit GEMM on the bf16 matrix cores (v_mfma_f32_16x16x32_bf16):
+ * D[m][pixel] = sum_k A[m][k] * X[k][pixel].  The pixel operand X is a bf16 NHWC "act" tensor
+ * whose values are exact in bf16 (spikes 0/1, residual sums 0..3, their bilinear upsamples k/16,
+ * and fp32 values pre-split into hi/mid/lo bf16 channels); the weight operand is stored split
+ * into three bf16 parts (hi, mid, lo), so every product is the exact fp32 product and the
+ * accumulation is fp32.  Act tensors: [B][H][W][cpitch] bf16 (uint16_t here), cpitch % 32 == 0,
+ * padding channels zero.  "k positions" = the act's channels; a kmap (int [cpitch]) names the
+ * reference input channel of each position (-1: padding), so one weight tensor of the reference
+ * feeds several positions (hi/mid/lo splits of an fp32 channel). */
+#define SNNFLOW_UNET_MAX_SEGS 4
+#define SNNFLOW_UNET_MODE_S1 0   /* stride-1 conv, pad ksize/2 */
+#define SNNFLOW_UNET_MODE_S2 1   /* stride-2 conv, pad ksize/2 */
+#define SNNFLOW_UNET_MODE_T2 2   /* transposed stride-2 conv (input gradient of a MODE_S2 conv) */
+#define SNNFLOW_UNET_EPI_STORE 0 /* out[pix*ld + m] = (or +=) D */
+#define SNNFLOW_UNET_EPI_LIF 1   /* ConvLIF membrane / spike / state epilogue (spiking_submodules.py:121-151, 265-300) */
+#define SNNFLOW_SG_ARCTAN 0      /* spiking_util.py:82-93, 108-109 */
+#define SNNFLOW_SG_SUPERSPIKE 1  /* :28-43, 96-97 */
+#define SNNFLOW_SG_MGSPIKE 2     /* :46-65, 100-101 */
+#define SNNFLOW_SG_TRIANGLE 3    /* :68-79, 104-105 */
+
+typedef struct {
+    const uint16_t* x;  /* act tensor bf16 [B][H][W][cpitch] */
+    int H, W, cpitch;
+    int mode;           /* SNNFLOW_UNET_MODE_* */
+    int kc0;            /* first 32-channel weight chunk of this segment within a tap */
+    int nparts;         /* weight parts multiplied with it: 3 (exact operand); 2, 1 for the mid / lo
+                           planes of a split operand (drops products below 2^-24 relative) */
+} snnflow_unet_seg;
+
+typedef struct {
+    int B, Ho, Wo;      /* output pixels: GEMM N = B*Ho*Wo */
+    int M;              /* valid output channels (GEMM M) */
+    int ksize;          /* odd conv kernel size (3) */
+    int nseg;
+    snnflow_unet_seg seg[SNNFLOW_UNET_MAX_SEGS];
+    const uint16_t* w;  /* bf16 [3][ksize^2][kct][mpad][32] (snnflow_unet_prep_weights) */
+    int kct, mpad;
+    int epi;            /* SNNFLOW_UNET_EPI_* */
+    /* EPI_STORE */
+    float* out; int ld; int accumulate;
+    /* EPI_LIF (ConvLIF cell; M = hidden channels, output resolution = cell resolution) */
+    const float* leak; const float* thresh; int hard_reset;
+    const float* prev_state;   /* fp32 [2][B][Ho][Wo][M] (v, z) or NULL (zeros) */
+    const uint16_t* residual;  /* act [pix][res_pitch] added to the spikes, or NULL */
+    int res_pitch;
+    float* state;              /* fp32 [2][B][Ho][Wo][M] out (v_out, z_out) */
+    float* current;            /* fp32 [pix][M] out: ff (+ rec), for the backward */
+    uint16_t* act;             /* act [pix][act_pitch] out: z_out (+ residual) */
+    int act_pitch;
+} snnflow_unet_conv_args;
+
+/* Convolution (forward of a cell with the LIF epilogue, or an input gradient with EPI_STORE). */
+int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream);
+
+/* Weight operand of snnflow_unet_conv from a torch conv weight w [cout][cin][k][k] (fp32):
+ * forward (transpose 0): dst[p][tap][kc0 + kc][m][kk] = part p of w[m][kmap[32 kc + kk]][tap]
+ *   for kc < nkc (m < cout; kmap entry -1 or m >= cout: 0);
+ * input gradient (transpose 1): dst[p][tap'][kc][m][kk] = part p of w[32 kc + kk][kmap[m]][tap],
+ *   m < mvalid (the gradient's k positions), tap = flip ? k^2-1-tap' : tap'.  dst is not cleared:
+ *   the caller zero-fills once (padding entries are never written). */
+int snnflow_unet_prep_weights(const float* w, int cout, int cin, int ksize, const int* kmap, int transpose,
+                              int flip, int mvalid, int kc0, int nkc, int kct, int mpad, uint16_t* dst,
+                              void* stream);
+
+/* Weight gradient of one input segment, accumulated (fp32 atomics) over pixels and calls:
+ * dwk[tap][k0 + k][m] += sum_pix X[gather(pix, tap)][k] * G[pix][m], G = g3 hi + mid + lo planes
+ * ([3][B*Ho*Wo][gpitch] bf16, part stride gpart), k < seg.cpitch. */
+typedef struct {
+    int B, Ho, Wo, M, ksize;
+    const uint16_t* g3; int gpitch; int64_t gpart;
+    snnflow_unet_seg seg;
+    int k0, ktot;       /* first k position of the segment in dwk, k positions per tap in dwk */
+    float* dwk;         /* fp32 [ksize^2][ktot][M] */
+} snnflow_unet_wgrad_args;
+int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream);
+
+/* dw[m][c][tap] (+)= sum over the (up to 3) positions k of input channel c (kmap_inv [cin][3], -1:
+ * none; positions relative to k0) of dwk[tap][k0 + k][m] (torch layout [cout][cin][k][k]). */
+int snnflow_unet_wgrad_finalize(const float* dwk, int ktot, const int* kmap_inv, int k0, int nk, int cout, int cin,
+                                int ksize, int accumulate, float* dw, void* stream);
+
+/* ConvLIF backward of one cell and step, per element (spiking_submodules.py:121-151, 265-300):
+ * x = v_out - th, sg = surrogate(x, width), gxs = (g_out + g_z) * sg, gv = g_v + gxs (+ residual
+ * path), g_cur = gv * (1 - leak) written as hi/mid/lo bf16 planes (padding channels 0);
+ * g_prev v-half = gv*leak*(1-z) (hard) | gv*leak (soft); z-half = 0 (detach) or the reset term;
+ * g_res += g_out; sums of dL/dthresh and dL/dleak(before sigmoid') into acc (fp64 [2*C]). */
+typedef struct {
+    int P, C;
+    const float* leak; const float* thresh; float width; int hard_reset, detach, surrogate;
+    const float* g_out; int g_pitch;           /* fp32 [P][g_pitch] or NULL */
+    const float* g_state;                       /* fp32 [2][P][C] or NULL */
+    const float* state; const float* prev_state; const float* current;
+    uint16_t* g_cur3; int gc_pitch; int64_t gc_part;
+    float* g_prev;                              /* fp32 [2][P][C] or NULL */
+    float* g_res; int gres_pitch;               /* or NULL */
+    double* acc;                                /* [2*C] */
+} snnflow_unet_lif_bwd_args;
+int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream);
+
+/* g_thresh = (thresh >= 0.01) * acc[c], g_leak = acc[C + c] * s * (1 - s), s = sigmoid(leak). */
+int snnflow_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,
+                                  float* g_leak, float* g_thresh, void* stream);
+
+/* fp32 channels (strided, e.g. NCHW or a state half) -> act [P][cpitch] bf16 with channels
+ * [hi(C) | mid(C) | lo(C) | 0] (split 1), or [value(C) | 0] (split 0, values exact in bf16). */
+int snnflow_unet_pack(const float* src, int B, int H, int W, int C, int64_t sb, int64_t sc, int64_t sh,
+                      int64_t sw, int split, uint16_t* dst, int cpitch, void* stream);
+
+/* Decoder input (unet.py:455-458 + spiking_submodules.py:415): bilinear x2 upsample
+ * (align_corners=False) of cat(pred, x, block) at h x w into act [B][2h][2w][cpitch] with
+ * channels [x (cx) | block (cb) | pred hi0 hi1 mid0 mid1 lo0 lo1 (if pred) | 0]. */
+int snnflow_unet_dec_in(const uint16_t* x, int cx, int px, const uint16_t* block, int cb, int pb,
+                        const float* pred, int B, int h, int w, uint16_t* dst, int cpitch, void* stream);
+/* Its backward from g_up fp32 [B][2h][2w][gpitch]: g_x [pix][gx_pitch] +=, g_block +=,
+ * g_pred [B][2][h][w] = (the pred channels' gradient at its hi position). */
+int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int has_pred, int B, int h, int w,
+                            float* g_x, int gx_pitch, float* g_block, int gb_pitch, float* g_pred, void* stream);
+
+/* Prediction layer (submodules.py:96-113, 1x1 conv + bias + tanh, unet.py:351-365) and the
+ * nearest upsample to the input resolution (model.py:840-850):
+ * flow = tanh(W x + b) [B][2][h][w]; flow_full [B][2][h*s][w*s] (s = up). */
+int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, const float* b, int B, int h,
+                          int wd, int up, float* flow, float* flow_full, void* stream);
+/* g_pre = (1 - flow^2) * (sum of g_full over the s x s block + g_extra) into gpre [B][2][h][w];
+ * g_x[pix][gx_pitch] += W^T g_pre; acc (fp64 [2C + 2]) += (dW, db) sums. */
+int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, const float* flow,
+                          const float* g_full, const float* g_extra, int B, int h, int wd, int up, float* gpre,
+                          float* g_x, int gx_pitch, double* acc, void* stream);
+int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream);
+
 const char* snnflow_last_error(void);
 int snnflow_abi_version(void);
 

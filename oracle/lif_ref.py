@@ -52,6 +52,11 @@ class WidthHeaviside(torch.autograd.Function):
             sg = 1 / (1 + width * x.abs()) ** 2
         elif ctx.kind == "trianglespike":  # :77
             sg = torch.relu(1 - width * x.abs())
+        elif ctx.kind == "mgspike":  # :59-64, gaussian :6-10
+            def gauss(mu, sigma):
+                return torch.exp(-((x - mu) * (x - mu)) / (2 * sigma * sigma)) / (sigma * math.sqrt(2 * math.pi))
+
+            sg = 1.15 * gauss(0.0, width) - 0.15 * gauss(width, 6 * width) - 0.15 * gauss(-width, 6 * width)
         else:
             raise NotImplementedError(ctx.kind)
         return g.clone() * sg, None, None

@@ -1,0 +1,1001 @@
+// Spiking U-Net (SpikingRecEVFlowNet) kernels for gfx950.
+//
+// Reference semantics:
+//   models/model.py:723-858           SpikingRecEVFlowNet (input encoding, nearest upsample of the flows)
+//   models/unet.py:310-461            SpikingMultiResUNetRecurrent (encoders, residual blocks,
+//                                     decoders with concatenated skips and predictions)
+//   models/spiking_submodules.py:29-151   ConvLIF (hard/soft reset, detached reset spikes, sigmoid leak,
+//                                          clamp_min(thresh, 0.01), residual added to the spikes)
+//   models/spiking_submodules.py:154-300  ConvLIFRecurrent (ff + rec conv of the previous spikes)
+//   models/spiking_submodules.py:303-417  blocks; :415 F.interpolate(x2, bilinear, align_corners=False)
+//   models/spiking_util.py:28-109         surrogate gradients
+//   models/submodules.py:96-113           ConvLayer (prediction: 1x1 conv + bias + tanh)
+//
+// Every convolution (forward, input gradient, weight gradient) is an implicit GEMM on
+// v_mfma_f32_16x16x32_bf16.  The pixel-side operand holds values that are exact in bf16 (spikes,
+// small integer residual sums, their bilinear upsamples k/16, and fp32 tensors stored as hi/mid/lo
+// bf16 planes or channels); the weight-side operand is split into three bf16 parts; so the
+// products are exact fp32 products accumulated in fp32 (no reduced-precision arithmetic).
+#include <cmath>
+
+#include "snnflow_dev.h"
+
+int snnflow_set_error(int code, const char* msg);
+#define SNN_FAIL(code, msg) return snnflow_set_error((code), (msg))
+#define SNN_CHECK_LAUNCH()                                                        \
+    do {                                                                          \
+        hipError_t e_ = hipGetLastError();                                        \
+        if (e_ != hipSuccess) return snnflow_set_error((int)e_, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float fx4 __attribute__((ext_vector_type(4)));
+
+constexpr int UNT = 256;     // threads per block (4 waves)
+constexpr int XP = 40;       // bf16 per LDS row: 32 k + 8 padding (80-B rows)
+
+__device__ inline uint4 ld16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ inline float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ inline uint16_t f2bf(float f) {
+    const __bf16 b = (__bf16)f;
+    return *reinterpret_cast<const uint16_t*>(&b);
+}
+
+// hi / mid / lo bf16 parts of an fp32 value (round to nearest each; exact sum for fp32 inputs)
+__device__ inline void split3(float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const __bf16 a = (__bf16)x;
+    const float r1 = x - (float)a;
+    const __bf16 b = (__bf16)r1;
+    const __bf16 c = (__bf16)(r1 - (float)b);
+    h = *reinterpret_cast<const uint16_t*>(&a);
+    m = *reinterpret_cast<const uint16_t*>(&b);
+    l = *reinterpret_cast<const uint16_t*>(&c);
+}
+
+// 16-bit element j of a 16-byte vector (constant j after unrolling)
+__device__ inline uint16_t h16(const uint4& v, int j) {
+    const uint32_t w = j < 2 ? v.x : (j < 4 ? v.y : (j < 6 ? v.z : v.w));
+    return (uint16_t)((j & 1) ? (w >> 16) : (w & 0xffff));
+}
+
+// bijective XCD-aware remap (guide §5.5 T1): logical tiles t, t+1, ... land on one XCD
+__device__ inline int xcd_remap(int bid, int nblk) {
+    const int xcd = bid % 8, q = nblk / 8, r = nblk % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Implicit-GEMM convolution: D[m][pix] = sum over (segment, tap, channel) of W[m][k] X[pix,tap][k]
+// Block tile BM (m) x BN (pixels); 4 waves as WAVES_M x WAVES_N, each 16*WMT m x 64 pixels.
+// One k-step = (segment, tap, 32-channel chunk): the X chunk (BN x 32 bf16, gathered with the
+// tap offset / stride / transposed stride) and the W chunk (nparts x BM x 32 bf16) are staged
+// through LDS; the next step's global loads are issued before this step's MFMAs.
+// ---------------------------------------------------------------------------------------------
+template <int WMT, int WAVES_M>
+struct ConvGeo {
+    static constexpr int WAVES_N = 4 / WAVES_M;
+    static constexpr int BM = 16 * WMT * WAVES_M;
+    static constexpr int BN = 64 * WAVES_N;
+    static constexpr int XR = BN / 64;              // 16-B X pieces per thread and step
+    static constexpr int WPIECES = 3 * BM * 4;      // 16-B W pieces per step (all parts)
+    static constexpr int WR = (WPIECES + UNT - 1) / UNT;
+};
+
+template <int WMT, int WAVES_M>
+__global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
+    using G = ConvGeo<WMT, WAVES_M>;
+    constexpr int BM = G::BM, BN = G::BN;
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[BN * XP];
+    __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * BM * XP];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+    const int P = a.B * a.Ho * a.Wo;
+    const int mtiles = (a.M + BM - 1) / BM, ntiles = (P + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
+    const int m0 = (t % mtiles) * BM, n0 = (t / mtiles) * BN;
+    const int ks = a.ksize, taps = ks * ks, pad = ks / 2;
+    const int64_t wpart = (int64_t)taps * a.kct * a.mpad * 32;
+
+    // this thread's X pieces: pixel (tid >> 2) + 64 r of the tile, 16-B piece q = tid & 3
+    const int q = tid & 3;
+    int pb[G::XR], py[G::XR], px[G::XR];
+    bool pv[G::XR];
+#pragma unroll
+    for (int r = 0; r < G::XR; ++r) {
+        const int n = n0 + (tid >> 2) + 64 * r;
+        pv[r] = n < P;
+        const int nn = pv[r] ? n : 0;
+        px[r] = nn % a.Wo;
+        const int rest = nn / a.Wo;
+        py[r] = rest % a.Ho;
+        pb[r] = rest / a.Ho;
+    }
+
+    uint4 xr[G::XR], wr[G::WR];
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+    // global loads of one k-step (segment sg, tap, chunk kc) into registers
+    auto load = [&](const snnflow_unet_seg& sg, int tap, int kc) {
+        const int ky = tap / ks, kx = tap - ky * ks;
+        const int mode = sg.mode, H = sg.H, W = sg.W, cp = sg.cpitch;
+#pragma unroll
+        for (int r = 0; r < G::XR; ++r) {
+            int iy, ix;
+            bool ok = pv[r];
+            if (mode == SNNFLOW_UNET_MODE_S1) {
+                iy = py[r] + ky - pad;
+                ix = px[r] + kx - pad;
+            } else if (mode == SNNFLOW_UNET_MODE_S2) {
+                iy = 2 * py[r] + ky - pad;
+                ix = 2 * px[r] + kx - pad;
+            } else {  // transposed stride 2: output pixel p receives input o with 2o + k - pad = p
+                const int ty = py[r] + pad - ky, tx = px[r] + pad - kx;
+                ok = ok && ty >= 0 && tx >= 0 && ((ty | tx) & 1) == 0;
+                iy = ty >> 1;
+                ix = tx >> 1;
+            }
+            ok = ok && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const int64_t off = ok ? (((int64_t)pb[r] * H + iy) * W + ix) * cp + kc * 32 + q * 8 : 0;
+            xr[r] = ld16(sg.x + off);
+            if (!ok) xr[r] = z4;
+        }
+        const int np = sg.nparts;
+        const int64_t wbase = ((int64_t)(tap * a.kct + sg.kc0 + kc) * a.mpad + m0) * 32;
+#pragma unroll
+        for (int r = 0; r < G::WR; ++r) {
+            const int e = tid + r * UNT;
+            const int part = e / (BM * 4), rem = e - part * (BM * 4);
+            const bool ok = e < G::WPIECES && part < np;
+            wr[r] = ld16(a.w + (ok ? part * wpart + wbase + (rem >> 2) * 32 + (rem & 3) * 8 : 0));
+            if (!ok) wr[r] = z4;
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int r = 0; r < G::XR; ++r)
+            *reinterpret_cast<uint4*>(&Xs[((tid >> 2) + 64 * r) * XP + q * 8]) = xr[r];
+#pragma unroll
+        for (int r = 0; r < G::WR; ++r) {
+            const int e = tid + r * UNT;
+            if (e < G::WPIECES) {
+                const int part = e / (BM * 4), rem = e - part * (BM * 4);
+                *reinterpret_cast<uint4*>(&Ws[(part * BM + (rem >> 2)) * XP + (rem & 3) * 8]) = wr[r];
+            }
+        }
+    };
+
+    fx4 acc[WMT][4];
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
+
+    // k-steps: segments (unrolled: constant kernarg indices), taps, 32-channel chunks; each step's
+    // successor is loaded before the step's MFMAs
+    load(a.seg[0], 0, 0);
+#pragma unroll
+    for (int s = 0; s < SNNFLOW_UNET_MAX_SEGS; ++s) {
+        if (s >= a.nseg) break;
+        const snnflow_unet_seg sg = a.seg[s];
+        const int nkc = sg.cpitch >> 5, nit = taps * nkc, np = sg.nparts;
+        for (int it = 0; it < nit; ++it) {
+            __syncthreads();  // the previous step's fragment reads are done
+            store();
+            __syncthreads();
+            if (it + 1 < nit) {
+                const int t2 = (it + 1) / nkc;
+                load(sg, t2, it + 1 - t2 * nkc);
+            } else if (s + 1 < SNNFLOW_UNET_MAX_SEGS && s + 1 < a.nseg) {
+                load(a.seg[s + 1 < SNNFLOW_UNET_MAX_SEGS ? s + 1 : s], 0, 0);
+            }
+            bf16x8 bx[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[(wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+#pragma unroll
+            for (int i = 0; i < WMT; ++i) {
+                const int row = wm * 16 * WMT + i * 16 + (lane & 15);
+                for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
+                    const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of pixel n
+    const int64_t plane = (int64_t)P * a.M;
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
+            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+            if (n >= P || m >= a.M) continue;
+            const fx4 v = acc[i][j];
+            if (a.epi == SNNFLOW_UNET_EPI_STORE) {
+                float* o = a.out + (int64_t)n * a.ld + m;
+                if (m + 3 < a.M) {
+                    float4 val = make_float4(v[0], v[1], v[2], v[3]);
+                    if (a.accumulate) {
+                        const float4 old = *reinterpret_cast<const float4*>(o);
+                        val = make_float4(old.x + val.x, old.y + val.y, old.z + val.z, old.w + val.w);
+                    }
+                    *reinterpret_cast<float4*>(o) = val;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (m + r < a.M) o[r] = a.accumulate ? o[r] + v[r] : v[r];
+                }
+                continue;
+            }
+            // ConvLIF (spiking_submodules.py:121-151 / 265-300), M = hidden channels (multiple of 4)
+            const int64_t e0 = (int64_t)n * a.M + m;
+            float vp[4] = {0.f, 0.f, 0.f, 0.f}, zp[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
+            if (a.prev_state) {
+                const float4 tv = *reinterpret_cast<const float4*>(a.prev_state + e0);
+                const float4 tz = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
+                vp[0] = tv.x; vp[1] = tv.y; vp[2] = tv.z; vp[3] = tv.w;
+                zp[0] = tz.x; zp[1] = tz.y; zp[2] = tz.z; zp[3] = tz.w;
+            }
+            if (a.residual) {
+                const uint2 rr = *reinterpret_cast<const uint2*>(a.residual + (int64_t)n * a.res_pitch + m);
+                rs[0] = bf2f(rr.x & 0xffff); rs[1] = bf2f(rr.x >> 16); rs[2] = bf2f(rr.y & 0xffff); rs[3] = bf2f(rr.y >> 16);
+            }
+            float vo[4], zo[4];
+            uint16_t ob[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float lam = 1.0f / (1.0f + expf(-a.leak[m + r]));
+                const float th0 = a.thresh[m + r], th = th0 < 0.01f ? 0.01f : th0;
+                vo[r] = a.hard_reset ? ((vp[r] * lam) * (1.0f - zp[r])) + ((1.0f - lam) * v[r])
+                                     : ((vp[r] * lam) + ((1.0f - lam) * v[r])) - (zp[r] * th);
+                zo[r] = (vo[r] - th > 0.0f) ? 1.0f : 0.0f;
+                ob[r] = f2bf(a.residual ? zo[r] + rs[r] : zo[r]);
+            }
+            *reinterpret_cast<float4*>(a.state + e0) = make_float4(vo[0], vo[1], vo[2], vo[3]);
+            *reinterpret_cast<float4*>(a.state + plane + e0) = make_float4(zo[0], zo[1], zo[2], zo[3]);
+            *reinterpret_cast<float4*>(a.current + e0) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<uint2*>(a.act + (int64_t)n * a.act_pitch + m) =
+                make_uint2((uint32_t)ob[0] | ((uint32_t)ob[1] << 16), (uint32_t)ob[2] | ((uint32_t)ob[3] << 16));
+        }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight gradient: D[k][m] = sum_pix X[gather(pix, tap)][k] * G[pix][m] with the pixel sum as the
+// GEMM K dimension (32 pixels per step): both operands are transposed into LDS ([k][pixel],
+// [m][pixel]); block tile 64 k x 64 m, 4 waves of 32 x 32; partial sums of a pixel range added to
+// dwk with fp32 atomics.
+// ---------------------------------------------------------------------------------------------
+constexpr int WG_BK = 64, WG_BM = 64;
+
+__global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, int ktiles, int mtiles, int nsplit,
+                                                    int steps) {
+    __shared__ __attribute__((aligned(16))) __bf16 Xt[WG_BK * XP];
+    __shared__ __attribute__((aligned(16))) __bf16 Gt[3 * WG_BM * XP];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wk = wave & 1, wmv = wave >> 1;
+    int b = blockIdx.x;
+    const int split = b % nsplit;
+    b /= nsplit;
+    const int mt = b % mtiles;
+    b /= mtiles;
+    const int kt = b % ktiles;
+    const int tap = b / ktiles;
+    const int ks = a.ksize, pad = ks / 2, ky = tap / ks, kx = tap - ky * ks;
+    const int P = a.B * a.Ho * a.Wo;
+    const snnflow_unet_seg& sg = a.seg;
+    const int pl = tid >> 3, pq = tid & 7;  // this thread's pixel (of 32) and 8-channel piece
+    const int kk = kt * WG_BK + pq * 8, mm = mt * WG_BM + pq * 8;
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+
+    fx4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 xr, gr[3];
+    auto load = [&](int st) {
+        const int n = (split * steps + st) * 32 + pl;
+        bool ok = n < P;
+        const int nn = ok ? n : 0;
+        const int ox = nn % a.Wo, rest = nn / a.Wo, oy = rest % a.Ho, bb = rest / a.Ho;
+        int iy, ix;
+        if (sg.mode == SNNFLOW_UNET_MODE_S1) {
+            iy = oy + ky - pad;
+            ix = ox + kx - pad;
+        } else {
+            iy = 2 * oy + ky - pad;
+            ix = 2 * ox + kx - pad;
+        }
+        const bool okx = ok && kk < sg.cpitch && iy >= 0 && iy < sg.H && ix >= 0 && ix < sg.W;
+        xr = ld16(sg.x + (okx ? (((int64_t)bb * sg.H + iy) * sg.W + ix) * sg.cpitch + kk : 0));
+        if (!okx) xr = z4;
+        const bool okg = ok && mm < a.gpitch;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            gr[p] = ld16(a.g3 + (okg ? p * a.gpart + (int64_t)nn * a.gpitch + mm : 0));
+            if (!okg) gr[p] = z4;
+        }
+    };
+    auto store = [&]() {
+        uint16_t* xt = reinterpret_cast<uint16_t*>(Xt);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xt[(pq * 8 + j) * XP + pl] = h16(xr, j);
+        uint16_t* gt = reinterpret_cast<uint16_t*>(Gt);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) gt[(p * WG_BM + pq * 8 + j) * XP + pl] = h16(gr[p], j);
+    };
+
+    const int total_steps = (P + 31) / 32;
+    const int st0 = split * steps;
+    const int nst = st0 >= total_steps ? 0 : (total_steps - st0 < steps ? total_steps - st0 : steps);
+    if (nst > 0) load(0);
+    for (int st = 0; st < nst; ++st) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (st + 1 < nst) load(st + 1);
+        bf16x8 ax[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            ax[i] = *reinterpret_cast<const bf16x8*>(&Xt[(wk * 32 + i * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+#pragma unroll
+        for (int p = 2; p >= 0; --p)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const bf16x8 bg =
+                    *reinterpret_cast<const bf16x8*>(&Gt[(p * WG_BM + wmv * 32 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bg, acc[i][j], 0, 0, 0);
+            }
+    }
+    if (nst == 0) return;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = kt * WG_BK + wk * 32 + i * 16 + 4 * (lane >> 4);
+            const int m = mt * WG_BM + wmv * 32 + j * 16 + (lane & 15);
+            if (m >= a.M) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (k + r < sg.cpitch) atomicAdd(a.dwk + ((int64_t)tap * a.ktot + a.k0 + k + r) * a.M + m, acc[i][j][r]);
+        }
+}
+
+__global__ void k_unet_wgrad_finalize(const float* __restrict__ dwk, int ktot, const int* __restrict__ inv, int k0,
+                                      int cout, int cin, int taps, int accumulate, float* __restrict__ dw) {
+    const int64_t n = (int64_t)cout * cin * taps;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int tap = (int)(e % taps);
+        const int64_t r = e / taps;
+        const int c = (int)(r % cin), m = (int)(r / cin);
+        float s = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int k = inv[c * 3 + j];
+            if (k >= 0) s += dwk[((int64_t)tap * ktot + k0 + k) * cout + m];
+        }
+        dw[e] = accumulate ? dw[e] + s : s;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Weight operand preparation (hi / mid / lo bf16 parts in the MFMA fragment order)
+// ---------------------------------------------------------------------------------------------
+__global__ void k_unet_prep_weights(const float* __restrict__ w, int cout, int cin, int ks, const int* __restrict__ kmap,
+                                    int transpose, int flip, int mvalid, int kc0, int nkc, int kct, int mpad,
+                                    uint16_t* __restrict__ dst) {
+    const int taps = ks * ks;
+    const int64_t per_part = (int64_t)taps * nkc * mpad * 32;
+    const int64_t n = 3 * per_part;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int part = (int)(e / per_part);
+        int64_t r = e - part * per_part;
+        const int kk = (int)(r % 32);
+        r /= 32;
+        const int m = (int)(r % mpad);
+        r /= mpad;
+        const int kc = (int)(r % nkc);
+        const int tap = (int)(r / nkc);
+        float v = 0.0f;
+        if (!transpose) {
+            const int c = kmap[kc * 32 + kk];
+            if (m < cout && c >= 0) v = w[((int64_t)m * cin + c) * taps + tap];
+        } else {
+            const int co = kc * 32 + kk;
+            const int c = m < mvalid ? kmap[m] : -1;
+            const int st = flip ? taps - 1 - tap : tap;
+            if (co < cout && c >= 0) v = w[((int64_t)co * cin + c) * taps + st];
+        }
+        uint16_t h, md, l;
+        split3(v, h, md, l);
+        const uint16_t o = part == 0 ? h : (part == 1 ? md : l);
+        dst[(int64_t)part * taps * kct * mpad * 32 + (((int64_t)tap * kct + kc0 + kc) * mpad + m) * 32 + kk] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ConvLIF backward (elementwise) with the surrogate gradients of spiking_util.py
+// ---------------------------------------------------------------------------------------------
+__device__ inline float gauss(float x, float mu, float sigma) {
+    // spiking_util.py:6-10: exp(-((x - mu) * (x - mu)) / (2 * sigma * sigma)) / (sigma * sqrt(2 pi))
+    const float d = x - mu;
+    return expf(-(d * d) / ((2.0f * sigma) * sigma)) / (sigma * sqrtf(2.0f * 3.14159265358979323846f));
+}
+
+__device__ inline float surrogate(float x, float w, int kind) {
+    switch (kind) {
+        case SNNFLOW_SG_SUPERSPIKE: {  // 1 / (1 + width * |x|) ** 2
+            const float d = 1.0f + w * fabsf(x);
+            return 1.0f / (d * d);
+        }
+        case SNNFLOW_SG_MGSPIKE:  // 1.15 N(x; 0, w) - 0.15 N(x; w, 6w) - 0.15 N(x; -w, 6w)
+            return (1.15f * gauss(x, 0.0f, w) - 0.15f * gauss(x, w, 6.0f * w)) - 0.15f * gauss(x, -w, 6.0f * w);
+        case SNNFLOW_SG_TRIANGLE:  // relu(1 - width * |x|)
+            return fmaxf(0.0f, 1.0f - w * fabsf(x));
+        default:  // arctanspike: 1 / (1 + width * x * x)
+            return 1.0f / (1.0f + (w * x) * x);
+    }
+}
+
+__global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args a) {
+    __shared__ float sums[2 * 512];
+    const int tid = threadIdx.x;
+    const int C = a.C, PQ = a.gc_pitch / 4, CQ = C / 4;
+    const int ppi = UNT / PQ;  // pixels per block iteration
+    const int quad = tid % PQ, pr = tid / PQ;
+    for (int i = tid; i < 2 * C; i += UNT) sums[i] = 0.0f;
+    __syncthreads();
+    const int64_t plane = (int64_t)a.P * C;
+    float st[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
+    const int c0 = quad * 4;
+    float lam[4] = {0.f, 0.f, 0.f, 0.f}, th[4] = {0.f, 0.f, 0.f, 0.f};
+    if (quad < CQ)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            lam[r] = 1.0f / (1.0f + expf(-a.leak[c0 + r]));
+            const float t0 = a.thresh[c0 + r];
+            th[r] = t0 < 0.01f ? 0.01f : t0;
+        }
+    if (pr < ppi) {
+        for (int64_t p = (int64_t)blockIdx.x * ppi + pr; p < a.P; p += (int64_t)gridDim.x * ppi) {
+            uint16_t* gh = a.g_cur3 + p * a.gc_pitch + c0;
+            if (quad >= CQ) {  // padding channels of the gradient planes
+#pragma unroll
+                for (int k = 0; k < 3; ++k) *reinterpret_cast<uint2*>(gh + k * a.gc_part) = make_uint2(0u, 0u);
+                continue;
+            }
+            const int64_t e0 = p * C + c0;
+            float go[4] = {0.f, 0.f, 0.f, 0.f}, gsv[4] = {0.f, 0.f, 0.f, 0.f}, gsz[4] = {0.f, 0.f, 0.f, 0.f};
+            float vp[4] = {0.f, 0.f, 0.f, 0.f}, zp[4] = {0.f, 0.f, 0.f, 0.f};
+            if (a.g_out) {
+                const float4 t = *reinterpret_cast<const float4*>(a.g_out + p * a.g_pitch + c0);
+                go[0] = t.x; go[1] = t.y; go[2] = t.z; go[3] = t.w;
+            }
+            if (a.g_state) {
+                const float4 t = *reinterpret_cast<const float4*>(a.g_state + e0);
+                const float4 u = *reinterpret_cast<const float4*>(a.g_state + plane + e0);
+                gsv[0] = t.x; gsv[1] = t.y; gsv[2] = t.z; gsv[3] = t.w;
+                gsz[0] = u.x; gsz[1] = u.y; gsz[2] = u.z; gsz[3] = u.w;
+            }
+            if (a.prev_state) {
+                const float4 t = *reinterpret_cast<const float4*>(a.prev_state + e0);
+                const float4 u = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
+                vp[0] = t.x; vp[1] = t.y; vp[2] = t.z; vp[3] = t.w;
+                zp[0] = u.x; zp[1] = u.y; zp[2] = u.z; zp[3] = u.w;
+            }
+            const float4 vo4 = *reinterpret_cast<const float4*>(a.state + e0);
+            const float4 I4 = *reinterpret_cast<const float4*>(a.current + e0);
+            const float vo[4] = {vo4.x, vo4.y, vo4.z, vo4.w}, I[4] = {I4.x, I4.y, I4.z, I4.w};
+            uint16_t hh[4], mm[4], ll[4];
+            float gvp[4], gzp[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float x = vo[r] - th[r];
+                const float gxs = (go[r] + gsz[r]) * surrogate(x, a.width, a.surrogate);
+                const float gv = gsv[r] + gxs;
+                split3(gv * (1.0f - lam[r]), hh[r], mm[r], ll[r]);
+                if (a.hard_reset) {
+                    gvp[r] = (gv * (1.0f - zp[r])) * lam[r];
+                    gzp[r] = a.detach ? 0.0f : -(gv * (vp[r] * lam[r]));
+                    sl[r] += gv * ((vp[r] * (1.0f - zp[r])) - I[r]);
+                    st[r] += -gxs;
+                } else {
+                    gvp[r] = gv * lam[r];
+                    gzp[r] = a.detach ? 0.0f : -(gv * th[r]);
+                    sl[r] += gv * (vp[r] - I[r]);
+                    st[r] += -gxs - gv * zp[r];
+                }
+            }
+            *reinterpret_cast<uint2*>(gh) = make_uint2((uint32_t)hh[0] | ((uint32_t)hh[1] << 16), (uint32_t)hh[2] | ((uint32_t)hh[3] << 16));
+            *reinterpret_cast<uint2*>(gh + a.gc_part) =
+                make_uint2((uint32_t)mm[0] | ((uint32_t)mm[1] << 16), (uint32_t)mm[2] | ((uint32_t)mm[3] << 16));
+            *reinterpret_cast<uint2*>(gh + 2 * a.gc_part) =
+                make_uint2((uint32_t)ll[0] | ((uint32_t)ll[1] << 16), (uint32_t)ll[2] | ((uint32_t)ll[3] << 16));
+            if (a.g_prev) {
+                *reinterpret_cast<float4*>(a.g_prev + e0) = make_float4(gvp[0], gvp[1], gvp[2], gvp[3]);
+                *reinterpret_cast<float4*>(a.g_prev + plane + e0) = make_float4(gzp[0], gzp[1], gzp[2], gzp[3]);
+            }
+            if (a.g_res) {
+                float4* gr = reinterpret_cast<float4*>(a.g_res + p * a.gres_pitch + c0);
+                const float4 o = *gr;
+                *gr = make_float4(o.x + go[0], o.y + go[1], o.z + go[2], o.w + go[3]);
+            }
+        }
+        if (quad < CQ)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                atomicAdd(&sums[c0 + r], st[r]);
+                atomicAdd(&sums[C + c0 + r], sl[r]);
+            }
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * C; i += UNT) atomicAdd(a.acc + i, (double)sums[i]);
+}
+
+__global__ void k_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,
+                                        float* g_leak, float* g_thresh) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < C; j += gridDim.x * blockDim.x) {
+        const float s = 1.0f / (1.0f + expf(-leak[j]));
+        const float gth = thresh[j] >= 0.01f ? (float)acc[j] : 0.0f;
+        const float glk = ((float)acc[C + j] * (1.0f - s)) * s;
+        g_thresh[j] = accumulate ? g_thresh[j] + gth : gth;
+        g_leak[j] = accumulate ? g_leak[j] + glk : glk;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Packing, decoder input (upsample + concat), prediction layers
+// ---------------------------------------------------------------------------------------------
+__global__ void k_unet_pack(const float* __restrict__ src, int B, int H, int W, int C, int64_t sb, int64_t sc,
+                            int64_t sh, int64_t sw, int split, uint16_t* __restrict__ dst, int cpitch) {
+    const int64_t n = (int64_t)B * H * W * cpitch;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e % cpitch);
+        const int64_t pix = e / cpitch;
+        const int x = (int)(pix % W), y = (int)((pix / W) % H), b = (int)(pix / ((int64_t)W * H));
+        const int part = split ? k / C : (k < C ? 0 : 3);
+        uint16_t o = 0;
+        if (part < 3) {
+            const int c = split ? k - part * C : k;
+            const float v = src[b * sb + c * sc + y * sh + x * sw];
+            uint16_t h, m, l;
+            split3(v, h, m, l);
+            o = split ? (part == 0 ? h : (part == 1 ? m : l)) : h;
+        }
+        dst[e] = o;
+    }
+}
+
+// bilinear x2, align_corners=False (torch area_pixel_compute_source_index with scale 1/2):
+// src = max(0, (dst + 0.5) * 0.5 - 0.5); i0 = floor(src); i1 = i0 + (i0 < n - 1); l1 = src - i0
+struct Lin { int i0, i1; float l0, l1; };
+__device__ inline Lin lin2(int d, int n) {
+    float s = ((float)d + 0.5f) * 0.5f - 0.5f;
+    s = s < 0.0f ? 0.0f : s;
+    Lin r;
+    r.i0 = (int)s;
+    r.i1 = r.i0 + (r.i0 < n - 1 ? 1 : 0);
+    r.l1 = s - (float)r.i0;
+    r.l0 = 1.0f - r.l1;
+    return r;
+}
+
+__device__ inline void ld4bf(const uint16_t* p, float (&v)[4]) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf2f(u.x & 0xffff); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffff); v[3] = bf2f(u.y >> 16);
+}
+
+__global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, const uint16_t* __restrict__ blk, int cb,
+                              int pbp, const float* __restrict__ pred, int B, int h, int w, uint16_t* __restrict__ dst,
+                              int cpitch) {
+    const int H = 2 * h, W = 2 * w, Q = cpitch / 4;
+    const int64_t n = (int64_t)B * H * W * Q;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e % Q) * 4;
+        const int64_t pix = e / Q;
+        const int X = (int)(pix % W), Y = (int)((pix / W) % H), b = (int)(pix / ((int64_t)W * H));
+        const Lin ly = lin2(Y, h), lx = lin2(X, w);
+        uint16_t o[4] = {0, 0, 0, 0};
+        const uint16_t* src = nullptr;
+        int sp = 0, c = 0;
+        if (k < cx) {
+            src = x; sp = pxp; c = k;
+        } else if (k < cx + cb) {
+            src = blk; sp = pbp; c = k - cx;
+        }
+        if (src) {
+            float a00[4], a01[4], a10[4], a11[4];
+            const int64_t r0 = ((int64_t)b * h + ly.i0) * w, r1 = ((int64_t)b * h + ly.i1) * w;
+            ld4bf(src + (r0 + lx.i0) * sp + c, a00);
+            ld4bf(src + (r0 + lx.i1) * sp + c, a01);
+            ld4bf(src + (r1 + lx.i0) * sp + c, a10);
+            ld4bf(src + (r1 + lx.i1) * sp + c, a11);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                o[r] = f2bf(ly.l0 * (lx.l0 * a00[r] + lx.l1 * a01[r]) + ly.l1 * (lx.l0 * a10[r] + lx.l1 * a11[r]));
+        } else if (pred && k < cx + cb + 8) {
+            float up[2];
+#pragma unroll
+            for (int ch = 0; ch < 2; ++ch) {
+                const float* pp = pred + ((int64_t)b * 2 + ch) * h * w;
+                const float v00 = pp[ly.i0 * w + lx.i0], v01 = pp[ly.i0 * w + lx.i1];
+                const float v10 = pp[ly.i1 * w + lx.i0], v11 = pp[ly.i1 * w + lx.i1];
+                up[ch] = ly.l0 * (lx.l0 * v00 + lx.l1 * v01) + ly.l1 * (lx.l0 * v10 + lx.l1 * v11);
+            }
+            uint16_t h0, m0, l0, h1, m1, l1;
+            split3(up[0], h0, m0, l0);
+            split3(up[1], h1, m1, l1);
+            if (k == cx + cb) {
+                o[0] = h0; o[1] = h1; o[2] = m0; o[3] = m1;
+            } else {
+                o[0] = l0; o[1] = l1;
+            }
+        }
+        *reinterpret_cast<uint2*>(dst + pix * cpitch + k) =
+            make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
+    }
+}
+
+// weight of high-res coordinate D's interpolation on low-res index i
+__device__ inline float lin_w(const Lin& l, int i) { return (l.i0 == i ? l.l0 : 0.0f) + (l.i1 == i ? l.l1 : 0.0f); }
+
+__global__ void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb, int has_pred, int B, int h,
+                                  int w, float* __restrict__ gx, int gxp, float* __restrict__ gb, int gbp,
+                                  float* __restrict__ gpred) {
+    const int H = 2 * h, W = 2 * w;
+    const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
+    const int64_t n = (int64_t)B * h * w * Q;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e % Q) * 4;
+        const int64_t pix = e / Q;
+        const int x = (int)(pix % w), y = (int)((pix / w) % h), b = (int)(pix / ((int64_t)w * h));
+        float s[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int Y = 2 * y - 1; Y <= 2 * y + 2; ++Y) {
+            if (Y < 0 || Y >= H) continue;
+            const float wy = lin_w(lin2(Y, h), y);
+            if (wy == 0.0f) continue;
+            for (int X = 2 * x - 1; X <= 2 * x + 2; ++X) {
+                if (X < 0 || X >= W) continue;
+                const float wx = lin_w(lin2(X, w), x);
+                if (wx == 0.0f) continue;
+                const float4 g = *reinterpret_cast<const float4*>(gup + (((int64_t)b * H + Y) * W + X) * gpitch + k);
+                const float ww = wy * wx;
+                s[0] += ww * g.x; s[1] += ww * g.y; s[2] += ww * g.z; s[3] += ww * g.w;
+            }
+        }
+        if (k < cx) {
+            float4* d = reinterpret_cast<float4*>(gx + pix * gxp + k);
+            const float4 o = *d;
+            *d = make_float4(o.x + s[0], o.y + s[1], o.z + s[2], o.w + s[3]);
+        } else if (k < cx + cb) {
+            float4* d = reinterpret_cast<float4*>(gb + pix * gbp + (k - cx));
+            const float4 o = *d;
+            *d = make_float4(o.x + s[0], o.y + s[1], o.z + s[2], o.w + s[3]);
+        } else {  // pred channels: positions hi0, hi1 (mid / lo positions carry the same gradient)
+            gpred[((int64_t)b * 2 + 0) * h * w + (int64_t)y * w + x] = s[0];
+            gpred[((int64_t)b * 2 + 1) * h * w + (int64_t)y * w + x] = s[1];
+        }
+    }
+}
+
+__global__ void k_unet_pred_fwd(const uint16_t* __restrict__ x, int cpitch, int C, const float* __restrict__ wt,
+                                const float* __restrict__ bias, int B, int h, int w, int up, float* __restrict__ flow,
+                                float* __restrict__ flow_full) {
+    const int64_t n = (int64_t)B * h * w;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int xx = (int)(p % w), y = (int)((p / w) % h), b = (int)(p / ((int64_t)w * h));
+        float s0 = 0.0f, s1 = 0.0f;
+        const uint16_t* xp = x + p * cpitch;
+        for (int c = 0; c < C; c += 4) {
+            float v[4];
+            ld4bf(xp + c, v);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                s0 += v[r] * wt[c + r];
+                s1 += v[r] * wt[C + c + r];
+            }
+        }
+        const float f0 = tanhf(s0 + bias[0]), f1 = tanhf(s1 + bias[1]);
+        flow[((int64_t)b * 2 + 0) * h * w + (int64_t)y * w + xx] = f0;
+        flow[((int64_t)b * 2 + 1) * h * w + (int64_t)y * w + xx] = f1;
+        const int Hf = h * up, Wf = w * up;
+        for (int dy = 0; dy < up; ++dy)
+            for (int dx = 0; dx < up; ++dx) {
+                const int64_t o = (int64_t)(y * up + dy) * Wf + (xx * up + dx);
+                flow_full[((int64_t)b * 2 + 0) * Hf * Wf + o] = f0;
+                flow_full[((int64_t)b * 2 + 1) * Hf * Wf + o] = f1;
+            }
+    }
+}
+
+// g_pre[b][ch][y][x] = (1 - f^2) * (sum of g_full over the up x up block + g_extra); db sums
+__global__ void k_unet_pred_gpre(const float* __restrict__ flow, const float* __restrict__ g_full,
+                                 const float* __restrict__ g_extra, int B, int h, int w, int up, float* __restrict__ gpre,
+                                 double* acc, int C) {
+    __shared__ float sb[2];
+    if (threadIdx.x < 2) sb[threadIdx.x] = 0.0f;
+    __syncthreads();
+    const int64_t n = (int64_t)B * h * w;
+    float t0 = 0.0f, t1 = 0.0f;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int xx = (int)(p % w), y = (int)((p / w) % h), b = (int)(p / ((int64_t)w * h));
+        const int Hf = h * up, Wf = w * up;
+        float gg[2];
+#pragma unroll
+        for (int ch = 0; ch < 2; ++ch) {
+            float g = 0.0f;
+            if (g_full) {
+                const float* gf = g_full + ((int64_t)b * 2 + ch) * Hf * Wf;
+                for (int dy = 0; dy < up; ++dy)
+                    for (int dx = 0; dx < up; ++dx) g += gf[(int64_t)(y * up + dy) * Wf + (xx * up + dx)];
+            }
+            const int64_t lo = ((int64_t)b * 2 + ch) * h * w + (int64_t)y * w + xx;
+            if (g_extra) g += g_extra[lo];
+            const float f = flow[lo];
+            gg[ch] = g * (1.0f - f * f);
+            gpre[lo] = gg[ch];
+        }
+        t0 += gg[0];
+        t1 += gg[1];
+    }
+    atomicAdd(&sb[0], t0);
+    atomicAdd(&sb[1], t1);
+    __syncthreads();
+    if (threadIdx.x < 2) atomicAdd(acc + 2 * C + threadIdx.x, (double)sb[threadIdx.x]);
+}
+
+// g_x[pix][c] += W[0][c] g_pre0 + W[1][c] g_pre1; dW sums (2C)
+__global__ __launch_bounds__(UNT) void k_unet_pred_bwd_x(const uint16_t* __restrict__ x, int cpitch, int C,
+                                                         const float* __restrict__ wt, const float* __restrict__ gpre,
+                                                         int B, int h, int w, float* __restrict__ gx, int gxp,
+                                                         double* acc) {
+    __shared__ float sw[2 * 512];
+    const int tid = threadIdx.x, CQ = C / 4;
+    const int ppi = UNT / CQ, quad = tid % CQ, pr = tid / CQ, c0 = quad * 4;
+    for (int i = tid; i < 2 * C; i += UNT) sw[i] = 0.0f;
+    __syncthreads();
+    const int64_t n = (int64_t)B * h * w;
+    float d0[4] = {0.f, 0.f, 0.f, 0.f}, d1[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pr < ppi) {
+        float w0[4], w1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            w0[r] = wt[c0 + r];
+            w1[r] = wt[C + c0 + r];
+        }
+        for (int64_t p = (int64_t)blockIdx.x * ppi + pr; p < n; p += (int64_t)gridDim.x * ppi) {
+            const int xx = (int)(p % w), y = (int)((p / w) % h), b = (int)(p / ((int64_t)w * h));
+            const float g0 = gpre[((int64_t)b * 2 + 0) * h * w + (int64_t)y * w + xx];
+            const float g1 = gpre[((int64_t)b * 2 + 1) * h * w + (int64_t)y * w + xx];
+            float v[4];
+            ld4bf(x + p * cpitch + c0, v);
+            float4* d = reinterpret_cast<float4*>(gx + p * gxp + c0);
+            const float4 o = *d;
+            *d = make_float4(o.x + (w0[0] * g0 + w1[0] * g1), o.y + (w0[1] * g0 + w1[1] * g1),
+                             o.z + (w0[2] * g0 + w1[2] * g1), o.w + (w0[3] * g0 + w1[3] * g1));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                d0[r] += g0 * v[r];
+                d1[r] += g1 * v[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            atomicAdd(&sw[c0 + r], d0[r]);
+            atomicAdd(&sw[C + c0 + r], d1[r]);
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < 2 * C; i += UNT) atomicAdd(acc + i, (double)sw[i]);
+}
+
+__global__ void k_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b) {
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < 2 * C + 2; j += gridDim.x * blockDim.x) {
+        const float v = (float)acc[j];
+        if (j < 2 * C) g_w[j] = accumulate ? g_w[j] + v : v;
+        else g_b[j - 2 * C] = accumulate ? g_b[j - 2 * C] + v : v;
+    }
+}
+
+int grid1d(int64_t n, int per, int cap) {
+    int64_t g = (n + per - 1) / per;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+template <int WMT, int WM>
+int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
+    using G = ConvGeo<WMT, WM>;
+    const int P = a.B * a.Ho * a.Wo;
+    const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN);
+    if (nb > 0x7fffffff) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: grid too large");
+    hipLaunchKernelGGL((k_unet_conv<WMT, WM>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
+    if (!a || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 || !a->w || a->nseg < 1 ||
+        a->nseg > SNNFLOW_UNET_MAX_SEGS || a->ksize < 1 || (a->ksize & 1) == 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: bad args");
+    if (a->mpad % 128 != 0 || a->mpad < a->M) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: mpad must cover M in multiples of 128");
+    for (int s = 0; s < a->nseg; ++s) {
+        const snnflow_unet_seg& g = a->seg[s];
+        if (!g.x || g.cpitch <= 0 || g.cpitch % 32 != 0 || g.H <= 0 || g.W <= 0 || g.nparts < 1 || g.nparts > 3 ||
+            g.mode < 0 || g.mode > 2 || g.kc0 < 0 || g.kc0 + g.cpitch / 32 > a->kct)
+            SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: bad segment");
+        if (((uintptr_t)g.x & 15) != 0) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: segment not 16-B aligned");
+    }
+    if (a->epi == SNNFLOW_UNET_EPI_STORE) {
+        if (!a->out || a->ld < a->M || (a->ld % 4) != 0) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: bad store output");
+    } else if (a->epi == SNNFLOW_UNET_EPI_LIF) {
+        if (!a->leak || !a->thresh || !a->state || !a->current || !a->act || a->M % 4 != 0 || a->act_pitch % 4 != 0 ||
+            (a->residual && a->res_pitch % 4 != 0))
+            SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: bad LIF epilogue");
+    } else {
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: unknown epilogue");
+    }
+    const hipStream_t s = (hipStream_t)stream;
+    if (a->M > 64) return launch_conv<4, 2>(*a, s);
+    if (a->M > 32) return launch_conv<2, 2>(*a, s);
+    if (a->M > 16) return launch_conv<2, 1>(*a, s);
+    return launch_conv<1, 1>(*a, s);
+}
+
+int snnflow_unet_prep_weights(const float* w, int cout, int cin, int ksize, const int* kmap, int transpose, int flip,
+                              int mvalid, int kc0, int nkc, int kct, int mpad, uint16_t* dst, void* stream) {
+    if (!w || !kmap || !dst || cout <= 0 || cin <= 0 || ksize <= 0 || nkc <= 0 || kc0 < 0 || kc0 + nkc > kct ||
+        mpad <= 0 || mpad % 128 != 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_prep_weights: bad args");
+    if (!transpose && cout > mpad) SNN_FAIL(SNNFLOW_E_ARG, "unet_prep_weights: cout > mpad");
+    if (transpose && (mvalid > mpad || nkc * 32 < cout)) SNN_FAIL(SNNFLOW_E_ARG, "unet_prep_weights: bad transpose dims");
+    const int64_t n = 3LL * ksize * ksize * nkc * mpad * 32;
+    hipLaunchKernelGGL(k_unet_prep_weights, dim3(grid1d(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, w, cout, cin,
+                       ksize, kmap, transpose, flip, mvalid, kc0, nkc, kct, mpad, dst);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
+    if (!a || !a->g3 || !a->dwk || !a->seg.x || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 ||
+        a->gpitch % 32 != 0 || a->seg.cpitch % 32 != 0 || a->seg.mode == SNNFLOW_UNET_MODE_T2 || a->ksize < 1)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: bad args");
+    const int P = a->B * a->Ho * a->Wo;
+    const int taps = a->ksize * a->ksize;
+    const int ktiles = (a->seg.cpitch + WG_BK - 1) / WG_BK, mtiles = (a->M + WG_BM - 1) / WG_BM;
+    const int64_t tiles = (int64_t)taps * ktiles * mtiles;
+    const int total_steps = (P + 31) / 32;
+    int nsplit = (int)((2048 + tiles - 1) / tiles);  // ~2048+ blocks
+    if (nsplit > total_steps / 4) nsplit = total_steps / 4;  // >= 4 steps (128 pixels) per block
+    if (nsplit < 1) nsplit = 1;
+    const int steps = (total_steps + nsplit - 1) / nsplit;
+    hipLaunchKernelGGL(k_unet_wgrad, dim3((unsigned)(tiles * nsplit)), dim3(UNT), 0, (hipStream_t)stream, *a, ktiles,
+                       mtiles, nsplit, steps);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_wgrad_finalize(const float* dwk, int ktot, const int* kmap_inv, int k0, int nk, int cout, int cin,
+                                int ksize, int accumulate, float* dw, void* stream) {
+    (void)nk;
+    if (!dwk || !kmap_inv || !dw || cout <= 0 || cin <= 0 || ksize <= 0) SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad_finalize: bad args");
+    const int64_t n = (int64_t)cout * cin * ksize * ksize;
+    hipLaunchKernelGGL(k_unet_wgrad_finalize, dim3(grid1d(n, 256, 4096)), dim3(256), 0, (hipStream_t)stream, dwk, ktot,
+                       kmap_inv, k0, cout, cin, ksize * ksize, accumulate, dw);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream) {
+    if (!a || a->P <= 0 || a->C <= 0 || a->C % 4 != 0 || a->C > 512 || !a->leak || !a->thresh || !a->state ||
+        !a->current || !a->g_cur3 || !a->acc || a->gc_pitch % 32 != 0 || a->gc_pitch < a->C || a->gc_pitch > 1024 ||
+        (a->g_out && a->g_pitch % 4 != 0) || (a->g_res && a->gres_pitch % 4 != 0) || a->surrogate < 0 ||
+        a->surrogate > 3)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_lif_bwd: bad args");
+    const int ppi = UNT / (a->gc_pitch / 4);
+    hipLaunchKernelGGL(k_unet_lif_bwd, dim3(grid1d((int64_t)a->P, ppi, 2048)), dim3(UNT), 0, (hipStream_t)stream, *a);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,
+                                  float* g_leak, float* g_thresh, void* stream) {
+    if (!acc || !leak || !thresh || !g_leak || !g_thresh || C <= 0) SNN_FAIL(SNNFLOW_E_ARG, "unet_cell_param_grads: bad args");
+    hipLaunchKernelGGL(k_unet_cell_param_grads, dim3(grid1d(C, 256, 64)), dim3(256), 0, (hipStream_t)stream, acc, leak,
+                       thresh, C, accumulate, g_leak, g_thresh);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_pack(const float* src, int B, int H, int W, int C, int64_t sb, int64_t sc, int64_t sh, int64_t sw,
+                      int split, uint16_t* dst, int cpitch, void* stream) {
+    if (!src || !dst || B <= 0 || H <= 0 || W <= 0 || C <= 0 || cpitch % 32 != 0 || (split ? 3 * C : C) > cpitch)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_pack: bad args");
+    const int64_t n = (int64_t)B * H * W * cpitch;
+    hipLaunchKernelGGL(k_unet_pack, dim3(grid1d(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src, B, H, W, C, sb,
+                       sc, sh, sw, split, dst, cpitch);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_dec_in(const uint16_t* x, int cx, int px, const uint16_t* block, int cb, int pb, const float* pred, int B,
+                        int h, int w, uint16_t* dst, int cpitch, void* stream) {
+    if (!x || !block || !dst || B <= 0 || h <= 0 || w <= 0 || cx % 4 != 0 || cb % 4 != 0 || cpitch % 32 != 0 ||
+        cx + cb + (pred ? 6 : 0) > cpitch)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in: bad args");
+    const int64_t n = (int64_t)B * 4 * h * w * (cpitch / 4);
+    hipLaunchKernelGGL(k_unet_dec_in, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, x, cx, px, block,
+                       cb, pb, pred, B, h, w, dst, cpitch);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int has_pred, int B, int h, int w, float* g_x,
+                            int gx_pitch, float* g_block, int gb_pitch, float* g_pred, void* stream) {
+    if (!g_up || !g_x || !g_block || (has_pred && !g_pred) || B <= 0 || h <= 0 || w <= 0 || cx % 4 != 0 ||
+        cb % 4 != 0 || gpitch % 4 != 0 || gx_pitch % 4 != 0 || gb_pitch % 4 != 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: bad args");
+    const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
+    const int64_t n = (int64_t)B * h * w * Q;
+    hipLaunchKernelGGL(k_unet_dec_in_bwd, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up, gpitch, cx,
+                       cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, const float* b, int B, int h, int wd,
+                          int up, float* flow, float* flow_full, void* stream) {
+    if (!x || !w || !b || !flow || !flow_full || C <= 0 || C % 4 != 0 || C > cpitch || B <= 0 || h <= 0 || wd <= 0 ||
+        up < 1)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_pred_fwd: bad args");
+    hipLaunchKernelGGL(k_unet_pred_fwd, dim3(grid1d((int64_t)B * h * wd, 256, 8192)), dim3(256), 0, (hipStream_t)stream, x,
+                       cpitch, C, w, b, B, h, wd, up, flow, flow_full);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, const float* flow, const float* g_full,
+                          const float* g_extra, int B, int h, int wd, int up, float* gpre, float* g_x, int gx_pitch,
+                          double* acc, void* stream) {
+    if (!x || !w || !flow || !gpre || !g_x || !acc || C <= 0 || C % 4 != 0 || C > 512 || B <= 0 || h <= 0 || wd <= 0 ||
+        up < 1 || gx_pitch % 4 != 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_pred_bwd: bad args");
+    const hipStream_t s = (hipStream_t)stream;
+    const int64_t n = (int64_t)B * h * wd;
+    hipLaunchKernelGGL(k_unet_pred_gpre, dim3(grid1d(n, 256, 1024)), dim3(256), 0, s, flow, g_full, g_extra, B, h, wd, up,
+                       gpre, acc, C);
+    const int ppi = UNT / (C / 4);
+    hipLaunchKernelGGL(k_unet_pred_bwd_x, dim3(grid1d(n, ppi, 2048)), dim3(UNT), 0, s, x, cpitch, C, w, gpre, B, h, wd,
+                       g_x, gx_pitch, acc);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream) {
+    if (!acc || !g_w || !g_b || C <= 0) SNN_FAIL(SNNFLOW_E_ARG, "unet_pred_param_grads: bad args");
+    hipLaunchKernelGGL(k_unet_pred_param_grads, dim3(grid1d(2 * C + 2, 256, 64)), dim3(256), 0, (hipStream_t)stream, acc,
+                       C, accumulate, g_w, g_b);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

@@ -11,7 +11,10 @@ from . import checkpoint, encodings  # noqa: F401  (checkpoint interchange, on-d
 from .loss import EventWarping
 from .metrics import AAE, AAE_Filtered, AAE_Weighted, AE_ofMeans, AEE, NAAE, NEE
 from .model import LIFFireFlowNet, LIFFireFlowNet_short, LIFFireNet, LIFFireNet_short
+from .unet import (SpikingMultiResUNetRecurrent, SpikingRecEVFlowNet, SpikingRecurrentConvLayer,
+                   SpikingResidualBlock, SpikingUpsampleConvLayer)
 
 __all__ = ["LIFFireNet", "LIFFireNet_short", "LIFFireFlowNet", "LIFFireFlowNet_short", "SNNtorch_ConvLIF",
            "SNNtorch_ConvLIFRecurrent", "ConvLIF", "ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping", "AEE",
-           "NEE", "AAE", "NAAE", "AE_ofMeans", "AAE_Weighted", "AAE_Filtered"]
+           "NEE", "AAE", "NAAE", "AE_ofMeans", "AAE_Weighted", "AAE_Filtered", "SpikingRecEVFlowNet",
+           "SpikingMultiResUNetRecurrent", "SpikingRecurrentConvLayer", "SpikingResidualBlock", "SpikingUpsampleConvLayer"]

@@ -163,6 +163,37 @@ class IweLossArgs(ctypes.Structure):
                 ("images", P), ("acc", P), ("persample", P), ("smooth", P), ("loss", P)]
 
 
+UNET_MAX_SEGS = 4
+UNET_MODE_S1, UNET_MODE_S2, UNET_MODE_T2 = 0, 1, 2
+UNET_EPI_STORE, UNET_EPI_LIF = 0, 1
+SURROGATES = {"arctanspike": 0, "superspike": 1, "mgspike": 2, "trianglespike": 3}
+
+
+class UNetSeg(ctypes.Structure):
+    _fields_ = [("x", P), ("H", I32), ("W", I32), ("cpitch", I32), ("mode", I32), ("kc0", I32), ("nparts", I32)]
+
+
+class UNetConvArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("Ho", I32), ("Wo", I32), ("M", I32), ("ksize", I32), ("nseg", I32),
+                ("seg", UNetSeg * UNET_MAX_SEGS), ("w", P), ("kct", I32), ("mpad", I32), ("epi", I32),
+                ("out", P), ("ld", I32), ("accumulate", I32),
+                ("leak", P), ("thresh", P), ("hard_reset", I32), ("prev_state", P), ("residual", P),
+                ("res_pitch", I32), ("state", P), ("current", P), ("act", P), ("act_pitch", I32)]
+
+
+class UNetWgradArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("Ho", I32), ("Wo", I32), ("M", I32), ("ksize", I32),
+                ("g3", P), ("gpitch", I32), ("gpart", I64), ("seg", UNetSeg), ("k0", I32), ("ktot", I32),
+                ("dwk", P)]
+
+
+class UNetLifBwdArgs(ctypes.Structure):
+    _fields_ = [("P", I32), ("C", I32), ("leak", P), ("thresh", P), ("width", F32), ("hard_reset", I32),
+                ("detach", I32), ("surrogate", I32), ("g_out", P), ("g_pitch", I32), ("g_state", P),
+                ("state", P), ("prev_state", P), ("current", P), ("g_cur3", P), ("gc_pitch", I32),
+                ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P)]
+
+
 EXPORTS = {
     "snnflow_abi_version": (I32, []),
     "snnflow_last_error": (ctypes.c_char_p, []),
@@ -198,6 +229,18 @@ EXPORTS = {
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),
     "snnflow_slot_supported": (I32, [I32, I32]),
     "snnflow_frag_halfs": (I32, [I32, I32]),
+    "snnflow_unet_conv": (I32, [ctypes.POINTER(UNetConvArgs), P]),
+    "snnflow_unet_prep_weights": (I32, [P, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, P, P]),
+    "snnflow_unet_wgrad": (I32, [ctypes.POINTER(UNetWgradArgs), P]),
+    "snnflow_unet_wgrad_finalize": (I32, [P, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
+    "snnflow_unet_lif_bwd": (I32, [ctypes.POINTER(UNetLifBwdArgs), P]),
+    "snnflow_unet_cell_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
+    "snnflow_unet_pack": (I32, [P, I32, I32, I32, I32, I64, I64, I64, I64, I32, P, I32, P]),
+    "snnflow_unet_dec_in": (I32, [P, I32, I32, P, I32, I32, P, I32, I32, I32, P, I32, P]),
+    "snnflow_unet_dec_in_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P]),
+    "snnflow_unet_pred_fwd": (I32, [P, I32, I32, P, P, I32, I32, I32, I32, P, P, P]),
+    "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, P]),
+    "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
 }
 MAX_SLOT_TASKS = 4
 MAX_COUNT_TENSORS = 16

@@ -9,9 +9,11 @@ spike, csrc/convlif.hip); backward = one kernel (surrogate + dgrad of both convs
 dL/dv_prev + threshold/leak sums), one deferred-weight-gradient launch, the slab
 reduction and the parameter-gradient finalisation.
 
-Implemented subset (anything else raises ``NotImplementedError`` at construction):
-kernel_size 3, stride 1, ``activation="arctanspike"``, ``detach=True``, ``norm=None``,
-no quantization, hidden sizes 4/8/16/32 and input sizes 1-5 or equal to the hidden size.
+Two kernel paths: the fused one-kernel-per-cell path above for kernel 3, stride 1, arctanspike,
+detach=True, hidden 4/8/16/32 and input sizes 1-5 or equal to the hidden size; every other
+supported cell (odd kernel sizes, stride 2, hidden sizes up to 512 in multiples of 4, the four
+surrogates of spiking_util.py, detach=False) runs on the implicit-GEMM kernels of csrc/unet.hip
+(``snnflow.unet.ConvLIFCellFn``).  Quantization and norm='weight'/'group' raise.
 """
 import ctypes
 import math
@@ -24,21 +26,28 @@ from ._lib import lib, ptr
 from .engine import _ptr_t, _x_strides, as_nhwc_state, empty_state
 
 _HIDDEN = (4, 8, 16, 32)
+_SURROGATES = ("arctanspike", "superspike", "mgspike", "trianglespike")
 
 
 def _check(input_size, hidden_size, kernel_size, stride, activation, detach, norm, quantization_config):
     if quantization_config is not None and quantization_config.get("enabled", False):
         raise NotImplementedError("quantized ConvLIF (brevitas) is not implemented on the HIP path")
-    if kernel_size != 3 or stride != 1:
-        raise NotImplementedError("ConvLIF: only kernel_size=3, stride=1 are implemented")
-    if activation != "arctanspike":
-        raise NotImplementedError(f"ConvLIF: activation {activation!r} (only 'arctanspike')")
-    if not detach:
-        raise NotImplementedError("ConvLIF: only detach=True is implemented")
+    if kernel_size % 2 != 1 or stride not in (1, 2):
+        raise NotImplementedError("ConvLIF: odd kernel sizes and strides 1, 2 are implemented")
+    if activation not in _SURROGATES:
+        raise NotImplementedError(f"ConvLIF: activation {activation!r}")
     if norm is not None:
-        raise NotImplementedError("ConvLIF: norm is not implemented")
-    if hidden_size not in _HIDDEN or not (1 <= input_size <= 5 or input_size == hidden_size):
-        raise NotImplementedError(f"ConvLIF: {input_size}->{hidden_size} channels have no compiled kernel")
+        raise NotImplementedError("ConvLIF: norm='weight'/'group' is not implemented")
+    if hidden_size % 4 != 0 or hidden_size > 512:
+        raise NotImplementedError(f"ConvLIF: hidden size {hidden_size} (multiples of 4 up to 512)")
+
+
+def _fixed_kernel(cell):
+    """True when the one-kernel-per-cell ConvLIF path (csrc/convlif.hip) covers the cell; else the
+    implicit-GEMM cell path of csrc/unet.hip runs (snnflow.unet.ConvLIFCellFn)."""
+    k = cell.ff.kernel_size[0]
+    return (k == 3 and cell.ff.stride[0] == 1 and cell.hidden_size in _HIDDEN and cell.activation == "arctanspike"
+            and cell.detach and (1 <= cell.input_size <= 5 or cell.input_size == cell.hidden_size))
 
 
 class _Cell(nn.Module):
@@ -72,6 +81,9 @@ class _Cell(nn.Module):
         if res is not None:
             res = res.expand(input_.shape[0], self.hidden_size, input_.shape[2], input_.shape[3])
         prev = None if prev_state is None else as_nhwc_state(prev_state)
+        if not _fixed_kernel(self):
+            from .unet import ConvLIFCellFn
+            return ConvLIFCellFn.apply(self, input_, prev, res, *self._params())
         return ConvLIFFn.apply(self, input_, prev, res, *self._params())
 
 

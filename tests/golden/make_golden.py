@@ -327,6 +327,50 @@ def lif_export_case(out):
                         threshold=thr.numpy(), spk=spk.numpy(), mem_out=mo.numpy())
 
 
+def unet_kwargs_ref(base=4, activations=("arctanspike", "arctanspike")):
+    """The train_SNN.yml model section for SpikingRecEVFlowNet, minus the keys the reference's
+    BaseUNet constructor rejects (quantization / tebn / mpbn: SURVEY f3)."""
+    return {"name": "SpikingRecEVFlowNet", "encoding": "cnt", "round_encoding": False, "norm_input": False,
+            "num_bins": 2, "base_num_channels": base, "kernel_size": 3, "activations": list(activations),
+            "mask_output": True,
+            "spiking_neuron": {"leak": [0.0, 1.0], "thresh": [0.0, 0.8], "learn_leak": True, "learn_thresh": True,
+                               "hard_reset": True}}
+
+
+def unet_case(ref_model, ref_flow, out, base=4, fname="unet_case.npz"):
+    """models/model.py SpikingRecEVFlowNet (SpikingMultiResUNetRecurrent of ConvLIF cells, reference
+    code end to end): T forwards with carried states, EventWarping over the 4 flow maps, backward."""
+    torch.manual_seed(17)
+    gen = torch.Generator().manual_seed(18)
+    H, W, B, N, T = 32, 32, 2, 200, 3
+    model = ref_model.SpikingRecEVFlowNet(unet_kwargs_ref(base))
+    config = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001,
+              "overwrite_intermediate": False}, "model": {"mask_output": True}}
+    lossf = ref_flow.EventWarping(config, "cpu")
+    rec = {"res": np.array([H, W]), "T": T, "base": base}
+    for k, v in model.state_dict().items():
+        rec[f"p0.{k}"] = v.numpy().copy()
+    for t in range(T):
+        ev, pol, cnt, mask = synth_events(gen, B, N, H, W)
+        cnt = cnt * 1.0
+        x = model(None, cnt)
+        lossf.event_flow_association(x["flow"], ev.clone(), pol, mask)
+        rec[f"cnt_{t}"] = cnt.numpy()
+        rec[f"events_{t}"] = ev.numpy()
+        rec[f"pol_{t}"] = pol.numpy()
+        rec[f"mask_{t}"] = mask.numpy()
+        for i, f in enumerate(x["flow"]):
+            rec[f"flow_{t}_{i}"] = f.detach().numpy()
+        for i, st in enumerate(model.states):
+            rec[f"state_{t}_{i}"] = st.detach().numpy()
+    loss = lossf()
+    loss.backward()
+    rec["loss"] = np.array(loss.item(), dtype=np.float32)
+    for n, p in model.named_parameters():
+        rec[f"g.{n}"] = p.grad.numpy()
+    np.savez_compressed(os.path.join(out, fname), **rec)
+
+
 def import_dataloader(ref_root):
     """dataloader/__init__.py imports h5py (absent): register the package without running
     it, then import the two pure-torch modules."""
@@ -360,6 +404,13 @@ def main():
         liffirenet_case(ref_model, ref_flow, HERE, "LIFFireNet", 8, "liffirenet_c8_case.npz")
         print("liffirenet_c8 fixture written")
         return
+    if only == ["unet"]:
+        import loss.flow as ref_flow
+        import models.model as ref_model
+        torch.set_num_threads(1)
+        unet_case(ref_model, ref_flow, HERE)
+        print("unet fixture written")
+        return
     if only == ["eval"]:
         import loss.flow as ref_flow
         import utils.iwe as ref_iwe
@@ -385,6 +436,7 @@ def main():
     ref_enc, ref_base = import_dataloader(ref_root)
     encodings_case(ref_enc, ref_base, out)
     eval_case(ref_flow, ref_iwe, out)
+    unet_case(ref_model, ref_flow, out)
     lif_export_case(out)
     print("golden fixtures written to", out)
 

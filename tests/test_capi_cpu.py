@@ -40,6 +40,8 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_wgrad_step": _lib.WgradStep, "snnflow_aee_args": _lib.AeeArgs, "snnflow_encode_args": _lib.EncodeArgs, "snnflow_convlif_params": _lib.ConvLifParams,
         "snnflow_convlif_fwd_args": _lib.ConvLifFwdArgs, "snnflow_convlif_bwd_args": _lib.ConvLifBwdArgs, "snnflow_wgrad_args": _lib.WgradArgs, "snnflow_iwe_loss_args": _lib.IweLossArgs,
         "snnflow_flow_metrics_args": _lib.FlowMetricsArgs,
+        "snnflow_unet_seg": _lib.UNetSeg, "snnflow_unet_conv_args": _lib.UNetConvArgs,
+        "snnflow_unet_wgrad_args": _lib.UNetWgradArgs, "snnflow_unet_lif_bwd_args": _lib.UNetLifBwdArgs,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
