@@ -39,10 +39,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--channels", type=int, default=8)
-    p.add_argument("--res", type=int, default=128)
-    p.add_argument("--batch", type=int, default=8, help="per-GPU batch (cfg2/cfg4: 8)")
-    p.add_argument("--T", type=int, default=10, help="windows per loss (window_loss / window)")
+    p.add_argument("--channels", type=int, default=None, help="base_num_channels (LIFFireNet: 8, U-Net: 32)")
+    p.add_argument("--res", type=int, default=None, help="LIFFireNet: 128 (cfg2), U-Net: 256 (cfg5)")
+    p.add_argument("--batch", type=int, default=None, help="per-GPU batch (cfg2/cfg4: 8; cfg5: 16)")
+    p.add_argument("--T", type=int, default=None, help="windows per loss (window_loss / window; cfg5: 20)")
     p.add_argument("--events", type=int, default=1000, help="events per window (data.window)")
     p.add_argument("--model", default="LIFFireNet")
     p.add_argument("--no-graph", action="store_true")
@@ -51,7 +51,12 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=3, help="distinct synthetic batches cycled in HBM")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsals)")
-    return p.parse_args()
+    a = p.parse_args()
+    unet = a.model == "SpikingRecEVFlowNet"
+    for k, lif, un in (("channels", 8, 32), ("res", 128, 256), ("batch", 8, 16), ("T", 10, 20)):
+        if getattr(a, k) is None:
+            setattr(a, k, un if unet else lif)
+    return a
 
 
 def algorithmic_bytes(name, C, P, cin0):
@@ -144,9 +149,22 @@ def main():
     state_bufs = None
     state_flat = None
 
+    unet = args.model == "SpikingRecEVFlowNet"
+
+    def get_states():
+        return model.multires_unetrec.states if unet else model._states
+
+    def set_states(st):
+        if unet:
+            model.multires_unetrec.states = st
+        else:
+            model._states = st
+
     def fwd_bwd():
         loss_fn.reset()
-        if args.per_step:
+        if unet:  # the reference loop: one forward per window (train_flow.py:232), 4 flow maps each
+            outs = [model(w["event_voxel"], w["event_cnt"]) for w in static]
+        elif args.per_step:
             outs = [model(w["event_voxel"], w["event_cnt"]) for w in static]
         else:  # the same T steps, kernels issued as wavefront launches (C = 8; else per step)
             outs = model.forward_sequence([w["event_voxel"] for w in static], [w["event_cnt"] for w in static])
@@ -163,22 +181,23 @@ def main():
         dp.clip_grad_norm_(params, 1.0)
         opt.step()
         nonlocal state_bufs, state_flat
+        states = get_states()
         if state_bufs is None:
-            src = _flat_span(model._states)
+            src = _flat_span(states)
             if src is not None:  # persistent buffers with the same back-to-back layout
                 state_flat = src.clone()
                 base = src.data_ptr()
                 state_bufs = [torch.empty(0, device=dev).set_(state_flat.untyped_storage(),
                                                               (s.data_ptr() - base) // 4, s.shape, s.stride())
-                              for s in model._states]
+                              for s in states]
             else:
-                state_bufs = [s.detach().clone() for s in model._states]
-        src = _flat_span(model._states)
+                state_bufs = [s.detach().clone() for s in states]
+        src = _flat_span(states)
         if src is not None and state_flat is not None:
             state_flat.copy_(src)  # the engine's states are back to back: one contiguous copy
         else:
-            torch._foreach_copy_(state_bufs, [s.detach() for s in model._states])
-        model._states = list(state_bufs)
+            torch._foreach_copy_(state_bufs, [s.detach() for s in states])
+        set_states(list(state_bufs))
 
     def step_eager():
         opt.zero_grad(set_to_none=True)
@@ -251,6 +270,36 @@ def main():
     step_eager()
     _lib.TIMER = None
     kern = timer.summary()
+    if unet:
+        roofline, kernels = _unet_roofline(kern)
+    else:
+        roofline, kernels = _firenet_roofline(kern, model, args, B, R, T)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_unet(args, pool[0][1]) if unet else cpu_baseline(args, pool[0][1])
+
+    if rank == 0:
+        line = {
+            "metric": (f"events/sec (train step) SpikingRecEVFlowNet T={T} {R}x{R}" if unet
+                       else "events/sec (train step) LIFFireNet T=10 128x128"),
+            "value": round(value, 1), "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"{args.model} train step: T={T} x {N}-event windows, {R}x{R}, "
+                                   f"batch {B}/GPU, base_num_channels {args.channels}, EventWarping + Adam",
+                       "global_batch": B * world, "parallelism": f"dp{world}",
+                       "hip_graph": not args.no_graph,
+                       "launch_order": "per-step" if (args.per_step or unet) else "wavefront"},
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _firenet_roofline(kern, model, args, B, R, T):
+    """HBM roofline of the dominant LIFFireNet kernel class (algorithmic bytes / HIP-event time)."""
     rec_layers = {i for i, (_, r) in enumerate(model.layer_spec) if r}
     classes = {}
     for name, v in kern.items():
@@ -270,27 +319,34 @@ def main():
     roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": _pmc_traffic(dominant, args), "bytes_per_launch": abytes, "avg_us": round(avg_us, 2)}
+    return roofline, kernels
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, pool[0][1])
 
-    if rank == 0:
-        line = {
-            "metric": "events/sec (train step) LIFFireNet T=10 128x128",
-            "value": round(value, 1), "unit": "events/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-            "config": {"workload": f"{args.model} train step: T={T} x {N}-event windows, {R}x{R}, "
-                                   f"batch {B}/GPU, base_num_channels {args.channels}, EventWarping + Adam",
-                       "global_batch": B * world, "parallelism": f"dp{world}",
-                       "hip_graph": not args.no_graph,
-                       "launch_order": "per-step" if args.per_step else "wavefront"},
-            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+# bf16 dense MFMA peak (MI355X_MICROARCH.md) over the three bf16 products that make one exact fp32 product
+# (weights split hi/mid/lo, operands exact in bf16): the peak rate of fp32-exact convolution FLOPs
+BF16_PEAK_TFLOPS = 2500.0
+BF16X3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3
+
+
+def _unet_roofline(kern):
+    """MFMA roofline of the dominant U-Net GEMM class: algorithmic (reference fp32 conv) FLOPs per
+    launch / HIP-event time, against the bf16x3 peak; every class listed with its own rate."""
+    kernels = {}
+    total = sum(v["total_ms"] for v in kern.values())
+    for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
+        e = {"launches": v["launches"], "avg_us": round(v["avg_us"], 2), "share": round(v["total_ms"] / total, 3)}
+        if v["work"]:
+            e["tflops"] = round(v["work"] / (v["total_ms"] * 1e-3) / 1e12, 1)
+        kernels[k] = e
+    gemm = {k: v for k, v in kern.items() if v["work"]}
+    dominant = max(gemm, key=lambda k: gemm[k]["total_ms"])
+    d = gemm[dominant]
+    achieved = d["work"] / (d["total_ms"] * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 1), "peak": round(BF16X3_PEAK_TFLOPS, 1),
+                "unit": "TFLOP/s", "frac": round(achieved / BF16X3_PEAK_TFLOPS, 4), "traffic": None,
+                "flops_per_launch": d["work"] / d["launches"], "avg_us": round(d["avg_us"], 2),
+                "peak_note": "bf16 dense 2.5 PF / 3 (hi/mid/lo weight products per exact fp32 product)"}
+    return roofline, kernels
 
 
 _KEYS = ("event_cnt", "event_list", "event_list_pol_mask", "event_mask")
@@ -399,6 +455,42 @@ def cpu_baseline(args, windows):
             "sample": f"{n} timed train steps (after 1 warm-up) of the same workload: {args.batch}x{args.T} windows "
                       f"of {args.events} events, {R}x{R}, C={args.channels}, Adam; oracle/ pure-PyTorch CPU "
                       f"restatement of the reference path, {threads} threads", "seconds": round(dt, 3)}
+
+
+def cpu_baseline_unet(args, windows):
+    """The U-Net oracle (oracle/unet_ref.py, pinned by the reference-generated fixture) on the host
+    cores: one sample's train step over 2 windows at the bench resolution and width (~10-30 s of CPU
+    work), scaled to events/s."""
+    from oracle import iwe_ref
+    from oracle.unet_ref import SpikingRecEVFlowNetRef
+
+    threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+    torch.set_num_threads(threads)
+    torch.manual_seed(0)
+    from snnflow.parser import train_snn_model_kwargs
+    model = SpikingRecEVFlowNetRef(train_snn_model_kwargs("SpikingRecEVFlowNet", base_num_channels=args.channels))
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+    R, nw = args.res, 2
+    cpu_w = [{k: v[:1].cpu() for k, v in w.items()} for w in windows[:nw]]
+    t0 = time.perf_counter()
+    flows = []
+    for w in cpu_w:
+        flows.append(model(None, w["event_cnt"])["flow"])
+    loss = 0
+    for i in range(4):
+        lf = iwe_ref.EventWarpingRef([R, R])
+        for t, w in enumerate(cpu_w):
+            lf.event_flow_association([flows[t][i]], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        loss = loss + lf()
+    (loss / 4).backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+    opt.step()
+    dt = time.perf_counter() - t0
+    ev = nw * args.events
+    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"1 train step of 1 sample x {nw} windows of {args.events} events, {R}x{R}, base {args.channels}; "
+                      f"oracle/unet_ref.py (CPU restatement of the reference U-Net), {threads} threads",
+            "seconds": round(dt, 3)}
 
 
 if __name__ == "__main__":

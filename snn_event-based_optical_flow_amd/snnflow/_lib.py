@@ -284,18 +284,21 @@ class KernelTimer:
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, a, b in self.records:
+        for name, a, b, work in self.records:
             ms = a.elapsed_time(b)
-            n, tot = out.get(name, (0, 0.0))
-            out[name] = (n + 1, tot + ms)
-        return {k: {"launches": n, "total_ms": tot, "avg_us": 1000.0 * tot / n} for k, (n, tot) in out.items()}
+            n, tot, w = out.get(name, (0, 0.0, 0.0))
+            out[name] = (n + 1, tot + ms, w + (work or 0.0))
+        return {k: {"launches": n, "total_ms": tot, "avg_us": 1000.0 * tot / n, "work": w}
+                for k, (n, tot, w) in out.items()}
 
 
 TIMER = None
 
 
-def call(name, fn, *args):
-    """Launch one C-ABI entry point; raise with the library's message on failure."""
+def call(name, fn, *args, work=None):
+    """Launch one C-ABI entry point; raise with the library's message on failure.  With a
+    KernelTimer installed the launch is bracketed by HIP events on the current stream and its
+    algorithmic `work` (FLOPs, if given) is recorded with it."""
     if TIMER is None:
         check(fn(*args), name)
         return
@@ -304,7 +307,7 @@ def call(name, fn, *args):
     a.record()
     check(fn(*args), name)
     b.record()
-    TIMER.records.append((name, a, b))
+    TIMER.records.append((name, a, b, work))
 
 
 def ptr(t):

@@ -347,6 +347,8 @@ class _CellPlan:
             raise NotImplementedError(f"activation {mod.activation!r}")
 
     def prep(self, s):
+        if not torch.cuda.is_current_stream_capturing():  # host copy of the act_width buffer (no read in a capture)
+            self.width = float(self.mod.act_width)
         for sg in self.segs:
             w = sg.weight.detach()
             cin = w.shape[1]
@@ -387,7 +389,14 @@ def conv_lif(plan, B, Ho, Wo, acts, prev_state, residual, state, current, act_ou
     if residual is not None:
         a.residual, a.res_pitch = ptr(residual), residual.shape[-1]
     a.state, a.current, a.act, a.act_pitch = ptr(state), ptr(current), ptr(act_out), act_out.shape[-1]
-    _lib.call("unet_conv", lib.snnflow_unet_conv, ctypes.byref(a), s)
+    _lib.call("unet_conv", lib.snnflow_unet_conv, ctypes.byref(a), s, work=_conv_flops(plan, B * Ho * Wo, acts))
+
+
+def _conv_flops(plan, P_out, acts=None):
+    """Algorithmic FLOPs of a cell's convolution(s) (the reference's fp32 conv: 2 * output pixels *
+    output channels * input channels * k^2), for the segments that take part."""
+    cin = sum(sg.weight.shape[1] for sg, a in zip(plan.segs, acts or [True] * len(plan.segs)) if a is not None)
+    return 2.0 * P_out * plan.C * cin * plan.taps
 
 
 def conv_dgrad(plan, sg, g3, B, Hi, Wi, out, ld, mvalid, accumulate, s):
@@ -401,7 +410,9 @@ def conv_dgrad(plan, sg, g3, B, Hi, Wi, out, ld, mvalid, accumulate, s):
     a.nseg = 3
     a.w, a.kct, a.mpad, a.epi = ptr(sg.wd), plan.gp // 32, sg.wd_mp, _lib.UNET_EPI_STORE
     a.out, a.ld, a.accumulate = ptr(out), ld, 1 if accumulate else 0
-    _lib.call("unet_conv(dgrad)", lib.snnflow_unet_conv, ctypes.byref(a), s)
+    Ho, Wo = g3.shape[2], g3.shape[3]
+    _lib.call("unet_dgrad", lib.snnflow_unet_conv, ctypes.byref(a), s,
+              work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
 
 
 def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
@@ -410,14 +421,15 @@ def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
     a.g3, a.gpitch, a.gpart = ptr(g3), g3.shape[-1], g3[0].numel()
     a.seg = _unet_seg(act, sg.mode, sg.kc0)
     a.k0, a.ktot, a.dwk = sg.k0, plan.ktot, ptr(plan.dwk)
-    _lib.call("unet_wgrad", lib.snnflow_unet_wgrad, ctypes.byref(a), s)
+    _lib.call("unet_wgrad", lib.snnflow_unet_wgrad, ctypes.byref(a), s,
+              work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
 
 
 def lif_bwd(plan, P, g_out, g_state, state, prev_state, current, g3, g_prev, g_res, s):
     m = plan.mod
     a = _lib.UNetLifBwdArgs()
     a.P, a.C = P, plan.C
-    a.leak, a.thresh, a.width = ptr(m.leak), ptr(m.thresh), float(m.act_width)
+    a.leak, a.thresh, a.width = ptr(m.leak), ptr(m.thresh), plan.width
     a.hard_reset, a.detach, a.surrogate = 1 if m.hard_reset else 0, 1 if m.detach else 0, plan.sg
     if g_out is not None:
         a.g_out, a.g_pitch = ptr(g_out), g_out.shape[-1]
@@ -557,26 +569,31 @@ class UNetEngine:
         self.bwd_open = True
 
     def finalize(self, s):
-        """Parameter gradients of the window, in self.params order."""
-        g = {}
+        """Parameter gradients of the window, in self.params order, as views of ONE flat buffer
+        (a single all-reduce / clip over it, snnflow.dp)."""
+        total = sum(p.numel() for p in self.params)
+        flat = torch.empty(total, device=self.dev)
+        views, off = {}, 0
+        for p in self.params:
+            views[id(p)] = flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
         for c in self.cells:
             m = c.mod
             for sg in c.segs:
                 w = sg.weight
-                gw = torch.empty_like(w)
                 _lib.call("unet_wgrad_finalize", lib.snnflow_unet_wgrad_finalize, ptr(c.dwk), c.ktot, ptr(sg.inv),
-                          sg.k0, sg.pitch, c.C, w.shape[1], c.ks, 0, ptr(gw), s)
-                g[id(w)] = gw
-            gl, gt = torch.empty_like(m.leak), torch.empty_like(m.thresh)
+                          sg.k0, sg.pitch, c.C, w.shape[1], c.ks, 0, ptr(views[id(w)]), s)
             _lib.call("unet_cell_param_grads", lib.snnflow_unet_cell_param_grads, ptr(c.acc), ptr(m.leak),
-                      ptr(m.thresh), c.C, 0, ptr(gl), ptr(gt), s)
-            g[id(m.leak)], g[id(m.thresh)] = gl, gt
+                      ptr(m.thresh), c.C, 0, ptr(views[id(m.leak)]), ptr(views[id(m.thresh)]), s)
         for p, acc in zip(self.preds, self.pred_acc):
-            gw, gb = torch.empty_like(p.weight), torch.empty_like(p.bias)
             _lib.call("unet_pred_param_grads", lib.snnflow_unet_pred_param_grads, ptr(acc), p.weight.shape[1], 0,
-                      ptr(gw), ptr(gb), s)
-            g[id(p.weight)], g[id(p.bias)] = gw, gb
-        return [g.get(id(p)) for p in self.params]
+                      ptr(views[id(p.weight)]), ptr(views[id(p.bias)]), s)
+        self.last_flat = flat
+        off, out = 0, []
+        for p in self.params:  # fresh views: AccumulateGrad adopts them as .grad
+            out.append(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return out
 
 
 class _StepCtx:
