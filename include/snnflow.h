@@ -448,6 +448,11 @@ int snnflow_lif_export(const float* x, const float* mem, const float* beta, cons
 /* clip_grad_norm_ (train_flow.py:265-266) over one flat gradient buffer of n floats, in place:
  * total = ||g||_2, g *= min(max_norm / (total + eps), 1); total_out (device, may be NULL). */
 int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float* total_out, void* stream);
+/* The same for large vectors (grid-wide, 3 launches, deterministic fixed-order fp64 partials);
+ * scratch: SNNFLOW_CLIP_SCRATCH doubles. */
+#define SNNFLOW_CLIP_SCRATCH 513
+int snnflow_clip_grad_norm_large(float* g, int64_t n, float max_norm, float eps, float* total_out,
+                                 double* scratch, void* stream);
 
 /* Activity log of LIFFireNet.forward(log=True) (models/model.py:188-205: per tensor
  * `l.detach().ne(0).float().mean()`): counts[i] = number of non-zero elements (NaN counts, -0 does
@@ -499,6 +504,11 @@ typedef struct {
     snnflow_unet_seg seg[SNNFLOW_UNET_MAX_SEGS];
     const uint16_t* w;  /* bf16 [3][ksize^2][kct][mpad][32] (snnflow_unet_prep_weights) */
     int kct, mpad;
+    int xparts;         /* 1: segments exact in bf16; 3: every segment is an fp32 tensor split into hi / mid /
+                           lo bf16 planes xpart elements apart (the 6 products above 2^-24 relative) */
+    int64_t xpart;
+    int pclass;         /* -1: all output pixels; 0..3: the parity class (py = pclass >> 1, px = pclass & 1) of
+                           a single MODE_T2 segment, whose taps of the other parities are skipped */
     int epi;            /* SNNFLOW_UNET_EPI_* */
     /* EPI_STORE */
     float* out; int ld; int accumulate;

@@ -2337,6 +2337,63 @@ int snnflow_slab_reduce(const snnflow_slab_desc* d, int n, int nblk, void* strea
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+// Large-vector form (the U-Net's ~20 M parameters): per-block fp64 partial sums of squares in a
+// fixed grid order, one block finishing the norm and the coefficient, a grid scaling the vector.
+constexpr int CLIP2_NB = 512;
+
+__global__ __launch_bounds__(256) void k_clip_partial(const float* __restrict__ g, int64_t n, double* partials) {
+    __shared__ double part[4];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const double v = g[i];
+        s += v * v;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) partials[blockIdx.x] = (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+__global__ void k_clip_coef(const double* partials, int nb, float max_norm, float eps, float* total_out, float* coef) {
+    if (threadIdx.x != 0) return;
+    double t = 0.0;
+    for (int i = 0; i < nb; ++i) t += partials[i];
+    const float total = (float)sqrt(t);
+    const float c = max_norm / (total + eps);
+    coef[0] = c < 1.0f ? c : 1.0f;
+    if (total_out) total_out[0] = total;
+}
+
+__global__ __launch_bounds__(256) void k_clip_scale(float* __restrict__ g, int64_t n, const float* coef) {
+    const float c = coef[0];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) g[i] = g[i] * c;
+}
+}  // namespace
+
+extern "C" {
+
+int snnflow_clip_grad_norm_large(float* g, int64_t n, float max_norm, float eps, float* total_out, double* scratch,
+                                 void* stream) {
+    if (!g || n < 0 || !scratch) SNN_FAIL(SNNFLOW_E_ARG, "clip_grad_norm_large: bad args");
+    const hipStream_t s = (hipStream_t)stream;
+    int64_t nb = (n + 255) / 256;
+    if (nb > CLIP2_NB) nb = CLIP2_NB;
+    if (nb < 1) nb = 1;
+    float* coef = reinterpret_cast<float*>(scratch + CLIP2_NB);
+    hipLaunchKernelGGL(k_clip_partial, dim3((unsigned)nb), dim3(256), 0, s, g, n, scratch);
+    hipLaunchKernelGGL(k_clip_coef, dim3(1), dim3(64), 0, s, scratch, (int)nb, max_norm, eps, total_out, coef);
+    int64_t gs = (n + 255) / 256;
+    if (gs > 4096) gs = 4096;
+    if (gs < 1) gs = 1;
+    hipLaunchKernelGGL(k_clip_scale, dim3((unsigned)gs), dim3(256), 0, s, g, n, coef);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
 int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float* total_out, void* stream) {
     if (!g || n < 0) SNN_FAIL(SNNFLOW_E_ARG, "clip_grad_norm: bad args");
     hipLaunchKernelGGL(k_clip_grad_norm, dim3(1), dim3(CLIP_NT), 0, (hipStream_t)stream, g, n, max_norm, eps, total_out);

@@ -75,32 +75,80 @@ __device__ inline int xcd_remap(int bid, int nblk) {
 // tap offset / stride / transposed stride) and the W chunk (nparts x BM x 32 bf16) are staged
 // through LDS; the next step's global loads are issued before this step's MFMAs.
 // ---------------------------------------------------------------------------------------------
-template <int WMT, int WAVES_M>
+template <int WMT, int WAVES_M, int XPARTS>
 struct ConvGeo {
     static constexpr int WAVES_N = 4 / WAVES_M;
     static constexpr int BM = 16 * WMT * WAVES_M;
     static constexpr int BN = 64 * WAVES_N;
-    static constexpr int XR = BN / 64;              // 16-B X pieces per thread and step
+    static constexpr int XR = BN / 64;              // 16-B X pieces per thread, plane and step
     static constexpr int WPIECES = 3 * BM * 4;      // 16-B W pieces per step (all parts)
     static constexpr int WR = (WPIECES + UNT - 1) / UNT;
 };
 
-template <int WMT, int WAVES_M>
+// Output-pixel domain of a conv launch: all pixels (pclass < 0) or one parity class of a
+// transposed stride-2 conv (output pixels (2yy + py, 2xx + px)), whose taps are then the
+// (ky, kx) with ky = (py + pad) mod 2 (+2 ...) -- the only taps that reach such a pixel.
+struct PixDom {
+    int cls, py, px, Hd, Wd, P;   // Hd x Wd: the domain's grid per image
+    int ky0, kx0, nty, ntx, kst;  // tap enumeration: ky = ky0 + kst * i (i < nty), likewise kx
+};
+
+__device__ inline PixDom pix_dom(const snnflow_unet_conv_args& a) {
+    PixDom d;
+    const int ks = a.ksize, pad = ks / 2;
+    d.cls = a.pclass;
+    if (d.cls < 0) {
+        d.py = d.px = 0;
+        d.Hd = a.Ho;
+        d.Wd = a.Wo;
+        d.ky0 = d.kx0 = 0;
+        d.nty = d.ntx = ks;
+        d.kst = 1;
+    } else {
+        d.py = d.cls >> 1;
+        d.px = d.cls & 1;
+        d.Hd = (a.Ho - d.py + 1) / 2;
+        d.Wd = (a.Wo - d.px + 1) / 2;
+        d.ky0 = (d.py + pad) & 1;
+        d.kx0 = (d.px + pad) & 1;
+        d.nty = (ks - d.ky0 + 1) / 2;
+        d.ntx = (ks - d.kx0 + 1) / 2;
+        d.kst = 2;
+    }
+    d.P = a.B * d.Hd * d.Wd;
+    return d;
+}
+
+// domain pixel n -> image, output row, output column
+__device__ inline void dom_pix(const PixDom& d, int n, int& b, int& y, int& x) {
+    const int xx = n % d.Wd, rest = n / d.Wd;
+    const int yy = rest % d.Hd;
+    b = rest / d.Hd;
+    y = d.cls < 0 ? yy : 2 * yy + d.py;
+    x = d.cls < 0 ? xx : 2 * xx + d.px;
+}
+
+// XPARTS == 1: X exact in bf16 (one plane), the weight parts of the segment (nparts) multiply it.
+// XPARTS == 3: X is an fp32 tensor as hi / mid / lo planes (a.xpart apart); the products above
+// 2^-24 relative are formed: X_hi x (W_hi, W_mid, W_lo), X_mid x (W_hi, W_mid), X_lo x W_hi.
+template <int WMT, int WAVES_M, int XPARTS>
 __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
-    using G = ConvGeo<WMT, WAVES_M>;
+    using G = ConvGeo<WMT, WAVES_M, XPARTS>;
     constexpr int BM = G::BM, BN = G::BN;
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[BN * XP];
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[XPARTS * BN * XP];
     __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * BM * XP];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave % WAVES_M, wn = wave / WAVES_M;
-    const int P = a.B * a.Ho * a.Wo;
+    const PixDom dom = pix_dom(a);
+    const int P = dom.P;
     const int mtiles = (a.M + BM - 1) / BM, ntiles = (P + BN - 1) / BN;
     const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
     const int m0 = (t % mtiles) * BM, n0 = (t / mtiles) * BN;
-    const int ks = a.ksize, taps = ks * ks, pad = ks / 2;
-    const int64_t wpart = (int64_t)taps * a.kct * a.mpad * 32;
+    const int ks = a.ksize, pad = ks / 2;
+    const int taps = dom.nty * dom.ntx;
+    const int64_t wpart = (int64_t)ks * ks * a.kct * a.mpad * 32;
 
     // this thread's X pieces: pixel (tid >> 2) + 64 r of the tile, 16-B piece q = tid & 3
     const int q = tid & 3;
@@ -110,18 +158,16 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
     for (int r = 0; r < G::XR; ++r) {
         const int n = n0 + (tid >> 2) + 64 * r;
         pv[r] = n < P;
-        const int nn = pv[r] ? n : 0;
-        px[r] = nn % a.Wo;
-        const int rest = nn / a.Wo;
-        py[r] = rest % a.Ho;
-        pb[r] = rest / a.Ho;
+        dom_pix(dom, pv[r] ? n : 0, pb[r], py[r], px[r]);
     }
 
-    uint4 xr[G::XR], wr[G::WR];
+    uint4 xr[XPARTS][G::XR], wr[G::WR];
     const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-    // global loads of one k-step (segment sg, tap, chunk kc) into registers
-    auto load = [&](const snnflow_unet_seg& sg, int tap, int kc) {
-        const int ky = tap / ks, kx = tap - ky * ks;
+    // global loads of one k-step (segment sg, tap index ti of the domain, chunk kc) into registers
+    auto load = [&](const snnflow_unet_seg& sg, int ti, int kc) {
+        const int ty_ = ti / dom.ntx;
+        const int ky = dom.ky0 + dom.kst * ty_, kx = dom.kx0 + dom.kst * (ti - ty_ * dom.ntx);
+        const int tap = ky * ks + kx;
         const int mode = sg.mode, H = sg.H, W = sg.W, cp = sg.cpitch;
 #pragma unroll
         for (int r = 0; r < G::XR; ++r) {
@@ -141,10 +187,13 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
             }
             ok = ok && iy >= 0 && iy < H && ix >= 0 && ix < W;
             const int64_t off = ok ? (((int64_t)pb[r] * H + iy) * W + ix) * cp + kc * 32 + q * 8 : 0;
-            xr[r] = ld16(sg.x + off);
-            if (!ok) xr[r] = z4;
+#pragma unroll
+            for (int xp = 0; xp < XPARTS; ++xp) {
+                xr[xp][r] = ld16(sg.x + xp * a.xpart + off);
+                if (!ok) xr[xp][r] = z4;
+            }
         }
-        const int np = sg.nparts;
+        const int np = XPARTS == 3 ? 3 : sg.nparts;
         const int64_t wbase = ((int64_t)(tap * a.kct + sg.kc0 + kc) * a.mpad + m0) * 32;
 #pragma unroll
         for (int r = 0; r < G::WR; ++r) {
@@ -157,8 +206,10 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
     };
     auto store = [&]() {
 #pragma unroll
-        for (int r = 0; r < G::XR; ++r)
-            *reinterpret_cast<uint4*>(&Xs[((tid >> 2) + 64 * r) * XP + q * 8]) = xr[r];
+        for (int xp = 0; xp < XPARTS; ++xp)
+#pragma unroll
+            for (int r = 0; r < G::XR; ++r)
+                *reinterpret_cast<uint4*>(&Xs[(xp * BN + (tid >> 2) + 64 * r) * XP + q * 8]) = xr[xp][r];
 #pragma unroll
         for (int r = 0; r < G::WR; ++r) {
             const int e = tid + r * UNT;
@@ -175,8 +226,8 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
 
-    // k-steps: segments (unrolled: constant kernarg indices), taps, 32-channel chunks; each step's
-    // successor is loaded before the step's MFMAs
+    // k-steps: segments (unrolled: constant kernarg indices), taps of the domain, 32-channel chunks;
+    // each step's successor is loaded before the step's MFMAs
     load(a.seg[0], 0, 0);
 #pragma unroll
     for (int s = 0; s < SNNFLOW_UNET_MAX_SEGS; ++s) {
@@ -193,35 +244,64 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
             } else if (s + 1 < SNNFLOW_UNET_MAX_SEGS && s + 1 < a.nseg) {
                 load(a.seg[s + 1 < SNNFLOW_UNET_MAX_SEGS ? s + 1 : s], 0, 0);
             }
-            bf16x8 bx[4];
+            if constexpr (XPARTS == 1) {
+                bf16x8 bx[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[(wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+                for (int j = 0; j < 4; ++j)
+                    bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[(wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
 #pragma unroll
-            for (int i = 0; i < WMT; ++i) {
-                const int row = wm * 16 * WMT + i * 16 + (lane & 15);
-                for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
-                    const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+                for (int i = 0; i < WMT; ++i) {
+                    const int row = wm * 16 * WMT + i * 16 + (lane & 15);
+                    for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
+                        const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
+                        for (int j = 0; j < 4; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < WMT; ++i) {
+                    const int row = wm * 16 * WMT + i * 16 + (lane & 15);
+                    bf16x8 aw[3];
+#pragma unroll
+                    for (int p = 0; p < 3; ++p)
+                        aw[p] = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int col = (wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8;
+                        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(&Xs[col]);
+                        const bf16x8 xm = *reinterpret_cast<const bf16x8*>(&Xs[BN * XP + col]);
+                        const bf16x8 xl = *reinterpret_cast<const bf16x8*>(&Xs[2 * BN * XP + col]);
+                        // smallest first: lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xl, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1], xm, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[2], xh, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xm, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1], xh, acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xh, acc[i][j], 0, 0, 0);
+                    }
                 }
             }
         }
     }
 
     // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of pixel n
-    const int64_t plane = (int64_t)P * a.M;
+    const int64_t Pfull = (int64_t)a.B * a.Ho * a.Wo;
+    const int64_t plane = Pfull * a.M;
 #pragma unroll
     for (int i = 0; i < WMT; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
-            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
-            if (n >= P || m >= a.M) continue;
+            const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
+            if (nd >= P || m >= a.M) continue;
+            int ob, oy, ox;
+            dom_pix(dom, nd, ob, oy, ox);
+            const int64_t n = ((int64_t)ob * a.Ho + oy) * a.Wo + ox;
             const fx4 v = acc[i][j];
             if (a.epi == SNNFLOW_UNET_EPI_STORE) {
-                float* o = a.out + (int64_t)n * a.ld + m;
+                float* o = a.out + n * a.ld + m;
                 if (m + 3 < a.M) {
                     float4 val = make_float4(v[0], v[1], v[2], v[3]);
                     if (a.accumulate) {
@@ -237,7 +317,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 continue;
             }
             // ConvLIF (spiking_submodules.py:121-151 / 265-300), M = hidden channels (multiple of 4)
-            const int64_t e0 = (int64_t)n * a.M + m;
+            const int64_t e0 = n * a.M + m;
             float vp[4] = {0.f, 0.f, 0.f, 0.f}, zp[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
             if (a.prev_state) {
                 const float4 tv = *reinterpret_cast<const float4*>(a.prev_state + e0);
@@ -246,11 +326,11 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 zp[0] = tz.x; zp[1] = tz.y; zp[2] = tz.z; zp[3] = tz.w;
             }
             if (a.residual) {
-                const uint2 rr = *reinterpret_cast<const uint2*>(a.residual + (int64_t)n * a.res_pitch + m);
+                const uint2 rr = *reinterpret_cast<const uint2*>(a.residual + n * a.res_pitch + m);
                 rs[0] = bf2f(rr.x & 0xffff); rs[1] = bf2f(rr.x >> 16); rs[2] = bf2f(rr.y & 0xffff); rs[3] = bf2f(rr.y >> 16);
             }
             float vo[4], zo[4];
-            uint16_t ob[4];
+            uint16_t ob16[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const float lam = 1.0f / (1.0f + expf(-a.leak[m + r]));
@@ -258,28 +338,47 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 vo[r] = a.hard_reset ? ((vp[r] * lam) * (1.0f - zp[r])) + ((1.0f - lam) * v[r])
                                      : ((vp[r] * lam) + ((1.0f - lam) * v[r])) - (zp[r] * th);
                 zo[r] = (vo[r] - th > 0.0f) ? 1.0f : 0.0f;
-                ob[r] = f2bf(a.residual ? zo[r] + rs[r] : zo[r]);
+                ob16[r] = f2bf(a.residual ? zo[r] + rs[r] : zo[r]);
             }
             *reinterpret_cast<float4*>(a.state + e0) = make_float4(vo[0], vo[1], vo[2], vo[3]);
             *reinterpret_cast<float4*>(a.state + plane + e0) = make_float4(zo[0], zo[1], zo[2], zo[3]);
             *reinterpret_cast<float4*>(a.current + e0) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<uint2*>(a.act + (int64_t)n * a.act_pitch + m) =
-                make_uint2((uint32_t)ob[0] | ((uint32_t)ob[1] << 16), (uint32_t)ob[2] | ((uint32_t)ob[3] << 16));
+            *reinterpret_cast<uint2*>(a.act + n * a.act_pitch + m) =
+                make_uint2((uint32_t)ob16[0] | ((uint32_t)ob16[1] << 16), (uint32_t)ob16[2] | ((uint32_t)ob16[3] << 16));
         }
 }
 
 // ---------------------------------------------------------------------------------------------
 // Weight gradient: D[k][m] = sum_pix X[gather(pix, tap)][k] * G[pix][m] with the pixel sum as the
-// GEMM K dimension (32 pixels per step): both operands are transposed into LDS ([k][pixel],
-// [m][pixel]); block tile 64 k x 64 m, 4 waves of 32 x 32; partial sums of a pixel range added to
-// dwk with fp32 atomics.
+// GEMM K dimension.  Both operands are NHWC (channel-contiguous), the MFMA wants 8 consecutive
+// pixels per lane: each thread loads 8x8 (pixel x channel) blocks with 16-B loads, transposes them
+// in registers (16-bit lane shuffles) and writes 16-B rows of [channel][pixel] LDS images.
+// Block tile 64 k x 64 m, 128 pixels per step (4 MFMA k-steps), 4 waves of 32 x 32; the partial
+// sums of a pixel range are added to dwk with fp32 atomics.
 // ---------------------------------------------------------------------------------------------
-constexpr int WG_BK = 64, WG_BM = 64;
+constexpr int WG_BK = 64, WG_BM = 64, WG_PS = 128, WG_PP = WG_PS + 8;
+
+// 8x8 transpose of 16-bit values: in[r] = channels 0..7 of pixel r -> out[c] = pixels 0..7 of channel c
+__device__ inline void transpose8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        uint32_t w[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4& a = in[2 * j];
+            const uint4& b = in[2 * j + 1];
+            const uint32_t wa = (c >> 1) == 0 ? a.x : ((c >> 1) == 1 ? a.y : ((c >> 1) == 2 ? a.z : a.w));
+            const uint32_t wb = (c >> 1) == 0 ? b.x : ((c >> 1) == 1 ? b.y : ((c >> 1) == 2 ? b.z : b.w));
+            w[j] = (c & 1) ? ((wa >> 16) | (wb & 0xffff0000u)) : ((wa & 0xffffu) | (wb << 16));
+        }
+        out[c] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
 
 __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, int ktiles, int mtiles, int nsplit,
                                                     int steps) {
-    __shared__ __attribute__((aligned(16))) __bf16 Xt[WG_BK * XP];
-    __shared__ __attribute__((aligned(16))) __bf16 Gt[3 * WG_BM * XP];
+    __shared__ __attribute__((aligned(16))) __bf16 Xt[WG_BK * WG_PP];
+    __shared__ __attribute__((aligned(16))) __bf16 Gt[3 * WG_BM * WG_PP];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wk = wave & 1, wmv = wave >> 1;
@@ -293,9 +392,13 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
     const int ks = a.ksize, pad = ks / 2, ky = tap / ks, kx = tap - ky * ks;
     const int P = a.B * a.Ho * a.Wo;
     const snnflow_unet_seg& sg = a.seg;
-    const int pl = tid >> 3, pq = tid & 7;  // this thread's pixel (of 32) and 8-channel piece
-    const int kk = kt * WG_BK + pq * 8, mm = mt * WG_BM + pq * 8;
     const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+
+    // staging units of this thread: unit u in [0, 512): u < 128 -> X block (pixel group u % 16,
+    // channel group u / 16); else G block (part, channel group, pixel group)
+    int ublk[2];
+    ublk[0] = tid;
+    ublk[1] = tid + 256;
 
     fx4 acc[2][2];
 #pragma unroll
@@ -303,65 +406,89 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 xr, gr[3];
+    uint4 rg[2][8];
     auto load = [&](int st) {
-        const int n = (split * steps + st) * 32 + pl;
-        bool ok = n < P;
-        const int nn = ok ? n : 0;
-        const int ox = nn % a.Wo, rest = nn / a.Wo, oy = rest % a.Ho, bb = rest / a.Ho;
-        int iy, ix;
-        if (sg.mode == SNNFLOW_UNET_MODE_S1) {
-            iy = oy + ky - pad;
-            ix = ox + kx - pad;
-        } else {
-            iy = 2 * oy + ky - pad;
-            ix = 2 * ox + kx - pad;
-        }
-        const bool okx = ok && kk < sg.cpitch && iy >= 0 && iy < sg.H && ix >= 0 && ix < sg.W;
-        xr = ld16(sg.x + (okx ? (((int64_t)bb * sg.H + iy) * sg.W + ix) * sg.cpitch + kk : 0));
-        if (!okx) xr = z4;
-        const bool okg = ok && mm < a.gpitch;
+        const int pbase = (split * steps + st) * WG_PS;
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-            gr[p] = ld16(a.g3 + (okg ? p * a.gpart + (int64_t)nn * a.gpitch + mm : 0));
-            if (!okg) gr[p] = z4;
+        for (int u = 0; u < 2; ++u) {
+            const int blk = ublk[u];
+            if (blk < 128) {  // X block
+                const int pg = blk & 15, cg = blk >> 4;
+                const int kk = kt * WG_BK + cg * 8;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int n = pbase + pg * 8 + r;
+                    bool ok = n < P && kk < sg.cpitch;
+                    const int nn = ok ? n : 0;
+                    const int ox = nn % a.Wo, rest = nn / a.Wo, oy = rest % a.Ho, bb = rest / a.Ho;
+                    const int iy = (sg.mode == SNNFLOW_UNET_MODE_S1 ? oy : 2 * oy) + ky - pad;
+                    const int ix = (sg.mode == SNNFLOW_UNET_MODE_S1 ? ox : 2 * ox) + kx - pad;
+                    ok = ok && iy >= 0 && iy < sg.H && ix >= 0 && ix < sg.W;
+                    rg[u][r] = ld16(sg.x + (ok ? (((int64_t)bb * sg.H + iy) * sg.W + ix) * sg.cpitch + kk : 0));
+                    if (!ok) rg[u][r] = z4;
+                }
+            } else {  // G block
+                const int gb = blk - 128;
+                const int pg = gb & 15, cg = (gb >> 4) & 7, part = gb >> 7;
+                const int mm = mt * WG_BM + cg * 8;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    const int n = pbase + pg * 8 + r;
+                    const bool ok = n < P && mm < a.gpitch;
+                    rg[u][r] = ld16(a.g3 + (ok ? part * a.gpart + (int64_t)n * a.gpitch + mm : 0));
+                    if (!ok) rg[u][r] = z4;
+                }
+            }
         }
     };
     auto store = [&]() {
-        uint16_t* xt = reinterpret_cast<uint16_t*>(Xt);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xt[(pq * 8 + j) * XP + pl] = h16(xr, j);
-        uint16_t* gt = reinterpret_cast<uint16_t*>(Gt);
+        for (int u = 0; u < 2; ++u) {
+            const int blk = ublk[u];
+            uint4 tr[8];
+            transpose8x8(rg[u], tr);
+            if (blk < 128) {
+                const int pg = blk & 15, cg = blk >> 4;
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+                for (int c = 0; c < 8; ++c) *reinterpret_cast<uint4*>(&Xt[(cg * 8 + c) * WG_PP + pg * 8]) = tr[c];
+            } else {
+                const int gb = blk - 128;
+                const int pg = gb & 15, cg = (gb >> 4) & 7, part = gb >> 7;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) gt[(p * WG_BM + pq * 8 + j) * XP + pl] = h16(gr[p], j);
+                for (int c = 0; c < 8; ++c)
+                    *reinterpret_cast<uint4*>(&Gt[(part * WG_BM + cg * 8 + c) * WG_PP + pg * 8]) = tr[c];
+            }
+        }
     };
 
-    const int total_steps = (P + 31) / 32;
+    const int total_steps = (P + WG_PS - 1) / WG_PS;
     const int st0 = split * steps;
     const int nst = st0 >= total_steps ? 0 : (total_steps - st0 < steps ? total_steps - st0 : steps);
-    if (nst > 0) load(0);
+    if (nst == 0) return;
+    load(0);
     for (int st = 0; st < nst; ++st) {
         __syncthreads();
         store();
         __syncthreads();
         if (st + 1 < nst) load(st + 1);
-        bf16x8 ax[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            ax[i] = *reinterpret_cast<const bf16x8*>(&Xt[(wk * 32 + i * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+        for (int kk = 0; kk < WG_PS / 32; ++kk) {
+            bf16x8 ax[2];
 #pragma unroll
-        for (int p = 2; p >= 0; --p)
+            for (int i = 0; i < 2; ++i)
+                ax[i] = *reinterpret_cast<const bf16x8*>(&Xt[(wk * 32 + i * 16 + (lane & 15)) * WG_PP + kk * 32 + (lane >> 4) * 8]);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const bf16x8 bg =
-                    *reinterpret_cast<const bf16x8*>(&Gt[(p * WG_BM + wmv * 32 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+            for (int p = 2; p >= 0; --p)
 #pragma unroll
-                for (int i = 0; i < 2; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bg, acc[i][j], 0, 0, 0);
-            }
+                for (int j = 0; j < 2; ++j) {
+                    const bf16x8 bg = *reinterpret_cast<const bf16x8*>(
+                        &Gt[(p * WG_BM + wmv * 32 + j * 16 + (lane & 15)) * WG_PP + kk * 32 + (lane >> 4) * 8]);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bg, acc[i][j], 0, 0, 0);
+                }
+        }
     }
-    if (nst == 0) return;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -818,13 +945,15 @@ int grid1d(int64_t n, int per, int cap) {
     return (int)g;
 }
 
-template <int WMT, int WM>
+template <int WMT, int WM, int XP_>
 int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
-    using G = ConvGeo<WMT, WM>;
-    const int P = a.B * a.Ho * a.Wo;
+    using G = ConvGeo<WMT, WM, XP_>;
+    int P = a.B * a.Ho * a.Wo;
+    if (a.pclass >= 0) P = a.B * ((a.Ho - (a.pclass >> 1) + 1) / 2) * ((a.Wo - (a.pclass & 1) + 1) / 2);
     const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN);
     if (nb > 0x7fffffff) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: grid too large");
-    hipLaunchKernelGGL((k_unet_conv<WMT, WM>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
+    if (nb == 0) return 0;
+    hipLaunchKernelGGL((k_unet_conv<WMT, WM, XP_>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -854,11 +983,18 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
     } else {
         SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: unknown epilogue");
     }
+    if (a->xparts != 1 && a->xparts != 3) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: xparts must be 1 or 3");
+    if (a->pclass >= 4 || (a->pclass >= 0 && (a->seg[0].mode != SNNFLOW_UNET_MODE_T2 || a->nseg != 1)))
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: parity classes are for one transposed stride-2 segment");
     const hipStream_t s = (hipStream_t)stream;
-    if (a->M > 64) return launch_conv<4, 2>(*a, s);
-    if (a->M > 32) return launch_conv<2, 2>(*a, s);
-    if (a->M > 16) return launch_conv<2, 1>(*a, s);
-    return launch_conv<1, 1>(*a, s);
+    if (a->xparts == 3) {  // input gradients: the fp32 gradient as three bf16 planes
+        if (a->M > 32) return launch_conv<2, 2, 3>(*a, s);
+        return launch_conv<2, 1, 3>(*a, s);
+    }
+    if (a->M > 64) return launch_conv<4, 2, 1>(*a, s);
+    if (a->M > 32) return launch_conv<2, 2, 1>(*a, s);
+    if (a->M > 16) return launch_conv<2, 1, 1>(*a, s);
+    return launch_conv<1, 1, 1>(*a, s);
 }
 
 int snnflow_unet_prep_weights(const float* w, int cout, int cin, int ksize, const int* kmap, int transpose, int flip,
@@ -883,9 +1019,9 @@ int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
     const int taps = a->ksize * a->ksize;
     const int ktiles = (a->seg.cpitch + WG_BK - 1) / WG_BK, mtiles = (a->M + WG_BM - 1) / WG_BM;
     const int64_t tiles = (int64_t)taps * ktiles * mtiles;
-    const int total_steps = (P + 31) / 32;
-    int nsplit = (int)((2048 + tiles - 1) / tiles);  // ~2048+ blocks
-    if (nsplit > total_steps / 4) nsplit = total_steps / 4;  // >= 4 steps (128 pixels) per block
+    const int total_steps = (P + WG_PS - 1) / WG_PS;
+    int nsplit = (int)((1024 + tiles - 1) / tiles);  // ~1024+ blocks
+    if (nsplit > total_steps / 4) nsplit = total_steps / 4;  // >= 4 steps (512 pixels) per block
     if (nsplit < 1) nsplit = 1;
     const int steps = (total_steps + nsplit - 1) / nsplit;
     hipLaunchKernelGGL(k_unet_wgrad, dim3((unsigned)(tiles * nsplit)), dim3(UNT), 0, (hipStream_t)stream, *a, ktiles,

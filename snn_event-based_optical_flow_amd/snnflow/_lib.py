@@ -175,7 +175,8 @@ class UNetSeg(ctypes.Structure):
 
 class UNetConvArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("Ho", I32), ("Wo", I32), ("M", I32), ("ksize", I32), ("nseg", I32),
-                ("seg", UNetSeg * UNET_MAX_SEGS), ("w", P), ("kct", I32), ("mpad", I32), ("epi", I32),
+                ("seg", UNetSeg * UNET_MAX_SEGS), ("w", P), ("kct", I32), ("mpad", I32), ("xparts", I32),
+                ("xpart", I64), ("pclass", I32), ("epi", I32),
                 ("out", P), ("ld", I32), ("accumulate", I32),
                 ("leak", P), ("thresh", P), ("hard_reset", I32), ("prev_state", P), ("residual", P),
                 ("res_pitch", I32), ("state", P), ("current", P), ("act", P), ("act_pitch", I32)]
@@ -224,6 +225,7 @@ EXPORTS = {
     "snnflow_iwe_interpolate_bwd": (I32, [P, P, I64, I32, I32, I32, I32, P, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
+    "snnflow_clip_grad_norm_large": (I32, [P, I64, F32, F32, P, P, P]),
     "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),
     "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),

@@ -79,6 +79,9 @@ class GradAllReduce:
             off += g.numel()
 
 
+_CLIP_SCRATCH = {}
+
+
 def clip_grad_norm_(params, max_norm, eps=1e-6):
     """torch.nn.utils.clip_grad_norm_ (2-norm) with the flat-buffer fast path: one
     norm and one scale over the engine's gradient buffer instead of per-tensor
@@ -88,11 +91,19 @@ def clip_grad_norm_(params, max_norm, eps=1e-6):
     if flat is None:
         return torch.nn.utils.clip_grad_norm_(params, max_norm)
     if flat.is_cuda and flat.dtype == torch.float32:
-        # one HIP launch: norm (fp64 accumulation) + scale in place
+        # one HIP launch: norm (fp64 accumulation) + scale in place; grid-wide for large vectors
         from . import _lib
         total = torch.empty((), device=flat.device)
-        _lib.call("clip_grad_norm", _lib.lib.snnflow_clip_grad_norm, flat.data_ptr(), flat.numel(), float(max_norm),
-                  float(eps), total.data_ptr(), _lib.stream_ptr(flat.device))
+        if flat.numel() <= (1 << 20):
+            _lib.call("clip_grad_norm", _lib.lib.snnflow_clip_grad_norm, flat.data_ptr(), flat.numel(), float(max_norm),
+                      float(eps), total.data_ptr(), _lib.stream_ptr(flat.device))
+        else:
+            scratch = _CLIP_SCRATCH.get(flat.device)
+            if scratch is None:
+                scratch = torch.empty(513, dtype=torch.float64, device=flat.device)
+                _CLIP_SCRATCH[flat.device] = scratch
+            _lib.call("clip_grad_norm_large", _lib.lib.snnflow_clip_grad_norm_large, flat.data_ptr(), flat.numel(),
+                      float(max_norm), float(eps), total.data_ptr(), scratch.data_ptr(), _lib.stream_ptr(flat.device))
         return total
     total = torch.linalg.vector_norm(flat, 2.0)  # host tensors (gloo tests): same math in torch
     coef = torch.clamp(max_norm / (total + eps), max=1.0)

@@ -381,7 +381,7 @@ def conv_lif(plan, B, Ho, Wo, acts, prev_state, residual, state, current, act_ou
             continue
         a.seg[n] = _unet_seg(act, sg.mode, sg.kc0)
         n += 1
-    a.nseg = n
+    a.nseg, a.xparts, a.pclass = n, 1, -1
     a.w, a.kct, a.mpad, a.epi = ptr(plan.wf), plan.kct, plan.mp, _lib.UNET_EPI_LIF
     m = plan.mod
     a.leak, a.thresh, a.hard_reset = ptr(m.leak), ptr(m.thresh), 1 if m.hard_reset else 0
@@ -400,19 +400,21 @@ def _conv_flops(plan, P_out, acts=None):
 
 
 def conv_dgrad(plan, sg, g3, B, Hi, Wi, out, ld, mvalid, accumulate, s):
-    """Input gradient of segment sg of a cell: transposed conv of the hi/mid/lo gradient planes
-    (nparts 3, 2, 1) into out [B*Hi*Wi][ld] (fp32)."""
+    """Input gradient of segment sg of a cell: transposed conv of the gradient held as hi/mid/lo
+    bf16 planes (xparts 3) into out [B*Hi*Wi][ld] (fp32).  A stride-2 segment's transposed conv
+    runs as four launches, one per output parity class, each over the taps that reach it."""
     a = _lib.UNetConvArgs()
     a.B, a.Ho, a.Wo, a.M, a.ksize = B, Hi, Wi, mvalid, plan.ks
-    mode = _lib.UNET_MODE_T2 if sg.mode == _lib.UNET_MODE_S2 else _lib.UNET_MODE_S1
-    for p in range(3):
-        a.seg[p] = _unet_seg(g3[p], mode, 0, 3 - p)
-    a.nseg = 3
+    t2 = sg.mode == _lib.UNET_MODE_S2
+    a.seg[0] = _unet_seg(g3[0], _lib.UNET_MODE_T2 if t2 else _lib.UNET_MODE_S1, 0, 3)
+    a.nseg, a.xparts, a.xpart = 1, 3, g3[0].numel()
     a.w, a.kct, a.mpad, a.epi = ptr(sg.wd), plan.gp // 32, sg.wd_mp, _lib.UNET_EPI_STORE
     a.out, a.ld, a.accumulate = ptr(out), ld, 1 if accumulate else 0
     Ho, Wo = g3.shape[2], g3.shape[3]
-    _lib.call("unet_dgrad", lib.snnflow_unet_conv, ctypes.byref(a), s,
-              work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
+    work = 2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps
+    for cls in (range(4) if t2 else (-1,)):
+        a.pclass = cls
+        _lib.call("unet_dgrad", lib.snnflow_unet_conv, ctypes.byref(a), s, work=work / 4 if t2 else work)
 
 
 def wgrad(plan, sg, g3, B, Ho, Wo, act, s):

@@ -268,3 +268,29 @@ def test_iwe_api_gradients_vs_oracle(dev):
     f2 = fl.to(dev).requires_grad_(True)
     _, wr = siwe.get_interpolation(ev.to(dev), f2, 1.0, [H, W], s, round_idx=True)
     assert not wr.requires_grad
+
+
+def test_clip_grad_norm_large_vs_torch(dev):
+    """The grid-wide clip (snnflow_clip_grad_norm_large, taken above 2^20 gradient floats: the U-Net's
+    ~20 M parameters) against torch.nn.utils.clip_grad_norm_ on the same gradients."""
+    from snnflow import dp
+
+    gen = torch.Generator().manual_seed(10)
+    shapes = [(512, 512, 3, 3), (77,), (1000, 1001), (2, 3)]
+    vals = [torch.randn(s, generator=gen) * 0.01 for s in shapes]
+    flat = torch.cat([v.reshape(-1) for v in vals]).to(dev)
+    ps, ref, off = [], [], 0
+    for v in vals:
+        p = torch.nn.Parameter(torch.zeros_like(v, device=dev))
+        p.grad = flat[off:off + v.numel()].view(v.shape)
+        off += v.numel()
+        ps.append(p)
+        q = torch.nn.Parameter(torch.zeros_like(v))
+        q.grad = v.clone()
+        ref.append(q)
+    assert flat.numel() > (1 << 20)
+    total = dp.clip_grad_norm_(ps, 1.0)
+    rtotal = torch.nn.utils.clip_grad_norm_(ref, 1.0)
+    np.testing.assert_allclose(total.item(), rtotal.item(), rtol=1e-5)
+    for p, q in zip(ps, ref):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), q.grad.numpy(), rtol=1e-5, atol=1e-9)
