@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=3, help="distinct synthetic batches cycled in HBM")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsals)")
+    p.add_argument("--dp-check", action="store_true",
+                   help="N>1 correctness check of this very step path (gloo rehearsal): the all-reduced "
+                        "gradient == the sum of the ranks' own gradients, parameters identical after the update")
     a = p.parse_args()
     unet = a.model == "SpikingRecEVFlowNet"
     for k, lif, un in (("channels", 8, 32), ("res", 128, 256), ("batch", 8, 16), ("T", 10, 20)):
@@ -242,6 +245,10 @@ def main():
 
     for i in range(2):  # graph warm replays
         step(i)
+    if args.dp_check:
+        _dp_check(world, rank, step_parts=(load_batch, graphs, fwd_bwd, sync_grads, update, opt), params=params)
+        dist.destroy_process_group()
+        return
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -296,6 +303,48 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _dp_check(world, rank, step_parts, params):
+    """One step of the N>1 path exactly as timed (graph 1: forward + backward; eager all-reduce;
+    graph 2: clip + Adam + state hand-over), checked: the all-reduced flat gradient equals the
+    SUM of every rank's own gradient (gathered through the host), and after the update every
+    rank holds the same parameters.  Rank 0 prints one JSON line."""
+    load_batch, graphs, fwd_bwd, sync_grads, update, opt = step_parts
+    load_batch(1)
+    if graphs:
+        graphs[0].replay()
+    else:
+        opt.zero_grad(set_to_none=True)
+        fwd_bwd()
+    torch.cuda.synchronize()
+    def grads():
+        return torch.cat([p.grad.detach().reshape(-1).cpu() for p in params])
+
+    local = grads()
+    sync_grads()
+    torch.cuda.synchronize()
+    reduced = grads()
+    locals_ = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(locals_, local)
+    want = locals_[0].double()
+    for t in locals_[1:]:
+        want = want + t.double()
+    err = float((reduced.double() - want).abs().max() / max(float(want.abs().max()), 1e-30))
+    distinct = float(max((t - locals_[0]).abs().max() for t in locals_[1:]))
+    if graphs:
+        graphs[1].replay()
+    else:
+        update()
+    torch.cuda.synchronize()
+    pflat = torch.cat([p.detach().reshape(-1).cpu() for p in params])
+    ps = [torch.empty_like(pflat) for _ in range(world)]
+    dist.all_gather(ps, pflat)
+    pdiff = float(max((t - ps[0]).abs().max() for t in ps[1:]))
+    if rank == 0:
+        print(json.dumps({"dp_check": {"world": world, "grad_numel": local.numel(), "allreduce_rel_err": err,
+                                       "ranks_local_grads_differ_by": distinct, "param_max_diff_after_update": pdiff}}),
+              flush=True)
 
 
 def _firenet_roofline(kern, model, args, B, R, T):

@@ -1,0 +1,38 @@
+"""The N>1 bench step path on the GPU (two graphs per step with the SUM all-reduce of the flat
+gradient buffer between them, bench.py step()), rehearsed with 2 fresh ranks sharing the box's
+one GPU over gloo (SNNFLOW_SHARE_GPU=1).  bench.py --dp-check replays one step exactly as timed
+and checks that the all-reduced gradient is the sum of the two ranks' own gradients (each rank
+draws its own synthetic stream, so they differ) and that after clip + Adam both ranks hold the
+same parameters.  The RCCL (nccl backend) path is the same code with another backend string; it
+runs only in the driver's 8-GPU scaling bench.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("extra", [[], ["--no-graph"]])
+def test_dp_step_two_ranks_shared_gpu(extra):
+    env = dict(os.environ, SNNFLOW_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    port = 29611 + len(extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--dist-backend", "gloo",
+           "--dp-check", "--batch", "2", "--pool", "2"] + extra
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, r.stdout[-2000:]
+    res = json.loads(lines[-1])["dp_check"]
+    print("\n[dp-check]", res)
+    assert res["world"] == 2
+    assert res["ranks_local_grads_differ_by"] > 0  # the ranks really saw different batches
+    assert res["allreduce_rel_err"] < 1e-6
+    assert res["param_max_diff_after_update"] == 0.0

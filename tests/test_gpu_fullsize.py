@@ -272,13 +272,16 @@ def test_iwe_api_gradients_vs_oracle(dev):
 
 def test_clip_grad_norm_large_vs_torch(dev):
     """The grid-wide clip (snnflow_clip_grad_norm_large, taken above 2^20 gradient floats: the U-Net's
-    ~20 M parameters) against torch.nn.utils.clip_grad_norm_ on the same gradients."""
+    ~20 M parameters) against the fp64 norm of the same gradients and torch.nn.utils.clip_grad_norm_.
+    The kernel sums squares in fp64, so it is compared with the fp64 truth at rtol 1e-6; torch's fp32
+    CPU norm of these 3.4 M floats is itself 3e-5 low (measured), hence rtol 1e-4 against torch."""
     from snnflow import dp
 
     gen = torch.Generator().manual_seed(10)
     shapes = [(512, 512, 3, 3), (77,), (1000, 1001), (2, 3)]
     vals = [torch.randn(s, generator=gen) * 0.01 for s in shapes]
     flat = torch.cat([v.reshape(-1) for v in vals]).to(dev)
+    truth = float(torch.cat([v.reshape(-1) for v in vals]).double().pow(2).sum().sqrt())
     ps, ref, off = [], [], 0
     for v in vals:
         p = torch.nn.Parameter(torch.zeros_like(v, device=dev))
@@ -291,6 +294,8 @@ def test_clip_grad_norm_large_vs_torch(dev):
     assert flat.numel() > (1 << 20)
     total = dp.clip_grad_norm_(ps, 1.0)
     rtotal = torch.nn.utils.clip_grad_norm_(ref, 1.0)
-    np.testing.assert_allclose(total.item(), rtotal.item(), rtol=1e-5)
-    for p, q in zip(ps, ref):
-        np.testing.assert_allclose(p.grad.cpu().numpy(), q.grad.numpy(), rtol=1e-5, atol=1e-9)
+    np.testing.assert_allclose(total.item(), truth, rtol=1e-6)
+    np.testing.assert_allclose(total.item(), rtotal.item(), rtol=1e-4)
+    coef = np.float32(1.0) / (np.float32(total.item()) + np.float32(1e-6))
+    for p, v in zip(ps, vals):
+        np.testing.assert_allclose(p.grad.cpu().numpy(), v.numpy() * coef, rtol=1e-6, atol=1e-12)
