@@ -36,5 +36,31 @@ def main(C=8, R=128, B=8, T=10, steps=3):
     torch.cuda.synchronize()
 
 
+def main_unet(R=256, B=16, T=20, base=32, steps=2):
+    """SpikingRecEVFlowNet (cfg5) eager train steps, the bench's unet mode without the graph."""
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    model = snnflow.SpikingRecEVFlowNet(train_snn_model_kwargs("SpikingRecEVFlowNet", base_num_channels=base)).to(dev)
+    cfg = {"loader": {"resolution": [R, R]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    lf = snnflow.EventWarping(cfg, dev)
+    opt = torch.optim.Adam(model.parameters(), lr=2e-4)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    wins = [make_window(B, 1000, R, R, gen, dev) for _ in range(T)]
+    for _ in range(steps):
+        lf.reset()
+        for w in wins:
+            out = model(w["event_voxel"], w["event_cnt"])
+            lf.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        lf().backward()
+        opt.step()
+        opt.zero_grad()
+        model.detach_states()
+    torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
-    main(*[int(a) for a in sys.argv[1:]])
+    if sys.argv[1:2] == ["unet"]:
+        main_unet(*[int(a) for a in sys.argv[2:]])
+    else:
+        main(*[int(a) for a in sys.argv[1:]])
