@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 15
+#define SNNFLOW_ABI_VERSION 16
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -601,6 +601,77 @@ int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, 
                           const float* g_full, const float* g_extra, int B, int h, int wd, int up, float* gpre,
                           float* g_x, int gx_pitch, double* acc, void* stream);
 int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Standalone BatchNorm2d over [P][C] channel-fastest rows (csrc/norm.hip): MPBN of the membrane
+ * (SNNtorch_spiking_submodules.py:66-121, applied at :313-317 / :558-562) and TEBN's inner BN
+ * (:18-63) when called as modules.  C must divide 256.  Train: fp64 batch sums (fixed-order
+ * partials), biased variance to normalise, unbiased variance into running_var with momentum,
+ * num_batches_tracked += 1; eval: running statistics.  save_mean / save_invstd [C] are written in
+ * both modes (the backward's inputs).  scratch: snnflow_bn_scratch_doubles(C) doubles.
+ * ------------------------------------------------------------------------------------------- */
+#define SNNFLOW_BN_PARTS 256
+typedef struct {
+    int64_t P;
+    int C;
+    int train;
+    const float* x;
+    float* y;
+    const float* weight;  /* [C] or NULL (affine off) */
+    const float* bias;    /* [C] or NULL */
+    float* running_mean;  /* [C] or NULL (track_running_stats=False; train only) */
+    float* running_var;
+    int64_t* num_batches_tracked; /* or NULL */
+    float momentum, eps;
+    float* save_mean;
+    float* save_invstd;
+    double* scratch;
+} snnflow_bn_fwd_args;
+int snnflow_bn_fwd(const snnflow_bn_fwd_args* a, void* stream);
+
+/* g_weight = sum g*xhat, g_bias = sum g (either NULL to skip); g_x (or NULL) = the BatchNorm input
+ * gradient (train: through the batch statistics; eval: weight*invstd*g). */
+typedef struct {
+    int64_t P;
+    int C;
+    int train;
+    const float* x;
+    const float* g;
+    const float* weight;
+    const float* save_mean;
+    const float* save_invstd;
+    float* g_x;
+    float* g_weight;
+    float* g_bias;
+    double* scratch;
+} snnflow_bn_bwd_args;
+int snnflow_bn_bwd(const snnflow_bn_bwd_args* a, void* stream);
+int snnflow_bn_scratch_doubles(int C);
+
+/* ConvLayer with a 1x1 kernel (models/submodules.py:16-113; LIFFireNet's pred, model.py:105-107,
+ * called as a module): out [B][cout][H][W] = act(W x + b), x of any strides (elements, b c h w).
+ * Backward: g_pre = g_out * act'(out) (from the output), g_x (if set, strides gxs) = W^T g_pre,
+ * g_w [cout][cin] / g_b [cout] (either NULL to skip) as fixed-order fp64 sums;
+ * scratch: SNNFLOW_BN_PARTS * cout * (cin + 1) doubles. */
+#define SNNFLOW_ACT_NONE 0
+#define SNNFLOW_ACT_TANH 1
+#define SNNFLOW_ACT_RELU 2
+#define SNNFLOW_ACT_SIGMOID 3
+#define SNNFLOW_PW_MAX_CIN 63
+#define SNNFLOW_PW_MAX_COUT 4
+typedef struct {
+    int B, H, W, cin, cout, act;
+    const float* x;
+    int64_t xs[4];
+    const float* w;
+    const float* b;
+    float* out;
+    float* g_x;
+    int64_t gxs[4];
+} snnflow_pointwise_args;
+int snnflow_pointwise_fwd(const snnflow_pointwise_args* a, void* stream);
+int snnflow_pointwise_bwd(const snnflow_pointwise_args* a, const float* g_out, int64_t gs_b, int64_t gs_c,
+                          float* g_w, float* g_b, double* scratch, void* stream);
 
 const char* snnflow_last_error(void);
 int snnflow_abi_version(void);

@@ -118,15 +118,49 @@ class LeakyRef(nn.Module):
 
 
 # ---------------------------------------------------------------------------
+# TEBN / MPBN (models/SNNtorch_spiking_submodules.py:18-121)
+# ---------------------------------------------------------------------------
+class TEBNRef(nn.Module):
+    """``TEBN`` (``:18-63``): ``BatchNorm2d(x) * p_t`` with ``p_t = p[t]`` for a valid step, else
+    ``p.mean(0)`` (the reference's cells never pass a step, ``models/model.py:172-180``)."""
+
+    def __init__(self, c, num_timesteps=4):
+        super().__init__()
+        self.bn = nn.BatchNorm2d(c, momentum=0.1, eps=1e-5)
+        self.p = nn.Parameter(torch.ones(num_timesteps, c, 1, 1))
+        self.num_timesteps = num_timesteps
+
+    def forward(self, x, timestep=None):
+        if timestep is not None and 0 <= timestep < self.num_timesteps:
+            pt = self.p[timestep:timestep + 1]
+        else:
+            pt = self.p.mean(dim=0, keepdim=True)
+        return self.bn(x) * pt
+
+
+class MPBNRef(nn.Module):
+    """``MPBN`` (``:66-95``): BatchNorm2d of the membrane."""
+
+    def __init__(self, c):
+        super().__init__()
+        self.bn = nn.BatchNorm2d(c, momentum=0.1, eps=1e-5)
+
+    def forward(self, mem):
+        return self.bn(mem)
+
+
+# ---------------------------------------------------------------------------
 # Cells
 # ---------------------------------------------------------------------------
 class SnnTorchCellRef(nn.Module):
     """``SNNtorch_ConvLIF`` (``SNNtorch_spiking_submodules.py:124-322``) and, with
     ``recurrent=True``, ``SNNtorch_ConvLIFRecurrent`` (``:324-567``), fp32 branch:
     conv3x3 (no bias) [+ conv3x3 of previous spikes] -> BatchNorm2d -> Leaky;
-    membrane detached, state = stack([mem, spk])."""
+    membrane detached, state = stack([mem, spk]).  ``tebn``: TEBN in place of the BatchNorm
+    (``:245-251``); ``mpbn``: state = stack([MPBN(mem), spk]) after the detach (``:313-317``)."""
 
-    def __init__(self, cin, c, k=3, recurrent=False, leak=(0.0, 1.0), thresh=(0.0, 0.8), hard_reset=True):
+    def __init__(self, cin, c, k=3, recurrent=False, leak=(0.0, 1.0), thresh=(0.0, 0.8), hard_reset=True,
+                 tebn=False, num_timesteps=4, mpbn=False):
         super().__init__()
         self.input_size, self.hidden_size, self.recurrent = cin, c, recurrent
         beta0 = torch.empty(c, 1, 1).uniform_(leak[0], leak[1])
@@ -138,7 +172,9 @@ class SnnTorchCellRef(nn.Module):
         nn.init.uniform_(self.ff.weight, -math.sqrt(1 / cin), math.sqrt(1 / cin))
         if recurrent:
             nn.init.uniform_(self.rec.weight, -math.sqrt(1 / c), math.sqrt(1 / c))
-        self.bn = nn.BatchNorm2d(c, momentum=0.1, eps=1e-5)
+        self.tebn = tebn
+        self.bn = TEBNRef(c, num_timesteps) if tebn else nn.BatchNorm2d(c, momentum=0.1, eps=1e-5)
+        self.mpbn = MPBNRef(c) if mpbn else None
 
     def forward(self, x, prev_state, residual=0, timestep=None):
         self.lif.threshold.data.clamp_(min=0.01)
@@ -146,10 +182,12 @@ class SnnTorchCellRef(nn.Module):
         if self.recurrent:
             prev_spk = torch.zeros_like(cur) if prev_state is None else prev_state[1]
             cur = cur + self.rec(prev_spk)
-        cur = self.bn(cur)
+        cur = self.bn(cur, timestep=timestep) if self.tebn else self.bn(cur)
         spk, mem = self.lif(cur, None if prev_state is None else prev_state[0])
         self.lif.detach_hidden()
         mem = mem.detach()
+        if self.mpbn is not None:
+            mem = self.mpbn(mem)
         return spk, torch.stack([mem, spk], dim=0)
 
 
@@ -242,8 +280,14 @@ class LIFFireNetRef(nn.Module):
         self.mask = unet_kwargs["mask_output"]
         c = unet_kwargs["base_num_channels"]
         k = unet_kwargs["kernel_size"]
+        tebn = unet_kwargs.get("tebn", {})  # models/model.py:74-81
+        nts = tebn.get("num_timesteps", 4) if isinstance(tebn, dict) else 4
+        tebn = tebn.get("enabled", False) if isinstance(tebn, dict) else bool(tebn)
+        mpbn = unet_kwargs.get("mpbn", {})
+        mpbn = mpbn.get("enabled", False) if isinstance(mpbn, dict) else bool(mpbn)
         for i, (cell, rec) in enumerate(self.spec):
-            setattr(self, cell, SnnTorchCellRef(self.num_bins if i == 0 else c, c, k, recurrent=rec))
+            setattr(self, cell, SnnTorchCellRef(self.num_bins if i == 0 else c, c, k, recurrent=rec, tebn=tebn,
+                                                num_timesteps=nts, mpbn=mpbn))
         self.pred = ConvLayerRef(c, 2, 1, activation="tanh", w_scale=0.01)
         self.num_recurrent_units = len(self.spec)
         self.reset_states()

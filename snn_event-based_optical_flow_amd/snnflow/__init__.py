@@ -6,6 +6,7 @@ Drop-in for the reference's ``models.model`` (LIFFireNet family), its spiking ce
 """
 from . import _lib  # noqa: F401  (loads libsnnflow.so or raises)
 from .cells import ConvLayer, Leaky, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
+from .norm import MPBN, TEBN
 from .convlif import ConvLIF, ConvLIFRecurrent
 from . import checkpoint, encodings  # noqa: F401  (checkpoint interchange, on-device event encodings)
 from .loss import EventWarping

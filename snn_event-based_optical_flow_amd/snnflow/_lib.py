@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 
 class Neuron(ctypes.Structure):
@@ -195,6 +195,27 @@ class UNetLifBwdArgs(ctypes.Structure):
                 ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P)]
 
 
+BN_PARTS = 256
+ACT = {None: 0, "tanh": 1, "relu": 2, "sigmoid": 3}
+PW_MAX_CIN, PW_MAX_COUT = 63, 4
+
+
+class BnFwdArgs(ctypes.Structure):
+    _fields_ = [("P", I64), ("C", I32), ("train", I32), ("x", P), ("y", P), ("weight", P), ("bias", P),
+                ("running_mean", P), ("running_var", P), ("num_batches_tracked", P), ("momentum", F32), ("eps", F32),
+                ("save_mean", P), ("save_invstd", P), ("scratch", P)]
+
+
+class BnBwdArgs(ctypes.Structure):
+    _fields_ = [("P", I64), ("C", I32), ("train", I32), ("x", P), ("g", P), ("weight", P), ("save_mean", P),
+                ("save_invstd", P), ("g_x", P), ("g_weight", P), ("g_bias", P), ("scratch", P)]
+
+
+class PointwiseArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("cout", I32), ("act", I32), ("x", P),
+                ("xs", I64 * 4), ("w", P), ("b", P), ("out", P), ("g_x", P), ("gxs", I64 * 4)]
+
+
 EXPORTS = {
     "snnflow_abi_version": (I32, []),
     "snnflow_last_error": (ctypes.c_char_p, []),
@@ -243,6 +264,11 @@ EXPORTS = {
     "snnflow_unet_pred_fwd": (I32, [P, I32, I32, P, P, I32, I32, I32, I32, P, P, P]),
     "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, P]),
     "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
+    "snnflow_bn_fwd": (I32, [ctypes.POINTER(BnFwdArgs), P]),
+    "snnflow_bn_bwd": (I32, [ctypes.POINTER(BnBwdArgs), P]),
+    "snnflow_bn_scratch_doubles": (I32, [I32]),
+    "snnflow_pointwise_fwd": (I32, [ctypes.POINTER(PointwiseArgs), P]),
+    "snnflow_pointwise_bwd": (I32, [ctypes.POINTER(PointwiseArgs), P, I64, I64, P, P, P, P]),
 }
 MAX_SLOT_TASKS = 4
 MAX_COUNT_TENSORS = 16

@@ -19,6 +19,7 @@ from . import _lib
 from ._lib import check, lib, ptr
 from .engine import (Workspace, _ptr_t, _x_strides, as_nhwc_state, empty_state,
                      neuron_struct)
+from .norm import MPBN, TEBN, MPBNStateFn, PointwiseFn
 
 
 class Leaky(nn.Module):
@@ -65,8 +66,6 @@ def _check_supported(kernel_size, stride, quantization_config, tebn, mpbn, norm,
         raise NotImplementedError("snnflow cells implement the reference's 3x3 / stride-1 convolutions")
     if quantization_config is not None and quantization_config.get("enabled", False):
         raise NotImplementedError("quantized (brevitas) cells are out of scope (DESIGN.md)")
-    if tebn or mpbn:
-        raise NotImplementedError("TEBN / MPBN (off in configs/train_SNN.yml) are not implemented yet")
     if norm is not None:
         raise NotImplementedError("norm='weight'/'group' variants are not implemented")
     if not detach:
@@ -77,7 +76,7 @@ class _SnnTorchCellBase(nn.Module):
     recurrent = False
 
     def _build(self, input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset,
-               stride=1):
+               stride=1, tebn=False, num_timesteps=4, mpbn=False):
         self.input_size, self.hidden_size = input_size, hidden_size
         pad = kernel_size // 2
         beta_init = torch.empty(hidden_size, 1, 1).uniform_(leak[0], leak[1])
@@ -93,22 +92,36 @@ class _SnnTorchCellBase(nn.Module):
         if self.recurrent:
             w_rec = math.sqrt(1 / hidden_size)
             nn.init.uniform_(self.rec.weight, -w_rec, w_rec)
-        self.bn = nn.BatchNorm2d(hidden_size, momentum=0.1, eps=1e-5)
-        self.tebn_enabled = False
-        self.mpbn_enabled = False
-        self.mpbn = None
+        # :245-263 / :469-487 -- TEBN in place of the BatchNorm, MPBN of the membrane
+        self.bn = TEBN(hidden_size, num_timesteps=num_timesteps, momentum=0.1, eps=1e-5) if tebn else \
+            nn.BatchNorm2d(hidden_size, momentum=0.1, eps=1e-5)
+        self.tebn_enabled = bool(tebn)
+        self.num_timesteps = num_timesteps
+        self.mpbn = MPBN(hidden_size, momentum=0.1, eps=1e-5) if mpbn else None
+        self.mpbn_enabled = bool(mpbn)
         self.detach = True
         self.exporting = False
 
+    @property
+    def batch_norm(self):
+        """The nn.BatchNorm2d of the input current (TEBN's inner one when TEBN is on)."""
+        return self.bn.bn if self.tebn_enabled else self.bn
+
     def forward(self, input_, prev_state, residual=0, timestep=None):
-        spk, state = CellFn.apply(self, input_, prev_state, *self._params())
+        spk, state = CellFn.apply(self, input_, prev_state, *self._params(timestep))
+        if self.mpbn_enabled:  # :313-317 / :558-562 (after the detach: no gradient into the LIF)
+            state = MPBNStateFn.apply(state, self.mpbn.bn.weight, self.mpbn.bn.bias, self.mpbn.bn)
         return spk, state
 
-    def _params(self):
+    def _params(self, timestep=None):
         ps = [self.ff.weight]
         if self.recurrent:
             ps.append(self.rec.weight)
-        return ps + [self.bn.weight, self.bn.bias, self.lif.beta, self.lif.threshold]
+        if self.tebn_enabled:  # BN(x) * p_t == BN with (weight * p_t, bias * p_t)
+            bw, bb = self.bn.affine(timestep)
+        else:
+            bw, bb = self.bn.weight, self.bn.bias
+        return ps + [bw, bb, self.lif.beta, self.lif.threshold]
 
 
 class SNNtorch_ConvLIF(_SnnTorchCellBase):
@@ -122,8 +135,8 @@ class SNNtorch_ConvLIF(_SnnTorchCellBase):
                  mpbn=False):
         super().__init__()
         _check_supported(kernel_size, stride, quantization_config, tebn, mpbn, norm, detach, activation)
-        self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset, stride)
-        self.num_timesteps = num_timesteps
+        self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset, stride,
+                    tebn, num_timesteps, mpbn)
 
 
 class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
@@ -139,14 +152,15 @@ class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
         _check_supported(kernel_size, 1, quantization_config, tebn, mpbn, norm, detach, activation)
         if input_size != hidden_size:
             raise NotImplementedError("recurrent cells with input_size != hidden_size are not compiled")
-        self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset)
-        self.num_timesteps = num_timesteps
+        self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset,
+                    1, tebn, num_timesteps, mpbn)
 
 
 class ConvLayer(nn.Module):
     """``models/submodules.py:ConvLayer`` (``:16-113``), fp32 branch, as used for
     LIFFireNet's ``pred`` (1x1, bias, tanh, ``w_scale`` init).  Inside LIFFireNet it
-    is fused into the last cell's LIF kernel; a standalone call uses torch's conv."""
+    is fused into the last cell's LIF kernel; a standalone call runs the HIP 1x1 kernel
+    (csrc/norm.hip, ``snnflow_pointwise_fwd/bwd``)."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride=1, activation="relu", norm=None,
                  BN_momentum=0.1, w_scale=None, quantization_config=None, exporting=False):
@@ -164,8 +178,11 @@ class ConvLayer(nn.Module):
         self.norm = norm
 
     def forward(self, x):
-        out = self.conv2d(x)
-        return self.activation(out) if self.activation is not None else out
+        if self.conv2d.kernel_size != (1, 1) or self.conv2d.stride != (1, 1):
+            raise NotImplementedError("ConvLayer: only the 1x1 prediction layer is implemented")
+        if self.activation_name not in _lib.ACT:
+            raise NotImplementedError(f"ConvLayer activation {self.activation_name!r}")
+        return PointwiseFn.apply(x.float(), self.conv2d.weight, self.conv2d.bias, self.activation_name)
 
 
 # ---------------------------------------------------------------------------
@@ -216,7 +233,7 @@ class CellFn(torch.autograd.Function):
         else:
             pn = as_nhwc_state(prev_state)
             mem, sp = pn[0], (pn[1] if cell.recurrent else None)
-        n = neuron_struct(cell)
+        n = neuron_struct(cell, params[-4], params[-3])
         y = torch.empty(B, H, W, C, device=dev)
         stats = torch.empty(2, C, device=dev)
         facc = ws.fwd_acc[0]
@@ -241,6 +258,7 @@ class CellFn(torch.autograd.Function):
         ctx.has_prev = prev_state is not None
         ctx.wbwd = (wff[1], wrec[1])
         ctx.wfwd = (wff[0], wrec[0])
+        ctx.bn_affine = (params[-4], params[-3])
         ctx.save_for_backward(x, y, stats, *(t for t in (mem, sp) if t is not None))
         ctx.set_materialize_grads(False)
         return spk, state
@@ -258,7 +276,7 @@ class CellFn(torch.autograd.Function):
         dev = x.device
         s = _lib.stream_ptr(dev)
         ws = _cell_ws(B, H, W, C, dev)
-        n = neuron_struct(cell)
+        n = neuron_struct(cell, *ctx.bn_affine)
         g_bw, g_bb = torch.empty(C, device=dev), torch.empty(C, device=dev)
         g_beta, g_th = torch.empty(C, device=dev), torch.empty(C, device=dev)
         ng = _lib.NeuronGrad(ptr(g_bw), ptr(g_bb), ptr(g_beta), ptr(g_th))
@@ -305,7 +323,7 @@ class CellFn(torch.autograd.Function):
         wa = _lib.WgradArgs()
         wa.B, wa.H, wa.W, wa.cin, wa.c, wa.nsteps, wa.accumulate = B, H, W, cin, C, 1, 0
         wa.rec = 1 if cell.recurrent else 0
-        wa.bn_weight, wa.slab_ff, wa.slab_rec = ptr(cell.bn.weight), ptr(slab_ff), _ptr_t(slab_rec)
+        wa.bn_weight, wa.slab_ff, wa.slab_rec = ptr(ctx.bn_affine[0]), ptr(slab_ff), _ptr_t(slab_rec)
         st = wa.steps[0]
         st.g_cur, st.y, st.stats, st.bnc = ptr(g_cur), ptr(y), ptr(stats), ptr(bnc)
         st.x = ptr(x)

@@ -51,11 +51,13 @@ def as_nhwc(t):
     return t.contiguous(memory_format=torch.channels_last).float()
 
 
-def neuron_struct(cell):
-    bn, lif = cell.bn, cell.lif
+def neuron_struct(cell, weight=None, bias=None):
+    """Neuron parameters of a cell for the kernels; weight/bias override the BatchNorm affine
+    parameters (TEBN folds its temporal weight into them, cells.py)."""
+    bn, lif = getattr(cell, "batch_norm", cell.bn), cell.lif
     train = bn.training or not bn.track_running_stats
     return _lib.Neuron(
-        ptr(bn.weight), ptr(bn.bias),
+        ptr(bn.weight if weight is None else weight), ptr(bn.bias if bias is None else bias),
         ptr(bn.running_mean) if bn.track_running_stats else None,
         ptr(bn.running_var) if bn.track_running_stats else None,
         ptr(bn.num_batches_tracked) if (bn.training and bn.track_running_stats) else None,

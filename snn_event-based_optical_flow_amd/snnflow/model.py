@@ -5,8 +5,9 @@ Same class names, constructor (``unet_kwargs`` dict of ``configs/train_SNN.yml``
 ``states`` / ``reset_states`` / ``detach_states`` / ``mask`` / ``init_cropping`` and
 ``forward(event_voxel, event_cnt, log, return_dict) -> {"flow": [B,2,H,W], "activity"}``.
 A forward call is one fused time step on the GPU (engine.FireNetStep).  If forward
-hooks are registered on a cell, the cells are called one by one instead (hooks see
-the reference's ``(spk, state)`` outputs).
+hooks are registered on a cell, or the cells carry TEBN / MPBN normalisation
+(``unet_kwargs["tebn"|"mpbn"]``, ``models/model.py:74-83``), the cells are called one by one
+instead (hooks see the reference's ``(spk, state)`` outputs).
 """
 import copy
 import ctypes
@@ -139,6 +140,12 @@ class _FireNetBase(BaseModel):
         mods = [getattr(self, n) for n, _ in self.layer_spec] + [self.pred]
         return any(m._forward_hooks or m._forward_pre_hooks for m in mods)
 
+    def _cellwise(self):
+        """Cells called one by one (each an autograd node on the HIP cell kernels): forward hooks
+        registered, or TEBN / MPBN cells (their extra normalisation sits between the fused kernels)."""
+        cells = [getattr(self, n) for n, _ in self.layer_spec]
+        return self._hooked() or any(c.tebn_enabled or c.mpbn_enabled for c in cells)
+
     def _input(self, event_voxel, event_cnt):
         if self.encoding == "voxel":
             x = event_voxel
@@ -168,7 +175,7 @@ class _FireNetBase(BaseModel):
             return []
         xs = [self._input(v, c) for v, c in pairs]
         eng = self.engine
-        if T == 1 or self._hooked() or not xs[0].is_cuda or not eng.sequence_ok(xs[0].shape[1]):
+        if T == 1 or self._cellwise() or not xs[0].is_cuda or not eng.sequence_ok(xs[0].shape[1]):
             outs = []
             for x in xs:  # already encoded / normalised: feed through the per-step path
                 outs.append(self._step(x, log))
@@ -200,7 +207,7 @@ class _FireNetBase(BaseModel):
         return out if return_dict else out["flow"][0]
 
     def _step(self, x, log):
-        if self._hooked():
+        if self._cellwise():
             h, outs = x, []
             for i, (name, _) in enumerate(self.layer_spec):
                 h, self._states[i] = getattr(self, name)(h, self._states[i])

@@ -179,9 +179,10 @@ def spiking_cells_case(ref_sub, out):
     np.savez_compressed(os.path.join(out, "spiking_cells_case.npz"), **rec)
 
 
-def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4, fname=None):
+def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4, fname=None, norm=False):
     """models/model.py LIFFireNet (reference wiring, conv, BN, states) with the
-    restated Leaky; T forwards + EventWarping + backward, train mode."""
+    restated Leaky; T forwards + EventWarping + backward, train mode.  norm: TEBN and MPBN
+    enabled (models/model.py:74-83) with their parameters perturbed from the ones/zeros init."""
     sys.path.insert(0, REPO)
     from oracle.lif_ref import make_unet_kwargs
 
@@ -190,7 +191,18 @@ def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4, fname=None
     H, W, B, N, T = 16, 16, 2, 128, 3
     kw = make_unet_kwargs(base_num_channels=C)
     kw["name"] = name
+    if norm:
+        kw["tebn"] = {"enabled": True, "num_timesteps": 4}
+        kw["mpbn"] = {"enabled": True}
     model = getattr(ref_model, name)(dict(kw))
+    if norm:
+        pg = torch.Generator().manual_seed(16)
+        with torch.no_grad():
+            for n, p in model.named_parameters():
+                if n.endswith("bn.p") or ".mpbn.bn.weight" in n:
+                    p.copy_(0.5 + torch.rand(p.shape, generator=pg))
+                elif ".mpbn.bn.bias" in n:
+                    p.copy_(0.4 * torch.rand(p.shape, generator=pg) - 0.2)
     model.train()
     config = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001,
               "overwrite_intermediate": False}, "model": {"mask_output": True}}
@@ -404,6 +416,13 @@ def main():
         liffirenet_case(ref_model, ref_flow, HERE, "LIFFireNet", 8, "liffirenet_c8_case.npz")
         print("liffirenet_c8 fixture written")
         return
+    if only == ["liffirenet_norm"]:  # TEBN + MPBN cells
+        import loss.flow as ref_flow
+        import models.model as ref_model
+        torch.set_num_threads(1)
+        liffirenet_case(ref_model, ref_flow, HERE, "LIFFireNet", 8, "liffirenet_norm_case.npz", norm=True)
+        print("liffirenet_norm fixture written")
+        return
     if only == ["unet"]:
         import loss.flow as ref_flow
         import models.model as ref_model
@@ -433,6 +452,7 @@ def main():
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 4)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet_short", 4)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 8, "liffirenet_c8_case.npz")
+    liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 8, "liffirenet_norm_case.npz", norm=True)
     ref_enc, ref_base = import_dataloader(ref_root)
     encodings_case(ref_enc, ref_base, out)
     eval_case(ref_flow, ref_iwe, out)

@@ -42,6 +42,8 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_flow_metrics_args": _lib.FlowMetricsArgs,
         "snnflow_unet_seg": _lib.UNetSeg, "snnflow_unet_conv_args": _lib.UNetConvArgs,
         "snnflow_unet_wgrad_args": _lib.UNetWgradArgs, "snnflow_unet_lif_bwd_args": _lib.UNetLifBwdArgs,
+        "snnflow_bn_fwd_args": _lib.BnFwdArgs, "snnflow_bn_bwd_args": _lib.BnBwdArgs,
+        "snnflow_pointwise_args": _lib.PointwiseArgs,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():
@@ -232,3 +234,20 @@ def test_event_warping_event_mask_shapes():
             assert torch.equal(ew.event_mask, want)
         else:
             assert torch.equal(ew.event_mask, masks[-1])
+
+
+def test_tebn_mpbn_model_loads_reference_state_dict_strict():
+    """LIFFireNet with TEBN + MPBN cells has the reference's parameter/buffer names
+    (bn.p, bn.bn.*, mpbn.bn.*): the reference model's state dict loads strict."""
+    import numpy as np
+    import torch
+    import snnflow
+    from oracle import lif_ref
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "liffirenet_norm_case.npz"))
+    kw = lif_ref.make_unet_kwargs(base_num_channels=int(g["C"]))
+    kw["tebn"], kw["mpbn"] = {"enabled": True, "num_timesteps": 4}, {"enabled": True}
+    model = snnflow.LIFFireNet(kw)
+    model.load_state_dict({k[3:]: torch.from_numpy(np.asarray(v)) for k, v in g.items() if k.startswith("p0.")},
+                          strict=True)
+    assert model.G1.tebn_enabled and model.G1.mpbn_enabled and model._cellwise()

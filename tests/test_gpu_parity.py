@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 GOLDEN_GRAD_TOL = 4e-6   # vs the reference-generated fixtures (fp32 CPU, oneDNN summation order);
                          # measured worst 1.5e-6 (head.lif.threshold, C=8)
 ORACLE_GRAD_TOL = 1e-5   # vs the CPU oracle on fresh inputs; measured worst 4.4e-6 (cell C=8 recurrent, ff.weight)
+NORM_GRAD_TOL = 1e-5     # TEBN + MPBN cells one by one vs their fixture; measured worst 4.2e-6 (G1.lif.beta)
 
 
 def _rel(a, b):
@@ -192,15 +193,18 @@ def test_cell_teacher_forced(dev, recurrent, C):
         _grad_check(f"cell C={C} rec={recurrent}", pairs, ORACLE_GRAD_TOL)
 
 
-def _run_golden_firenet(g, name, dev, seq=False):
+def _run_golden_firenet(g, name, dev, seq=False, norm=False, tol=GOLDEN_GRAD_TOL):
     """seq: the T windows through model.forward_sequence (wavefront launches; only the final
-    step's states are observable there) instead of T model() calls."""
+    step's states are observable there) instead of T model() calls.  norm: TEBN + MPBN cells."""
     import snnflow
     from oracle import lif_ref
 
     T, C = int(g["T"]), int(g["C"])
     H, W = list(g["res"])
-    model = getattr(snnflow, name)(lif_ref.make_unet_kwargs(base_num_channels=C)).to(dev).train()
+    kw = lif_ref.make_unet_kwargs(base_num_channels=C)
+    if norm:
+        kw["tebn"], kw["mpbn"] = {"enabled": True, "num_timesteps": 4}, {"enabled": True}
+    model = getattr(snnflow, name)(kw).to(dev).train()
     model.load_state_dict(_sd(g, "p0.", dev))
     cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
            "model": {"mask_output": True}}
@@ -223,7 +227,7 @@ def _run_golden_firenet(g, name, dev, seq=False):
     for n, p in model.named_parameters():
         assert p.grad is not None, n
     _grad_check(f"golden {name} C={C} seq={seq}", [(n, p.grad.cpu().numpy(), g[f"g.{n}"])
-                                                   for n, p in model.named_parameters()], GOLDEN_GRAD_TOL)
+                                                   for n, p in model.named_parameters()], tol)
     for k, v in model.state_dict().items():
         np.testing.assert_allclose(v.cpu().numpy(), g[f"p1.{k}"], rtol=1e-5, atol=1e-6, err_msg=k)
 
@@ -238,6 +242,99 @@ def test_liffirenet_short_vs_golden(golden, dev):
 
 def test_liffirenet_c8_vs_golden(golden, dev):
     _run_golden_firenet(golden("liffirenet_c8_case.npz"), "LIFFireNet", dev)
+
+
+def test_liffirenet_tebn_mpbn_vs_golden(golden, dev):
+    """TEBN + MPBN cells (SNNtorch_spiking_submodules.py:18-121; reference-generated fixture with
+    perturbed p and MPBN affine parameters): the cells run one by one on the HIP cell kernels with
+    the temporal weight folded into the BatchNorm affine and MPBN on the standalone BatchNorm kernel;
+    forward_sequence takes the same path."""
+    _run_golden_firenet(golden("liffirenet_norm_case.npz"), "LIFFireNet", dev, norm=True, tol=NORM_GRAD_TOL)
+    _run_golden_firenet(golden("liffirenet_norm_case.npz"), "LIFFireNet", dev, seq=True, norm=True, tol=NORM_GRAD_TOL)
+
+
+@pytest.mark.parametrize("C,train,affine", [(8, True, True), (32, True, True), (16, False, True), (4, True, False)])
+def test_batchnorm_rows_vs_torch(dev, C, train, affine):
+    """The standalone BatchNorm kernel (csrc/norm.hip) against torch.nn.BatchNorm2d in fp64 on the
+    same data: output, running statistics, num_batches_tracked and all gradients."""
+    from snnflow.norm import batch_norm_nchw
+
+    gen = torch.Generator().manual_seed(C)
+    x = torch.randn(3, C, 17, 23, generator=gen) * 2 + 0.5
+    gy = torch.randn(3, C, 17, 23, generator=gen)
+    bn = torch.nn.BatchNorm2d(C, affine=affine).to(dev)
+    ref = torch.nn.BatchNorm2d(C, affine=affine).double()
+    if affine:
+        with torch.no_grad():
+            w, b = torch.rand(C, generator=gen) + 0.5, torch.randn(C, generator=gen) * 0.1
+            bn.weight.copy_(w), bn.bias.copy_(b), ref.weight.copy_(w.double()), ref.bias.copy_(b.double())
+    with torch.no_grad():
+        rm, rv = torch.randn(C, generator=gen) * 0.1, torch.rand(C, generator=gen) + 0.5
+        bn.running_mean.copy_(rm), bn.running_var.copy_(rv), ref.running_mean.copy_(rm.double()), ref.running_var.copy_(rv.double())
+    bn.train(train)
+    ref.train(train)
+    xd = x.to(dev).requires_grad_(True)
+    xr = x.double().requires_grad_(True)
+    y = batch_norm_nchw(xd, bn)
+    yr = ref(xr)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
+    (y * gy.to(dev)).sum().backward()
+    (yr * gy.double()).sum().backward()
+    np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), rtol=1e-4, atol=1e-5)
+    if affine:
+        np.testing.assert_allclose(bn.weight.grad.cpu().numpy(), ref.weight.grad.numpy(), rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(bn.bias.grad.cpu().numpy(), ref.bias.grad.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(bn.running_mean.cpu().numpy(), ref.running_mean.numpy(), rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(bn.running_var.cpu().numpy(), ref.running_var.numpy(), rtol=1e-6, atol=1e-7)
+    assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked)
+
+
+def test_tebn_timestep_and_mpbn_threshold(dev):
+    """TEBN with an explicit time step (p[t], :56-57) and without (p.mean(0)), and MPBN's
+    get_effective_threshold in eval mode (:97-121), against the oracle restatement."""
+    import snnflow
+    from oracle.lif_ref import TEBNRef
+
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 8, 9, 10, generator=gen)
+    m = snnflow.TEBN(8, num_timesteps=4).to(dev)
+    r = TEBNRef(8, 4)
+    with torch.no_grad():
+        p = torch.rand(4, 8, 1, 1, generator=gen) + 0.5
+        m.p.copy_(p), r.p.copy_(p)
+    for t in (None, 2, 7):
+        m.zero_grad(), r.zero_grad()
+        y, yr = m(x.to(dev), timestep=t), r(x, timestep=t)
+        np.testing.assert_allclose(y.detach().cpu().numpy(), yr.detach().numpy(), rtol=1e-5, atol=1e-5)
+        (y * y).sum().backward()
+        (yr * yr).sum().backward()
+        np.testing.assert_allclose(m.p.grad.cpu().numpy(), r.p.grad.numpy(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(m.bn.weight.grad.cpu().numpy(), r.bn.weight.grad.numpy(), rtol=1e-4, atol=1e-5)
+    mp = snnflow.MPBN(8).to(dev).eval()
+    th = torch.rand(8, 1, 1, device=dev)
+    with torch.no_grad():
+        mp.bn.running_var.fill_(4.0), mp.bn.running_mean.fill_(0.5)
+    eff = mp.get_effective_threshold(th)
+    np.testing.assert_allclose(eff.cpu().numpy(), (th.view(1, 8, 1, 1) * np.sqrt(4.0 + 1e-5) + 0.5).cpu().numpy(), rtol=1e-6)
+
+
+def test_convlayer_pointwise_vs_golden(golden, dev):
+    """ConvLayer called as a module (1x1 + bias + tanh) on the HIP pointwise kernels against the
+    reference-generated fixture (models/submodules.py:16-113)."""
+    import snnflow
+
+    g = golden("convlayer_case.npz")
+    layer = snnflow.ConvLayer(6, 2, 1, activation="tanh", w_scale=0.3).to(dev)
+    with torch.no_grad():
+        layer.conv2d.weight.copy_(torch.from_numpy(g["w"]))
+        layer.conv2d.bias.copy_(torch.from_numpy(g["b"]))
+    x = torch.from_numpy(g["x"]).to(dev).requires_grad_(True)
+    y = layer(x)
+    np.testing.assert_allclose(y.detach().cpu().numpy(), g["y"], rtol=1e-6, atol=1e-7)
+    (y * torch.arange(y.numel(), device=dev).view_as(y).float()).sum().backward()
+    np.testing.assert_allclose(layer.conv2d.weight.grad.cpu().numpy(), g["gw"], rtol=1e-5)
+    np.testing.assert_allclose(layer.conv2d.bias.grad.cpu().numpy(), g["gb"], rtol=1e-5)
+    assert x.grad is not None and torch.isfinite(x.grad).all()
 
 
 @pytest.mark.parametrize("case,name", [("liffirenet_c8_case.npz", "LIFFireNet"),
