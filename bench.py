@@ -183,6 +183,9 @@ def main():
     def update():
         dp.clip_grad_norm_(params, 1.0)
         opt.step()
+        if args.no_graph:  # the reference loop's hand-over (train_flow.py:262-279)
+            model.detach_states()
+            return
         nonlocal state_bufs, state_flat
         states = get_states()
         if state_bufs is None:
@@ -252,6 +255,11 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    prof = None
+    if os.environ.get("SNNFLOW_BENCH_PROFILE") == "1":  # host-side profile of the timed loop (stderr)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
@@ -259,6 +267,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
     if world > 1:
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 16
+#define SNNFLOW_ABI_VERSION 17
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -601,6 +601,78 @@ int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, 
                           const float* g_full, const float* g_extra, int B, int h, int wd, int up, float* gpre,
                           float* g_x, int gx_pitch, double* acc, void* stream);
 int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Per-time-step driver of the LIFFireNet family (csrc/firenet_step.cpp, host code): one call
+ * launches the L+1 forward kernels of a time step (snnflow_conv_fwd x L + snnflow_lif_fwd), one
+ * call the L+1 backward kernels (snnflow_lif_bwd + snnflow_layer_bwd x L), one call the deferred
+ * weight gradients of a BPTT window (snnflow_wgrad per layer + snnflow_slab_reduce).  It replaces
+ * the Python argument building of the eager drop-in path (models/model.py:135-207 called once
+ * per window by train_flow.py:231-279); the kernels and their arguments are those of the
+ * single-kernel entry points above.  The plan holds what is constant across steps; the io
+ * structs what each step allocates.
+ * ------------------------------------------------------------------------------------------- */
+#define SNNFLOW_MAX_LAYERS 8
+typedef struct snnflow_firenet_plan {
+    int L, B, H, W, c, cin0;
+    int rec[SNNFLOW_MAX_LAYERS];
+    int train[SNNFLOW_MAX_LAYERS];          /* BatchNorm batch statistics (else running) */
+    snnflow_neuron n[SNNFLOW_MAX_LAYERS];
+    const float* wt_fwd_ff[SNNFLOW_MAX_LAYERS];
+    const float* wt_fwd_rec[SNNFLOW_MAX_LAYERS];
+    const float* wt_bwd_ff[SNNFLOW_MAX_LAYERS];
+    const float* wt_bwd_rec[SNNFLOW_MAX_LAYERS];
+    const uint16_t* wf_ff[SNNFLOW_MAX_LAYERS];   /* forward fragments (c = 16, 32) or NULL */
+    const uint16_t* wf_rec[SNNFLOW_MAX_LAYERS];
+    const uint16_t* wd_ff[SNNFLOW_MAX_LAYERS];   /* input-gradient fragments or NULL */
+    const uint16_t* wd_rec[SNNFLOW_MAX_LAYERS];
+    double* fwd_acc; int64_t fwd_acc_stride;     /* [L][stride] doubles, zero_n = stride */
+    double* bwd_acc; int64_t bwd_acc_stride;
+    const float* pred_w; const float* pred_b;
+    float* slab_ff[SNNFLOW_MAX_LAYERS];          /* per-block weight-gradient slabs */
+    float* slab_rec[SNNFLOW_MAX_LAYERS];
+    int nblk;
+} snnflow_firenet_plan;
+
+typedef struct snnflow_firenet_fwd_io {
+    const float* x; int64_t xs[4];               /* event tensor (strided b, c, h, w) */
+    float* ys;                                   /* [L][B][H][W][c] pre-BN currents */
+    float* stats;                                /* [L][2][c] */
+    float* states;                               /* [L][2][B][H][W][c] */
+    float* flow;                                 /* [B][2][H][W] */
+    const float* mem_in[SNNFLOW_MAX_LAYERS];     /* incoming membranes (NHWC) or NULL (zeros) */
+    const float* s_prev[SNNFLOW_MAX_LAYERS];     /* previous spikes of recurrent layers or NULL */
+} snnflow_firenet_fwd_io;
+int snnflow_firenet_fwd(const snnflow_firenet_plan* p, const snnflow_firenet_fwd_io* io, void* stream);
+
+typedef struct snnflow_firenet_bwd_io {
+    const float* ys; const float* stats; const float* flow;
+    const float* mem_in[SNNFLOW_MAX_LAYERS];
+    const float* g_state[SNNFLOW_MAX_LAYERS];    /* grads of the state outputs (NHWC states) or NULL */
+    const float* g_flow; int64_t gflow_sb, gflow_sc;
+    float* g_cur;                                /* [L][B][H][W][c] out */
+    float* bnc;                                  /* [L][2][c] out */
+    float* g_prev[SNNFLOW_MAX_LAYERS];           /* grads of the previous states or NULL */
+    int ext[SNNFLOW_MAX_LAYERS];                 /* previous state not produced by this model */
+    float* g_x; int64_t gxs[4];                  /* head input gradient or NULL */
+    snnflow_neuron_grad ng[SNNFLOW_MAX_LAYERS];
+    float* g_pred_w; float* g_pred_b;
+    int accumulate;                              /* add into the neuron / pred gradients */
+} snnflow_firenet_bwd_io;
+int snnflow_firenet_bwd(const snnflow_firenet_plan* p, const snnflow_firenet_bwd_io* io, void* stream);
+
+/* One time step's tensors for the deferred weight gradients (the backward's g_cur / bnc and the
+ * forward's ys / stats / states, the step's input and the previous spikes). */
+typedef struct snnflow_firenet_wgrad_step {
+    const float* g_cur; const float* bnc; const float* ys; const float* stats;
+    const float* x; int64_t xs[4];
+    const float* states;
+    const float* s_prev[SNNFLOW_MAX_LAYERS];
+} snnflow_firenet_wgrad_step;
+/* Weight gradients of every layer over nsteps steps (order as given) into the plan's slabs, then
+ * the fixed-order slab sums into g_ff[l] / g_rec[l]. */
+int snnflow_firenet_wgrad(const snnflow_firenet_plan* p, const snnflow_firenet_wgrad_step* steps, int nsteps,
+                          float* const* g_ff, float* const* g_rec, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Standalone BatchNorm2d over [P][C] channel-fastest rows (csrc/norm.hip): MPBN of the membrane

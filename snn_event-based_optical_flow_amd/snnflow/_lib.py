@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 
 class Neuron(ctypes.Structure):
@@ -195,6 +195,36 @@ class UNetLifBwdArgs(ctypes.Structure):
                 ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P)]
 
 
+MAX_LAYERS = 8
+PL = P * MAX_LAYERS
+
+
+class FireNetPlan(ctypes.Structure):
+    _fields_ = [("L", I32), ("B", I32), ("H", I32), ("W", I32), ("c", I32), ("cin0", I32),
+                ("rec", I32 * MAX_LAYERS), ("train", I32 * MAX_LAYERS), ("n", Neuron * MAX_LAYERS),
+                ("wt_fwd_ff", PL), ("wt_fwd_rec", PL), ("wt_bwd_ff", PL), ("wt_bwd_rec", PL),
+                ("wf_ff", PL), ("wf_rec", PL), ("wd_ff", PL), ("wd_rec", PL),
+                ("fwd_acc", P), ("fwd_acc_stride", I64), ("bwd_acc", P), ("bwd_acc_stride", I64),
+                ("pred_w", P), ("pred_b", P), ("slab_ff", PL), ("slab_rec", PL), ("nblk", I32)]
+
+
+class FireNetFwdIo(ctypes.Structure):
+    _fields_ = [("x", P), ("xs", I64 * 4), ("ys", P), ("stats", P), ("states", P), ("flow", P),
+                ("mem_in", PL), ("s_prev", PL)]
+
+
+class FireNetBwdIo(ctypes.Structure):
+    _fields_ = [("ys", P), ("stats", P), ("flow", P), ("mem_in", PL), ("g_state", PL),
+                ("g_flow", P), ("gflow_sb", I64), ("gflow_sc", I64), ("g_cur", P), ("bnc", P),
+                ("g_prev", PL), ("ext", I32 * MAX_LAYERS), ("g_x", P), ("gxs", I64 * 4),
+                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32)]
+
+
+class FireNetWgradStep(ctypes.Structure):
+    _fields_ = [("g_cur", P), ("bnc", P), ("ys", P), ("stats", P), ("x", P), ("xs", I64 * 4), ("states", P),
+                ("s_prev", PL)]
+
+
 BN_PARTS = 256
 ACT = {None: 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 PW_MAX_CIN, PW_MAX_COUT = 63, 4
@@ -264,6 +294,9 @@ EXPORTS = {
     "snnflow_unet_pred_fwd": (I32, [P, I32, I32, P, P, I32, I32, I32, I32, P, P, P]),
     "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, P]),
     "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
+    "snnflow_firenet_fwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetFwdIo), P]),
+    "snnflow_firenet_bwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), P]),
+    "snnflow_firenet_wgrad": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetWgradStep), I32, P, P, P]),
     "snnflow_bn_fwd": (I32, [ctypes.POINTER(BnFwdArgs), P]),
     "snnflow_bn_bwd": (I32, [ctypes.POINTER(BnBwdArgs), P]),
     "snnflow_bn_scratch_doubles": (I32, [I32]),
@@ -346,9 +379,15 @@ def ptr(t):
 
 
 def stream_ptr(device=None):
+    """Raw HIP stream of the current stream on `device` (torch's getter without the Stream object)."""
     if not torch.cuda.is_available():
         raise SnnflowError("snnflow kernels need a HIP device (none visible); there is no CPU fallback")
-    return torch.cuda.current_stream(device).cuda_stream
+    if isinstance(device, str):
+        device = torch.device(device)
+    idx = device.index if isinstance(device, torch.device) else device
+    if idx is None:
+        idx = torch.cuda.current_device()
+    return torch._C._cuda_getCurrentRawStream(idx)
 
 
 def require_device(t, name):

@@ -51,6 +51,22 @@ class Leaky(nn.Module):
         self.reset_mechanism = reset_mechanism
         self.mem = None
 
+    @property
+    def mem(self):
+        """Membrane cache (snntorch's ``Leaky.mem``).  The fused step leaves it as a lazy view spec
+        (storage, shape, strides, offset) into its state buffer: built on first read."""
+        lazy = self.__dict__.get("_mem_lazy")
+        if lazy is not None:
+            st, shape, stride, off = lazy
+            self.__dict__["_mem"] = st.as_strided(shape, stride, off).detach()
+            self.__dict__["_mem_lazy"] = None
+        return self.__dict__.get("_mem")
+
+    @mem.setter
+    def mem(self, value):
+        self.__dict__["_mem_lazy"] = None
+        self.__dict__["_mem"] = value
+
     def detach_hidden(self):
         if self.mem is not None:
             self.mem = self.mem.detach()

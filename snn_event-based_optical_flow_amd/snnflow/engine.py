@@ -115,14 +115,25 @@ class PreppedWeights:
         self.frag = {}   # i -> uint16 [snnflow_frag_halfs] forward-conv bf16 fragments (C = 16, 32) or None
         self.fragb = {}  # i -> the same for the input-gradient conv
         self.key = None
+        self.gen = 0  # bumped whenever the buffers are re-allocated
 
     def ensure(self, weights, thresholds, stream, refresh=True):
-        key = tuple((w.data_ptr(), w._version) for w in weights) + tuple((t.data_ptr(), t._version) for t in thresholds)
-        if key != self.key:
+        """`weights` / `thresholds` are the engine's cached lists (re-built when a parameter is replaced
+        or moved): a new list re-checks pointers and buffers, the same list only the version counters."""
+        ver = sum(w._version for w in weights) + sum(t._version for t in thresholds)
+        same = self.__dict__.get("src") is weights
+        if not same:
+            key = tuple((w.data_ptr(), w._version) for w in weights) + tuple((t.data_ptr(), t._version) for t in thresholds)
+            if key != self.key:
+                refresh = True
+            self.key = key
+            self.src = weights
+        elif ver != self.__dict__.get("ver"):
             refresh = True
-        self.key = key
+        self.ver = ver
         fresh = False
-        for i, w in enumerate(weights):
+        shapes = tuple((w.data_ptr(), w.numel()) for w in weights) if not same else self.shapes
+        for i, w in enumerate(weights if shapes != self.__dict__.get("shapes") else ()):
             f = self.fwd.get(i)
             if f is None or f.numel() != w.numel() or f.device != w.device:
                 self.fwd[i] = torch.empty(w.numel(), device=w.device)
@@ -132,6 +143,9 @@ class PreppedWeights:
                 self.frag[i] = torch.empty(nf, dtype=torch.int16, device=w.device) if nf else None
                 self.fragb[i] = torch.empty(nf, dtype=torch.int16, device=w.device) if nf else None
                 fresh = True
+        self.shapes = shapes
+        if fresh:
+            self.gen += 1
         if not (refresh or fresh):
             return
         descs = []
@@ -174,6 +188,34 @@ class FireNetEngine:
         self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
         self.seq_states = None
         self.prep_stale = True  # re-prepare weights at the next forward (set after each backward)
+        self.lifs = [c.lif for c in self.cells]
+        self.bns = [getattr(c, "batch_norm", c.bn) for c in self.cells]
+        self._plist = None     # cached param_list() (+ identity checks), see param_list
+        self._neurons = None   # cached neuron structs keyed by the BatchNorms' train flags
+
+    def __deepcopy__(self, memo):  # (copy.deepcopy(model)): ctypes caches are rebuilt, not copied
+        import copy
+        new = self.__class__.__new__(self.__class__)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            new.__dict__[k] = None if k in ("_neurons", "_plist", "_prep_ws", "_prep_map", "_plan", "_gviews", "_layout",
+                                            "_anchor") \
+                else copy.deepcopy(v, memo)
+        return new
+
+    def invalidate(self):
+        """Drop cached parameter lists / neuron structs (the model's _apply moved or replaced tensors)."""
+        self._plist = None
+        self._neurons = None
+        self._prep_ws = None
+
+    def neurons(self):
+        """neuron_struct of every cell, cached: the pointers only change when the model's tensors are
+        moved or replaced (_apply -> invalidate, or a Parameter re-assignment, caught by param_list)."""
+        key = tuple(bn.training for bn in self.bns)
+        if self._neurons is None or self._neurons[0] != key:
+            self._neurons = (key, [neuron_struct(c) for c in self.cells])
+        return self._neurons[1]
 
     def sequence_ok(self, cin0):
         """True if FireNetSequence's wavefront launches take this model (C = 8, cin0 2 or 4)."""
@@ -181,6 +223,27 @@ class FireNetEngine:
 
     # parameter order = Function input order after the states
     def param_list(self):
+        """Cached; re-validated per call by identity against the owning modules' _parameters dicts."""
+        pl = self._plist
+        if pl is not None and all(d.get(k) is v for d, k, v in pl[1]):
+            return pl[0]
+        ps = self._param_list()
+        checks = []
+        for cell, rec in zip(self.cells, self.rec):
+            checks.append((cell.ff._parameters, "weight", cell.ff.weight))
+            if rec:
+                checks.append((cell.rec._parameters, "weight", cell.rec.weight))
+            bn = getattr(cell, "batch_norm", cell.bn)
+            checks += [(bn._parameters, "weight", bn.weight), (bn._parameters, "bias", bn.bias),
+                       (cell.lif._parameters, "beta", cell.lif._parameters.get("beta")),
+                       (cell.lif._parameters, "threshold", cell.lif._parameters.get("threshold"))]
+        checks += [(self.pred._parameters, "weight", self.pred.weight), (self.pred._parameters, "bias", self.pred.bias)]
+        self._plist = (tuple(ps), checks)
+        self._neurons = None
+        self._prep_ws = None
+        return self._plist[0]
+
+    def _param_list(self):
         ps = []
         for cell, rec in zip(self.cells, self.rec):
             ps.append(cell.ff.weight)
@@ -198,12 +261,20 @@ class FireNetEngine:
         return self.ws
 
     def prep_weights(self, stream, refresh=True):
-        ws = []
-        for cell, rec in zip(self.cells, self.rec):
-            ws.append(cell.ff.weight)
-            if rec:
-                ws.append(cell.rec.weight)
-        self.prep.ensure(ws, [c.lif.threshold for c in self.cells], stream, refresh)
+        ws = self.__dict__.get("_prep_ws")
+        if ws is None or self._plist is None:  # conv weights in PreppedWeights order (param_list validates)
+            ws = []
+            for cell, rec in zip(self.cells, self.rec):
+                ws.append(cell.ff.weight)
+                if rec:
+                    ws.append(cell.rec.weight)
+            self._prep_ws = ws
+            self._prep_th = [c.lif.threshold for c in self.cells]
+            self._prep_map = None
+        self.prep.ensure(ws, self._prep_th, stream, refresh)
+        m = self._prep_map
+        if m is not None and m[0] == self.prep.gen:
+            return m[1], m[2]
         # map layer -> prepped buffers
         fwd, bwd, frag, fragb, i = [], [], [], [], 0
         for rec in self.rec:
@@ -218,19 +289,51 @@ class FireNetEngine:
             frag.append((ff[2], rc[2]))
             fragb.append((ff[3], rc[3]))
         self.frags, self.fragsb = frag, fragb
+        self._prep_map = (self.prep.gen, fwd, bwd)
         return fwd, bwd
 
-    def open_chain(self, device):
+    def flat_layout_for(self, params):
+        """[(offset, numel, shape)] of `params` packed back to back (the flat gradient buffer)."""
+        layout = self.__dict__.get("_layout")
+        if layout is None or layout[0] != [id(p) for p in params]:
+            lay, off = [], 0
+            for p in params:
+                lay.append((off, p.numel(), p.shape))
+                off += p.numel()
+            layout = ([id(p) for p in params], lay, off)
+            self._layout = layout
+        return layout[1]
+
+    def anchor(self, states):
+        """The ParamAnchor of the BPTT chain a step with previous `states` belongs to: the current
+        one if a recurrent state carries this engine's graph (the chain continues), else a new one
+        (None without autograd)."""
         params = self.param_list()
-        total = sum(p.numel() for p in params)
-        self.flat = torch.empty(total, device=device)
-        views, layout, off = [], [], 0
-        for p in params:
-            views.append(self.flat[off:off + p.numel()].view_as(p))
-            layout.append((off, p.numel(), p.shape))
-            off += p.numel()
-        self.flat_views = views
-        self.flat_layout = layout
+        if not torch.is_grad_enabled() or not any(p.requires_grad for p in params):
+            return None
+        cont = False
+        for p, rec in zip(states, self.rec):
+            if rec and p is not None and p.requires_grad and getattr(p.grad_fn, "eng", None) is self:
+                cont = True
+                break
+        a = self.__dict__.get("_anchor")
+        if not cont or a is None or a[0] is not params:
+            self._anchor = (params, ParamAnchor.apply(self, *params))
+        return self._anchor[1]
+
+    def prepped(self):
+        """The prepared weight buffers of the last forward (no re-validation: the backward of a step
+        runs on the weights its forward saw)."""
+        m = self.__dict__.get("_prep_map")
+        if m is None:
+            raise _lib.SnnflowError("backward before any forward of this model")
+        return m[1], m[2]
+
+    def open_chain(self, device):
+        self.flat_layout = self.flat_layout_for(self.param_list())
+        o, n, _ = self.flat_layout[-1]
+        self.flat = torch.empty(o + n, device=device)
+        self.flat_views = True  # (gradient destinations are addressed through flat_layout)
         self.bwd_open = True
 
     def launch_wgrad(self, l, B, H, W, cin0, ws, stream):
@@ -248,9 +351,9 @@ class FireNetEngine:
             a.exact_inputs = 1 if l > 0 else 0
             a.bn_weight = ptr(self.cells[l].bn.weight)
             a.slab_ff, a.slab_rec = ptr(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
-            for k, (gcur, bnc, ys, stats, x, states, s_prev) in enumerate(chunk):
+            for k, (gcur, bnc, ys, stats, x, states, s_prev, _) in enumerate(chunk):
                 st = a.steps[k]
-                st.g_cur, st.y, st.stats, st.bnc = ptr(gcur[l]), ptr(ys[l]), ptr(stats[l]), ptr(bnc[l])
+                st.g_cur, st.y, st.stats, st.bnc = gcur[l], ys[l], stats[l], bnc[l]
                 if l == 0:
                     st.x = ptr(x)
                     st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
@@ -264,30 +367,94 @@ class FireNetEngine:
         descs = []
         for l in range(self.L):
             gff, grec, _ = glayers[l]
-            descs.append(_lib.SlabDesc(ptr(ws.slab_ff[l]), ptr(gff), gff.numel()))
+            cin = self.cells[l].input_size
+            descs.append(_lib.SlabDesc(ptr(ws.slab_ff[l]), gff, self.C * cin * 9))
             if grec is not None:
-                descs.append(_lib.SlabDesc(ptr(ws.slab_rec[l]), ptr(grec), grec.numel()))
+                descs.append(_lib.SlabDesc(ptr(ws.slab_rec[l]), grec, self.C * self.C * 9))
         for i0 in range(0, len(descs), 16):
             chunk = (_lib.SlabDesc * len(descs[i0:i0 + 16]))(*descs[i0:i0 + 16])
             _lib.call("slab_reduce", lib.snnflow_slab_reduce, chunk, len(descs[i0:i0 + 16]), ws.nblk, stream)
 
-    def flush_weight_grads(self, B, H, W, cin0, ws, glayers, stream):
-        """All deferred weight gradients on `stream` (serial form of the root step's tail)."""
-        for l in range(self.L):
-            self.launch_wgrad(l, B, H, W, cin0, ws, stream)
-        self.launch_slab_reduce(ws, glayers, stream)
+    def flush_weight_grads(self, B, H, W, cin0, ws, glayers, stream, plan=None):
+        """All deferred weight gradients on `stream` (serial form of the root step's tail): one
+        snnflow_firenet_wgrad call given the step driver's plan, else (per-kernel timing) the
+        per-layer launches from Python."""
+        if plan is None or _lib.TIMER is not None:
+            for l in range(self.L):
+                self.launch_wgrad(l, B, H, W, cin0, ws, stream)
+            self.launch_slab_reduce(ws, glayers, stream)
+            self.pending = []
+            return
+        L = self.L
+        steps = (_lib.FireNetWgradStep * len(self.pending))()
+        for k, (gcur, bnc, ys, stats, x, states, s_prev, _) in enumerate(self.pending):
+            st = steps[k]
+            st.g_cur, st.bnc, st.ys, st.stats = gcur.base, bnc.base, ys.base, stats.base
+            st.x = x.data_ptr()
+            st.xs[0], st.xs[1], st.xs[2], st.xs[3] = x.stride()
+            st.states = states[0].data_ptr()
+            for l in range(L):
+                st.s_prev[l] = _ptr_t(s_prev[l])
+        gff = (ctypes.c_void_p * L)(*[glayers[l][0] for l in range(L)])
+        grec = (ctypes.c_void_p * L)(*[glayers[l][1] for l in range(L)])
+        _lib.call("firenet_wgrad", lib.snnflow_firenet_wgrad, ctypes.byref(plan), steps, len(self.pending), gff, grec,
+                  stream)
         self.pending = []
 
+    def plan(self, B, H, W, cin0, ws, wfwd, wbwd):
+        """The C step driver's constant arguments (snnflow_firenet_plan), cached per model state."""
+        neurons = self.neurons()
+        train = tuple(bn.training or not bn.track_running_stats for bn in self.bns)
+        key = (B, H, W, cin0, id(ws), ws.fwd_acc.data_ptr(), self.prep.gen, id(neurons), train,
+               self.pred.weight.data_ptr(), self.pred.bias.data_ptr())
+        pl = self.__dict__.get("_plan")
+        if pl is not None and pl[0] == key:
+            return pl[1]
+        L = self.L
+        if L > _lib.MAX_LAYERS:
+            raise _lib.SnnflowError(f"at most {_lib.MAX_LAYERS} layers")
+        p = _lib.FireNetPlan()
+        p.L, p.B, p.H, p.W, p.c, p.cin0 = L, B, H, W, self.C, cin0
+        for l in range(L):
+            p.rec[l] = 1 if self.rec[l] else 0
+            p.train[l] = 1 if train[l] else 0
+            p.n[l] = neurons[l]
+            p.wt_fwd_ff[l], p.wt_fwd_rec[l] = _ptr_t(wfwd[l][0]), _ptr_t(wfwd[l][1])
+            p.wt_bwd_ff[l], p.wt_bwd_rec[l] = _ptr_t(wbwd[l][0]), _ptr_t(wbwd[l][1])
+            p.wf_ff[l], p.wf_rec[l] = _ptr_t(self.frags[l][0]), _ptr_t(self.frags[l][1])
+            p.wd_ff[l], p.wd_rec[l] = _ptr_t(self.fragsb[l][0]), _ptr_t(self.fragsb[l][1])
+            p.slab_ff[l], p.slab_rec[l] = _ptr_t(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
+        p.fwd_acc, p.fwd_acc_stride = ws.fwd_acc.data_ptr(), ws.fwd_acc.stride(0)
+        p.bwd_acc, p.bwd_acc_stride = ws.bwd_acc.data_ptr(), ws.bwd_acc.stride(0)
+        p.pred_w, p.pred_b = ptr(self.pred.weight), ptr(self.pred.bias)
+        p.nblk = ws.nblk
+        self._plan = (key, p)
+        return p
+
     def grad_views(self):
-        """Per-layer gradient destinations inside the flat buffer."""
-        v = iter(self.flat_views)
+        """Per-layer gradient destinations inside the flat buffer (cached per chain)."""
+        gv = self.__dict__.get("_gviews")
+        if gv is not None and gv[0] is self.flat:
+            return gv[1]
+        gv = self._grad_views()
+        self._gviews = (self.flat, gv)
+        return gv
+
+    def _grad_views(self):
+        """(per layer: (dW_ff ptr, dW_rec ptr or None, NeuronGrad), pred dW ptr, pred db ptr) by offset
+        into the flat buffer (param_list order)."""
+        base = self.flat.data_ptr()
+        v = iter(self.flat_layout)
+
+        def nxt():
+            return base + 4 * next(v)[0]
         layers = []
         for rec in self.rec:
-            gff = next(v)
-            grec = next(v) if rec else None
-            gbw, gbb, gbeta, gth = next(v), next(v), next(v), next(v)
-            layers.append((gff, grec, _lib.NeuronGrad(ptr(gbw), ptr(gbb), ptr(gbeta), ptr(gth))))
-        gpw, gpb = next(v), next(v)
+            gff = nxt()
+            grec = nxt() if rec else None
+            gbw, gbb, gbeta, gth = nxt(), nxt(), nxt(), nxt()
+            layers.append((gff, grec, _lib.NeuronGrad(gbw, gbb, gbeta, gth)))
+        gpw, gpb = nxt(), nxt()
         return layers, gpw, gpb
 
 
@@ -303,12 +470,30 @@ def _spk_half(state_nhwc):
 
 
 
+class _Rows:
+    """Device pointers of t[0], t[1], ... by address arithmetic (indexing a tensor builds a view,
+    a few microseconds each; the eager per-step path needs ~100 of them per time step)."""
+    __slots__ = ("base", "step")
+
+    def __init__(self, t):
+        self.base = t.data_ptr()
+        self.step = t.stride(0) * t.element_size()
+
+    def __getitem__(self, i):
+        return self.base + i * self.step
+
+
+def _rows(t):
+    return t if isinstance(t, _Rows) else _Rows(t)
+
+
 # ---------------------------------------------------------------------------
 # Kernel arguments of one time step (shared by the per-step and the sequence Functions)
 # ---------------------------------------------------------------------------
 def _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, facc, neurons, train, wfwd, wbwd):
     """Forward kernel K_l (l < L) of one step: conv(head) for l == 0, else LIF(l-1) on the
     halo + conv(l).  facc[l]: layer l's BatchNorm batch-sum accumulator."""
+    ys, stats, facc = _rows(ys), _rows(stats), _rows(facc)
     a = _lib.ConvFwdArgs()
     a.B, a.H, a.W, a.c = B, H, W, eng.C
     if l == 0:
@@ -317,13 +502,13 @@ def _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, 
         a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
     else:
         a.cin, a.lif_in = eng.C, 1
-        a.prev_y, a.prev_mem = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1])
-        a.prev_acc, a.prev_stats = ptr(facc[l - 1]), ptr(stats[l - 1])
+        a.prev_y, a.prev_mem = ys[l - 1], _ptr_t(mem_in[l - 1])
+        a.prev_acc, a.prev_stats = facc[l - 1], stats[l - 1]
         a.prev, a.prev_state = neurons[l - 1], ptr(states[l - 1])
     a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), ptr(wfwd[l][1])
     a.wt_ff_t, a.wt_rec_t = ptr(wbwd[l][0]), ptr(wbwd[l][1])  # MFMA B operand layout
     a.s_prev = _ptr_t(s_prev[l])
-    a.y, a.acc = ptr(ys[l]), (ptr(facc[l]) if train[l] else None)
+    a.y, a.acc = ys[l], (facc[l] if train[l] else None)
     fr = getattr(eng, "frags", None)
     if fr is not None:  # pre-split bf16 fragments of the spike convs (C = 16, 32)
         a.wf_ff, a.wf_rec = _ptr_t(fr[l][0]), _ptr_t(fr[l][1])
@@ -333,9 +518,10 @@ def _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, 
 def _fwd_top_args(eng, B, H, W, ys, stats, states, mem_in, facc, neurons, flow):
     """Forward kernel K_L of one step: LIF of the last layer + pred."""
     L = eng.L
+    ys, stats, facc = _rows(ys), _rows(stats), _rows(facc)
     f = _lib.LifFwdArgs()
     f.B, f.H, f.W, f.c = B, H, W, eng.C
-    f.y, f.mem, f.acc, f.stats = ptr(ys[L - 1]), _ptr_t(mem_in[L - 1]), ptr(facc[L - 1]), ptr(stats[L - 1])
+    f.y, f.mem, f.acc, f.stats = ys[L - 1], _ptr_t(mem_in[L - 1]), facc[L - 1], stats[L - 1]
     f.n, f.state = neurons[L - 1], ptr(states[L - 1])
     f.pred_w, f.pred_b, f.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), ptr(flow)
     return f
@@ -345,15 +531,16 @@ def _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, g
     """Backward kernel of the top of one step: pred backward + LIF backward of layer L-1.
     g_flow: dL/dflow with unit W and channel-plane strides, or None."""
     top = eng.L - 1
+    ys, stats, gcur, bacc = _rows(ys), _rows(stats), _rows(gcur), _rows(bacc)
     b = _lib.LifBwdArgs()
     b.B, b.H, b.W, b.c = B, H, W, eng.C
-    b.y, b.mem, b.stats, b.n = ptr(ys[top]), _ptr_t(mem_in[top]), ptr(stats[top]), neurons[top]
+    b.y, b.mem, b.stats, b.n = ys[top], _ptr_t(mem_in[top]), stats[top], neurons[top]
     b.g_state = _ptr_t(gst[top])
     b.pred_w, b.flow = ptr(eng.pred.weight), ptr(flow)
     if g_flow is not None:
         b.g_flow, b.gflow_sb, b.gflow_sc = ptr(g_flow), g_flow.stride(0), g_flow.stride(1)
-    b.g_cur, b.g_mem = ptr(gcur[top]), _ptr_t(gmem[top])
-    b.acc = ptr(bacc[top])
+    b.g_cur, b.g_mem = gcur[top], _ptr_t(gmem[top])
+    b.acc = bacc[top]
     return b
 
 
@@ -362,12 +549,13 @@ def _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur
     """Backward kernel of layer l of one step: BN backward + dgrad of layer l's convs
     [+ LIF backward of layer l-1]; gx: input gradient of the head (l == 0) or None."""
     C, L = eng.C, eng.L
+    ys, stats, gcur, bacc, bnc = _rows(ys), _rows(stats), _rows(gcur), _rows(bacc), _rows(bnc)
     a = _lib.LayerBwdArgs()
     a.B, a.H, a.W, a.c = B, H, W, C
-    a.y, a.stats, a.g_cur, a.acc_in, a.n = ptr(ys[l]), ptr(stats[l]), ptr(gcur[l]), ptr(bacc[l]), neurons[l]
-    a.ng, a.accumulate, a.bnc_out = glayers[l][2], acc, ptr(bnc[l])
+    a.y, a.stats, a.g_cur, a.acc_in, a.n = ys[l], stats[l], gcur[l], bacc[l], neurons[l]
+    a.ng, a.accumulate, a.bnc_out = glayers[l][2], acc, bnc[l]
     if l == L - 1:
-        a.has_pred, a.g_pred_w, a.g_pred_b = 1, ptr(gpw), ptr(gpb)
+        a.has_pred, a.g_pred_w, a.g_pred_b = 1, gpw, gpb
     if eng.rec[l]:
         a.wt_bwd_rec, a.wt_fwd_rec = ptr(wbwd[l][1]), ptr(wfwd[l][1])
         if g_prev[l] is not None:
@@ -379,10 +567,10 @@ def _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur
     if l > 0:
         a.cin, a.lif_in = C, 1
         a.wt_bwd_ff, a.wt_fwd_ff = ptr(wbwd[l][0]), ptr(wfwd[l][0])
-        a.prev_y, a.prev_mem, a.prev_stats, a.prev = ptr(ys[l - 1]), _ptr_t(mem_in[l - 1]), ptr(stats[l - 1]), neurons[l - 1]
+        a.prev_y, a.prev_mem, a.prev_stats, a.prev = ys[l - 1], _ptr_t(mem_in[l - 1]), stats[l - 1], neurons[l - 1]
         a.prev_g_state = _ptr_t(gst[l - 1])
-        a.prev_g_cur, a.prev_g_mem = ptr(gcur[l - 1]), _ptr_t(gmem[l - 1])
-        a.acc_out = ptr(bacc[l - 1])
+        a.prev_g_cur, a.prev_g_mem = gcur[l - 1], _ptr_t(gmem[l - 1])
+        a.acc_out = bacc[l - 1]
     else:
         a.cin, a.lif_in = cin0, 0
         if gx is not None:
@@ -390,6 +578,54 @@ def _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur
             a.g_x = ptr(gx)
             a.gxs_b, a.gxs_c, a.gxs_h, a.gxs_w = _x_strides(gx)
     return a
+
+
+def _fwd_step_kernels(eng, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, flow, ws, wfwd, wbwd, s):
+    """The L+1 forward kernels of one step launched one by one (what snnflow_firenet_fwd does)."""
+    L = eng.L
+    neurons = eng.neurons()
+    train = [bn.training or not bn.track_running_stats for bn in eng.bns]
+    facc = _Rows(ws.fwd_acc)
+    zn = ws.fwd_acc.shape[1]
+    ys, stats = _Rows(ys), _Rows(stats)
+    # K0: conv(head)  (zeroes fwd_acc[L-1], consumed by the previous step's last kernel)
+    # K_l: LIF(l-1) on the halo + conv(l)  (zeroes fwd_acc[l-2], consumed by K_{l-1})
+    for l in range(L):
+        a = _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, facc, neurons, train, wfwd,
+                           wbwd)
+        if l == 0:
+            a.zero0, a.zero_n = facc[L - 1], zn
+        elif l >= 2:
+            a.zero0, a.zero_n = facc[l - 2], zn
+        _lib.call(f"conv_fwd[{l}]" if l else "conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
+    # K_L: LIF of the last layer + pred  (zeroes fwd_acc[L-2])
+    f = _fwd_top_args(eng, B, H, W, ys, stats, states, mem_in, facc, neurons, flow)
+    if L >= 2:
+        f.zero0, f.zero_n = facc[L - 2], zn
+    _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
+
+
+class ParamAnchor(torch.autograd.Function):
+    """One autograd node standing for all parameters of a FireNet model within one BPTT chain.
+
+    Every FireNetStep of the chain takes the anchor instead of the ~32 parameter tensors (the
+    per-call cost of an autograd Function grows with its inputs); the chain's root step returns
+    the engine's flat gradient buffer as the anchor's gradient, and this node hands out
+    per-parameter views of it -- fresh views, no other reference, which AccumulateGrad adopts as
+    ``.grad`` without a copy (all gradients then live in one flat buffer, dp.flat_grad_buffer)."""
+
+    @staticmethod
+    def forward(ctx, eng, *params):
+        ctx.layout = eng.flat_layout_for(params)
+        ctx.set_materialize_grads(False)
+        return torch.empty(ctx.layout[-1][0] + ctx.layout[-1][1], device=params[0].device)
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is None:
+            return (None,) * (1 + len(ctx.layout))
+        return (None, *[g[o:o + n].view(shp) if ctx.needs_input_grad[1 + i] else None
+                        for i, (o, n, shp) in enumerate(ctx.layout)])
 
 
 class FireNetStep(torch.autograd.Function):
@@ -404,74 +640,71 @@ class FireNetStep(torch.autograd.Function):
         ws = eng.workspace(B, H, W, dev)
         wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale)
         eng.prep_stale = False
-        cells = eng.cells
-
         ys = torch.empty(L, B, H, W, C, device=dev)
         stats = torch.empty(L, 2, C, device=dev)
         # all L states of the step in one allocation, back to back (a state hand-over, e.g. the
         # bench's graph-replay detach, is then a single contiguous copy)
         n1 = 2 * B * H * W * C
         st_all = torch.empty(L * n1, device=dev)
-        states = [st_all[l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
-                  for l in range(L)]
+        sst = nhwc_state_strides(B, C, H, W)
+        states = [st_all.as_strided((2, B, C, H, W), sst, l * n1) for l in range(L)]
         flow = torch.empty(B, 2, H, W, device=dev)
 
-        mem_in, s_prev, prev_nhwc = [], [], []
+        # incoming membranes / previous spikes as pointers; `keep` holds their tensors (the whole
+        # previous state, or the cell's membrane cache) for the backward and the deferred wgrad
+        mem_in, s_prev, keep = [], [], []
+        half = 4 * (n1 // 2)
         root = True
         ext = [False] * L  # prev state requiring grad that this engine did not produce
         for l in range(L):
             p = prev[l]
             if p is None:
-                cache = cells[l].lif.mem
-                mem_in.append(cache if (cache is not None and tuple(cache.shape) == (B, C, H, W)
-                                        and cache.device == dev) else None)
+                cache = eng.lifs[l].mem
+                ok = cache is not None and cache.shape == (B, C, H, W) and cache.device == dev
+                mem_in.append(cache.data_ptr() if ok else None)
                 s_prev.append(None)
-                prev_nhwc.append(None)
+                keep.append(cache if ok else None)
             else:
                 pn = as_nhwc_state(p)
-                prev_nhwc.append(pn)
-                mem_in.append(pn[0])
-                s_prev.append(pn[1] if eng.rec[l] else None)
+                base = pn.data_ptr()
+                mem_in.append(base)
+                s_prev.append(base + half if eng.rec[l] else None)
+                keep.append(pn)
                 ours = getattr(p.grad_fn, "eng", None) is eng
                 if eng.rec[l] and p.requires_grad and ours:
                     root = False
                 ext[l] = p.requires_grad and not ours
-        neurons = [neuron_struct(c) for c in cells]
-        train = [c.bn.training or not c.bn.track_running_stats for c in cells]
-        facc = ws.fwd_acc
-        zn = facc.shape[1]
+        ys_t, stats_t = ys, stats
+        plan = None if _lib.TIMER is not None else eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
         try:
-            # K0: conv(head)  (zeroes fwd_acc[L-1], consumed by the previous step's last kernel)
-            # K_l: LIF(l-1) on the halo + conv(l)  (zeroes fwd_acc[l-2], consumed by K_{l-1})
-            for l in range(L):
-                a = _fwd_conv_args(eng, l, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, facc, neurons,
-                                   train, wfwd, wbwd)
-                if l == 0:
-                    a.zero0, a.zero_n = ptr(facc[L - 1]), zn
-                elif l >= 2:
-                    a.zero0, a.zero_n = ptr(facc[l - 2]), zn
-                _lib.call(f"conv_fwd[{l}]" if l else "conv_fwd[0]", lib.snnflow_conv_fwd, ctypes.byref(a), s)
-            # K_L: LIF of the last layer + pred  (zeroes fwd_acc[L-2])
-            f = _fwd_top_args(eng, B, H, W, ys, stats, states, mem_in, facc, neurons, flow)
-            if L >= 2:
-                f.zero0, f.zero_n = ptr(facc[L - 2]), zn
-            _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
+            if plan is not None:  # one call of the C step driver
+                io = _lib.FireNetFwdIo()
+                io.x = x.data_ptr()
+                io.xs[0], io.xs[1], io.xs[2], io.xs[3] = x.stride()
+                io.ys, io.stats, io.states, io.flow = ys.data_ptr(), stats.data_ptr(), st_all.data_ptr(), flow.data_ptr()
+                for l in range(L):
+                    io.mem_in[l] = mem_in[l]
+                    io.s_prev[l] = s_prev[l]
+                _lib.call("firenet_fwd", lib.snnflow_firenet_fwd, ctypes.byref(plan), ctypes.byref(io), s)
+            else:  # per-kernel launches (KernelTimer attribution): the same kernels and arguments
+                _fwd_step_kernels(eng, B, H, W, cin0, x, ys, stats, states, mem_in, s_prev, flow, ws, wfwd, wbwd, s)
         except Exception:
             ws.reset_acc()
             raise
 
-        for l in range(L):
-            cells[l].lif.mem = states[l][0].detach()
+        mst = (H * W * C, 1, W * C, C)
+        for l in range(L):  # snn.Leaky's membrane cache, materialised on first read (cells.Leaky.mem)
+            eng.lifs[l].__dict__["_mem_lazy"] = (st_all, (B, C, H, W), mst, l * n1)
 
         ctx.eng = eng
         ctx.root = root
         ctx.ext = ext
         ctx.shape = (B, H, W, cin0)
         ctx.has_prev = [p is not None for p in prev]
-        ctx.has_mem = [m is not None for m in mem_in]
-        saved = [x, ys, stats, flow] + states
-        saved += [m for m in mem_in if m is not None]
-        saved += [sp for sp in s_prev if sp is not None]
+        ctx.keep = [k is not None for k in keep]
+        ctx.ptrs = (mem_in, s_prev)
+        saved = [x, ys_t, stats_t, flow] + states
+        saved += [k for k in keep if k is not None]
         ctx.save_for_backward(*saved)
         ctx.set_materialize_grads(False)
         return (flow, *states)
@@ -484,27 +717,22 @@ class FireNetStep(torch.autograd.Function):
         saved = list(ctx.saved_tensors)
         x, ys, stats, flow = saved[:4]
         states = saved[4:4 + L]
-        rest = saved[4 + L:]
-        mem_in = []
-        for l in range(L):
-            mem_in.append(rest.pop(0) if ctx.has_mem[l] else None)
-        s_prev = []
-        for l in range(L):
-            s_prev.append(rest.pop(0) if (ctx.has_prev[l] and eng.rec[l]) else None)
+        keep = saved[4 + L:]  # tensors behind the mem_in / s_prev pointers (alive while saved here)
+        mem_in, s_prev = ctx.ptrs
 
         dev = x.device
         s = _lib.stream_ptr(dev)
         ws = eng.workspace(B, H, W, dev)
-        wfwd, wbwd = eng.prep_weights(s, refresh=False)
+        wfwd, wbwd = eng.prepped()  # the buffers of the forward (same weights)
         if not eng.bwd_open:
             eng.open_chain(dev)
             acc = 0
         else:
             acc = 1
         glayers, gpw, gpb = eng.grad_views()
-        neurons = [neuron_struct(c) for c in eng.cells]
-        bacc = ws.bwd_acc
-        zn = bacc.shape[1]
+        neurons = eng.neurons()
+        bacc = _Rows(ws.bwd_acc)
+        zn = ws.bwd_acc.shape[1]
         gst = [as_nhwc_state(g) if g is not None else None for g in g_states]
         # gradients of the previous states: the spike half of recurrent cells (rec dgrad);
         # for states that did not come from this engine also the membrane half
@@ -521,31 +749,51 @@ class FireNetStep(torch.autograd.Function):
         gmem = [g_prev[l] if (g_prev[l] is not None and ctx.ext[l]) else None for l in range(L)]
 
         # per-step buffers kept until the deferred weight gradients run (root step)
-        gcur = torch.empty(L, B, H, W, C, device=dev)   # dL/d BN-output of every layer
-        bnc = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
-        eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev))
+        gcur_t = torch.empty(L, B, H, W, C, device=dev)   # dL/d BN-output of every layer
+        bnc_t = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
+        gcur, bnc, ys, stats = _Rows(gcur_t), _Rows(bnc_t), _Rows(ys), _Rows(stats)
+        # pending: row pointers for the deferred wgrad + the tensors behind them (kept alive)
+        eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev, (keep, gcur_t, bnc_t, saved)))
         # (the deferred weight gradients stay on this stream after the chain: a side stream
         # overlapping them with the root step's chain measured slower under graph replay,
         # 2.48 -> 2.72 ms per cfg2 train step)
         try:
-            # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
             if g_flow is not None and (g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32):
                 g_flow = g_flow.contiguous().float()
-            b = _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, gcur, gmem, bacc)
-            b.zero0, b.zero_n = ptr(bacc[0]), zn
-            _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
-
             gx = None
             if ctx.needs_input_grad[1]:
                 gx = torch.empty_like(x)
-            for l in range(L - 1, -1, -1):
-                a = _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur, gmem, bacc, bnc,
-                                    glayers, gpw, gpb, acc, wfwd, wbwd, g_prev, ctx.ext, gx)
-                if l + 1 <= L - 1:
-                    a.zero0, a.zero_n = ptr(bacc[l + 1]), zn
-                _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+            plan = None if _lib.TIMER is not None else eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
+            if plan is not None:  # one call of the C step driver
+                io = _lib.FireNetBwdIo()
+                io.ys, io.stats, io.flow = ys.base, stats.base, flow.data_ptr()
+                for l in range(L):
+                    io.mem_in[l] = mem_in[l]
+                    io.g_state[l] = _ptr_t(gst[l])
+                    io.g_prev[l] = _ptr_t(g_prev[l])
+                    io.ext[l] = 1 if ctx.ext[l] else 0
+                    io.ng[l] = glayers[l][2]
+                if g_flow is not None:
+                    io.g_flow, io.gflow_sb, io.gflow_sc = g_flow.data_ptr(), g_flow.stride(0), g_flow.stride(1)
+                io.g_cur, io.bnc = gcur.base, bnc.base
+                if gx is not None:
+                    io.g_x = gx.data_ptr()
+                    io.gxs[0], io.gxs[1], io.gxs[2], io.gxs[3] = gx.stride()
+                io.g_pred_w, io.g_pred_b, io.accumulate = gpw, gpb, acc
+                _lib.call("firenet_bwd", lib.snnflow_firenet_bwd, ctypes.byref(plan), ctypes.byref(io), s)
+            else:  # per-kernel launches (KernelTimer attribution): the same kernels and arguments
+                # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
+                b = _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, gcur, gmem, bacc)
+                b.zero0, b.zero_n = bacc[0], zn
+                _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
+                for l in range(L - 1, -1, -1):
+                    a = _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur, gmem, bacc, bnc,
+                                        glayers, gpw, gpb, acc, wfwd, wbwd, g_prev, ctx.ext, gx)
+                    if l + 1 <= L - 1:
+                        a.zero0, a.zero_n = bacc[l + 1], zn
+                    _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
             if ctx.root:
-                eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s)
+                eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
         except Exception:
             ws.reset_acc()
             eng.bwd_open = False
@@ -553,20 +801,23 @@ class FireNetStep(torch.autograd.Function):
             eng.prep_stale = True
             raise
 
-        grads = [None] * len(eng.flat_layout)
+        g_anchor = None
         if ctx.root:
-            # fresh views, no other reference: AccumulateGrad adopts them as .grad
-            # instead of copying (all gradients then live in one flat buffer)
-            grads = [eng.flat[o:o + n].view(shp) for o, n, shp in eng.flat_layout]
+            # the whole flat gradient buffer to the chain's parameter anchor (ParamAnchor splits it
+            # into per-parameter views once every step of the chain is done)
+            g_anchor = eng.flat if ctx.needs_input_grad[2 + L] else None
             eng.flat_views = None
             eng.bwd_open = False
             eng.last_flat = eng.flat
             eng.prep_stale = True
-        return (None, gx, *g_prev, *grads)
+        return (None, gx, *g_prev, g_anchor)
 
 
 def _ptr_t(t):
-    return None if t is None else t.data_ptr()
+    """Device pointer of a tensor, an int pointer passed through, None -> NULL."""
+    if t is None or isinstance(t, int):
+        return t
+    return t.data_ptr()
 
 
 # ---------------------------------------------------------------------------
@@ -643,8 +894,8 @@ class FireNetSequence(torch.autograd.Function):
                 ext[l] = p.requires_grad and not ours
         mem_in = [mem0] + [[states[t - 1][l][0] for l in range(L)] for t in range(1, T)]
         s_prev = [sprev0] + [[states[t - 1][l][1] if eng.rec[l] else None for l in range(L)] for t in range(1, T)]
-        neurons = [neuron_struct(c) for c in cells]
-        train = [c.bn.training or not c.bn.track_running_stats for c in cells]
+        neurons = eng.neurons()
+        train = [bn.training or not bn.track_running_stats for bn in eng.bns]
 
         for tasks in wavefront_slots(T, L + 1):
             convs, top = [], None
@@ -703,7 +954,7 @@ class FireNetSequence(torch.autograd.Function):
         if fresh:
             eng.open_chain(dev)
         glayers, gpw, gpb = eng.grad_views()
-        neurons = [neuron_struct(c) for c in eng.cells]
+        neurons = eng.neurons()
         bacc = torch.zeros(T, L, _lib.acc_storage(_lib.bwd_acc_len(C)), dtype=torch.float64, device=dev)
         gcur = torch.empty(T, L, B, H, W, C, device=dev)
         bnc = torch.empty(T, L, 2, C, device=dev)
@@ -738,7 +989,8 @@ class FireNetSequence(torch.autograd.Function):
 
         # the deferred weight gradients see the steps in the per-step path's order (last first)
         for t in range(T - 1, -1, -1):
-            eng.pending.append((gcur[t], bnc[t], ys[t], stats[t], xs[t], states[t], s_prev[t]))
+            eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys[t]), _Rows(stats[t]), xs[t], states[t], s_prev[t],
+                                (gcur, bnc, ys, stats)))
         try:
             # backward kernel j of step t: j = 0 top (pred + LIF of layer L-1), j >= 1 layer L-j;
             # in reversed time tau = T-1-t the dependencies have the forward's shape

@@ -109,9 +109,10 @@ class EventWarping(torch.nn.Module):
         self.reset()
 
     def reset(self):
-        self._passes = 0
-        self._events, self._pols, self._masks, self._flows = [], [], [], []
-        self._final_flow = None
+        d = self.__dict__  # plain attributes (Module.__setattr__ skipped: once per window matters)
+        d["_passes"] = 0
+        d["_events"], d["_pols"], d["_masks"], d["_flows"] = [], [], [], []
+        d["_final_flow"] = None
 
     @property
     def num_events(self):
@@ -135,7 +136,7 @@ class EventWarping(torch.nn.Module):
         self._pols.append(pol_mask.float().contiguous())
         self._masks.append(event_mask.float())
         self._flows.append(list(flow_list))
-        self._passes += 1
+        self.__dict__["_passes"] += 1
 
     def overwrite_intermediate_flow(self, flow_list):
         """``loss/flow.py:123-150``: every window uses the final flow estimate."""

@@ -136,15 +136,27 @@ class _FireNetBase(BaseModel):
     def init_cropping(self, width, height):
         pass
 
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        if self._engine is not None:  # tensors moved or replaced: drop cached pointers
+            self._engine.invalidate()
+        return out
+
+    def _mods(self):
+        """The cells + pred (cached module list; submodules are not re-assigned)."""
+        m = self.__dict__.get("_mods_cache")
+        if m is None:
+            m = [getattr(self, n) for n, _ in self.layer_spec] + [self.pred]
+            self.__dict__["_mods_cache"] = m
+        return m
+
     def _hooked(self):
-        mods = [getattr(self, n) for n, _ in self.layer_spec] + [self.pred]
-        return any(m._forward_hooks or m._forward_pre_hooks for m in mods)
+        return any(m._forward_hooks or m._forward_pre_hooks for m in self._mods())
 
     def _cellwise(self):
         """Cells called one by one (each an autograd node on the HIP cell kernels): forward hooks
         registered, or TEBN / MPBN cells (their extra normalisation sits between the fused kernels)."""
-        cells = [getattr(self, n) for n, _ in self.layer_spec]
-        return self._hooked() or any(c.tebn_enabled or c.mpbn_enabled for c in cells)
+        return self._hooked() or any(c.tebn_enabled or c.mpbn_enabled for c in self._mods()[:-1])
 
     def _input(self, event_voxel, event_cnt):
         if self.encoding == "voxel":
@@ -215,12 +227,14 @@ class _FireNetBase(BaseModel):
             flow = self.pred(h)
         else:
             eng = self.engine
-            res = FireNetStep.apply(eng, x, *self._states, *eng.param_list())
+            res = FireNetStep.apply(eng, x, *self._states, eng.anchor(self._states))
             flow, new_states = res[0], list(res[1:])
-            self._states = new_states
-            outs = [st[1] for st in new_states]
+            self.__dict__["_states"] = new_states  # (plain attribute; skips Module.__setattr__)
+            outs = None
         activity = None
         if isinstance(log, bool) and log and not self.exporting:
+            if outs is None:
+                outs = [st[1] for st in new_states]
             activity = activity_log(self._activity_names(), [x] + outs + [flow])
         return {"flow": [flow], "activity": activity}
 

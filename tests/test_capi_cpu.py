@@ -44,6 +44,8 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_unet_wgrad_args": _lib.UNetWgradArgs, "snnflow_unet_lif_bwd_args": _lib.UNetLifBwdArgs,
         "snnflow_bn_fwd_args": _lib.BnFwdArgs, "snnflow_bn_bwd_args": _lib.BnBwdArgs,
         "snnflow_pointwise_args": _lib.PointwiseArgs,
+        "snnflow_firenet_plan": _lib.FireNetPlan, "snnflow_firenet_fwd_io": _lib.FireNetFwdIo,
+        "snnflow_firenet_bwd_io": _lib.FireNetBwdIo, "snnflow_firenet_wgrad_step": _lib.FireNetWgradStep,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():

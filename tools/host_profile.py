@@ -52,13 +52,20 @@ def main(steps=10, seq=False, C=8, R=128, B=8, T=10):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     print(f"eager {'sequence' if seq else 'per-step'}: {1e3 * dt:.3f} ms/step, {B * T * 1000 / dt / 1e6:.2f} M events/s")
+    if "--noprof" in sys.argv:
+        return
+    # the backward Functions run on autograd's device thread: profile with it run inline
+    torch.autograd.set_multithreading_enabled(False)
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
     pr.disable()
-    pstats.Stats(pr).sort_stats("cumulative").print_stats(35)
+    torch.autograd.set_multithreading_enabled(True)
+    st = pstats.Stats(pr)
+    st.sort_stats("cumulative").print_stats(35)
+    st.sort_stats("tottime").print_stats(40)
 
 
 if __name__ == "__main__":
