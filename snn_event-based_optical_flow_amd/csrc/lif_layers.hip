@@ -44,11 +44,15 @@
 #ifndef SNNFLOW_TRACE
 #define SNNFLOW_TRACE 0
 #endif
+#ifndef SNNFLOW_TRACE_MINGRID
+#define SNNFLOW_TRACE_MINGRID 0  // stamp only launches of at least this many blocks (slot launches: 4 tasks)
+#endif
 #if SNNFLOW_TRACE
 __device__ unsigned long long g_trace[4][4096][8];
 #define TRACE_AT(on, kind, k)                                                                  \
     do {                                                                                      \
-        if ((on) && threadIdx.x == 0 && blockIdx.x < 4096) g_trace[kind][blockIdx.x][k] = wall_clock64(); \
+        if ((on) && threadIdx.x == 0 && blockIdx.x < 4096 && gridDim.x >= SNNFLOW_TRACE_MINGRID) \
+            g_trace[kind][blockIdx.x][k] = wall_clock64();                                    \
     } while (0)
 #else
 #define TRACE_AT(on, kind, k) do { } while (0)
