@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 17
+#define SNNFLOW_ABI_VERSION 18
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -521,7 +521,17 @@ typedef struct {
     float* current;            /* fp32 [pix][M] out: ff (+ rec), for the backward */
     uint16_t* act;             /* act [pix][act_pitch] out: z_out (+ residual) */
     int act_pitch;
+    /* ABI 18, split-K (ksplit 0 or 1: off): the k-steps of every output tile are dealt to ksplit blocks,
+     * each writing its fp32 partial tile to partial [ksplit][P][M] (P = output pixels of the launch's
+     * domain); a second kernel sums them in split order (deterministic) and applies the epilogue.  For
+     * the deep layers, whose output tiles alone leave most of the 256 CUs idle. */
+    int ksplit;
+    float* partial;
 } snnflow_unet_conv_args;
+#define SNNFLOW_UNET_MAX_KSPLIT 16
+/* Split-K factor the library chooses for a launch (1: none); the caller then sets ksplit and a
+ * partial buffer of ksplit * P * M floats. */
+int snnflow_unet_conv_ksplit(const snnflow_unet_conv_args* a);
 
 /* Convolution (forward of a cell with the LIF epilogue, or an input gradient with EPI_STORE). */
 int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream);

@@ -128,6 +128,72 @@ __device__ inline void dom_pix(const PixDom& d, int n, int& b, int& y, int& x) {
     x = d.cls < 0 ? xx : 2 * xx + d.px;
 }
 
+// Epilogue of one output element quad (domain pixel nd, channels m .. m+3): EPI_STORE (optionally
+// accumulating) or the ConvLIF update (spiking_submodules.py:121-151 / 265-300).
+__device__ inline void conv_epilogue(const snnflow_unet_conv_args& a, const PixDom& dom, int nd, int m, float v0,
+                                     float v1, float v2, float v3) {
+    const float v[4] = {v0, v1, v2, v3};
+    const int64_t Pfull = (int64_t)a.B * a.Ho * a.Wo;
+    const int64_t plane = Pfull * a.M;
+    int ob, oy, ox;
+    dom_pix(dom, nd, ob, oy, ox);
+    const int64_t n = ((int64_t)ob * a.Ho + oy) * a.Wo + ox;
+    if (a.epi == SNNFLOW_UNET_EPI_STORE) {
+        float* o = a.out + n * a.ld + m;
+        if (m + 3 < a.M) {
+            float4 val = make_float4(v[0], v[1], v[2], v[3]);
+            if (a.accumulate) {
+                const float4 old = *reinterpret_cast<const float4*>(o);
+                val = make_float4(old.x + val.x, old.y + val.y, old.z + val.z, old.w + val.w);
+            }
+            *reinterpret_cast<float4*>(o) = val;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (m + r < a.M) o[r] = a.accumulate ? o[r] + v[r] : v[r];
+        }
+        return;
+    }
+    // ConvLIF, M = hidden channels (multiple of 4)
+    const int64_t e0 = n * a.M + m;
+    float vp[4] = {0.f, 0.f, 0.f, 0.f}, zp[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.prev_state) {
+        const float4 tv = *reinterpret_cast<const float4*>(a.prev_state + e0);
+        const float4 tz = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
+        vp[0] = tv.x; vp[1] = tv.y; vp[2] = tv.z; vp[3] = tv.w;
+        zp[0] = tz.x; zp[1] = tz.y; zp[2] = tz.z; zp[3] = tz.w;
+    }
+    if (a.residual) {
+        const uint2 rr = *reinterpret_cast<const uint2*>(a.residual + n * a.res_pitch + m);
+        rs[0] = bf2f(rr.x & 0xffff); rs[1] = bf2f(rr.x >> 16); rs[2] = bf2f(rr.y & 0xffff); rs[3] = bf2f(rr.y >> 16);
+    }
+    float vo[4], zo[4];
+    uint16_t ob16[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float lam = 1.0f / (1.0f + expf(-a.leak[m + r]));
+        const float th0 = a.thresh[m + r], th = th0 < 0.01f ? 0.01f : th0;
+        vo[r] = a.hard_reset ? ((vp[r] * lam) * (1.0f - zp[r])) + ((1.0f - lam) * v[r])
+                             : ((vp[r] * lam) + ((1.0f - lam) * v[r])) - (zp[r] * th);
+        zo[r] = (vo[r] - th > 0.0f) ? 1.0f : 0.0f;
+        ob16[r] = f2bf(a.residual ? zo[r] + rs[r] : zo[r]);
+    }
+    *reinterpret_cast<float4*>(a.state + e0) = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    *reinterpret_cast<float4*>(a.state + plane + e0) = make_float4(zo[0], zo[1], zo[2], zo[3]);
+    *reinterpret_cast<float4*>(a.current + e0) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<uint2*>(a.act + n * a.act_pitch + m) =
+        make_uint2((uint32_t)ob16[0] | ((uint32_t)ob16[1] << 16), (uint32_t)ob16[2] | ((uint32_t)ob16[3] << 16));
+}
+
+// Segment k of the launch through constant kernarg indices (a dynamic index would copy the array to scratch).
+__device__ inline snnflow_unet_seg seg_at(const snnflow_unet_conv_args& a, int k) {
+    snnflow_unet_seg r = a.seg[0];
+#pragma unroll
+    for (int i = 1; i < SNNFLOW_UNET_MAX_SEGS; ++i)
+        if (k == i) r = a.seg[i];
+    return r;
+}
+
 // XPARTS == 1: X exact in bf16 (one plane), the weight parts of the segment (nparts) multiply it.
 // XPARTS == 3: X is an fp32 tensor as hi / mid / lo planes (a.xpart apart); the products above
 // 2^-24 relative are formed: X_hi x (W_hi, W_mid, W_lo), X_mid x (W_hi, W_mid), X_lo x W_hi.
@@ -143,8 +209,10 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
     const int wm = wave % WAVES_M, wn = wave / WAVES_M;
     const PixDom dom = pix_dom(a);
     const int P = dom.P;
-    const int mtiles = (a.M + BM - 1) / BM, ntiles = (P + BN - 1) / BN;
-    const int t = xcd_remap(blockIdx.x, mtiles * ntiles);
+    const int mtiles = (a.M + BM - 1) / BM, ntiles = (P + BN - 1) / BN, ntc = mtiles * ntiles;
+    const int ksplit = a.ksplit > 1 ? a.ksplit : 1;
+    const int tl = xcd_remap(blockIdx.x, ntc * ksplit);
+    const int split = tl / ntc, t = tl - split * ntc;
     const int m0 = (t % mtiles) * BM, n0 = (t / mtiles) * BN;
     const int ks = a.ksize, pad = ks / 2;
     const int taps = dom.nty * dom.ntx;
@@ -226,69 +294,88 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
 
-    // k-steps: segments (unrolled: constant kernarg indices), taps of the domain, 32-channel chunks;
-    // each step's successor is loaded before the step's MFMAs
-    load(a.seg[0], 0, 0);
+    // k-steps: (segment, tap of the domain, 32-channel chunk) flattened; split-K blocks take a
+    // contiguous range of them; each step's successor is loaded before the step's MFMAs
+    int nits[SNNFLOW_UNET_MAX_SEGS];
+    int ftot = 0;
 #pragma unroll
-    for (int s = 0; s < SNNFLOW_UNET_MAX_SEGS; ++s) {
-        if (s >= a.nseg) break;
-        const snnflow_unet_seg sg = a.seg[s];
-        const int nkc = sg.cpitch >> 5, nit = taps * nkc, np = sg.nparts;
-        for (int it = 0; it < nit; ++it) {
-            __syncthreads();  // the previous step's fragment reads are done
-            store();
-            __syncthreads();
-            if (it + 1 < nit) {
-                const int t2 = (it + 1) / nkc;
-                load(sg, t2, it + 1 - t2 * nkc);
-            } else if (s + 1 < SNNFLOW_UNET_MAX_SEGS && s + 1 < a.nseg) {
-                load(a.seg[s + 1 < SNNFLOW_UNET_MAX_SEGS ? s + 1 : s], 0, 0);
+    for (int k = 0; k < SNNFLOW_UNET_MAX_SEGS; ++k) {
+        nits[k] = k < a.nseg ? taps * (a.seg[k].cpitch >> 5) : 0;
+        ftot += nits[k];
+    }
+    const int f0 = (int)((int64_t)ftot * split / ksplit), f1 = (int)((int64_t)ftot * (split + 1) / ksplit);
+    // flat step f -> segment k, tap index, chunk
+    auto locate = [&](int f, int& k, int& ti, int& kc) {
+        k = 0;
+#pragma unroll
+        for (int i = 0; i < SNNFLOW_UNET_MAX_SEGS - 1; ++i)
+            if (k == i && f >= nits[i]) {
+                f -= nits[i];
+                k = i + 1;
             }
-            if constexpr (XPARTS == 1) {
-                bf16x8 bx[4];
+        const int nkc = seg_at(a, k).cpitch >> 5;
+        ti = f / nkc;
+        kc = f - ti * nkc;
+    };
+    if (f0 < f1) {
+        int k, ti, kc;
+        locate(f0, k, ti, kc);
+        load(seg_at(a, k), ti, kc);
+    }
+    for (int f = f0; f < f1; ++f) {
+        int k, ti, kc;
+        locate(f, k, ti, kc);
+        const int np = seg_at(a, k).nparts;
+        __syncthreads();  // the previous step's fragment reads are done
+        store();
+        __syncthreads();
+        if (f + 1 < f1) {
+            int k2, ti2, kc2;
+            locate(f + 1, k2, ti2, kc2);
+            load(seg_at(a, k2), ti2, kc2);
+        }
+        if constexpr (XPARTS == 1) {
+            bf16x8 bx[4];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[(wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+            for (int j = 0; j < 4; ++j)
+                bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[(wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
 #pragma unroll
-                for (int i = 0; i < WMT; ++i) {
-                    const int row = wm * 16 * WMT + i * 16 + (lane & 15);
-                    for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
-                        const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+            for (int i = 0; i < WMT; ++i) {
+                const int row = wm * 16 * WMT + i * 16 + (lane & 15);
+                for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
+                    const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
-                    }
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
                 }
-            } else {
+            }
+        } else {
 #pragma unroll
-                for (int i = 0; i < WMT; ++i) {
-                    const int row = wm * 16 * WMT + i * 16 + (lane & 15);
-                    bf16x8 aw[3];
+            for (int i = 0; i < WMT; ++i) {
+                const int row = wm * 16 * WMT + i * 16 + (lane & 15);
+                bf16x8 aw[3];
 #pragma unroll
-                    for (int p = 0; p < 3; ++p)
-                        aw[p] = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+                for (int p = 0; p < 3; ++p)
+                    aw[p] = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int col = (wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8;
-                        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(&Xs[col]);
-                        const bf16x8 xm = *reinterpret_cast<const bf16x8*>(&Xs[BN * XP + col]);
-                        const bf16x8 xl = *reinterpret_cast<const bf16x8*>(&Xs[2 * BN * XP + col]);
-                        // smallest first: lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xl, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1], xm, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[2], xh, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xm, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1], xh, acc[i][j], 0, 0, 0);
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xh, acc[i][j], 0, 0, 0);
-                    }
+                for (int j = 0; j < 4; ++j) {
+                    const int col = (wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8;
+                    const bf16x8 xh = *reinterpret_cast<const bf16x8*>(&Xs[col]);
+                    const bf16x8 xm = *reinterpret_cast<const bf16x8*>(&Xs[BN * XP + col]);
+                    const bf16x8 xl = *reinterpret_cast<const bf16x8*>(&Xs[2 * BN * XP + col]);
+                    // smallest first: lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xl, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1], xm, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[2], xh, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xm, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[1], xh, acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[0], xh, acc[i][j], 0, 0, 0);
                 }
             }
         }
     }
 
-    // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of pixel n
-    const int64_t Pfull = (int64_t)a.B * a.Ho * a.Wo;
-    const int64_t plane = Pfull * a.M;
+    // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of domain pixel nd
 #pragma unroll
     for (int i = 0; i < WMT; ++i)
 #pragma unroll
@@ -296,56 +383,43 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
             const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
             const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
             if (nd >= P || m >= a.M) continue;
-            int ob, oy, ox;
-            dom_pix(dom, nd, ob, oy, ox);
-            const int64_t n = ((int64_t)ob * a.Ho + oy) * a.Wo + ox;
             const fx4 v = acc[i][j];
-            if (a.epi == SNNFLOW_UNET_EPI_STORE) {
-                float* o = a.out + n * a.ld + m;
-                if (m + 3 < a.M) {
-                    float4 val = make_float4(v[0], v[1], v[2], v[3]);
-                    if (a.accumulate) {
-                        const float4 old = *reinterpret_cast<const float4*>(o);
-                        val = make_float4(old.x + val.x, old.y + val.y, old.z + val.z, old.w + val.w);
-                    }
-                    *reinterpret_cast<float4*>(o) = val;
+            if (ksplit > 1) {  // split-K: this split's partial sums, reduced by k_unet_conv_reduce
+                float* o = a.partial + ((int64_t)split * P + nd) * a.M + m;
+                if (m + 3 < a.M && (a.M & 3) == 0) {
+                    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        if (m + r < a.M) o[r] = a.accumulate ? o[r] + v[r] : v[r];
+                        if (m + r < a.M) o[r] = v[r];
                 }
                 continue;
             }
-            // ConvLIF (spiking_submodules.py:121-151 / 265-300), M = hidden channels (multiple of 4)
-            const int64_t e0 = n * a.M + m;
-            float vp[4] = {0.f, 0.f, 0.f, 0.f}, zp[4] = {0.f, 0.f, 0.f, 0.f}, rs[4] = {0.f, 0.f, 0.f, 0.f};
-            if (a.prev_state) {
-                const float4 tv = *reinterpret_cast<const float4*>(a.prev_state + e0);
-                const float4 tz = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
-                vp[0] = tv.x; vp[1] = tv.y; vp[2] = tv.z; vp[3] = tv.w;
-                zp[0] = tz.x; zp[1] = tz.y; zp[2] = tz.z; zp[3] = tz.w;
-            }
-            if (a.residual) {
-                const uint2 rr = *reinterpret_cast<const uint2*>(a.residual + n * a.res_pitch + m);
-                rs[0] = bf2f(rr.x & 0xffff); rs[1] = bf2f(rr.x >> 16); rs[2] = bf2f(rr.y & 0xffff); rs[3] = bf2f(rr.y >> 16);
-            }
-            float vo[4], zo[4];
-            uint16_t ob16[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float lam = 1.0f / (1.0f + expf(-a.leak[m + r]));
-                const float th0 = a.thresh[m + r], th = th0 < 0.01f ? 0.01f : th0;
-                vo[r] = a.hard_reset ? ((vp[r] * lam) * (1.0f - zp[r])) + ((1.0f - lam) * v[r])
-                                     : ((vp[r] * lam) + ((1.0f - lam) * v[r])) - (zp[r] * th);
-                zo[r] = (vo[r] - th > 0.0f) ? 1.0f : 0.0f;
-                ob16[r] = f2bf(a.residual ? zo[r] + rs[r] : zo[r]);
-            }
-            *reinterpret_cast<float4*>(a.state + e0) = make_float4(vo[0], vo[1], vo[2], vo[3]);
-            *reinterpret_cast<float4*>(a.state + plane + e0) = make_float4(zo[0], zo[1], zo[2], zo[3]);
-            *reinterpret_cast<float4*>(a.current + e0) = make_float4(v[0], v[1], v[2], v[3]);
-            *reinterpret_cast<uint2*>(a.act + n * a.act_pitch + m) =
-                make_uint2((uint32_t)ob16[0] | ((uint32_t)ob16[1] << 16), (uint32_t)ob16[2] | ((uint32_t)ob16[3] << 16));
+            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3]);
         }
+}
+
+// Split-K reduction: the partial tiles of the ksplit blocks of an output tile summed in split order
+// (deterministic), then the launch's epilogue.  One thread per (domain pixel, 4 output channels).
+__global__ __launch_bounds__(UNT) void k_unet_conv_reduce(snnflow_unet_conv_args a) {
+    const PixDom dom = pix_dom(a);
+    const int P = dom.P, mq = (a.M + 3) / 4;
+    const int64_t e = (int64_t)blockIdx.x * UNT + threadIdx.x;
+    if (e >= (int64_t)P * mq) return;
+    const int nd = (int)(e / mq), m = (int)(e - (int64_t)nd * mq) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < a.ksplit; ++sp) {
+        const float* o = a.partial + ((int64_t)sp * P + nd) * a.M + m;
+        if (m + 3 < a.M && (a.M & 3) == 0) {
+            const float4 u = *reinterpret_cast<const float4*>(o);
+            v[0] += u.x; v[1] += u.y; v[2] += u.z; v[3] += u.w;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (m + r < a.M) v[r] += o[r];
+        }
+    }
+    conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -356,7 +430,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
 // Block tile 64 k x 64 m, 128 pixels per step (4 MFMA k-steps), 4 waves of 32 x 32; the partial
 // sums of a pixel range are added to dwk with fp32 atomics.
 // ---------------------------------------------------------------------------------------------
-constexpr int WG_BK = 64, WG_BM = 64, WG_PS = 128, WG_PP = WG_PS + 8;
+constexpr int WG_PS = 64, WG_PP = WG_PS + 8;
 
 // 8x8 transpose of 16-bit values: in[r] = channels 0..7 of pixel r -> out[c] = pixels 0..7 of channel c
 __device__ inline void transpose8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
@@ -375,14 +449,31 @@ __device__ inline void transpose8x8(const uint4 (&in)[8], uint4 (&out)[8]) {
     }
 }
 
+// Block tile TK (input channels k) x TM (output channels m) of one tap, WG_PS pixels per step; 4 waves
+// as 2 x 2, each (TK/2) x (TM/2): per 32-pixel MFMA k-step a wave reads TK/32 X and 3*TM/32 G fragments
+// (16 B per lane) for (TK/32)*(TM/32)*3 MFMAs, so the larger tiles halve the LDS reads per MFMA of
+// the 64 x 64 form.  Staging: 8x8 (pixel x channel) blocks loaded with 16-B loads, transposed in
+// registers, written as 16-B rows of the [channel][pixel] LDS images; the next step's loads are
+// issued before this step's MFMAs.
+template <int TK, int TM>
+struct WgGeo {
+    static constexpr int XB = TK * WG_PS / 64;          // 8x8 X blocks per step
+    static constexpr int GB = 3 * TM * WG_PS / 64;      // 8x8 G blocks (3 planes)
+    static constexpr int U = (XB + GB + UNT - 1) / UNT; // blocks per thread
+    static constexpr int NI = TK / 32, NJ = TM / 32;    // 16-row MFMA tiles per wave (k, m)
+};
+
+template <int TK, int TM>
 __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, int ktiles, int mtiles, int nsplit,
                                                     int steps) {
-    __shared__ __attribute__((aligned(16))) __bf16 Xt[WG_BK * WG_PP];
-    __shared__ __attribute__((aligned(16))) __bf16 Gt[3 * WG_BM * WG_PP];
+    using G = WgGeo<TK, TM>;
+    constexpr int NI = G::NI, NJ = G::NJ, PGS = WG_PS / 8;  // pixel groups per step
+    __shared__ __attribute__((aligned(16))) __bf16 Xt[TK * WG_PP];
+    __shared__ __attribute__((aligned(16))) __bf16 Gt[3 * TM * WG_PP];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wk = wave & 1, wmv = wave >> 1;
-    int b = blockIdx.x;
+    int b = xcd_remap(blockIdx.x, (int)gridDim.x);
     const int split = b % nsplit;
     b /= nsplit;
     const int mt = b % mtiles;
@@ -394,27 +485,21 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
     const snnflow_unet_seg& sg = a.seg;
     const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
 
-    // staging units of this thread: unit u in [0, 512): u < 128 -> X block (pixel group u % 16,
-    // channel group u / 16); else G block (part, channel group, pixel group)
-    int ublk[2];
-    ublk[0] = tid;
-    ublk[1] = tid + 256;
-
-    fx4 acc[2][2];
+    fx4 acc[NI][NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < NJ; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 rg[2][8];
+    uint4 rg[G::U][8];
     auto load = [&](int st) {
         const int pbase = (split * steps + st) * WG_PS;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int blk = ublk[u];
-            if (blk < 128) {  // X block
-                const int pg = blk & 15, cg = blk >> 4;
-                const int kk = kt * WG_BK + cg * 8;
+        for (int u = 0; u < G::U; ++u) {
+            const int blk = tid + u * UNT;
+            if (blk < G::XB) {  // X block: pixel group, channel group
+                const int pg = blk % PGS, cg = blk / PGS;
+                const int kk = kt * TK + cg * 8;
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     const int n = pbase + pg * 8 + r;
@@ -427,10 +512,10 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
                     rg[u][r] = ld16(sg.x + (ok ? (((int64_t)bb * sg.H + iy) * sg.W + ix) * sg.cpitch + kk : 0));
                     if (!ok) rg[u][r] = z4;
                 }
-            } else {  // G block
-                const int gb = blk - 128;
-                const int pg = gb & 15, cg = (gb >> 4) & 7, part = gb >> 7;
-                const int mm = mt * WG_BM + cg * 8;
+            } else if (blk < G::XB + G::GB) {  // G block: plane, channel group, pixel group
+                const int gb = blk - G::XB;
+                const int pg = gb % PGS, cg = (gb / PGS) % (TM / 8), part = gb / (PGS * (TM / 8));
+                const int mm = mt * TM + cg * 8;
 #pragma unroll
                 for (int r = 0; r < 8; ++r) {
                     const int n = pbase + pg * 8 + r;
@@ -443,20 +528,21 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
     };
     auto store = [&]() {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int blk = ublk[u];
+        for (int u = 0; u < G::U; ++u) {
+            const int blk = tid + u * UNT;
+            if (blk >= G::XB + G::GB) continue;
             uint4 tr[8];
             transpose8x8(rg[u], tr);
-            if (blk < 128) {
-                const int pg = blk & 15, cg = blk >> 4;
+            if (blk < G::XB) {
+                const int pg = blk % PGS, cg = blk / PGS;
 #pragma unroll
                 for (int c = 0; c < 8; ++c) *reinterpret_cast<uint4*>(&Xt[(cg * 8 + c) * WG_PP + pg * 8]) = tr[c];
             } else {
-                const int gb = blk - 128;
-                const int pg = gb & 15, cg = (gb >> 4) & 7, part = gb >> 7;
+                const int gb = blk - G::XB;
+                const int pg = gb % PGS, cg = (gb / PGS) % (TM / 8), part = gb / (PGS * (TM / 8));
 #pragma unroll
                 for (int c = 0; c < 8; ++c)
-                    *reinterpret_cast<uint4*>(&Gt[(part * WG_BM + cg * 8 + c) * WG_PP + pg * 8]) = tr[c];
+                    *reinterpret_cast<uint4*>(&Gt[(part * TM + cg * 8 + c) * WG_PP + pg * 8]) = tr[c];
             }
         }
     };
@@ -473,28 +559,29 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
         if (st + 1 < nst) load(st + 1);
 #pragma unroll
         for (int kk = 0; kk < WG_PS / 32; ++kk) {
-            bf16x8 ax[2];
+            bf16x8 ax[NI];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
-                ax[i] = *reinterpret_cast<const bf16x8*>(&Xt[(wk * 32 + i * 16 + (lane & 15)) * WG_PP + kk * 32 + (lane >> 4) * 8]);
+            for (int i = 0; i < NI; ++i)
+                ax[i] = *reinterpret_cast<const bf16x8*>(
+                    &Xt[(wk * (TK / 2) + i * 16 + (lane & 15)) * WG_PP + kk * 32 + (lane >> 4) * 8]);
 #pragma unroll
             for (int p = 2; p >= 0; --p)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) {
+                for (int j = 0; j < NJ; ++j) {
                     const bf16x8 bg = *reinterpret_cast<const bf16x8*>(
-                        &Gt[(p * WG_BM + wmv * 32 + j * 16 + (lane & 15)) * WG_PP + kk * 32 + (lane >> 4) * 8]);
+                        &Gt[(p * TM + wmv * (TM / 2) + j * 16 + (lane & 15)) * WG_PP + kk * 32 + (lane >> 4) * 8]);
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < NI; ++i)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[i], bg, acc[i][j], 0, 0, 0);
                 }
         }
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int k = kt * WG_BK + wk * 32 + i * 16 + 4 * (lane >> 4);
-            const int m = mt * WG_BM + wmv * 32 + j * 16 + (lane & 15);
+        for (int j = 0; j < NJ; ++j) {
+            const int k = kt * TK + wk * (TK / 2) + i * 16 + 4 * (lane >> 4);
+            const int m = mt * TM + wmv * (TM / 2) + j * 16 + (lane & 15);
             if (m >= a.M) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -945,22 +1032,67 @@ int grid1d(int64_t n, int per, int cap) {
     return (int)g;
 }
 
+inline int dom_pixels(const snnflow_unet_conv_args& a) {
+    if (a.pclass >= 0) return a.B * ((a.Ho - (a.pclass >> 1) + 1) / 2) * ((a.Wo - (a.pclass & 1) + 1) / 2);
+    return a.B * a.Ho * a.Wo;
+}
+
 template <int WMT, int WM, int XP_>
 int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
     using G = ConvGeo<WMT, WM, XP_>;
-    int P = a.B * a.Ho * a.Wo;
-    if (a.pclass >= 0) P = a.B * ((a.Ho - (a.pclass >> 1) + 1) / 2) * ((a.Wo - (a.pclass & 1) + 1) / 2);
-    const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN);
+    const int P = dom_pixels(a);
+    const int ks = a.ksplit > 1 ? a.ksplit : 1;
+    const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN) * ks;
     if (nb > 0x7fffffff) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: grid too large");
     if (nb == 0) return 0;
     hipLaunchKernelGGL((k_unet_conv<WMT, WM, XP_>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
+    if (ks > 1) {
+        const int64_t n = (int64_t)P * ((a.M + 3) / 4);
+        hipLaunchKernelGGL(k_unet_conv_reduce, dim3((unsigned)((n + UNT - 1) / UNT)), dim3(UNT), 0, s, a);
+    }
     SNN_CHECK_LAUNCH();
     return 0;
+}
+
+// Output tiles of a launch for its tile configuration (the selection of snnflow_unet_conv).
+inline void conv_tile(const snnflow_unet_conv_args& a, int& bm, int& bn) {
+    if (a.xparts == 3) {
+        bm = a.M > 32 ? 64 : 32;
+        bn = a.M > 32 ? 128 : 256;
+    } else if (a.M > 64) {
+        bm = 128; bn = 128;
+    } else if (a.M > 32) {
+        bm = 64; bn = 128;
+    } else if (a.M > 16) {
+        bm = 32; bn = 256;
+    } else {
+        bm = 16; bn = 256;
+    }
 }
 
 }  // namespace
 
 extern "C" {
+
+int snnflow_unet_conv_ksplit(const snnflow_unet_conv_args* a) {
+    if (!a || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 || a->nseg < 1 || a->nseg > SNNFLOW_UNET_MAX_SEGS ||
+        a->ksize < 1)
+        return 1;
+    int bm, bn;
+    conv_tile(*a, bm, bn);
+    const int64_t tiles = (int64_t)((a->M + bm - 1) / bm) * ((dom_pixels(*a) + bn - 1) / bn);
+    int taps = a->ksize * a->ksize;
+    if (a->pclass >= 0) {
+        const int pad = a->ksize / 2, ky0 = ((a->pclass >> 1) + pad) & 1, kx0 = ((a->pclass & 1) + pad) & 1;
+        taps = ((a->ksize - ky0 + 1) / 2) * ((a->ksize - kx0 + 1) / 2);
+    }
+    int64_t steps = 0;
+    for (int k = 0; k < a->nseg; ++k) steps += (int64_t)taps * (a->seg[k].cpitch / 32);
+    // about two resident 4-wave blocks per CU (256 CUs) and at least 16 k-steps per split
+    int ks = 1;
+    while (ks < SNNFLOW_UNET_MAX_KSPLIT && tiles * ks < 512 && steps / (2 * ks) >= 16) ks *= 2;
+    return ks;
+}
 
 int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
     if (!a || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 || !a->w || a->nseg < 1 ||
@@ -984,6 +1116,8 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
         SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: unknown epilogue");
     }
     if (a->xparts != 1 && a->xparts != 3) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: xparts must be 1 or 3");
+    if (a->ksplit > 1 && (!a->partial || a->ksplit > SNNFLOW_UNET_MAX_KSPLIT))
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: split-K needs the partial buffer (ksplit <= SNNFLOW_UNET_MAX_KSPLIT)");
     if (a->pclass >= 4 || (a->pclass >= 0 && (a->seg[0].mode != SNNFLOW_UNET_MODE_T2 || a->nseg != 1)))
         SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: parity classes are for one transposed stride-2 segment");
     const hipStream_t s = (hipStream_t)stream;
@@ -1011,23 +1145,59 @@ int snnflow_unet_prep_weights(const float* w, int cout, int cin, int ksize, cons
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+template <int TK, int TM>
+int launch_wgrad(const snnflow_unet_wgrad_args& a, hipStream_t s) {
+    const int P = a.B * a.Ho * a.Wo;
+    const int taps = a.ksize * a.ksize;
+    const int ktiles = (a.seg.cpitch + TK - 1) / TK, mtiles = (a.M + TM - 1) / TM;
+    const int64_t tiles = (int64_t)taps * ktiles * mtiles;
+    const int total_steps = (P + WG_PS - 1) / WG_PS;
+    int nsplit = (int)((1024 + tiles - 1) / tiles);  // ~1024+ blocks
+    if (nsplit > total_steps / 8) nsplit = total_steps / 8;  // >= 8 steps (512 pixels) per block
+    if (nsplit < 1) nsplit = 1;
+    const int steps = (total_steps + nsplit - 1) / nsplit;
+    hipLaunchKernelGGL((k_unet_wgrad<TK, TM>), dim3((unsigned)(tiles * nsplit)), dim3(UNT), 0, s, a, ktiles, mtiles,
+                       nsplit, steps);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
 int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
     if (!a || !a->g3 || !a->dwk || !a->seg.x || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 ||
         a->gpitch % 32 != 0 || a->seg.cpitch % 32 != 0 || a->seg.mode == SNNFLOW_UNET_MODE_T2 || a->ksize < 1)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: bad args");
-    const int P = a->B * a->Ho * a->Wo;
-    const int taps = a->ksize * a->ksize;
-    const int ktiles = (a->seg.cpitch + WG_BK - 1) / WG_BK, mtiles = (a->M + WG_BM - 1) / WG_BM;
-    const int64_t tiles = (int64_t)taps * ktiles * mtiles;
-    const int total_steps = (P + WG_PS - 1) / WG_PS;
-    int nsplit = (int)((1024 + tiles - 1) / tiles);  // ~1024+ blocks
-    if (nsplit > total_steps / 4) nsplit = total_steps / 4;  // >= 4 steps (512 pixels) per block
-    if (nsplit < 1) nsplit = 1;
-    const int steps = (total_steps + nsplit - 1) / nsplit;
-    hipLaunchKernelGGL(k_unet_wgrad, dim3((unsigned)(tiles * nsplit)), dim3(UNT), 0, (hipStream_t)stream, *a, ktiles,
-                       mtiles, nsplit, steps);
-    SNN_CHECK_LAUNCH();
-    return 0;
+    const hipStream_t s = (hipStream_t)stream;
+    // tiles sized to the layer: m 32 / 64 / 128; k the first of 128, 160 (m <= 64: registers), 96, 64, 32
+    // whose padding of the segment's channel pitch stays within 1/5 (else the least padding) -- fewer
+    // wasted MFMAs and G loads on thin layers, wide tiles elsewhere
+    const int tm = a->M <= 32 ? 32 : (a->M <= 64 ? 64 : 128);
+    const int cp = a->seg.cpitch;
+    int tk = 0, best = 1 << 30, tbest = 32;
+    for (int c : {128, 160, 96, 64, 32}) {
+        if (c == 160 && tm > 64) continue;
+        const int padded = (cp + c - 1) / c * c;
+        if (tk == 0 && 5 * (padded - cp) <= cp) tk = c;
+        if (padded < best) {
+            best = padded;
+            tbest = c;
+        }
+    }
+    if (tk == 0) tk = tbest;
+#define WG_CASE(K_, M_) \
+    if (tk == K_ && tm == M_) return launch_wgrad<K_, M_>(*a, s);
+    WG_CASE(160, 32) WG_CASE(160, 64) WG_CASE(160, 128)
+    WG_CASE(128, 32) WG_CASE(128, 64) WG_CASE(128, 128)
+    WG_CASE(96, 32) WG_CASE(96, 64) WG_CASE(96, 128)
+    WG_CASE(64, 32) WG_CASE(64, 64) WG_CASE(64, 128)
+    WG_CASE(32, 32) WG_CASE(32, 64) WG_CASE(32, 128)
+#undef WG_CASE
+    SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: no tile");
 }
 
 int snnflow_unet_wgrad_finalize(const float* dwk, int ktot, const int* kmap_inv, int k0, int nk, int cout, int cin,

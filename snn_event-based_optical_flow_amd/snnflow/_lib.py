@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 
 class Neuron(ctypes.Structure):
@@ -179,7 +179,8 @@ class UNetConvArgs(ctypes.Structure):
                 ("xpart", I64), ("pclass", I32), ("epi", I32),
                 ("out", P), ("ld", I32), ("accumulate", I32),
                 ("leak", P), ("thresh", P), ("hard_reset", I32), ("prev_state", P), ("residual", P),
-                ("res_pitch", I32), ("state", P), ("current", P), ("act", P), ("act_pitch", I32)]
+                ("res_pitch", I32), ("state", P), ("current", P), ("act", P), ("act_pitch", I32),
+                ("ksplit", I32), ("partial", P)]
 
 
 class UNetWgradArgs(ctypes.Structure):
@@ -283,6 +284,7 @@ EXPORTS = {
     "snnflow_slot_supported": (I32, [I32, I32]),
     "snnflow_frag_halfs": (I32, [I32, I32]),
     "snnflow_unet_conv": (I32, [ctypes.POINTER(UNetConvArgs), P]),
+    "snnflow_unet_conv_ksplit": (I32, [ctypes.POINTER(UNetConvArgs)]),
     "snnflow_unet_prep_weights": (I32, [P, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "snnflow_unet_wgrad": (I32, [ctypes.POINTER(UNetWgradArgs), P]),
     "snnflow_unet_wgrad_finalize": (I32, [P, I32, P, I32, I32, I32, I32, I32, I32, P, P]),

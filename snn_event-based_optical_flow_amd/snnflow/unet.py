@@ -21,6 +21,7 @@ accumulated on the device and returned by its first step.
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -371,6 +372,29 @@ def _unet_seg(act, mode, kc0, nparts=3):
     return _lib.UNetSeg(ptr(act), H, W, pitch, mode, kc0, nparts)
 
 
+_PARTIAL = {}
+_SHAPES = os.environ.get("SNNFLOW_UNET_SHAPES") == "1"  # profiling: kernel names carry the GEMM shape
+
+
+def _name(kind, M, K, P):
+    return f"{kind}[M{M} K{K} P{P}]" if _SHAPES else kind
+
+
+def _split_k(a, P, dev):
+    """Split-K of a launch (library's choice) with the shared partial-sum workspace (stream-ordered
+    reuse; sized by the largest request, which the eager warm-up steps make before any graph capture)."""
+    ks = lib.snnflow_unet_conv_ksplit(ctypes.byref(a))
+    if ks <= 1:
+        a.ksplit, a.partial = 1, None
+        return
+    n = ks * P * a.M
+    buf = _PARTIAL.get(dev)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(n, device=dev)
+        _PARTIAL[dev] = buf
+    a.ksplit, a.partial = ks, buf.data_ptr()
+
+
 def conv_lif(plan, B, Ho, Wo, acts, prev_state, residual, state, current, act_out, s):
     """Forward of one cell: implicit GEMM over its segments + the LIF epilogue."""
     a = _lib.UNetConvArgs()
@@ -389,7 +413,9 @@ def conv_lif(plan, B, Ho, Wo, acts, prev_state, residual, state, current, act_ou
     if residual is not None:
         a.residual, a.res_pitch = ptr(residual), residual.shape[-1]
     a.state, a.current, a.act, a.act_pitch = ptr(state), ptr(current), ptr(act_out), act_out.shape[-1]
-    _lib.call("unet_conv", lib.snnflow_unet_conv, ctypes.byref(a), s, work=_conv_flops(plan, B * Ho * Wo, acts))
+    _split_k(a, B * Ho * Wo, state.device)
+    _lib.call(_name("unet_conv", a.M, sum(a.seg[i].cpitch for i in range(n)), B * Ho * Wo), lib.snnflow_unet_conv,
+              ctypes.byref(a), s, work=_conv_flops(plan, B * Ho * Wo, acts))
 
 
 def _conv_flops(plan, P_out, acts=None):
@@ -414,7 +440,10 @@ def conv_dgrad(plan, sg, g3, B, Hi, Wi, out, ld, mvalid, accumulate, s):
     work = 2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps
     for cls in (range(4) if t2 else (-1,)):
         a.pclass = cls
-        _lib.call("unet_dgrad", lib.snnflow_unet_conv, ctypes.byref(a), s, work=work / 4 if t2 else work)
+        P = B * ((Hi - (cls >> 1) + 1) // 2) * ((Wi - (cls & 1) + 1) // 2) if t2 else B * Hi * Wi
+        _split_k(a, P, out.device)
+        _lib.call(_name("unet_dgrad", a.M, a.seg[0].cpitch, P), lib.snnflow_unet_conv, ctypes.byref(a), s,
+                  work=work / 4 if t2 else work)
 
 
 def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
@@ -423,7 +452,7 @@ def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
     a.g3, a.gpitch, a.gpart = ptr(g3), g3.shape[-1], g3[0].numel()
     a.seg = _unet_seg(act, sg.mode, sg.kc0)
     a.k0, a.ktot, a.dwk = sg.k0, plan.ktot, ptr(plan.dwk)
-    _lib.call("unet_wgrad", lib.snnflow_unet_wgrad, ctypes.byref(a), s,
+    _lib.call(_name("unet_wgrad", plan.C, a.seg.cpitch, B * Ho * Wo), lib.snnflow_unet_wgrad, ctypes.byref(a), s,
               work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
 
 
