@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 18
+#define SNNFLOW_ABI_VERSION 19
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -555,7 +555,12 @@ typedef struct {
     snnflow_unet_seg seg;
     int k0, ktot;       /* first k position of the segment in dwk, k positions per tap in dwk */
     float* dwk;         /* fp32 [ksize^2][ktot][M] */
+    /* ABI 19, optional: workspace of snnflow_unet_wgrad_partial_floats() floats; with it the pixel
+     * splits write partial tiles that one more kernel adds to dwk in split order (deterministic, no
+     * atomics); NULL: fp32 atomics into dwk */
+    float* partial;
 } snnflow_unet_wgrad_args;
+int64_t snnflow_unet_wgrad_partial_floats(const snnflow_unet_wgrad_args* a);
 int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream);
 
 /* dw[m][c][tap] (+)= sum over the (up to 3) positions k of input channel c (kmap_inv [cin][3], -1:

@@ -550,8 +550,8 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
     const int total_steps = (P + WG_PS - 1) / WG_PS;
     const int st0 = split * steps;
     const int nst = st0 >= total_steps ? 0 : (total_steps - st0 < steps ? total_steps - st0 : steps);
-    if (nst == 0) return;
-    load(0);
+    if (nst == 0 && !a.partial) return;
+    if (nst > 0) load(0);
     for (int st = 0; st < nst; ++st) {
         __syncthreads();
         store();
@@ -576,6 +576,20 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
                 }
         }
     }
+    if (a.partial) {  // this split's tile, summed in split order by k_unet_wgrad_reduce (deterministic)
+        const int KP = ktiles * TK, MP = mtiles * TM;
+        float* part = a.partial + ((int64_t)split * (ks * ks) + tap) * KP * MP;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int k = kt * TK + wk * (TK / 2) + i * 16 + 4 * (lane >> 4);
+                const int m = mt * TM + wmv * (TM / 2) + j * 16 + (lane & 15);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) part[(int64_t)(k + r) * MP + m] = acc[i][j][r];
+            }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -587,6 +601,20 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
             for (int r = 0; r < 4; ++r)
                 if (k + r < sg.cpitch) atomicAdd(a.dwk + ((int64_t)tap * a.ktot + a.k0 + k + r) * a.M + m, acc[i][j][r]);
         }
+}
+
+// dwk[tap][k0 + k][m] += sum over the splits (fixed order) of the partial tiles.
+__global__ void k_unet_wgrad_reduce(snnflow_unet_wgrad_args a, int nsplit, int KP, int MP) {
+    const int taps = a.ksize * a.ksize, K = a.seg.cpitch, M = a.M;
+    const int64_t n = (int64_t)taps * K * M;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int m = (int)(e % M);
+        const int64_t r = e / M;
+        const int k = (int)(r % K), tap = (int)(r / K);
+        float sum = 0.0f;
+        for (int sp = 0; sp < nsplit; ++sp) sum += a.partial[(((int64_t)sp * taps + tap) * KP + k) * MP + m];
+        a.dwk[((int64_t)tap * a.ktot + a.k0 + k) * M + m] += sum;
+    }
 }
 
 __global__ void k_unet_wgrad_finalize(const float* __restrict__ dwk, int ktot, const int* __restrict__ inv, int k0,
@@ -1057,7 +1085,7 @@ int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
 // Output tiles of a launch for its tile configuration (the selection of snnflow_unet_conv).
 inline void conv_tile(const snnflow_unet_conv_args& a, int& bm, int& bn) {
     if (a.xparts == 3) {
-        bm = a.M > 32 ? 64 : 32;
+        bm = a.M > 64 ? 128 : (a.M > 32 ? 64 : 32);
         bn = a.M > 32 ? 128 : 256;
     } else if (a.M > 64) {
         bm = 128; bn = 128;
@@ -1122,6 +1150,7 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
         SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: parity classes are for one transposed stride-2 segment");
     const hipStream_t s = (hipStream_t)stream;
     if (a->xparts == 3) {  // input gradients: the fp32 gradient as three bf16 planes
+        if (a->M > 64) return launch_conv<4, 2, 3>(*a, s);
         if (a->M > 32) return launch_conv<2, 2, 3>(*a, s);
         return launch_conv<2, 1, 3>(*a, s);
     }
@@ -1148,37 +1177,51 @@ int snnflow_unet_prep_weights(const float* w, int cout, int cin, int ksize, cons
 }  // extern "C"
 
 namespace {
+struct WgPlan { int ktiles, mtiles, nsplit, steps; int64_t tiles; };
+
+template <int TK, int TM>
+WgPlan wgrad_plan(const snnflow_unet_wgrad_args& a) {
+    WgPlan p;
+    const int P = a.B * a.Ho * a.Wo;
+    p.ktiles = (a.seg.cpitch + TK - 1) / TK;
+    p.mtiles = (a.M + TM - 1) / TM;
+    p.tiles = (int64_t)a.ksize * a.ksize * p.ktiles * p.mtiles;
+    const int total_steps = (P + WG_PS - 1) / WG_PS;
+    p.nsplit = (int)((1024 + p.tiles - 1) / p.tiles);  // ~1024+ blocks
+    if (p.nsplit > total_steps / 8) p.nsplit = total_steps / 8;  // >= 8 steps (512 pixels) per block
+    if (p.nsplit < 1) p.nsplit = 1;
+    p.steps = (total_steps + p.nsplit - 1) / p.nsplit;
+    return p;
+}
+
+template <int TK, int TM>
+int64_t wgrad_partial_floats(const snnflow_unet_wgrad_args& a) {
+    const WgPlan p = wgrad_plan<TK, TM>(a);
+    return (int64_t)p.nsplit * a.ksize * a.ksize * p.ktiles * TK * p.mtiles * TM;
+}
+
 template <int TK, int TM>
 int launch_wgrad(const snnflow_unet_wgrad_args& a, hipStream_t s) {
-    const int P = a.B * a.Ho * a.Wo;
-    const int taps = a.ksize * a.ksize;
-    const int ktiles = (a.seg.cpitch + TK - 1) / TK, mtiles = (a.M + TM - 1) / TM;
-    const int64_t tiles = (int64_t)taps * ktiles * mtiles;
-    const int total_steps = (P + WG_PS - 1) / WG_PS;
-    int nsplit = (int)((1024 + tiles - 1) / tiles);  // ~1024+ blocks
-    if (nsplit > total_steps / 8) nsplit = total_steps / 8;  // >= 8 steps (512 pixels) per block
-    if (nsplit < 1) nsplit = 1;
-    const int steps = (total_steps + nsplit - 1) / nsplit;
-    hipLaunchKernelGGL((k_unet_wgrad<TK, TM>), dim3((unsigned)(tiles * nsplit)), dim3(UNT), 0, s, a, ktiles, mtiles,
-                       nsplit, steps);
+    const WgPlan p = wgrad_plan<TK, TM>(a);
+    hipLaunchKernelGGL((k_unet_wgrad<TK, TM>), dim3((unsigned)(p.tiles * p.nsplit)), dim3(UNT), 0, s, a, p.ktiles,
+                       p.mtiles, p.nsplit, p.steps);
+    if (a.partial) {
+        const int64_t n = (int64_t)a.ksize * a.ksize * a.seg.cpitch * a.M;
+        hipLaunchKernelGGL(k_unet_wgrad_reduce, dim3(grid1d(n, 256, 4096)), dim3(256), 0, s, a, p.nsplit,
+                           p.ktiles * TK, p.mtiles * TM);
+    }
     SNN_CHECK_LAUNCH();
     return 0;
 }
-}  // namespace
 
-extern "C" {
-
-int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
-    if (!a || !a->g3 || !a->dwk || !a->seg.x || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 ||
-        a->gpitch % 32 != 0 || a->seg.cpitch % 32 != 0 || a->seg.mode == SNNFLOW_UNET_MODE_T2 || a->ksize < 1)
-        SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: bad args");
-    const hipStream_t s = (hipStream_t)stream;
-    // tiles sized to the layer: m 32 / 64 / 128; k the first of 128, 160 (m <= 64: registers), 96, 64, 32
-    // whose padding of the segment's channel pitch stays within 1/5 (else the least padding) -- fewer
-    // wasted MFMAs and G loads on thin layers, wide tiles elsewhere
-    const int tm = a->M <= 32 ? 32 : (a->M <= 64 ? 64 : 128);
-    const int cp = a->seg.cpitch;
-    int tk = 0, best = 1 << 30, tbest = 32;
+// Tile of a launch: m 32 / 64 / 128; k the first of 128, 160 (m <= 64: registers), 96, 64, 32 whose
+// padding of the segment's channel pitch stays within 1/5 (else the least padding) -- fewer wasted
+// MFMAs and G loads on thin layers, wide tiles elsewhere.
+void wgrad_tile(const snnflow_unet_wgrad_args& a, int& tk, int& tm) {
+    tm = a.M <= 32 ? 32 : (a.M <= 64 ? 64 : 128);
+    const int cp = a.seg.cpitch;
+    int best = 1 << 30, tbest = 32;
+    tk = 0;
     for (int c : {128, 160, 96, 64, 32}) {
         if (c == 160 && tm > 64) continue;
         const int padded = (cp + c - 1) / c * c;
@@ -1189,14 +1232,43 @@ int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
         }
     }
     if (tk == 0) tk = tbest;
-#define WG_CASE(K_, M_) \
-    if (tk == K_ && tm == M_) return launch_wgrad<K_, M_>(*a, s);
-    WG_CASE(160, 32) WG_CASE(160, 64) WG_CASE(160, 128)
-    WG_CASE(128, 32) WG_CASE(128, 64) WG_CASE(128, 128)
-    WG_CASE(96, 32) WG_CASE(96, 64) WG_CASE(96, 128)
-    WG_CASE(64, 32) WG_CASE(64, 64) WG_CASE(64, 128)
-    WG_CASE(32, 32) WG_CASE(32, 64) WG_CASE(32, 128)
-#undef WG_CASE
+}
+
+#define WG_DISPATCH(FN, ARGS)                                                        \
+    {                                                                               \
+        int tk, tm;                                                                 \
+        wgrad_tile(*a, tk, tm);                                                     \
+        if (tk == 160 && tm == 32) return FN<160, 32> ARGS;                                 \
+        if (tk == 160 && tm == 64) return FN<160, 64> ARGS;                                 \
+        if (tk == 128 && tm == 32) return FN<128, 32> ARGS;                                 \
+        if (tk == 128 && tm == 64) return FN<128, 64> ARGS;                                 \
+        if (tk == 128 && tm == 128) return FN<128, 128> ARGS;                               \
+        if (tk == 96 && tm == 32) return FN<96, 32> ARGS;                                   \
+        if (tk == 96 && tm == 64) return FN<96, 64> ARGS;                                   \
+        if (tk == 96 && tm == 128) return FN<96, 128> ARGS;                                 \
+        if (tk == 64 && tm == 32) return FN<64, 32> ARGS;                                   \
+        if (tk == 64 && tm == 64) return FN<64, 64> ARGS;                                   \
+        if (tk == 64 && tm == 128) return FN<64, 128> ARGS;                                 \
+        if (tk == 32 && tm == 32) return FN<32, 32> ARGS;                                   \
+        if (tk == 32 && tm == 64) return FN<32, 64> ARGS;                                   \
+        if (tk == 32 && tm == 128) return FN<32, 128> ARGS;                                 \
+    }
+}  // namespace
+
+extern "C" {
+
+int64_t snnflow_unet_wgrad_partial_floats(const snnflow_unet_wgrad_args* a) {
+    if (!a || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 || a->seg.cpitch <= 0 || a->ksize < 1) return 0;
+    WG_DISPATCH(wgrad_partial_floats, (*a))
+    return 0;
+}
+
+int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
+    if (!a || !a->g3 || !a->dwk || !a->seg.x || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 ||
+        a->gpitch % 32 != 0 || a->seg.cpitch % 32 != 0 || a->seg.mode == SNNFLOW_UNET_MODE_T2 || a->ksize < 1)
+        SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: bad args");
+    const hipStream_t s = (hipStream_t)stream;
+    WG_DISPATCH(launch_wgrad, (*a, s))
     SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: no tile");
 }
 

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 
 class Neuron(ctypes.Structure):
@@ -186,7 +186,7 @@ class UNetConvArgs(ctypes.Structure):
 class UNetWgradArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("Ho", I32), ("Wo", I32), ("M", I32), ("ksize", I32),
                 ("g3", P), ("gpitch", I32), ("gpart", I64), ("seg", UNetSeg), ("k0", I32), ("ktot", I32),
-                ("dwk", P)]
+                ("dwk", P), ("partial", P)]
 
 
 class UNetLifBwdArgs(ctypes.Structure):
@@ -287,6 +287,7 @@ EXPORTS = {
     "snnflow_unet_conv_ksplit": (I32, [ctypes.POINTER(UNetConvArgs)]),
     "snnflow_unet_prep_weights": (I32, [P, I32, I32, I32, P, I32, I32, I32, I32, I32, I32, I32, P, P]),
     "snnflow_unet_wgrad": (I32, [ctypes.POINTER(UNetWgradArgs), P]),
+    "snnflow_unet_wgrad_partial_floats": (I64, [ctypes.POINTER(UNetWgradArgs)]),
     "snnflow_unet_wgrad_finalize": (I32, [P, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
     "snnflow_unet_lif_bwd": (I32, [ctypes.POINTER(UNetLifBwdArgs), P]),
     "snnflow_unet_cell_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),

@@ -380,6 +380,14 @@ def _name(kind, M, K, P):
     return f"{kind}[M{M} K{K} P{P}]" if _SHAPES else kind
 
 
+def _workspace(n, dev):
+    buf = _PARTIAL.get(dev)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(n, device=dev)
+        _PARTIAL[dev] = buf
+    return buf
+
+
 def _split_k(a, P, dev):
     """Split-K of a launch (library's choice) with the shared partial-sum workspace (stream-ordered
     reuse; sized by the largest request, which the eager warm-up steps make before any graph capture)."""
@@ -387,12 +395,7 @@ def _split_k(a, P, dev):
     if ks <= 1:
         a.ksplit, a.partial = 1, None
         return
-    n = ks * P * a.M
-    buf = _PARTIAL.get(dev)
-    if buf is None or buf.numel() < n:
-        buf = torch.empty(n, device=dev)
-        _PARTIAL[dev] = buf
-    a.ksplit, a.partial = ks, buf.data_ptr()
+    a.ksplit, a.partial = ks, _workspace(ks * P * a.M, dev).data_ptr()
 
 
 def conv_lif(plan, B, Ho, Wo, acts, prev_state, residual, state, current, act_out, s):
@@ -452,6 +455,8 @@ def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
     a.g3, a.gpitch, a.gpart = ptr(g3), g3.shape[-1], g3[0].numel()
     a.seg = _unet_seg(act, sg.mode, sg.kc0)
     a.k0, a.ktot, a.dwk = sg.k0, plan.ktot, ptr(plan.dwk)
+    n = lib.snnflow_unet_wgrad_partial_floats(ctypes.byref(a))  # deterministic split sums
+    a.partial = _workspace(n, plan.dwk.device).data_ptr() if n > 0 else None
     _lib.call(_name("unet_wgrad", plan.C, a.seg.cpitch, B * Ho * Wo), lib.snnflow_unet_wgrad, ctypes.byref(a), s,
               work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
 
