@@ -1085,7 +1085,7 @@ int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
 // Output tiles of a launch for its tile configuration (the selection of snnflow_unet_conv).
 inline void conv_tile(const snnflow_unet_conv_args& a, int& bm, int& bn) {
     if (a.xparts == 3) {
-        bm = a.M > 64 ? 128 : (a.M > 32 ? 64 : 32);
+        bm = (a.M > 128 && a.M <= 160) ? 160 : (a.M > 64 ? 128 : (a.M > 32 ? 64 : 32));
         bn = a.M > 32 ? 128 : 256;
     } else if (a.M > 64) {
         bm = 128; bn = 128;
@@ -1150,6 +1150,7 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
         SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: parity classes are for one transposed stride-2 segment");
     const hipStream_t s = (hipStream_t)stream;
     if (a->xparts == 3) {  // input gradients: the fp32 gradient as three bf16 planes
+        if (a->M > 128 && a->M <= 160) return launch_conv<5, 2, 3>(*a, s);
         if (a->M > 64) return launch_conv<4, 2, 3>(*a, s);
         if (a->M > 32) return launch_conv<2, 2, 3>(*a, s);
         return launch_conv<2, 1, 3>(*a, s);
