@@ -61,7 +61,10 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 // images layout: [dir 2][img 4][B][HW].
 // Events of a sample are dealt to SPLAT_SPLIT blocks per band; each writes its own partial
 // image set (images + split * 8*B*HW), summed in fixed order by k_iwe_loss.
-constexpr int SPLAT_NT = 1024, SPLAT_BAND = 4096, SPLAT_SPLIT = 4;
+#ifndef SNNFLOW_SPLAT_SPLIT
+#define SNNFLOW_SPLAT_SPLIT 4
+#endif
+constexpr int SPLAT_NT = 1024, SPLAT_BAND = 4096, SPLAT_SPLIT = SNNFLOW_SPLAT_SPLIT;
 
 __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands) {
     __shared__ float img[4][SPLAT_BAND];
@@ -108,59 +111,35 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
         for (int j = tid; j < np; j += SPLAT_NT) out[(int64_t)q * imgsz + j] = img[q][j];
 }
 
-// Smoothness terms where pixel (h,w) of window t is the first element 'a' of the pair.
-struct SmoothTerms { float v[5]; };
-
 __device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
 
-__device__ inline SmoothTerms smooth_at(const snnflow_iwe_loss_args& a, int b, int t, int h, int w) {
-    const int64_t HWp = (int64_t)a.H * a.W;
-    const float* fx = flow_of(a, b, t);
-    const float* fy = fx + HWp;
-    const float* m = mask_of(a, b, t);
-    const int p = h * a.W + w;
-    SmoothTerms r;
-    const bool sm = a.smoothing_mask != 0;
-    auto term = [&](int pb, const float* fxb, const float* fyb, const float* mb) {
-        const float d = (fx[p] - fxb[pb]) + (fy[p] - fyb[pb]);
-        const float c = charb(d);
-        return sm ? (m[p] * mb[pb]) * c : c;
-    };
-    r.v[0] = (w + 1 < a.W) ? term(p + 1, fx, fy, m) : 0.0f;                         // dx
-    r.v[1] = (h + 1 < a.H) ? term(p + a.W, fx, fy, m) : 0.0f;                       // dy
-    r.v[2] = (h + 1 < a.H && w + 1 < a.W) ? term(p + a.W + 1, fx, fy, m) : 0.0f;    // dxdy_dr
-    r.v[3] = (h >= 1 && w + 1 < a.W) ? term(p - a.W + 1, fx, fy, m) : 0.0f;         // dxdy_ur
-    r.v[4] = 0.0f;                                                                  // dt
-    if (t + 1 < a.tf && !a.overwrite_intermediate) {
-        const float* fx2 = flow_of(a, b, t + 1);
-        r.v[4] = term(p, fx2, fx2 + HWp, mask_of(a, b, t + 1));
-    }
-    return r;
+// Per (sample, range of windows, chunk of NT pixels): IWE loss terms of both directions
+// (first-range blocks) + the smoothness terms of the range's windows, reduced per block and
+// stored as one row of partial sums acc[block][LOSS_NV] (no atomics; k_iwe_finalize sums rows
+// in fixed order).  Row: {S+, S-, nz} x {fw, bw}, then the five smoothness sums.
+// The window loop carries the centre pixel of window t+1 (needed by the dt term) into the next
+// iteration, so every flow / mask map is read once per pixel instead of twice.
+constexpr int LOSS_NV = 11;
+constexpr int LOSS_MIN_BLOCKS = 2048;  // split the window loop until the grid has this many blocks
+
+__host__ __device__ inline int loss_chunks(int64_t HWp) { return (int)((HWp + NT - 1) / NT); }
+__host__ __device__ inline int loss_tsplit(int B, int64_t HWp, int tf) {
+    const int64_t base = (int64_t)B * loss_chunks(HWp);
+    const int64_t s = (LOSS_MIN_BLOCKS + base - 1) / base;
+    return s < 1 ? 1 : (s > tf ? tf : (int)s);
 }
 
-// Per (sample, window t, chunk of NT pixels): IWE loss terms of both directions (t == 0
-// blocks) + the smoothness terms of window t, reduced per block and stored as one row of
-// partial sums acc[block][LOSS_NV] (no atomics; k_iwe_finalize sums rows in fixed order).
-// Row: {S+, S-, nz} x {fw, bw}, then the five smoothness sums.
-constexpr int LOSS_NV = 11;
-
-// Each block covers LOSS_CPB chunks of NT pixels of one (sample, window): one partial row
-// per LOSS_CPB * NT pixels keeps the fixed-order reduction in k_iwe_finalize short.
-constexpr int LOSS_CPB = 4;
-
-__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int groups) {
+__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit) {
     __shared__ float red[NT / 64][LOSS_NV];
-    const int tid = threadIdx.x, grp = blockIdx.x % groups, t = (blockIdx.x / groups) % a.tf,
-              b = blockIdx.x / (groups * a.tf);
+    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, tg = (blockIdx.x / chunks) % tsplit,
+              b = blockIdx.x / (chunks * tsplit);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     float v[LOSS_NV];
 #pragma unroll
     for (int j = 0; j < LOSS_NV; ++j) v[j] = 0.0f;
-#pragma unroll
-    for (int cc = 0; cc < LOSS_CPB; ++cc) {
-        const int p = (grp * LOSS_CPB + cc) * NT + tid;
-        if (p >= HWp) break;
-        if (t == 0) {
+    const int p = chunk * NT + tid;
+    if (p < HWp) {
+        if (tg == 0) {
             const float T = (float)a.T;
 #pragma unroll
             for (int d = 0; d < 2; ++d) {
@@ -185,9 +164,33 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int gr
             }
         }
         const int h = p / a.W, w = p - h * a.W;
-        const SmoothTerms sm = smooth_at(a, b, t, h, w);
-#pragma unroll
-        for (int j = 0; j < 5; ++j) v[6 + j] += sm.v[j];
+        const bool right = w + 1 < a.W, down = h + 1 < a.H, up = h >= 1, sm = a.smoothing_mask != 0;
+        const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
+        const float* f0 = flow_of(a, b, t0);
+        float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
+        for (int t = t0; t < t1; ++t) {
+            const float* fx = flow_of(a, b, t);
+            const float* fy = fx + HWp;
+            const float* m = mask_of(a, b, t);
+            // pair ('a' = centre of window t, 'b' = (bx, by, bm)): masked Charbonnier term
+            auto term = [&](float bx, float by, float bm) {
+                const float dd = (cx - bx) + (cy - by);
+                const float c = charb(dd);
+                return sm ? (cm * bm) * c : c;
+            };
+            if (right) v[6] += term(fx[p + 1], fy[p + 1], m[p + 1]);                        // dx
+            if (down) v[7] += term(fx[p + a.W], fy[p + a.W], m[p + a.W]);                   // dy
+            if (down && right) v[8] += term(fx[p + a.W + 1], fy[p + a.W + 1], m[p + a.W + 1]);  // dxdy_dr
+            if (up && right) v[9] += term(fx[p - a.W + 1], fy[p - a.W + 1], m[p - a.W + 1]);    // dxdy_ur
+            if (t + 1 < a.tf) {
+                const float* f2 = flow_of(a, b, t + 1);
+                const float nx = f2[p], ny = f2[HWp + p], nm = mask_of(a, b, t + 1)[p];
+                if (!a.overwrite_intermediate) v[10] += term(nx, ny, nm);                    // dt
+                cx = nx;
+                cy = ny;
+                cm = nm;
+            }
+        }
     }
     const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
@@ -209,11 +212,10 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int gr
 // of samples w, w + 16, ... (all 11 columns), then the smoothness sums add up over samples.
 constexpr int FIN_NT = 1024;
 
-__global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int groups) {
+__global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int rows_b) {
     __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
     __shared__ double smp[64][5];          // per-sample smoothness sums
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int rows_b = groups * a.tf;
     // wave w reduces samples w, w + 16, ...: lane-strided rows, all 11 columns at once
     for (int b = wv; b < a.B; b += FIN_NT / 64) {
         double s[LOSS_NV];
@@ -268,18 +270,19 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
     a.loss[0] = total + a.weight * sm;
 }
 
-// Per (sample, window t, pixel): dL/d(images) for both directions (t == 0 blocks) and the
-// smoothness part of dL/dflow_t (plain stores: g_flows is fully written here; the events
-// add into it afterwards).
+// Per (sample, range of windows, pixel): dL/d(images) for both directions (first-range blocks)
+// and the smoothness part of dL/dflow_t (plain stores: g_flows is fully written here; the
+// events add into it afterwards).  As in k_iwe_loss the window loop carries the centre pixel
+// of window t+1, and the dt pair (t, t+1) is differentiated once: +g for window t, -g for t+1.
 __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
-                                                        float* g_flows, int chunks) {
-    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, t = (blockIdx.x / chunks) % a.tf,
-              b = blockIdx.x / (chunks * a.tf);
+                                                        float* g_flows, int chunks, int tsplit) {
+    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, tg = (blockIdx.x / chunks) % tsplit,
+              b = blockIdx.x / (chunks * tsplit);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
     if (p >= HWp) return;
     const float g = g_loss[0];
-    if (t == 0) {
+    if (tg == 0) {
         const float T = (float)a.T;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
@@ -309,40 +312,58 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
     const int comps = a.overwrite_intermediate ? 4 : 5;
     const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
     const int h = p / a.W, w = p - h * a.W;
-    const bool sm = a.smoothing_mask != 0;
-    const float* fx = flow_of(a, b, t);
-    const float* fy = fx + HWp;
-    const float* m = mask_of(a, b, t);
-    float acc = 0.0f;
-    // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
-    auto pairgrad = [&](const float* fxa, const float* fya, const float* ma, int pa, const float* fxb,
-                        const float* fyb, const float* mb, int pb) {
-        const float dd = (fxa[pa] - fxb[pb]) + (fya[pa] - fyb[pb]);
+    const bool sm = a.smoothing_mask != 0, dt_terms = !a.overwrite_intermediate;
+    // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
+    auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
+        const float dd = (ax - bx) + (ay - by);
         const float c = charb(dd);
-        const float mk = sm ? ma[pa] * mb[pb] : 1.0f;
+        const float mk = sm ? am * bm : 1.0f;
         return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
     };
-    if (w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + 1);
-    if (w >= 1) acc -= pairgrad(fx, fy, m, p - 1, fx, fy, m, p);
-    if (h + 1 < a.H) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W);
-    if (h >= 1) acc -= pairgrad(fx, fy, m, p - a.W, fx, fy, m, p);
-    if (h + 1 < a.H && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p + a.W + 1);
-    if (h >= 1 && w >= 1) acc -= pairgrad(fx, fy, m, p - a.W - 1, fx, fy, m, p);
-    if (h >= 1 && w + 1 < a.W) acc += pairgrad(fx, fy, m, p, fx, fy, m, p - a.W + 1);
-    if (h + 1 < a.H && w >= 1) acc -= pairgrad(fx, fy, m, p + a.W - 1, fx, fy, m, p);
-    if (!a.overwrite_intermediate) {
-        if (t + 1 < a.tf) {
-            const float* fx2 = flow_of(a, b, t + 1);
-            acc += pairgrad(fx, fy, m, p, fx2, fx2 + HWp, mask_of(a, b, t + 1), p);
-        }
-        if (t >= 1) {
-            const float* fx0 = flow_of(a, b, t - 1);
-            acc -= pairgrad(fx0, fx0 + HWp, mask_of(a, b, t - 1), p, fx, fy, m, p);
-        }
+    const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
+    const float* f0 = flow_of(a, b, t0);
+    float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
+    float gprev = 0.0f;  // gradient of the dt pair (t-1, t) w.r.t. window t-1
+    if (dt_terms && t0 >= 1) {
+        const float* fp = flow_of(a, b, t0 - 1);
+        gprev = pg(fp[p], fp[HWp + p], mask_of(a, b, t0 - 1)[p], cx, cy, cm);
     }
-    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
-    gf[p] = acc;
-    gf[HWp + p] = acc;
+    for (int t = t0; t < t1; ++t) {
+        const float* fx = flow_of(a, b, t);
+        const float* fy = fx + HWp;
+        const float* m = mask_of(a, b, t);
+        float acc = 0.0f;
+        // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
+        auto fwd = [&](int q) { return pg(cx, cy, cm, fx[q], fy[q], m[q]); };
+        auto bwd = [&](int q) { return pg(fx[q], fy[q], m[q], cx, cy, cm); };
+        if (w + 1 < a.W) acc += fwd(p + 1);
+        if (w >= 1) acc -= bwd(p - 1);
+        if (h + 1 < a.H) acc += fwd(p + a.W);
+        if (h >= 1) acc -= bwd(p - a.W);
+        if (h + 1 < a.H && w + 1 < a.W) acc += fwd(p + a.W + 1);
+        if (h >= 1 && w >= 1) acc -= bwd(p - a.W - 1);
+        if (h >= 1 && w + 1 < a.W) acc += fwd(p - a.W + 1);
+        if (h + 1 < a.H && w >= 1) acc -= bwd(p + a.W - 1);
+        float nx = 0.0f, ny = 0.0f, nm = 0.0f, gnext = 0.0f;
+        if (t + 1 < a.tf) {
+            const float* f2 = flow_of(a, b, t + 1);
+            nx = f2[p];
+            ny = f2[HWp + p];
+            nm = mask_of(a, b, t + 1)[p];
+            if (dt_terms) {
+                gnext = pg(cx, cy, cm, nx, ny, nm);
+                acc += gnext;
+            }
+        }
+        if (dt_terms && t >= 1) acc -= gprev;
+        float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+        gf[p] = acc;
+        gf[HWp + p] = acc;
+        gprev = gnext;
+        cx = nx;
+        cy = ny;
+        cm = nm;
+    }
 }
 
 // Per event: gather dL/d(images) at the 4 corners of both warps, chain through the
@@ -500,8 +521,8 @@ extern "C" {
 int snnflow_iwe_scratch_floats(int B, int H, int W) { return SPLAT_SPLIT * 8 * B * H * W; }
 
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
-    const int64_t groups = ((int64_t)H * W + LOSS_CPB * NT - 1) / (LOSS_CPB * NT);
-    return (int)((int64_t)B * tf * groups * LOSS_NV);
+    const int64_t HWp = (int64_t)H * W;
+    return (int)((int64_t)B * loss_tsplit(B, HWp, tf) * loss_chunks(HWp) * LOSS_NV);
 }
 
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
@@ -510,9 +531,9 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     const int64_t HWp = (int64_t)a->H * a->W;
     const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
     hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands * SPLAT_SPLIT), dim3(SPLAT_NT), 0, s, *a, nbands);
-    const int groups = (int)((HWp + LOSS_CPB * NT - 1) / (LOSS_CPB * NT));
-    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * a->tf * groups), dim3(NT), 0, s, *a, groups);
-    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, groups);
+    const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
+    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit);
+    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, tsplit * chunks);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -523,9 +544,9 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
-    const int chunks = (int)((HWp + NT - 1) / NT);
-    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * a->tf * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
-                       chunks);
+    const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
+    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
+                       chunks, tsplit);
     if (a->M > 0)
         hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a, gimg,
                            g_flows);
