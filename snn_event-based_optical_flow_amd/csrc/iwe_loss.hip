@@ -24,6 +24,15 @@ int snnflow_set_error(int code, const char* msg);
 
 namespace {
 
+// Bijective XCD-aware block order: consecutive logical blocks land on one XCD (blocks b and b+8
+// share an XCD under round-robin dispatch), so the neighbouring rows one block reads that the
+// next block owns, or a sample's events and images, stay in that XCD's L2.
+__device__ inline int xcd_block() {
+    const int bid = blockIdx.x, nb = gridDim.x;
+    const int x = bid % 8, q = nb / 8, r = nb % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
 __device__ inline int pass_of(const int32_t* off, int T, int i) {
     int k = 0;
     while (k + 1 < T && i >= off[k + 1]) ++k;
@@ -69,7 +78,8 @@ constexpr int SPLAT_NT = 1024, SPLAT_BAND = 4096, SPLAT_SPLIT = SNNFLOW_SPLAT_SP
 __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands) {
     __shared__ float img[4][SPLAT_BAND];
     const int tid = threadIdx.x;
-    const int split = blockIdx.x % SPLAT_SPLIT, rest = blockIdx.x / SPLAT_SPLIT;
+    const int blk = xcd_block();
+    const int split = blk % SPLAT_SPLIT, rest = blk / SPLAT_SPLIT;
     const int band = rest % nbands, d = (rest / nbands) % 2, b = rest / (2 * nbands);
     const int64_t HWp = (int64_t)a.H * a.W, imgsz = (int64_t)a.B * HWp;
     const int p0 = band * SPLAT_BAND;
@@ -131,8 +141,8 @@ __host__ __device__ inline int loss_tsplit(int B, int64_t HWp, int tf) {
 
 __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit) {
     __shared__ float red[NT / 64][LOSS_NV];
-    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, tg = (blockIdx.x / chunks) % tsplit,
-              b = blockIdx.x / (chunks * tsplit);
+    const int blk = xcd_block();
+    const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     float v[LOSS_NV];
 #pragma unroll
@@ -203,7 +213,7 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
         double s = 0.0;
 #pragma unroll
         for (int w2 = 0; w2 < NT / 64; ++w2) s += (double)red[w2][tid];
-        a.acc[(int64_t)blockIdx.x * LOSS_NV + tid] = s;
+        a.acc[(int64_t)blk * LOSS_NV + tid] = s;
     }
 }
 
@@ -276,8 +286,8 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
 // of window t+1, and the dt pair (t, t+1) is differentiated once: +g for window t, -g for t+1.
 __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
                                                         float* g_flows, int chunks, int tsplit) {
-    const int tid = threadIdx.x, chunk = blockIdx.x % chunks, tg = (blockIdx.x / chunks) % tsplit,
-              b = blockIdx.x / (chunks * tsplit);
+    const int blk = xcd_block();
+    const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
     if (p >= HWp) return;
@@ -373,7 +383,8 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
     const int64_t HWp = (int64_t)a.H * a.W;
     const int64_t n = (int64_t)a.B * a.M;
     const int64_t img = (int64_t)a.B * HWp;
-    for (int64_t e = (int64_t)blockIdx.x * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
+    // XCD-ordered blocks: a sample's events (and so its image gathers) on one XCD's L2
+    for (int64_t e = (int64_t)xcd_block() * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
         const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
         const EventRef r = event_ref(a, b, i);
         const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
@@ -548,7 +559,7 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
                        chunks, tsplit);
     if (a->M > 0)
-        hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M, NT, 8192)), dim3(NT), 0, s, *a, gimg,
+        hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M, NT, 65536)), dim3(NT), 0, s, *a, gimg,
                            g_flows);
     SNN_CHECK_LAUNCH();
     return 0;

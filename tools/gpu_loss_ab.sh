@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
   -k "warping or iwe or cfg2_train_step or forward_sequence_matches" tests/ > gpurun_out/loss/tests.txt 2>&1 || { tail -30 gpurun_out/loss/tests.txt; exit 3; }
 tail -3 gpurun_out/loss/tests.txt
 export TMPDIR=/tmp
-for v in "" split2 split1; do
+for v in ${VARIANTS:-""}; do
   unset SNNFLOW_LIB; [ -n "$v" ] && export SNNFLOW_LIB=$GRAFT_REPO_ROOT/snn_event-based_optical_flow_amd/snnflow/libsnnflow_$v.so
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/loss/ks_${v:-base} -o run --output-format csv -- python3 tools/prof_step.py > gpurun_out/loss/ks_${v:-base}.log 2>&1 || exit 3
   f=$(find gpurun_out/loss/ks_${v:-base} -name "*kernel_stats.csv" | head -1)
