@@ -617,6 +617,168 @@ __global__ void k_unet_wgrad_reduce(snnflow_unet_wgrad_args a, int nsplit, int K
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Tap-fused weight gradient of a stride-1 3x3 conv on 64-pixel row strips (Wo % 64 == 0): one block
+// owns a TK x TM (k x m) tile of all nine taps, so X and G are read once per k/m tile instead of
+// once per tap (k_unet_wgrad re-reads them nine times; at 256^2 and 128^2 that re-read is the
+// HBM traffic).  Per strip (image b, output row oy, columns x0 .. x0+63) the LDS holds X rows
+// oy-1 .. oy+1, columns x0-1 .. x0+64, pixel-major [row][pixel][k], and the three G planes
+// [part][pixel][m], both copied with plain 16-B loads; the MFMA operands (reduction = pixels)
+// come out column-major through ds_read_b64_tr_b16, and a tap is a shift of the X pixel rows.
+// 4 waves as WK x WM, each NI x NJ 16x16 tiles of every tap (9 * NI * NJ accumulators).
+// ---------------------------------------------------------------------------------------------
+template <int NI, int NJ, int WK, int WM>
+struct WrGeo {
+    static constexpr int TK = 16 * NI * WK, TM = 16 * NJ * WM;
+    static constexpr int XS = TK + 8, GS = TM + 8;  // bf16 per LDS pixel row (16-B multiple)
+    static constexpr int XROWS = 72;                 // 66 pixels of a strip's halo row, padded
+    static constexpr int XQ = TK / 8, GQ = TM / 8;   // 16-B pieces per pixel
+    static constexpr int XPIECES = 3 * 66 * XQ, GPIECES = 3 * 64 * GQ;
+    static constexpr int XR = (XPIECES + UNT - 1) / UNT, GR = (GPIECES + UNT - 1) / UNT;
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// ds_read_b64_tr_b16 pair -> one 16x16x32 operand: lane (16 g + i) receives column i of the 8
+// pixel rows starting at `rows` (the two 4-row blocks), 8 consecutive reduction elements.
+__device__ inline bf16x8 tr_operand(const __bf16* rows, int stride, int col0) {
+    const int lane = threadIdx.x & 63, q = (lane & 15) >> 2, pp = lane & 3;
+    const __bf16* p0 = rows + q * stride + col0 + 4 * pp;
+    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
+    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * stride));
+    const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int NI, int NJ, int WK, int WM>
+__global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args a, int ktiles, int mtiles, int nsplit,
+                                                         int spb) {
+    using G = WrGeo<NI, NJ, WK, WM>;
+    constexpr int TK = G::TK, TM = G::TM, XS = G::XS, GS = G::GS, XROWS = G::XROWS;
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[3 * XROWS * XS];
+    __shared__ __attribute__((aligned(16))) __bf16 Gs[3 * 64 * GS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wk = wave % WK, wm = wave / WK;
+    int b = xcd_remap(blockIdx.x, (int)gridDim.x);
+    const int split = b % nsplit;
+    b /= nsplit;
+    const int mt = b % mtiles, kt = b / mtiles;
+    const int H = a.Ho, W = a.Wo, spr = W / 64;
+    const int nstrips = a.B * H * spr;
+    const int s0 = split * spb, s1 = s0 + spb < nstrips ? s0 + spb : nstrips;
+    const snnflow_unet_seg& sg = a.seg;
+    const int kbase = kt * TK, mbase = mt * TM, cp = sg.cpitch;
+    const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+
+    fx4 acc[9][NI][NJ];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[t][i][j] = fx4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 xr[G::XR], gr[G::GR];
+    auto load = [&](int st) {
+        const int xs_ = st % spr, rest = st / spr, oy = rest % H, bb = rest / H, x0 = xs_ * 64;
+#pragma unroll
+        for (int r = 0; r < G::XR; ++r) {
+            const int e = tid + r * UNT;
+            const int row = e / (66 * G::XQ), rem = e - row * (66 * G::XQ), j = rem / G::XQ, c8 = rem - j * G::XQ;
+            const int iy = oy + row - 1, ix = x0 - 1 + j, kk = kbase + 8 * c8;
+            const bool ok = e < G::XPIECES && iy >= 0 && iy < H && ix >= 0 && ix < W && kk < cp;
+            xr[r] = ld16(sg.x + (ok ? (((int64_t)bb * H + iy) * W + ix) * cp + kk : 0));
+            if (!ok) xr[r] = z4;
+        }
+#pragma unroll
+        for (int r = 0; r < G::GR; ++r) {
+            const int e = tid + r * UNT;
+            const int part = e / (64 * G::GQ), rem = e - part * (64 * G::GQ), j = rem / G::GQ, c8 = rem - j * G::GQ;
+            const int mm = mbase + 8 * c8;
+            const bool ok = e < G::GPIECES && mm < a.gpitch;
+            const int64_t n = ((int64_t)bb * H + oy) * W + x0 + j;
+            gr[r] = ld16(a.g3 + (ok ? part * a.gpart + n * a.gpitch + mm : 0));
+            if (!ok) gr[r] = z4;
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int r = 0; r < G::XR; ++r) {
+            const int e = tid + r * UNT;
+            if (e < G::XPIECES) {
+                const int row = e / (66 * G::XQ), rem = e - row * (66 * G::XQ), j = rem / G::XQ, c8 = rem - j * G::XQ;
+                *reinterpret_cast<uint4*>(&Xs[(row * XROWS + j) * XS + 8 * c8]) = xr[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < G::GR; ++r) {
+            const int e = tid + r * UNT;
+            if (e < G::GPIECES) {
+                const int part = e / (64 * G::GQ), rem = e - part * (64 * G::GQ), j = rem / G::GQ, c8 = rem - j * G::GQ;
+                *reinterpret_cast<uint4*>(&Gs[(part * 64 + j) * GS + 8 * c8]) = gr[r];
+            }
+        }
+    };
+
+    const int g4 = lane >> 4;
+    if (s0 < s1) load(s0);
+    for (int st = s0; st < s1; ++st) {
+        __syncthreads();
+        store();
+        __syncthreads();
+        if (st + 1 < s1) load(st + 1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int px = kk * 32 + g4 * 8;  // this lane group's first reduction pixel
+            bf16x8 bgf[3][NJ];
+#pragma unroll
+            for (int part = 0; part < 3; ++part)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+                    bgf[part][j] = tr_operand(&Gs[(part * 64 + px) * GS], GS, wm * (TM / WM) + j * 16);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    bf16x8 axf[NI];
+#pragma unroll
+                    for (int i = 0; i < NI; ++i)
+                        axf[i] = tr_operand(&Xs[(ky * XROWS + px + kx) * XS], XS, wk * (TK / WK) + i * 16);
+#pragma unroll
+                    for (int part = 2; part >= 0; --part)  // lo, mid, hi
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                            for (int i = 0; i < NI; ++i)
+                                acc[ky * 3 + kx][i][j] =
+                                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(axf[i], bgf[part][j], acc[ky * 3 + kx][i][j], 0, 0, 0);
+                }
+        }
+    }
+    // lane holds k rows 4 (lane >> 4) .. +3 and m column (lane & 15) of each 16 x 16 tile
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int k = kbase + wk * (TK / WK) + i * 16 + 4 * (lane >> 4);
+                const int m = mbase + wm * (TM / WM) + j * 16 + (lane & 15);
+                if (a.partial) {  // split partial tiles, summed in split order by k_unet_wgrad_reduce
+                    const int KP = ktiles * TK, MP = mtiles * TM;
+                    float* part = a.partial + ((int64_t)split * 9 + t) * KP * MP;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) part[(int64_t)(k + r) * MP + m] = acc[t][i][j][r];
+                } else if (m < a.M) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (k + r < cp) atomicAdd(a.dwk + ((int64_t)t * a.ktot + a.k0 + k + r) * a.M + m, acc[t][i][j][r]);
+                }
+            }
+}
+
 __global__ void k_unet_wgrad_finalize(const float* __restrict__ dwk, int ktot, const int* __restrict__ inv, int k0,
                                       int cout, int cin, int taps, int accumulate, float* __restrict__ dw) {
     const int64_t n = (int64_t)cout * cin * taps;
@@ -1215,6 +1377,62 @@ int launch_wgrad(const snnflow_unet_wgrad_args& a, hipStream_t s) {
     return 0;
 }
 
+// Tap-fused row-strip weight gradient (k_unet_wgrad_rows): stride-1 3x3 convs whose rows split
+// into 64-pixel strips.  SNNFLOW_UNET_WROWS=0 turns it off (A/B), read once.
+bool wrows_eligible(const snnflow_unet_wgrad_args& a) {
+    static const int on = [] {
+        const char* e = getenv("SNNFLOW_UNET_WROWS");
+        return e ? atoi(e) : 1;
+    }();
+    return on && a.seg.mode == SNNFLOW_UNET_MODE_S1 && a.ksize == 3 && a.Wo % 64 == 0 && a.seg.H == a.Ho &&
+           a.seg.W == a.Wo;
+}
+
+template <int NI, int NJ, int WK, int WM>
+WgPlan wrows_plan(const snnflow_unet_wgrad_args& a) {
+    using G = WrGeo<NI, NJ, WK, WM>;
+    WgPlan p;
+    p.ktiles = (a.seg.cpitch + G::TK - 1) / G::TK;
+    p.mtiles = (a.M + G::TM - 1) / G::TM;
+    p.tiles = (int64_t)p.ktiles * p.mtiles;
+    const int nstrips = a.B * a.Ho * (a.Wo / 64);
+    int ns = (int)((1024 + p.tiles - 1) / p.tiles);  // ~1024+ blocks, >= 4 strips each
+    if (ns > nstrips / 4) ns = nstrips / 4;
+    if (ns < 1) ns = 1;
+    p.steps = (nstrips + ns - 1) / ns;                 // strips per block
+    p.nsplit = (nstrips + p.steps - 1) / p.steps;
+    return p;
+}
+
+template <int NI, int NJ, int WK, int WM>
+int64_t wrows_partial_floats(const snnflow_unet_wgrad_args& a) {
+    using G = WrGeo<NI, NJ, WK, WM>;
+    const WgPlan p = wrows_plan<NI, NJ, WK, WM>(a);
+    return (int64_t)p.nsplit * 9 * p.ktiles * G::TK * p.mtiles * G::TM;
+}
+
+template <int NI, int NJ, int WK, int WM>
+int launch_wrows(const snnflow_unet_wgrad_args& a, hipStream_t s) {
+    using G = WrGeo<NI, NJ, WK, WM>;
+    const WgPlan p = wrows_plan<NI, NJ, WK, WM>(a);
+    hipLaunchKernelGGL((k_unet_wgrad_rows<NI, NJ, WK, WM>), dim3((unsigned)(p.tiles * p.nsplit)), dim3(UNT), 0, s, a,
+                       p.ktiles, p.mtiles, p.nsplit, p.steps);
+    if (a.partial) {
+        const int64_t n = (int64_t)9 * a.seg.cpitch * a.M;
+        hipLaunchKernelGGL(k_unet_wgrad_reduce, dim3(grid1d(n, 256, 4096)), dim3(256), 0, s, a, p.nsplit,
+                           p.ktiles * G::TK, p.mtiles * G::TM);
+    }
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+// M <= 32: 4 waves along k (64 x 32 tile); else 2 x 2 waves (32 x 64)
+#define WR_DISPATCH(FN, ARGS)                                    \
+    {                                                            \
+        if (a->M <= 32) return FN<1, 2, 4, 1> ARGS;              \
+        return FN<1, 2, 2, 2> ARGS;                              \
+    }
+
 // Tile of a launch: m 32 / 64 / 128; k the first of 128, 160 (m <= 64: registers), 96, 64, 32 whose
 // padding of the segment's channel pitch stays within 1/5 (else the least padding) -- fewer wasted
 // MFMAs and G loads on thin layers, wide tiles elsewhere.
@@ -1260,6 +1478,7 @@ extern "C" {
 
 int64_t snnflow_unet_wgrad_partial_floats(const snnflow_unet_wgrad_args* a) {
     if (!a || a->B <= 0 || a->Ho <= 0 || a->Wo <= 0 || a->M <= 0 || a->seg.cpitch <= 0 || a->ksize < 1) return 0;
+    if (wrows_eligible(*a)) WR_DISPATCH(wrows_partial_floats, (*a))
     WG_DISPATCH(wgrad_partial_floats, (*a))
     return 0;
 }
@@ -1269,6 +1488,7 @@ int snnflow_unet_wgrad(const snnflow_unet_wgrad_args* a, void* stream) {
         a->gpitch % 32 != 0 || a->seg.cpitch % 32 != 0 || a->seg.mode == SNNFLOW_UNET_MODE_T2 || a->ksize < 1)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: bad args");
     const hipStream_t s = (hipStream_t)stream;
+    if (wrows_eligible(*a)) WR_DISPATCH(launch_wrows, (*a, s))
     WG_DISPATCH(launch_wgrad, (*a, s))
     SNN_FAIL(SNNFLOW_E_ARG, "unet_wgrad: no tile");
 }
