@@ -603,6 +603,26 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad(snnflow_unet_wgrad_args a, i
         }
 }
 
+// First pass of a two-pass split reduction (many splits): chunk c of WG_RCHUNK consecutive splits
+// summed in split order into tmp[c][tap][k][m] (the layout of the partial tiles with KP = K, MP = M).
+constexpr int WG_RCHUNK = 16;
+__global__ void k_unet_wgrad_reduce_chunks(snnflow_unet_wgrad_args a, int nsplit, int KP, int MP, float* tmp) {
+    const int taps = a.ksize * a.ksize, K = a.seg.cpitch, M = a.M;
+    const int64_t n = (int64_t)taps * K * M;
+    const int nch = (nsplit + WG_RCHUNK - 1) / WG_RCHUNK;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * nch; e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e / n);
+        const int64_t o = e - (int64_t)c * n;
+        const int m = (int)(o % M);
+        const int64_t r = o / M;
+        const int k = (int)(r % K), tap = (int)(r / K);
+        const int sp1 = (c + 1) * WG_RCHUNK < nsplit ? (c + 1) * WG_RCHUNK : nsplit;
+        float sum = 0.0f;
+        for (int sp = c * WG_RCHUNK; sp < sp1; ++sp) sum += a.partial[(((int64_t)sp * taps + tap) * KP + k) * MP + m];
+        tmp[e] = sum;
+    }
+}
+
 // dwk[tap][k0 + k][m] += sum over the splits (fixed order) of the partial tiles.
 __global__ void k_unet_wgrad_reduce(snnflow_unet_wgrad_args a, int nsplit, int KP, int MP) {
     const int taps = a.ksize * a.ksize, K = a.seg.cpitch, M = a.M;
@@ -618,45 +638,45 @@ __global__ void k_unet_wgrad_reduce(snnflow_unet_wgrad_args a, int nsplit, int K
 }
 
 // ---------------------------------------------------------------------------------------------
-// Tap-fused weight gradient of a stride-1 3x3 conv on 64-pixel row strips (Wo % 64 == 0): one block
-// owns a TK x TM (k x m) tile of all nine taps, so X and G are read once per k/m tile instead of
-// once per tap (k_unet_wgrad re-reads them nine times; at 256^2 and 128^2 that re-read is the
-// HBM traffic).  Per strip (image b, output row oy, columns x0 .. x0+63) the LDS holds X rows
-// oy-1 .. oy+1, columns x0-1 .. x0+64, pixel-major [row][pixel][k], and the three G planes
-// [part][pixel][m], both copied with plain 16-B loads; the MFMA operands (reduction = pixels)
-// come out column-major through ds_read_b64_tr_b16, and a tap is a shift of the X pixel rows.
+// Tap-fused weight gradient of a 3x3 conv (stride S = 1 or 2) on strips of 64 output pixels: one
+// block owns a TK x TM (k x m) tile of all nine taps, so X and G are read once per k/m tile instead
+// of once per tap (k_unet_wgrad re-reads them nine times; at 256^2 and 128^2 that re-read is the HBM
+// traffic).  A strip is R = 64 / TW rows of TW = min(Wo, 64) output pixels; the LDS holds its input
+// halo (XH x XW pixels: (R + 2) x (TW + 2) at stride 1, (2R + 1) x (2TW + 1) at stride 2),
+// pixel-major [pixel][k], and the three G planes [part][pixel][m], both copied with plain 16-B
+// loads.  The MFMA operands (reduction = pixels) come out column-major through ds_read_b64_tr_b16,
+// every lane addressing its own pixel row, so a tap is an offset of those rows.
 // 4 waves as WK x WM, each NI x NJ 16x16 tiles of every tap (9 * NI * NJ accumulators).
 // ---------------------------------------------------------------------------------------------
-template <int NI, int NJ, int WK, int WM>
+template <int NI, int NJ, int WK, int WM, int S>
 struct WrGeo {
     static constexpr int TK = 16 * NI * WK, TM = 16 * NJ * WM;
-    static constexpr int XS = TK + 8, GS = TM + 8;  // bf16 per LDS pixel row (16-B multiple)
-    static constexpr int XROWS = 72;                 // 66 pixels of a strip's halo row, padded
-    static constexpr int XQ = TK / 8, GQ = TM / 8;   // 16-B pieces per pixel
-    static constexpr int XPIECES = 3 * 66 * XQ, GPIECES = 3 * 64 * GQ;
-    static constexpr int XR = (XPIECES + UNT - 1) / UNT, GR = (GPIECES + UNT - 1) / UNT;
+    static constexpr int XS = TK + 8, GS = TM + 8;    // bf16 per LDS pixel row (16-B multiple)
+    static constexpr int XPIX = S == 1 ? 198 : 387;   // halo pixels, largest strip shape (TW 64)
+    static constexpr int XQ = TK / 8, GQ = TM / 8;     // 16-B pieces per pixel
+    static constexpr int GPIECES = 3 * 64 * GQ;
+    static constexpr int XR = (XPIX * XQ + UNT - 1) / UNT, GR = (GPIECES + UNT - 1) / UNT;
 };
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// ds_read_b64_tr_b16 pair -> one 16x16x32 operand: lane (16 g + i) receives column i of the 8
-// pixel rows starting at `rows` (the two 4-row blocks), 8 consecutive reduction elements.
-__device__ inline bf16x8 tr_operand(const __bf16* rows, int stride, int col0) {
-    const int lane = threadIdx.x & 63, q = (lane & 15) >> 2, pp = lane & 3;
-    const __bf16* p0 = rows + q * stride + col0 + 4 * pp;
-    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0));
-    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p0 + 4 * stride));
+// ds_read_b64_tr_b16 pair -> one 16x16x32 operand: lane (16 g + i) receives column i of 8 pixel rows
+// (the rows lanes 4q+p of its group address in r0 (rows 0..3) and r1 (rows 4..7), 4p .. 4p+3
+// already added), 8 consecutive reduction elements.
+__device__ inline bf16x8 tr_pair(const __bf16* r0, const __bf16* r1) {
+    const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(r0));
+    const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(r1));
     const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int NI, int NJ, int WK, int WM>
+template <int NI, int NJ, int WK, int WM, int S>
 __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args a, int ktiles, int mtiles, int nsplit,
                                                          int spb) {
-    using G = WrGeo<NI, NJ, WK, WM>;
-    constexpr int TK = G::TK, TM = G::TM, XS = G::XS, GS = G::GS, XROWS = G::XROWS;
-    __shared__ __attribute__((aligned(16))) __bf16 Xs[3 * XROWS * XS];
+    using G = WrGeo<NI, NJ, WK, WM, S>;
+    constexpr int TK = G::TK, TM = G::TM, XS = G::XS, GS = G::GS;
+    __shared__ __attribute__((aligned(16))) __bf16 Xs[G::XPIX * XS];
     __shared__ __attribute__((aligned(16))) __bf16 Gs[3 * 64 * GS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -665,11 +685,16 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
     const int split = b % nsplit;
     b /= nsplit;
     const int mt = b % mtiles, kt = b / mtiles;
-    const int H = a.Ho, W = a.Wo, spr = W / 64;
-    const int nstrips = a.B * H * spr;
-    const int s0 = split * spb, s1 = s0 + spb < nstrips ? s0 + spb : nstrips;
+    const int H = a.Ho, W = a.Wo;
     const snnflow_unet_seg& sg = a.seg;
-    const int kbase = kt * TK, mbase = mt * TM, cp = sg.cpitch;
+    const int Hi = sg.H, Wi = sg.W, cp = sg.cpitch;
+    // strip geometry: TW output columns x R rows (TW a power of two, 8..64)
+    const int TW = W < 64 ? W : 64, lgw = 31 - __builtin_clz(TW), R = 64 >> lgw;
+    const int XW = S == 1 ? TW + 2 : 2 * TW + 1, XH = S == 1 ? R + 2 : 2 * R + 1, xpieces = XH * XW * G::XQ;
+    const int spr = W / TW, spi = (H / R) * spr;  // strips per strip-row, per image
+    const int nstrips = a.B * spi;
+    const int s0 = split * spb, s1 = s0 + spb < nstrips ? s0 + spb : nstrips;
+    const int kbase = kt * TK, mbase = mt * TM;
     const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
 
     fx4 acc[9][NI][NJ];
@@ -682,14 +707,15 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
 
     uint4 xr[G::XR], gr[G::GR];
     auto load = [&](int st) {
-        const int xs_ = st % spr, rest = st / spr, oy = rest % H, bb = rest / H, x0 = xs_ * 64;
+        const int bb = st / spi, rest = st - bb * spi, oy0 = (rest / spr) * R, x0 = (rest % spr) * TW;
+        const int iy0 = S * oy0 - 1, ix0 = S * x0 - 1;
 #pragma unroll
         for (int r = 0; r < G::XR; ++r) {
             const int e = tid + r * UNT;
-            const int row = e / (66 * G::XQ), rem = e - row * (66 * G::XQ), j = rem / G::XQ, c8 = rem - j * G::XQ;
-            const int iy = oy + row - 1, ix = x0 - 1 + j, kk = kbase + 8 * c8;
-            const bool ok = e < G::XPIECES && iy >= 0 && iy < H && ix >= 0 && ix < W && kk < cp;
-            xr[r] = ld16(sg.x + (ok ? (((int64_t)bb * H + iy) * W + ix) * cp + kk : 0));
+            const int pix = e / G::XQ, c8 = e - pix * G::XQ, row = pix / XW, j = pix - row * XW;
+            const int iy = iy0 + row, ix = ix0 + j, kk = kbase + 8 * c8;
+            const bool ok = e < xpieces && iy >= 0 && iy < Hi && ix >= 0 && ix < Wi && kk < cp;
+            xr[r] = ld16(sg.x + (ok ? (((int64_t)bb * Hi + iy) * Wi + ix) * cp + kk : 0));
             if (!ok) xr[r] = z4;
         }
 #pragma unroll
@@ -698,7 +724,8 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             const int part = e / (64 * G::GQ), rem = e - part * (64 * G::GQ), j = rem / G::GQ, c8 = rem - j * G::GQ;
             const int mm = mbase + 8 * c8;
             const bool ok = e < G::GPIECES && mm < a.gpitch;
-            const int64_t n = ((int64_t)bb * H + oy) * W + x0 + j;
+            // the strip's 64 output pixels are consecutive in G (whole rows when TW < W is false)
+            const int64_t n = ((int64_t)bb * H + oy0 + (j >> lgw)) * W + x0 + (j & (TW - 1));
             gr[r] = ld16(a.g3 + (ok ? part * a.gpart + n * a.gpitch + mm : 0));
             if (!ok) gr[r] = z4;
         }
@@ -707,9 +734,9 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
 #pragma unroll
         for (int r = 0; r < G::XR; ++r) {
             const int e = tid + r * UNT;
-            if (e < G::XPIECES) {
-                const int row = e / (66 * G::XQ), rem = e - row * (66 * G::XQ), j = rem / G::XQ, c8 = rem - j * G::XQ;
-                *reinterpret_cast<uint4*>(&Xs[(row * XROWS + j) * XS + 8 * c8]) = xr[r];
+            if (e < xpieces) {
+                const int pix = e / G::XQ, c8 = e - pix * G::XQ;
+                *reinterpret_cast<uint4*>(&Xs[pix * XS + 8 * c8]) = xr[r];
             }
         }
 #pragma unroll
@@ -722,7 +749,16 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
         }
     };
 
-    const int g4 = lane >> 4;
+    // this lane's pixel rows of the transposed reads: output pixel n = 32 kk + 8 g + q (+ 4)
+    const int g4 = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+    int xrow[2][2];  // [kk][half]: halo pixel of the tap (0, 0)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int n = kk * 32 + g4 * 8 + q + 4 * h, r = n >> lgw, c = n & (TW - 1);
+            xrow[kk][h] = S * r * XW + S * c;
+        }
     if (s0 < s1) load(s0);
     for (int st = s0; st < s1; ++st) {
         __syncthreads();
@@ -731,21 +767,26 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
         if (st + 1 < s1) load(st + 1);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            const int px = kk * 32 + g4 * 8;  // this lane group's first reduction pixel
+            const int gp = kk * 32 + g4 * 8 + q;  // G pixel row of this lane (first half)
             bf16x8 bgf[3][NJ];
 #pragma unroll
             for (int part = 0; part < 3; ++part)
 #pragma unroll
-                for (int j = 0; j < NJ; ++j)
-                    bgf[part][j] = tr_operand(&Gs[(part * 64 + px) * GS], GS, wm * (TM / WM) + j * 16);
+                for (int j = 0; j < NJ; ++j) {
+                    const __bf16* r0 = &Gs[(part * 64 + gp) * GS + wm * (TM / WM) + j * 16 + 4 * pp];
+                    bgf[part][j] = tr_pair(r0, r0 + 4 * GS);
+                }
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
+                    const int toff = ky * XW + kx;
                     bf16x8 axf[NI];
 #pragma unroll
-                    for (int i = 0; i < NI; ++i)
-                        axf[i] = tr_operand(&Xs[(ky * XROWS + px + kx) * XS], XS, wk * (TK / WK) + i * 16);
+                    for (int i = 0; i < NI; ++i) {
+                        const int col = wk * (TK / WK) + i * 16 + 4 * pp;
+                        axf[i] = tr_pair(&Xs[(xrow[kk][0] + toff) * XS + col], &Xs[(xrow[kk][1] + toff) * XS + col]);
+                    }
 #pragma unroll
                     for (int part = 2; part >= 0; --part)  // lo, mid, hi
 #pragma unroll
@@ -1342,6 +1383,30 @@ int snnflow_unet_prep_weights(const float* w, int cout, int cin, int ksize, cons
 namespace {
 struct WgPlan { int ktiles, mtiles, nsplit, steps; int64_t tiles; };
 
+// Floats of the split reduction's chunk sums behind the partial tiles (two passes above WG_RCHUNK splits).
+int64_t wgrad_tmp_floats(const snnflow_unet_wgrad_args& a, int nsplit) {
+    if (nsplit <= WG_RCHUNK) return 0;
+    return (int64_t)((nsplit + WG_RCHUNK - 1) / WG_RCHUNK) * a.ksize * a.ksize * a.seg.cpitch * a.M;
+}
+
+// dwk += the split sums of the partial tiles ([nsplit][taps][KP][MP] at a.partial), in split order;
+// above WG_RCHUNK splits through chunk sums (fixed association, so still deterministic).
+void launch_wgrad_reduce(const snnflow_unet_wgrad_args& a, int nsplit, int KP, int MP, int64_t partial_floats,
+                         hipStream_t s) {
+    const int64_t n = (int64_t)a.ksize * a.ksize * a.seg.cpitch * a.M;
+    if (nsplit <= WG_RCHUNK) {
+        hipLaunchKernelGGL(k_unet_wgrad_reduce, dim3(grid1d(n, 256, 4096)), dim3(256), 0, s, a, nsplit, KP, MP);
+        return;
+    }
+    const int nch = (nsplit + WG_RCHUNK - 1) / WG_RCHUNK;
+    float* tmp = a.partial + partial_floats;
+    hipLaunchKernelGGL(k_unet_wgrad_reduce_chunks, dim3(grid1d(n * nch, 256, 16384)), dim3(256), 0, s, a, nsplit, KP, MP,
+                       tmp);
+    snnflow_unet_wgrad_args b = a;
+    b.partial = tmp;
+    hipLaunchKernelGGL(k_unet_wgrad_reduce, dim3(grid1d(n, 256, 4096)), dim3(256), 0, s, b, nch, a.seg.cpitch, a.M);
+}
+
 template <int TK, int TM>
 WgPlan wgrad_plan(const snnflow_unet_wgrad_args& a) {
     WgPlan p;
@@ -1358,9 +1423,14 @@ WgPlan wgrad_plan(const snnflow_unet_wgrad_args& a) {
 }
 
 template <int TK, int TM>
-int64_t wgrad_partial_floats(const snnflow_unet_wgrad_args& a) {
+int64_t wgrad_tiles_floats(const snnflow_unet_wgrad_args& a) {
     const WgPlan p = wgrad_plan<TK, TM>(a);
     return (int64_t)p.nsplit * a.ksize * a.ksize * p.ktiles * TK * p.mtiles * TM;
+}
+
+template <int TK, int TM>
+int64_t wgrad_partial_floats(const snnflow_unet_wgrad_args& a) {
+    return wgrad_tiles_floats<TK, TM>(a) + wgrad_tmp_floats(a, wgrad_plan<TK, TM>(a).nsplit);
 }
 
 template <int TK, int TM>
@@ -1368,11 +1438,7 @@ int launch_wgrad(const snnflow_unet_wgrad_args& a, hipStream_t s) {
     const WgPlan p = wgrad_plan<TK, TM>(a);
     hipLaunchKernelGGL((k_unet_wgrad<TK, TM>), dim3((unsigned)(p.tiles * p.nsplit)), dim3(UNT), 0, s, a, p.ktiles,
                        p.mtiles, p.nsplit, p.steps);
-    if (a.partial) {
-        const int64_t n = (int64_t)a.ksize * a.ksize * a.seg.cpitch * a.M;
-        hipLaunchKernelGGL(k_unet_wgrad_reduce, dim3(grid1d(n, 256, 4096)), dim3(256), 0, s, a, p.nsplit,
-                           p.ktiles * TK, p.mtiles * TM);
-    }
+    if (a.partial) launch_wgrad_reduce(a, p.nsplit, p.ktiles * TK, p.mtiles * TM, wgrad_tiles_floats<TK, TM>(a), s);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -1384,53 +1450,60 @@ bool wrows_eligible(const snnflow_unet_wgrad_args& a) {
         const char* e = getenv("SNNFLOW_UNET_WROWS");
         return e ? atoi(e) : 1;
     }();
-    return on && a.seg.mode == SNNFLOW_UNET_MODE_S1 && a.ksize == 3 && a.Wo % 64 == 0 && a.seg.H == a.Ho &&
-           a.seg.W == a.Wo;
+    if (!on || a.ksize != 3 || a.Wo < 8 || (a.Wo % 64 != 0 && 64 % a.Wo != 0)) return false;
+    const int tw = a.Wo < 64 ? a.Wo : 64, r = 64 / tw;
+    if (a.Ho % r != 0) return false;
+    if (a.seg.mode == SNNFLOW_UNET_MODE_S1) return a.seg.H == a.Ho && a.seg.W == a.Wo;
+    // stride 2 (pad 1): input (2Ho or 2Ho - 1) x ..., 32 x 64 tiles only (X staging registers)
+    return a.seg.mode == SNNFLOW_UNET_MODE_S2 && a.M > 32 && (a.seg.H + 1) / 2 == a.Ho && (a.seg.W + 1) / 2 == a.Wo;
 }
 
-template <int NI, int NJ, int WK, int WM>
+template <int NI, int NJ, int WK, int WM, int S>
 WgPlan wrows_plan(const snnflow_unet_wgrad_args& a) {
-    using G = WrGeo<NI, NJ, WK, WM>;
+    using G = WrGeo<NI, NJ, WK, WM, S>;
     WgPlan p;
     p.ktiles = (a.seg.cpitch + G::TK - 1) / G::TK;
     p.mtiles = (a.M + G::TM - 1) / G::TM;
     p.tiles = (int64_t)p.ktiles * p.mtiles;
-    const int nstrips = a.B * a.Ho * (a.Wo / 64);
-    int ns = (int)((1024 + p.tiles - 1) / p.tiles);  // ~1024+ blocks, >= 4 strips each
-    if (ns > nstrips / 4) ns = nstrips / 4;
+    const int nstrips = a.B * a.Ho * a.Wo / 64;
+    int ns = (int)((1024 + p.tiles - 1) / p.tiles);  // ~1024+ blocks, >= 8 strips each (the partial
+    if (ns > nstrips / 8) ns = nstrips / 8;           // tile of a block is ~2 strips of input bytes)
     if (ns < 1) ns = 1;
     p.steps = (nstrips + ns - 1) / ns;                 // strips per block
     p.nsplit = (nstrips + p.steps - 1) / p.steps;
     return p;
 }
 
-template <int NI, int NJ, int WK, int WM>
-int64_t wrows_partial_floats(const snnflow_unet_wgrad_args& a) {
-    using G = WrGeo<NI, NJ, WK, WM>;
-    const WgPlan p = wrows_plan<NI, NJ, WK, WM>(a);
+template <int NI, int NJ, int WK, int WM, int S>
+int64_t wrows_tiles_floats(const snnflow_unet_wgrad_args& a) {
+    using G = WrGeo<NI, NJ, WK, WM, S>;
+    const WgPlan p = wrows_plan<NI, NJ, WK, WM, S>(a);
     return (int64_t)p.nsplit * 9 * p.ktiles * G::TK * p.mtiles * G::TM;
 }
 
-template <int NI, int NJ, int WK, int WM>
+template <int NI, int NJ, int WK, int WM, int S>
+int64_t wrows_partial_floats(const snnflow_unet_wgrad_args& a) {
+    return wrows_tiles_floats<NI, NJ, WK, WM, S>(a) + wgrad_tmp_floats(a, wrows_plan<NI, NJ, WK, WM, S>(a).nsplit);
+}
+
+template <int NI, int NJ, int WK, int WM, int S>
 int launch_wrows(const snnflow_unet_wgrad_args& a, hipStream_t s) {
-    using G = WrGeo<NI, NJ, WK, WM>;
-    const WgPlan p = wrows_plan<NI, NJ, WK, WM>(a);
-    hipLaunchKernelGGL((k_unet_wgrad_rows<NI, NJ, WK, WM>), dim3((unsigned)(p.tiles * p.nsplit)), dim3(UNT), 0, s, a,
+    using G = WrGeo<NI, NJ, WK, WM, S>;
+    const WgPlan p = wrows_plan<NI, NJ, WK, WM, S>(a);
+    hipLaunchKernelGGL((k_unet_wgrad_rows<NI, NJ, WK, WM, S>), dim3((unsigned)(p.tiles * p.nsplit)), dim3(UNT), 0, s, a,
                        p.ktiles, p.mtiles, p.nsplit, p.steps);
-    if (a.partial) {
-        const int64_t n = (int64_t)9 * a.seg.cpitch * a.M;
-        hipLaunchKernelGGL(k_unet_wgrad_reduce, dim3(grid1d(n, 256, 4096)), dim3(256), 0, s, a, p.nsplit,
-                           p.ktiles * G::TK, p.mtiles * G::TM);
-    }
+    if (a.partial)
+        launch_wgrad_reduce(a, p.nsplit, p.ktiles * G::TK, p.mtiles * G::TM, wrows_tiles_floats<NI, NJ, WK, WM, S>(a), s);
     SNN_CHECK_LAUNCH();
     return 0;
 }
 
 // M <= 32: 4 waves along k (64 x 32 tile); else 2 x 2 waves (32 x 64)
-#define WR_DISPATCH(FN, ARGS)                                    \
-    {                                                            \
-        if (a->M <= 32) return FN<1, 2, 4, 1> ARGS;              \
-        return FN<1, 2, 2, 2> ARGS;                              \
+#define WR_DISPATCH(FN, ARGS)                                                  \
+    {                                                                          \
+        if (a->seg.mode == SNNFLOW_UNET_MODE_S2) return FN<1, 2, 2, 2, 2> ARGS; \
+        if (a->M <= 32) return FN<1, 2, 4, 1, 1> ARGS;                         \
+        return FN<1, 2, 2, 2, 1> ARGS;                                         \
     }
 
 // Tile of a launch: m 32 / 64 / 128; k the first of 128, 160 (m <= 64: registers), 96, 64, 32 whose
