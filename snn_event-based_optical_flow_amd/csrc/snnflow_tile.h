@@ -720,22 +720,63 @@ __device__ inline void pin(float (&v)[N]) {
 // Block-level sums of per-thread floats, then one fp64 atomic add per sum.  The block's
 // threads form PARTS groups of NT consecutive threads (whole waves); each group sums
 // its own NV values and dst(part, j) is the accumulator address of sum j of group part.
+// One LDS scratch for the block sums of every kernel variant (a __shared__ array in the templated
+// function would be allocated once per instantiation, all of them in a wavefront launch).
+constexpr int kSumScratch = 8 * 4 * 48;  // waves x rows x sums (C = 32 backward: 3 * 16)
+__device__ inline float* sum_scratch() {
+    __shared__ float buf[kSumScratch];
+    return buf;
+}
+
 template <int NV, int PARTS, typename Dst>
 __device__ void block_atomic_sum_parts(const float (&v)[NV], Dst dst) {
     constexpr int WPP = NT / 64, NW = WPP * PARTS;
-    __shared__ float red[NW][NV];
+    if constexpr (NW * 4 * NV > kSumScratch) {  // many sums (C = 32 top LIF backward): wave totals
+        __shared__ float wred[NW][NV];
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const float s = wave_total(v[j]);
+            if (lane == 0) wred[wv][j] = s;
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < PARTS * NV; t += NT * PARTS) {
+            const int part = t / NV, j = t - part * NV;
+            double s = 0.0;
+#pragma unroll
+            for (int w = 0; w < WPP; ++w) s += (double)wred[part * WPP + w][j];
+            atomicAdd(dst(part, j), s);
+        }
+        return;
+    }
+    // 16-lane row totals by DPP (four chains at a time, no readlane round trips), the four row
+    // totals of every wave through LDS, then the per-part sum in fp64
+    float* red = sum_scratch();  // [NW * 4][NV]
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-        const float s = wave_total(v[j]);
-        if (lane == 0) red[wv][j] = s;
+    for (int j0 = 0; j0 < NV; j0 += 4) {
+        constexpr int G = 4;
+        float r[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) r[j] = j0 + j < NV ? v[j0 + j] + dppf<0xB1>(v[j0 + j]) : 0.0f;
+#pragma unroll
+        for (int j = 0; j < G; ++j) r[j] += dppf<0x4E>(r[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) r[j] += dppf<0x141>(r[j]);
+#pragma unroll
+        for (int j = 0; j < G; ++j) r[j] += dppf<0x140>(r[j]);
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int j = 0; j < G; ++j)
+                if (j0 + j < NV) red[(wv * 4 + (lane >> 4)) * NV + j0 + j] = r[j];
+        }
     }
     __syncthreads();
     for (int t = threadIdx.x; t < PARTS * NV; t += NT * PARTS) {
         const int part = t / NV, j = t - part * NV;
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < WPP; ++w) s += (double)red[part * WPP + w][j];
+        for (int w = 0; w < 4 * WPP; ++w) s += (double)red[(part * 4 * WPP + w) * NV + j];
         atomicAdd(dst(part, j), s);
     }
 }
