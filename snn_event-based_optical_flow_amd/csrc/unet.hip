@@ -202,7 +202,10 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
     using G = ConvGeo<WMT, WAVES_M, XPARTS>;
     constexpr int BM = G::BM, BN = G::BN;
     __shared__ __attribute__((aligned(16))) __bf16 Xs[XPARTS * BN * XP];
-    __shared__ __attribute__((aligned(16))) __bf16 Ws[3 * BM * XP];
+    // spike inputs stage the weight parts through LDS (shared by the block's WAVES_N waves); the
+    // three-plane gradient inputs read each wave's weight fragments straight from global memory
+    constexpr bool DW = XPARTS == 3;
+    __shared__ __attribute__((aligned(16))) __bf16 Ws[DW ? 8 : 3 * BM * XP];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -229,7 +232,8 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
         dom_pix(dom, pv[r] ? n : 0, pb[r], py[r], px[r]);
     }
 
-    uint4 xr[XPARTS][G::XR], wr[G::WR];
+    uint4 xr[XPARTS][G::XR], wr[DW ? 1 : G::WR];
+    bf16x8 wf[DW ? WMT : 1][3];
     const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
     // global loads of one k-step (segment sg, tap index ti of the domain, chunk kc) into registers
     auto load = [&](const snnflow_unet_seg& sg, int ti, int kc) {
@@ -261,6 +265,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 if (!ok) xr[xp][r] = z4;
             }
         }
+        if constexpr (DW) return;
         const int np = XPARTS == 3 ? 3 : sg.nparts;
         const int64_t wbase = ((int64_t)(tap * a.kct + sg.kc0 + kc) * a.mpad + m0) * 32;
 #pragma unroll
@@ -272,6 +277,21 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
             if (!ok) wr[r] = z4;
         }
     };
+    // this wave's weight fragments of one k-step (DW): the prepared layout [part][tap][kc][mpad][32]
+    // makes a 16-row fragment one contiguous 1-KB read per wave
+    auto load_w = [&](const snnflow_unet_seg& sg, int ti, int kc) {
+        if constexpr (DW) {
+            const int ty_ = ti / dom.ntx;
+            const int ky = dom.ky0 + dom.kst * ty_, kx = dom.kx0 + dom.kst * (ti - ty_ * dom.ntx);
+            const int tap = ky * ks + kx;
+            const int64_t wbase =
+                ((int64_t)(tap * a.kct + sg.kc0 + kc) * a.mpad + m0 + wm * 16 * WMT + (lane & 15)) * 32 + (lane >> 4) * 8;
+#pragma unroll
+            for (int i = 0; i < WMT; ++i)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) wf[i][p] = __builtin_bit_cast(bf16x8, ld16(a.w + p * wpart + wbase + i * 16 * 32));
+        }
+    };
     auto store = [&]() {
 #pragma unroll
         for (int xp = 0; xp < XPARTS; ++xp)
@@ -279,7 +299,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
             for (int r = 0; r < G::XR; ++r)
                 *reinterpret_cast<uint4*>(&Xs[(xp * BN + (tid >> 2) + 64 * r) * XP + q * 8]) = xr[xp][r];
 #pragma unroll
-        for (int r = 0; r < G::WR; ++r) {
+        for (int r = 0; r < (DW ? 0 : G::WR); ++r) {
             const int e = tid + r * UNT;
             if (e < G::WPIECES) {
                 const int part = e / (BM * 4), rem = e - part * (BM * 4);
@@ -321,6 +341,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
         int k, ti, kc;
         locate(f0, k, ti, kc);
         load(seg_at(a, k), ti, kc);
+        load_w(seg_at(a, k), ti, kc);
     }
     for (int f = f0; f < f1; ++f) {
         int k, ti, kc;
@@ -329,8 +350,8 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
         __syncthreads();  // the previous step's fragment reads are done
         store();
         __syncthreads();
+        int k2 = 0, ti2 = 0, kc2 = 0;
         if (f + 1 < f1) {
-            int k2, ti2, kc2;
             locate(f + 1, k2, ti2, kc2);
             load(seg_at(a, k2), ti2, kc2);
         }
@@ -352,11 +373,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
         } else {
 #pragma unroll
             for (int i = 0; i < WMT; ++i) {
-                const int row = wm * 16 * WMT + i * 16 + (lane & 15);
-                bf16x8 aw[3];
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    aw[p] = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+                const bf16x8* aw = wf[DW ? i : 0];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int col = (wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8;
@@ -373,6 +390,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 }
             }
         }
+        if (f + 1 < f1) load_w(seg_at(a, k2), ti2, kc2);  // after this step's MFMAs have read wf
     }
 
     // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of domain pixel nd
