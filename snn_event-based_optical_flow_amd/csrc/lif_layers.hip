@@ -1850,6 +1850,63 @@ __device__ inline T kernarg_copy(const __attribute__((address_space(4))) T* p) {
     return r;
 }
 
+// The copy above loses the address space of the pointers (kernel arguments are global; a struct
+// rebuilt from kernarg dwords is generic), and generic pointers compile to flat_* instructions,
+// which count on the LDS counter too: every LDS wait of a body then also waited for its
+// outstanding HBM loads and stores.  An empty asm hands each pointer back as a global one.
+template <typename T>
+__device__ inline T* as_global_ptr(T* p) {
+    __attribute__((address_space(1))) T* g;
+    asm("" : "=s"(g) : "0"(p));
+    return (T*)g;
+}
+#define SNN_G(x) (x) = as_global_ptr(x)
+
+__device__ inline void globalize(snnflow_neuron& n) {
+    SNN_G(n.bn_weight); SNN_G(n.bn_bias); SNN_G(n.running_mean); SNN_G(n.running_var);
+    SNN_G(n.num_batches_tracked); SNN_G(n.beta); SNN_G(n.threshold);
+}
+__device__ inline void globalize(snnflow_neuron_grad& n) {
+    SNN_G(n.bn_weight); SNN_G(n.bn_bias); SNN_G(n.beta); SNN_G(n.threshold);
+}
+__device__ inline void globalize(snnflow_conv_fwd_args& a) {
+    SNN_G(a.x); SNN_G(a.prev_y); SNN_G(a.prev_mem); SNN_G(a.prev_acc); SNN_G(a.prev_stats);
+    globalize(a.prev);
+    SNN_G(a.prev_state); SNN_G(a.wt_ff); SNN_G(a.wt_rec); SNN_G(a.wt_ff_t); SNN_G(a.wt_rec_t); SNN_G(a.s_prev);
+    SNN_G(a.y); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1); SNN_G(a.wf_ff); SNN_G(a.wf_rec);
+}
+__device__ inline void globalize(snnflow_lif_fwd_args& a) {
+    SNN_G(a.y); SNN_G(a.mem); SNN_G(a.acc); SNN_G(a.stats);
+    globalize(a.n);
+    SNN_G(a.state); SNN_G(a.pred_w); SNN_G(a.pred_b); SNN_G(a.flow); SNN_G(a.zero0); SNN_G(a.zero1);
+}
+__device__ inline void globalize(snnflow_lif_bwd_args& a) {
+    SNN_G(a.y); SNN_G(a.mem); SNN_G(a.stats);
+    globalize(a.n);
+    SNN_G(a.g_out); SNN_G(a.g_state); SNN_G(a.pred_w); SNN_G(a.flow); SNN_G(a.g_flow); SNN_G(a.g_cur);
+    SNN_G(a.g_mem); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1);
+}
+__device__ inline void globalize(snnflow_layer_bwd_args& a) {
+    SNN_G(a.y); SNN_G(a.stats); SNN_G(a.g_cur); SNN_G(a.acc_in);
+    globalize(a.n);
+    globalize(a.ng);
+    SNN_G(a.g_pred_w); SNN_G(a.g_pred_b); SNN_G(a.bnc_out); SNN_G(a.wt_bwd_ff); SNN_G(a.wt_bwd_rec);
+    SNN_G(a.wt_fwd_ff); SNN_G(a.wt_fwd_rec); SNN_G(a.g_x); SNN_G(a.g_state_prev); SNN_G(a.prev_y);
+    SNN_G(a.prev_mem); SNN_G(a.prev_stats);
+    globalize(a.prev);
+    SNN_G(a.prev_g_state); SNN_G(a.prev_g_cur); SNN_G(a.prev_g_mem); SNN_G(a.acc_out); SNN_G(a.zero0);
+    SNN_G(a.zero1); SNN_G(a.wd_ff); SNN_G(a.wd_rec);
+}
+#undef SNN_G
+
+// A task's argument struct from the kernarg segment, pointers global.
+template <typename T>
+__device__ inline T task_args(const __attribute__((address_space(4))) T* p) {
+    T r = kernarg_copy(p);
+    globalize(r);
+    return r;
+}
+
 // Task of this block (block ranges ascending; ntask <= kSlotTasks) and its Grid.
 template <typename P>
 __device__ inline int slot_task(const __attribute__((address_space(4))) P* pp, Grid& g) {
@@ -1874,7 +1931,7 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
     switch (pp->kind[k]) {
 #define FWD_CONV(KIND, ...)                                   \
     case KIND: {                                              \
-        const snnflow_conv_fwd_args a = kernarg_copy(&pp->conv[k]);          \
+        const snnflow_conv_fwd_args a = task_args(&pp->conv[k]);             \
         conv_fwd_body<__VA_ARGS__>(a, g, pool);               \
         break;                                                \
     }
@@ -1888,12 +1945,12 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
         FWD_CONV(SK_LIF_REC, C, C, true, true, 2)
 #undef FWD_CONV
         case SK_TOP: {
-            const snnflow_lif_fwd_args a = kernarg_copy(&pp->lif);
+            const snnflow_lif_fwd_args a = task_args(&pp->lif);
             lif_fwd_body<C, false, NT * 2>(a, g);
             break;
         }
         case SK_TOP_PRED: {
-            const snnflow_lif_fwd_args a = kernarg_copy(&pp->lif);
+            const snnflow_lif_fwd_args a = task_args(&pp->lif);
             lif_fwd_body<C, true, NT * 2>(a, g);
             break;
         }
@@ -1915,7 +1972,7 @@ __global__ __launch_bounds__(NT * 2, SNNFLOW_BWD_SLOT_WAVES) void k_bwd_slot(Bwd
     switch (pp->kind[k]) {
 #define BWD_LAYER(KIND, ...)                                  \
     case KIND: {                                              \
-        const snnflow_layer_bwd_args a = kernarg_copy(&pp->layer[k]);        \
+        const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);           \
         layer_bwd_body<__VA_ARGS__>(a, g, pool);              \
         break;                                                \
     }
@@ -1927,12 +1984,12 @@ __global__ __launch_bounds__(NT * 2, SNNFLOW_BWD_SLOT_WAVES) void k_bwd_slot(Bwd
         BWD_LAYER(SK_LIF_REC, C, C, true, true, 2)
 #undef BWD_LAYER
         case SK_TOP: {
-            const snnflow_lif_bwd_args a = kernarg_copy(&pp->lif);
+            const snnflow_lif_bwd_args a = task_args(&pp->lif);
             lif_bwd_body<C, false, NT * 2>(a, g);
             break;
         }
         case SK_TOP_PRED: {
-            const snnflow_lif_bwd_args a = kernarg_copy(&pp->lif);
+            const snnflow_lif_bwd_args a = task_args(&pp->lif);
             lif_bwd_body<C, true, NT * 2>(a, g);
             break;
         }
