@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 19
+#define SNNFLOW_ABI_VERSION 20
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -444,6 +444,15 @@ int snnflow_flow_metrics_rows(int B, int H, int W);
  * m' = beta[c]*mem + x; spk = m' >= thr[c]; mem_out = spk ? 0 : m'  (NCHW). */
 int snnflow_lif_export(const float* x, const float* mem, const float* beta, const float* thr,
                        int N, int C, int HW, float* spk, float* mem_out, void* stream);
+
+/* Threshold gradient of the subtract-reset neuron (snn.Leaky reset_mechanism "subtract",
+ * SNNtorch_spiking_submodules.py:171, hard_reset=False): v = beta*m + I - r*theta with the reset
+ * r = H(m - theta) detached, so theta also receives -sum r * dL/dv through v; the fused LIF
+ * backward kernels form the zero-reset part -sum dL/dv.  Adds -sum_px [mem - thr > 0] * g_cur
+ * per channel to g_theta[c] (g_cur = dL/dv and mem = the incoming membrane, NHWC [npix][c];
+ * float atomics).  c = 4, 8, 16 or 32. */
+int snnflow_lif_theta_subtract(const float* g_cur, const float* mem, const float* thr, int64_t npix, int c,
+                               float* g_theta, void* stream);
 
 /* clip_grad_norm_ (train_flow.py:265-266) over one flat gradient buffer of n floats, in place:
  * total = ||g||_2, g *= min(max_norm / (total + eps), 1); total_out (device, may be NULL). */

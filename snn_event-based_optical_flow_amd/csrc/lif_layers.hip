@@ -752,6 +752,262 @@ __global__ __launch_bounds__(NT) void k_lif_bwd(snnflow_lif_bwd_args a) {
     lif_bwd_body<C, PRED, NT>(a, hw_grid());
 }
 
+// Standalone (per-step) LIF launches: one thread per (pixel, channel quad), `items` pixels of
+// the block's contiguous range per thread.  The one-thread-per-pixel bodies above keep a pixel's
+// C channels in one thread (the wavefront launches' C = 8 top task); at C = 16 / 32 that
+// serialises 2-4x the loads and stores per thread and, backward, reduces 3C + 2C + 2 sums per
+// thread through the block.  Here a thread holds one float4 of each tensor and 12 (+ 10 with
+// the prediction) running sums; lanes of equal quad are reduced once per block.
+// Grids of one resident round (no tail): forward 6 blocks per CU (58-72 VGPRs), backward 4
+// (78-108 VGPRs); each thread then takes `items` pixels.
+constexpr int kLifQFwdBlocks = 6 * 256, kLifQBwdBlocks = 4 * 256;
+
+__host__ __device__ constexpr int lifq_ppb(int C) { return NT / (C / 4); }
+
+inline int lifq_items(int64_t npix, int C, int target) {
+    const int64_t b1 = (npix + lifq_ppb(C) - 1) / lifq_ppb(C);
+    const int64_t it = (b1 + target - 1) / target;
+    return (int)(it < 1 ? 1 : it);
+}
+
+inline int lifq_grid(int64_t npix, int C, int items) {
+    const int64_t per = (int64_t)lifq_ppb(C) * items;
+    const int64_t g = (npix + per - 1) / per;
+    return (int)(g < 1 ? 1 : g);
+}
+
+// OR of a lane value over the Q consecutive lanes of one pixel (Q a power of two <= 8)
+template <int Q>
+__device__ inline unsigned quad_or(unsigned v) {
+#pragma unroll
+    for (int o = 1; o < Q; o <<= 1) v |= (unsigned)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+template <int C, bool PRED>
+__global__ __launch_bounds__(NT) void k_lif_fwd_q(snnflow_lif_fwd_args a, int items) {
+    constexpr int Q = C / 4, PPB = lifq_ppb(C);
+    static_assert(Q >= 1 && Q <= 8 && (Q & (Q - 1)) == 0, "C = 4, 8, 16, 32");
+    __shared__ LifCoef coef[C];
+    const int tid = threadIdx.x, q = tid % Q, ps = tid / Q;
+    const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
+    const float4* y4 = reinterpret_cast<const float4*>(a.y);
+    const float4* m4 = reinterpret_cast<const float4*>(a.mem);
+    const bool lead = blockIdx.x == 0;
+    AccGather<2 * C> gat;
+    if (a.n.bn_train) acc_gather_load<2 * C>(a.acc, 2 * C, gat);
+    const NeuronRegs nr = load_neuron(a.n, C, lead);
+    int64_t p = (int64_t)blockIdx.x * items * PPB + ps;
+    int64_t pc = p < npix ? p : npix - 1;  // unconditional 16-B loads
+    float4 yv = y4[pc * Q + q], mv = ld4_or_zero(m4, y4, pc * Q + q);
+    __shared__ double sums[2 * C];
+    if (a.n.bn_train) acc_gather_reduce<2 * C>(gat, sums);
+    lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr, lead);
+    __syncthreads();
+    zero_consumed(a.zero0, a.zero1, a.zero_n);
+    const bool zr = a.n.zero_reset != 0;
+    const LifCoef kc[4] = {coef[4 * q], coef[4 * q + 1], coef[4 * q + 2], coef[4 * q + 3]};
+    float4* st4 = reinterpret_cast<float4*>(a.state);
+    for (int it = 0; it < items; ++it) {
+        const bool act = p < npix;
+        const int64_t pn = p + PPB, pcn = pn < npix ? pn : npix - 1;
+        float4 yn = yv, mn = mv;
+        if (it + 1 < items) {  // next pixel's loads in flight during this one's math
+            yn = y4[pcn * Q + q];
+            mn = ld4_or_zero(m4, y4, pcn * Q + q);
+        }
+        const Lif4 o = lif_step4(yv, mv, kc, zr);
+        if (act) {
+            st4[p * Q + q] = o.mout;
+            st4[plane4 + p * Q + q] = o.s;
+        }
+        if constexpr (PRED) {
+            // the pixel's C spikes as a bit mask on each of its lanes; the 1x1 conv then runs in
+            // lane q = o (q = 0 for both outputs at C = 4) in channel order, as one thread per
+            // pixel does (bit-identical flows)
+            unsigned bits = (o.s.x > 0.f ? 1u : 0u) | (o.s.y > 0.f ? 2u : 0u) | (o.s.z > 0.f ? 4u : 0u) |
+                            (o.s.w > 0.f ? 8u : 0u);
+            bits = quad_or<Q>(bits << (4 * q));
+            const cfloat_ptr pw = as_const(a.pred_w);
+            const int64_t b = pc / HWp, hw = pc - b * HWp;
+#pragma unroll
+            for (int ou = 0; ou < 2; ++ou) {
+                if (act && q == (Q >= 2 ? ou : 0)) {
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) acc = fmaf(pw[ou * C + c], ((bits >> c) & 1u) ? 1.0f : 0.0f, acc);
+                    a.flow[(b * 2 + ou) * HWp + hw] = tanhf(acc + a.pred_b[ou]);
+                }
+            }
+        }
+        p = pn;
+        pc = pcn;
+        yv = yn;
+        mv = mn;
+    }
+}
+
+template <int C, bool PRED>
+__global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int items) {
+    constexpr int Q = C / 4, PPB = lifq_ppb(C);
+    constexpr int NVQ = 12 + (PRED ? 10 : 0);  // (g, (y - mean) g, g m') x 4 [+ (gpre0 s, gpre1 s) x 4 + gpre0, gpre1]
+    static_assert(Q >= 1 && Q <= 8 && (Q & (Q - 1)) == 0, "C = 4, 8, 16, 32");
+    __shared__ LifCoef coef[C];
+    __shared__ float meanv[C];
+    __shared__ float red[NT / 64][Q][NVQ];
+    const int tid = threadIdx.x, q = tid % Q, ps = tid / Q, lane = tid & 63, wv = tid >> 6;
+    const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
+    LifCoef kci = {0.f, 0.f, 0.f, 0.f};
+    float mu = 0.f;
+    if (tid < C) {
+        kci = lif_coef(a.n, a.stats, C, tid);
+        mu = a.stats[tid];
+    }
+    const float4* y4 = reinterpret_cast<const float4*>(a.y);
+    const float4* m4 = reinterpret_cast<const float4*>(a.mem);
+    const float4* go4 = reinterpret_cast<const float4*>(a.g_out);
+    const float4* gst4 = reinterpret_cast<const float4*>(a.g_state);
+    float4* gc4 = reinterpret_cast<float4*>(a.g_cur);
+    float4* gm4 = reinterpret_cast<float4*>(a.g_mem);
+    struct Px { float4 y, m, g; float fl[2], gf[2]; };
+    auto load = [&](int64_t pp, Px& x) {
+        const int64_t pc = pp < npix ? pp : npix - 1;
+        const int64_t i = pc * Q + q;
+        x.y = y4[i];
+        x.m = ld4_or_zero(m4, y4, i);
+        x.g = ld4_or_zero(go4, y4, i);
+        const float4 t = ld4_or_zero(gst4 ? gst4 + plane4 : nullptr, y4, i);
+        if (gst4) x.g = make_float4(x.g.x + t.x, x.g.y + t.y, x.g.z + t.z, x.g.w + t.w);
+        x.fl[0] = x.fl[1] = x.gf[0] = x.gf[1] = 0.f;
+        if constexpr (PRED) {
+            if (a.g_flow) {
+                const int64_t b = pc / HWp, hw = pc - b * HWp;
+#pragma unroll
+                for (int o = 0; o < 2; ++o) {
+                    x.fl[o] = a.flow[(b * 2 + o) * HWp + hw];
+                    x.gf[o] = a.g_flow[b * a.gflow_sb + o * a.gflow_sc + hw];
+                }
+            }
+        }
+    };
+    int64_t p = (int64_t)blockIdx.x * items * PPB + ps;
+    Px cur;
+    load(p, cur);
+    if (tid < C) {
+        coef[tid] = kci;
+        meanv[tid] = mu;
+    }
+    __syncthreads();
+    const bool zr = a.n.zero_reset != 0;
+    const LifCoef kc[4] = {coef[4 * q], coef[4 * q + 1], coef[4 * q + 2], coef[4 * q + 3]};
+    const float mq[4] = {meanv[4 * q], meanv[4 * q + 1], meanv[4 * q + 2], meanv[4 * q + 3]};
+    const cfloat_ptr pw = as_const(a.pred_w);
+    float v[NVQ];
+#pragma unroll
+    for (int j = 0; j < NVQ; ++j) v[j] = 0.0f;
+    for (int it = 0; it < items; ++it) {
+        Px nx = cur;
+        if (it + 1 < items) load(p + PPB, nx);
+        if (p < npix) {
+            float gpre[2] = {0.0f, 0.0f};
+            if constexpr (PRED) {
+                if (a.g_flow) {
+#pragma unroll
+                    for (int o = 0; o < 2; ++o) gpre[o] = cur.gf[o] * (1.0f - cur.fl[o] * cur.fl[o]);  // tanh backward
+                }
+            }
+            const float yi[4] = {cur.y.x, cur.y.y, cur.y.z, cur.y.w};
+            const float mi[4] = {cur.m.x, cur.m.y, cur.m.z, cur.m.w};
+            const float gi[4] = {cur.g.x, cur.g.y, cur.g.z, cur.g.w};
+            float go[4], gmo[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int c = 4 * q + j;
+                float g = gi[j];
+                if constexpr (PRED) {
+                    if (a.g_flow) g = g + (pw[c] * gpre[0] + pw[C + c] * gpre[1]);
+                }
+                const LifOut o = lif_step(yi[j], mi[j], kc[j], zr);
+                const float gv = atan_sg(o.v - kc[j].theta) * g;
+                go[j] = gv;
+                gmo[j] = mem_grad(gv, mi[j], kc[j], zr);
+                v[j] += gv;
+                v[4 + j] += (yi[j] - mq[j]) * gv;
+                v[8 + j] += gv * o.mprime;
+                if constexpr (PRED) {
+                    v[12 + j] += gpre[0] * o.s;
+                    v[16 + j] += gpre[1] * o.s;
+                }
+            }
+            gc4[p * Q + q] = make_float4(go[0], go[1], go[2], go[3]);
+            if (gm4) gm4[p * Q + q] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
+            if constexpr (PRED) {
+                if (q == 0) {
+                    v[20] += gpre[0];
+                    v[21] += gpre[1];
+                }
+            }
+        }
+        p += PPB;
+        cur = nx;
+    }
+    // lanes of equal quad (lane % Q) summed across the wave, then the four waves in order
+#pragma unroll
+    for (int j = 0; j < NVQ; ++j) {
+#pragma unroll
+        for (int o = Q; o < 64; o <<= 1) v[j] += __shfl_xor(v[j], o, 64);
+    }
+    if (lane < Q) {
+#pragma unroll
+        for (int j = 0; j < NVQ; ++j) red[wv][lane][j] = v[j];
+    }
+    __syncthreads();
+    double* acc = acc_shard(a.acc, SNNFLOW_BWD_ACC(C), (int)blockIdx.x);
+    for (int e = tid; e < Q * NVQ; e += NT) {
+        const int qq = e / NVQ, j = e - qq * NVQ;
+        if (j >= 20 && qq != 0) continue;  // the per-pixel prediction-bias sums live in quad 0
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) t += red[w][qq][j];
+        const int k = j < 20 ? (j / 4) * C + 4 * qq + (j & 3) : 5 * C + (j - 20);
+        atomicAdd(acc + k, (double)t);
+    }
+    zero_consumed(a.zero0, a.zero1, a.zero_n);  // last: no load waits behind these stores
+}
+
+// Subtract-reset threshold gradient (include/snnflow.h snnflow_lif_theta_subtract): thread per
+// float4 of the NHWC tensors, grid-stride (the channel quad of a thread is fixed), per-block
+// channel totals through LDS, one float atomic per channel and block.
+template <int C>
+__global__ __launch_bounds__(NT) void k_lif_theta_subtract(const float* __restrict__ g_cur, const float* __restrict__ mem,
+                                                        const float* __restrict__ thr, int64_t npix, float* g_theta) {
+    constexpr int Q = C / 4;
+    __shared__ float4 part[NT];
+    const int tid = threadIdx.x, q = tid % Q;
+    const float t0 = thr[4 * q], t1 = thr[4 * q + 1], t2 = thr[4 * q + 2], t3 = thr[4 * q + 3];
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t n4 = npix * Q, stride = (int64_t)gridDim.x * NT;  // stride % Q == 0 (Q | 256)
+    for (int64_t e = (int64_t)blockIdx.x * NT + tid; e < n4; e += stride) {
+        const float4 g = reinterpret_cast<const float4*>(g_cur)[e];
+        const float4 m = reinterpret_cast<const float4*>(mem)[e];
+        acc.x += (m.x - t0 > 0.0f) ? g.x : 0.0f;
+        acc.y += (m.y - t1 > 0.0f) ? g.y : 0.0f;
+        acc.z += (m.z - t2 > 0.0f) ? g.z : 0.0f;
+        acc.w += (m.w - t3 > 0.0f) ? g.w : 0.0f;
+    }
+    part[tid] = acc;
+    __syncthreads();
+    if (tid < C) {
+        const int qq = tid / 4, j = tid & 3;
+        float s = 0.0f;
+        for (int k = qq; k < NT; k += Q) {
+            const float4 v = part[k];
+            s += j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+        }
+        atomicAdd(g_theta + tid, -s);
+    }
+}
+
 // BatchNorm backward of one float4 of channels (torch batch_norm_cpu_backward, train):
 // dx = ((g - grad_mean) - (y - mean) * k) * invstd * gamma.
 struct BnBwdLds { float mean, inv, gm, k, w; };
@@ -2151,7 +2407,10 @@ static int lif_fwd_check(const snnflow_lif_fwd_args* a) {
 int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
     if (const int e = lif_fwd_check(a)) return e;
     const hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(elem_grid((int64_t)a->B * a->H * a->W)), block(NT);
+    const int64_t npix = (int64_t)a->B * a->H * a->W;
+    // C <= 8: one thread per pixel (measured faster there); C >= 16: quad layout
+    const int items = lifq_items(npix, a->c, kLifQFwdBlocks);
+    const dim3 grid(a->c >= 16 ? lifq_grid(npix, a->c, items) : elem_grid(npix)), block(NT);
     const bool pred = a->pred_w != nullptr;
     switch (a->c) {
 #define LIF_FWD_CASE(CC)                                                                     \
@@ -2159,7 +2418,13 @@ int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
         if (pred) hipLaunchKernelGGL((k_lif_fwd<CC, true>), grid, block, 0, s, *a);          \
         else hipLaunchKernelGGL((k_lif_fwd<CC, false>), grid, block, 0, s, *a);              \
         break;
-        LIF_FWD_CASE(4) LIF_FWD_CASE(8) LIF_FWD_CASE(16) LIF_FWD_CASE(32)
+#define LIF_FWD_Q_CASE(CC)                                                                   \
+    case CC:                                                                                 \
+        if (pred) hipLaunchKernelGGL((k_lif_fwd_q<CC, true>), grid, block, 0, s, *a, items); \
+        else hipLaunchKernelGGL((k_lif_fwd_q<CC, false>), grid, block, 0, s, *a, items);     \
+        break;
+        LIF_FWD_CASE(4) LIF_FWD_CASE(8) LIF_FWD_Q_CASE(16) LIF_FWD_Q_CASE(32)
+#undef LIF_FWD_Q_CASE
 #undef LIF_FWD_CASE
         default: SNN_FAIL(SNNFLOW_E_CHANNELS, "lif_fwd: c must be 4, 8, 16 or 32");
     }
@@ -2177,16 +2442,43 @@ int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
     if (const int e = lif_bwd_check(a)) return e;
     const bool pred = a->pred_w != nullptr;
     const hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(elem_grid((int64_t)a->B * a->H * a->W)), block(NT);
+    const int64_t npix = (int64_t)a->B * a->H * a->W;
+    const int items = lifq_items(npix, a->c, kLifQBwdBlocks);
+    const dim3 grid(a->c >= 16 ? lifq_grid(npix, a->c, items) : elem_grid(npix)), block(NT);
     switch (a->c) {
 #define LIF_BWD_CASE(CC)                                                                     \
     case CC:                                                                                 \
         if (pred) hipLaunchKernelGGL((k_lif_bwd<CC, true>), grid, block, 0, s, *a);          \
         else hipLaunchKernelGGL((k_lif_bwd<CC, false>), grid, block, 0, s, *a);              \
         break;
-        LIF_BWD_CASE(4) LIF_BWD_CASE(8) LIF_BWD_CASE(16) LIF_BWD_CASE(32)
+#define LIF_BWD_Q_CASE(CC)                                                                   \
+    case CC:                                                                                 \
+        if (pred) hipLaunchKernelGGL((k_lif_bwd_q<CC, true>), grid, block, 0, s, *a, items); \
+        else hipLaunchKernelGGL((k_lif_bwd_q<CC, false>), grid, block, 0, s, *a, items);     \
+        break;
+        LIF_BWD_CASE(4) LIF_BWD_CASE(8) LIF_BWD_Q_CASE(16) LIF_BWD_Q_CASE(32)
+#undef LIF_BWD_Q_CASE
 #undef LIF_BWD_CASE
         default: SNN_FAIL(SNNFLOW_E_CHANNELS, "lif_bwd: c must be 4, 8, 16 or 32");
+    }
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_lif_theta_subtract(const float* g_cur, const float* mem, const float* thr, int64_t npix, int c,
+                               float* g_theta, void* stream) {
+    if (!g_cur || !mem || !thr || !g_theta || npix <= 0) SNN_FAIL(SNNFLOW_E_ARG, "lif_theta_subtract: bad args");
+    const int64_t n4 = npix * (c / 4);
+    int64_t g = (n4 + NT - 1) / NT;
+    if (g > 1024) g = 1024;
+    const dim3 grid((unsigned)g), block(NT);
+    const hipStream_t s = (hipStream_t)stream;
+    switch (c) {
+        case 4: hipLaunchKernelGGL(k_lif_theta_subtract<4>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
+        case 8: hipLaunchKernelGGL(k_lif_theta_subtract<8>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
+        case 16: hipLaunchKernelGGL(k_lif_theta_subtract<16>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
+        case 32: hipLaunchKernelGGL(k_lif_theta_subtract<32>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
+        default: SNN_FAIL(SNNFLOW_E_CHANNELS, "lif_theta_subtract: c must be 4, 8, 16 or 32");
     }
     SNN_CHECK_LAUNCH();
     return 0;

@@ -18,7 +18,7 @@ import torch.nn as nn
 from . import _lib
 from ._lib import check, lib, ptr
 from .engine import (Workspace, _ptr_t, _x_strides, as_nhwc_state, empty_state,
-                     neuron_struct)
+                     neuron_struct, theta_subtract)
 from .norm import MPBN, TEBN, MPBNStateFn, PointwiseFn
 
 
@@ -333,6 +333,7 @@ class CellFn(torch.autograd.Function):
             if g_prev is not None:
                 a.g_state_prev, a.zero_mem_half = ptr(g_prev), 0
         _lib.call("layer_bwd", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+        theta_subtract(cell, g_cur, mem, B * H * W, ptr(g_th), s)
         # weight gradients of this single step (snnflow_wgrad with one step)
         slab_ff = torch.empty(ws.nblk, C * cin * 9, device=dev)
         slab_rec = torch.empty(ws.nblk, C * C * 9, device=dev) if cell.recurrent else None

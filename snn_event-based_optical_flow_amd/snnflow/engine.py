@@ -487,6 +487,17 @@ def _rows(t):
     return t if isinstance(t, _Rows) else _Rows(t)
 
 
+def theta_subtract(cell, g_cur, mem, npix, g_theta, stream):
+    """Subtract-reset cells (``hard_reset=False``): the threshold's gradient through the reset term
+    of v = beta*m + I - r*theta (snn.Leaky, r detached), -sum [m > theta] * dL/dv, added to
+    g_theta after the fused LIF backward has written the zero-reset part.  g_cur / mem: device
+    pointers (NHWC); no-op for zero-reset cells or a step without an incoming membrane."""
+    if cell.lif.reset_mechanism != "subtract" or mem is None:
+        return
+    _lib.call("lif_theta_subtract", lib.snnflow_lif_theta_subtract, _ptr_t(g_cur), _ptr_t(mem),
+              ptr(cell.lif.threshold), npix, cell.hidden_size, g_theta, stream)
+
+
 # ---------------------------------------------------------------------------
 # Kernel arguments of one time step (shared by the per-step and the sequence Functions)
 # ---------------------------------------------------------------------------
@@ -792,6 +803,8 @@ class FireNetStep(torch.autograd.Function):
                     if l + 1 <= L - 1:
                         a.zero0, a.zero_n = bacc[l + 1], zn
                     _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+            for l in range(L):
+                theta_subtract(eng.cells[l], gcur[l], mem_in[l], B * H * W, glayers[l][2].threshold, s)
             if ctx.root:
                 eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
         except Exception:
@@ -1010,6 +1023,9 @@ class FireNetSequence(torch.autograd.Function):
                 arr = (_lib.LayerBwdArgs * max(len(layers), 1))(*layers)
                 _lib.call("bwd_slot", lib.snnflow_bwd_slot, arr, len(layers),
                           ctypes.byref(top) if top is not None else None, s)
+            for l in range(L):
+                for t in range(T):
+                    theta_subtract(eng.cells[l], gcur[t][l], mem_in[t][l], B * H * W, glayers[l][2].threshold, s)
             if ctx.root:
                 eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s)
         except Exception:

@@ -1009,6 +1009,42 @@ def test_engine_gradients_wide_vs_oracle(dev, C):
                                    in zip(model.named_parameters(), ref.named_parameters())], ORACLE_GRAD_TOL)
 
 
+@pytest.mark.parametrize("recurrent", [False, True])
+def test_subtract_reset_cell_vs_oracle(dev, recurrent):
+    """A standalone SNNtorch_ConvLIF(Recurrent) cell with hard_reset=False (snn.Leaky reset_mechanism
+    "subtract", SNNtorch_spiking_submodules.py:171; reachable through the cell constructors only:
+    LIFFireNet does not pass spiking_neuron to its cells, models/model.py:53-56, 83-107) over 3
+    calls against SnnTorchCellRef: spikes, states and every parameter gradient.  The threshold's
+    gradient includes -sum r * dL/dv through v = beta*m + I - r*theta (snnflow_lif_theta_subtract)."""
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(31)
+    C, B, H, W = 8, 2, 24, 40
+    cls = snnflow.SNNtorch_ConvLIFRecurrent if recurrent else snnflow.SNNtorch_ConvLIF
+    cell = cls(C, C, 3, hard_reset=False, thresh=(0.2, 0.4)).to(dev).train()
+    ref = lif_ref.SnnTorchCellRef(C, C, 3, recurrent=recurrent, hard_reset=False).train()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in cell.state_dict().items()}, strict=False)
+    gen = torch.Generator().manual_seed(37)
+    xs = [(torch.rand(B, C, H, W, generator=gen) * 2.0) for _ in range(3)]
+    st, rst = None, None
+    loss = rloss = 0.0
+    for x in xs:
+        spk, st = cell(x.to(dev), st)
+        rspk, rst = ref(x, rst)
+        np.testing.assert_array_equal(spk.detach().cpu().numpy(), rspk.detach().numpy())
+        # (the subtract-reset membrane is not reset to 0: values up to ~3 carry fp32 rounding)
+        np.testing.assert_allclose(st.detach().cpu().numpy(), rst.detach().numpy(), rtol=1e-5, atol=1e-5)
+        wgt = torch.linspace(0.5, 1.5, C).view(1, C, 1, 1)
+        loss = loss + (spk * wgt.to(dev)).sum()
+        rloss = rloss + (rspk * wgt).sum()
+    loss.backward()
+    rloss.backward()
+    rp = dict(ref.named_parameters())
+    _grad_check(f"subtract cell rec={recurrent}", [(n, a.grad.cpu().numpy(), rp[n].grad.numpy())
+                                                   for n, a in cell.named_parameters()], ORACLE_GRAD_TOL)
+
+
 def test_forward_sequence_chained_without_detach(dev):
     """Two forward_sequence calls whose states are not detached in between (one BPTT window of
     2T steps): the second call's backward must hand its state gradients to the first (non-root
