@@ -340,19 +340,38 @@ def check(rc, what):
 
 
 class KernelTimer:
-    """Brackets every C-ABI launch with HIP events on the launch stream (opt-in; used
-    by bench.py to time the dominant kernel live).  records: list of (name, start, end)."""
+    """Brackets C-ABI launches with HIP events on the launch stream (opt-in; used by bench.py to
+    time the dominant kernel live).  records: list of (name, start, end, work, launches).
+
+    The wavefront launches (GROUPED) come in runs of consecutive launches of one kernel (the 26
+    forward or backward slots of a sequence): one event pair brackets the whole run and the run's
+    time is divided by its launch count.  An event pair around every single launch would add the
+    event commands' dispatch latency to each of these ~20-30 us kernels."""
+
+    GROUPED = ("fwd_slot", "bwd_slot")
 
     def __init__(self):
         self.records = []
+        self.open = None  # [name, start event, launches, work] of the run in progress
+
+    def close(self):
+        """End the open run of grouped launches (called before any other launch and by the
+        engine right after a wavefront loop)."""
+        if self.open is not None:
+            name, a, n, work = self.open
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            self.records.append((name, a, b, work, n))
+            self.open = None
 
     def summary(self):
+        self.close()
         torch.cuda.synchronize()
         out = {}
-        for name, a, b, work in self.records:
+        for name, a, b, work, cnt in self.records:
             ms = a.elapsed_time(b)
             n, tot, w = out.get(name, (0, 0.0, 0.0))
-            out[name] = (n + 1, tot + ms, w + (work or 0.0))
+            out[name] = (n + cnt, tot + ms, w + (work or 0.0))
         return {k: {"launches": n, "total_ms": tot, "avg_us": 1000.0 * tot / n, "work": w}
                 for k, (n, tot, w) in out.items()}
 
@@ -360,19 +379,37 @@ class KernelTimer:
 TIMER = None
 
 
+def timer_close():
+    """Close the KernelTimer's open run of grouped launches (no-op without a timer)."""
+    if TIMER is not None:
+        TIMER.close()
+
+
 def call(name, fn, *args, work=None):
     """Launch one C-ABI entry point; raise with the library's message on failure.  With a
-    KernelTimer installed the launch is bracketed by HIP events on the current stream and its
-    algorithmic `work` (FLOPs, if given) is recorded with it."""
+    KernelTimer installed the launch is bracketed by HIP events on the current stream (runs of
+    KernelTimer.GROUPED launches share one pair) and its algorithmic `work` (FLOPs, if given) is
+    recorded with it."""
     if TIMER is None:
         check(fn(*args), name)
         return
+    if name in TIMER.GROUPED:
+        if TIMER.open is None or TIMER.open[0] != name:
+            TIMER.close()
+            a = torch.cuda.Event(enable_timing=True)
+            a.record()
+            TIMER.open = [name, a, 0, 0.0]
+        check(fn(*args), name)
+        TIMER.open[2] += 1
+        TIMER.open[3] += work or 0.0
+        return
+    TIMER.close()
     a = torch.cuda.Event(enable_timing=True)
     b = torch.cuda.Event(enable_timing=True)
     a.record()
     check(fn(*args), name)
     b.record()
-    TIMER.records.append((name, a, b, work))
+    TIMER.records.append((name, a, b, work, 1))
 
 
 def ptr(t):

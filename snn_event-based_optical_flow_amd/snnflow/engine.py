@@ -920,6 +920,7 @@ class FireNetSequence(torch.autograd.Function):
                     top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons, flows[t])
             arr = (_lib.ConvFwdArgs * max(len(convs), 1))(*convs)
             _lib.call("fwd_slot", lib.snnflow_fwd_slot, arr, len(convs), ctypes.byref(top) if top is not None else None, s)
+        _lib.timer_close()
 
         for l in range(L):
             cells[l].lif.mem = states[T - 1][l][0].detach()
@@ -1023,6 +1024,7 @@ class FireNetSequence(torch.autograd.Function):
                 arr = (_lib.LayerBwdArgs * max(len(layers), 1))(*layers)
                 _lib.call("bwd_slot", lib.snnflow_bwd_slot, arr, len(layers),
                           ctypes.byref(top) if top is not None else None, s)
+            _lib.timer_close()
             for l in range(L):
                 for t in range(T):
                     theta_subtract(eng.cells[l], gcur[t][l], mem_in[t][l], B * H * W, glayers[l][2].threshold, s)
