@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 20
+#define SNNFLOW_ABI_VERSION 21
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -164,6 +164,10 @@ typedef struct snnflow_lif_bwd_args {
     float* g_mem;               /* NHWC grad of the membrane input (beta*(1-r)*g_v) or NULL */
     double* acc;                /* += SNNFLOW_BWD_ACC(c) sums (storage SNNFLOW_ACC_LEN of it) */
     double* zero0; double* zero1; int zero_n;
+    /* 1: the membrane half of g_state carries gradient (cells with detach=False,
+     * SNNtorch_spiking_submodules.py:309-311: mem_out = v - (s - r)*v | v - (s - r)*theta is not
+     * detached); its threshold part sum g_mo*(1 - s + r) goes to acc[3c + ch].  No prediction. */
+    int mem_grad_in;
 } snnflow_lif_bwd_args;
 int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream);
 

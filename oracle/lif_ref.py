@@ -156,13 +156,14 @@ class SnnTorchCellRef(nn.Module):
     """``SNNtorch_ConvLIF`` (``SNNtorch_spiking_submodules.py:124-322``) and, with
     ``recurrent=True``, ``SNNtorch_ConvLIFRecurrent`` (``:324-567``), fp32 branch:
     conv3x3 (no bias) [+ conv3x3 of previous spikes] -> BatchNorm2d -> Leaky;
-    membrane detached, state = stack([mem, spk]).  ``tebn``: TEBN in place of the BatchNorm
+    membrane detached (unless ``detach=False``, :309-311), state = stack([mem, spk]).  ``tebn``: TEBN in place of the BatchNorm
     (``:245-251``); ``mpbn``: state = stack([MPBN(mem), spk]) after the detach (``:313-317``)."""
 
     def __init__(self, cin, c, k=3, recurrent=False, leak=(0.0, 1.0), thresh=(0.0, 0.8), hard_reset=True,
-                 tebn=False, num_timesteps=4, mpbn=False):
+                 tebn=False, num_timesteps=4, mpbn=False, detach=True):
         super().__init__()
         self.input_size, self.hidden_size, self.recurrent = cin, c, recurrent
+        self.detach = detach
         beta0 = torch.empty(c, 1, 1).uniform_(leak[0], leak[1])
         th0 = torch.empty(c, 1, 1).uniform_(thresh[0], thresh[1])
         self.ff = nn.Conv2d(cin, c, k, padding=k // 2, bias=False)
@@ -184,8 +185,9 @@ class SnnTorchCellRef(nn.Module):
             cur = cur + self.rec(prev_spk)
         cur = self.bn(cur, timestep=timestep) if self.tebn else self.bn(cur)
         spk, mem = self.lif(cur, None if prev_state is None else prev_state[0])
-        self.lif.detach_hidden()
-        mem = mem.detach()
+        if self.detach:  # :309-311
+            self.lif.detach_hidden()
+            mem = mem.detach()
         if self.mpbn is not None:
             mem = self.mpbn(mem)
         return spk, torch.stack([mem, spk], dim=0)

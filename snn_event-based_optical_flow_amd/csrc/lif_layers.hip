@@ -196,7 +196,8 @@ __device__ void neuron_grads(const NeuronGradRegs& r, const double* sums, int C,
         const double gsum = sums[c], dotp = sums[C + c], gbm = sums[2 * C + c];
         const float gw = (float)(dotp * (double)r.inv);
         const float gb = (float)gsum;
-        const float gth = -(float)gsum;
+        // (no prediction: sums[3C + c] holds the membrane-output part of a detach=False cell, else 0)
+        const float gth = has_pred ? -(float)gsum : (float)(sums[3 * C + c] - gsum);
         const float gbe = (r.be >= 0.0f && r.be <= 1.0f) ? (float)gbm : 0.0f;
         ng.bn_weight[c] = r.o0 + gw;
         ng.bn_bias[c] = r.o1 + gb;
@@ -646,9 +647,29 @@ __global__ __launch_bounds__(NT) void k_lif_fwd(snnflow_lif_fwd_args a) {
 
 // Surrogate-gradient backward of the top LIF (+ pred): one thread per pixel; BN/neuron
 // sums into acc (block partials, fp64 atomics).
+// dL/dv of snn.Leaky when the membrane output also carries gradient g_mo (detach=False,
+// SNNtorch_spiking_submodules.py:309-311), from g_s (spike output) and the reset r = H(m - theta)
+// (detached): zero reset m_out = v (1 - s + r) -> g_v = sg (g_s - v g_mo) + g_mo (1 - s + r);
+// subtract reset m_out = v - (s - r) theta -> g_v = sg (g_s - theta g_mo) + g_mo.  The threshold
+// then receives -sum g_v (+ -sum r g_v, subtract: snnflow_lif_theta_subtract) plus gth =
+// g_mo (1 - s + r), summed separately.
+struct MemOutGrad { float gv, gth; };
+
+__device__ inline MemOutGrad mem_out_grad(float gs, float gmo, float m, const LifOut& o, const LifCoef& k, bool zr) {
+    const float sg = atan_sg(o.v - k.theta);
+    const float r = (m - k.theta > 0.0f) ? 1.0f : 0.0f;
+    const float keep = (1.0f - o.s) + r;
+    MemOutGrad d;
+    d.gv = zr ? sg * (gs - o.v * gmo) + gmo * keep : sg * (gs - k.theta * gmo) + gmo;
+    d.gth = gmo * keep;
+    return d;
+}
+
 template <int C, bool PRED, int NTH>
 __device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
-    constexpr int NV = 3 * C + (PRED ? 2 * C + 2 : 0), Q = C / 4;
+    // sums: (g, (y - mean) g, g m') per channel, then [pred: (gpre0 s, gpre1 s) per channel, gpre0,
+    // gpre1] or [no pred: the membrane-gradient threshold part g_mo (1 - s + r) per channel]
+    constexpr int NV = 3 * C + (PRED ? 2 * C + 2 : C), Q = C / 4;
     static_assert(NTH % NT == 0, "whole 256-thread parts");
     __shared__ LifCoef coef[C];
     __shared__ float meanv[C];
@@ -666,10 +687,12 @@ __device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
         mu = a.stats[tid];
     }
     float4 yv[Q], mv[Q], gs[Q];
+    [[maybe_unused]] float4 gmo4[PRED ? 1 : Q];
     const float4* y4 = reinterpret_cast<const float4*>(a.y);
     const float4* m4 = reinterpret_cast<const float4*>(a.mem);
     const float4* go4 = reinterpret_cast<const float4*>(a.g_out);
     const float4* gst4 = reinterpret_cast<const float4*>(a.g_state);
+    [[maybe_unused]] const bool mgi = !PRED && a.mem_grad_in && gst4;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         yv[q] = y4[pc * Q + q];  // unconditional 16-B loads (clamped pixel)
@@ -678,6 +701,7 @@ __device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
         const float4 t = ld4_or_zero(gst4 ? gst4 + plane4 : nullptr, y4, pc * Q + q);
         if (gst4) g = make_float4(g.x + t.x, g.y + t.y, g.z + t.z, g.w + t.w);
         gs[q] = g;
+        if constexpr (!PRED) gmo4[q] = ld4_or_zero(mgi ? gst4 : nullptr, y4, pc * Q + q);
     }
     float fl[2] = {0.f, 0.f}, gf[2] = {0.f, 0.f};
     if constexpr (PRED) {
@@ -723,7 +747,15 @@ __device__ void lif_bwd_body(const snnflow_lif_bwd_args& a, const Grid g) {
                     if (a.g_flow) g = g + (pw[c] * gpre[0] + pw[C + c] * gpre[1]);
                 }
                 const LifOut o = lif_step(yi[j], mi[j], coef[c], zr);
-                const float gv = atan_sg(o.v - coef[c].theta) * g;
+                float gv = atan_sg(o.v - coef[c].theta) * g;
+                if constexpr (!PRED) {
+                    if (mgi) {
+                        const float gm = j == 0 ? gmo4[q].x : (j == 1 ? gmo4[q].y : (j == 2 ? gmo4[q].z : gmo4[q].w));
+                        const MemOutGrad d = mem_out_grad(g, gm, mi[j], o, coef[c], zr);
+                        gv = d.gv;
+                        v[3 * C + c] += d.gth;
+                    }
+                }
                 go[j] = gv;
                 gmo[j] = mem_grad(gv, mi[j], coef[c], zr);
                 v[c] += gv;
@@ -850,7 +882,9 @@ __global__ __launch_bounds__(NT) void k_lif_fwd_q(snnflow_lif_fwd_args a, int it
 template <int C, bool PRED>
 __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int items) {
     constexpr int Q = C / 4, PPB = lifq_ppb(C);
-    constexpr int NVQ = 12 + (PRED ? 10 : 0);  // (g, (y - mean) g, g m') x 4 [+ (gpre0 s, gpre1 s) x 4 + gpre0, gpre1]
+    // (g, (y - mean) g, g m') x 4, then [pred: (gpre0 s, gpre1 s) x 4 + gpre0, gpre1] or
+    // [no pred: g_mo (1 - s + r) x 4, the membrane-output threshold part of detach=False cells]
+    constexpr int NVQ = 12 + (PRED ? 10 : 4);
     static_assert(Q >= 1 && Q <= 8 && (Q & (Q - 1)) == 0, "C = 4, 8, 16, 32");
     __shared__ LifCoef coef[C];
     __shared__ float meanv[C];
@@ -869,7 +903,8 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
     const float4* gst4 = reinterpret_cast<const float4*>(a.g_state);
     float4* gc4 = reinterpret_cast<float4*>(a.g_cur);
     float4* gm4 = reinterpret_cast<float4*>(a.g_mem);
-    struct Px { float4 y, m, g; float fl[2], gf[2]; };
+    const bool mgi = !PRED && a.mem_grad_in && gst4;
+    struct Px { float4 y, m, g, gm; float fl[2], gf[2]; };
     auto load = [&](int64_t pp, Px& x) {
         const int64_t pc = pp < npix ? pp : npix - 1;
         const int64_t i = pc * Q + q;
@@ -878,6 +913,7 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
         x.g = ld4_or_zero(go4, y4, i);
         const float4 t = ld4_or_zero(gst4 ? gst4 + plane4 : nullptr, y4, i);
         if (gst4) x.g = make_float4(x.g.x + t.x, x.g.y + t.y, x.g.z + t.z, x.g.w + t.w);
+        x.gm = ld4_or_zero(mgi ? gst4 : nullptr, y4, i);
         x.fl[0] = x.fl[1] = x.gf[0] = x.gf[1] = 0.f;
         if constexpr (PRED) {
             if (a.g_flow) {
@@ -928,7 +964,15 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
                     if (a.g_flow) g = g + (pw[c] * gpre[0] + pw[C + c] * gpre[1]);
                 }
                 const LifOut o = lif_step(yi[j], mi[j], kc[j], zr);
-                const float gv = atan_sg(o.v - kc[j].theta) * g;
+                float gv = atan_sg(o.v - kc[j].theta) * g;
+                if constexpr (!PRED) {
+                    if (mgi) {
+                        const float gm = j == 0 ? cur.gm.x : (j == 1 ? cur.gm.y : (j == 2 ? cur.gm.z : cur.gm.w));
+                        const MemOutGrad d = mem_out_grad(g, gm, mi[j], o, kc[j], zr);
+                        gv = d.gv;
+                        v[12 + j] += d.gth;
+                    }
+                }
                 go[j] = gv;
                 gmo[j] = mem_grad(gv, mi[j], kc[j], zr);
                 v[j] += gv;
@@ -965,7 +1009,7 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
     double* acc = acc_shard(a.acc, SNNFLOW_BWD_ACC(C), (int)blockIdx.x);
     for (int e = tid; e < Q * NVQ; e += NT) {
         const int qq = e / NVQ, j = e - qq * NVQ;
-        if (j >= 20 && qq != 0) continue;  // the per-pixel prediction-bias sums live in quad 0
+        if (PRED && j >= 20 && qq != 0) continue;  // the per-pixel prediction-bias sums live in quad 0
         float t = 0.0f;
 #pragma unroll
         for (int w = 0; w < NT / 64; ++w) t += red[w][qq][j];
@@ -2435,6 +2479,7 @@ int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
 static int lif_bwd_check(const snnflow_lif_bwd_args* a) {
     if (!a || !a->y || !a->stats || !a->g_cur || !a->acc) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: bad args");
     if (a->pred_w && !a->flow) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: pred needs flow");
+    if (a->mem_grad_in && a->pred_w) SNN_FAIL(SNNFLOW_E_ARG, "lif_bwd: mem_grad_in without prediction only");
     return 0;
 }
 

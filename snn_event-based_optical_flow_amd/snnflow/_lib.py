@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 
 class Neuron(ctypes.Structure):
@@ -54,7 +54,7 @@ class LifBwdArgs(ctypes.Structure):
                 ("g_out", P), ("g_state", P), ("pred_w", P), ("flow", P), ("g_flow", P),
                 ("gflow_sb", I64), ("gflow_sc", I64),
                 ("g_cur", P), ("g_mem", P), ("acc", P),
-                ("zero0", P), ("zero1", P), ("zero_n", I32)]
+                ("zero0", P), ("zero1", P), ("zero_n", I32), ("mem_grad_in", I32)]
 
 
 class LayerBwdArgs(ctypes.Structure):

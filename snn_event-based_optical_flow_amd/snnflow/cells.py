@@ -84,15 +84,15 @@ def _check_supported(kernel_size, stride, quantization_config, tebn, mpbn, norm,
         raise NotImplementedError("quantized (brevitas) cells are out of scope (DESIGN.md)")
     if norm is not None:
         raise NotImplementedError("norm='weight'/'group' variants are not implemented")
-    if not detach:
-        raise NotImplementedError("detach=False is not implemented")
+    if not detach and mpbn:
+        raise NotImplementedError("detach=False together with MPBN is not implemented")
 
 
 class _SnnTorchCellBase(nn.Module):
     recurrent = False
 
     def _build(self, input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset,
-               stride=1, tebn=False, num_timesteps=4, mpbn=False):
+               stride=1, tebn=False, num_timesteps=4, mpbn=False, detach=True):
         self.input_size, self.hidden_size = input_size, hidden_size
         pad = kernel_size // 2
         beta_init = torch.empty(hidden_size, 1, 1).uniform_(leak[0], leak[1])
@@ -115,7 +115,7 @@ class _SnnTorchCellBase(nn.Module):
         self.num_timesteps = num_timesteps
         self.mpbn = MPBN(hidden_size, momentum=0.1, eps=1e-5) if mpbn else None
         self.mpbn_enabled = bool(mpbn)
-        self.detach = True
+        self.detach = bool(detach)
         self.exporting = False
 
     @property
@@ -124,7 +124,16 @@ class _SnnTorchCellBase(nn.Module):
         return self.bn.bn if self.tebn_enabled else self.bn
 
     def forward(self, input_, prev_state, residual=0, timestep=None):
+        if not self.detach and prev_state is None:
+            # detach=False: snn.Leaky continues from its (non-detached) membrane cache, so the
+            # gradient reaches the call that produced it; zero spikes as the recurrent input
+            cache = self.lif.mem
+            B, _, H, W = input_.shape
+            if cache is not None and tuple(cache.shape) == (B, self.hidden_size, H, W) and cache.device == input_.device:
+                prev_state = torch.stack([cache, torch.zeros_like(cache)])
         spk, state = CellFn.apply(self, input_, prev_state, *self._params(timestep))
+        # SNNtorch_spiking_submodules.py:309-311: detach_hidden() + mem_out.detach() unless detach=False
+        self.lif.mem = state[0].detach() if self.detach else state[0]
         if self.mpbn_enabled:  # :313-317 / :558-562 (after the detach: no gradient into the LIF)
             state = MPBNStateFn.apply(state, self.mpbn.bn.weight, self.mpbn.bn.bias, self.mpbn.bn)
         return spk, state
@@ -152,7 +161,7 @@ class SNNtorch_ConvLIF(_SnnTorchCellBase):
         super().__init__()
         _check_supported(kernel_size, stride, quantization_config, tebn, mpbn, norm, detach, activation)
         self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset, stride,
-                    tebn, num_timesteps, mpbn)
+                    tebn, num_timesteps, mpbn, detach)
 
 
 class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
@@ -169,7 +178,7 @@ class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
         if input_size != hidden_size:
             raise NotImplementedError("recurrent cells with input_size != hidden_size are not compiled")
         self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset,
-                    1, tebn, num_timesteps, mpbn)
+                    1, tebn, num_timesteps, mpbn, detach)
 
 
 class ConvLayer(nn.Module):
@@ -267,7 +276,6 @@ class CellFn(torch.autograd.Function):
         f.B, f.H, f.W, f.c = B, H, W, C
         f.y, f.mem, f.acc, f.stats, f.n, f.state = ptr(y), _ptr_t(mem), ptr(facc), ptr(stats), n, ptr(state)
         _lib.call("lif_fwd", lib.snnflow_lif_fwd, ctypes.byref(f), s)
-        cell.lif.mem = state[0].detach()
         spk = state[1].detach().clone()  # a separate output tensor (same values as state[1])
         ctx.cell = cell
         ctx.has_mem, ctx.has_sp = mem is not None, sp is not None
@@ -308,6 +316,8 @@ class CellFn(torch.autograd.Function):
             b.g_out = ptr(gs)
         gst = as_nhwc_state(g_state) if g_state is not None else None
         b.g_state = _ptr_t(gst)
+        # detach=False: the membrane half of the state output carries gradient too
+        b.mem_grad_in = 1 if (gst is not None and not cell.detach) else 0
         g_prev = None
         if ctx.has_prev and ctx.needs_input_grad[2]:
             g_prev = torch.zeros((2, B, C, H, W), device=dev).as_strided(

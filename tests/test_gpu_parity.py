@@ -1045,6 +1045,46 @@ def test_subtract_reset_cell_vs_oracle(dev, recurrent):
                                                    for n, a in cell.named_parameters()], ORACLE_GRAD_TOL)
 
 
+@pytest.mark.parametrize("recurrent,hard", [(False, True), (True, True), (False, False), (True, False)])
+def test_detach_false_cell_vs_oracle(dev, recurrent, hard):
+    """SNNtorch_ConvLIF(Recurrent)(detach=False) (SNNtorch_spiking_submodules.py:309-311: the
+    membrane output keeps its graph, BPTT through the membrane): 4 calls, the first two chained
+    through prev_state, the third with prev_state=None (snn.Leaky continues from its non-detached
+    membrane cache), the fourth chained again; the loss uses spikes AND final membranes, so the
+    membrane-output gradient path (mem_grad_in) and its threshold part are exercised.  Every
+    parameter gradient and the input gradients against SnnTorchCellRef."""
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(41)
+    C, B, H, W = 8, 2, 24, 40
+    cls = snnflow.SNNtorch_ConvLIFRecurrent if recurrent else snnflow.SNNtorch_ConvLIF
+    cell = cls(C, C, 3, hard_reset=hard, detach=False, thresh=(0.2, 0.4)).to(dev).train()
+    ref = lif_ref.SnnTorchCellRef(C, C, 3, recurrent=recurrent, hard_reset=hard, detach=False).train()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in cell.state_dict().items()}, strict=False)
+    gen = torch.Generator().manual_seed(43)
+    xs = [(torch.rand(B, C, H, W, generator=gen) * 2.0).requires_grad_(True) for _ in range(4)]
+    xd = [x.detach().to(dev).requires_grad_(True) for x in xs]
+    st = rst = None
+    loss = rloss = 0.0
+    wgt = torch.linspace(0.5, 1.5, C).view(1, C, 1, 1)
+    for i, (x, xg) in enumerate(zip(xs, xd)):
+        if i == 2:
+            st = rst = None
+        spk, st = cell(xg, st)
+        rspk, rst = ref(x, rst)
+        np.testing.assert_array_equal(spk.detach().cpu().numpy(), rspk.detach().numpy())
+        np.testing.assert_allclose(st.detach().cpu().numpy(), rst.detach().numpy(), rtol=1e-5, atol=1e-5)
+        loss = loss + (spk * wgt.to(dev)).sum() + 0.1 * (st[0] * wgt.to(dev)).sum()
+        rloss = rloss + (rspk * wgt).sum() + 0.1 * (rst[0] * wgt).sum()
+    loss.backward()
+    rloss.backward()
+    rp = dict(ref.named_parameters())
+    pairs = [(n, a.grad.cpu().numpy(), rp[n].grad.numpy()) for n, a in cell.named_parameters()]
+    pairs += [(f"x{i}", a.grad.cpu().numpy(), b.grad.numpy()) for i, (a, b) in enumerate(zip(xd, xs))]
+    _grad_check(f"detach=False rec={recurrent} hard={hard}", pairs, ORACLE_GRAD_TOL)
+
+
 def test_forward_sequence_chained_without_detach(dev):
     """Two forward_sequence calls whose states are not detached in between (one BPTT window of
     2T steps): the second call's backward must hand its state gradients to the first (non-root
