@@ -816,27 +816,43 @@ __device__ inline unsigned quad_or(unsigned v) {
     return v;
 }
 
+// NTH threads per block (NT standalone, NT * 2 as a wavefront task); g: the block's grid (a task's
+// block range inside a wavefront launch); each thread takes `items` = ceil(npix / (PPB g.nb)) pixels.
+template <int C, int NTH>
+__device__ inline int lifq_body_items(int64_t npix, const Grid& g) {
+    const int64_t per = (int64_t)(NTH / (C / 4)) * g.nb;
+    return (int)((npix + per - 1) / per);
+}
+
+// LDS (floats, carved out of the caller's pool: inside a wavefront launch the task kinds share one
+// pool) of the quad bodies
+template <int C>
+constexpr int kLifQFwdLds = 4 * C + 4 * C;  // coef[C], sums[2C] (doubles)
 template <int C, bool PRED>
-__global__ __launch_bounds__(NT) void k_lif_fwd_q(snnflow_lif_fwd_args a, int items) {
-    constexpr int Q = C / 4, PPB = lifq_ppb(C);
+constexpr int kLifQBwdLds = 4 * C + C + (C / 4) * (12 + (PRED ? 10 : 4));  // coef[C], meanv[C], red[Q][NVQ]
+
+template <int C, bool PRED, int NTH>
+__device__ void lif_fwd_q_body(const snnflow_lif_fwd_args& a, const Grid g, float* lds) {
+    constexpr int Q = C / 4, PPB = NTH / Q;
     static_assert(Q >= 1 && Q <= 8 && (Q & (Q - 1)) == 0, "C = 4, 8, 16, 32");
-    __shared__ LifCoef coef[C];
+    LifCoef* const coef = reinterpret_cast<LifCoef*>(lds);
+    double* const sums = reinterpret_cast<double*>(lds + 4 * C);
     const int tid = threadIdx.x, q = tid % Q, ps = tid / Q;
     const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
+    const int items = lifq_body_items<C, NTH>(npix, g);
     const float4* y4 = reinterpret_cast<const float4*>(a.y);
     const float4* m4 = reinterpret_cast<const float4*>(a.mem);
-    const bool lead = blockIdx.x == 0;
+    const bool lead = g.bid == 0;
     AccGather<2 * C> gat;
     if (a.n.bn_train) acc_gather_load<2 * C>(a.acc, 2 * C, gat);
     const NeuronRegs nr = load_neuron(a.n, C, lead);
-    int64_t p = (int64_t)blockIdx.x * items * PPB + ps;
+    int64_t p = (int64_t)g.bid * items * PPB + ps;
     int64_t pc = p < npix ? p : npix - 1;  // unconditional 16-B loads
     float4 yv = y4[pc * Q + q], mv = ld4_or_zero(m4, y4, pc * Q + q);
-    __shared__ double sums[2 * C];
     if (a.n.bn_train) acc_gather_reduce<2 * C>(gat, sums);
     lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr, lead);
     __syncthreads();
-    zero_consumed(a.zero0, a.zero1, a.zero_n);
+    zero_consumed(a.zero0, a.zero1, a.zero_n, g);
     const bool zr = a.n.zero_reset != 0;
     const LifCoef kc[4] = {coef[4 * q], coef[4 * q + 1], coef[4 * q + 2], coef[4 * q + 3]};
     float4* st4 = reinterpret_cast<float4*>(a.state);
@@ -880,17 +896,25 @@ __global__ __launch_bounds__(NT) void k_lif_fwd_q(snnflow_lif_fwd_args a, int it
 }
 
 template <int C, bool PRED>
-__global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int items) {
-    constexpr int Q = C / 4, PPB = lifq_ppb(C);
+__global__ __launch_bounds__(NT) void k_lif_fwd_q(snnflow_lif_fwd_args a) {
+    __shared__ __attribute__((aligned(16))) float pool[kLifQFwdLds<C>];
+    lif_fwd_q_body<C, PRED, NT>(a, hw_grid(), pool);
+}
+
+template <int C, bool PRED, int NTH>
+__device__ void lif_bwd_q_body(const snnflow_lif_bwd_args& a, const Grid gr, float* lds) {
+    constexpr int Q = C / 4, PPB = NTH / Q;
     // (g, (y - mean) g, g m') x 4, then [pred: (gpre0 s, gpre1 s) x 4 + gpre0, gpre1] or
     // [no pred: g_mo (1 - s + r) x 4, the membrane-output threshold part of detach=False cells]
     constexpr int NVQ = 12 + (PRED ? 10 : 4);
     static_assert(Q >= 1 && Q <= 8 && (Q & (Q - 1)) == 0, "C = 4, 8, 16, 32");
-    __shared__ LifCoef coef[C];
-    __shared__ float meanv[C];
-    __shared__ float red[NT / 64][Q][NVQ];
-    const int tid = threadIdx.x, q = tid % Q, ps = tid / Q, lane = tid & 63, wv = tid >> 6;
+    static_assert(kLifQBwdLds<C, PRED> == 5 * C + Q * NVQ, "LDS size");
+    LifCoef* const coef = reinterpret_cast<LifCoef*>(lds);
+    float* const meanv = lds + 4 * C;
+    float(*const red)[NVQ] = reinterpret_cast<float(*)[NVQ]>(lds + 5 * C);  // [Q][NVQ] block totals (LDS atomics)
+    const int tid = threadIdx.x, q = tid % Q, ps = tid / Q, lane = tid & 63;
     const int64_t HWp = (int64_t)a.H * a.W, npix = (int64_t)a.B * HWp, plane4 = npix * Q;
+    const int items = lifq_body_items<C, NTH>(npix, gr);
     LifCoef kci = {0.f, 0.f, 0.f, 0.f};
     float mu = 0.f;
     if (tid < C) {
@@ -926,13 +950,14 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
             }
         }
     };
-    int64_t p = (int64_t)blockIdx.x * items * PPB + ps;
+    int64_t p = (int64_t)gr.bid * items * PPB + ps;
     Px cur;
     load(p, cur);
     if (tid < C) {
         coef[tid] = kci;
         meanv[tid] = mu;
     }
+    for (int e = tid; e < Q * NVQ; e += NTH) (&red[0][0])[e] = 0.0f;
     __syncthreads();
     const bool zr = a.n.zero_reset != 0;
     const LifCoef kc[4] = {coef[4 * q], coef[4 * q + 1], coef[4 * q + 2], coef[4 * q + 3]};
@@ -995,7 +1020,7 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
         p += PPB;
         cur = nx;
     }
-    // lanes of equal quad (lane % Q) summed across the wave, then the four waves in order
+    // lanes of equal quad (lane % Q) summed across the wave, the waves' totals through LDS atomics
 #pragma unroll
     for (int j = 0; j < NVQ; ++j) {
 #pragma unroll
@@ -1003,20 +1028,23 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a, int it
     }
     if (lane < Q) {
 #pragma unroll
-        for (int j = 0; j < NVQ; ++j) red[wv][lane][j] = v[j];
+        for (int j = 0; j < NVQ; ++j) atomicAdd(&red[lane][j], v[j]);
     }
     __syncthreads();
-    double* acc = acc_shard(a.acc, SNNFLOW_BWD_ACC(C), (int)blockIdx.x);
-    for (int e = tid; e < Q * NVQ; e += NT) {
+    double* acc = acc_shard(a.acc, SNNFLOW_BWD_ACC(C), gr.bid);
+    for (int e = tid; e < Q * NVQ; e += NTH) {
         const int qq = e / NVQ, j = e - qq * NVQ;
         if (PRED && j >= 20 && qq != 0) continue;  // the per-pixel prediction-bias sums live in quad 0
-        float t = 0.0f;
-#pragma unroll
-        for (int w = 0; w < NT / 64; ++w) t += red[w][qq][j];
         const int k = j < 20 ? (j / 4) * C + 4 * qq + (j & 3) : 5 * C + (j - 20);
-        atomicAdd(acc + k, (double)t);
+        atomicAdd(acc + k, (double)red[qq][j]);
     }
-    zero_consumed(a.zero0, a.zero1, a.zero_n);  // last: no load waits behind these stores
+    zero_consumed(a.zero0, a.zero1, a.zero_n, gr);  // last: no load waits behind these stores
+}
+
+template <int C, bool PRED>
+__global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a) {
+    __shared__ __attribute__((aligned(16))) float pool[kLifQBwdLds<C, PRED>];
+    lif_bwd_q_body<C, PRED, NT>(a, hw_grid(), pool);
 }
 
 // Subtract-reset threshold gradient (include/snnflow.h snnflow_lif_theta_subtract): thread per
@@ -1787,9 +1815,14 @@ __global__ __launch_bounds__(NT * 2) void k_wgrad_bf(snnflow_wgrad_args) {
     constexpr int RX = Halo4<C, NTB>::R;
     using O = Own4<C, NTB>;
     static_assert(NW == 8, "8 waves");
-    __shared__ __attribute__((aligned(16))) float Gt[C * Gm::GS];
-    __shared__ __attribute__((aligned(16))) unsigned short Xt[C * Gm::XS];
-    __shared__ __attribute__((aligned(16))) unsigned short St[REC ? C * Gm::XS : 8];
+    // one pool for G^T, X^T, S^T: the row-group reduction at the end aliases all of it
+    // (separate __shared__ arrays are not guaranteed to be contiguous)
+    constexpr int GF = C * Gm::GS, XF = C * Gm::XS / 2, SF = REC ? C * Gm::XS / 2 : 4;
+    constexpr int RF = Gm::TG * Gm::TPW * 256;
+    __shared__ __attribute__((aligned(16))) float pool[(GF + XF + SF > RF ? GF + XF + SF : RF)];
+    float* const Gt = pool;
+    unsigned short* const Xt = reinterpret_cast<unsigned short*>(pool + GF);
+    unsigned short* const St = reinterpret_cast<unsigned short*>(pool + GF + XF);
     __shared__ BnBwdLds coef[SNNFLOW_MAX_WGRAD_STEPS][C];
 
     const cwgrad_ptr ap = (cwgrad_ptr)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1963,7 +1996,7 @@ __global__ __launch_bounds__(NT * 2) void k_wgrad_bf(snnflow_wgrad_args) {
     }
 
     // row groups 1..RG-1 add into row group 0 through LDS (fixed order), aliasing Gt/Xt/St
-    float* red = Gt;  // [TG][TPW][64][4] floats
+    float* red = pool;  // [TG][TPW][64][4] floats (RF)
 #pragma unroll 1
     for (int q = 1; q < Gm::RG; ++q) {
         if (rg == q) {
@@ -2126,15 +2159,25 @@ struct BwdSlotParams {
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+// Task kinds compiled into the slot kernels: every kind at C = 8; at C = 16 / 32 only those of the
+// LIFFireNet family (2- or 4-bin head, LIF-fed layers, top LIF): the plain C-channel convs would set
+// the pool to ~100 KB and the registers to ~146, i.e. one block per CU for every task.
+template <int C>
+constexpr bool kSlotAllKinds = C == 8;
+
 template <int C>
 struct SlotLds {
-    static constexpr int FWD = cmax(cmax(cmax(ConvFwdLds<1, C, false, false, 2>::FLOATS, ConvFwdLds<2, C, false, false, 2>::FLOATS),
-                                         cmax(ConvFwdLds<4, C, false, false, 2>::FLOATS, ConvFwdLds<5, C, false, false, 2>::FLOATS)),
-                                    cmax(cmax(ConvFwdLds<C, C, false, false, 2>::FLOATS, ConvFwdLds<C, C, false, true, 2>::FLOATS),
+    static constexpr int FWD_ALL = cmax(cmax(ConvFwdLds<1, C, false, false, 2>::FLOATS, ConvFwdLds<5, C, false, false, 2>::FLOATS),
+                                        cmax(ConvFwdLds<C, C, false, false, 2>::FLOATS, ConvFwdLds<C, C, false, true, 2>::FLOATS));
+    static constexpr int FWD = cmax(cmax(kSlotAllKinds<C> ? FWD_ALL : 0, kLifQFwdLds<C>),
+                                    cmax(cmax(ConvFwdLds<2, C, false, false, 2>::FLOATS, ConvFwdLds<4, C, false, false, 2>::FLOATS),
                                          cmax(ConvFwdLds<C, C, true, false, 2>::FLOATS, ConvFwdLds<C, C, true, true, 2>::FLOATS)));
-    static constexpr int BWD = cmax(cmax(LayerBwdLds<2, C, false, false, 2>::FLOATS, LayerBwdLds<4, C, false, false, 2>::FLOATS),
-                                    cmax(cmax(LayerBwdLds<C, C, false, false, 2>::FLOATS, LayerBwdLds<C, C, false, true, 2>::FLOATS),
-                                         cmax(LayerBwdLds<C, C, true, false, 2>::FLOATS, LayerBwdLds<C, C, true, true, 2>::FLOATS)));
+    static constexpr bool BFG = C >= 16;  // LIF-fed layers: bf16 six-product input gradients from global fragments
+    static constexpr int BWD_ALL = cmax(LayerBwdLds<C, C, false, false, 2>::FLOATS, LayerBwdLds<C, C, false, true, 2>::FLOATS);
+    static constexpr int BWD = cmax(cmax(cmax(kSlotAllKinds<C> ? BWD_ALL : 0, kLifQBwdLds<C, true>),
+                                         cmax(LayerBwdLds<2, C, false, false, 2>::FLOATS, LayerBwdLds<4, C, false, false, 2>::FLOATS)),
+                                    cmax(LayerBwdLds<C, C, true, false, 2, BFG>::FLOATS,
+                                         LayerBwdLds<C, C, true, true, 2, BFG>::FLOATS));
 };
 
 // A by-value copy of a kernarg-resident struct (dword loads from the constant address
@@ -2229,29 +2272,34 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
     if (g.bid >= g.nb) return;  // padding block of a range
     __shared__ __attribute__((aligned(16))) float pool[SlotLds<C>::FWD];
     switch (pp->kind[k]) {
-#define FWD_CONV(KIND, ...)                                   \
+#define FWD_CONV(ALL, KIND, ...)                              \
     case KIND: {                                              \
-        const snnflow_conv_fwd_args a = task_args(&pp->conv[k]);             \
-        conv_fwd_body<__VA_ARGS__>(a, g, pool);               \
+        if constexpr (ALL || kSlotAllKinds<C>) {              \
+            const snnflow_conv_fwd_args a = task_args(&pp->conv[k]);         \
+            conv_fwd_body<__VA_ARGS__>(a, g, pool);           \
+        }                                                     \
         break;                                                \
     }
-        FWD_CONV(SK_HEAD1, 1, C, false, false, 2)
-        FWD_CONV(SK_HEAD2, 2, C, false, false, 2)
-        FWD_CONV(SK_HEAD4, 4, C, false, false, 2)
-        FWD_CONV(SK_HEAD5, 5, C, false, false, 2)
-        FWD_CONV(SK_PLAIN, C, C, false, false, 2)
-        FWD_CONV(SK_PLAIN_REC, C, C, false, true, 2)
-        FWD_CONV(SK_LIF, C, C, true, false, 2)
-        FWD_CONV(SK_LIF_REC, C, C, true, true, 2)
+        FWD_CONV(false, SK_HEAD1, 1, C, false, false, 2)
+        FWD_CONV(true, SK_HEAD2, 2, C, false, false, 2)
+        FWD_CONV(true, SK_HEAD4, 4, C, false, false, 2)
+        FWD_CONV(false, SK_HEAD5, 5, C, false, false, 2)
+        FWD_CONV(false, SK_PLAIN, C, C, false, false, 2)
+        FWD_CONV(false, SK_PLAIN_REC, C, C, false, true, 2)
+        FWD_CONV(true, SK_LIF, C, C, true, false, 2)
+        FWD_CONV(true, SK_LIF_REC, C, C, true, true, 2)
 #undef FWD_CONV
-        case SK_TOP: {
-            const snnflow_lif_fwd_args a = task_args(&pp->lif);
-            lif_fwd_body<C, false, NT * 2>(a, g);
+        case SK_TOP: {  // (LIFFireNet's top layer always carries the prediction: C = 8 only)
+            if constexpr (kSlotAllKinds<C>) {
+                const snnflow_lif_fwd_args a = task_args(&pp->lif);
+                lif_fwd_body<C, false, NT * 2>(a, g);
+            }
             break;
         }
         case SK_TOP_PRED: {
             const snnflow_lif_fwd_args a = task_args(&pp->lif);
-            lif_fwd_body<C, true, NT * 2>(a, g);
+            if constexpr (C >= 16) lif_fwd_q_body<C, true, NT * 2>(a, g, pool);
+            else lif_fwd_body<C, true, NT * 2>(a, g);
             break;
         }
         default: break;
@@ -2262,7 +2310,7 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
 #define SNNFLOW_BWD_SLOT_WAVES 6  // min waves per SIMD: 3 blocks per CU (measured: 2 per CU is 15 % slower)
 #endif
 template <int C>
-__global__ __launch_bounds__(NT * 2, SNNFLOW_BWD_SLOT_WAVES) void k_bwd_slot(BwdSlotParams) {
+__global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L32_WAVES) void k_bwd_slot(BwdSlotParams) {
     typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
     const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
     Grid g;
@@ -2270,27 +2318,32 @@ __global__ __launch_bounds__(NT * 2, SNNFLOW_BWD_SLOT_WAVES) void k_bwd_slot(Bwd
     if (g.bid >= g.nb) return;
     __shared__ __attribute__((aligned(16))) float pool[SlotLds<C>::BWD];
     switch (pp->kind[k]) {
-#define BWD_LAYER(KIND, ...)                                  \
+#define BWD_LAYER(ALL, KIND, ...)                             \
     case KIND: {                                              \
-        const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);           \
-        layer_bwd_body<__VA_ARGS__>(a, g, pool);              \
+        if constexpr (ALL || kSlotAllKinds<C>) {              \
+            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);       \
+            layer_bwd_body<__VA_ARGS__>(a, g, pool);          \
+        }                                                     \
         break;                                                \
     }
-        BWD_LAYER(SK_HEAD2, 2, C, false, false, 2)
-        BWD_LAYER(SK_HEAD4, 4, C, false, false, 2)
-        BWD_LAYER(SK_PLAIN, C, C, false, false, 2)
-        BWD_LAYER(SK_PLAIN_REC, C, C, false, true, 2)
-        BWD_LAYER(SK_LIF, C, C, true, false, 2)
-        BWD_LAYER(SK_LIF_REC, C, C, true, true, 2)
+        BWD_LAYER(true, SK_HEAD2, 2, C, false, false, 2)
+        BWD_LAYER(true, SK_HEAD4, 4, C, false, false, 2)
+        BWD_LAYER(false, SK_PLAIN, C, C, false, false, 2)
+        BWD_LAYER(false, SK_PLAIN_REC, C, C, false, true, 2)
+        BWD_LAYER(true, SK_LIF, C, C, true, false, 2, SlotLds<C>::BFG)
+        BWD_LAYER(true, SK_LIF_REC, C, C, true, true, 2, SlotLds<C>::BFG)
 #undef BWD_LAYER
         case SK_TOP: {
-            const snnflow_lif_bwd_args a = task_args(&pp->lif);
-            lif_bwd_body<C, false, NT * 2>(a, g);
+            if constexpr (kSlotAllKinds<C>) {
+                const snnflow_lif_bwd_args a = task_args(&pp->lif);
+                lif_bwd_body<C, false, NT * 2>(a, g);
+            }
             break;
         }
         case SK_TOP_PRED: {
             const snnflow_lif_bwd_args a = task_args(&pp->lif);
-            lif_bwd_body<C, true, NT * 2>(a, g);
+            if constexpr (C >= 16) lif_bwd_q_body<C, true, NT * 2>(a, g, pool);
+            else lif_bwd_body<C, true, NT * 2>(a, g);
             break;
         }
         default: break;
@@ -2464,8 +2517,8 @@ int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream) {
         break;
 #define LIF_FWD_Q_CASE(CC)                                                                   \
     case CC:                                                                                 \
-        if (pred) hipLaunchKernelGGL((k_lif_fwd_q<CC, true>), grid, block, 0, s, *a, items); \
-        else hipLaunchKernelGGL((k_lif_fwd_q<CC, false>), grid, block, 0, s, *a, items);     \
+        if (pred) hipLaunchKernelGGL((k_lif_fwd_q<CC, true>), grid, block, 0, s, *a); \
+        else hipLaunchKernelGGL((k_lif_fwd_q<CC, false>), grid, block, 0, s, *a);     \
         break;
         LIF_FWD_CASE(4) LIF_FWD_CASE(8) LIF_FWD_Q_CASE(16) LIF_FWD_Q_CASE(32)
 #undef LIF_FWD_Q_CASE
@@ -2498,8 +2551,8 @@ int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
         break;
 #define LIF_BWD_Q_CASE(CC)                                                                   \
     case CC:                                                                                 \
-        if (pred) hipLaunchKernelGGL((k_lif_bwd_q<CC, true>), grid, block, 0, s, *a, items); \
-        else hipLaunchKernelGGL((k_lif_bwd_q<CC, false>), grid, block, 0, s, *a, items);     \
+        if (pred) hipLaunchKernelGGL((k_lif_bwd_q<CC, true>), grid, block, 0, s, *a); \
+        else hipLaunchKernelGGL((k_lif_bwd_q<CC, false>), grid, block, 0, s, *a);     \
         break;
         LIF_BWD_CASE(4) LIF_BWD_CASE(8) LIF_BWD_Q_CASE(16) LIF_BWD_Q_CASE(32)
 #undef LIF_BWD_Q_CASE
@@ -2556,7 +2609,17 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
 
 // C = 8 only: one layer-step of C = 16 / 32 already fills the chip for a launch (and the
 // merged variants would spill registers there).
-static bool slot_c(int c) { return c == 8; }
+static bool slot_c(int c) { return c == 8 || c == 16 || c == 32; }
+
+// Blocks of the top (LIF [+ pred]) task: C = 8 one pixel per thread; C >= 16 the quad layout
+// (lif_*_q_body), sized like a conv task so its blocks last about as long as theirs.
+static int slot_top_blocks(int c, int B, int H, int W) {
+    const int64_t npix = (int64_t)B * H * W;
+    if (c < 16) return (int)((npix + 2 * NT - 1) / (2 * NT));
+    const int64_t ppb = 2 * NT / (c / 4), target = snnflow_conv_blocks(B, H, W);
+    const int64_t items = (npix + ppb * target - 1) / (ppb * target);
+    return (int)((npix + ppb * items - 1) / (ppb * items));
+}
 
 int snnflow_slot_supported(int c, int cin0) { return slot_c(c) && (cin0 == 2 || cin0 == 4) ? 1 : 0; }
 
@@ -2576,7 +2639,7 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
     FwdSlotParams p = {};
     const int c = nconv ? conv[0].c : lif->c;
     const int B = nconv ? conv[0].B : lif->B, H = nconv ? conv[0].H : lif->H, W = nconv ? conv[0].W : lif->W;
-    if (!slot_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c must be 8");
+    if (!slot_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c must be 8, 16 or 32");
     for (int i = 0; i < nconv; ++i) {
         const snnflow_conv_fwd_args& a = conv[i];
         if (const int e = conv_fwd_check(&a)) return e;
@@ -2595,6 +2658,8 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         } else {
             SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: unsupported cin");
         }
+        if (c != 8 && !(kind == SK_HEAD2 || kind == SK_HEAD4 || kind == SK_LIF || kind == SK_LIF_REC))
+            SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c = 16 / 32 runs the LIFFireNet task kinds only");
         p.conv[i] = a;
         p.kind[i] = kind;
         p.nblk[i] = snnflow_conv_blocks(B, H, W);
@@ -2603,14 +2668,17 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         if (const int e = lif_fwd_check(lif)) return e;
         if (lif->c != c || lif->B != B || lif->H != H || lif->W != W)
             SNN_FAIL(SNNFLOW_E_ARG, "fwd_slot: tasks of different shapes");
+        if (c != 8 && !lif->pred_w) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c = 16 / 32 top task needs the prediction");
         p.lif = *lif;
         p.kind[nconv] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
-        p.nblk[nconv] = (int)(((int64_t)B * H * W + 2 * NT - 1) / (2 * NT));
+        p.nblk[nconv] = slot_top_blocks(c, B, H, W);
     }
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_fwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    if (c == 8) hipLaunchKernelGGL(k_fwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    else if (c == 16) hipLaunchKernelGGL(k_fwd_slot<16>, dim3(nb), dim3(2 * NT), 0, s, p);
+    else hipLaunchKernelGGL(k_fwd_slot<32>, dim3(nb), dim3(2 * NT), 0, s, p);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -2622,7 +2690,7 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
     BwdSlotParams p = {};
     const int c = nlayer ? layer[0].c : lif->c;
     const int B = nlayer ? layer[0].B : lif->B, H = nlayer ? layer[0].H : lif->H, W = nlayer ? layer[0].W : lif->W;
-    if (!slot_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c must be 8");
+    if (!slot_c(c)) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c must be 8, 16 or 32");
     for (int i = 0; i < nlayer; ++i) {
         const snnflow_layer_bwd_args& a = layer[i];
         if (const int e = layer_bwd_check(&a)) return e;
@@ -2630,6 +2698,8 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         int kind;
         if (a.lif_in) {
             if (a.cin != c) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: lif_in requires cin == c");
+            if (c >= 16 && (!a.wd_ff || (a.wt_bwd_rec && a.g_state_prev && !a.wd_rec)))
+                SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: c >= 16 needs the pre-split input-gradient fragments wd_ff / wd_rec");
             kind = a.wt_bwd_rec ? SK_LIF_REC : SK_LIF;
         } else if (a.wt_bwd_rec) {
             if (a.cin != c) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: recurrent cell requires cin == c");
@@ -2641,6 +2711,8 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         } else {
             SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: unsupported cin (2, 4 or c)");
         }
+        if (c != 8 && !(kind == SK_HEAD2 || kind == SK_HEAD4 || kind == SK_LIF || kind == SK_LIF_REC))
+            SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c = 16 / 32 runs the LIFFireNet task kinds only");
         p.layer[i] = a;
         p.kind[i] = kind;
         p.nblk[i] = layer_bwd_blocks(a);
@@ -2649,14 +2721,18 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         if (const int e = lif_bwd_check(lif)) return e;
         if (lif->c != c || lif->B != B || lif->H != H || lif->W != W)
             SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: tasks of different shapes");
+        if (lif->mem_grad_in) SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: mem_grad_in is a standalone-cell option");
+        if (c != 8 && !lif->pred_w) SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c = 16 / 32 top task needs the prediction");
         p.lif = *lif;
         p.kind[nlayer] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
-        p.nblk[nlayer] = (int)(((int64_t)B * H * W + 2 * NT - 1) / (2 * NT));
+        p.nblk[nlayer] = slot_top_blocks(c, B, H, W);
     }
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_bwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    if (c == 8) hipLaunchKernelGGL(k_bwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    else if (c == 16) hipLaunchKernelGGL(k_bwd_slot<16>, dim3(nb), dim3(2 * NT), 0, s, p);
+    else hipLaunchKernelGGL(k_bwd_slot<32>, dim3(nb), dim3(2 * NT), 0, s, p);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -218,7 +218,7 @@ class FireNetEngine:
         return self._neurons[1]
 
     def sequence_ok(self, cin0):
-        """True if FireNetSequence's wavefront launches take this model (C = 8, cin0 2 or 4)."""
+        """True if FireNetSequence's wavefront launches take this model (C = 8, 16, 32; cin0 2 or 4)."""
         return bool(lib.snnflow_slot_supported(self.C, cin0))
 
     # parameter order = Function input order after the states

@@ -134,7 +134,8 @@ def test_slot_and_fragment_entry_points_validate_without_gpu():
     from snnflow import _lib
 
     lib = _lib.lib
-    assert lib.snnflow_slot_supported(8, 2) == 1 and lib.snnflow_slot_supported(32, 2) == 0
+    assert lib.snnflow_slot_supported(8, 2) == 1 and lib.snnflow_slot_supported(32, 2) == 1
+    assert lib.snnflow_slot_supported(16, 4) == 1 and lib.snnflow_slot_supported(12, 2) == 0
     assert lib.snnflow_slot_supported(8, 5) == 0
     conv = (_lib.ConvFwdArgs * 5)()
     assert lib.snnflow_fwd_slot(conv, 5, None, None) == -1          # more than 4 tasks
@@ -146,8 +147,12 @@ def test_slot_and_fragment_entry_points_validate_without_gpu():
     conv[1].H = 16
     assert lib.snnflow_fwd_slot(conv, 2, None, None) == -1          # tasks of different shapes
     assert b"shapes" in lib.snnflow_last_error()
-    conv[0].c = conv[1].c = 16
-    assert lib.snnflow_fwd_slot(conv, 1, None, None) == -2          # c != 8
+    conv[0].c = conv[1].c = 12
+    assert lib.snnflow_fwd_slot(conv, 1, None, None) == -2          # c not 8, 16 or 32
+    conv[0].c = conv[0].cin = 32
+    conv[0].wt_ff_t = 1
+    assert lib.snnflow_fwd_slot(conv, 1, None, None) == -2          # c = 32: LIFFireNet task kinds only (no plain conv)
+    assert b"task kinds" in lib.snnflow_last_error()
     layer = (_lib.LayerBwdArgs * 1)()
     assert lib.snnflow_bwd_slot(layer, 1, None, None) == -2         # c = 0
     layer[0].c = 8

@@ -841,7 +841,15 @@ def test_forward_sequence_matches_per_step_full_size(dev, H, B):
     assert all(torch.isfinite(p.grad).all() for p in mb.parameters())
 
 
-def _check_sequence_vs_per_step(dev, H, W, T, name, B, N, iters):
+@pytest.mark.parametrize("C", [16, 32])
+def test_forward_sequence_matches_per_step_wide(dev, C):
+    """C = 16 / 32 wavefront launches (LIFFireNet task kinds in k_fwd_slot / k_bwd_slot, the top
+    LIF in the quad layout, bf16 six-product input gradients from global fragments) against the
+    per-step calls: flows, loss, gradients, states, running statistics over two windows."""
+    _check_sequence_vs_per_step(dev, 48, 64, 3, "LIFFireNet", B=2, N=300, iters=2, C=C)
+
+
+def _check_sequence_vs_per_step(dev, H, W, T, name, B, N, iters, C=8):
     """T steps through model.forward_sequence (wavefront launches, FireNetSequence) against T
     model.forward calls (FireNetStep) of an identical copy: flows, loss, every parameter
     gradient, final states, lif.mem caches and BatchNorm running statistics, over two
@@ -855,9 +863,10 @@ def _check_sequence_vs_per_step(dev, H, W, T, name, B, N, iters):
     from snnflow.synthetic import make_window
 
     torch.manual_seed(5)
-    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=C)
     ma = getattr(snnflow, name)(dict(kw)).to(dev).train()
     mb = copy.deepcopy(ma)
+    assert mb.engine.sequence_ok(2)  # the wavefront path runs
     cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
            "model": {"mask_output": True}}
     ea, eb = snnflow.EventWarping(cfg, dev), snnflow.EventWarping(cfg, dev)
