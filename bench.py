@@ -169,7 +169,7 @@ def main():
             outs = [model(w["event_voxel"], w["event_cnt"]) for w in static]
         elif args.per_step:
             outs = [model(w["event_voxel"], w["event_cnt"]) for w in static]
-        else:  # the same T steps, kernels issued as wavefront launches (C = 8; else per step)
+        else:  # the same T steps, kernels issued as wavefront launches (C = 8, 16, 32; else per step)
             outs = model.forward_sequence([w["event_voxel"] for w in static], [w["event_cnt"] for w in static])
         for t in range(T):
             w = static[t]
