@@ -178,7 +178,7 @@ class _FireNetBase(BaseModel):
         ``lif.mem`` caches as T ``forward`` calls -- returns their T result dicts -- with the
         steps' kernels issued as wavefront launches (engine.FireNetSequence).  With ``log`` the T
         activity dicts come from one count launch per 16 tensors and one read-back.  Falls back to
-        T ``forward`` calls where those launches do not apply (hooks, C != 8)."""
+        T ``forward`` calls where those launches do not apply (hooks, TEBN/MPBN, C = 4)."""
         seq = event_voxels if self.encoding == "voxel" else event_cnts
         T = len(seq)
         none = [None] * T
