@@ -378,13 +378,23 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
 
 // Per event: gather dL/d(images) at the 4 corners of both warps, chain through the
 // bilinear weights to the warped position and the per-event flow, scatter into g_flows.
+// Eight lanes per event, one per (direction d, corner q): the event / flow loads are shared
+// (same addresses), each lane gathers its corner's four image gradients, the corners are summed by
+// lane exchange before the (flow_scaling, dt) factor of their direction, the directions after it,
+// and lane 0 of the group adds to g_flows.  (One thread per event left ~5 waves per CU with a
+// chain of 2 x 16 dependent-address gathers each: latency-bound.)
+constexpr int kBwdLanes = 8;
+
 __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
                                                       float* g_flows) {
     const int64_t HWp = (int64_t)a.H * a.W;
     const int64_t n = (int64_t)a.B * a.M;
     const int64_t img = (int64_t)a.B * HWp;
-    // XCD-ordered blocks: a sample's events (and so its image gathers) on one XCD's L2
-    for (int64_t e = (int64_t)xcd_block() * NT + threadIdx.x; e < n; e += (int64_t)gridDim.x * NT) {
+    const int sub = threadIdx.x & (kBwdLanes - 1), d = sub >> 2, q = sub & 3;
+    // XCD-ordered blocks: a sample's events (and so its image gathers) on one XCD's L2; an event's
+    // eight lanes are consecutive lanes of one wave and leave the loop together
+    for (int64_t t = (int64_t)xcd_block() * NT + threadIdx.x; t < n * kBwdLanes; t += (int64_t)gridDim.x * NT) {
+        const int64_t e = t / kBwdLanes;
         const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
         const EventRef r = event_ref(a, b, i);
         const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
@@ -393,34 +403,39 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
         const float* fl = flow_of(a, b, kf);
         const float fy = fl[HWp + pix], fx = fl[pix];
         const float pm0 = r.pol[0], pm1 = r.pol[1];
-        float gfy = 0.0f, gfx = 0.0f;
+        const float tref = d == 0 ? (float)a.T : 0.0f;
+        const float tsw = d == 0 ? ts : (float)a.T - ts;
+        Corner c[4];
+        float wy, wx;
+        warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+        Corner cq = c[0];
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            const float tref = d == 0 ? (float)a.T : 0.0f;
-            const float tsw = d == 0 ? ts : (float)a.T - ts;
-            Corner c[4];
-            float wy, wx;
-            warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+        for (int k = 1; k < 4; ++k)
+            if (q == k) cq = c[k];
+        float gwy = 0.0f, gwx = 0.0f;
+        if (cq.inb) {
             const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
-            float gwy = 0.0f, gwx = 0.0f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (!c[q].inb) continue;
-                const int id = c[q].idx;
-                const float gwt = (gb[id] * pm0 + gb[img + id] * pm1) +
-                                  (gb[2 * img + id] * (tsw * pm0) + gb[3 * img + id] * (tsw * pm1));
-                // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
-                const float gay = gwt * c[q].ax, gax = gwt * c[q].ay;
-                gwy += -(gay * relu_tie(1.0f - fabsf(c[q].dy))) * sgnf(c[q].dy);
-                gwx += -(gax * relu_tie(1.0f - fabsf(c[q].dx))) * sgnf(c[q].dx);
-            }
-            const float dt = tref - ts;
-            gfy += (gwy * a.flow_scaling) * dt;
-            gfx += (gwx * a.flow_scaling) * dt;
+            const int id = cq.idx;
+            const float gwt = (gb[id] * pm0 + gb[img + id] * pm1) +
+                              (gb[2 * img + id] * (tsw * pm0) + gb[3 * img + id] * (tsw * pm1));
+            // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
+            const float gay = gwt * cq.ax, gax = gwt * cq.ay;
+            gwy = -(gay * relu_tie(1.0f - fabsf(cq.dy))) * sgnf(cq.dy);
+            gwx = -(gax * relu_tie(1.0f - fabsf(cq.dx))) * sgnf(cq.dx);
         }
-        float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
-        if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
-        if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
+        gwy += __shfl_xor(gwy, 1, 64);
+        gwx += __shfl_xor(gwx, 1, 64);
+        gwy += __shfl_xor(gwy, 2, 64);
+        gwx += __shfl_xor(gwx, 2, 64);
+        const float dt = tref - ts;
+        float gfy = (gwy * a.flow_scaling) * dt, gfx = (gwx * a.flow_scaling) * dt;
+        gfy += __shfl_xor(gfy, 4, 64);
+        gfx += __shfl_xor(gfx, 4, 64);
+        if (sub == 0) {
+            float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+            if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
+            if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
+        }
     }
 }
 
@@ -559,7 +574,7 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
                        chunks, tsplit);
     if (a->M > 0)
-        hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M, NT, 65536)), dim3(NT), 0, s, *a, gimg,
+        hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s, *a, gimg,
                            g_flows);
     SNN_CHECK_LAUNCH();
     return 0;
