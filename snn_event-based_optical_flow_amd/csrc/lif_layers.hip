@@ -2611,6 +2611,33 @@ int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream) {
 // merged variants would spill registers there).
 static bool slot_c(int c) { return c == 8 || c == 16 || c == 32; }
 
+// Block order of a wavefront launch at C = 16 / 32: the blocks are dispatched in index order, so
+// the tasks whose blocks live longest (recurrent convs, then the other LIF-fed convs, then heads)
+// take the first ranges and the short ones fill the last round (the top task is always last).
+// Measured (profiles/r02/ab_slot_order.txt): C = 32 6.50 -> 6.435 ms; at C = 8 the same order is
+// slower (fwd slot 20.9 -> 21.8 us), which keeps the layer order.
+#ifndef SNNFLOW_SLOT_ORDER
+#define SNNFLOW_SLOT_ORDER 1
+#endif
+static int slot_rank(int kind) {
+    switch (kind) {
+        case SK_LIF_REC: case SK_PLAIN_REC: return 0;
+        case SK_LIF: case SK_PLAIN: return 1;
+        default: return 2;
+    }
+}
+
+extern "C++" template <typename A>
+static void slot_sort(A* args, int* kind, int* nblk, int n) {
+    if (!SNNFLOW_SLOT_ORDER) return;
+    for (int i = 1; i < n; ++i)  // stable insertion sort by rank
+        for (int j = i; j > 0 && slot_rank(kind[j]) < slot_rank(kind[j - 1]); --j) {
+            const A ta = args[j]; args[j] = args[j - 1]; args[j - 1] = ta;
+            const int tk = kind[j]; kind[j] = kind[j - 1]; kind[j - 1] = tk;
+            const int tn = nblk[j]; nblk[j] = nblk[j - 1]; nblk[j - 1] = tn;
+        }
+}
+
 // Blocks of the top (LIF [+ pred]) task: C = 8 one pixel per thread; C >= 16 the quad layout
 // (lif_*_q_body), sized like a conv task so its blocks last about as long as theirs.
 static int slot_top_blocks(int c, int B, int H, int W) {
@@ -2673,6 +2700,7 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         p.kind[nconv] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
         p.nblk[nconv] = slot_top_blocks(c, B, H, W);
     }
+    if (c != 8) slot_sort(p.conv, p.kind, p.nblk, nconv);
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
@@ -2727,6 +2755,7 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         p.kind[nlayer] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
         p.nblk[nlayer] = slot_top_blocks(c, B, H, W);
     }
+    if (c != 8) slot_sort(p.layer, p.kind, p.nblk, nlayer);
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
