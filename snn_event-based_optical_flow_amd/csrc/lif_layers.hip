@@ -2627,11 +2627,15 @@ static int slot_rank(int kind) {
     }
 }
 
+#ifndef SNNFLOW_SLOT_ORDER8
+#define SNNFLOW_SLOT_ORDER8 0  // C = 8: 0 layer order, 1 longest first, 2 shortest first (A/B only)
+#endif
 extern "C++" template <typename A>
-static void slot_sort(A* args, int* kind, int* nblk, int n) {
+static void slot_sort(A* args, int* kind, int* nblk, int n, bool reverse = false) {
     if (!SNNFLOW_SLOT_ORDER) return;
+    const int sg = reverse ? -1 : 1;
     for (int i = 1; i < n; ++i)  // stable insertion sort by rank
-        for (int j = i; j > 0 && slot_rank(kind[j]) < slot_rank(kind[j - 1]); --j) {
+        for (int j = i; j > 0 && sg * slot_rank(kind[j]) < sg * slot_rank(kind[j - 1]); --j) {
             const A ta = args[j]; args[j] = args[j - 1]; args[j - 1] = ta;
             const int tk = kind[j]; kind[j] = kind[j - 1]; kind[j - 1] = tk;
             const int tn = nblk[j]; nblk[j] = nblk[j - 1]; nblk[j - 1] = tn;
@@ -2701,6 +2705,7 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         p.nblk[nconv] = slot_top_blocks(c, B, H, W);
     }
     if (c != 8) slot_sort(p.conv, p.kind, p.nblk, nconv);
+    else if (SNNFLOW_SLOT_ORDER8) slot_sort(p.conv, p.kind, p.nblk, nconv, SNNFLOW_SLOT_ORDER8 == 2);
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
@@ -2756,6 +2761,7 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         p.nblk[nlayer] = slot_top_blocks(c, B, H, W);
     }
     if (c != 8) slot_sort(p.layer, p.kind, p.nblk, nlayer);
+    else if (SNNFLOW_SLOT_ORDER8) slot_sort(p.layer, p.kind, p.nblk, nlayer, SNNFLOW_SLOT_ORDER8 == 2);
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
