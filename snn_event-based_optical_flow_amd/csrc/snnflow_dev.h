@@ -164,13 +164,30 @@ __device__ inline int64_t halo_idx4(int e, const Tile& tl, int H, int W) {
     return (((int64_t)tl.b * H + h) * W + w) * Q + q;
 }
 
-template <int CH, int NTH = NT>
+// BASE: the halo's origin (pixel (h0 - 1, w0 - 1) of image b) is block-uniform, so its 64-bit offset
+// is scalar math once per call and each element adds a 32-bit (row, column, quad) offset to it
+// (measured: forward slot 20.8 -> 20.5 us, backward slot 24.4 -> 25.0 us, hence per call site).
+template <int CH, int NTH = NT, bool BASE = false>
 __device__ inline void halo_load(const float* __restrict__ src, const Tile& tl, int H, int W,
                                  float4 (&r)[Halo4<CH, NTH>::R]) {
+    if constexpr (BASE) {
+        constexpr int Q = CH / 4;
+        const float4* base = reinterpret_cast<const float4*>(src) +
+                             (((int64_t)tl.b * H + (tl.h0 - 1)) * W + (tl.w0 - 1)) * Q;
 #pragma unroll
-    for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
-        const int64_t k = halo_idx4<CH>(threadIdx.x + i * NTH, tl, H, W);
-        r[i] = (k >= 0) ? reinterpret_cast<const float4*>(src)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
+            const int e = threadIdx.x + i * NTH;
+            const int p = e / Q, q = e - p * Q;
+            const int rr = p / HWD, cc = p - rr * HWD;
+            const bool ok = e < Halo4<CH, NTH>::E && in_image(tl.h0 + rr - 1, tl.w0 + cc - 1, H, W);
+            r[i] = ok ? base[(rr * W + cc) * Q + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
+            const int64_t k = halo_idx4<CH>(threadIdx.x + i * NTH, tl, H, W);
+            r[i] = (k >= 0) ? reinterpret_cast<const float4*>(src)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
 }
 
