@@ -5,8 +5,9 @@ T=10 forwards of LIFFireNet on 1000-event windows, EventWarping loss, backward,
 SUM all-reduce of gradients across ranks (data parallel, weak scaling), clip_grad_norm_
 (1.0), Adam (lr 2e-4), truncated-BPTT state detach, loss reset.  Synthetic seeded
 event windows resident in HBM (configs/train_SNN.yml shapes: 128x128, batch 8 per
-GPU, base_num_channels 8).  The whole step is captured once into a HIP graph
-(torch.cuda.graph) and replayed; every kernel on the path is in libsnnflow.so.
+GPU, base_num_channels 8).  The whole step is captured into a HIP graph (torch.cuda.graph),
+one graph per resident batch of the pool, each reading its batch in place, and the graphs are
+replayed in turn; every kernel on the path is in libsnnflow.so.
 
     python bench.py [--gpus N --steps K --warmup W --channels C --res R --batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU, RCCL)
@@ -143,10 +144,12 @@ def main():
     # synthetic data, resident in HBM; per-rank stream seeded by (seed, rank)
     gen = torch.Generator(device=dev).manual_seed(dp.stream_seed(1, rank))
     pool = [_pack([make_window(B, N, R, R, gen, dev) for _ in range(T)]) for _ in range(args.pool)]
-    static_flat, static = _pack_like(pool[0])
+    static_flat, static_views = _pack_like(pool[0])
+    cur = {"views": static_views}  # the windows fwd_bwd reads (graph capture: one resident batch each)
 
-    def load_batch(i):  # one device copy of the next resident batch into the graph's input buffer
+    def load_batch(i):  # eager steps: one device copy of the next resident batch into the input buffer
         static_flat.copy_(pool[i % len(pool)][0], non_blocking=True)
+        cur["views"] = static_views
 
     # persistent state buffers: detach_states() == copy into them (the reference clones)
     state_bufs = None
@@ -164,6 +167,7 @@ def main():
             model._states = st
 
     def fwd_bwd():
+        static = cur["views"]
         loss_fn.reset()
         if unet:  # the reference loop: one forward per window (train_flow.py:232), 4 flow maps each
             outs = [model(w["event_voxel"], w["event_cnt"]) for w in static]
@@ -221,35 +225,45 @@ def main():
     torch.cuda.current_stream(dev).wait_stream(s_side)
     torch.cuda.synchronize(dev)
 
+    # HIP graphs.  N = 1: one graph per resident batch of the pool (forward, backward, clip, Adam,
+    # state hand-over), each reading its batch in place: no per-step input copy.  Every capture starts
+    # from set_to_none gradients, so each graph owns its gradient buffer and everything that reads it
+    # (clip, Adam) is inside the same graph.  N > 1: one forward + backward graph over a fixed input
+    # buffer (refilled by load_batch), the eager all-reduce, then the update graph.
     graphs = []
+    g_upd = None
+    multi = world == 1
     if not args.no_graph:
-        opt.zero_grad(set_to_none=True)
-        g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
-            fwd_bwd()
-            if world == 1:
+        for j in range(len(pool) if multi else 1):
+            opt.zero_grad(set_to_none=True)
+            cur["views"] = pool[j][1] if multi else static_views
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                fwd_bwd()
+                if multi:
+                    update()
+            graphs.append(g)
+        if not multi:
+            g_upd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_upd, pool=graphs[0].pool()):
                 update()
-        graphs.append(g1)
-        if world > 1:
-            g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, pool=g1.pool()):
-                update()
-            graphs.append(g2)
 
     def step(i):
-        load_batch(i)
-        if graphs:
-            graphs[0].replay()
-            if world > 1:
-                sync_grads()
-                graphs[1].replay()
-        else:
+        if not graphs:
+            load_batch(i)
             step_eager()
+        elif multi:
+            graphs[i % len(graphs)].replay()
+        else:
+            load_batch(i)
+            graphs[0].replay()
+            sync_grads()
+            g_upd.replay()
 
     for i in range(2):  # graph warm replays
         step(i)
     if args.dp_check:
-        _dp_check(world, rank, step_parts=(load_batch, graphs, fwd_bwd, sync_grads, update, opt), params=params)
+        _dp_check(world, rank, step_parts=(load_batch, graphs, g_upd, fwd_bwd, sync_grads, update, opt), params=params)
         dist.destroy_process_group()
         return
     if world > 1:
@@ -322,7 +336,7 @@ def _dp_check(world, rank, step_parts, params):
     graph 2: clip + Adam + state hand-over), checked: the all-reduced flat gradient equals the
     SUM of every rank's own gradient (gathered through the host), and after the update every
     rank holds the same parameters.  Rank 0 prints one JSON line."""
-    load_batch, graphs, fwd_bwd, sync_grads, update, opt = step_parts
+    load_batch, graphs, g_upd, fwd_bwd, sync_grads, update, opt = step_parts
     load_batch(1)
     if graphs:
         graphs[0].replay()
@@ -345,7 +359,7 @@ def _dp_check(world, rank, step_parts, params):
     err = float((reduced.double() - want).abs().max() / max(float(want.abs().max()), 1e-30))
     distinct = float(max((t - locals_[0]).abs().max() for t in locals_[1:]))
     if graphs:
-        graphs[1].replay()
+        g_upd.replay()
     else:
         update()
     torch.cuda.synchronize()

@@ -388,13 +388,13 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     }
     float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
     if constexpr (PF_REC) {
-        if (has_rec) halo_load<C, NTB, true>(a.s_prev, tl, H, W, rs);
+        if (has_rec) halo_load<C, NTB, (C <= 8)>(a.s_prev, tl, H, W, rs);
     }
     if constexpr (LIF_IN) {
         constexpr int R = Halo4<CIN, NTB>::R, Q = CIN / 4;
         float4 ry[R], rm[R];
-        halo_load<CIN, NTB, true>(a.prev_y, tl, H, W, ry);
-        if (a.prev_mem) halo_load<CIN, NTB, true>(a.prev_mem, tl, H, W, rm);
+        halo_load<CIN, NTB, (CIN <= 8)>(a.prev_y, tl, H, W, ry);
+        if (a.prev_mem) halo_load<CIN, NTB, (CIN <= 8)>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
         __shared__ double sums[2 * CIN];
         if (a.prev.bn_train) acc_gather_reduce<2 * CIN>(gat, sums);

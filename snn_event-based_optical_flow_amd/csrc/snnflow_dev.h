@@ -166,7 +166,8 @@ __device__ inline int64_t halo_idx4(int e, const Tile& tl, int H, int W) {
 
 // BASE: the halo's origin (pixel (h0 - 1, w0 - 1) of image b) is block-uniform, so its 64-bit offset
 // is scalar math once per call and each element adds a 32-bit (row, column, quad) offset to it
-// (measured: forward slot 20.8 -> 20.5 us, backward slot 24.4 -> 25.0 us, hence per call site).
+// (measured at C = 8: forward slot 20.8 -> 20.5 us, backward slot 24.4 -> 25.0 us; at C = 32 the
+// forward slot 87 -> 110 us: used for the C = 8 forward halos only).
 template <int CH, int NTH = NT, bool BASE = false>
 __device__ inline void halo_load(const float* __restrict__ src, const Tile& tl, int H, int W,
                                  float4 (&r)[Halo4<CH, NTH>::R]) {
