@@ -51,7 +51,9 @@ def parse():
                    help="T model() calls (FireNetStep) instead of model.forward_sequence (wavefront launches)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--pool", type=int, default=3, help="distinct synthetic batches cycled in HBM")
-    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsals)")
+    p.add_argument("--dist-backend", default=None,
+                   help="nccl (= RCCL; the default when a GPU is present) or gloo (rehearsals, CPU, "
+                        "SNNFLOW_SHARE_GPU=1)")
     p.add_argument("--dp-check", action="store_true",
                    help="N>1 correctness check of this very step path (gloo rehearsal): the all-reduced "
                         "gradient == the sum of the ranks' own gradients, parameters identical after the update")
@@ -111,17 +113,58 @@ def classify(name, rec_layers):
     return name
 
 
+def resolve_backend(requested, n_devices, share_gpu):
+    """The process-group backend: an explicit --dist-backend wins; ranks sharing one GPU
+    (SNNFLOW_SHARE_GPU=1 rehearsals) need gloo; otherwise RCCL ("nccl") whenever a GPU is
+    visible, gloo on a CPU-only host."""
+    if requested:
+        return requested
+    if share_gpu:
+        return "gloo"
+    return "nccl" if n_devices > 0 else "gloo"
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, n):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): start N
+    fresh rank processes through torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) and
+    pass their output through.  This parent never touches the GPU (torch.cuda.device_count() does
+    not initialise it on this image) and never re-execs itself: the ranks are children, and the
+    parent exits with their exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the launched world size",
+              file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("SNNFLOW_SHARE_GPU") == "1":  # rehearsal: several ranks on one device (gloo)
+    share = os.environ.get("SNNFLOW_SHARE_GPU") == "1"
+    if share:  # rehearsal: several ranks on one device (gloo)
         local = local % torch.cuda.device_count()
+    backend = None
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group(args.dist_backend, init_method="env://")
+        backend = resolve_backend(args.dist_backend, torch.cuda.device_count(), share)
+        dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
 
     import snnflow
@@ -321,7 +364,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
             "config": {"workload": f"{args.model} train step: T={T} x {N}-event windows, {R}x{R}, "
                                    f"batch {B}/GPU, base_num_channels {args.channels}, EventWarping + Adam",
-                       "global_batch": B * world, "parallelism": f"dp{world}",
+                       "global_batch": B * world, "parallelism": f"dp{world}", "collective": backend,
                        "hip_graph": not args.no_graph,
                        "launch_order": "per-step" if (args.per_step or unet) else "wavefront"},
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
@@ -368,7 +411,7 @@ def _dp_check(world, rank, step_parts, params):
     dist.all_gather(ps, pflat)
     pdiff = float(max((t - ps[0]).abs().max() for t in ps[1:]))
     if rank == 0:
-        print(json.dumps({"dp_check": {"world": world, "grad_numel": local.numel(), "allreduce_rel_err": err,
+        print(json.dumps({"dp_check": {"world": world, "backend": dist.get_backend(), "grad_numel": local.numel(), "allreduce_rel_err": err,
                                        "ranks_local_grads_differ_by": distinct, "param_max_diff_after_update": pdiff}}),
               flush=True)
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 21
+#define SNNFLOW_ABI_VERSION 22
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -453,10 +453,13 @@ int snnflow_lif_export(const float* x, const float* mem, const float* beta, cons
  * SNNtorch_spiking_submodules.py:171, hard_reset=False): v = beta*m + I - r*theta with the reset
  * r = H(m - theta) detached, so theta also receives -sum r * dL/dv through v; the fused LIF
  * backward kernels form the zero-reset part -sum dL/dv.  Adds -sum_px [mem - thr > 0] * g_cur
- * per channel to g_theta[c] (g_cur = dL/dv and mem = the incoming membrane, NHWC [npix][c];
- * float atomics).  c = 4, 8, 16 or 32. */
+ * per channel to g_theta[c] (g_cur = dL/dv and mem = the incoming membrane, NHWC [npix][c]).
+ * Deterministic: per-block channel totals go to scratch (SNNFLOW_THETA_SCRATCH floats) and one
+ * block sums them in block order (fp64).  c = 4, 8, 16 or 32. */
+#define SNNFLOW_THETA_BLOCKS 1024
+#define SNNFLOW_THETA_SCRATCH (SNNFLOW_THETA_BLOCKS * 32)
 int snnflow_lif_theta_subtract(const float* g_cur, const float* mem, const float* thr, int64_t npix, int c,
-                               float* g_theta, void* stream);
+                               float* g_theta, float* scratch, void* stream);
 
 /* clip_grad_norm_ (train_flow.py:265-266) over one flat gradient buffer of n floats, in place:
  * total = ||g||_2, g *= min(max_norm / (total + eps), 1); total_out (device, may be NULL). */
@@ -749,7 +752,8 @@ int snnflow_bn_bwd(const snnflow_bn_bwd_args* a, void* stream);
 int snnflow_bn_scratch_doubles(int C);
 
 /* ConvLayer with a 1x1 kernel (models/submodules.py:16-113; LIFFireNet's pred, model.py:105-107,
- * called as a module): out [B][cout][H][W] = act(W x + b), x of any strides (elements, b c h w).
+ * the U-Net's multires preds, unet.py:255-262, cin up to 8 x base channels; called as a module):
+ * out [B][cout][H][W] = act(W x + b), x of any strides (elements, b c h w).
  * Backward: g_pre = g_out * act'(out) (from the output), g_x (if set, strides gxs) = W^T g_pre,
  * g_w [cout][cin] / g_b [cout] (either NULL to skip) as fixed-order fp64 sums;
  * scratch: SNNFLOW_BN_PARTS * cout * (cin + 1) doubles. */
@@ -757,7 +761,7 @@ int snnflow_bn_scratch_doubles(int C);
 #define SNNFLOW_ACT_TANH 1
 #define SNNFLOW_ACT_RELU 2
 #define SNNFLOW_ACT_SIGMOID 3
-#define SNNFLOW_PW_MAX_CIN 63
+#define SNNFLOW_PW_MAX_CIN 256
 #define SNNFLOW_PW_MAX_COUT 4
 typedef struct {
     int B, H, W, cin, cout, act;

@@ -1049,12 +1049,13 @@ __global__ __launch_bounds__(NT) void k_lif_bwd_q(snnflow_lif_bwd_args a) {
 
 // Subtract-reset threshold gradient (include/snnflow.h snnflow_lif_theta_subtract): thread per
 // float4 of the NHWC tensors, grid-stride (the channel quad of a thread is fixed), per-block
-// channel totals through LDS, one float atomic per channel and block.
+// channel totals through LDS into part[block][C]; k_lif_theta_reduce then sums the blocks' totals
+// in block order (fp64) -- no atomics, so the gradient is the same on every run.
 template <int C>
 __global__ __launch_bounds__(NT) void k_lif_theta_subtract(const float* __restrict__ g_cur, const float* __restrict__ mem,
-                                                        const float* __restrict__ thr, int64_t npix, float* g_theta) {
+                                                        const float* __restrict__ thr, int64_t npix, float* part) {
     constexpr int Q = C / 4;
-    __shared__ float4 part[NT];
+    __shared__ float4 lds[NT];
     const int tid = threadIdx.x, q = tid % Q;
     const float t0 = thr[4 * q], t1 = thr[4 * q + 1], t2 = thr[4 * q + 2], t3 = thr[4 * q + 3];
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1067,17 +1068,26 @@ __global__ __launch_bounds__(NT) void k_lif_theta_subtract(const float* __restri
         acc.z += (m.z - t2 > 0.0f) ? g.z : 0.0f;
         acc.w += (m.w - t3 > 0.0f) ? g.w : 0.0f;
     }
-    part[tid] = acc;
+    lds[tid] = acc;
     __syncthreads();
     if (tid < C) {
         const int qq = tid / 4, j = tid & 3;
         float s = 0.0f;
         for (int k = qq; k < NT; k += Q) {
-            const float4 v = part[k];
+            const float4 v = lds[k];
             s += j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
         }
-        atomicAdd(g_theta + tid, -s);
+        part[(int64_t)blockIdx.x * C + tid] = s;
     }
+}
+
+__global__ __launch_bounds__(64) void k_lif_theta_reduce(const float* __restrict__ part, int nblk, int c,
+                                                      float* g_theta) {
+    const int ch = threadIdx.x;
+    if (ch >= c) return;
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += (double)part[(int64_t)b * c + ch];
+    g_theta[ch] -= (float)s;
 }
 
 // BatchNorm backward of one float4 of channels (torch batch_norm_cpu_backward, train):
@@ -2564,20 +2574,23 @@ int snnflow_lif_bwd(const snnflow_lif_bwd_args* a, void* stream) {
 }
 
 int snnflow_lif_theta_subtract(const float* g_cur, const float* mem, const float* thr, int64_t npix, int c,
-                               float* g_theta, void* stream) {
-    if (!g_cur || !mem || !thr || !g_theta || npix <= 0) SNN_FAIL(SNNFLOW_E_ARG, "lif_theta_subtract: bad args");
+                               float* g_theta, float* scratch, void* stream) {
+    if (!g_cur || !mem || !thr || !g_theta || !scratch || npix <= 0)
+        SNN_FAIL(SNNFLOW_E_ARG, "lif_theta_subtract: bad args");
     const int64_t n4 = npix * (c / 4);
     int64_t g = (n4 + NT - 1) / NT;
-    if (g > 1024) g = 1024;
+    if (g > SNNFLOW_THETA_BLOCKS) g = SNNFLOW_THETA_BLOCKS;
     const dim3 grid((unsigned)g), block(NT);
     const hipStream_t s = (hipStream_t)stream;
     switch (c) {
-        case 4: hipLaunchKernelGGL(k_lif_theta_subtract<4>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
-        case 8: hipLaunchKernelGGL(k_lif_theta_subtract<8>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
-        case 16: hipLaunchKernelGGL(k_lif_theta_subtract<16>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
-        case 32: hipLaunchKernelGGL(k_lif_theta_subtract<32>, grid, block, 0, s, g_cur, mem, thr, npix, g_theta); break;
+        case 4: hipLaunchKernelGGL(k_lif_theta_subtract<4>, grid, block, 0, s, g_cur, mem, thr, npix, scratch); break;
+        case 8: hipLaunchKernelGGL(k_lif_theta_subtract<8>, grid, block, 0, s, g_cur, mem, thr, npix, scratch); break;
+        case 16: hipLaunchKernelGGL(k_lif_theta_subtract<16>, grid, block, 0, s, g_cur, mem, thr, npix, scratch); break;
+        case 32: hipLaunchKernelGGL(k_lif_theta_subtract<32>, grid, block, 0, s, g_cur, mem, thr, npix, scratch); break;
         default: SNN_FAIL(SNNFLOW_E_CHANNELS, "lif_theta_subtract: c must be 4, 8, 16 or 32");
     }
+    SNN_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_lif_theta_reduce, dim3(1), dim3(64), 0, s, scratch, (int)g, c, g_theta);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -201,7 +201,10 @@ __global__ __launch_bounds__(BN_NT) void k_pw_bwd(snnflow_pointwise_args a, cons
     const int64_t HW = (int64_t)a.H * a.W, P = (int64_t)a.B * HW;
     const int nk = a.cout * (a.cin + 1);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    double tot[4] = {0.0, 0.0, 0.0, 0.0};  // this thread's share of the block's nk sums (k = lane + 64 j)
+    constexpr int NJ = (SNNFLOW_PW_MAX_COUT * (SNNFLOW_PW_MAX_CIN + 1) + 63) / 64;
+    double tot[NJ];  // this thread's share of the block's nk sums (k = lane + 64 j)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) tot[j] = 0.0;
     for (int64_t base = (int64_t)blockIdx.x * BN_NT; base < P; base += (int64_t)gridDim.x * BN_NT) {
         const int64_t p = base + threadIdx.x;
         float gp[SNNFLOW_PW_MAX_COUT];
@@ -250,7 +253,8 @@ __global__ __launch_bounds__(BN_NT) void k_pw_bwd(snnflow_pointwise_args a, cons
             if (lane == 0) red[wv][k] = v;
         }
         __syncthreads();
-        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
             const int k = lane + 64 * j;
             if (wv == 0 && k < nk) {
                 double s = 0.0;
@@ -261,7 +265,8 @@ __global__ __launch_bounds__(BN_NT) void k_pw_bwd(snnflow_pointwise_args a, cons
         __syncthreads();
     }
     if (wv == 0)
-        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
             const int k = lane + 64 * j;
             if (k < nk) part[(int64_t)blockIdx.x * nk + k] = tot[j];
         }

@@ -18,7 +18,8 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 21
+ABI_VERSION = 22
+THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
 class Neuron(ctypes.Structure):
@@ -228,7 +229,7 @@ class FireNetWgradStep(ctypes.Structure):
 
 BN_PARTS = 256
 ACT = {None: 0, "tanh": 1, "relu": 2, "sigmoid": 3}
-PW_MAX_CIN, PW_MAX_COUT = 63, 4
+PW_MAX_CIN, PW_MAX_COUT = 256, 4
 
 
 class BnFwdArgs(ctypes.Structure):
@@ -276,7 +277,7 @@ EXPORTS = {
     "snnflow_iwe_corners_bwd": (I32, [P, P, I32, I32, F32, I32, I32, F32, P, P, P]),
     "snnflow_iwe_interpolate_bwd": (I32, [P, P, I64, I32, I32, I32, I32, P, P, P]),
     "snnflow_lif_export": (I32, [P, P, P, P, I32, I32, I32, P, P, P]),
-    "snnflow_lif_theta_subtract": (I32, [P, P, P, I64, I32, P, P]),
+    "snnflow_lif_theta_subtract": (I32, [P, P, P, I64, I32, P, P, P]),
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
     "snnflow_clip_grad_norm_large": (I32, [P, I64, F32, F32, P, P, P]),
     "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),

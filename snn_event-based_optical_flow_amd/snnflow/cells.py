@@ -201,6 +201,12 @@ class ConvLayer(nn.Module):
         self.activation = getattr(torch, activation) if activation is not None else None
         self.activation_name = activation
         self.norm = norm
+        # the reference builds the norm layer (state-dict keys) but its forward never applies it:
+        # the normalisation block is commented out (submodules.py:98-102)
+        if norm == "BN":
+            self.norm_layer = nn.BatchNorm2d(out_channels, momentum=BN_momentum)
+        elif norm == "IN":
+            self.norm_layer = nn.InstanceNorm2d(out_channels, track_running_stats=True)
 
     def forward(self, x):
         if self.conv2d.kernel_size != (1, 1) or self.conv2d.stride != (1, 1):

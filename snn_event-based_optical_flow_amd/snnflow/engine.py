@@ -191,7 +191,8 @@ class FireNetEngine:
         self.lifs = [c.lif for c in self.cells]
         self.bns = [getattr(c, "batch_norm", c.bn) for c in self.cells]
         self._plist = None     # cached param_list() (+ identity checks), see param_list
-        self._neurons = None   # cached neuron structs keyed by the BatchNorms' train flags
+        self._neurons = None   # cached neuron structs, re-validated per call (neurons())
+        self._gen = 0          # bumped whenever the neuron structs are rebuilt or invalidate() runs
 
     def __deepcopy__(self, memo):  # (copy.deepcopy(model)): ctypes caches are rebuilt, not copied
         import copy
@@ -204,17 +205,34 @@ class FireNetEngine:
         return new
 
     def invalidate(self):
-        """Drop cached parameter lists / neuron structs (the model's _apply moved or replaced tensors)."""
+        """Drop cached parameter lists / neuron structs / step-driver plans (the model's _apply moved
+        or replaced tensors)."""
         self._plist = None
         self._neurons = None
         self._prep_ws = None
+        self._prep_map = None
+        self._plan = None
+        self._gen = self.__dict__.get("_gen", 0) + 1
+
+    def _neuron_key(self):
+        """Everything neuron_struct reads, per cell: the tensors themselves (held by the cache, so a
+        replaced tensor can never alias a freed one's identity) and the scalar options."""
+        key = []
+        for c, bn, lif in zip(self.cells, self.bns, self.lifs):
+            key += (bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                    lif.beta, lif.threshold, bn.training, bn.track_running_stats, bn.momentum, bn.eps,
+                    c.hard_reset)
+        return key
 
     def neurons(self):
-        """neuron_struct of every cell, cached: the pointers only change when the model's tensors are
-        moved or replaced (_apply -> invalidate, or a Parameter re-assignment, caught by param_list)."""
-        key = tuple(bn.training for bn in self.bns)
-        if self._neurons is None or self._neurons[0] != key:
+        """neuron_struct of every cell, cached and re-validated on every call against the tensors and
+        options it was built from (identity for tensors, equality for scalars).  A rebuild bumps the
+        engine generation, which keys the C step driver's plan (it holds copies of the structs)."""
+        key = self._neuron_key()
+        n = self._neurons
+        if n is None or not all(a is b if isinstance(a, torch.Tensor) else a == b for a, b in zip(n[0], key)):
             self._neurons = (key, [neuron_struct(c) for c in self.cells])
+            self._gen = self.__dict__.get("_gen", 0) + 1
         return self._neurons[1]
 
     def sequence_ok(self, cin0):
@@ -405,7 +423,7 @@ class FireNetEngine:
         """The C step driver's constant arguments (snnflow_firenet_plan), cached per model state."""
         neurons = self.neurons()
         train = tuple(bn.training or not bn.track_running_stats for bn in self.bns)
-        key = (B, H, W, cin0, id(ws), ws.fwd_acc.data_ptr(), self.prep.gen, id(neurons), train,
+        key = (B, H, W, cin0, id(ws), ws.fwd_acc.data_ptr(), self.prep.gen, self._gen, train,
                self.pred.weight.data_ptr(), self.pred.bias.data_ptr())
         pl = self.__dict__.get("_plan")
         if pl is not None and pl[0] == key:
@@ -494,8 +512,10 @@ def theta_subtract(cell, g_cur, mem, npix, g_theta, stream):
     pointers (NHWC); no-op for zero-reset cells or a step without an incoming membrane."""
     if cell.lif.reset_mechanism != "subtract" or mem is None:
         return
+    dev = cell.lif.threshold.device
+    scratch = torch.empty(_lib.THETA_SCRATCH, device=dev)  # stream-ordered reuse by the caching allocator
     _lib.call("lif_theta_subtract", lib.snnflow_lif_theta_subtract, _ptr_t(g_cur), _ptr_t(mem),
-              ptr(cell.lif.threshold), npix, cell.hidden_size, g_theta, stream)
+              ptr(cell.lif.threshold), npix, cell.hidden_size, g_theta, ptr(scratch), stream)
 
 
 # ---------------------------------------------------------------------------

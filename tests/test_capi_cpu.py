@@ -56,6 +56,7 @@ def test_struct_layouts_match_c(tmp_path):
         lines.append(f'printf("acc_fwd_{c_} %d\\n", SNNFLOW_ACC_LEN(2 * {c_}));')
         lines.append(f'printf("acc_bwd_{c_} %d\\n", SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC({c_})));')
     lines.append(f'printf("abi %d\\n", SNNFLOW_ABI_VERSION);')
+    lines.append(f'printf("theta_scratch %d\\n", SNNFLOW_THETA_SCRATCH);')
     lines.append("return 0;}")
     c = tmp_path / "layout.c"
     c.write_text("\n".join(lines))
@@ -67,6 +68,7 @@ def test_struct_layouts_match_c(tmp_path):
         assert int(got[f"acc_fwd_{c_}"]) == _lib.acc_storage(2 * c_)
         assert int(got[f"acc_bwd_{c_}"]) == _lib.acc_storage(_lib.bwd_acc_len(c_))
     assert int(got["abi"]) == _lib.ABI_VERSION
+    assert int(got["theta_scratch"]) == _lib.THETA_SCRATCH
     for cname, py in structs.items():
         assert int(got[f"{cname} size"]) == ctypes.sizeof(py), cname
         for fname, _ in py._fields_:

@@ -107,3 +107,51 @@ def test_clip_matches_torch(flat_layout):
     assert abs(float(n1) - float(n2)) <= 1e-5 * float(n2)
     for p, r in zip(ps, ref):
         torch.testing.assert_close(p.grad, r.grad, rtol=1e-5, atol=1e-7)
+
+
+def _bench():
+    import importlib.util
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(root, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_bench_backend_resolution():
+    """`bench.py --gpus N` without --dist-backend runs RCCL ("nccl") when a GPU is visible, gloo on a
+    CPU-only host or when ranks share one GPU (SNNFLOW_SHARE_GPU=1); an explicit choice wins."""
+    b = _bench()
+    assert b.resolve_backend(None, 8, False) == "nccl"
+    assert b.resolve_backend(None, 1, False) == "nccl"
+    assert b.resolve_backend(None, 0, False) == "gloo"
+    assert b.resolve_backend(None, 1, True) == "gloo"
+    assert b.resolve_backend("gloo", 8, False) == "gloo"
+    assert b.resolve_backend("nccl", 1, True) == "nccl"
+
+
+def test_bench_gpus_flag_spawns_ranks(monkeypatch):
+    """A plain `bench.py --gpus 2` (no WORLD_SIZE) starts its two ranks itself as children through
+    torch.distributed.run on 127.0.0.1 with the same arguments, and exits with their exit code;
+    the parent does no GPU work (the launch is intercepted here before any rank would start)."""
+    import subprocess
+    import sys as _sys
+    b = _bench()
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 7
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(_sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    with pytest.raises(SystemExit) as e:
+        b.main()
+    assert e.value.code == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "2"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"

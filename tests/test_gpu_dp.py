@@ -36,3 +36,22 @@ def test_dp_step_two_ranks_shared_gpu(extra):
     assert res["ranks_local_grads_differ_by"] > 0  # the ranks really saw different batches
     assert res["allreduce_rel_err"] < 1e-6
     assert res["param_max_diff_after_update"] == 0.0
+
+
+def test_bench_gpus_flag_launches_its_ranks():
+    """`python bench.py --gpus 2` with no launcher and no WORLD_SIZE: bench.py starts the two ranks
+    itself (children through torch.distributed.run; the ranks share the box's one GPU over gloo
+    here) and the step path runs with world == 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(SNNFLOW_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1",
+           "--no-cpu-baseline", "--dp-check", "--batch", "2", "--pool", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, r.stdout[-2000:]
+    res = json.loads(lines[-1])["dp_check"]
+    print("\n[dp-check via --gpus]", res)
+    assert res["world"] == 2
+    assert res["allreduce_rel_err"] < 1e-6
+    assert res["param_max_diff_after_update"] == 0.0

@@ -1,7 +1,7 @@
 """GPU parity at the headline configuration and measured precision bounds.
 
 * ``test_cfg2_train_step_vs_oracle``: BASELINE cfg2 (LIFFireNet, 128x128, B=8, T=10 windows of
-  1000 events, C=8) -- the north star's claim "AEE within 1e-4 of reference" -- through the
+  1000 events, C=8), cfg3 (256x256, B=4) and the C=32 width at the cfg2 shape -- the north star's claim "AEE within 1e-4 of reference" -- through the
   bench's wavefront path (``forward_sequence``) and the reference loop's per-step path, against
   the CPU oracle (oracle/lif_ref.py + oracle/iwe_ref.py, the reference's PyTorch path restated
   and pinned by the golden fixtures).  Two oracle runs on the same windows and initial weights:
@@ -168,27 +168,38 @@ def _report(tag, r, per_layer):
           + ", ".join(f"{k}={v:.1e}" for k, v in r["grad_rel"].items()))
 
 
+# (tag, batch, resolution, base_num_channels): BASELINE cfg2; cfg3 (256x256, B=4); the README /
+# default-checkpoint width C=32 at the cfg2 shape
+HEADLINE = [("cfg2", 8, 128, 8), ("cfg3", 4, 256, 8), ("cfg2-C32", 8, 128, 32)]
+
+
 @pytest.mark.parametrize("path", ["sequence", "per_step"])
-def test_cfg2_train_step_vs_oracle(dev, path):
+@pytest.mark.parametrize("tag,B,H,C", HEADLINE, ids=[h[0] for h in HEADLINE])
+def test_cfg2_train_step_vs_oracle(dev, path, tag, B, H, C):
     from snnflow.synthetic import make_window
 
-    B, H, T, N, C = 8, 128, 10, 1000, 8
+    T, N = 10, 1000
     gen = torch.Generator(device=dev).manual_seed(1)
     wins = [make_window(B, N, H, H, gen, dev) for _ in range(T)]
     cpu_wins = [{k: v.cpu() for k, v in w.items()} for w in wins]
     model, init, flows, loss, states = _gpu_run(dev, path, wins, C)
 
-    # 1. free-running oracle: the reference path's own trajectory; flips counted and reported
+    # 1. free-running oracle: the reference path's own trajectory; flips counted and reported.  At
+    #    C = 8 the trajectory stays put (asserted); at C = 32 one near-threshold flip cascades
+    #    through the recurrence (SURVEY finding 4: two fp32 CPU runs of the reference itself that
+    #    differ only in conv summation order diverge the same way), so there the flip-corrected
+    #    leg below is the assertion and the free-running figures are reported only.
     ref, rflows, rloss, flips, _ = _oracle_run(init, C, cpu_wins, states, eps=None)
-    free = _compare(f"cfg2 {path} free-running", model, flows, loss, ref, rflows, rloss, flips, cpu_wins)
+    free = _compare(f"{tag} {path} free-running", model, flows, loss, ref, rflows, rloss, flips, cpu_wins)
     rate = flips.sum() / (flips.size * B * C * H * H)
-    print(f"[cfg2 {path}] free-running flips {int(flips.sum())}, rate {rate:.2e} per spike")
-    assert rate < 1e-6, rate
+    print(f"[{tag} {path}] free-running flips {int(flips.sum())}, rate {rate:.2e} per spike")
+    if C == 8:
+        assert rate < 1e-6, rate
 
     # 2. near-threshold flips adopted (|v - theta| <= 1e-4): every other spike must agree, and
     #    then the whole train step matches at the north star's tolerances
     ref, rflows, rloss, flips, hard = _oracle_run(init, C, cpu_wins, states, eps=1e-4)
-    r = _compare(f"cfg2 {path} flip-corrected", model, flows, loss, ref, rflows, rloss, flips, cpu_wins)
+    r = _compare(f"{tag} {path} flip-corrected", model, flows, loss, ref, rflows, rloss, flips, cpu_wins)
     assert hard == 0, f"{hard} spikes differ away from the threshold"
     assert abs(r["loss"][0] - r["loss"][1]) <= 1e-5 * abs(r["loss"][1]), r["loss"]
     assert max(r["flow_rel"]) <= 1e-4 and r["flow_maxabs"] <= 1e-4, (r["flow_rel"], r["flow_maxabs"])
