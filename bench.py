@@ -532,14 +532,33 @@ def _pmc_traffic(kernel, args):
     return d.get(key, {}).get(kernel)
 
 
+_THREADS_NOTE = ("threads = min(affinity, 16): a GPU box grants each GPU a 16-CPU share (OMP_NUM_THREADS=16 "
+                 "there) while os.cpu_count() / the affinity mask show the whole machine")
+
+
+def _cpu_threads():
+    return max(1, min(len(os.sched_getaffinity(0)), 16))
+
+
+def _cpu_model():
+    """Host CPU model name (/proc/cpuinfo), recorded beside cpu_baseline.cores."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(args, windows):
     """The CPU oracle (pure-PyTorch restatement of the reference path, same op sequence)
     timed on this host: one full train step of the same workload after one warm-up
     step, then whole train steps until ~10 s of CPU work (bounded sample, >= 1 step)."""
     from oracle import iwe_ref, lif_ref
 
-    threads = len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, 16))
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     kw = lif_ref.make_unet_kwargs(base_num_channels=args.channels)
@@ -569,7 +588,8 @@ def cpu_baseline(args, windows):
             break
     dt = time.perf_counter() - t0
     ev = n * args.batch * args.T * args.events
-    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "kind": "port",
+    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "cpu_model": _cpu_model(),
+            "threads_note": _THREADS_NOTE, "kind": "port",
             "sample": f"{n} timed train steps (after 1 warm-up) of the same workload: {args.batch}x{args.T} windows "
                       f"of {args.events} events, {R}x{R}, C={args.channels}, Adam; oracle/ pure-PyTorch CPU "
                       f"restatement of the reference path, {threads} threads", "seconds": round(dt, 3)}
@@ -582,7 +602,7 @@ def cpu_baseline_unet(args, windows):
     from oracle import iwe_ref
     from oracle.unet_ref import SpikingRecEVFlowNetRef
 
-    threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(0)
     from snnflow.parser import train_snn_model_kwargs
@@ -605,7 +625,8 @@ def cpu_baseline_unet(args, windows):
     opt.step()
     dt = time.perf_counter() - t0
     ev = nw * args.events
-    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "kind": "port",
+    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "cpu_model": _cpu_model(),
+            "threads_note": _THREADS_NOTE, "kind": "port",
             "sample": f"1 train step of 1 sample x {nw} windows of {args.events} events, {R}x{R}, base {args.channels}; "
                       f"oracle/unet_ref.py (CPU restatement of the reference U-Net), {threads} threads",
             "seconds": round(dt, 3)}

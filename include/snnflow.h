@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 22
+#define SNNFLOW_ABI_VERSION 23
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -204,6 +204,18 @@ typedef struct snnflow_layer_bwd_args {
     /* ABI 15, optional: bf16 fragments of wt_fwd_ff / wt_fwd_rec (snnflow_prep_desc.frag_bwd)
      * for the input-gradient convs of the cin == c kernels at c = 16, 32 (else f32 matrix cores) */
     const uint16_t* wd_ff; const uint16_t* wd_rec;
+    /* ABI 23, optional: the layer's weight gradients fused into this backward task (lif_in = 1,
+     * c = cin = 8, wavefront launches only -- snnflow_bwd_slot; the single-task call ignores them).
+     * The task already holds G = dL/dy of its tile with the halo (BN backward applied) and
+     * recomputes layer l-1's spikes x of its tile for the LIF backward, so
+     *   dW_ff[co][ci][k] += sum_{q in tile} x[q][ci] G[q - k][co]     (= sum_p G[p][co] x[p + k][ci])
+     * and, with s_prev (NHWC [B][H][W][c] spikes of layer l at the previous step; NULL: zero state),
+     *   dW_rec[co][ci][k] += sum_{q in tile} s_prev[q][ci] G[q - k][co]
+     * go to the block's row of wslab_ff / wslab_rec ([snnflow_conv_blocks()][c*cin*9], the
+     * deferred path's slab layout): written (wslab_accumulate = 0) or added.  Rows are per tile and
+     * every (layer, step) task of a pass runs in its own launch, so the accumulation over the steps
+     * is a fixed-order read-modify-write (deterministic); snnflow_slab_reduce sums the rows. */
+    float* wslab_ff; float* wslab_rec; const float* s_prev; int wslab_accumulate;
 } snnflow_layer_bwd_args;
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
 

@@ -1119,9 +1119,166 @@ struct LayerBwdLds {
     static_assert(!BF6 || G >= NT * Pad<CIN>::v, "output staging aliases the gradient tile");
 };
 
-template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false>
+// ds_read_b64_tr_b16 pair -> one 16x16x32 bf16 operand: lane (16 g + i) receives column i of 8
+// LDS rows (rows 0..3 addressed by lanes 4q + p of its group through r0, rows 4..7 through r1, each
+// already offset by 4p columns): 8 consecutive reduction elements of channel i.
+typedef short s16x4w __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4w lds_s16x4w;
+__device__ inline bf16x8 tr8(const __bf16* r0, const __bf16* r1) {
+    const s16x4w v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4w*)(r0));
+    const s16x4w v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4w*)(r1));
+    const short __attribute__((ext_vector_type(8))) v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// Fused weight gradients of a C = 8 LIF-fed layer (snnflow_layer_bwd_args.wslab_*, wavefront
+// launches): LDS layout inside the weight-fragment regions, which are free once the input-gradient
+// convs are done.  wl_x: X = layer l-1's spikes of the tile [256][8] bf16 (1024 floats), then the
+// per-tap results R [c][cin][9] (576 floats) and the tap-8 partials of the 8 waves [8][64];
+// wl_r (recurrent cells): the same for the previous-step spikes S.
+constexpr int kWgfX = NT * 8 / 2, kWgfR = 8 * 8 * 9, kWgfP = 8 * 64;
+constexpr int kWgfFloats = kWgfX + kWgfR + kWgfP;
+
+// Stage of the fused weight gradients, between the input-gradient convs and the store of their
+// results (G, the bf16 hi/mid/lo gradient tile with its halo, is still intact):
+//   1. the old slab values (accumulate) and the previous-step spikes are loaded;
+//   2. barrier (weight fragments dead); X = this pixel's recomputed layer l-1 spikes, S = s_prev;
+//   3. barrier; wave w runs tap w over the 8 tile rows (K = 32 pixels each) and row w of tap 8:
+//      D[co][ci] += G[q - k][co] X[q][ci] as lo, mid, hi products (exact f32 products: spikes are
+//      0/1), A = G through the transposed LDS reads (rows = pixels shifted by the tap), B = X;
+//   4. results to R / the tap-8 partials (the caller's barrier completes them).
+template <bool REC>
+__device__ void fused_wgrad_old(const snnflow_layer_bwd_args& a, const Grid& g, float (&wold)[4]) {
+    const int tid = threadIdx.x;
+    const bool acc_in = a.wslab_accumulate != 0;
+    const bool has_s = REC && a.s_prev != nullptr && a.wslab_rec != nullptr;
+    if (acc_in) {
+        const float* sf = a.wslab_ff + (int64_t)g.bid * kWgfR;
+        wold[0] = sf[tid];
+        if (tid + 2 * NT < kWgfR) wold[1] = sf[tid + 2 * NT];
+        if constexpr (REC) {
+            if (has_s) {
+                const float* sr = a.wslab_rec + (int64_t)g.bid * kWgfR;
+                wold[2] = sr[tid];
+                if (tid + 2 * NT < kWgfR) wold[3] = sr[tid + 2 * NT];
+            }
+        }
+    }
+}
+
+template <bool REC>
+__device__ void fused_wgrad_stage(const snnflow_layer_bwd_args& a, const float* G, float* wl_x, float* wl_r,
+                                  const float (&xsp)[4], const float4& sp, int pt, int ci0) {
+    constexpr int C = 8, PART = HN * C;
+    const int tid = threadIdx.x;
+    const bool has_s = REC && a.s_prev != nullptr && a.wslab_rec != nullptr;
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    __bf16* X = reinterpret_cast<__bf16*>(wl_x);
+    __bf16* S = reinterpret_cast<__bf16*>(wl_r);
+    const bf16x4 xs = {(__bf16)xsp[0], (__bf16)xsp[1], (__bf16)xsp[2], (__bf16)xsp[3]};
+    __syncthreads();  // every wave is done with the staged input-gradient results: the regions are free
+    *reinterpret_cast<bf16x4*>(X + pt * C + ci0) = xs;
+    if constexpr (REC) {
+        if (has_s) *reinterpret_cast<bf16x4*>(S + pt * C + ci0) = bf16x4{(__bf16)sp.x, (__bf16)sp.y, (__bf16)sp.z, (__bf16)sp.w};
+    }
+    __syncthreads();
+
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+    const __bf16* G3 = reinterpret_cast<const __bf16*>(G);
+    const int j0 = 8 * g4 + qq;  // tile column of this lane's first pixel row (the second: + 4)
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc8 = acc, accr = acc, acc8r = acc;
+    auto kstep = [&](int tap, int row, f32x4& d, f32x4& dr) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const int hp = (row + 2 - ky) * HWD + (j0 + 2 - kx);
+        const __bf16* ga = G3 + hp * C + 4 * pp;
+        const bf16x8 ah = tr8(ga, ga + 4 * C);
+        const bf16x8 am = tr8(ga + PART, ga + PART + 4 * C);
+        const bf16x8 al = tr8(ga + 2 * PART, ga + 2 * PART + 4 * C);
+        const int q = row * TW + j0;
+        const __bf16* xb = X + q * C + 4 * pp;
+        const bf16x8 b = tr8(xb, xb + 4 * C);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, d, 0, 0, 0);
+        if constexpr (REC) {
+            if (has_s) {
+                const __bf16* sb = S + q * C + 4 * pp;
+                const bf16x8 bs = tr8(sb, sb + 4 * C);
+                dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bs, dr, 0, 0, 0);
+                dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs, dr, 0, 0, 0);
+                dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs, dr, 0, 0, 0);
+            }
+        }
+    };
+#pragma unroll 2
+    for (int row = 0; row < TH; ++row) kstep(wv, row, acc, accr);
+    kstep(8, wv, acc8, acc8r);
+    // lane: D[co = 4 g4 + j][ci = lane & 15]; co, ci < 8 are the layer's
+    const int ci = lane & 15;
+    if (ci < C && g4 < 2) {
+        float* R = wl_x + kWgfX;
+        float* P8 = R + kWgfR;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = 4 * g4 + j;
+            R[(co * C + ci) * 9 + wv] = acc[j];
+            P8[wv * 64 + co * C + ci] = acc8[j];
+        }
+        if constexpr (REC) {
+            if (has_s) {
+                float* Rr = wl_r + kWgfX;
+                float* P8r = Rr + kWgfR;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int co = 4 * g4 + j;
+                    Rr[(co * C + ci) * 9 + wv] = accr[j];
+                    P8r[wv * 64 + co * C + ci] = acc8r[j];
+                }
+            }
+        }
+    }
+}
+
+// The block's slab rows: element e of [c][cin][9] = R[e] (taps 0..7) or the tap-8 partials of the
+// 8 waves summed in wave order; written or added to the old value (fixed order over the steps).
+template <bool REC>
+__device__ void fused_wgrad_store(const snnflow_layer_bwd_args& a, const Grid& g, const float* wl_x,
+                                  const float* wl_r, const float (&wold)[4]) {
+    const int tid = threadIdx.x;
+    const bool acc_in = a.wslab_accumulate != 0;
+    const bool has_s = REC && a.s_prev != nullptr && a.wslab_rec != nullptr;
+    auto value = [&](const float* base, int e) {
+        const float* R = base + kWgfX;
+        const int tap = e % 9;
+        if (tap < 8) return R[e];
+        const float* P8 = R + kWgfR;
+        const int k = e / 9;
+        float v = P8[k];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) v += P8[w * 64 + k];
+        return v;
+    };
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int e = tid + i * 2 * NT;
+        if (e < kWgfR) {
+            a.wslab_ff[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[i] + value(wl_x, e) : value(wl_x, e);
+            if constexpr (REC) {
+                if (a.wslab_rec) {
+                    if (has_s) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[2 + i] + value(wl_r, e) : value(wl_r, e);
+                    else if (!acc_in) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = 0.0f;
+                }
+            }
+        }
+    }
+}
+
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false, bool WGF = false>
 __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, float* lds) {
     using LB = LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT, BFG>;
+    static_assert(!WGF || (LIF_IN && C == 8 && CIN == 8 && SPLIT == 2 && LB::BF6 && LB::FR >= kWgfFloats),
+                  "fused weight gradients: C = 8 LIF-fed layers with LDS weight fragments");
     constexpr int NTB = NT * SPLIT;
     constexpr int CI = CIN / SPLIT, CR = C / SPLIT;  // input / recurrent channels per thread group
     static_assert(CI * SPLIT == CIN && CR * SPLIT == C, "channel split");
@@ -1200,6 +1357,9 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     // layer l-1's inputs of the LIF backward at this thread's pixel; C = 32 loads them only after
     // the input-gradient convs (48 registers fewer across the matrix-core loop)
     constexpr bool LATE_D = C >= 32 || (C == 8 && (REC ? SNNFLOW_LATE_D_REC8 : SNNFLOW_LATE_D_FF8));
+    [[maybe_unused]] float wold[4] = {0.f, 0.f, 0.f, 0.f};  // slab rows' old values (e = tid, tid + 512)
+    [[maybe_unused]] float4 wsp = z4;                        // previous-step spikes (recurrent conv input)
+    [[maybe_unused]] const bool wgf = WGF && a.wslab_ff != nullptr;
     auto load_prev = [&]() {
         if constexpr (LIF_IN) {
             constexpr int Q4 = CIN / 4;
@@ -1216,6 +1376,9 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                 dm[q] = ld4_or_zero(pm4, py4, base + q);
                 dg[q] = ld4_or_zero(pg4 ? pg4 + plane4 : nullptr, py4, base + q);
             }
+        }
+        if constexpr (WGF && REC) {  // previous-step spikes of this pixel (recurrent conv input)
+            if (wgf && a.s_prev && a.wslab_rec && in) wsp = reinterpret_cast<const float4*>(a.s_prev)[pix * 2 + ci0 / 4];
         }
     };
     if constexpr (!LATE_D) load_prev();
@@ -1340,20 +1503,23 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         }
         if constexpr (LATE_D) load_prev();
         __syncthreads();
+        // results staged through LDS: the gradient tile G, or (fused weight gradients, which still
+        // read G) the weight-fragment regions wl_x.. (free now; the slot pool holds both of them)
+        float* const dgo = (WGF && wgf) ? wl_x : G;
         if (do_x) {
-            mfma_store<false>(ax, ax, G);
+            mfma_store<false>(ax, ax, dgo);
             __syncthreads();
-            const float* gl = G + pt * Pad<CIN>::v + ci0;
+            const float* gl = dgo + pt * Pad<CIN>::v + ci0;
 #pragma unroll
             for (int ci = 0; ci < CI; ++ci) gx[ci] = gl[ci];
         }
         if constexpr (REC) {
             if (do_r) {
                 __syncthreads();
-                mfma_store<false>(arr, arr, G);
+                mfma_store<false>(arr, arr, dgo);
                 __syncthreads();
                 if (in) {
-                    const float* rl = G + pt * PC + cr0;
+                    const float* rl = dgo + pt * PC + cr0;
                     const int64_t plane = (int64_t)a.B * H * W * C;
                     float* gsp = a.g_state_prev + pix * C + cr0;
 #pragma unroll
@@ -1392,6 +1558,10 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         float vd[NVP];
 #pragma unroll
         for (int j = 0; j < NVP; ++j) vd[j] = 0.0f;
+        [[maybe_unused]] float xsp[4] = {0.f, 0.f, 0.f, 0.f};  // layer l-1's spikes (fused weight gradients)
+        if constexpr (WGF) {
+            if (wgf) fused_wgrad_old<REC>(a, g, wold);  // in flight during the LIF backward
+        }
         if (in && !PROBE_OFF(8)) {
             const bool zr = a.prev.zero_reset != 0;
             float4* gc4 = reinterpret_cast<float4*>(a.prev_g_cur) + pix * (CIN / 4) + ci0 / 4;
@@ -1408,6 +1578,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                     const float gs = gx[cl] + gi[j];
                     const LifOut o = lif_step(yi[j], mi[j], pcoef[ci], zr);
                     const float gv = atan_sg(o.v - pcoef[ci].theta) * gs;
+                    if constexpr (WGF) xsp[cl & 3] = o.s;
                     go[j] = gv;
                     gmo[j] = mem_grad(gv, mi[j], pcoef[ci], zr);
                     vd[cl] = gv;
@@ -1426,6 +1597,14 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                 return acc + k * CIN + pp * CI + jj;
             });
         TRACE_AT(TR, TK, 5);
+        if constexpr (WGF) {
+            if (wgf) {
+                fused_wgrad_stage<REC>(a, G, wl_x, wl_r, xsp, wsp, pt, ci0);
+                __syncthreads();
+                fused_wgrad_store<REC>(a, g, wl_x, wl_r, wold);
+            }
+        }
+        TRACE_AT(TR, TK, 6);
     } else {
         if (a.g_x && a.wt_bwd_ff && in) {
             float* gb = a.g_x + (int64_t)tl.b * a.gxs_b + h * a.gxs_h + w * a.gxs_w;
@@ -2248,7 +2427,7 @@ __device__ inline void globalize(snnflow_layer_bwd_args& a) {
     SNN_G(a.prev_mem); SNN_G(a.prev_stats);
     globalize(a.prev);
     SNN_G(a.prev_g_state); SNN_G(a.prev_g_cur); SNN_G(a.prev_g_mem); SNN_G(a.acc_out); SNN_G(a.zero0);
-    SNN_G(a.zero1); SNN_G(a.wd_ff); SNN_G(a.wd_rec);
+    SNN_G(a.zero1); SNN_G(a.wd_ff); SNN_G(a.wd_rec); SNN_G(a.wslab_ff); SNN_G(a.wslab_rec); SNN_G(a.s_prev);
 }
 #undef SNN_G
 
@@ -2321,6 +2500,10 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
 #endif
 template <int C>
 __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L32_WAVES) void k_bwd_slot(BwdSlotParams) {
+    // fused weight gradients (C = 8): the input-gradient results are staged in the two weight-fragment
+    // regions, which the pool holds for every task kind
+    static_assert(C != 8 || SlotLds<C>::BWD >= LayerBwdLds<C, C, true, true, 2>::FLOATS, "fused wgrad staging");
+    static_assert(C != 8 || 2 * LayerBwdLds<C, C, true, true, 2>::FR >= NT * Pad<C>::v, "dgrad staging size");
     typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
     const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
     Grid g;
@@ -2340,8 +2523,8 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L
         BWD_LAYER(true, SK_HEAD4, 4, C, false, false, 2)
         BWD_LAYER(false, SK_PLAIN, C, C, false, false, 2)
         BWD_LAYER(false, SK_PLAIN_REC, C, C, false, true, 2)
-        BWD_LAYER(true, SK_LIF, C, C, true, false, 2, SlotLds<C>::BFG)
-        BWD_LAYER(true, SK_LIF_REC, C, C, true, true, 2, SlotLds<C>::BFG)
+        BWD_LAYER(true, SK_LIF, C, C, true, false, 2, SlotLds<C>::BFG, C == 8)
+        BWD_LAYER(true, SK_LIF_REC, C, C, true, true, 2, SlotLds<C>::BFG, C == 8)
 #undef BWD_LAYER
         case SK_TOP: {
             if constexpr (kSlotAllKinds<C>) {

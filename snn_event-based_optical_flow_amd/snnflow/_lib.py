@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 22
+ABI_VERSION = 23
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -68,7 +68,8 @@ class LayerBwdArgs(ctypes.Structure):
                 ("g_state_prev", P), ("zero_mem_half", I32),
                 ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),
                 ("prev_g_state", P), ("prev_g_cur", P), ("prev_g_mem", P), ("acc_out", P),
-                ("zero0", P), ("zero1", P), ("zero_n", I32), ("wd_ff", P), ("wd_rec", P)]
+                ("zero0", P), ("zero1", P), ("zero_n", I32), ("wd_ff", P), ("wd_rec", P),
+                ("wslab_ff", P), ("wslab_rec", P), ("s_prev", P), ("wslab_accumulate", I32)]
 
 
 MAX_WGRAD_STEPS = 32

@@ -184,6 +184,9 @@ class FireNetEngine:
         self.flat = None
         self.flat_views = None
         self.pending = []   # per-step tensors of the open backward chain (deferred wgrad)
+        self.pending_layers = []  # per pending step: the layers whose weight gradients are still deferred
+        self.slab_live = [False] * self.L      # slab rows of layer l hold partial sums of this chain
+        self.fuse_wgrad = self.C == 8          # wavefront backward computes layers >= 1's dW in place
         self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
         self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
         self.seq_states = None
@@ -348,23 +351,27 @@ class FireNetEngine:
         return m[1], m[2]
 
     def open_chain(self, device):
+        self.slab_live = [False] * self.L
         self.flat_layout = self.flat_layout_for(self.param_list())
         o, n, _ = self.flat_layout[-1]
         self.flat = torch.empty(o + n, device=device)
         self.flat_views = True  # (gradient destinations are addressed through flat_layout)
         self.bwd_open = True
 
-    def launch_wgrad(self, l, B, H, W, cin0, ws, stream):
-        """Deferred weight gradients of layer l over all pending time steps (one snnflow_wgrad
-        launch per <= 32 steps) into the layer's per-block slabs (x,
-        s_prev, y, stats saved per step)."""
-        C, rec, steps = self.C, self.rec[l], self.pending
+    def launch_wgrad(self, l, B, H, W, cin0, ws, stream, steps=None):
+        """Deferred weight gradients of layer l over the given pending time steps (default: all;
+        one snnflow_wgrad launch per <= 32 steps) into the layer's per-block slabs (SURVEY
+        Appendix D: x, s_prev, y, stats saved per step), added to what the chain's fused steps
+        already left there."""
+        C, rec = self.C, self.rec[l]
+        steps = self.pending if steps is None else steps
         for i0 in range(0, len(steps), _lib.MAX_WGRAD_STEPS):
             chunk = steps[i0:i0 + _lib.MAX_WGRAD_STEPS]
             a = _lib.WgradArgs()
             a.B, a.H, a.W, a.c = B, H, W, C
             a.cin = cin0 if l == 0 else C
-            a.nsteps, a.accumulate, a.rec = len(chunk), 1 if i0 else 0, 1 if rec else 0
+            a.nsteps, a.rec = len(chunk), 1 if rec else 0
+            a.accumulate = 1 if (i0 or self.slab_live[l]) else 0
             # layers >= 1: x and s_prev are spikes of this engine (0/1, exact in bf16)
             a.exact_inputs = 1 if l > 0 else 0
             a.bn_weight = ptr(self.cells[l].bn.weight)
@@ -379,6 +386,7 @@ class FireNetEngine:
                     st.x, (st.xs_b, st.xs_c, st.xs_h, st.xs_w) = _spk_half(states[l - 1])
                 st.s_prev = _ptr_t(s_prev[l]) if rec else None
             _lib.call(f"wgrad[{l}]", lib.snnflow_wgrad, ctypes.byref(a), stream)
+            self.slab_live[l] = True
 
     def launch_slab_reduce(self, ws, glayers, stream):
         """Fixed-order fp64 sum of every layer's per-block slabs into the flat gradient buffer."""
@@ -397,11 +405,14 @@ class FireNetEngine:
         """All deferred weight gradients on `stream` (serial form of the root step's tail): one
         snnflow_firenet_wgrad call given the step driver's plan, else (per-kernel timing) the
         per-layer launches from Python."""
-        if plan is None or _lib.TIMER is not None:
+        partial = any(len(ls) < self.L for ls in self.pending_layers) or any(self.slab_live)
+        if plan is None or _lib.TIMER is not None or partial:
             for l in range(self.L):
-                self.launch_wgrad(l, B, H, W, cin0, ws, stream)
+                steps = [e for e, ls in zip(self.pending, self.pending_layers) if l in ls]
+                if steps:
+                    self.launch_wgrad(l, B, H, W, cin0, ws, stream, steps)
             self.launch_slab_reduce(ws, glayers, stream)
-            self.pending = []
+            self.pending, self.pending_layers = [], []
             return
         L = self.L
         steps = (_lib.FireNetWgradStep * len(self.pending))()
@@ -417,7 +428,7 @@ class FireNetEngine:
         grec = (ctypes.c_void_p * L)(*[glayers[l][1] for l in range(L)])
         _lib.call("firenet_wgrad", lib.snnflow_firenet_wgrad, ctypes.byref(plan), steps, len(self.pending), gff, grec,
                   stream)
-        self.pending = []
+        self.pending, self.pending_layers = [], []
 
     def plan(self, B, H, W, cin0, ws, wfwd, wbwd):
         """The C step driver's constant arguments (snnflow_firenet_plan), cached per model state."""
@@ -785,6 +796,7 @@ class FireNetStep(torch.autograd.Function):
         gcur, bnc, ys, stats = _Rows(gcur_t), _Rows(bnc_t), _Rows(ys), _Rows(stats)
         # pending: row pointers for the deferred wgrad + the tensors behind them (kept alive)
         eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev, (keep, gcur_t, bnc_t, saved)))
+        eng.pending_layers.append(tuple(range(L)))
         # (the deferred weight gradients stay on this stream after the chain: a side stream
         # overlapping them with the root step's chain measured slower under graph replay,
         # 2.48 -> 2.72 ms per cfg2 train step)
@@ -830,7 +842,7 @@ class FireNetStep(torch.autograd.Function):
         except Exception:
             ws.reset_acc()
             eng.bwd_open = False
-            eng.pending = []
+            eng.pending, eng.pending_layers = [], []
             eng.prep_stale = True
             raise
 
@@ -1022,9 +1034,11 @@ class FireNetSequence(torch.autograd.Function):
             gfl.append(g)
 
         # the deferred weight gradients see the steps in the per-step path's order (last first)
+        fuse = eng.fuse_wgrad  # layers >= 1: dW inside the backward slot tasks (wslab_*)
         for t in range(T - 1, -1, -1):
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys[t]), _Rows(stats[t]), xs[t], states[t], s_prev[t],
                                 (gcur, bnc, ys, stats)))
+            eng.pending_layers.append((0,) if fuse else tuple(range(L)))
         try:
             # backward kernel j of step t: j = 0 top (pred + LIF of layer L-1), j >= 1 layer L-j;
             # in reversed time tau = T-1-t the dependencies have the forward's shape
@@ -1038,9 +1052,17 @@ class FireNetSequence(torch.autograd.Function):
                                             flows[t], gcur[t], gmem[t], bacc[t])
                     else:
                         l = L - j
-                        layers.append(_bwd_layer_args(eng, l, B, H, W, cin0, ys[t], stats[t], mem_in[t], neurons,
-                                                      g_into[t], gcur[t], gmem[t], bacc[t], bnc[t], glayers, gpw, gpb,
-                                                      acc, wfwd, wbwd, g_out[t], ext[t], gxs[t] if l == 0 else None))
+                        a = _bwd_layer_args(eng, l, B, H, W, cin0, ys[t], stats[t], mem_in[t], neurons,
+                                            g_into[t], gcur[t], gmem[t], bacc[t], bnc[t], glayers, gpw, gpb,
+                                            acc, wfwd, wbwd, g_out[t], ext[t], gxs[t] if l == 0 else None)
+                        if fuse and l > 0:
+                            a.wslab_ff = ws.slab_ff[l].data_ptr()
+                            if eng.rec[l]:
+                                a.wslab_rec = ws.slab_rec[l].data_ptr()
+                                a.s_prev = _ptr_t(s_prev[t][l])
+                            a.wslab_accumulate = 1 if eng.slab_live[l] else 0
+                            eng.slab_live[l] = True
+                        layers.append(a)
                 arr = (_lib.LayerBwdArgs * max(len(layers), 1))(*layers)
                 _lib.call("bwd_slot", lib.snnflow_bwd_slot, arr, len(layers),
                           ctypes.byref(top) if top is not None else None, s)
@@ -1053,7 +1075,7 @@ class FireNetSequence(torch.autograd.Function):
         except Exception:
             ws.reset_acc()
             eng.bwd_open = False
-            eng.pending = []
+            eng.pending, eng.pending_layers = [], []
             eng.prep_stale = True
             raise
 

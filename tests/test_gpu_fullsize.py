@@ -27,10 +27,12 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-# relative-L2 bound on every parameter gradient of the cfg2 train step when the spikes agree:
-# ~2x the worst case measured on MI355X (2.8e-6, R1b.ff.weight; profiles/r02/gpu_tests_*.txt,
-# DESIGN.md section 3).
-GRAD_TOL = 6e-6
+# relative-L2 bound on every parameter gradient of the train step when the spikes agree: ~2x the
+# worst case measured on MI355X (profiles/r03/gpu_tests_*.txt).  cfg2: 2.9e-6
+# (G1.bn.weight).  cfg3 sums 2x the pixels per channel and its oracle's own fp32 sums round more:
+# 7.7e-6 (head.bn.bias).  C=32: 2.3e-5 (pred.conv2d.bias: two sums over 1.3 M pixel-steps of terms
+# of both signs; the conv weights 3-4e-6).
+GRAD_TOL = {"cfg2": 6e-6, "cfg3": 1.6e-5, "cfg2-C32": 5e-5}
 
 
 def _rel(a, b):
@@ -205,7 +207,7 @@ def test_cfg2_train_step_vs_oracle(dev, path, tag, B, H, C):
     assert max(r["flow_rel"]) <= 1e-4 and r["flow_maxabs"] <= 1e-4, (r["flow_rel"], r["flow_maxabs"])
     assert np.abs(r["aee"][0] - r["aee"][1]).max() <= 1e-4, r["aee"]
     for n, v in r["grad_rel"].items():
-        assert v <= GRAD_TOL, (n, v)
+        assert v <= GRAD_TOL[tag], (n, v)
     if int(free["flips"].sum()) == 0:  # nothing was adopted: the free-running run IS the comparison
         assert np.abs(free["aee"][0] - free["aee"][1]).max() <= 1e-4
 

@@ -488,10 +488,10 @@ def test_replaced_parameters_after_forward(dev, sequence):
         model.R2b.bn.running_mean = torch.full_like(model.R2b.bn.running_mean, 0.25)
     model.R1b.bn.momentum = 0.3
     model.zero_grad(set_to_none=True)
-    got = run(model)
     fresh = snnflow.LIFFireNet(dict(kw)).to(dev).train()
-    fresh.load_state_dict(model.state_dict())
+    fresh.load_state_dict(model.state_dict())  # the replaced tensors' values, before the next step
     fresh.R1b.bn.momentum = 0.3
+    got = run(model)
     want = run(fresh)
     assert torch.equal(got, want)
     assert torch.equal(model.R1b.bn.running_mean, fresh.R1b.bn.running_mean)

@@ -197,41 +197,20 @@ def _ref_cells(ref):
     return out
 
 
-def test_unet_cfg5_shapes_vs_oracle(dev):
-    """BASELINE cfg5's layer shapes: SpikingRecEVFlowNet at 256x256, base 32 (20.4 M parameters,
-    64..512 channels), B=2, T=2 windows of 1000 events -- so the tiles, split-K factors and chunked
-    split reductions the cfg5 bench selects (csrc/unet.hip) run here -- against the oracle
-    (oracle/unet_ref.py).  Flip-corrected like test_gpu_fullsize.py: where an oracle spike differs
-    from ours and the oracle membrane lies within 1e-4 of the threshold, the oracle adopts our
-    spike straight-through (its graph kept); any other differing spike fails.  Then every flow map,
-    state, the loss and every parameter gradient must match."""
-    import snnflow
-    from oracle import iwe_ref
-    from oracle.unet_ref import SpikingRecEVFlowNetRef
-    from snnflow.synthetic import make_window
-
-    base, H, B, T, eps = 32, 256, 2, 2, 1e-4
-    torch.manual_seed(5)
-    model = snnflow.SpikingRecEVFlowNet(_kw(base)).to(dev)
-    ref = SpikingRecEVFlowNetRef(_kw(base))
-    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
-    gen = torch.Generator(device=dev).manual_seed(3)
-    wins = [make_window(B, 1000, H, H, gen, dev) for _ in range(T)]
-    flows, ours = [], []
-    for w in wins:
-        flows.append(model(None, w["event_cnt"])["flow"])
-        ours.append([s.detach().cpu() for s in model.states])
-
+def _patch_flips(ref, ours_states, eps, counters):
+    """Flip correction of the oracle U-Net (see test_unet_cfg5_shapes_vs_oracle): every cell adopts
+    our spike straight-through where its own differs; the ones whose membrane is not within eps of
+    the threshold are counted as hard.  Returns the per-step target setter."""
     cells = _ref_cells(ref)
-    counters = {"flips": 0, "hard": 0}
-
-    def patch(cell, target):
+    targets = []
+    for cell, i, j in cells:
+        tgt = {}
         orig = type(cell).forward
 
-        def fwd(x, prev, residual=0):
+        def fwd(x, prev, residual=0, cell=cell, tgt=tgt, orig=orig):
             out, st = orig(cell, x, prev, residual)
             v, s = st[0], st[1]
-            o = target["state"]
+            o = tgt["state"].to(s.dtype)
             diff = s.detach() != o
             n = int(diff.sum())
             if n:
@@ -244,22 +223,61 @@ def test_unet_cfg5_shapes_vs_oracle(dev):
                 out = s + residual
             return out, st
         cell.forward = fwd
-
-    targets = []
-    for cell, i, j in cells:
-        tgt = {}
-        patch(cell, tgt)
         targets.append((tgt, i, j))
-    rflows = []
-    for t, w in enumerate(wins):
+
+    def set_step(t):
         for tgt, i, j in targets:
-            st = ours[t][i]
+            st = ours_states[t][i]
             tgt["state"] = (st[j] if j is not None else st)[1]
+    return set_step
+
+
+def test_unet_cfg5_shapes_vs_oracle(dev):
+    """BASELINE cfg5's layer shapes: SpikingRecEVFlowNet at 256x256, base 32 (20.4 M parameters,
+    64..512 channels), B=2, T=2 windows of 1000 events -- so the tiles, split-K factors and chunked
+    split reductions the cfg5 bench selects (csrc/unet.hip) run here -- against the oracle
+    (oracle/unet_ref.py).  Flip-corrected like test_gpu_fullsize.py: where an oracle spike differs
+    from ours and the oracle membrane lies within 1e-4 of the threshold, the oracle adopts our
+    spike straight-through (its graph kept); any other differing spike fails.  Flows, states and
+    the loss must then match (rtol 1e-4 / 1e-5).  Parameter gradients: at this size the fp32
+    oracle's own summation error reaches 1e-4 on the deep, low-resolution layers, so both are
+    measured against an fp64 run of the oracle (same flip correction, seeded with the fp32
+    oracle's dL/dflow): ours must be within max(2 x the fp32 oracle's error, 2e-5) of fp64."""
+    import copy
+
+    import snnflow
+    from oracle import iwe_ref
+    from oracle.unet_ref import SpikingRecEVFlowNetRef
+    from snnflow.synthetic import make_window
+
+    base, H, B, T, eps = 32, 256, 2, 2, 1e-4
+    torch.manual_seed(5)
+    model = snnflow.SpikingRecEVFlowNet(_kw(base)).to(dev)
+    ref = SpikingRecEVFlowNetRef(_kw(base))
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    ref64 = copy.deepcopy(ref).double()
+    gen = torch.Generator(device=dev).manual_seed(3)
+    wins = [make_window(B, 1000, H, H, gen, dev) for _ in range(T)]
+    flows, ours = [], []
+    for w in wins:
+        flows.append(model(None, w["event_cnt"])["flow"])
+        ours.append([s.detach().cpu() for s in model.states])
+
+    counters = {"flips": 0, "hard": 0}
+    step32 = _patch_flips(ref, ours, eps, counters)
+    c64 = {"flips": 0, "hard": 0}
+    step64 = _patch_flips(ref64, ours, eps, c64)
+    rflows, rflows64 = [], []
+    for t, w in enumerate(wins):
+        step32(t)
         rflows.append(ref(None, w["event_cnt"].cpu())["flow"])
+        step64(t)
+        rflows64.append(ref64(None, w["event_cnt"].cpu().double())["flow"])
         for k, (a, b) in enumerate(zip(ours[t], ref.states)):
             np.testing.assert_allclose(a.numpy(), b.detach().numpy(), rtol=1e-4, atol=1e-4, err_msg=f"state {t} {k}")
-    print(f"\n[unet cfg5 shapes] spike flips {counters['flips']} (away from the threshold: {counters['hard']})")
-    assert counters["hard"] == 0
+    print(f"\n[unet cfg5 shapes] spike flips {counters['flips']} (away from the threshold: {counters['hard']}); "
+          f"fp64 oracle: {c64['flips']} ({c64['hard']})")
+    assert counters["hard"] == 0 and c64["hard"] == 0
     worst = 0.0
     for t in range(T):
         for i in range(4):
@@ -280,11 +298,21 @@ def test_unet_cfg5_shapes_vs_oracle(dev):
     rloss = rloss / 4
     np.testing.assert_allclose(loss.item(), rloss.item(), rtol=1e-5)
     loss.backward()
+    allr = [f for fs in rflows for f in fs]
+    seeds = torch.autograd.grad(rloss, allr, retain_graph=True)
     rloss.backward()
-    errs = {n: _rel(a.grad.cpu().numpy(), b.grad.numpy()) for (n, a), (_, b) in
-            zip(model.named_parameters(), ref.named_parameters())}
-    w = max(errs.items(), key=lambda kv: kv[1])
+    sur = sum((f * g.double()).sum() for f, g in zip([f for fs in rflows64 for f in fs], seeds))
+    sur.backward()
+    e_ours, e_32 = {}, {}
+    for (n, a), (_, b), (_, c) in zip(model.named_parameters(), ref.named_parameters(), ref64.named_parameters()):
+        g64 = c.grad.numpy()
+        e_ours[n] = _rel(a.grad.cpu().numpy(), g64)
+        e_32[n] = _rel(b.grad.numpy(), g64)
+    w = max(e_ours.items(), key=lambda kv: kv[1])
     print(f"[unet cfg5 shapes] max |dflow| {worst:.2e}; loss {loss.item():.9g} vs {rloss.item():.9g}; "
-          f"grad rel-L2 worst {w[0]} {w[1]:.2e} over {len(errs)} tensors")
-    for n, e in errs.items():
-        assert e < GRAD_TOL, (n, e)
+          f"grad rel-L2 vs fp64: ours worst {w[0]} {w[1]:.2e} (fp32 oracle there {e_32[w[0]]:.2e}; "
+          f"fp32 oracle worst {max(e_32.values()):.2e}) over {len(e_ours)} tensors")
+    print("[unet cfg5 shapes] ours/oracle32 vs fp64: " + ", ".join(
+        f"{n}={e_ours[n]:.1e}/{e_32[n]:.1e}" for n in sorted(e_ours, key=lambda k: -e_ours[k])[:20]))
+    for n in e_ours:
+        assert e_ours[n] <= max(2 * e_32[n], 2e-5), (n, e_ours[n], e_32[n])

@@ -20,8 +20,8 @@ import torch  # noqa: E402
 
 KINDS = {0: ("conv_fwd", ["prologue", "lif_halo", "conv", "store+sums"]),
          1: ("conv_fwd_rec", ["prologue", "lif_halo", "conv", "store+sums"]),
-         2: ("layer_bwd", ["prologue", "bn_bwd_halo", "dgrad", "lif_bwd+store", "sums"]),
-         3: ("layer_bwd_rec", ["prologue", "bn_bwd_halo", "dgrad", "lif_bwd+store", "sums"])}
+         2: ("layer_bwd", ["prologue", "bn_bwd_halo", "dgrad", "lif_bwd+store", "sums", "fused_wgrad"]),
+         3: ("layer_bwd_rec", ["prologue", "bn_bwd_halo", "dgrad", "lif_bwd+store", "sums", "fused_wgrad"])}
 
 
 def main(C=8, R=128, B=8, T=10):
