@@ -41,7 +41,9 @@ class WidthHeaviside(torch.autograd.Function):
     def forward(ctx, x, width, kind):
         ctx.save_for_backward(x, width)
         ctx.kind = kind
-        return x.gt(0).float()
+        # the reference's x.gt(0).float(): identical for its fp32 tensors; the dtype of x keeps an
+        # fp64 run of the oracle in fp64 (tests/test_gpu_unet.py measures precision against one)
+        return x.gt(0).to(x.dtype)
 
     @staticmethod
     def backward(ctx, g):

@@ -92,6 +92,7 @@ __device__ inline float mem_grad(float gv, float m, const LifCoef& k, bool zero_
 // the halo loads instead of following the batch-sum gather.
 struct NeuronRegs { float w, b, beta, theta, rm, rv; };
 
+template <bool SC1 = false>
 __device__ inline NeuronRegs load_neuron(const snnflow_neuron& n, int C, bool lead) {
     NeuronRegs r = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int c = threadIdx.x;
@@ -101,9 +102,10 @@ __device__ inline NeuronRegs load_neuron(const snnflow_neuron& n, int C, bool le
         r.beta = n.beta[c];
         r.theta = n.threshold[c];
         // running statistics: every block in eval mode, block 0 (the updater) in train mode
+        // (SC1: the previous step's updater ran on another CU of this launch)
         if (n.running_mean && (!n.bn_train || lead)) {
-            r.rm = n.running_mean[c];
-            r.rv = n.running_var[c];
+            r.rm = ld1<SC1>(n.running_mean + c);
+            r.rv = ld1<SC1>(n.running_var + c);
         }
     }
     return r;
@@ -137,7 +139,7 @@ __device__ inline BnStat bn_stat(const snnflow_neuron& n, const NeuronRegs& r, c
 // (momentum, unbiased variance) and num_batches_tracked += 1 of torch's BatchNorm2d.
 // `sums`: LDS totals from acc_gather (train mode only); r: load_neuron of this thread.
 __device__ void lif_prologue(const snnflow_neuron& n, const NeuronRegs& r, const double* sums, int C, double N,
-                             float* stats_out, LifCoef* coef, float* mean_out, bool lead) {
+                             float* stats_out, LifCoef* coef, float* mean_out, bool lead, bool inlaunch = false) {
     const int c = threadIdx.x;
     if (c < C) {
         const BnStat st = bn_stat(n, r, sums, C, c, N);
@@ -160,7 +162,13 @@ __device__ void lif_prologue(const snnflow_neuron& n, const NeuronRegs& r, const
             }
         }
     }
-    if (c == 0 && lead && n.bn_train && n.num_batches_tracked) n.num_batches_tracked[0] += 1;
+    if (c == 0 && lead && n.bn_train && n.num_batches_tracked) {
+        if (inlaunch)  // updated by several tasks of one persistent launch: coherent atomic
+            __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(n.num_batches_tracked), 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        else
+            n.num_batches_tracked[0] += 1;
+    }
 }
 
 // Layer-l gradients of (gamma, bn bias, beta, threshold) [and pred] from the LIF-backward
@@ -341,7 +349,7 @@ struct ConvFwdLds {
     static_assert(!BT || !REC || PF_REC, "bf16 spike tile: s_prev needs its own tile");
 };
 
-template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT>
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool SC1 = false>
 __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, float* lds) {
     using L = ConvFwdLds<CIN, C, LIF_IN, REC, SPLIT>;
     constexpr int NTB = NT * SPLIT, CO = C / SPLIT;
@@ -368,8 +376,8 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     AccGather<LIF_IN ? 2 * CIN : 1> gat;
     NeuronRegs nr = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if constexpr (LIF_IN) {
-        if (a.prev.bn_train) acc_gather_load<2 * CIN>(a.prev_acc, 2 * CIN, gat);
-        nr = load_neuron(a.prev, CIN, g.bid == 0);
+        if (a.prev.bn_train) acc_gather_load<2 * CIN, SC1>(a.prev_acc, 2 * CIN, gat);
+        nr = load_neuron<SC1>(a.prev, CIN, g.bid == 0);
     }
     constexpr bool WL = L::WL, FRAG = L::FRAG;
     WStage<WL ? 9 * C * C : 1, NTB> sw_ff, sw_rec;
@@ -388,17 +396,17 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     }
     float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
     if constexpr (PF_REC) {
-        if (has_rec) halo_load<C, NTB, (C <= 8)>(a.s_prev, tl, H, W, rs);
+        if (has_rec) halo_load<C, NTB, (C <= 8), SC1>(a.s_prev, tl, H, W, rs);
     }
     if constexpr (LIF_IN) {
         constexpr int R = Halo4<CIN, NTB>::R, Q = CIN / 4;
         float4 ry[R], rm[R];
-        halo_load<CIN, NTB, (CIN <= 8)>(a.prev_y, tl, H, W, ry);
-        if (a.prev_mem) halo_load<CIN, NTB, (CIN <= 8)>(a.prev_mem, tl, H, W, rm);
+        halo_load<CIN, NTB, (CIN <= 8), SC1>(a.prev_y, tl, H, W, ry);
+        if (a.prev_mem) halo_load<CIN, NTB, (CIN <= 8), SC1>(a.prev_mem, tl, H, W, rm);
         else zero4(rm, R);
         __shared__ double sums[2 * CIN];
         if (a.prev.bn_train) acc_gather_reduce<2 * CIN>(gat, sums);
-        lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr, g.bid == 0);
+        lif_prologue(a.prev, nr, sums, CIN, (double)a.B * H * W, a.prev_stats, coef, nullptr, g.bid == 0, SC1);
         __syncthreads();
         // (stores issued after the gather: CDNA's vmcnt counts stores, so zeroing before the
         // gather made its wait include the store acknowledgements)
@@ -590,7 +598,7 @@ __global__ __launch_bounds__(NT * SPLIT) void k_conv_fwd(snnflow_conv_fwd_args a
 
 // LIF (+ 1x1 pred conv + tanh) over pixels: one thread per pixel, all C channels.
 // NTH threads (= pixels) per block: NT for its own launch, NT * 2 inside a wavefront launch.
-template <int C, bool PRED, int NTH>
+template <int C, bool PRED, int NTH, bool SC1 = false>
 __device__ void lif_fwd_body(const snnflow_lif_fwd_args& a, const Grid g) {
     constexpr int Q = C / 4;
     __shared__ LifCoef coef[C];
@@ -603,17 +611,17 @@ __device__ void lif_fwd_body(const snnflow_lif_fwd_args& a, const Grid g) {
     const int64_t pc = act ? p : npix - 1;  // unconditional 16-B loads
     // BN-sum replicas and per-channel parameters first: their math then overlaps the pixel loads
     AccGather<2 * C> gat;
-    if (a.n.bn_train) acc_gather_load<2 * C>(a.acc, 2 * C, gat);
-    const NeuronRegs nr = load_neuron(a.n, C, g.bid == 0);
+    if (a.n.bn_train) acc_gather_load<2 * C, SC1>(a.acc, 2 * C, gat);
+    const NeuronRegs nr = load_neuron<SC1>(a.n, C, g.bid == 0);
     float4 yv[Q], mv[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        yv[q] = y4[pc * Q + q];
-        mv[q] = ld4_or_zero(m4, y4, pc * Q + q);
+        yv[q] = ld4<SC1>(y4, pc * Q + q);
+        mv[q] = ld4_or_zero_sc<SC1>(m4, y4, pc * Q + q);
     }
     __shared__ double sums[2 * C];
     if (a.n.bn_train) acc_gather_reduce<2 * C>(gat, sums);
-    lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr, g.bid == 0);
+    lif_prologue(a.n, nr, sums, C, (double)npix, a.stats, coef, nullptr, g.bid == 0, SC1);
     __syncthreads();
     zero_consumed(a.zero0, a.zero1, a.zero_n, g);  // after the gather (vmcnt counts stores)
     if (!act) return;
@@ -2544,6 +2552,224 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L
 }
 
 // ---------------------------------------------------------------------------
+// Persistent dataflow forward of a window (snnflow_fwd_seq, include/snnflow.h).
+// sync: [0, 8) per-XCD queue heads, [8] timeout flag, [16 + t (L+1) + k] completion counter of
+// layer-step (k, t) (blocks done).  Items of queue x, in wavefront order (slot m = k + 2t, t
+// ascending inside a slot): for every layer-step its blocks of XCD x's images -- conv layer-steps
+// the tiles bid = x + 8 i (block_tile maps them to images [x B/8, (x+1) B/8)), the top LIF
+// layer-step the pixel blocks [x n/8, (x+1) n/8).
+// ---------------------------------------------------------------------------
+struct SeqFwdParams {
+    int T, L, nconv, ntop;  // blocks per conv / top layer-step
+    int rec[SNNFLOW_MAX_LAYERS];
+    int* sync;
+    const snnflow_conv_fwd_args* conv;  // [T][L] (k2_seq_build)
+    const snnflow_lif_fwd_args* top;    // [T]
+};
+
+#ifndef SNNFLOW_SEQ_SC1
+#define SNNFLOW_SEQ_SC1 1    // sc1 loads of handed-off bytes (A/B: 0 = plain loads)
+#endif
+#ifndef SNNFLOW_SEQ_FENCE
+#define SNNFLOW_SEQ_FENCE 0  // agent release before every completion count, acquire after every wait (A/B)
+#endif
+constexpr bool kSeqSc1 = SNNFLOW_SEQ_SC1 != 0;
+constexpr int kSeqSyncHead = 0, kSeqSyncErr = 8, kSeqSyncDone = 16;
+constexpr unsigned kSeqSpinLimit = 1u << 22;  // polls of one dependency before giving up (~0.5 s)
+
+__device__ inline int xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 7u);
+}
+
+__global__ void k_debug_xcc(int* out) {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    if (threadIdx.x == 0) out[blockIdx.x] = (int)v;
+}
+
+// Lane 0: wait until counter j has reached `need` (relaxed agent-scope polls, s_sleep between);
+// on timeout raise the error flag and go on (the launch then completes with invalid results
+// instead of hanging the GPU).
+__device__ inline void seq_wait(int* sync, int j, int need) {
+    int* c = sync + kSeqSyncDone + j;
+    unsigned spins = 0;
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > kSeqSpinLimit) {
+            __hip_atomic_store(sync + kSeqSyncErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+    }
+}
+
+// The slot-path argument structs of layer-step (k, t), from the window's tensors (the layout of
+// engine.FireNetSequence.forward / _fwd_conv_args / _fwd_top_args).
+__device__ inline void seq_fwd_conv_args(const snnflow_fwd_seq_args& p, int k, int t, snnflow_conv_fwd_args& a) {
+    const int L = p.L, C = p.c;
+    const int64_t ny = (int64_t)p.B * p.H * p.W * C, n1 = 2 * ny;
+    auto ys = [&](int tt, int l) { return p.ys + ((int64_t)tt * L + l) * ny; };
+    auto st = [&](int tt, int l) { return p.states + ((int64_t)tt * L + l) * n1; };
+    a = snnflow_conv_fwd_args{};
+    a.B = p.B; a.H = p.H; a.W = p.W; a.c = C;
+    if (k == 0) {
+        a.cin = p.cin0; a.lif_in = 0;
+        a.x = p.x[t]; a.xs_b = p.xs[0]; a.xs_c = p.xs[1]; a.xs_h = p.xs[2]; a.xs_w = p.xs[3];
+    } else {
+        a.cin = C; a.lif_in = 1;
+        a.prev_y = ys(t, k - 1);
+        a.prev_mem = t == 0 ? p.mem0[k - 1] : st(t - 1, k - 1);
+        a.prev_acc = p.facc + ((int64_t)t * L + k - 1) * p.facc_stride;
+        a.prev_stats = p.stats + ((int64_t)t * L + k - 1) * 2 * C;
+        a.prev = p.n[k - 1];
+        a.prev_state = st(t, k - 1);
+    }
+    a.wt_ff = p.wt_ff[k]; a.wt_rec = p.wt_rec[k]; a.wt_ff_t = p.wt_ff_t[k]; a.wt_rec_t = p.wt_rec_t[k];
+    if (p.rec[k]) a.s_prev = t == 0 ? p.sprev0[k] : st(t - 1, k) + ny;
+    a.y = ys(t, k);
+    a.acc = p.train[k] ? p.facc + ((int64_t)t * L + k) * p.facc_stride : nullptr;
+}
+
+__device__ inline void seq_fwd_top_args(const snnflow_fwd_seq_args& p, int t, snnflow_lif_fwd_args& f) {
+    const int L = p.L, C = p.c, l = L - 1;
+    const int64_t ny = (int64_t)p.B * p.H * p.W * C, n1 = 2 * ny;
+    f = snnflow_lif_fwd_args{};
+    f.B = p.B; f.H = p.H; f.W = p.W; f.c = C;
+    f.y = p.ys + ((int64_t)t * L + l) * ny;
+    f.mem = t == 0 ? p.mem0[l] : p.states + ((int64_t)(t - 1) * L + l) * n1;
+    f.acc = p.facc + ((int64_t)t * L + l) * p.facc_stride;
+    f.stats = p.stats + ((int64_t)t * L + l) * 2 * C;
+    f.n = p.n[l];
+    f.state = p.states + ((int64_t)t * L + l) * n1;
+    f.pred_w = p.pred_w; f.pred_b = p.pred_b; f.flow = p.flow[t];
+}
+
+// Every layer-step's argument structs into the work area, read by k_fwd_seq through the scalar
+// cache like kernel arguments (one thread per layer-step).
+__global__ void k_fwd_seq_build(snnflow_fwd_seq_args p, snnflow_conv_fwd_args* conv, snnflow_lif_fwd_args* top) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x, K = p.L + 1;
+    if (j >= p.T * K) return;
+    const int t = j / K, k = j - t * K;
+    if (k < p.L) {
+        snnflow_conv_fwd_args a;
+        seq_fwd_conv_args(p, k, t, a);
+        conv[t * p.L + k] = a;
+    } else {
+        snnflow_lif_fwd_args f;
+        seq_fwd_top_args(p, t, f);
+        top[t] = f;
+    }
+}
+
+// One work item (kept out of line: inlined into the item loop, the bodies' per-thread loop-invariant
+// address math would be hoisted and held across every phase of every variant, 149 VGPRs).
+template <typename T>
+__device__ inline T* uniform_ptr(T* p) {  // a wave-uniform pointer argument back into SGPRs
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(((uint64_t)hi << 32) | lo);
+}
+
+template <int C>
+__device__ __attribute__((noinline)) void seq_fwd_item(const SeqFwdParams* pg, int k, int t, int i, int q, float* pool) {
+    typedef const __attribute__((address_space(4))) SeqFwdParams* cptr;
+    const cptr pp = (cptr)uniform_ptr(pg);
+    k = __builtin_amdgcn_readfirstlane(k);
+    t = __builtin_amdgcn_readfirstlane(t);
+    i = __builtin_amdgcn_readfirstlane(i);
+    q = __builtin_amdgcn_readfirstlane(q);
+    pool = uniform_ptr(pool);
+    const int L = pp->L, nconv = pp->nconv, ntop = pp->ntop;
+#ifndef SEQV
+#define SEQV 15
+#endif
+    if (k < L) {
+        const snnflow_conv_fwd_args a =
+            task_args((const __attribute__((address_space(4))) snnflow_conv_fwd_args*)pp->conv + (t * L + k));
+        const Grid g{q + 8 * i, nconv};
+        if (k == 0) {
+            if constexpr (SEQV & 1) {
+                if (a.cin == 2) conv_fwd_body<2, C, false, false, 2, kSeqSc1>(a, g, pool);
+                else conv_fwd_body<4, C, false, false, 2, kSeqSc1>(a, g, pool);
+            }
+        } else if (pp->rec[k]) {
+            if constexpr (SEQV & 2) conv_fwd_body<C, C, true, true, 2, kSeqSc1>(a, g, pool);
+        } else {
+            if constexpr (SEQV & 4) conv_fwd_body<C, C, true, false, 2, kSeqSc1>(a, g, pool);
+        }
+    } else {
+        if constexpr (SEQV & 8) {
+            const snnflow_lif_fwd_args f =
+                task_args((const __attribute__((address_space(4))) snnflow_lif_fwd_args*)pp->top + t);
+            lif_fwd_body<C, true, NT * 2, kSeqSc1>(f, Grid{q * (ntop / 8) + i, ntop});
+        }
+    }
+}
+
+template <int C>
+__global__ __launch_bounds__(NT * 2, 6) void k_fwd_seq(SeqFwdParams) {
+    typedef const __attribute__((address_space(4))) SeqFwdParams* cptr;
+    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+    __shared__ __attribute__((aligned(16))) float pool[SlotLds<C>::FWD];
+    __shared__ int s_item;
+    const int tid = threadIdx.x;
+    const int T = pp->T, L = pp->L, K = L + 1, M = K + 2 * (T - 1);
+    const int nconv = pp->nconv, ntop = pp->ntop;
+    int* const sync = (int*)pp->sync;
+    const int q = xcc_id();
+    // scan position in the queue's wavefront order (items a block takes only increase)
+    int m = 0, t = 0, base = 0;
+    auto first_t = [&](int mm) { const int lo = mm - L; return lo > 0 ? (lo + 1) / 2 : 0; };
+    t = first_t(0);
+    for (;;) {
+        if (tid == 0) s_item = __hip_atomic_fetch_add(sync + kSeqSyncHead + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const int item = __builtin_amdgcn_readfirstlane(s_item);
+        // item -> (k, t, i): advance over whole layer-steps
+        int k = 0;
+        bool found = false;
+        while (m < M) {
+            k = m - 2 * t;
+            if (k < 0 || t >= T) {  // past this slot's last layer-step
+                ++m;
+                t = first_t(m);
+                continue;
+            }
+            const int cnt = (k < L ? nconv : ntop) / 8;
+            if (item < base + cnt) { found = true; break; }
+            base += cnt;
+            ++t;
+        }
+        if (!found) break;
+        const int i = item - base;
+        const int j = t * K + k;
+        // dependencies (lane 0 polls, the barrier releases every wave's loads behind it)
+        if (tid == 0) {
+            if (k >= 1) seq_wait(sync, t * K + k - 1, k - 1 < L ? nconv : ntop);
+            if (k >= 1 && t >= 1) seq_wait(sync, (t - 1) * K + k, k < L ? nconv : ntop);
+            if (k >= 1 && k < L && pp->rec[k] && t >= 1) seq_wait(sync, (t - 1) * K + k + 1, k + 1 < L ? nconv : ntop);
+            if (SNNFLOW_SEQ_FENCE) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        seq_fwd_item<C>((const SeqFwdParams*)pp, k, t, i, q, pool);
+        // completion: every wave's stores and atomics acknowledged, then one count
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            if (SNNFLOW_SEQ_FENCE) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __hip_atomic_fetch_add(sync + kSeqSyncDone + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Host dispatch
 // ---------------------------------------------------------------------------
 bool valid_c(int c) { return c == 4 || c == 8 || c == 16 || c == 32; }
@@ -2964,6 +3190,72 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
     if (c == 8) hipLaunchKernelGGL(k_bwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
     else if (c == 16) hipLaunchKernelGGL(k_bwd_slot<16>, dim3(nb), dim3(2 * NT), 0, s, p);
     else hipLaunchKernelGGL(k_bwd_slot<32>, dim3(nb), dim3(2 * NT), 0, s, p);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_seq_sync_ints(int T, int L) { return kSeqSyncDone + T * (L + 1); }
+
+// Diagnostics: the XCC id each of n blocks of a 512-thread launch runs on (tests only).
+int snnflow_debug_xcc(int* out, int n, void* stream) {
+    hipLaunchKernelGGL(k_debug_xcc, dim3(n), dim3(2 * NT), 0, (hipStream_t)stream, out);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+// work area: sync ints (padded to 256 B), then the conv argument structs [T][L], then the top ones [T]
+static size_t seq_sync_bytes(int T, int L) { return ((size_t)snnflow_seq_sync_ints(T, L) * sizeof(int) + 255) / 256 * 256; }
+size_t snnflow_seq_work_bytes(int T, int L) {
+    return seq_sync_bytes(T, L) + (size_t)T * L * sizeof(snnflow_conv_fwd_args) + (size_t)T * sizeof(snnflow_lif_fwd_args) + 256;
+}
+
+int snnflow_seq_supported(int c, int B, int H, int W, int T, int L) {
+    const int64_t npix = (int64_t)B * H * W;
+    return (c == 8 && B > 0 && B % 8 == 0 && npix % (2 * NT) == 0 && T >= 1 && T <= SNNFLOW_SEQ_MAX_T && L >= 1 &&
+            L <= SNNFLOW_MAX_LAYERS) ? 1 : 0;
+}
+
+int snnflow_fwd_seq(const snnflow_fwd_seq_args* a, void* stream) {
+    if (!a || !a->sync || !a->ys || !a->stats || !a->states || !a->facc || !a->pred_w || !a->pred_b)
+        SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: bad arguments");
+    if (!snnflow_seq_supported(a->c, a->B, a->H, a->W, a->T, a->L))
+        SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: unsupported shape (c == 8, B % 8 == 0, B*H*W % 512 == 0, T <= 16)");
+    if (a->cin0 != 2 && a->cin0 != 4) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_seq: cin0 must be 2 or 4");
+    for (int t = 0; t < a->T; ++t)
+        if (!a->x[t] || !a->flow[t]) SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: step input / flow missing");
+    for (int l = 0; l < a->L; ++l) {
+        if (!a->wt_ff[l] || !a->wt_ff_t[l] || (a->rec[l] && (!a->wt_rec[l] || !a->wt_rec_t[l])))
+            SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: weights");
+        if (l == 0 && a->rec[0]) SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: the head is feed-forward");
+    }
+    SeqFwdParams p = {};
+    p.T = a->T; p.L = a->L;
+    p.nconv = snnflow_conv_blocks(a->B, a->H, a->W);
+    p.ntop = slot_top_blocks(a->c, a->B, a->H, a->W);
+    if (p.nconv % 8 || p.ntop % 8) SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: block counts must be multiples of 8");
+    for (int l = 0; l < a->L; ++l) p.rec[l] = a->rec[l] ? 1 : 0;
+    char* work = reinterpret_cast<char*>(a->sync);
+    p.sync = a->sync;
+    snnflow_conv_fwd_args* conv = reinterpret_cast<snnflow_conv_fwd_args*>(work + seq_sync_bytes(a->T, a->L));
+    snnflow_lif_fwd_args* top = reinterpret_cast<snnflow_lif_fwd_args*>(conv + a->T * a->L);
+    p.conv = conv;
+    p.top = top;
+    const hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(a->sync, 0, sizeof(int) * snnflow_seq_sync_ints(a->T, a->L), s);
+    if (e != hipSuccess) return snnflow_set_error((int)e, "fwd_seq: memset");
+    const int ntask = a->T * (a->L + 1);
+    hipLaunchKernelGGL(k_fwd_seq_build, dim3((ntask + 63) / 64), dim3(64), 0, s, *a, conv, top);
+    // grid: every block resident (a waiting block must never keep an item's producer from a CU)
+    static int cus = 0, per_cu = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return snnflow_set_error(SNNFLOW_E_ARG, "fwd_seq: device query");
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_fwd_seq<8>, 2 * NT, 0) != hipSuccess) nb = 1;
+        per_cu = nb < 1 ? 1 : (nb > 3 ? 3 : nb);
+    }
+    hipLaunchKernelGGL(k_fwd_seq<8>, dim3(cus * per_cu), dim3(2 * NT), 0, s, p);
     SNN_CHECK_LAUNCH();
     return 0;
 }

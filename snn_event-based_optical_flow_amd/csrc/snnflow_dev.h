@@ -142,6 +142,52 @@ __device__ inline void st_state4(float4* base, int64_t i, const float4& v) {
 
 __device__ inline bool in_image(int h, int w, int H, int W) { return h >= 0 && h < H && w >= 0 && w < W; }
 
+// Loads of bytes another workgroup of the SAME launch wrote (the persistent dataflow kernels,
+// snnflow_fwd_seq): SC1 = `sc1` loads, which bypass this CU's vector L1 and are served by the XCD's
+// L2 (MI355X_MICROARCH.md, inter-workgroup visibility): never a stale L1 copy.  Producer and
+// consumer of such bytes run on the same XCD there (XCD-affine work queues), so the L2 is shared;
+// the base pointer must be wave-uniform (buffer descriptor in SGPRs).  SC1 = false: plain loads.
+// (the b128 result must be taken as an unsigned vector: read through an int vector and
+// __builtin_bit_cast per element, ROCm 7.2 narrows the load to one dword and broadcasts it)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ inline float4 u4f(const u32x4& v) {
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+template <bool SC1>
+__device__ inline float4 ld4(const float4* base, int64_t i) {
+    if constexpr (SC1) {
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(base), (short)0, 0x7fffffff, 0x00020000);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16), 0, 16);  // aux 16 = sc1
+        return u4f(v);
+    } else {
+        return base[i];
+    }
+}
+template <bool SC1>
+__device__ inline float ld1(const float* p) {
+    if constexpr (SC1) {
+        return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+    } else {
+        return *p;
+    }
+}
+template <bool SC1>
+__device__ inline double ld_f64(const double* p) {
+    if constexpr (SC1) {
+        return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    } else {
+        return *p;
+    }
+}
+template <bool SC1>
+__device__ inline float4 ld4_or_zero_sc(const float4* p, const float4* fallback, int64_t i) {
+    const float4 t = ld4<SC1>(p ? p : fallback, i);
+    return p ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 // A C-channel NHWC halo tile as float4 elements e = pixel * (C/4) + quad, distributed
 // round-robin over the block's NTH threads (element e -> thread e % NTH, slot e / NTH),
 // so a thread issues all R of its loads before using any (register prefetch).
@@ -168,10 +214,28 @@ __device__ inline int64_t halo_idx4(int e, const Tile& tl, int H, int W) {
 // is scalar math once per call and each element adds a 32-bit (row, column, quad) offset to it
 // (measured at C = 8: forward slot 20.8 -> 20.5 us, backward slot 24.4 -> 25.0 us; at C = 32 the
 // forward slot 87 -> 110 us: used for the C = 8 forward halos only).
-template <int CH, int NTH = NT, bool BASE = false>
+template <int CH, int NTH = NT, bool BASE = false, bool SC1 = false>
 __device__ inline void halo_load(const float* __restrict__ src, const Tile& tl, int H, int W,
                                  float4 (&r)[Halo4<CH, NTH>::R]) {
-    if constexpr (BASE) {
+    if constexpr (SC1) {  // BASE addressing through one sc1 buffer descriptor at the halo origin
+        constexpr int Q = CH / 4;
+        const float4* base = reinterpret_cast<const float4*>(src) +
+                             (((int64_t)tl.b * H + (tl.h0 - 1)) * W + (tl.w0 - 1)) * Q;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(base), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
+            const int e = threadIdx.x + i * NTH;
+            const int p = e / Q, q = e - p * Q;
+            const int rr = p / HWD, cc = p - rr * HWD;
+            const bool ok = e < Halo4<CH, NTH>::E && in_image(tl.h0 + rr - 1, tl.w0 + cc - 1, H, W);
+            // outside the image: an offset past num_records, which the range check turns into zeros
+            // without a memory access (the descriptor base itself may lie before the tensor)
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? ((rr * W + cc) * Q + q) * 16 : (int)0x7ffffff0,
+                                                                  0, 16);
+            r[i] = ok ? u4f(v) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    } else if constexpr (BASE) {
         constexpr int Q = CH / 4;
         const float4* base = reinterpret_cast<const float4*>(src) +
                              (((int64_t)tl.b * H + (tl.h0 - 1)) * W + (tl.w0 - 1)) * Q;

@@ -811,7 +811,7 @@ struct AccGather {
     double v[PER];
 };
 
-template <int M>
+template <int M, bool SC1 = false>
 __device__ inline void acc_gather_load(const double* acc, int n, AccGather<M>& r) {
     using A = AccGather<M>;
     const int tid = threadIdx.x, st = acc_stride(n);
@@ -819,7 +819,7 @@ __device__ inline void acc_gather_load(const double* acc, int n, AccGather<M>& r
 #pragma unroll
     for (int k = 0; k < A::PER; ++k) {
         const int sh = g + k * A::TPJ;
-        r.v[k] = (tid < A::TPJ * M && sh < kAccShards) ? acc[sh * st + j] : 0.0;
+        r.v[k] = (tid < A::TPJ * M && sh < kAccShards) ? ld_f64<SC1>(acc + sh * st + j) : 0.0;
     }
 }
 

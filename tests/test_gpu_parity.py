@@ -1337,3 +1337,55 @@ def test_log_activity_with_forward_hooks(dev):
             for n in a:
                 assert abs(a[n] - b[n]) <= 1e-4, n
     assert len(seen) == 2
+
+
+@pytest.mark.parametrize("name,H,W,T", [("LIFFireNet", 32, 32, 5), ("LIFFireNet", 64, 32, 1), ("LIFFireNet", 32, 48, 16),
+                                        ("LIFFireNet_short", 32, 32, 4), ("LIFFireFlowNet", 32, 32, 3)])
+def test_persistent_forward_matches_slots(dev, monkeypatch, name, H, W, T):
+    """The persistent dataflow forward (snnflow_fwd_seq: one launch, per-XCD work queues, per
+    layer-step completion counters) against the wavefront slot launches (SNNFLOW_SEQ=0) on the same
+    window: flows, every state, the lif.mem caches, BatchNorm running statistics and
+    num_batches_tracked, the backward's gradients; and the launch's timeout flag is clear.  Same
+    per-(layer, step) arithmetic; only the fp64 batch-sum atomics may add in another order."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow import _lib
+    from snnflow.synthetic import make_window
+
+    B = 8
+    torch.manual_seed(21)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    ma = getattr(snnflow, name)(dict(kw)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    assert _lib.lib.snnflow_seq_supported(8, B, H, W, T, ma.engine.L)
+    gen = torch.Generator(device=dev).manual_seed(22)
+    wins = [make_window(B, 500, H, W, gen, dev) for _ in range(T)]
+    res = {}
+    for tag, m, flag in (("seq", ma, "1"), ("slots", mb, "0")):
+        monkeypatch.setenv("SNNFLOW_SEQ", flag)
+        m.engine.last_seq_work = None
+        outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+        loss = sum(((o["flow"][0] * (t + 1)) ** 2).sum() for t, o in enumerate(outs))
+        loss.backward()
+        torch.cuda.synchronize()
+        res[tag] = outs
+        if flag == "1":
+            work = m.engine.last_seq_work
+            assert work is not None, "the persistent path did not run"
+            assert int(work[:64].view(torch.int32)[8].item()) == 0, "dependency wait timed out"
+        else:
+            assert m.engine.last_seq_work is None
+    for t in range(T):
+        np.testing.assert_allclose(res["seq"][t]["flow"][0].detach().cpu().numpy(),
+                                   res["slots"][t]["flow"][0].detach().cpu().numpy(), rtol=1e-6, atol=1e-8)
+    for sa, sb in zip(ma.states, mb.states):
+        np.testing.assert_allclose(sa.detach().cpu().numpy(), sb.detach().cpu().numpy(), rtol=1e-6, atol=1e-7)
+    for (n, a), (_, b) in zip(ma.named_buffers(), mb.named_buffers()):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-8, err_msg=n)
+    for n, _ in ma.layer_spec:
+        np.testing.assert_allclose(getattr(ma, n).lif.mem.cpu().numpy(), getattr(mb, n).lif.mem.cpu().numpy(),
+                                   rtol=1e-6, atol=1e-7)
+    for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
+        assert _rel(a.grad.cpu().numpy(), b.grad.cpu().numpy()) < 1e-5, n
