@@ -2574,7 +2574,7 @@ struct SeqFwdParams {
 #define SNNFLOW_SEQ_FENCE 0  // agent release before every completion count, acquire after every wait (A/B)
 #endif
 constexpr bool kSeqSc1 = SNNFLOW_SEQ_SC1 != 0;
-constexpr int kSeqSyncHead = 0, kSeqSyncErr = 8, kSeqSyncDone = 16;
+constexpr int kSeqSyncHead = 0, kSeqSyncErr = 8, kSeqSyncDone = 24;
 constexpr unsigned kSeqSpinLimit = 1u << 22;  // polls of one dependency before giving up (~0.5 s)
 
 __device__ inline int xcc_id() {
@@ -2592,11 +2592,25 @@ __global__ void k_debug_xcc(int* out) {
 // Lane 0: wait until counter j has reached `need` (relaxed agent-scope polls, s_sleep between);
 // on timeout raise the error flag and go on (the launch then completes with invalid results
 // instead of hanging the GPU).
+#ifndef SNNFLOW_SEQ_POLL
+#define SNNFLOW_SEQ_POLL 0  // 0: sc1 load polls; 1: atomic fetch-add(0) polls (A/B)
+#endif
+#ifndef SNNFLOW_SEQ_SLEEP
+#define SNNFLOW_SEQ_SLEEP 2  // s_sleep argument between polls (x 64 cycles), doubled up to 32x (A/B)
+#endif
+__device__ inline int seq_poll(int* c) {
+    if (SNNFLOW_SEQ_POLL) return __hip_atomic_fetch_add(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ inline void seq_wait(int* sync, int j, int need) {
     int* c = sync + kSeqSyncDone + j;
-    unsigned spins = 0;
-    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-        __builtin_amdgcn_s_sleep(2);
+    unsigned spins = 0, nap = 0;
+    while (seq_poll(c) < need) {
+        // back off: a few short naps, then longer ones (every poller is a load on this one line)
+        if (nap < 4) __builtin_amdgcn_s_sleep(SNNFLOW_SEQ_SLEEP);
+        else if (nap < 8) __builtin_amdgcn_s_sleep(4 * SNNFLOW_SEQ_SLEEP);
+        else __builtin_amdgcn_s_sleep(16 * SNNFLOW_SEQ_SLEEP > 127 ? 127 : 16 * SNNFLOW_SEQ_SLEEP);
+        ++nap;
         if (++spins > kSeqSpinLimit) {
             __hip_atomic_store(sync + kSeqSyncErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
@@ -2671,15 +2685,21 @@ __device__ inline T* uniform_ptr(T* p) {  // a wave-uniform pointer argument bac
     return (T*)(((uint64_t)hi << 32) | lo);
 }
 
+// The LDS pool of the persistent forward at namespace scope: referenced by name inside the
+// out-of-line item function, its accesses stay ds_* (a pool handed in as a pointer argument is a
+// generic pointer there: flat_* accesses, whose waits also wait for every outstanding HBM load).
+__shared__ __attribute__((aligned(16))) float g_seq_fwd_pool[SlotLds<8>::FWD];
+
 template <int C>
-__device__ __attribute__((noinline)) void seq_fwd_item(const SeqFwdParams* pg, int k, int t, int i, int q, float* pool) {
+__device__ __attribute__((noinline)) void seq_fwd_item(const SeqFwdParams* pg, int k, int t, int i, int q) {
+    static_assert(C == 8, "persistent forward: C = 8");
+    float* const pool = g_seq_fwd_pool;
     typedef const __attribute__((address_space(4))) SeqFwdParams* cptr;
     const cptr pp = (cptr)uniform_ptr(pg);
     k = __builtin_amdgcn_readfirstlane(k);
     t = __builtin_amdgcn_readfirstlane(t);
     i = __builtin_amdgcn_readfirstlane(i);
     q = __builtin_amdgcn_readfirstlane(q);
-    pool = uniform_ptr(pool);
     const int L = pp->L, nconv = pp->nconv, ntop = pp->ntop;
 #ifndef SEQV
 #define SEQV 15
@@ -2711,7 +2731,6 @@ template <int C>
 __global__ __launch_bounds__(NT * 2, 6) void k_fwd_seq(SeqFwdParams) {
     typedef const __attribute__((address_space(4))) SeqFwdParams* cptr;
     const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
-    __shared__ __attribute__((aligned(16))) float pool[SlotLds<C>::FWD];
     __shared__ int s_item;
     const int tid = threadIdx.x;
     const int T = pp->T, L = pp->L, K = L + 1, M = K + 2 * (T - 1);
@@ -2722,7 +2741,10 @@ __global__ __launch_bounds__(NT * 2, 6) void k_fwd_seq(SeqFwdParams) {
     int m = 0, t = 0, base = 0;
     auto first_t = [&](int mm) { const int lo = mm - L; return lo > 0 ? (lo + 1) / 2 : 0; };
     t = first_t(0);
+    // timing counters (wall clock, 100 MHz): grab + dependency wait, item bodies
+    unsigned long long tw = 0, ti = 0, nitems = 0;
     for (;;) {
+        const unsigned long long c0 = wall_clock64();
         if (tid == 0) s_item = __hip_atomic_fetch_add(sync + kSeqSyncHead + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         const int item = __builtin_amdgcn_readfirstlane(s_item);
@@ -2755,7 +2777,11 @@ __global__ __launch_bounds__(NT * 2, 6) void k_fwd_seq(SeqFwdParams) {
             }
         }
         __syncthreads();
-        seq_fwd_item<C>((const SeqFwdParams*)pp, k, t, i, q, pool);
+        const unsigned long long c1 = wall_clock64();
+        seq_fwd_item<C>((const SeqFwdParams*)pp, k, t, i, q);
+        tw += c1 - c0;
+        ti += wall_clock64() - c1;
+        ++nitems;
         // completion: every wave's stores and atomics acknowledged, then one count
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -2766,6 +2792,13 @@ __global__ __launch_bounds__(NT * 2, 6) void k_fwd_seq(SeqFwdParams) {
             }
             __hip_atomic_fetch_add(sync + kSeqSyncDone + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+    if (tid == 0) {  // ints [10, 18) of the sync area: (wait ticks, item ticks, blocks, items) as u64
+        unsigned long long* st = reinterpret_cast<unsigned long long*>(sync + 10);
+        __hip_atomic_fetch_add(st, tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(st + 1, ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(st + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(st + 3, nitems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

@@ -1339,7 +1339,7 @@ def test_log_activity_with_forward_hooks(dev):
     assert len(seen) == 2
 
 
-@pytest.mark.parametrize("name,H,W,T", [("LIFFireNet", 32, 32, 5), ("LIFFireNet", 64, 32, 1), ("LIFFireNet", 32, 48, 16),
+@pytest.mark.parametrize("name,H,W,T", [("LIFFireNet", 32, 32, 5), ("LIFFireNet", 64, 32, 2), ("LIFFireNet", 32, 48, 16),
                                         ("LIFFireNet_short", 32, 32, 4), ("LIFFireFlowNet", 32, 32, 3)])
 def test_persistent_forward_matches_slots(dev, monkeypatch, name, H, W, T):
     """The persistent dataflow forward (snnflow_fwd_seq: one launch, per-XCD work queues, per
