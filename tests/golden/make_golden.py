@@ -16,6 +16,7 @@ produced by reference code end to end.
 
 Outputs are small .npz files (inputs + expected outputs), nothing else.
 """
+import json
 import os
 import sys
 import types
@@ -177,6 +178,48 @@ def spiking_cells_case(ref_sub, out):
             rec[f"{tag}.z_{t}"] = outs[t].detach().numpy()
         rec[f"{tag}.v_last"] = state[0].detach().numpy()
     np.savez_compressed(os.path.join(out, "spiking_cells_case.npz"), **rec)
+
+
+# the cell options outside spiking_cells_case (other surrogates, soft reset, detach=False, stride 2)
+CELL_VARIANTS = [tuple(v) for v in json.load(open(os.path.join(HERE, "cell_variants.json")))["variants"]]
+
+
+def spiking_cell_variants_case(ref_sub, out):
+    """models/spiking_submodules.py ConvLIF / ConvLIFRecurrent for CELL_VARIANTS: 2 steps from a
+    random initial state; spikes, states and the gradients of the inputs, the initial state and
+    every parameter of loss = sum(z * wz) + 0.3 * sum(v) per step."""
+    rec = {}
+    for i, (tag, recurrent, stride, cin, C, act, width, hard, detach) in enumerate(CELL_VARIANTS):
+        torch.manual_seed(60 + i)
+        kw = dict(activation=act, act_width=width, leak=(0.0, 1.0), thresh=(0.5, 0.2), hard_reset=hard, detach=detach)
+        cell = (ref_sub.ConvLIFRecurrent(cin, C, 3, **kw) if recurrent
+                else ref_sub.ConvLIF(cin, C, 3, stride=stride, **kw))
+        gen = torch.Generator().manual_seed(70 + i)
+        B, H, W = 2, 8, 12
+        Ho, Wo = H // stride, W // stride
+        s0 = torch.randn(2, B, C, Ho, Wo, generator=gen) * 0.5
+        s0[1] = (s0[1] > 0).float()
+        s0.requires_grad_(True)
+        xs = [((torch.rand(B, cin, H, W, generator=gen) < 0.5).float() * 1.5).requires_grad_(True) for _ in range(2)]
+        state, loss = s0, 0
+        for t in range(2):
+            z, state = cell(xs[t], state)
+            wz = torch.randn(B, C, Ho, Wo, generator=gen)
+            loss = loss + (z * wz).sum() + 0.3 * state[0].sum()
+            rec[f"{tag}.x_{t}"] = xs[t].detach().numpy()
+            rec[f"{tag}.wz_{t}"] = wz.numpy()
+            rec[f"{tag}.z_{t}"] = z.detach().numpy()
+            rec[f"{tag}.state_{t}"] = state.detach().numpy()
+        loss.backward()
+        rec[f"{tag}.s0"] = s0.detach().numpy()
+        rec[f"{tag}.gs0"] = s0.grad.numpy()
+        for t in range(2):
+            rec[f"{tag}.gx_{t}"] = xs[t].grad.numpy()
+        for k, v in cell.state_dict().items():
+            rec[f"{tag}.p.{k}"] = v.numpy()
+        for n, p in cell.named_parameters():
+            rec[f"{tag}.g.{n}"] = p.grad.numpy()
+    np.savez_compressed(os.path.join(out, "spiking_cell_variants_case.npz"), **rec)
 
 
 def liffirenet_case(ref_model, ref_flow, out, name="LIFFireNet", C=4, fname=None, norm=False):
@@ -423,6 +466,12 @@ def main():
         liffirenet_case(ref_model, ref_flow, HERE, "LIFFireNet", 8, "liffirenet_norm_case.npz", norm=True)
         print("liffirenet_norm fixture written")
         return
+    if only == ["cell_variants"]:
+        import models.spiking_submodules as ref_sub_sp
+        torch.set_num_threads(1)
+        spiking_cell_variants_case(ref_sub_sp, HERE)
+        print("cell variants fixture written")
+        return
     if only == ["unet"]:
         import loss.flow as ref_flow
         import models.model as ref_model
@@ -448,6 +497,7 @@ def main():
     loss_case(ref_flow, out)
     loss_case(ref_flow, out, overwrite=True, name="loss_case_overwrite.npz")
     spiking_cells_case(ref_sub_sp, out)
+    spiking_cell_variants_case(ref_sub_sp, out)
     convlayer_case(ref_sub, out)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet", 4)
     liffirenet_case(ref_model, ref_flow, out, "LIFFireNet_short", 4)

@@ -316,3 +316,45 @@ def test_unet_cfg5_shapes_vs_oracle(dev):
         f"{n}={e_ours[n]:.1e}/{e_32[n]:.1e}" for n in sorted(e_ours, key=lambda k: -e_ours[k])[:20]))
     for n in e_ours:
         assert e_ours[n] <= max(2 * e_32[n], 2e-5), (n, e_ours[n], e_32[n])
+
+
+def _cell_variants():
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "cell_variants.json")) as f:
+        return [tuple(v) for v in json.load(f)["variants"]]
+
+
+CELL_VARIANTS = _cell_variants()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", CELL_VARIANTS, ids=[v[0] for v in CELL_VARIANTS])
+def test_convlif_variants_vs_golden(golden, dev, variant):
+    """HIP ConvLIF / ConvLIFRecurrent against the REFERENCE-generated fixture of the cell options
+    outside the default one (make_golden.py:spiking_cell_variants_case: SuperSpike, MultiGauss,
+    Triangle surrogates with their widths, soft reset, detach=False, stride 2): spikes exact, states
+    rtol 1e-5, gradients of inputs, initial state and parameters rel-L2 < 1e-4."""
+    import snnflow
+    tag, recurrent, stride, cin, C, act, width, hard, detach = variant
+    g = golden("spiking_cell_variants_case.npz")
+    kw = dict(activation=act, act_width=width, hard_reset=hard, detach=detach)
+    cell = (snnflow.ConvLIFRecurrent(cin, C, 3, **kw) if recurrent
+            else snnflow.ConvLIF(cin, C, 3, stride=stride, **kw)).to(dev)
+    cell.load_state_dict({k[len(tag) + 3:]: torch.from_numpy(v).to(dev) for k, v in g.items()
+                          if k.startswith(f"{tag}.p.")})
+    s0 = torch.from_numpy(g[f"{tag}.s0"]).to(dev).requires_grad_(True)
+    xs = [torch.from_numpy(g[f"{tag}.x_{t}"]).to(dev).requires_grad_(True) for t in range(2)]
+    state, loss = s0, 0
+    for t in range(2):
+        z, state = cell(xs[t], state)
+        np.testing.assert_array_equal(z.detach().cpu().numpy(), g[f"{tag}.z_{t}"])
+        np.testing.assert_allclose(state.detach().cpu().numpy(), g[f"{tag}.state_{t}"], rtol=1e-5, atol=1e-5)
+        loss = loss + (z * torch.from_numpy(g[f"{tag}.wz_{t}"]).to(dev)).sum() + 0.3 * state[0].sum()
+    loss.backward()
+    errs = {"state0": _rel(s0.grad.cpu().numpy(), g[f"{tag}.gs0"])}
+    errs.update({f"x{t}": _rel(xs[t].grad.cpu().numpy(), g[f"{tag}.gx_{t}"]) for t in range(2)})
+    errs.update({n: _rel(p.grad.cpu().numpy(), g[f"{tag}.g.{n}"]) for n, p in cell.named_parameters()})
+    print(f"\n[variant {tag}] " + ", ".join(f"{k}={v:.1e}" for k, v in errs.items()))
+    for n, e in errs.items():
+        assert e < 1e-4, (n, e)
