@@ -7,6 +7,7 @@
 //   w = pos + ((tref - ts_k) * f) * s    ts_k = ts + k (f32), no FMA (-ffp-contract=off)
 //   y0 = floor(wy), y1 = floor(wy + 1)    (not floor(wy) + 1)
 //   idx = (cy*inb)*W + cx*inb computed in f32
+#include <type_traits>
 #include <cmath>
 
 #include "snnflow_dev.h"
@@ -68,49 +69,124 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 // every event of its sample, adds the bilinear corners that fall into the band with LDS
 // atomics, then writes the band once (no memset, no global atomics).
 // images layout: [dir 2][img 4][B][HW].
-// Events of a sample are dealt to SPLAT_SPLIT blocks per band; each writes its own partial
-// image set (images + split * 8*B*HW), summed in fixed order by k_iwe_loss.
+// Events of a sample are dealt to nsplit <= SPLAT_SPLIT blocks per band (splat_nsplit: as many as
+// fill the chip once); each writes its own partial image set (images + split * 8*B*HW), summed in
+// fixed order by k_iwe_loss.
+// Deterministic accumulation (SNNFLOW_SPLAT_FIXED, default): every corner contribution v is split
+// exactly into two 64-bit fixed-point integers, v = H 2^-32 + L 2^-75 (H = rint(v 2^32) in double,
+// L = rint((v - H 2^-32) 2^75): exact for |v| >= 2^-51), and the two are added with integer LDS
+// atomics.  Integer addition is associative, so the band totals -- the whole IWE -- are the same
+// bits on every run whatever order the events' atomics land in, and they are the exact sums of the
+// fp32 contributions (rounded once to fp32 at the end).  Two words because the loss reads ratios
+// (ts image / count image, loss/flow.py:219-233) that do not shrink with the weights: a pixel hit
+// only by a 1e-7 corner still contributes ts^2 to the loss, so the fraction needs relative, not
+// absolute, precision.  Range: |sum| < 2^31 per pixel and image.  (0: fp32 LDS atomics,
+// order-dependent rounding.)
+#ifndef SNNFLOW_SPLAT_FIXED
+#define SNNFLOW_SPLAT_FIXED 1
+#endif
 #ifndef SNNFLOW_SPLAT_SPLIT
 #define SNNFLOW_SPLAT_SPLIT 4
 #endif
-constexpr int SPLAT_NT = 1024, SPLAT_BAND = 4096, SPLAT_SPLIT = SNNFLOW_SPLAT_SPLIT;
+constexpr bool kSplatFixed = SNNFLOW_SPLAT_FIXED != 0;
+constexpr int SPLAT_NT = 1024, SPLAT_BAND = kSplatFixed ? 2048 : 4096, SPLAT_SPLIT = SNNFLOW_SPLAT_SPLIT;
 
-__global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands) {
-    __shared__ float img[4][SPLAT_BAND];
+struct SplatLdsF {  // fp32 images
+    float v[4][SPLAT_BAND];
+    __device__ void zero(int tid) { for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&v[0][0])[j] = 0.0f; }
+    __device__ void add(int q, int i, float x) { atomicAdd(&v[q][i], x); }
+    __device__ float get(int q, int i) const { return v[q][i]; }
+};
+struct SplatLdsX {  // exact two-word fixed point
+    unsigned long long hi[4][SPLAT_BAND], lo[4][SPLAT_BAND];
+    __device__ void zero(int tid) {
+        for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&hi[0][0])[j] = 0, (&lo[0][0])[j] = 0;
+    }
+    __device__ void add(int q, int i, float x) {
+        const double d = (double)x;
+        const double h = rint(d * 0x1p32);               // exact: x has 24 significant bits
+        const double r = d - h * 0x1p-32;                // exact, |r| <= 2^-33
+        const long long l = (long long)rint(r * 0x1p75);
+        atomicAdd(&hi[q][i], (unsigned long long)(long long)h);
+        if (l != 0) atomicAdd(&lo[q][i], (unsigned long long)l);  // zero for every |x| >= 2^-9
+    }
+    __device__ float get(int q, int i) const {
+        return (float)((double)(long long)hi[q][i] * 0x1p-32 + (double)(long long)lo[q][i] * 0x1p-75);
+    }
+};
+typedef std::conditional_t<kSplatFixed, SplatLdsX, SplatLdsF> SplatLds;
+
+// Events per thread and pass: their loads (event, polarity, then the flow gather) are all issued
+// before any of them is splatted, so a thread waits for one chain of dependent loads per SPLAT_U
+// events instead of per event.
+constexpr int SPLAT_U = 4;
+
+// Partial image sets per band: enough blocks for one per CU (256), at most SPLAT_SPLIT.
+__host__ __device__ inline int splat_nsplit(int B, int nbands) {
+    const int base = B * 2 * nbands, s = (256 + base - 1) / base;
+    return s < 1 ? 1 : (s > SPLAT_SPLIT ? SPLAT_SPLIT : s);
+}
+
+__global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands, int nsplit) {
+    __shared__ SplatLds img;
     const int tid = threadIdx.x;
     const int blk = xcd_block();
-    const int split = blk % SPLAT_SPLIT, rest = blk / SPLAT_SPLIT;
+    const int split = blk % nsplit, rest = blk / nsplit;
     const int band = rest % nbands, d = (rest / nbands) % 2, b = rest / (2 * nbands);
     const int64_t HWp = (int64_t)a.H * a.W, imgsz = (int64_t)a.B * HWp;
     const int p0 = band * SPLAT_BAND;
     const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
-    for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&img[0][0])[j] = 0.0f;
+    img.zero(tid);
     __syncthreads();
     const float tref = d == 0 ? (float)a.T : 0.0f;
-    for (int i = split * SPLAT_NT + tid; i < a.M; i += SPLAT_SPLIT * SPLAT_NT) {
-        const EventRef r = event_ref(a, b, i);
-        const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
-        const float pm0 = r.pol[0], pm1 = r.pol[1];
-        const int pix = (int)(y * (float)a.W + x);
-        const float* fl = flow_of(a, b, a.tf == 1 ? 0 : r.k);
-        const float fy = fl[HWp + pix], fx = fl[pix];
-        const float tsw = d == 0 ? ts : (float)a.T - ts;
-        Corner c[4];
-        float wy, wx;
-        warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+    const int stride = nsplit * SPLAT_NT;
+    for (int i0 = split * SPLAT_NT + tid; i0 < a.M; i0 += SPLAT_U * stride) {
+        float4 ev[SPLAT_U];
+        float2 pm[SPLAT_U];
+        int kk[SPLAT_U];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float wt = c[q].wt;
-            const int li = c[q].idx - p0;
-            if (wt == 0.0f || li < 0 || li >= np) continue;
-            const float wts = wt * tsw;
-            if (pm0 != 0.0f) {
-                atomicAdd(&img[0][li], wt * pm0);
-                atomicAdd(&img[2][li], wts * pm0);
+        for (int u = 0; u < SPLAT_U; ++u) {
+            const int i = i0 + u * stride;
+            kk[u] = -1;
+            if (i < a.M) {
+                const EventRef r = event_ref(a, b, i);
+                ev[u] = *reinterpret_cast<const float4*>(r.ev);
+                pm[u] = *reinterpret_cast<const float2*>(r.pol);
+                kk[u] = r.k;
             }
-            if (pm1 != 0.0f) {
-                atomicAdd(&img[1][li], wt * pm1);
-                atomicAdd(&img[3][li], wts * pm1);
+        }
+        float fy[SPLAT_U], fx[SPLAT_U];
+#pragma unroll
+        for (int u = 0; u < SPLAT_U; ++u) {
+            if (kk[u] < 0) continue;
+            const int pix = (int)(ev[u].y * (float)a.W + ev[u].z);
+            const float* fl = flow_of(a, b, a.tf == 1 ? 0 : kk[u]);
+            fy[u] = fl[HWp + pix];
+            fx[u] = fl[pix];
+        }
+#pragma unroll
+        for (int u = 0; u < SPLAT_U; ++u) {
+            if (kk[u] < 0) continue;
+            const float ts = ev[u].x + (float)kk[u], y = ev[u].y, x = ev[u].z;
+            const float pm0 = pm[u].x, pm1 = pm[u].y;
+            const float tsw = d == 0 ? ts : (float)a.T - ts;
+            Corner c[4];
+            float wy, wx;
+            warp4(ts, y, x, fy[u], fx[u], tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float wt = c[q].wt;
+                const int li = c[q].idx - p0;
+                if (wt == 0.0f || li < 0 || li >= np) continue;
+                const float wts = wt * tsw;
+                if (pm0 != 0.0f) {
+                    img.add(0, li, wt * pm0);
+                    img.add(2, li, wts * pm0);
+                }
+                if (pm1 != 0.0f) {
+                    img.add(1, li, wt * pm1);
+                    img.add(3, li, wts * pm1);
+                }
             }
         }
     }
@@ -118,7 +194,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
     float* out = a.images + (int64_t)split * 8 * imgsz + (int64_t)d * 4 * imgsz + (int64_t)b * HWp + p0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        for (int j = tid; j < np; j += SPLAT_NT) out[(int64_t)q * imgsz + j] = img[q][j];
+        for (int j = tid; j < np; j += SPLAT_NT) out[(int64_t)q * imgsz + j] = img.get(q, j);
 }
 
 __device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
@@ -139,7 +215,7 @@ __host__ __device__ inline int loss_tsplit(int B, int64_t HWp, int tf) {
     return s < 1 ? 1 : (s > tf ? tf : (int)s);
 }
 
-__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit) {
+__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit, int nsplit) {
     __shared__ float red[NT / 64][LOSS_NV];
     const int blk = xcd_block();
     const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
@@ -159,8 +235,7 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     float v0 = base[q * img];
-#pragma unroll
-                    for (int sp = 1; sp < SPLAT_SPLIT; ++sp) v0 += base[(int64_t)sp * 8 * img + q * img];
+                    for (int sp = 1; sp < nsplit; ++sp) v0 += base[(int64_t)sp * 8 * img + q * img];
                     q4[q] = v0;
                 }
 #pragma unroll
@@ -556,9 +631,10 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
     const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
-    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands * SPLAT_SPLIT), dim3(SPLAT_NT), 0, s, *a, nbands);
+    const int nsplit = splat_nsplit(a->B, nbands);
+    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands * nsplit), dim3(SPLAT_NT), 0, s, *a, nbands, nsplit);
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
-    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit);
+    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit, nsplit);
     hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, tsplit * chunks);
     SNN_CHECK_LAUNCH();
     return 0;

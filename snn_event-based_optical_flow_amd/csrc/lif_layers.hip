@@ -2005,9 +2005,19 @@ struct WbGeo {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// C = 32 feed-forward weight gradients without the register prefetch of the next step (A/B):
+// <= 128 VGPRs, two blocks per CU (66 KB LDS), so the 512-tile grid of cfg2 is one round and the
+// other block's math covers a block's loads.
+#ifndef SNNFLOW_WG32_PF
+#define SNNFLOW_WG32_PF 1
+#endif
 template <int C, bool REC>
-__global__ __launch_bounds__(NT * 2) void k_wgrad_bf(snnflow_wgrad_args) {
+constexpr bool kWgPf = !(C == 32 && !REC && !SNNFLOW_WG32_PF);
+
+template <int C, bool REC>
+__global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(snnflow_wgrad_args) {
     using Gm = WbGeo<C, REC>;
+    constexpr bool PF = kWgPf<C, REC>;
     constexpr int NTB = NT * 2, NW = NTB / 64, Q = C / 4;
     constexpr int RX = Halo4<C, NTB>::R;
     using O = Own4<C, NTB>;
@@ -2083,9 +2093,10 @@ __global__ __launch_bounds__(NT * 2) void k_wgrad_bf(snnflow_wgrad_args) {
 #pragma unroll
     for (int j = 0; j < Gm::TPW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    issue(0);
+    if constexpr (PF) issue(0);
     __syncthreads();  // coef
     for (int t = 0; t < nsteps; ++t) {
+        if constexpr (!PF) issue(t);
         // stage step t: G^T (BN backward of g_cur, zero outside the image), X^T, S^T
 #pragma unroll
         for (int i = 0; i < O::R; ++i) {
@@ -2129,7 +2140,11 @@ __global__ __launch_bounds__(NT * 2) void k_wgrad_bf(snnflow_wgrad_args) {
             }
         }
         __syncthreads();
-        if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
+        if constexpr (PF) {
+        if constexpr (PF) {
+            if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
+        }
+        }
 
         // compute: this wave's tile rows r = rg, rg + RG, ...
 #pragma unroll

@@ -1389,3 +1389,41 @@ def test_persistent_forward_matches_slots(dev, monkeypatch, name, H, W, T):
                                    rtol=1e-6, atol=1e-7)
     for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
         assert _rel(a.grad.cpu().numpy(), b.grad.cpu().numpy()) < 1e-5, n
+
+
+def test_iwe_loss_bit_reproducible(dev):
+    """The IWE splat accumulates in 64-bit fixed point (csrc/iwe_loss.hip, SNNFLOW_SPLAT_FIXED):
+    the loss is the same bits on every run even where hundreds of events pile onto a few pixels
+    (LDS atomics landing in a different order each run), and matches the oracle (fp32 sequential
+    index_put_, loss/flow.py:178-303) to rtol 1e-5."""
+    import snnflow
+    from oracle import iwe_ref
+
+    H, W, B, N, T = 64, 64, 4, 6000, 3
+    gen = torch.Generator().manual_seed(77)
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    wins = []
+    for t in range(T):
+        # events crowded onto a 6x6 patch: ~40 events and up to 4 corners per pixel per window
+        ys = torch.randint(20, 26, (B, N), generator=gen).float()
+        xs = torch.randint(30, 36, (B, N), generator=gen).float()
+        ts = torch.sort(torch.rand(B, N, generator=gen), dim=1).values
+        ps = torch.randint(0, 2, (B, N), generator=gen).float() * 2 - 1
+        ev = torch.stack([ts, ys, xs, ps], dim=2)
+        pol = torch.stack([(ps > 0).float(), (ps < 0).float()], dim=2)
+        mask = torch.zeros(B, 1, H, W)
+        mask[:, :, 20:26, 30:36] = 1
+        flow = (torch.rand(B, 2, H, W, generator=gen) - 0.5) * 0.05
+        wins.append((ev, pol, mask, flow))
+    losses = []
+    for rep in range(5):
+        lf = snnflow.EventWarping(cfg, dev)
+        for ev, pol, mask, flow in wins:
+            lf.event_flow_association([flow.to(dev)], ev.to(dev), pol.to(dev), mask.to(dev))
+        losses.append(lf().item())
+    assert all(v == losses[0] for v in losses), losses
+    rl = iwe_ref.EventWarpingRef([H, W])
+    for ev, pol, mask, flow in wins:
+        rl.event_flow_association([flow], ev, pol, mask)
+    np.testing.assert_allclose(losses[0], rl().item(), rtol=1e-5)
