@@ -610,24 +610,32 @@ def cpu_baseline_unet(args, windows):
     opt = torch.optim.Adam(model.parameters(), lr=2e-4)
     R, nw = args.res, 2
     cpu_w = [{k: v[:1].cpu() for k, v in w.items()} for w in windows[:nw]]
-    t0 = time.perf_counter()
-    flows = []
-    for w in cpu_w:
-        flows.append(model(None, w["event_cnt"])["flow"])
-    loss = 0
-    for i in range(4):
-        lf = iwe_ref.EventWarpingRef([R, R])
-        for t, w in enumerate(cpu_w):
-            lf.event_flow_association([flows[t][i]], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
-        loss = loss + lf()
-    (loss / 4).backward()
-    torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
-    opt.step()
+
+    def step():
+        flows = [model(None, w["event_cnt"])["flow"] for w in cpu_w]
+        loss = 0
+        for i in range(4):
+            lf = iwe_ref.EventWarpingRef([R, R])
+            for t, w in enumerate(cpu_w):
+                lf.event_flow_association([flows[t][i]], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            loss = loss + lf()
+        opt.zero_grad(set_to_none=True)
+        (loss / 4).backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        model.reset_states()
+
+    step()  # warm-up (first-touch allocations)
+    n, t0 = 0, time.perf_counter()
+    while n == 0 or time.perf_counter() - t0 < 10.0:
+        step()
+        n += 1
     dt = time.perf_counter() - t0
-    ev = nw * args.events
+    ev = n * nw * args.events
     return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "cpu_model": _cpu_model(),
             "threads_note": _THREADS_NOTE, "kind": "port",
-            "sample": f"1 train step of 1 sample x {nw} windows of {args.events} events, {R}x{R}, base {args.channels}; "
+            "sample": f"{n} timed train steps (after 1 warm-up) of 1 sample x {nw} windows of {args.events} events, "
+                      f"{R}x{R}, base {args.channels}; "
                       f"oracle/unet_ref.py (CPU restatement of the reference U-Net), {threads} threads",
             "seconds": round(dt, 3)}
 

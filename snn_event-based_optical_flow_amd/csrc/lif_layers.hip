@@ -2011,6 +2011,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef SNNFLOW_WG32_PF
 #define SNNFLOW_WG32_PF 1
 #endif
+#ifndef SNNFLOW_WG32_SPLIT
+#define SNNFLOW_WG32_SPLIT 1  // C = 32: k_wgrad_bf32 (two blocks per CU) for feed-forward layers (2: recurrent too)
+#endif
 template <int C, bool REC>
 constexpr bool kWgPf = !(C == 32 && !REC && !SNNFLOW_WG32_PF);
 
@@ -2246,6 +2249,223 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
                     *d = accumulate ? *d + v[r4] : v[r4];
                 }
             }
+    }
+}
+
+// C = 32 weight gradients at two blocks per CU (k_wgrad_bf<32> needs 212-244 VGPRs, one block per
+// CU, so the 512-tile grid of cfg2 took two rounds).  Same arithmetic and slab layout as
+// k_wgrad_bf; what changes is the split of the work and the staging:
+//   * wave w: output tiles of (ci-tile nt = w & 1, co-tile mt = (w >> 1) & 1) -- all 3 x 3 taps,
+//     per source 9 accumulator tiles (36 VGPRs) and ONE co-tile's A fragments (hi/mid/lo, 12
+//     VGPRs) -- over the tile rows r = (w >> 2) + 2 i (two row groups, summed in LDS at the end);
+//   * no next-step loads held in registers: each step's G / y / x loads are issued and stored to LDS
+//     in batches (the other resident block's math covers them);
+//   * recurrent cells stage S into the X buffer after the X pass (one X buffer: G^T 33 KB + X^T 26 KB
+//     + BN coefficients 20 KB = 80 KB of LDS, two blocks per CU; <= 128 VGPRs).
+// ---------------------------------------------------------------------------
+template <bool REC>
+__global__ __launch_bounds__(NT * 2, 4) void k_wgrad_bf32(snnflow_wgrad_args) {
+    constexpr int C = 32, NTB = NT * 2, Q = C / 4;
+    constexpr int GS = NT + 4, XS = 10 * 40 + 8;
+    constexpr int RX = Halo4<C, NTB>::R;
+    using O = Own4<C, NTB>;
+    constexpr int NS = REC ? 2 : 1;      // sources: x (ff conv), s_prev (rec conv)
+    constexpr int GF = C * GS, XF = C * XS / 2;
+    constexpr int RF = 4 * 9 * 256;      // one source's row-group exchange [4 tg][9][64][4]
+    static_assert(RF <= GF + XF, "exchange fits the staging pool");
+    __shared__ __attribute__((aligned(16))) float pool[GF + XF];
+    float* const Gt = pool;
+    unsigned short* const Xt = reinterpret_cast<unsigned short*>(pool + GF);
+    __shared__ BnBwdLds coef[SNNFLOW_MAX_WGRAD_STEPS][C];
+
+    const cwgrad_ptr ap = (cwgrad_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+    const int tid = threadIdx.x, lane = tid & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nt = wv & 1, mt = (wv >> 1) & 1, rg = wv >> 2;
+    const int H = ap->H, W = ap->W, nsteps = ap->nsteps;
+    const Tile tl = block_tile(H, W);
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    for (int e = tid; e < nsteps * C; e += NTB) {
+        const int t = e / C, c = e - t * C;
+        const float* st = ap->steps[t].stats;
+        const float* bc = ap->steps[t].bnc;
+        BnBwdLds k = {0.f, 1.f, 0.f, 0.f, 1.f};
+        if (st) {
+            k.mean = st[c];
+            k.inv = st[C + c];
+            k.gm = bc[c];
+            k.k = bc[C + c];
+            k.w = ap->bn_weight[c];
+        }
+        coef[t][c] = k;
+    }
+
+    // halo float4 element (pixel p, quad q) -> 4 bf16 of the channel-major tile
+    auto put_halo = [&](int e, const float4& v) {
+        const int p = e / Q, q = e - p * Q;
+        const int hr = p / HWD, hc = p - hr * HWD;
+        unsigned short* d = Xt + (4 * q) * XS + hr * 40 + hc;
+        d[0] = __builtin_bit_cast(unsigned short, (__bf16)v.x);
+        d[XS] = __builtin_bit_cast(unsigned short, (__bf16)v.y);
+        d[2 * XS] = __builtin_bit_cast(unsigned short, (__bf16)v.z);
+        d[3 * XS] = __builtin_bit_cast(unsigned short, (__bf16)v.w);
+    };
+    // the conv input of step t (x or s_prev) into X^T: dense NHWC halo, or an element-wise gather
+    auto stage_x = [&](const float* src, int64_t sb, int64_t sc, int64_t sh, int64_t sw, bool dense) {
+        if (dense) {  // two batches of loads (12 VGPRs each: the accumulators stay live)
+            constexpr int RH = (RX + 1) / 2;
+#pragma unroll
+            for (int h2 = 0; h2 < RX; h2 += RH) {
+                float4 rx[RH];
+#pragma unroll
+                for (int i = 0; i < RH; ++i) {
+                    const int e = tid + (h2 + i) * NTB;
+                    const int64_t k = (h2 + i) < RX && e < Halo4<C, NTB>::E ? halo_idx4<C>(e, tl, H, W) : -1;
+                    rx[i] = k >= 0 ? reinterpret_cast<const float4*>(src)[k] : z4;
+                }
+#pragma unroll
+                for (int i = 0; i < RH; ++i) {
+                    const int e = tid + (h2 + i) * NTB;
+                    if ((h2 + i) < RX && e < Halo4<C, NTB>::E) put_halo(e, rx[i]);
+                }
+            }
+        } else {
+            for (int e = tid; e < HN * C; e += NTB) {
+                const int p = e / C, c = e - p * C;
+                const int hr = p / HWD, hc = p - hr * HWD;
+                const int h = tl.h0 + hr - 1, w = tl.w0 + hc - 1;
+                const float v = in_image(h, w, H, W) ? src[tl.b * sb + c * sc + h * sh + w * sw] : 0.f;
+                Xt[c * XS + hr * 40 + hc] = __builtin_bit_cast(unsigned short, (__bf16)v);
+            }
+        }
+    };
+
+    f32x4 acc[NS][9];
+#pragma unroll
+    for (int sidx = 0; sidx < NS; ++sidx)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc[sidx][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // one source's MFMAs of the staged step: rows r = rg, rg + 2, ..., 9 taps of (nt, mt)
+    auto compute = [&](f32x4 (&d)[9]) {
+#pragma unroll 1
+        for (int r = rg; r < TH; r += 2) {
+            bf16x8 ah, am, al;
+            {
+                const int co = mt * 16 + m;
+                const float* src = Gt + co * GS + r * TW + 8 * g;
+                const float4 u = *reinterpret_cast<const float4*>(src), v = *reinterpret_cast<const float4*>(src + 4);
+                const float a8[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const __bf16 h = (__bf16)a8[j];
+                    const float r1 = a8[j] - (float)h;
+                    const __bf16 md = (__bf16)r1;
+                    ah[j] = h;
+                    am[j] = md;
+                    al[j] = (__bf16)(r1 - (float)md);
+                }
+            }
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                const unsigned short* T = Xt + (nt * 16 + m) * XS + (r + ky) * 40 + 8 * g;
+                const u32x4 u = *reinterpret_cast<const u32x4*>(T);
+                const uint2 v = *reinterpret_cast<const uint2*>(T + 8);
+                const unsigned int w6[5] = {u.x, u.y, u.z, u.w, v.x};
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    u32x4 bw;
+                    if (kx == 0) bw = u32x4{w6[0], w6[1], w6[2], w6[3]};
+                    else if (kx == 2) bw = u32x4{w6[1], w6[2], w6[3], w6[4]};
+                    else bw = u32x4{__builtin_amdgcn_alignbit(w6[1], w6[0], 16), __builtin_amdgcn_alignbit(w6[2], w6[1], 16),
+                                    __builtin_amdgcn_alignbit(w6[3], w6[2], 16), __builtin_amdgcn_alignbit(w6[4], w6[3], 16)};
+                    const bf16x8 b = __builtin_bit_cast(bf16x8, bw);
+                    f32x4& o = d[ky * 3 + kx];
+                    o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, o, 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    __syncthreads();  // coef
+    for (int t = 0; t < nsteps; ++t) {
+        const auto& sp = ap->steps[t];
+        // G^T = BN backward of g_cur (zero outside the image), two batches of loads
+#pragma unroll
+        for (int h2 = 0; h2 < O::R; h2 += 2) {
+            float4 rg4[2], ry4[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int e = tid + (h2 + i) * NTB;
+                const int p = e / Q, q = e - p * Q;
+                const int ty = p / TW, tx = p - ty * TW;
+                const int h = tl.h0 + ty, w = tl.w0 + tx;
+                const bool ok = e < O::E && h < H && w < W;
+                const int64_t k = ok ? (((int64_t)tl.b * H + h) * W + w) * Q + q : 0;
+                rg4[i] = ok ? reinterpret_cast<const float4*>(sp.g_cur)[k] : z4;
+                ry4[i] = ok ? reinterpret_cast<const float4*>(sp.y)[k] : z4;
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int e = tid + (h2 + i) * NTB;
+                if (e < O::E) {
+                    const int p = e / Q, q = e - p * Q;
+                    const int ty = p / TW, tx = p - ty * TW;
+                    const bool img = tl.h0 + ty < H && tl.w0 + tx < W;
+                    const float4 gv = img ? bn_bwd4(rg4[i], ry4[i], &coef[t][4 * q]) : z4;
+                    float* d = Gt + (4 * q) * GS + p;
+                    d[0] = gv.x;
+                    d[GS] = gv.y;
+                    d[2 * GS] = gv.z;
+                    d[3 * GS] = gv.w;
+                }
+            }
+        }
+        const bool dense = sp.xs_c == 1 && sp.xs_w == C && sp.xs_h == (int64_t)W * C && sp.xs_b == (int64_t)H * W * C;
+        stage_x(sp.x, sp.xs_b, sp.xs_c, sp.xs_h, sp.xs_w, dense);
+        __syncthreads();
+        compute(acc[0]);
+        if constexpr (REC) {
+            if (sp.s_prev != nullptr) {
+                __syncthreads();  // X^T reads done
+                stage_x(sp.s_prev, 0, 0, 0, 0, true);
+                __syncthreads();
+                compute(acc[NS - 1]);
+            }
+        }
+        __syncthreads();  // before the next step overwrites the tiles
+    }
+
+    // row group 1 adds into row group 0 through LDS (fixed order), one source at a time
+    const int64_t blk = blockIdx.x;
+    const int accumulate = ap->accumulate;
+    float* red = pool;
+    const int tg = wv & 3;
+#pragma unroll
+    for (int sidx = 0; sidx < NS; ++sidx) {
+        if (rg == 1) {
+#pragma unroll
+            for (int j = 0; j < 9; ++j) *reinterpret_cast<f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4) = acc[sidx][j];
+        }
+        __syncthreads();
+        if (rg == 0) {
+            float* slab = (sidx == 0 ? ap->slab_ff : ap->slab_rec) + blk * (C * C * 9);
+            const int ci = nt * 16 + m;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const f32x4 v = acc[sidx][j] + *reinterpret_cast<const f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4);
+#pragma unroll
+                for (int r4 = 0; r4 < 4; ++r4) {
+                    const int co = mt * 16 + 4 * g + r4;
+                    float* d = slab + ((int64_t)co * C + ci) * 9 + j;
+                    *d = accumulate ? *d + v[r4] : v[r4];
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -3350,8 +3570,16 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
             if (a->rec) hipLaunchKernelGGL((k_wgrad_bf<16, true>), grid, blk, 0, s, *a);
             else hipLaunchKernelGGL((k_wgrad_bf<16, false>), grid, blk, 0, s, *a);
         } else {
-            if (a->rec) hipLaunchKernelGGL((k_wgrad_bf<32, true>), grid, blk, 0, s, *a);
-            else hipLaunchKernelGGL((k_wgrad_bf<32, false>), grid, blk, 0, s, *a);
+            // feed-forward layers: k_wgrad_bf32 (two blocks per CU: 197 -> 164 us per cfg2 layer);
+            // recurrent ones keep k_wgrad_bf (the split form's second staging pass measured 296 -> 315 us)
+            if (a->rec) {
+                if (SNNFLOW_WG32_SPLIT > 1) hipLaunchKernelGGL((k_wgrad_bf32<true>), grid, blk, 0, s, *a);
+                else hipLaunchKernelGGL((k_wgrad_bf<32, true>), grid, blk, 0, s, *a);
+            } else if (SNNFLOW_WG32_SPLIT) {
+                hipLaunchKernelGGL((k_wgrad_bf32<false>), grid, blk, 0, s, *a);
+            } else {
+                hipLaunchKernelGGL((k_wgrad_bf<32, false>), grid, blk, 0, s, *a);
+            }
         }
         SNN_CHECK_LAUNCH();
         return 0;

@@ -417,6 +417,205 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
         }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same implicit GEMM for exact-in-bf16 inputs (XPARTS = 1) with its operands brought in by
+// LDS-DMA (gfx950 global_load_lds_dwordx4 / buffer_load_dwordx4 ... lds): every k-step's X and W
+// tiles go from global memory straight into one of NSTAGE LDS buffers, NSTAGE - 1 k-steps ahead of
+// the MFMAs that read them -- no registers hold them in flight and there is no LDS store phase, so
+// one barrier per k-step and a two-step lookahead replace the register-staged single-step pipeline.
+// LDS rows are 64 B (32 bf16) with the four 16-B pieces of row n XOR-swizzled by (n >> 2) & 3, so the
+// 16 lanes of a ds_read_b128 phase (16 consecutive rows, one piece) hit 16 distinct bank groups;
+// the swizzle is applied on the load side (lane writes slot (n, s) with piece s ^ swz(n)).
+// X pixels outside the input (padding, transposed-conv holes) come from a buffer load whose offset
+// lies past the segment's extent: zeros.
+// ---------------------------------------------------------------------------------------------
+template <int N>
+__device__ inline void wait_vm() {  // s_waitcnt vmcnt(N), the other counters untouched
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ inline int swz(int n) { return (n >> 2) & 3; }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int WMT, int WAVES_M, int NSTAGE>
+__global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a) {
+    using G = ConvGeo<WMT, WAVES_M, 1>;
+    constexpr int BM = G::BM, BN = G::BN;
+    constexpr int XB = BN * 64;                   // X tile bytes: BN rows x 32 bf16
+    constexpr int WSL = 3 * BM * 4;               // W 16-B slots: 3 parts x BM rows x 4 pieces
+    constexpr int LW = (WSL / 64 + 3) / 4;        // W wave-loads per wave (uniform; tail slots are dummies)
+    constexpr int LX = BN / 64;                   // X wave-loads per wave (4 BN slots / 64 lanes / 4 waves)
+    constexpr int LPS = LX + LW;                  // loads per wave and k-step
+    constexpr int WB = 4 * LW * 1024;
+    constexpr int SB = XB + WB;
+    static_assert(4 * LW * 64 >= WSL, "W slots");
+    __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * SB];
+
+    const int tid = threadIdx.x, lane = tid & 63, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+    const PixDom dom = pix_dom(a);
+    const int P = dom.P;
+    const int mtiles = (a.M + BM - 1) / BM, ntiles = (P + BN - 1) / BN, ntc = mtiles * ntiles;
+    const int ksplit = a.ksplit > 1 ? a.ksplit : 1;
+    const int tl = xcd_remap(blockIdx.x, ntc * ksplit);
+    const int split = tl / ntc, t = tl - split * ntc;
+    const int m0 = (t % mtiles) * BM, n0 = (t / mtiles) * BN;
+    const int ks = a.ksize, pad = ks / 2;
+    const int taps = dom.nty * dom.ntx;
+    const int64_t wpart = (int64_t)ks * ks * a.kct * a.mpad * 32;
+
+    // this lane's X slots: wave-load j = wave * LX + i, slot e = 64 j + lane -> tile row e >> 2, slot e & 3
+    int pb[LX], py[LX], px[LX], xq[LX];
+    bool pv[LX];
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+        const int e = (wave * LX + i) * 64 + lane, r = e >> 2;
+        const int n = n0 + r;
+        pv[i] = n < P;
+        dom_pix(dom, pv[i] ? n : 0, pb[i], py[i], px[i]);
+        xq[i] = (e & 3) ^ swz(r);
+    }
+    // W slots: wave-load j = wave * LW + i, slot e -> part, row, piece (dummy slots reload slot 0)
+    int wofs[LW];
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+        int e = (wave * LW + i) * 64 + lane;
+        if (e >= WSL) e = 0;
+        const int part = e / (BM * 4), rem = e - part * (BM * 4), rr = rem >> 2;
+        wofs[i] = (m0 + rr) * 32 + (((rem & 3) ^ swz(rr)) * 8);
+        wofs[i] |= part << 28;  // part in the top bits (offsets < 2^28 elements per part row block)
+    }
+
+    int nits[SNNFLOW_UNET_MAX_SEGS];
+    int ftot = 0;
+#pragma unroll
+    for (int k = 0; k < SNNFLOW_UNET_MAX_SEGS; ++k) {
+        nits[k] = k < a.nseg ? taps * (a.seg[k].cpitch >> 5) : 0;
+        ftot += nits[k];
+    }
+    const int f0 = (int)((int64_t)ftot * split / ksplit), f1 = (int)((int64_t)ftot * (split + 1) / ksplit);
+    auto locate = [&](int f, int& k, int& ti, int& kc) {
+        k = 0;
+#pragma unroll
+        for (int i = 0; i < SNNFLOW_UNET_MAX_SEGS - 1; ++i)
+            if (k == i && f >= nits[i]) {
+                f -= nits[i];
+                k = i + 1;
+            }
+        const int nkc = seg_at(a, k).cpitch >> 5;
+        ti = f / nkc;
+        kc = f - ti * nkc;
+    };
+    // the LPS loads of flat k-step f into stage buffer b
+    auto issue = [&](int f, int b) {
+        int k, ti, kc;
+        locate(f, k, ti, kc);
+        const snnflow_unet_seg sg = seg_at(a, k);
+        const int ty_ = ti / dom.ntx;
+        const int ky = dom.ky0 + dom.kst * ty_, kx = dom.kx0 + dom.kst * (ti - ty_ * dom.ntx);
+        const int tap = ky * ks + kx;
+        const int mode = sg.mode, H = sg.H, W = sg.W, cp = sg.cpitch;
+        const uint32_t extent = (uint32_t)((int64_t)a.B * H * W * cp * 2);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(sg.x), (short)0, (int)extent, 0x00020000);
+        char* const sb = lds + b * SB;
+#pragma unroll
+        for (int i = 0; i < LX; ++i) {
+            int iy, ix;
+            bool ok = pv[i];
+            if (mode == SNNFLOW_UNET_MODE_S1) {
+                iy = py[i] + ky - pad;
+                ix = px[i] + kx - pad;
+            } else if (mode == SNNFLOW_UNET_MODE_S2) {
+                iy = 2 * py[i] + ky - pad;
+                ix = 2 * px[i] + kx - pad;
+            } else {
+                const int tyy = py[i] + pad - ky, txx = px[i] + pad - kx;
+                ok = ok && tyy >= 0 && txx >= 0 && ((tyy | txx) & 1) == 0;
+                iy = tyy >> 1;
+                ix = txx >> 1;
+            }
+            ok = ok && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const uint32_t off =
+                ok ? (uint32_t)(((((int64_t)pb[i] * H + iy) * W + ix) * cp + kc * 32 + xq[i] * 8) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(sb + (wave * LX + i) * 1024), 16, off, 0, 0, 0);
+        }
+        const int np = sg.nparts;
+        const uint16_t* wb = a.w + ((int64_t)(tap * a.kct + sg.kc0 + kc) * a.mpad) * 32;
+#pragma unroll
+        for (int i = 0; i < LW; ++i) {
+            int part = (int)((uint32_t)wofs[i] >> 28);
+            if (part >= np) part = 0;  // unused part of this segment: a harmless duplicate load
+            const uint16_t* src = wb + part * wpart + (wofs[i] & 0x0fffffff);
+            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + XB + (wave * LW + i) * 1024), 16, 0, 0);
+        }
+    };
+
+    fx4 acc[WMT][4];
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int i = 0; i < NSTAGE - 1; ++i)
+        if (f0 + i < f1) issue(f0 + i, i);
+    for (int f = f0; f < f1; ++f) {
+        const int ahead = f1 - 1 - f;  // k-steps issued after f (at most NSTAGE - 2)
+        if constexpr (NSTAGE >= 3) {
+            if (ahead >= 1) wait_vm<LPS>();
+            else wait_vm<0>();
+        } else {
+            wait_vm<0>();
+        }
+        __syncthreads();  // stage f in LDS for every wave; every wave is done with stage f - 1
+        if (f + NSTAGE - 1 < f1) issue(f + NSTAGE - 1, (f - f0 + NSTAGE - 1) % NSTAGE);
+        int k, ti, kc;
+        locate(f, k, ti, kc);
+        const int np = seg_at(a, k).nparts;
+        const char* sb = lds + ((f - f0) % NSTAGE) * SB;  // (split-K blocks start at f0)
+        bf16x8 bx[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = wn * 64 + j * 16 + (lane & 15);
+            bx[j] = *reinterpret_cast<const bf16x8*>(sb + (n * 4 + (gq ^ swz(n))) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < WMT; ++i) {
+            const int row = wm * 16 * WMT + i * 16 + (lane & 15);
+            for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
+                const bf16x8 aw = *reinterpret_cast<const bf16x8*>(sb + XB + ((p * BM + row) * 4 + (gq ^ swz(row))) * 16);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
+            }
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
+            const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
+            if (nd >= P || m >= a.M) continue;
+            const fx4 v = acc[i][j];
+            if (ksplit > 1) {
+                float* o = a.partial + ((int64_t)split * P + nd) * a.M + m;
+                if (m + 3 < a.M && (a.M & 3) == 0) {
+                    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (m + r < a.M) o[r] = v[r];
+                }
+                continue;
+            }
+            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3]);
+        }
+}
+
 // Split-K reduction: the partial tiles of the ksplit blocks of an output tile summed in split order
 // (deterministic), then the launch's epilogue.  One thread per (domain pixel, 4 output channels).
 __global__ __launch_bounds__(UNT) void k_unet_conv_reduce(snnflow_unet_conv_args a) {
@@ -1303,6 +1502,32 @@ int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
     return 0;
 }
 
+#ifndef SNNFLOW_UNET_DMA
+#define SNNFLOW_UNET_DMA 1     // forward convs (exact-in-bf16 inputs) through k_unet_conv_dma
+#endif
+#ifndef SNNFLOW_UNET_NSTAGE
+#define SNNFLOW_UNET_NSTAGE 2  // LDS buffers of k_unet_conv_dma (cfg5: 2 -> 278.6 ms, 3 -> 308.2 ms: 72 KB of LDS, two blocks per CU)
+#endif
+template <int WMT, int WM>
+int launch_conv_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
+    using G = ConvGeo<WMT, WM, 1>;
+    const int P = dom_pixels(a);
+    const int ks = a.ksplit > 1 ? a.ksplit : 1;
+    const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN) * ks;
+    if (nb > 0x7fffffff) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: grid too large");
+    if (nb == 0) return 0;
+    for (int k = 0; k < a.nseg; ++k)  // 32-bit buffer offsets; out-of-range offsets read zeros
+        if ((int64_t)a.B * a.seg[k].H * a.seg[k].W * a.seg[k].cpitch * 2 >= 0x80000000LL)
+            return launch_conv<WMT, WM, 1>(a, s);
+    hipLaunchKernelGGL((k_unet_conv_dma<WMT, WM, SNNFLOW_UNET_NSTAGE>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
+    if (ks > 1) {
+        const int64_t n = (int64_t)P * ((a.M + 3) / 4);
+        hipLaunchKernelGGL(k_unet_conv_reduce, dim3((unsigned)((n + UNT - 1) / UNT)), dim3(UNT), 0, s, a);
+    }
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
 // Output tiles of a launch for its tile configuration (the selection of snnflow_unet_conv).
 inline void conv_tile(const snnflow_unet_conv_args& a, int& bm, int& bn) {
     if (a.xparts == 3) {
@@ -1375,6 +1600,12 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
         if (a->M > 64) return launch_conv<4, 2, 3>(*a, s);
         if (a->M > 32) return launch_conv<2, 2, 3>(*a, s);
         return launch_conv<2, 1, 3>(*a, s);
+    }
+    if (SNNFLOW_UNET_DMA) {  // LDS-DMA operands, NSTAGE-deep
+        if (a->M > 64) return launch_conv_dma<4, 2>(*a, s);
+        if (a->M > 32) return launch_conv_dma<2, 2>(*a, s);
+        if (a->M > 16) return launch_conv_dma<2, 1>(*a, s);
+        return launch_conv_dma<1, 1>(*a, s);
     }
     if (a->M > 64) return launch_conv<4, 2, 1>(*a, s);
     if (a->M > 32) return launch_conv<2, 2, 1>(*a, s);

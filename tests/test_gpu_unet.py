@@ -96,7 +96,7 @@ def test_unet_vs_oracle(dev, base, H, acts, hard):
     W = H
     ew, rew = snnflow.EventWarping(_cfg(H, W), dev), None
     gen = torch.Generator(device=dev).manual_seed(3)
-    flows, rflows, wins, flips = [], [], [], 0
+    flows, rflows, wins, flips, nspk = [], [], [], 0, 0
     for t in range(3):
         w = make_window(2, 1000, H, W, gen, dev)
         wins.append(w)
@@ -105,8 +105,13 @@ def test_unet_vs_oracle(dev, base, H, acts, hard):
         flows.append(out["flow"])
         rflows.append(rout["flow"])
         for a, b in zip(model.states, ref.states):
-            flips += int((_spk(a) != (b.detach()[:, 1] if b.dim() == 6 else b.detach()[1])).sum())
-    print(f"\n[unet base={base} {H}x{W} {acts} hard={hard}] spike flips {flips}")
+            sb = b.detach()[:, 1] if b.dim() == 6 else b.detach()[1]
+            flips += int((_spk(a) != sb).sum())
+            nspk += sb.numel()
+    print(f"\n[unet base={base} {H}x{W} {acts} hard={hard}] spike flips {flips} of {nspk}")
+    # a near-threshold flip (fp32 summation order) cascades through the recurrence to a few hundred
+    # at most; a wrong kernel flips percents of all spikes -- that fails instead of skipping
+    assert flips <= 1e-4 * nspk, f"{flips} spike flips of {nspk}: not rounding noise"
     if flips:
         pytest.skip(f"{flips} near-threshold spike flips (chaotic recurrence): rerun with another seed")
     for t in range(3):
