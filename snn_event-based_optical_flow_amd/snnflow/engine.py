@@ -16,6 +16,8 @@ by the first step of the window ("root"), so autograd performs no per-step
 gradient additions.
 """
 import ctypes
+import functools
+import operator
 
 import torch
 
@@ -202,7 +204,7 @@ class FireNetEngine:
         new = self.__class__.__new__(self.__class__)
         memo[id(self)] = new
         for k, v in self.__dict__.items():
-            new.__dict__[k] = None if k in ("_neurons", "_plist", "_prep_ws", "_prep_map", "_plan", "_gviews", "_layout",
+            new.__dict__[k] = None if k in ("_neurons", "_nk_src", "_plist", "_prep_ws", "_prep_map", "_plan", "_gviews", "_layout",
                                             "_anchor") \
                 else copy.deepcopy(v, memo)
         return new
@@ -219,24 +221,36 @@ class FireNetEngine:
 
     def _neuron_key(self):
         """Everything neuron_struct reads, per cell: the tensors themselves (held by the cache, so a
-        replaced tensor can never alias a freed one's identity) and the scalar options."""
-        key = []
-        for c, bn, lif in zip(self.cells, self.bns, self.lifs):
-            key += (bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                    lif.beta, lif.threshold, bn.training, bn.track_running_stats, bn.momentum, bn.eps,
-                    c.hard_reset)
-        return key
+        replaced tensor can never alias a freed one's identity) and the scalar options.  Read from
+        the modules' _parameters / _buffers dicts directly (nn.Module.__getattr__ costs ~0.3 us a
+        lookup; this runs three times per time step on the eager path)."""
+        src = self.__dict__.get("_nk_src")
+        if src is None:
+            src = [(c, bn, bn._parameters, bn._buffers, lif._parameters, lif._buffers)
+                   for c, bn, lif in zip(self.cells, self.bns, self.lifs)]
+            self._nk_src = src
+        tens, scal = [], []
+        for c, bn, bp, bb, lp, lb in src:
+            tens += (bp.get("weight"), bp.get("bias"), bb.get("running_mean"), bb.get("running_var"),
+                     bb.get("num_batches_tracked"), lp["beta"] if "beta" in lp else lb.get("beta"),
+                     lp["threshold"] if "threshold" in lp else lb.get("threshold"))
+            scal += (bn.training, bn.track_running_stats, bn.momentum, bn.eps, c.hard_reset)
+        return tens, scal
 
     def neurons(self):
         """neuron_struct of every cell, cached and re-validated on every call against the tensors and
         options it was built from (identity for tensors, equality for scalars).  A rebuild bumps the
         engine generation, which keys the C step driver's plan (it holds copies of the structs)."""
-        key = self._neuron_key()
+        tens, scal = self._neuron_key()
         n = self._neurons
-        if n is None or not all(a is b if isinstance(a, torch.Tensor) else a == b for a, b in zip(n[0], key)):
-            self._neurons = (key, [neuron_struct(c) for c in self.cells])
+        if n is None or n[1] != scal or not all(map(operator.is_, n[0], tens)):
+            self._neurons = (tens, scal, [neuron_struct(c) for c in self.cells])
             self._gen = self.__dict__.get("_gen", 0) + 1
-        return self._neurons[1]
+        return self._neurons[2]
+
+    def any_subtract(self):
+        """True if some cell uses the subtract reset (theta_subtract has work)."""
+        return any(lif.reset_mechanism == "subtract" for lif in self.lifs)
 
     def sequence_ok(self, cin0):
         """True if FireNetSequence's wavefront launches take this model (C = 8, 16, 32; cin0 2 or 4)."""
@@ -835,8 +849,9 @@ class FireNetStep(torch.autograd.Function):
                     if l + 1 <= L - 1:
                         a.zero0, a.zero_n = bacc[l + 1], zn
                     _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
-            for l in range(L):
-                theta_subtract(eng.cells[l], gcur[l], mem_in[l], B * H * W, glayers[l][2].threshold, s)
+            if eng.any_subtract():
+                for l in range(L):
+                    theta_subtract(eng.cells[l], gcur[l], mem_in[l], B * H * W, glayers[l][2].threshold, s)
             if ctx.root:
                 eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
         except Exception:
@@ -879,6 +894,55 @@ def _seq_ok(eng, B, H, W, T, cin0, xs):
         return False
     st = xs[0].stride()
     return all(x.stride() == st for x in xs)
+
+
+@functools.lru_cache(maxsize=64)
+def capped_slots(T, K, rec, cap):
+    """Launch order of the (kernel k < K, step t < T) grid with at most `cap` tasks per launch,
+    from its exact dependencies: (k-1, t), (k, t-1), and (k+1, t-1) where rec[k] (a recurrent
+    layer reads spikes the next kernel of the previous step wrote).  List scheduling, longest
+    remaining dependency chain first.  A task is one 512-block layer-step at cfg2 and a launch
+    runs in rounds of 768 resident blocks: three tasks are exactly two rounds, four take a
+    third, 2/3-full round -- wavefront_slots' 26 launches are 62 rounds, this schedule (cap 3)
+    29 launches and 56 rounds (measured slower all the same: see slot_cap).
+    Returns [[(k, t), ...] per launch]."""
+    if cap <= 0:
+        return wavefront_slots(T, K)
+
+    def deps(k, t):
+        d = []
+        if k >= 1:
+            d.append((k - 1, t))
+        if t >= 1:
+            d.append((k, t - 1))
+            if k + 1 < K and rec[k]:
+                d.append((k + 1, t - 1))
+        return d
+    tasks = [(k, t) for t in range(T) for k in range(K)]
+    succ = {x: [] for x in tasks}
+    for x in tasks:
+        for d in deps(*x):
+            succ[d].append(x)
+    chain = {}
+    for x in reversed(tasks):  # successors come later in (t, k) order
+        chain[x] = 1 + max((chain[y] for y in succ[x]), default=0)
+    done, launches = set(), []
+    while len(done) < len(tasks):
+        ready = [x for x in tasks if x not in done and all(d in done for d in deps(*x))]
+        ready.sort(key=lambda x: (-chain[x], x[1], x[0]))
+        pick = ready[:cap]
+        launches.append(pick)
+        done.update(pick)
+    return launches
+
+
+def slot_cap():
+    """Tasks per slot launch (SNNFLOW_SLOT_CAP; 0, the default: the plain wavefront order).  Measured
+    (profiles/r03/ab_slot_cap.txt): cap 3 is slower at cfg2 (1.545-1.552 vs 1.491-1.504 ms: a
+    3-task launch takes 28.4 / 20.1 us against 30.5 / 21.3 us for 4 tasks, so the time follows the
+    work, not the block rounds) and at C = 32 (6.56 vs 6.50 ms)."""
+    import os
+    return int(os.environ.get("SNNFLOW_SLOT_CAP", "0"))
 
 
 def wavefront_slots(T, K):
@@ -979,7 +1043,8 @@ class FireNetSequence(torch.autograd.Function):
             _lib.call("fwd_seq", lib.snnflow_fwd_seq, ctypes.byref(sa), s)
             eng.last_seq_work = work  # tests read the timeout flag (int 8 of the work area)
         else:
-            for tasks in wavefront_slots(T, L + 1):
+            frec = tuple(bool(eng.rec[k]) if k < L else False for k in range(L + 1))
+            for tasks in capped_slots(T, L + 1, frec, slot_cap()):
                 convs, top = [], None
                 for k, t in tasks:
                     if k < L:
@@ -1082,8 +1147,12 @@ class FireNetSequence(torch.autograd.Function):
             eng.pending_layers.append((0,) if fuse else tuple(range(L)))
         try:
             # backward kernel j of step t: j = 0 top (pred + LIF of layer L-1), j >= 1 layer L-j;
-            # in reversed time tau = T-1-t the dependencies have the forward's shape
-            for tasks in wavefront_slots(T, L + 1):
+            # in reversed time tau = T-1-t the dependencies have the forward's shape: (j-1, tau)
+            # (the BN-backward sums of layer L-j), (j, tau-1) (the membrane gradient from step t+1),
+            # and (j+1, tau-1) where layer L-j-1 is recurrent (its spikes' gradient from the
+            # recurrent dgrad of step t+1)
+            brec = tuple(bool(eng.rec[L - 1 - j]) if j < L else False for j in range(L + 1))
+            for tasks in capped_slots(T, L + 1, brec, slot_cap()):
                 layers, top = [], None
                 for j, tau in tasks:
                     t = T - 1 - tau
