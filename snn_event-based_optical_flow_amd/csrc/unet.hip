@@ -35,9 +35,13 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float fx4 __attribute__((ext_vector_type(4)));
 
 constexpr int UNT = 256;     // threads per block (4 waves)
-constexpr int XP = 40;       // bf16 per LDS row: 32 k + 8 padding (80-B rows)
+constexpr int XP = 32;       // bf16 per LDS row of k_unet_conv: 32 k (64-B rows, 16-B pieces swizzled: xoff)
 
 __device__ inline uint4 ld16(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+
+__device__ inline int swz(int n);
+// bf16 offset of piece p (8 bf16) of LDS row n of a k_unet_conv tile: 64-B rows, pieces XOR-swizzled
+__device__ inline int xoff(int n, int p) { return n * XP + ((p ^ swz(n)) << 3); }
 
 __device__ inline float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 __device__ inline uint16_t f2bf(float f) {
@@ -128,10 +132,25 @@ __device__ inline void dom_pix(const PixDom& d, int n, int& b, int& y, int& x) {
     x = d.cls < 0 ? xx : 2 * xx + d.px;
 }
 
+// Per-channel LIF constants of output channels m .. m+3: sigmoid(leak) and clamp_min(thresh, 0.01)
+// (spiking_submodules.py:133-136), computed once per lane and channel quad, not per output element.
+struct LifQuad { float lam[4], th[4]; };
+__device__ inline LifQuad lif_quad(const snnflow_unet_conv_args& a, int m) {
+    LifQuad q;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool ok = a.epi == SNNFLOW_UNET_EPI_LIF && m + r < a.M;
+        q.lam[r] = ok ? 1.0f / (1.0f + expf(-a.leak[m + r])) : 0.0f;
+        const float th0 = ok ? a.thresh[m + r] : 1.0f;
+        q.th[r] = th0 < 0.01f ? 0.01f : th0;
+    }
+    return q;
+}
+
 // Epilogue of one output element quad (domain pixel nd, channels m .. m+3): EPI_STORE (optionally
 // accumulating) or the ConvLIF update (spiking_submodules.py:121-151 / 265-300).
 __device__ inline void conv_epilogue(const snnflow_unet_conv_args& a, const PixDom& dom, int nd, int m, float v0,
-                                     float v1, float v2, float v3) {
+                                     float v1, float v2, float v3, const LifQuad& lq) {
     const float v[4] = {v0, v1, v2, v3};
     const int64_t Pfull = (int64_t)a.B * a.Ho * a.Wo;
     const int64_t plane = Pfull * a.M;
@@ -171,8 +190,7 @@ __device__ inline void conv_epilogue(const snnflow_unet_conv_args& a, const PixD
     uint16_t ob16[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const float lam = 1.0f / (1.0f + expf(-a.leak[m + r]));
-        const float th0 = a.thresh[m + r], th = th0 < 0.01f ? 0.01f : th0;
+        const float lam = lq.lam[r], th = lq.th[r];
         vo[r] = a.hard_reset ? ((vp[r] * lam) * (1.0f - zp[r])) + ((1.0f - lam) * v[r])
                              : ((vp[r] * lam) + ((1.0f - lam) * v[r])) - (zp[r] * th);
         zo[r] = (vo[r] - th > 0.0f) ? 1.0f : 0.0f;
@@ -297,13 +315,13 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
         for (int xp = 0; xp < XPARTS; ++xp)
 #pragma unroll
             for (int r = 0; r < G::XR; ++r)
-                *reinterpret_cast<uint4*>(&Xs[(xp * BN + (tid >> 2) + 64 * r) * XP + q * 8]) = xr[xp][r];
+                *reinterpret_cast<uint4*>(&Xs[xoff(xp * BN + (tid >> 2) + 64 * r, q)]) = xr[xp][r];
 #pragma unroll
         for (int r = 0; r < (DW ? 0 : G::WR); ++r) {
             const int e = tid + r * UNT;
             if (e < G::WPIECES) {
                 const int part = e / (BM * 4), rem = e - part * (BM * 4);
-                *reinterpret_cast<uint4*>(&Ws[(part * BM + (rem >> 2)) * XP + (rem & 3) * 8]) = wr[r];
+                *reinterpret_cast<uint4*>(&Ws[xoff(part * BM + (rem >> 2), rem & 3)]) = wr[r];
             }
         }
     };
@@ -359,12 +377,12 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
             bf16x8 bx[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-                bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[(wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8]);
+                bx[j] = *reinterpret_cast<const bf16x8*>(&Xs[xoff(wn * 64 + j * 16 + (lane & 15), lane >> 4)]);
 #pragma unroll
             for (int i = 0; i < WMT; ++i) {
                 const int row = wm * 16 * WMT + i * 16 + (lane & 15);
                 for (int p = np - 1; p >= 0; --p) {  // lo, mid, hi: smallest products first
-                    const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[(p * BM + row) * XP + (lane >> 4) * 8]);
+                    const bf16x8 aw = *reinterpret_cast<const bf16x8*>(&Ws[xoff(p * BM + row, lane >> 4)]);
 #pragma unroll
                     for (int j = 0; j < 4; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw, bx[j], acc[i][j], 0, 0, 0);
@@ -376,7 +394,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 const bf16x8* aw = wf[DW ? i : 0];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int col = (wn * 64 + j * 16 + (lane & 15)) * XP + (lane >> 4) * 8;
+                    const int col = xoff(wn * 64 + j * 16 + (lane & 15), lane >> 4);  // (BN * XP keeps the swizzle)
                     const bf16x8 xh = *reinterpret_cast<const bf16x8*>(&Xs[col]);
                     const bf16x8 xm = *reinterpret_cast<const bf16x8*>(&Xs[BN * XP + col]);
                     const bf16x8 xl = *reinterpret_cast<const bf16x8*>(&Xs[2 * BN * XP + col]);
@@ -395,7 +413,8 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
 
     // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of domain pixel nd
 #pragma unroll
-    for (int i = 0; i < WMT; ++i)
+    for (int i = 0; i < WMT; ++i) {
+        const LifQuad lq = lif_quad(a, m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
@@ -413,8 +432,9 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                 }
                 continue;
             }
-            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3]);
+            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lq);
         }
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -434,7 +454,13 @@ __device__ inline void wait_vm() {  // s_waitcnt vmcnt(N), the other counters un
     static_assert(N >= 0 && N < 64, "vmcnt");
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
-__device__ inline int swz(int n) { return (n >> 2) & 3; }
+// ds_read_b128 serves a wave in four 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same
+// +32 (MI355X_MICROARCH.md, LDS); a group of the operand reads (lane -> row base + (lane & 15), piece
+// lane >> 4) holds rows r + 4q (q = 0..3) of each residue r = row mod 4 with pieces {g, g^1, g^1, g}
+// (g = the group's lowest piece).  Row n's 16-B slot in its 256-B bank row is 4 (n mod 4) + piece';
+// with piece' = piece ^ ((n >> 2) & 2) the four q of every residue land on four distinct slots:
+// conflict-free.  (A (n >> 2) & 3 swizzle is 2-way on these groups.)
+__device__ inline int swz(int n) { return (n >> 2) & 2; }
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -496,61 +522,95 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
         ftot += nits[k];
     }
     const int f0 = (int)((int64_t)ftot * split / ksplit), f1 = (int)((int64_t)ftot * (split + 1) / ksplit);
-    auto locate = [&](int f, int& k, int& ti, int& kc) {
-        k = 0;
+
+    // k-step iterator (segment k, tap (ty, tx) of the domain, 32-channel chunk kc): wave-uniform, advanced
+    // incrementally -- the flat-index divisions run once per block, not per k-step
+    struct It { int k, ty, tx, kc; };
+    auto start = [&](int f) {
+        It it;
+        it.k = 0;
 #pragma unroll
         for (int i = 0; i < SNNFLOW_UNET_MAX_SEGS - 1; ++i)
-            if (k == i && f >= nits[i]) {
+            if (it.k == i && f >= nits[i]) {
                 f -= nits[i];
-                k = i + 1;
+                it.k = i + 1;
             }
-        const int nkc = seg_at(a, k).cpitch >> 5;
-        ti = f / nkc;
-        kc = f - ti * nkc;
+        const int nkc = seg_at(a, it.k).cpitch >> 5;
+        const int ti = f / nkc;
+        it.kc = f - ti * nkc;
+        it.ty = ti / dom.ntx;
+        it.tx = ti - it.ty * dom.ntx;
+        return it;
     };
-    // the LPS loads of flat k-step f into stage buffer b
-    auto issue = [&](int f, int b) {
-        int k, ti, kc;
-        locate(f, k, ti, kc);
+    auto advance = [&](It& it) {
+        if (++it.kc == (seg_at(a, it.k).cpitch >> 5)) {
+            it.kc = 0;
+            if (++it.tx == dom.ntx) {
+                it.tx = 0;
+                if (++it.ty == dom.nty) {
+                    it.ty = 0;
+                    ++it.k;
+                }
+            }
+        }
+    };
+
+    // per segment, per lane: element offset of each X slot's pixel at tap (0, 0) (+ its piece), the
+    // taps inside the input as a bit mask, and each W slot's element offset (part chosen for nparts):
+    // a k-step's load address is then one add and one bit test
+    int cur_k = -1, sW = 0, scp = 0, snp = 0, skc0 = 0;
+    int xbase[LX], wsel[LW];
+    uint32_t vmask[LX];
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.seg[0].x), (short)0, 0, 0x00020000);
+    auto load_seg = [&](int k) {
         const snnflow_unet_seg sg = seg_at(a, k);
-        const int ty_ = ti / dom.ntx;
-        const int ky = dom.ky0 + dom.kst * ty_, kx = dom.kx0 + dom.kst * (ti - ty_ * dom.ntx);
-        const int tap = ky * ks + kx;
-        const int mode = sg.mode, H = sg.H, W = sg.W, cp = sg.cpitch;
-        const uint32_t extent = (uint32_t)((int64_t)a.B * H * W * cp * 2);
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(sg.x), (short)0, (int)extent, 0x00020000);
-        char* const sb = lds + b * SB;
+        const int H = sg.H, W = sg.W, cp = sg.cpitch;
+        const bool s2 = sg.mode == SNNFLOW_UNET_MODE_S2;
+        rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(sg.x), (short)0,
+                                               (int)((int64_t)a.B * H * W * cp * 2), 0x00020000);
+        sW = W;
+        scp = cp;
+        snp = sg.nparts;
+        skc0 = sg.kc0;
 #pragma unroll
         for (int i = 0; i < LX; ++i) {
-            int iy, ix;
-            bool ok = pv[i];
-            if (mode == SNNFLOW_UNET_MODE_S1) {
-                iy = py[i] + ky - pad;
-                ix = px[i] + kx - pad;
-            } else if (mode == SNNFLOW_UNET_MODE_S2) {
-                iy = 2 * py[i] + ky - pad;
-                ix = 2 * px[i] + kx - pad;
-            } else {
-                const int tyy = py[i] + pad - ky, txx = px[i] + pad - kx;
-                ok = ok && tyy >= 0 && txx >= 0 && ((tyy | txx) & 1) == 0;
-                iy = tyy >> 1;
-                ix = txx >> 1;
-            }
-            ok = ok && iy >= 0 && iy < H && ix >= 0 && ix < W;
-            const uint32_t off =
-                ok ? (uint32_t)(((((int64_t)pb[i] * H + iy) * W + ix) * cp + kc * 32 + xq[i] * 8) * 2) : 0x80000000u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(sb + (wave * LX + i) * 1024), 16, off, 0, 0, 0);
+            const int iy0 = (s2 ? 2 * py[i] : py[i]) - pad, ix0 = (s2 ? 2 * px[i] : px[i]) - pad;
+            xbase[i] = ((pb[i] * H + iy0) * W + ix0) * cp + xq[i] * 8;
+            uint32_t m = 0u;
+            if (pv[i])
+                for (int ky = 0; ky < ks; ++ky)
+                    for (int kx = 0; kx < ks; ++kx)
+                        if (iy0 + ky >= 0 && iy0 + ky < H && ix0 + kx >= 0 && ix0 + kx < W) m |= 1u << (ky * ks + kx);
+            vmask[i] = m;
         }
-        const int np = sg.nparts;
-        const uint16_t* wb = a.w + ((int64_t)(tap * a.kct + sg.kc0 + kc) * a.mpad) * 32;
 #pragma unroll
         for (int i = 0; i < LW; ++i) {
             int part = (int)((uint32_t)wofs[i] >> 28);
-            if (part >= np) part = 0;  // unused part of this segment: a harmless duplicate load
-            const uint16_t* src = wb + part * wpart + (wofs[i] & 0x0fffffff);
-            __builtin_amdgcn_global_load_lds((const void*)src, (lds_void*)(sb + XB + (wave * LW + i) * 1024), 16, 0, 0);
+            if (part >= snp) part = 0;  // unused part of this segment: a harmless duplicate load
+            wsel[i] = part * (int)wpart + (wofs[i] & 0x0fffffff);
         }
+    };
+    uint32_t npq = 0u;  // nparts of the issued, not yet computed k-steps: 2 bits per stage buffer
+    // the LPS loads of k-step `it` into stage buffer b
+    auto issue = [&](const It& it, int b) {
+        if (it.k != cur_k) {
+            load_seg(it.k);
+            cur_k = it.k;
+        }
+        const int ky = dom.ky0 + dom.kst * it.ty, kx = dom.kx0 + dom.kst * it.tx;
+        const int tap = ky * ks + kx;
+        const int sdelta = (ky * sW + kx) * scp + it.kc * 32;
+        char* const sb = lds + b * SB;
+#pragma unroll
+        for (int i = 0; i < LX; ++i) {
+            const uint32_t off = ((vmask[i] >> tap) & 1u) ? (uint32_t)(xbase[i] + sdelta) * 2u : 0x80000000u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(sb + (wave * LX + i) * 1024), 16, off, 0, 0, 0);
+        }
+        const uint16_t* wb = a.w + ((int64_t)(tap * a.kct + skc0 + it.kc) * a.mpad) * 32;
+#pragma unroll
+        for (int i = 0; i < LW; ++i)
+            __builtin_amdgcn_global_load_lds((const void*)(wb + wsel[i]), (lds_void*)(sb + XB + (wave * LW + i) * 1024), 16, 0, 0);
+        npq |= (uint32_t)snp << (2 * b);
     };
 
     fx4 acc[WMT][4];
@@ -559,9 +619,13 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
 
+    It iss = start(f0);  // the next k-step to issue
 #pragma unroll
     for (int i = 0; i < NSTAGE - 1; ++i)
-        if (f0 + i < f1) issue(f0 + i, i);
+        if (f0 + i < f1) {
+            issue(iss, i);
+            advance(iss);
+        }
     for (int f = f0; f < f1; ++f) {
         const int ahead = f1 - 1 - f;  // k-steps issued after f (at most NSTAGE - 2)
         if constexpr (NSTAGE >= 3) {
@@ -571,11 +635,14 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
             wait_vm<0>();
         }
         __syncthreads();  // stage f in LDS for every wave; every wave is done with stage f - 1
-        if (f + NSTAGE - 1 < f1) issue(f + NSTAGE - 1, (f - f0 + NSTAGE - 1) % NSTAGE);
-        int k, ti, kc;
-        locate(f, k, ti, kc);
-        const int np = seg_at(a, k).nparts;
-        const char* sb = lds + ((f - f0) % NSTAGE) * SB;  // (split-K blocks start at f0)
+        const int bcur = (f - f0) % NSTAGE;  // (split-K blocks start at f0)
+        const int np = (int)((npq >> (2 * bcur)) & 3u);
+        npq &= ~(3u << (2 * bcur));
+        if (f + NSTAGE - 1 < f1) {
+            issue(iss, (f - f0 + NSTAGE - 1) % NSTAGE);
+            advance(iss);
+        }
+        const char* sb = lds + bcur * SB;
         bf16x8 bx[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -594,7 +661,8 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
     }
 
 #pragma unroll
-    for (int i = 0; i < WMT; ++i)
+    for (int i = 0; i < WMT; ++i) {
+        const LifQuad lq = lif_quad(a, m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4));
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
@@ -612,8 +680,9 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
                 }
                 continue;
             }
-            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3]);
+            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lq);
         }
+    }
 }
 
 // Split-K reduction: the partial tiles of the ksplit blocks of an output tile summed in split order
@@ -636,7 +705,7 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_reduce(snnflow_unet_conv_args
                 if (m + r < a.M) v[r] += o[r];
         }
     }
-    conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3]);
+    conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lif_quad(a, m));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1516,8 +1585,13 @@ int launch_conv_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
     const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN) * ks;
     if (nb > 0x7fffffff) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: grid too large");
     if (nb == 0) return 0;
-    for (int k = 0; k < a.nseg; ++k)  // 32-bit buffer offsets; out-of-range offsets read zeros
-        if ((int64_t)a.B * a.seg[k].H * a.seg[k].W * a.seg[k].cpitch * 2 >= 0x80000000LL)
+    // 32-bit buffer offsets (out-of-range offsets read zeros), stride-1 / stride-2 segments, taps as a
+    // 32-bit mask, 32-bit W offsets; anything else runs the register-staged kernel
+    if (a.pclass >= 0 || a.ksize * a.ksize > 32 || 3LL * a.ksize * a.ksize * a.kct * a.mpad * 32 >= 0x80000000LL)
+        return launch_conv<WMT, WM, 1>(a, s);
+    for (int k = 0; k < a.nseg; ++k)
+        if ((int64_t)a.B * a.seg[k].H * a.seg[k].W * a.seg[k].cpitch * 2 >= 0x80000000LL ||
+            (a.seg[k].mode != SNNFLOW_UNET_MODE_S1 && a.seg[k].mode != SNNFLOW_UNET_MODE_S2))
             return launch_conv<WMT, WM, 1>(a, s);
     hipLaunchKernelGGL((k_unet_conv_dma<WMT, WM, SNNFLOW_UNET_NSTAGE>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
     if (ks > 1) {
