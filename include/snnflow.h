@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 24
+#define SNNFLOW_ABI_VERSION 25
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -655,8 +655,14 @@ typedef struct {
     float* g_prev;                              /* fp32 [2][P][C] or NULL */
     float* g_res; int gres_pitch;               /* or NULL */
     double* acc;                                /* [2*C] */
+    /* ABI 25, optional: workspace of snnflow_unet_lif_bwd_partial_doubles(P, C, gc_pitch) doubles ([2C][blocks]); with
+     * it every block writes its sums there and a second kernel adds them to acc in block order
+     * (deterministic, and no contention of ~2,000 blocks' fp64 atomics on 2*C addresses); NULL: the
+     * blocks add to acc by fp64 atomics. */
+    double* partial;
 } snnflow_unet_lif_bwd_args;
 int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream);
+int snnflow_unet_lif_bwd_partial_doubles(int P, int C, int gc_pitch);
 
 /* g_thresh = (thresh >= 0.01) * acc[c], g_leak = acc[C + c] * s * (1 - s), s = sigmoid(leak). */
 int snnflow_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,

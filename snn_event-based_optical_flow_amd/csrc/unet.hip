@@ -685,6 +685,178 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
     }
 }
 
+// Input gradients (XPARTS = 3: the fp32 gradient as hi / mid / lo bf16 planes, one segment, stride 1
+// or a parity class of the transposed stride-2 conv) with the three X planes brought in by LDS-DMA,
+// double-buffered, and each wave's weight fragments (DW layout) as register loads issued for the next
+// k-step right after the m-tile that used them.  Addresses as in k_unet_conv_dma: per-lane pixel bases
+// and tap masks set once, an incremental k-step iterator; in a parity class the input pixel of domain
+// tap (ty, tx) is (iy0 - ty, ix0 - tx), a stride-1 tap adds (ty, tx).
+template <int WMT, int WAVES_M>
+__global__ __launch_bounds__(UNT) void k_unet_dgrad_dma(snnflow_unet_conv_args a) {
+    using G = ConvGeo<WMT, WAVES_M, 3>;
+    constexpr int BM = G::BM, BN = G::BN, NSTAGE = 2;
+    constexpr int XB = BN * 64;                   // one plane's tile bytes
+    constexpr int LX = BN / 64;                   // wave-loads per wave and plane
+    constexpr int SB = 3 * XB;
+    __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * SB];
+
+    const int tid = threadIdx.x, lane = tid & 63, gq = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave % WAVES_M, wn = wave / WAVES_M;
+    const PixDom dom = pix_dom(a);
+    const int P = dom.P;
+    const int mtiles = (a.M + BM - 1) / BM, ntiles = (P + BN - 1) / BN, ntc = mtiles * ntiles;
+    const int ksplit = a.ksplit > 1 ? a.ksplit : 1;
+    const int tl = xcd_remap(blockIdx.x, ntc * ksplit);
+    const int split = tl / ntc, t = tl - split * ntc;
+    const int m0 = (t % mtiles) * BM, n0 = (t / mtiles) * BN;
+    const int ks = a.ksize, pad = ks / 2;
+    const int wpart = (int)((int64_t)ks * ks * a.kct * a.mpad * 32);
+    const snnflow_unet_seg sg = a.seg[0];
+    const int H = sg.H, W = sg.W, cp = sg.cpitch, nkc = cp >> 5;
+    const bool t2 = sg.mode == SNNFLOW_UNET_MODE_T2;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(sg.x), (short)0, (int)(2 * a.xpart + (int64_t)a.B * H * W * cp) * 2, 0x00020000);
+
+    // this lane's X slots (the same pixels in all three planes): pixel base at domain tap (0, 0), tap mask
+    int xbase[LX];
+    uint32_t vmask[LX];
+#pragma unroll
+    for (int i = 0; i < LX; ++i) {
+        const int e = (wave * LX + i) * 64 + lane, r = e >> 2;
+        const int n = n0 + r;
+        int pb, py, px;
+        dom_pix(dom, n < P ? n : 0, pb, py, px);
+        const int q = (e & 3) ^ swz(r);
+        // domain tap (ty, tx) reads input (iy0 + sy ty, ix0 + sy tx)
+        const int iy0 = t2 ? (py + pad - dom.ky0) >> 1 : py - pad, ix0 = t2 ? (px + pad - dom.kx0) >> 1 : px - pad;
+        const int sy = t2 ? -1 : 1;
+        xbase[i] = ((pb * H + iy0) * W + ix0) * cp + q * 8;
+        uint32_t m = 0u;
+        if (n < P)
+            for (int ty = 0; ty < dom.nty; ++ty)
+                for (int tx = 0; tx < dom.ntx; ++tx) {
+                    const int iy = iy0 + sy * ty, ix = ix0 + sy * tx;
+                    // (t2: py + pad - ky >= 0 for the class's taps is iy >= 0)
+                    if (iy >= 0 && iy < H && ix >= 0 && ix < W) m |= 1u << (ty * dom.ntx + tx);
+                }
+        vmask[i] = m;
+    }
+    const int sy = t2 ? -1 : 1;
+    const int wlane = (m0 + wm * 16 * WMT + (lane & 15)) * 32 + gq * 8;  // this lane's fragment row / piece
+
+    const int taps = dom.nty * dom.ntx, ftot = taps * nkc;
+    const int f0 = (int)((int64_t)ftot * split / ksplit), f1 = (int)((int64_t)ftot * (split + 1) / ksplit);
+    struct It { int ty, tx, kc; };
+    It iss;
+    {
+        const int ti = f0 / nkc;
+        iss.kc = f0 - ti * nkc;
+        iss.ty = ti / dom.ntx;
+        iss.tx = ti - iss.ty * dom.ntx;
+    }
+    auto advance = [&](It& it) {
+        if (++it.kc == nkc) {
+            it.kc = 0;
+            if (++it.tx == dom.ntx) {
+                it.tx = 0;
+                ++it.ty;
+            }
+        }
+    };
+    auto wstep = [&](const It& it) {  // element offset of k-step it's weight rows (part 0)
+        const int ky = dom.ky0 + dom.kst * it.ty, kx = dom.kx0 + dom.kst * it.tx;
+        return ((ky * ks + kx) * a.kct + sg.kc0 + it.kc) * a.mpad * 32;
+    };
+    auto issue_x = [&](const It& it, int b) {
+        const int tbit = it.ty * dom.ntx + it.tx;
+        const int sdelta = sy * (it.ty * W + it.tx) * cp + it.kc * 32;
+        char* const sb = lds + b * SB;
+#pragma unroll
+        for (int xp = 0; xp < 3; ++xp)
+#pragma unroll
+            for (int i = 0; i < LX; ++i) {
+                const uint32_t off = ((vmask[i] >> tbit) & 1u) ? (uint32_t)(xp * (int)a.xpart + xbase[i] + sdelta) * 2u
+                                                              : 0x80000000u;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(sb + xp * XB + (wave * LX + i) * 1024), 16, off,
+                                                         0, 0, 0);
+            }
+    };
+    bf16x8 wf[WMT][3];
+    auto load_wi = [&](int ws, int i) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+            wf[i][p] = __builtin_bit_cast(bf16x8, ld16(a.w + p * wpart + ws + wlane + i * 16 * 32));
+    };
+
+    fx4 acc[WMT][4];
+#pragma unroll
+    for (int i = 0; i < WMT; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fx4{0.f, 0.f, 0.f, 0.f};
+
+    if (f0 < f1) {
+        issue_x(iss, 0);
+        const int ws = wstep(iss);
+#pragma unroll
+        for (int i = 0; i < WMT; ++i) load_wi(ws, i);
+        advance(iss);
+    }
+    for (int f = f0; f < f1; ++f) {
+        wait_vm<0>();     // this k-step's planes (DMA) and weight fragments (registers) have landed
+        __syncthreads();  // ... for every wave; every wave is done with the other buffer
+        const bool more = f + 1 < f1;
+        const int ws_next = more ? wstep(iss) : 0;
+        if (more) issue_x(iss, (f - f0 + 1) & 1);
+        const char* sb = lds + ((f - f0) & 1) * SB;
+#pragma unroll
+        for (int i = 0; i < WMT; ++i) {
+            const bf16x8 w0 = wf[i][0], w1 = wf[i][1], w2 = wf[i][2];
+            if (more) load_wi(ws_next, i);  // the next k-step's fragments of this m-tile, in flight from here
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = wn * 64 + j * 16 + (lane & 15);
+                const int o = (n * 4 + (gq ^ swz(n))) * 16;
+                const bf16x8 xh = *reinterpret_cast<const bf16x8*>(sb + o);
+                const bf16x8 xm = *reinterpret_cast<const bf16x8*>(sb + XB + o);
+                const bf16x8 xl = *reinterpret_cast<const bf16x8*>(sb + 2 * XB + o);
+                // smallest first: lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, xl, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, xm, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w2, xh, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, xm, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, xh, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, xh, acc[i][j], 0, 0, 0);
+            }
+        }
+        if (more) advance(iss);
+    }
+
+#pragma unroll
+    for (int i = 0; i < WMT; ++i) {
+        const LifQuad lq = lif_quad(a, m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
+            const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
+            if (nd >= P || m >= a.M) continue;
+            const fx4 v = acc[i][j];
+            if (ksplit > 1) {
+                float* o = a.partial + ((int64_t)split * P + nd) * a.M + m;
+                if (m + 3 < a.M && (a.M & 3) == 0) {
+                    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (m + r < a.M) o[r] = v[r];
+                }
+                continue;
+            }
+            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lq);
+        }
+    }
+}
+
 // Split-K reduction: the partial tiles of the ksplit blocks of an output tile summed in split order
 // (deterministic), then the launch's epilogue.  One thread per (domain pixel, 4 output channels).
 __global__ __launch_bounds__(UNT) void k_unet_conv_reduce(snnflow_unet_conv_args a) {
@@ -1274,7 +1446,29 @@ __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args 
             }
     }
     __syncthreads();
-    for (int i = tid; i < 2 * C; i += UNT) atomicAdd(a.acc + i, (double)sums[i]);
+    if (a.partial) {  // this block's sums; k_unet_lif_bwd_reduce adds the blocks in order
+        for (int i = tid; i < 2 * C; i += UNT) a.partial[(int64_t)i * gridDim.x + blockIdx.x] = (double)sums[i];
+    } else {
+        for (int i = tid; i < 2 * C; i += UNT) atomicAdd(a.acc + i, (double)sums[i]);
+    }
+}
+
+// acc[i] += sum over blocks b of partial[i][b], in a fixed order (per thread a strided run of blocks,
+// coalesced, then a fixed LDS tree): one block per sum index i.
+__global__ __launch_bounds__(UNT) void k_unet_lif_bwd_reduce(const double* __restrict__ part, int nblk, int n2,
+                                                             double* acc) {
+    __shared__ double red[UNT];
+    const int i = blockIdx.x, tid = threadIdx.x;
+    double v = 0.0;
+    for (int b = tid; b < nblk; b += UNT) v += part[(int64_t)i * nblk + b];
+    red[tid] = v;
+    __syncthreads();
+#pragma unroll
+    for (int o = UNT / 2; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    if (tid == 0) acc[i] += red[0];
 }
 
 __global__ void k_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,
@@ -1602,6 +1796,33 @@ int launch_conv_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
     return 0;
 }
 
+#ifndef SNNFLOW_UNET_DGRAD_DMA
+#define SNNFLOW_UNET_DGRAD_DMA 1  // input gradients through k_unet_dgrad_dma
+#endif
+template <int WMT, int WM>
+int launch_dgrad_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
+    using G = ConvGeo<WMT, WM, 3>;
+    const snnflow_unet_seg& g = a.seg[0];
+    // one segment, 32-bit buffer offsets over the three planes, taps as a 32-bit mask, 32-bit W offsets;
+    // a transposed segment only as a parity class
+    if (a.nseg != 1 || a.ksize * a.ksize > 32 || 3LL * a.ksize * a.ksize * a.kct * a.mpad * 32 >= 0x80000000LL ||
+        (2 * a.xpart + (int64_t)a.B * g.H * g.W * g.cpitch) * 2 >= 0x80000000LL ||
+        (g.mode == SNNFLOW_UNET_MODE_T2) != (a.pclass >= 0) || g.mode == SNNFLOW_UNET_MODE_S2)
+        return launch_conv<WMT, WM, 3>(a, s);
+    const int P = dom_pixels(a);
+    const int ks = a.ksplit > 1 ? a.ksplit : 1;
+    const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN) * ks;
+    if (nb > 0x7fffffff) SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: grid too large");
+    if (nb == 0) return 0;
+    hipLaunchKernelGGL((k_unet_dgrad_dma<WMT, WM>), dim3((unsigned)nb), dim3(UNT), 0, s, a);
+    if (ks > 1) {
+        const int64_t n = (int64_t)P * ((a.M + 3) / 4);
+        hipLaunchKernelGGL(k_unet_conv_reduce, dim3((unsigned)((n + UNT - 1) / UNT)), dim3(UNT), 0, s, a);
+    }
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
 // Output tiles of a launch for its tile configuration (the selection of snnflow_unet_conv).
 inline void conv_tile(const snnflow_unet_conv_args& a, int& bm, int& bn) {
     if (a.xparts == 3) {
@@ -1670,6 +1891,13 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
         SNN_FAIL(SNNFLOW_E_ARG, "unet_conv: parity classes are for one transposed stride-2 segment");
     const hipStream_t s = (hipStream_t)stream;
     if (a->xparts == 3) {  // input gradients: the fp32 gradient as three bf16 planes
+        if (SNNFLOW_UNET_DGRAD_DMA) {
+            if (a->M > 128 && a->M <= 160) return launch_dgrad_dma<5, 2>(*a, s);
+            if (a->M > 64) return launch_dgrad_dma<4, 2>(*a, s);
+            if (a->M > 32) return launch_dgrad_dma<2, 2>(*a, s);
+            // M <= 32 keeps the register-staged kernel: its 256-pixel tiles would need 96 KB of LDS
+            // and 257 VGPRs double-buffered
+        }
         if (a->M > 128 && a->M <= 160) return launch_conv<5, 2, 3>(*a, s);
         if (a->M > 64) return launch_conv<4, 2, 3>(*a, s);
         if (a->M > 32) return launch_conv<2, 2, 3>(*a, s);
@@ -1907,9 +2135,18 @@ int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream) {
         a->surrogate > 3)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_lif_bwd: bad args");
     const int ppi = UNT / (a->gc_pitch / 4);
-    hipLaunchKernelGGL(k_unet_lif_bwd, dim3(grid1d((int64_t)a->P, ppi, 2048)), dim3(UNT), 0, (hipStream_t)stream, *a);
+    const int nblk = grid1d((int64_t)a->P, ppi, 2048);
+    hipLaunchKernelGGL(k_unet_lif_bwd, dim3(nblk), dim3(UNT), 0, (hipStream_t)stream, *a);
+    if (a->partial)
+        hipLaunchKernelGGL(k_unet_lif_bwd_reduce, dim3(2 * a->C), dim3(UNT), 0, (hipStream_t)stream, a->partial, nblk,
+                           2 * a->C, a->acc);
     SNN_CHECK_LAUNCH();
     return 0;
+}
+
+int snnflow_unet_lif_bwd_partial_doubles(int P, int C, int gc_pitch) {
+    if (P <= 0 || C <= 0 || gc_pitch < 4) return 0;
+    return grid1d((int64_t)P, UNT / (gc_pitch / 4), 2048) * 2 * C;
 }
 
 int snnflow_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,

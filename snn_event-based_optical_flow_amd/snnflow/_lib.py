@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 24
+ABI_VERSION = 25
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -195,7 +195,7 @@ class UNetLifBwdArgs(ctypes.Structure):
     _fields_ = [("P", I32), ("C", I32), ("leak", P), ("thresh", P), ("width", F32), ("hard_reset", I32),
                 ("detach", I32), ("surrogate", I32), ("g_out", P), ("g_pitch", I32), ("g_state", P),
                 ("state", P), ("prev_state", P), ("current", P), ("g_cur3", P), ("gc_pitch", I32),
-                ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P)]
+                ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P), ("partial", P)]
 
 
 MAX_LAYERS = 8
@@ -312,6 +312,7 @@ EXPORTS = {
     "snnflow_unet_wgrad_partial_floats": (I64, [ctypes.POINTER(UNetWgradArgs)]),
     "snnflow_unet_wgrad_finalize": (I32, [P, I32, P, I32, I32, I32, I32, I32, I32, P, P]),
     "snnflow_unet_lif_bwd": (I32, [ctypes.POINTER(UNetLifBwdArgs), P]),
+    "snnflow_unet_lif_bwd_partial_doubles": (I32, [I32, I32, I32]),
     "snnflow_unet_cell_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_unet_pack": (I32, [P, I32, I32, I32, I32, I64, I64, I64, I64, I32, P, I32, P]),
     "snnflow_unet_dec_in": (I32, [P, I32, I32, P, I32, I32, P, I32, I32, I32, P, I32, P]),

@@ -475,6 +475,13 @@ def lif_bwd(plan, P, g_out, g_state, state, prev_state, current, g3, g_prev, g_r
     if g_res is not None:
         a.g_res, a.gres_pitch = ptr(g_res), g_res.shape[-1]
     a.acc = ptr(plan.acc)
+    # per-block sums reduced in block order (deterministic; no fp64 atomic contention on 2C addresses)
+    n = int(lib.snnflow_unet_lif_bwd_partial_doubles(P, plan.C, a.gc_pitch))
+    part = plan.__dict__.get("lif_part")
+    if part is None or part.numel() < n or part.device != plan.acc.device:
+        part = torch.empty(n, dtype=torch.float64, device=plan.acc.device)
+        plan.lif_part = part
+    a.partial = ptr(part)
     _lib.call("unet_lif_bwd", lib.snnflow_unet_lif_bwd, ctypes.byref(a), s)
 
 

@@ -7,7 +7,7 @@ timeout -k 10 700 $T tests/test_gpu_unet.py tests/test_gpu_parity.py -k "unet or
 rc=$?
 tail -2 gpurun_out/t_unet3.log
 if [ $rc -ne 0 ]; then grep -E "^FAILED|^E " gpurun_out/t_unet3.log | head -20; exit $rc; fi
-for v in libsnnflow libsnnflow_unetns3; do
+for v in libsnnflow; do
   SNNFLOW_LIB=snn_event-based_optical_flow_amd/snnflow/$v.so SNNFLOW_UNET_SHAPES=1 timeout -k 10 400 python bench.py --model SpikingRecEVFlowNet --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/unet3_$v.json 2> gpurun_out/unet3_$v.err || { tail -20 gpurun_out/unet3_$v.err; exit 4; }
   python -c "
 import json;d=json.load(open('gpurun_out/unet3_$v.json'));k=d['kernels']
