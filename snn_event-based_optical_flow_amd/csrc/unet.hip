@@ -1485,13 +1485,15 @@ __global__ void k_unet_cell_param_grads(const double* acc, const float* leak, co
 // ---------------------------------------------------------------------------------------------
 // Packing, decoder input (upsample + concat), prediction layers
 // ---------------------------------------------------------------------------------------------
+template <typename I>
 __global__ void k_unet_pack(const float* __restrict__ src, int B, int H, int W, int C, int64_t sb, int64_t sc,
                             int64_t sh, int64_t sw, int split, uint16_t* __restrict__ dst, int cpitch) {
-    const int64_t n = (int64_t)B * H * W * cpitch;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        const int k = (int)(e % cpitch);
-        const int64_t pix = e / cpitch;
-        const int x = (int)(pix % W), y = (int)((pix / W) % H), b = (int)(pix / ((int64_t)W * H));
+    const I n = (I)B * H * W * cpitch;
+    for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
+        const int k = (int)(e % (I)cpitch);
+        const I pix = e / (I)cpitch;
+        const I py = pix / (I)W;
+        const int x = (int)(pix - py * (I)W), y = (int)(py % (I)H), b = (int)(py / (I)H);
         const int part = split ? k / C : (k < C ? 0 : 3);
         uint16_t o = 0;
         if (part < 3) {
@@ -1524,15 +1526,19 @@ __device__ inline void ld4bf(const uint16_t* p, float (&v)[4]) {
     v[0] = bf2f(u.x & 0xffff); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xffff); v[3] = bf2f(u.y >> 16);
 }
 
+// (I: the element index type -- 32-bit whenever the launch's element count allows: the index
+// divisions are then 32-bit, a fraction of the 64-bit emulation's instructions)
+template <typename I>
 __global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, const uint16_t* __restrict__ blk, int cb,
                               int pbp, const float* __restrict__ pred, int B, int h, int w, uint16_t* __restrict__ dst,
                               int cpitch) {
     const int H = 2 * h, W = 2 * w, Q = cpitch / 4;
-    const int64_t n = (int64_t)B * H * W * Q;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        const int k = (int)(e % Q) * 4;
-        const int64_t pix = e / Q;
-        const int X = (int)(pix % W), Y = (int)((pix / W) % H), b = (int)(pix / ((int64_t)W * H));
+    const I n = (I)B * H * W * Q;
+    for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
+        const int k = (int)(e % (I)Q) * 4;
+        const I pix = e / (I)Q;
+        const I py = pix / (I)W;
+        const int X = (int)(pix - py * (I)W), Y = (int)(py % (I)H), b = (int)(py / (I)H);
         const Lin ly = lin2(Y, h), lx = lin2(X, w);
         uint16_t o[4] = {0, 0, 0, 0};
         const uint16_t* src = nullptr;
@@ -1578,16 +1584,18 @@ __global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, c
 // weight of high-res coordinate D's interpolation on low-res index i
 __device__ inline float lin_w(const Lin& l, int i) { return (l.i0 == i ? l.l0 : 0.0f) + (l.i1 == i ? l.l1 : 0.0f); }
 
+template <typename I>
 __global__ void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb, int has_pred, int B, int h,
                                   int w, float* __restrict__ gx, int gxp, float* __restrict__ gb, int gbp,
                                   float* __restrict__ gpred) {
     const int H = 2 * h, W = 2 * w;
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
-    const int64_t n = (int64_t)B * h * w * Q;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        const int k = (int)(e % Q) * 4;
-        const int64_t pix = e / Q;
-        const int x = (int)(pix % w), y = (int)((pix / w) % h), b = (int)(pix / ((int64_t)w * h));
+    const I n = (I)B * h * w * Q;
+    for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
+        const int k = (int)(e % (I)Q) * 4;
+        const I pix = e / (I)Q;
+        const I pyy = pix / (I)w;
+        const int x = (int)(pix - pyy * (I)w), y = (int)(pyy % (I)h), b = (int)(pyy / (I)h);
         float s[4] = {0.f, 0.f, 0.f, 0.f};
         for (int Y = 2 * y - 1; Y <= 2 * y + 2; ++Y) {
             if (Y < 0 || Y >= H) continue;
@@ -1702,10 +1710,12 @@ __global__ __launch_bounds__(UNT) void k_unet_pred_bwd_x(const uint16_t* __restr
             w0[r] = wt[c0 + r];
             w1[r] = wt[C + c0 + r];
         }
+        const int hw = h * w;  // (< 2^31: checked by the host)
         for (int64_t p = (int64_t)blockIdx.x * ppi + pr; p < n; p += (int64_t)gridDim.x * ppi) {
-            const int xx = (int)(p % w), y = (int)((p / w) % h), b = (int)(p / ((int64_t)w * h));
-            const float g0 = gpre[((int64_t)b * 2 + 0) * h * w + (int64_t)y * w + xx];
-            const float g1 = gpre[((int64_t)b * 2 + 1) * h * w + (int64_t)y * w + xx];
+            // 32-bit index math: image b and in-image offset (the 64-bit divisions cost ~4x)
+            const uint32_t b = (uint32_t)p / (uint32_t)hw, r = (uint32_t)p - b * (uint32_t)hw;
+            const float g0 = gpre[((int64_t)b * 2 + 0) * hw + r];
+            const float g1 = gpre[((int64_t)b * 2 + 1) * hw + r];
             float v[4];
             ld4bf(x + p * cpitch + c0, v);
             float4* d = reinterpret_cast<float4*>(gx + p * gxp + c0);
@@ -2163,8 +2173,12 @@ int snnflow_unet_pack(const float* src, int B, int H, int W, int C, int64_t sb, 
     if (!src || !dst || B <= 0 || H <= 0 || W <= 0 || C <= 0 || cpitch % 32 != 0 || (split ? 3 * C : C) > cpitch)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_pack: bad args");
     const int64_t n = (int64_t)B * H * W * cpitch;
-    hipLaunchKernelGGL(k_unet_pack, dim3(grid1d(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src, B, H, W, C, sb,
-                       sc, sh, sw, split, dst, cpitch);
+    if (n < (1LL << 31))
+        hipLaunchKernelGGL(k_unet_pack<uint32_t>, dim3(grid1d(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src, B, H, W,
+                           C, sb, sc, sh, sw, split, dst, cpitch);
+    else
+        hipLaunchKernelGGL(k_unet_pack<int64_t>, dim3(grid1d(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src, B, H, W,
+                           C, sb, sc, sh, sw, split, dst, cpitch);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -2175,8 +2189,13 @@ int snnflow_unet_dec_in(const uint16_t* x, int cx, int px, const uint16_t* block
         cx + cb + (pred ? 6 : 0) > cpitch)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in: bad args");
     const int64_t n = (int64_t)B * 4 * h * w * (cpitch / 4);
-    hipLaunchKernelGGL(k_unet_dec_in, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, x, cx, px, block,
-                       cb, pb, pred, B, h, w, dst, cpitch);
+    // 32-bit element indices (and pixel * pitch offsets, <= 4 n) when they fit
+    if (n < (1LL << 30))
+        hipLaunchKernelGGL(k_unet_dec_in<uint32_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, x, cx,
+                           px, block, cb, pb, pred, B, h, w, dst, cpitch);
+    else
+        hipLaunchKernelGGL(k_unet_dec_in<int64_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, x, cx,
+                           px, block, cb, pb, pred, B, h, w, dst, cpitch);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -2188,8 +2207,13 @@ int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int h
         SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: bad args");
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
     const int64_t n = (int64_t)B * h * w * Q;
-    hipLaunchKernelGGL(k_unet_dec_in_bwd, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up, gpitch, cx,
-                       cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred);
+    const int64_t offs = (int64_t)B * h * w * (gx_pitch > gb_pitch ? gx_pitch : gb_pitch);
+    if (n < (1LL << 30) && offs < (1LL << 31))
+        hipLaunchKernelGGL(k_unet_dec_in_bwd<uint32_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
+                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred);
+    else
+        hipLaunchKernelGGL(k_unet_dec_in_bwd<int64_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
+                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -2209,7 +2233,7 @@ int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, 
                           const float* g_extra, int B, int h, int wd, int up, float* gpre, float* g_x, int gx_pitch,
                           double* acc, void* stream) {
     if (!x || !w || !flow || !gpre || !g_x || !acc || C <= 0 || C % 4 != 0 || C > 512 || B <= 0 || h <= 0 || wd <= 0 ||
-        up < 1 || gx_pitch % 4 != 0)
+        up < 1 || gx_pitch % 4 != 0 || (int64_t)B * h * wd >= (1LL << 31))
         SNN_FAIL(SNNFLOW_E_ARG, "unet_pred_bwd: bad args");
     const hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)B * h * wd;
