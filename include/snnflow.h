@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 25
+#define SNNFLOW_ABI_VERSION 26
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -660,6 +660,8 @@ typedef struct {
      * (deterministic, and no contention of ~2,000 blocks' fp64 atomics on 2*C addresses); NULL: the
      * blocks add to acc by fp64 atomics. */
     double* partial;
+    /* ABI 26: 1 = g_res is written (g_res = g_out: its first contribution), 0 = added to. */
+    int res_assign;
 } snnflow_unet_lif_bwd_args;
 int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream);
 int snnflow_unet_lif_bwd_partial_doubles(int P, int C, int gc_pitch);
@@ -679,9 +681,11 @@ int snnflow_unet_pack(const float* src, int B, int H, int W, int C, int64_t sb, 
 int snnflow_unet_dec_in(const uint16_t* x, int cx, int px, const uint16_t* block, int cb, int pb,
                         const float* pred, int B, int h, int w, uint16_t* dst, int cpitch, void* stream);
 /* Its backward from g_up fp32 [B][2h][2w][gpitch]: g_x [pix][gx_pitch] +=, g_block +=,
- * g_pred [B][2][h][w] = (the pred channels' gradient at its hi position). */
+ * g_pred [B][2][h][w] = (the pred channels' gradient at its hi position).  assign (ABI 26): bit 0
+ * writes g_x, bit 1 writes g_block (=, their first contribution; else +=). */
 int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int has_pred, int B, int h, int w,
-                            float* g_x, int gx_pitch, float* g_block, int gb_pitch, float* g_pred, void* stream);
+                            float* g_x, int gx_pitch, float* g_block, int gb_pitch, float* g_pred, int assign,
+                            void* stream);
 
 /* Prediction layer (submodules.py:96-113, 1x1 conv + bias + tanh, unet.py:351-365) and the
  * nearest upsample to the input resolution (model.py:840-850):
@@ -689,10 +693,11 @@ int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int h
 int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, const float* b, int B, int h,
                           int wd, int up, float* flow, float* flow_full, void* stream);
 /* g_pre = (1 - flow^2) * (sum of g_full over the s x s block + g_extra) into gpre [B][2][h][w];
- * g_x[pix][gx_pitch] += W^T g_pre; acc (fp64 [2C + 2]) += (dW, db) sums. */
+ * g_x[pix][gx_pitch] += W^T g_pre (assign, ABI 26: = instead of +=); acc (fp64 [2C + 2]) += (dW, db)
+ * sums. */
 int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, const float* flow,
                           const float* g_full, const float* g_extra, int B, int h, int wd, int up, float* gpre,
-                          float* g_x, int gx_pitch, double* acc, void* stream);
+                          float* g_x, int gx_pitch, double* acc, int assign, void* stream);
 int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

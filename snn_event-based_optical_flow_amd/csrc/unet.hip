@@ -1354,6 +1354,9 @@ __device__ inline float surrogate(float x, float w, int kind) {
     }
 }
 
+// One pixel's loads of k_unet_lif_bwd (a channel quad): issued one iteration ahead.
+struct LifBwdIn { float4 go, gsv, gsz, vp, zp, vo, I; };
+
 __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args a) {
     __shared__ float sums[2 * 512];
     const int tid = threadIdx.x;
@@ -1373,36 +1376,45 @@ __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args 
             const float t0 = a.thresh[c0 + r];
             th[r] = t0 < 0.01f ? 0.01f : t0;
         }
-    if (pr < ppi) {
-        for (int64_t p = (int64_t)blockIdx.x * ppi + pr; p < a.P; p += (int64_t)gridDim.x * ppi) {
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](int64_t p) {
+        LifBwdIn v = {z4, z4, z4, z4, z4, z4, z4};
+        const int64_t e0 = p * C + c0;
+        if (a.g_out) v.go = *reinterpret_cast<const float4*>(a.g_out + p * a.g_pitch + c0);
+        if (a.g_state) {
+            v.gsv = *reinterpret_cast<const float4*>(a.g_state + e0);
+            v.gsz = *reinterpret_cast<const float4*>(a.g_state + plane + e0);
+        }
+        if (a.prev_state) {
+            v.vp = *reinterpret_cast<const float4*>(a.prev_state + e0);
+            v.zp = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
+        }
+        v.vo = *reinterpret_cast<const float4*>(a.state + e0);
+        v.I = *reinterpret_cast<const float4*>(a.current + e0);
+        return v;
+    };
+    const int64_t stride = (int64_t)gridDim.x * ppi;
+    int64_t p = (int64_t)blockIdx.x * ppi + pr;
+    if (pr < ppi && quad >= CQ) {  // padding channels of the gradient planes
+        for (; p < a.P; p += stride) {
             uint16_t* gh = a.g_cur3 + p * a.gc_pitch + c0;
-            if (quad >= CQ) {  // padding channels of the gradient planes
 #pragma unroll
-                for (int k = 0; k < 3; ++k) *reinterpret_cast<uint2*>(gh + k * a.gc_part) = make_uint2(0u, 0u);
-                continue;
-            }
+            for (int k = 0; k < 3; ++k) *reinterpret_cast<uint2*>(gh + k * a.gc_part) = make_uint2(0u, 0u);
+        }
+    } else if (pr < ppi && p < a.P) {
+        LifBwdIn cur = load(p);
+        for (; p < a.P; p += stride) {
+            // the next pixel's loads go out before this one's stores (no aliasing between them)
+            LifBwdIn nxt = cur;
+            if (p + stride < a.P) nxt = load(p + stride);
             const int64_t e0 = p * C + c0;
-            float go[4] = {0.f, 0.f, 0.f, 0.f}, gsv[4] = {0.f, 0.f, 0.f, 0.f}, gsz[4] = {0.f, 0.f, 0.f, 0.f};
-            float vp[4] = {0.f, 0.f, 0.f, 0.f}, zp[4] = {0.f, 0.f, 0.f, 0.f};
-            if (a.g_out) {
-                const float4 t = *reinterpret_cast<const float4*>(a.g_out + p * a.g_pitch + c0);
-                go[0] = t.x; go[1] = t.y; go[2] = t.z; go[3] = t.w;
-            }
-            if (a.g_state) {
-                const float4 t = *reinterpret_cast<const float4*>(a.g_state + e0);
-                const float4 u = *reinterpret_cast<const float4*>(a.g_state + plane + e0);
-                gsv[0] = t.x; gsv[1] = t.y; gsv[2] = t.z; gsv[3] = t.w;
-                gsz[0] = u.x; gsz[1] = u.y; gsz[2] = u.z; gsz[3] = u.w;
-            }
-            if (a.prev_state) {
-                const float4 t = *reinterpret_cast<const float4*>(a.prev_state + e0);
-                const float4 u = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
-                vp[0] = t.x; vp[1] = t.y; vp[2] = t.z; vp[3] = t.w;
-                zp[0] = u.x; zp[1] = u.y; zp[2] = u.z; zp[3] = u.w;
-            }
-            const float4 vo4 = *reinterpret_cast<const float4*>(a.state + e0);
-            const float4 I4 = *reinterpret_cast<const float4*>(a.current + e0);
-            const float vo[4] = {vo4.x, vo4.y, vo4.z, vo4.w}, I[4] = {I4.x, I4.y, I4.z, I4.w};
+            const float go[4] = {cur.go.x, cur.go.y, cur.go.z, cur.go.w};
+            const float gsv[4] = {cur.gsv.x, cur.gsv.y, cur.gsv.z, cur.gsv.w};
+            const float gsz[4] = {cur.gsz.x, cur.gsz.y, cur.gsz.z, cur.gsz.w};
+            const float vp[4] = {cur.vp.x, cur.vp.y, cur.vp.z, cur.vp.w};
+            const float zp[4] = {cur.zp.x, cur.zp.y, cur.zp.z, cur.zp.w};
+            const float vo[4] = {cur.vo.x, cur.vo.y, cur.vo.z, cur.vo.w};
+            const float I[4] = {cur.I.x, cur.I.y, cur.I.z, cur.I.w};
             uint16_t hh[4], mm[4], ll[4];
             float gvp[4], gzp[4];
 #pragma unroll
@@ -1423,6 +1435,7 @@ __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args 
                     st[r] += -gxs - gv * zp[r];
                 }
             }
+            uint16_t* gh = a.g_cur3 + p * a.gc_pitch + c0;
             *reinterpret_cast<uint2*>(gh) = make_uint2((uint32_t)hh[0] | ((uint32_t)hh[1] << 16), (uint32_t)hh[2] | ((uint32_t)hh[3] << 16));
             *reinterpret_cast<uint2*>(gh + a.gc_part) =
                 make_uint2((uint32_t)mm[0] | ((uint32_t)mm[1] << 16), (uint32_t)mm[2] | ((uint32_t)mm[3] << 16));
@@ -1434,20 +1447,28 @@ __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args 
             }
             if (a.g_res) {
                 float4* gr = reinterpret_cast<float4*>(a.g_res + p * a.gres_pitch + c0);
-                const float4 o = *gr;
-                *gr = make_float4(o.x + go[0], o.y + go[1], o.z + go[2], o.w + go[3]);
+                if (a.res_assign) {
+                    *gr = cur.go;
+                } else {
+                    const float4 o = *gr;
+                    *gr = make_float4(o.x + go[0], o.y + go[1], o.z + go[2], o.w + go[3]);
+                }
             }
+            cur = nxt;
         }
-        if (quad < CQ)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                atomicAdd(&sums[c0 + r], st[r]);
-                atomicAdd(&sums[C + c0 + r], sl[r]);
-            }
     }
+    if (pr < ppi && quad < CQ)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            atomicAdd(&sums[c0 + r], st[r]);
+            atomicAdd(&sums[C + c0 + r], sl[r]);
+        }
     __syncthreads();
-    if (a.partial) {  // this block's sums; k_unet_lif_bwd_reduce adds the blocks in order
-        for (int i = tid; i < 2 * C; i += UNT) a.partial[(int64_t)i * gridDim.x + blockIdx.x] = (double)sums[i];
+    if (a.partial) {  // this block's sums; k_unet_lif_bwd_reduce adds the blocks in column order
+        // column: XCD-aware (the blocks of one XCD own consecutive columns, so each 64-B line of
+        // the [2C][blocks] buffer is completed in one L2 -- no partial-line write-backs)
+        const int col = xcd_remap(blockIdx.x, (int)gridDim.x);
+        for (int i = tid; i < 2 * C; i += UNT) a.partial[(int64_t)i * gridDim.x + col] = (double)sums[i];
     } else {
         for (int i = tid; i < 2 * C; i += UNT) atomicAdd(a.acc + i, (double)sums[i]);
     }
@@ -1587,7 +1608,7 @@ __device__ inline float lin_w(const Lin& l, int i) { return (l.i0 == i ? l.l0 : 
 template <typename I>
 __global__ void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb, int has_pred, int B, int h,
                                   int w, float* __restrict__ gx, int gxp, float* __restrict__ gb, int gbp,
-                                  float* __restrict__ gpred) {
+                                  float* __restrict__ gpred, int assign) {
     const int H = 2 * h, W = 2 * w;
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
     const I n = (I)B * h * w * Q;
@@ -1610,14 +1631,16 @@ __global__ void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int
                 s[0] += ww * g.x; s[1] += ww * g.y; s[2] += ww * g.z; s[3] += ww * g.w;
             }
         }
-        if (k < cx) {
-            float4* d = reinterpret_cast<float4*>(gx + pix * gxp + k);
-            const float4 o = *d;
-            *d = make_float4(o.x + s[0], o.y + s[1], o.z + s[2], o.w + s[3]);
-        } else if (k < cx + cb) {
-            float4* d = reinterpret_cast<float4*>(gb + pix * gbp + (k - cx));
-            const float4 o = *d;
-            *d = make_float4(o.x + s[0], o.y + s[1], o.z + s[2], o.w + s[3]);
+        if (k < cx + cb) {
+            const bool to_x = k < cx;
+            float4* d = to_x ? reinterpret_cast<float4*>(gx + pix * gxp + k)
+                             : reinterpret_cast<float4*>(gb + pix * gbp + (k - cx));
+            if (assign & (to_x ? 1 : 2)) {  // first contribution: no read of a zeroed buffer
+                *d = make_float4(s[0], s[1], s[2], s[3]);
+            } else {
+                const float4 o = *d;
+                *d = make_float4(o.x + s[0], o.y + s[1], o.z + s[2], o.w + s[3]);
+            }
         } else {  // pred channels: positions hi0, hi1 (mid / lo positions carry the same gradient)
             gpred[((int64_t)b * 2 + 0) * h * w + (int64_t)y * w + x] = s[0];
             gpred[((int64_t)b * 2 + 1) * h * w + (int64_t)y * w + x] = s[1];
@@ -1695,7 +1718,7 @@ __global__ void k_unet_pred_gpre(const float* __restrict__ flow, const float* __
 __global__ __launch_bounds__(UNT) void k_unet_pred_bwd_x(const uint16_t* __restrict__ x, int cpitch, int C,
                                                          const float* __restrict__ wt, const float* __restrict__ gpre,
                                                          int B, int h, int w, float* __restrict__ gx, int gxp,
-                                                         double* acc) {
+                                                         double* acc, int assign) {
     __shared__ float sw[2 * 512];
     const int tid = threadIdx.x, CQ = C / 4;
     const int ppi = UNT / CQ, quad = tid % CQ, pr = tid / CQ, c0 = quad * 4;
@@ -1719,7 +1742,7 @@ __global__ __launch_bounds__(UNT) void k_unet_pred_bwd_x(const uint16_t* __restr
             float v[4];
             ld4bf(x + p * cpitch + c0, v);
             float4* d = reinterpret_cast<float4*>(gx + p * gxp + c0);
-            const float4 o = *d;
+            const float4 o = assign ? make_float4(0.f, 0.f, 0.f, 0.f) : *d;
             *d = make_float4(o.x + (w0[0] * g0 + w1[0] * g1), o.y + (w0[1] * g0 + w1[1] * g1),
                              o.z + (w0[2] * g0 + w1[2] * g1), o.w + (w0[3] * g0 + w1[3] * g1));
 #pragma unroll
@@ -2138,14 +2161,21 @@ int snnflow_unet_wgrad_finalize(const float* dwk, int ktot, const int* kmap_inv,
     return 0;
 }
 
+// k_unet_lif_bwd's grid: at least LIF_BWD_ITERS pixel rounds per block (small deep levels: fewer,
+// fuller blocks and fewer partial sums), at most 2048 blocks
+constexpr int LIF_BWD_ITERS = 4;
+static int lif_bwd_blocks(int64_t P, int gc_pitch) {
+    const int ppi = UNT / (gc_pitch / 4);
+    return grid1d((P + ppi - 1) / ppi, LIF_BWD_ITERS, 2048);
+}
+
 int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream) {
     if (!a || a->P <= 0 || a->C <= 0 || a->C % 4 != 0 || a->C > 512 || !a->leak || !a->thresh || !a->state ||
         !a->current || !a->g_cur3 || !a->acc || a->gc_pitch % 32 != 0 || a->gc_pitch < a->C || a->gc_pitch > 1024 ||
         (a->g_out && a->g_pitch % 4 != 0) || (a->g_res && a->gres_pitch % 4 != 0) || a->surrogate < 0 ||
         a->surrogate > 3)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_lif_bwd: bad args");
-    const int ppi = UNT / (a->gc_pitch / 4);
-    const int nblk = grid1d((int64_t)a->P, ppi, 2048);
+    const int nblk = lif_bwd_blocks(a->P, a->gc_pitch);
     hipLaunchKernelGGL(k_unet_lif_bwd, dim3(nblk), dim3(UNT), 0, (hipStream_t)stream, *a);
     if (a->partial)
         hipLaunchKernelGGL(k_unet_lif_bwd_reduce, dim3(2 * a->C), dim3(UNT), 0, (hipStream_t)stream, a->partial, nblk,
@@ -2156,7 +2186,7 @@ int snnflow_unet_lif_bwd(const snnflow_unet_lif_bwd_args* a, void* stream) {
 
 int snnflow_unet_lif_bwd_partial_doubles(int P, int C, int gc_pitch) {
     if (P <= 0 || C <= 0 || gc_pitch < 4) return 0;
-    return grid1d((int64_t)P, UNT / (gc_pitch / 4), 2048) * 2 * C;
+    return lif_bwd_blocks(P, gc_pitch) * 2 * C;
 }
 
 int snnflow_unet_cell_param_grads(const double* acc, const float* leak, const float* thresh, int C, int accumulate,
@@ -2201,7 +2231,7 @@ int snnflow_unet_dec_in(const uint16_t* x, int cx, int px, const uint16_t* block
 }
 
 int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int has_pred, int B, int h, int w, float* g_x,
-                            int gx_pitch, float* g_block, int gb_pitch, float* g_pred, void* stream) {
+                            int gx_pitch, float* g_block, int gb_pitch, float* g_pred, int assign, void* stream) {
     if (!g_up || !g_x || !g_block || (has_pred && !g_pred) || B <= 0 || h <= 0 || w <= 0 || cx % 4 != 0 ||
         cb % 4 != 0 || gpitch % 4 != 0 || gx_pitch % 4 != 0 || gb_pitch % 4 != 0)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: bad args");
@@ -2210,10 +2240,10 @@ int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int h
     const int64_t offs = (int64_t)B * h * w * (gx_pitch > gb_pitch ? gx_pitch : gb_pitch);
     if (n < (1LL << 30) && offs < (1LL << 31))
         hipLaunchKernelGGL(k_unet_dec_in_bwd<uint32_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
-                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred);
+                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign);
     else
         hipLaunchKernelGGL(k_unet_dec_in_bwd<int64_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
-                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred);
+                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -2231,7 +2261,7 @@ int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, 
 
 int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, const float* flow, const float* g_full,
                           const float* g_extra, int B, int h, int wd, int up, float* gpre, float* g_x, int gx_pitch,
-                          double* acc, void* stream) {
+                          double* acc, int assign, void* stream) {
     if (!x || !w || !flow || !gpre || !g_x || !acc || C <= 0 || C % 4 != 0 || C > 512 || B <= 0 || h <= 0 || wd <= 0 ||
         up < 1 || gx_pitch % 4 != 0 || (int64_t)B * h * wd >= (1LL << 31))
         SNN_FAIL(SNNFLOW_E_ARG, "unet_pred_bwd: bad args");
@@ -2241,7 +2271,7 @@ int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, 
                        gpre, acc, C);
     const int ppi = UNT / (C / 4);
     hipLaunchKernelGGL(k_unet_pred_bwd_x, dim3(grid1d(n, ppi, 2048)), dim3(UNT), 0, s, x, cpitch, C, w, gpre, B, h, wd,
-                       g_x, gx_pitch, acc);
+                       g_x, gx_pitch, acc, assign);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 25
+ABI_VERSION = 26
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -195,7 +195,8 @@ class UNetLifBwdArgs(ctypes.Structure):
     _fields_ = [("P", I32), ("C", I32), ("leak", P), ("thresh", P), ("width", F32), ("hard_reset", I32),
                 ("detach", I32), ("surrogate", I32), ("g_out", P), ("g_pitch", I32), ("g_state", P),
                 ("state", P), ("prev_state", P), ("current", P), ("g_cur3", P), ("gc_pitch", I32),
-                ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P), ("partial", P)]
+                ("gc_part", I64), ("g_prev", P), ("g_res", P), ("gres_pitch", I32), ("acc", P), ("partial", P),
+                ("res_assign", I32)]
 
 
 MAX_LAYERS = 8
@@ -316,9 +317,9 @@ EXPORTS = {
     "snnflow_unet_cell_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_unet_pack": (I32, [P, I32, I32, I32, I32, I64, I64, I64, I64, I32, P, I32, P]),
     "snnflow_unet_dec_in": (I32, [P, I32, I32, P, I32, I32, P, I32, I32, I32, P, I32, P]),
-    "snnflow_unet_dec_in_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P]),
+    "snnflow_unet_dec_in_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, P]),
     "snnflow_unet_pred_fwd": (I32, [P, I32, I32, P, P, I32, I32, I32, I32, P, P, P]),
-    "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, P]),
+    "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, I32, P]),
     "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
     "snnflow_firenet_fwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetFwdIo), P]),
     "snnflow_firenet_bwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), P]),

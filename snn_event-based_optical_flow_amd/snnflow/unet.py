@@ -461,7 +461,7 @@ def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
               work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
 
 
-def lif_bwd(plan, P, g_out, g_state, state, prev_state, current, g3, g_prev, g_res, s):
+def lif_bwd(plan, P, g_out, g_state, state, prev_state, current, g3, g_prev, g_res, s, res_assign=False):
     m = plan.mod
     a = _lib.UNetLifBwdArgs()
     a.P, a.C = P, plan.C
@@ -474,6 +474,7 @@ def lif_bwd(plan, P, g_out, g_state, state, prev_state, current, g3, g_prev, g_r
     a.g_prev = ptr(g_prev)
     if g_res is not None:
         a.g_res, a.gres_pitch = ptr(g_res), g_res.shape[-1]
+        a.res_assign = 1 if res_assign else 0
     a.acc = ptr(plan.acc)
     # per-block sums reduced in block order (deterministic; no fp64 atomic contention on 2C addresses)
     n = int(lib.snnflow_unet_lif_bwd_partial_doubles(P, plan.C, a.gc_pitch))
@@ -762,7 +763,9 @@ class UNetStep(torch.autograd.Function):
             eng.open_window()
         keys = [f"e{i}{c}" for i in range(4) for c in "cr"] + [f"r{j}{c}" for j in range(len(eng.res)) for c in "ab"]
         keys += [f"d{i}" for i in range(4)]
-        gacts = {k: torch.zeros(S.acts[k].shape, device=dev) for k in keys}  # dL/d act (fp32, act layout)
+        # dL/d act (fp32, act layout), not zero-filled: each buffer's first contribution is written
+        # (assign / accumulate=False), the later ones added
+        gacts = {k: torch.empty(S.acts[k].shape, device=dev) for k in keys}
         g_prev_out = [None] * len(g_states)
 
         def gstate_cell(i, cell, C, h, w):
@@ -792,7 +795,7 @@ class UNetStep(torch.autograd.Function):
                 gf = gf.float().contiguous()
             _lib.call("unet_pred_bwd", lib.snnflow_unet_pred_bwd, ptr(act), act.shape[-1], C, ptr(pw.weight),
                       ptr(S.flows_lo[i]), ptr(gf), ptr(g_extra), B, h2, w2, H // h2, ptr(gpre), ptr(gacts[f"d{i}"]),
-                      gacts[f"d{i}"].shape[-1], ptr(eng.pred_acc[i]), s)
+                      gacts[f"d{i}"].shape[-1], ptr(eng.pred_acc[i]), 1 if i == 3 else 0, s)
             g3 = g3_buf(P, C)
             gp = torch.empty(1, 2, P, C, device=dev)
             st = S.states[6 + i]
@@ -807,7 +810,7 @@ class UNetStep(torch.autograd.Function):
             gb = gacts[f"e{3 - i}r"]
             g_extra = torch.empty(B, 2, h, w, device=dev) if d.has_pred else None
             _lib.call("unet_dec_in_bwd", lib.snnflow_unet_dec_in_bwd, ptr(gup), din.shape[-1], d.cx, d.cx,
-                      1 if d.has_pred else 0, B, h, w, ptr(gx), gx.shape[-1], ptr(gb), gb.shape[-1], ptr(g_extra), s)
+                      1 if d.has_pred else 0, B, h, w, ptr(gx), gx.shape[-1], ptr(gb), gb.shape[-1], ptr(g_extra), 3, s)
         # residual blocks, last first
         h, w = H // 16, W // 16
         for j in range(len(eng.res) - 1, -1, -1):
@@ -818,9 +821,9 @@ class UNetStep(torch.autograd.Function):
             xin_key = "r0b" if j == 1 else "e3r"
             g3 = g3_buf(P, C)
             lif_bwd(pb, P, gacts[f"r{j}b"], gstate_cell(4 + j, 1, C, h, w), st[1], S.prev[4 + j][1], S.cur[4 + j][1],
-                    g3, gp[1], gacts[xin_key], s)
+                    g3, gp[1], gacts[xin_key], s, res_assign=xin_key != "e3r")
             wgrad(pb, pb.segs[0], g3, B, h, w, S.acts[f"r{j}a"], s)
-            conv_dgrad(pb, pb.segs[0], g3.view(3, B, h, w, -1), B, h, w, gacts[f"r{j}a"], pad32(C), pad32(C), True, s)
+            conv_dgrad(pb, pb.segs[0], g3.view(3, B, h, w, -1), B, h, w, gacts[f"r{j}a"], pad32(C), pad32(C), False, s)
             g3 = g3_buf(P, C)
             lif_bwd(pa, P, gacts[f"r{j}a"], gstate_cell(4 + j, 0, C, h, w), st[0], S.prev[4 + j][0], S.cur[4 + j][0],
                     g3, gp[0], None, s)
@@ -843,7 +846,7 @@ class UNetStep(torch.autograd.Function):
                 wgrad(pr, pr.segs[1], g3, B, h, w, zp, s)
                 # previous spikes feed the recurrent conv before the reset detach (spiking_submodules.py:279, 288-289)
                 conv_dgrad(pr, pr.segs[1], g3.view(3, B, h, w, -1), B, h, w, gp[1, 1], C, C, True, s)
-            conv_dgrad(pr, pr.segs[0], g3.view(3, B, h, w, -1), B, h, w, gacts[f"e{i}c"], pad32(C), pad32(C), True, s)
+            conv_dgrad(pr, pr.segs[0], g3.view(3, B, h, w, -1), B, h, w, gacts[f"e{i}c"], pad32(C), pad32(C), False, s)
             g3 = g3_buf(P, C)
             lif_bwd(pc, P, gacts[f"e{i}c"], gstate_cell(i, 0, C, h, w), st[0], S.prev[i][0], S.cur[i][0], g3, gp[0],
                     None, s)
