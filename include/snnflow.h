@@ -417,9 +417,11 @@ typedef struct snnflow_iwe_loss_args {
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
 /* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch
- * [2][4][B][H*W]. */
+ * [2][4][B][H*W].  gev (ABI 26, optional): scratch [B][M][2] floats; with it the per-event flow
+ * gradients are stored, then summed per pixel in exact two-word fixed point (order-independent:
+ * bit-reproducible g_flows); NULL: fp32 atomics into g_flows (order-dependent rounding). */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
-                         float* g_flows, void* stream);
+                         float* g_flows, float* gev, void* stream);
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf);
 int snnflow_iwe_scratch_floats(int B, int H, int W);  /* floats of the images scratch */
 
@@ -694,10 +696,12 @@ int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, 
                           int wd, int up, float* flow, float* flow_full, void* stream);
 /* g_pre = (1 - flow^2) * (sum of g_full over the s x s block + g_extra) into gpre [B][2][h][w];
  * g_x[pix][gx_pitch] += W^T g_pre (assign, ABI 26: = instead of +=); acc (fp64 [2C + 2]) += (dW, db)
- * sums. */
+ * sums.  partial (ABI 26, optional): workspace of snnflow_unet_pred_bwd_partial_doubles doubles; with
+ * it the blocks' sums are added to acc in a fixed order (bit-reproducible), else by fp64 atomics. */
 int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, const float* flow,
                           const float* g_full, const float* g_extra, int B, int h, int wd, int up, float* gpre,
-                          float* g_x, int gx_pitch, double* acc, int assign, void* stream);
+                          float* g_x, int gx_pitch, double* acc, int assign, double* partial, void* stream);
+int snnflow_unet_pred_bwd_partial_doubles(int B, int h, int wd, int C);
 int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

@@ -461,7 +461,7 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
 constexpr int kBwdLanes = 8;
 
 __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
-                                                      float* g_flows) {
+                                                      float* g_flows, float* gev) {
     const int64_t HWp = (int64_t)a.H * a.W;
     const int64_t n = (int64_t)a.B * a.M;
     const int64_t img = (int64_t)a.B * HWp;
@@ -507,10 +507,57 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
         gfy += __shfl_xor(gfy, 4, 64);
         gfx += __shfl_xor(gfx, 4, 64);
         if (sub == 0) {
-            float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
-            if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
-            if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
+            if (gev) {  // summed per pixel by k_iwe_bwd_scatter
+                *reinterpret_cast<float2*>(gev + 2 * e) = make_float2(gfx, gfy);
+            } else {
+                float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+                if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
+                if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
+            }
         }
+    }
+}
+
+// Per-pixel sums of the per-event flow gradients (an event scatters into its own pixel): one block
+// per (sample, flow window, band of SPLAT_BAND pixels) scans the window's events, adds those of its
+// band into LDS in exact two-word fixed point (SplatLdsX: integer adds, so the sum does not depend on
+// the order of the events), then adds each touched pixel's total to g_flows once.
+struct GevLds {
+    unsigned long long hi[2][SPLAT_BAND], lo[2][SPLAT_BAND];
+};
+
+__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_args a, const float* __restrict__ gev,
+                                                              float* g_flows, int nbands) {
+    __shared__ GevLds img;
+    const int tid = threadIdx.x;
+    const int band = blockIdx.x % nbands, rest = blockIdx.x / nbands, t = rest % a.tf, b = rest / a.tf;
+    const int64_t HWp = (int64_t)a.H * a.W;
+    const int p0 = band * SPLAT_BAND;
+    const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
+    for (int j = tid; j < 2 * SPLAT_BAND; j += SPLAT_NT) (&img.hi[0][0])[j] = 0, (&img.lo[0][0])[j] = 0;
+    __syncthreads();
+    const int i0 = a.tf == 1 ? 0 : a.off[t], i1 = a.tf == 1 ? a.M : a.off[t + 1];
+    for (int i = i0 + tid; i < i1; i += SPLAT_NT) {
+        const EventRef r = event_ref(a, b, i);
+        const int q = (int)(r.ev[1] * (float)a.W + r.ev[2]) - p0;
+        if (q < 0 || q >= np) continue;
+        const float2 g = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i));
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const double d = (double)(c == 0 ? g.x : g.y);
+            if (d == 0.0) continue;
+            const double h = rint(d * 0x1p32);
+            const long long l = (long long)rint((d - h * 0x1p-32) * 0x1p75);
+            atomicAdd(&img.hi[c][q], (unsigned long long)(long long)h);
+            if (l != 0) atomicAdd(&img.lo[c][q], (unsigned long long)l);
+        }
+    }
+    __syncthreads();
+    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
+    for (int j = tid; j < 2 * np; j += SPLAT_NT) {
+        const int c = j / np, q = j - c * np;
+        const unsigned long long h = img.hi[c][q], l = img.lo[c][q];
+        if (h | l) gf[c * HWp + q] += (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75);
     }
 }
 
@@ -640,7 +687,7 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     return 0;
 }
 
-int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows,
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows, float* gev,
                          void* stream) {
     if (int rc = check_loss_args(a)) return rc;
     if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
@@ -649,9 +696,14 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
     hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
                        chunks, tsplit);
-    if (a->M > 0)
+    if (a->M > 0) {
         hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s, *a, gimg,
-                           g_flows);
+                           g_flows, gev);
+        if (gev) {
+            const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
+            hipLaunchKernelGGL(k_iwe_bwd_scatter, dim3(a->B * a->tf * nbands), dim3(SPLAT_NT), 0, s, *a, gev, g_flows, nbands);
+        }
+    }
     SNN_CHECK_LAUNCH();
     return 0;
 }

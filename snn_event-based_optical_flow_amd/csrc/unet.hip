@@ -1106,10 +1106,23 @@ __global__ void k_unet_wgrad_reduce(snnflow_unet_wgrad_args a, int nsplit, int K
 // every lane addressing its own pixel row, so a tap is an offset of those rows.
 // 4 waves as WK x WM, each NI x NJ 16x16 tiles of every tap (9 * NI * NJ accumulators).
 // ---------------------------------------------------------------------------------------------
+// LDS rows of the tap-fused weight gradient: 32-B chunks (16 bf16) XOR-swizzled by bits of the row
+// so that a ds_read_b64_tr_b16 half-wave (8 pixel rows {n..n+3, n+d..n+d+3}, 32 B each; d = 8 at
+// stride 1, rows doubled at stride 2) covers all 64 banks once (exhaustive search over pads and
+// row-bit XOR masks, every strip width 16..64; width 8 keeps <= 2-way).  Stride 2 pads X rows by one
+// chunk.
+template <int NCH, int S>
+__device__ __forceinline__ int wr_swz(int row) {
+    if constexpr (NCH == 2) return (row >> (S == 1 ? 3 : 4)) & 1;
+    else return ((row >> 1) & 1) | (((row >> (S == 1 ? 3 : 4)) & 1) << 1);
+}
+
 template <int NI, int NJ, int WK, int WM, int S>
 struct WrGeo {
     static constexpr int TK = 16 * NI * WK, TM = 16 * NJ * WM;
-    static constexpr int XS = TK + 8, GS = TM + 8;    // bf16 per LDS pixel row (16-B multiple)
+    static constexpr int XCH = TK / 16, GCH = TM / 16;  // 32-B chunks per row
+    static_assert((XCH == 2 || XCH == 4) && (GCH == 2 || GCH == 4), "wgrad_rows: 2 or 4 chunks per row");
+    static constexpr int XS = TK + (S == 2 ? 16 : 0), GS = TM;  // bf16 per LDS pixel row
     static constexpr int XPIX = S == 1 ? 198 : 387;   // halo pixels, largest strip shape (TW 64)
     static constexpr int XQ = TK / 8, GQ = TM / 8;     // 16-B pieces per pixel
     static constexpr int GPIECES = 3 * 64 * GQ;
@@ -1194,7 +1207,8 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             const int e = tid + r * UNT;
             if (e < xpieces) {
                 const int pix = e / G::XQ, c8 = e - pix * G::XQ;
-                *reinterpret_cast<uint4*>(&Xs[pix * XS + 8 * c8]) = xr[r];
+                *reinterpret_cast<uint4*>(&Xs[pix * XS + (((c8 >> 1) ^ wr_swz<G::XCH, S>(pix)) << 4) + 8 * (c8 & 1)]) =
+                    xr[r];
             }
         }
 #pragma unroll
@@ -1202,7 +1216,8 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             const int e = tid + r * UNT;
             if (e < G::GPIECES) {
                 const int part = e / (64 * G::GQ), rem = e - part * (64 * G::GQ), j = rem / G::GQ, c8 = rem - j * G::GQ;
-                *reinterpret_cast<uint4*>(&Gs[(part * 64 + j) * GS + 8 * c8]) = gr[r];
+                const int row = part * 64 + j;
+                *reinterpret_cast<uint4*>(&Gs[row * GS + (((c8 >> 1) ^ wr_swz<G::GCH, 1>(row)) << 4) + 8 * (c8 & 1)]) = gr[r];
             }
         }
     };
@@ -1231,8 +1246,9 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             for (int part = 0; part < 3; ++part)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    const __bf16* r0 = &Gs[(part * 64 + gp) * GS + wm * (TM / WM) + j * 16 + 4 * pp];
-                    bgf[part][j] = tr_pair(r0, r0 + 4 * GS);
+                    const int ch = (wm * (TM / WM)) / 16 + j, row0 = part * 64 + gp, row1 = row0 + 4;
+                    bgf[part][j] = tr_pair(&Gs[row0 * GS + ((ch ^ wr_swz<G::GCH, 1>(row0)) << 4) + 4 * pp],
+                                           &Gs[row1 * GS + ((ch ^ wr_swz<G::GCH, 1>(row1)) << 4) + 4 * pp]);
                 }
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
@@ -1240,10 +1256,12 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
                 for (int kx = 0; kx < 3; ++kx) {
                     const int toff = ky * XW + kx;
                     bf16x8 axf[NI];
+                    const int xr0 = xrow[kk][0] + toff, xr1 = xrow[kk][1] + toff;
+                    const int sw0 = wr_swz<G::XCH, S>(xr0), sw1 = wr_swz<G::XCH, S>(xr1);
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
-                        const int col = wk * (TK / WK) + i * 16 + 4 * pp;
-                        axf[i] = tr_pair(&Xs[(xrow[kk][0] + toff) * XS + col], &Xs[(xrow[kk][1] + toff) * XS + col]);
+                        const int ch = (wk * (TK / WK)) / 16 + i;
+                        axf[i] = tr_pair(&Xs[xr0 * XS + ((ch ^ sw0) << 4) + 4 * pp], &Xs[xr1 * XS + ((ch ^ sw1) << 4) + 4 * pp]);
                     }
 #pragma unroll
                     for (int part = 2; part >= 0; --part)  // lo, mid, hi
@@ -1358,13 +1376,11 @@ __device__ inline float surrogate(float x, float w, int kind) {
 struct LifBwdIn { float4 go, gsv, gsz, vp, zp, vo, I; };
 
 __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args a) {
-    __shared__ float sums[2 * 512];
+    __shared__ float red[2 * UNT * 4];  // [pixel row][2C] thread sums (ppi * C <= UNT * 4)
     const int tid = threadIdx.x;
     const int C = a.C, PQ = a.gc_pitch / 4, CQ = C / 4;
     const int ppi = UNT / PQ;  // pixels per block iteration
     const int quad = tid % PQ, pr = tid / PQ;
-    for (int i = tid; i < 2 * C; i += UNT) sums[i] = 0.0f;
-    __syncthreads();
     const int64_t plane = (int64_t)a.P * C;
     float st[4] = {0.f, 0.f, 0.f, 0.f}, sl[4] = {0.f, 0.f, 0.f, 0.f};
     const int c0 = quad * 4;
@@ -1460,17 +1476,21 @@ __global__ __launch_bounds__(UNT) void k_unet_lif_bwd(snnflow_unet_lif_bwd_args 
     if (pr < ppi && quad < CQ)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            atomicAdd(&sums[c0 + r], st[r]);
-            atomicAdd(&sums[C + c0 + r], sl[r]);
+            red[pr * 2 * C + c0 + r] = st[r];
+            red[pr * 2 * C + C + c0 + r] = sl[r];
         }
     __syncthreads();
-    if (a.partial) {  // this block's sums; k_unet_lif_bwd_reduce adds the blocks in column order
-        // column: XCD-aware (the blocks of one XCD own consecutive columns, so each 64-B line of
-        // the [2C][blocks] buffer is completed in one L2 -- no partial-line write-backs)
-        const int col = xcd_remap(blockIdx.x, (int)gridDim.x);
-        for (int i = tid; i < 2 * C; i += UNT) a.partial[(int64_t)i * gridDim.x + col] = (double)sums[i];
-    } else {
-        for (int i = tid; i < 2 * C; i += UNT) atomicAdd(a.acc + i, (double)sums[i]);
+    // the block's sums in a fixed order (pixel rows in sequence: bit-reproducible, unlike LDS atomics)
+    for (int i = tid; i < 2 * C; i += UNT) {
+        float v = 0.0f;
+        for (int q = 0; q < ppi; ++q) v += red[q * 2 * C + i];
+        if (a.partial) {  // this block's sums; k_unet_lif_bwd_reduce adds the blocks in column order
+            // column: XCD-aware (the blocks of one XCD own consecutive columns, so each 64-B line of
+            // the [2C][blocks] buffer is completed in one L2 -- no partial-line write-backs)
+            a.partial[(int64_t)i * gridDim.x + xcd_remap(blockIdx.x, (int)gridDim.x)] = (double)v;
+        } else {
+            atomicAdd(a.acc + i, (double)v);
+        }
     }
 }
 
@@ -1506,25 +1526,35 @@ __global__ void k_unet_cell_param_grads(const double* acc, const float* leak, co
 // ---------------------------------------------------------------------------------------------
 // Packing, decoder input (upsample + concat), prediction layers
 // ---------------------------------------------------------------------------------------------
+// one thread per (pixel, 8 consecutive act channels): one 16-B store, source reads coalesced along
+// x (NCHW) or along the channels (NHWC)
 template <typename I>
 __global__ void k_unet_pack(const float* __restrict__ src, int B, int H, int W, int C, int64_t sb, int64_t sc,
                             int64_t sh, int64_t sw, int split, uint16_t* __restrict__ dst, int cpitch) {
-    const I n = (I)B * H * W * cpitch;
+    const int G = cpitch / 8;
+    const I n = (I)B * H * W * G;
     for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
-        const int k = (int)(e % (I)cpitch);
-        const I pix = e / (I)cpitch;
+        const int g = (int)(e % (I)G);
+        const I pix = e / (I)G;
         const I py = pix / (I)W;
         const int x = (int)(pix - py * (I)W), y = (int)(py % (I)H), b = (int)(py / (I)H);
-        const int part = split ? k / C : (k < C ? 0 : 3);
-        uint16_t o = 0;
-        if (part < 3) {
-            const int c = split ? k - part * C : k;
-            const float v = src[b * sb + c * sc + y * sh + x * sw];
-            uint16_t h, m, l;
-            split3(v, h, m, l);
-            o = split ? (part == 0 ? h : (part == 1 ? m : l)) : h;
+        const float* sp = src + b * sb + y * sh + x * sw;
+        uint16_t o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = 8 * g + j;
+            const int part = split ? k / C : (k < C ? 0 : 3);
+            o[j] = 0;
+            if (part < 3) {
+                const float v = sp[(split ? k - part * C : k) * sc];
+                uint16_t hh, mm, ll;
+                split3(v, hh, mm, ll);
+                o[j] = split ? (part == 0 ? hh : (part == 1 ? mm : ll)) : hh;
+            }
         }
-        dst[e] = o;
+        *reinterpret_cast<uint4*>(dst + pix * cpitch + 8 * g) =
+            make_uint4((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16),
+                       (uint32_t)o[4] | ((uint32_t)o[5] << 16), (uint32_t)o[6] | ((uint32_t)o[7] << 16));
     }
 }
 
@@ -1549,18 +1579,36 @@ __device__ inline void ld4bf(const uint16_t* p, float (&v)[4]) {
 
 // (I: the element index type -- 32-bit whenever the launch's element count allows: the index
 // divisions are then 32-bit, a fraction of the 64-bit emulation's instructions)
-template <typename I>
-__global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, const uint16_t* __restrict__ blk, int cb,
-                              int pbp, const float* __restrict__ pred, int B, int h, int w, uint16_t* __restrict__ dst,
-                              int cpitch) {
+// Row-oriented decoder input: block = (output row b*H + Y, chunk of DEC_CHUNK (X, channel quad)
+// elements of it), the row's vertical interpolation uniform; blocks of one XCD take consecutive
+// rows (their low-res rows shared in that XCD's L2).  (X, quad) from the in-row index by a float
+// reciprocal with a +-1 correction (exact for in-row indices < 2^24).
+constexpr int DEC_CHUNK = 1024;
+
+__device__ inline void row_split(int e, int Q, float invQ, int& X, int& q) {
+    X = (int)((float)e * invQ);
+    q = e - X * Q;
+    if (q < 0) { --X; q += Q; } else if (q >= Q) { ++X; q -= Q; }
+}
+
+__global__ __launch_bounds__(256) void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp,
+                                                     const uint16_t* __restrict__ blk, int cb, int pbp,
+                                                     const float* __restrict__ pred, int B, int h, int w,
+                                                     uint16_t* __restrict__ dst, int cpitch, int nchunk) {
     const int H = 2 * h, W = 2 * w, Q = cpitch / 4;
-    const I n = (I)B * H * W * Q;
-    for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
-        const int k = (int)(e % (I)Q) * 4;
-        const I pix = e / (I)Q;
-        const I py = pix / (I)W;
-        const int X = (int)(pix - py * (I)W), Y = (int)(py % (I)H), b = (int)(py / (I)H);
-        const Lin ly = lin2(Y, h), lx = lin2(X, w);
+    const int lin = xcd_remap(blockIdx.x, (int)gridDim.x);
+    const int row = lin / nchunk, chunk = lin - row * nchunk;
+    const int b = row / H, Y = row - b * H;
+    const Lin ly = lin2(Y, h);
+    const int64_t r0 = ((int64_t)b * h + ly.i0) * w, r1 = ((int64_t)b * h + ly.i1) * w;
+    const float invQ = 1.0f / (float)Q;
+    const int e1 = min((chunk + 1) * DEC_CHUNK, W * Q);
+    uint16_t* drow = dst + (int64_t)row * W * cpitch;
+    for (int e = chunk * DEC_CHUNK + (int)threadIdx.x; e < e1; e += 256) {
+        int X, q;
+        row_split(e, Q, invQ, X, q);
+        const int k = 4 * q;
+        const Lin lx = lin2(X, w);
         uint16_t o[4] = {0, 0, 0, 0};
         const uint16_t* src = nullptr;
         int sp = 0, c = 0;
@@ -1571,7 +1619,6 @@ __global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, c
         }
         if (src) {
             float a00[4], a01[4], a10[4], a11[4];
-            const int64_t r0 = ((int64_t)b * h + ly.i0) * w, r1 = ((int64_t)b * h + ly.i1) * w;
             ld4bf(src + (r0 + lx.i0) * sp + c, a00);
             ld4bf(src + (r0 + lx.i1) * sp + c, a01);
             ld4bf(src + (r1 + lx.i0) * sp + c, a10);
@@ -1597,7 +1644,7 @@ __global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, c
                 o[0] = l0; o[1] = l1;
             }
         }
-        *reinterpret_cast<uint2*>(dst + pix * cpitch + k) =
+        *reinterpret_cast<uint2*>(drow + (int64_t)X * cpitch + k) =
             make_uint2((uint32_t)o[0] | ((uint32_t)o[1] << 16), (uint32_t)o[2] | ((uint32_t)o[3] << 16));
     }
 }
@@ -1605,32 +1652,49 @@ __global__ void k_unet_dec_in(const uint16_t* __restrict__ x, int cx, int pxp, c
 // weight of high-res coordinate D's interpolation on low-res index i
 __device__ inline float lin_w(const Lin& l, int i) { return (l.i0 == i ? l.l0 : 0.0f) + (l.i1 == i ? l.l1 : 0.0f); }
 
-template <typename I>
-__global__ void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb, int has_pred, int B, int h,
-                                  int w, float* __restrict__ gx, int gxp, float* __restrict__ gb, int gbp,
-                                  float* __restrict__ gpred, int assign) {
+// Row-oriented (as k_unet_dec_in): block = (low-res row b*h + y, chunk of its (x, quad) elements);
+// the four high-res rows it gathers and their weights uniform, consecutive rows on one XCD (each
+// high-res row is read by two low-res rows: the second read hits that XCD's L2).
+__global__ __launch_bounds__(256) void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb,
+                                                         int has_pred, int B, int h, int w, float* __restrict__ gx,
+                                                         int gxp, float* __restrict__ gb, int gbp,
+                                                         float* __restrict__ gpred, int assign, int nchunk) {
     const int H = 2 * h, W = 2 * w;
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
-    const I n = (I)B * h * w * Q;
-    for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
-        const int k = (int)(e % (I)Q) * 4;
-        const I pix = e / (I)Q;
-        const I pyy = pix / (I)w;
-        const int x = (int)(pix - pyy * (I)w), y = (int)(pyy % (I)h), b = (int)(pyy / (I)h);
+    const int lin = xcd_remap(blockIdx.x, (int)gridDim.x);
+    const int row = lin / nchunk, chunk = lin - row * nchunk;
+    const int b = row / h, y = row - b * h;
+    float wy[4];
+    const float* gr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int Y = 2 * y - 1 + j;
+        const bool ok = Y >= 0 && Y < H;
+        wy[j] = ok ? lin_w(lin2(Y, h), y) : 0.0f;
+        gr[j] = gup + ((int64_t)b * H + (ok ? Y : 0)) * W * gpitch;
+    }
+    const float invQ = 1.0f / (float)Q;
+    const int e1 = min((chunk + 1) * DEC_CHUNK, w * Q);
+    for (int e = chunk * DEC_CHUNK + (int)threadIdx.x; e < e1; e += 256) {
+        int x, q;
+        row_split(e, Q, invQ, x, q);
+        const int k = 4 * q;
         float s[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int Y = 2 * y - 1; Y <= 2 * y + 2; ++Y) {
-            if (Y < 0 || Y >= H) continue;
-            const float wy = lin_w(lin2(Y, h), y);
-            if (wy == 0.0f) continue;
-            for (int X = 2 * x - 1; X <= 2 * x + 2; ++X) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (wy[j] == 0.0f) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int X = 2 * x - 1 + i;
                 if (X < 0 || X >= W) continue;
                 const float wx = lin_w(lin2(X, w), x);
                 if (wx == 0.0f) continue;
-                const float4 g = *reinterpret_cast<const float4*>(gup + (((int64_t)b * H + Y) * W + X) * gpitch + k);
-                const float ww = wy * wx;
+                const float4 g = *reinterpret_cast<const float4*>(gr[j] + (int64_t)X * gpitch + k);
+                const float ww = wy[j] * wx;
                 s[0] += ww * g.x; s[1] += ww * g.y; s[2] += ww * g.z; s[3] += ww * g.w;
             }
         }
+        const int64_t pix = (int64_t)row * w + x;
         if (k < cx + cb) {
             const bool to_x = k < cx;
             float4* d = to_x ? reinterpret_cast<float4*>(gx + pix * gxp + k)
@@ -1679,12 +1743,10 @@ __global__ void k_unet_pred_fwd(const uint16_t* __restrict__ x, int cpitch, int 
 }
 
 // g_pre[b][ch][y][x] = (1 - f^2) * (sum of g_full over the up x up block + g_extra); db sums
-__global__ void k_unet_pred_gpre(const float* __restrict__ flow, const float* __restrict__ g_full,
+__global__ __launch_bounds__(256) void k_unet_pred_gpre(const float* __restrict__ flow, const float* __restrict__ g_full,
                                  const float* __restrict__ g_extra, int B, int h, int w, int up, float* __restrict__ gpre,
-                                 double* acc, int C) {
-    __shared__ float sb[2];
-    if (threadIdx.x < 2) sb[threadIdx.x] = 0.0f;
-    __syncthreads();
+                                 double* acc, int C, double* partial) {
+    __shared__ float sb[2][256];
     const int64_t n = (int64_t)B * h * w;
     float t0 = 0.0f, t1 = 0.0f;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
@@ -1708,22 +1770,33 @@ __global__ void k_unet_pred_gpre(const float* __restrict__ flow, const float* __
         t0 += gg[0];
         t1 += gg[1];
     }
-    atomicAdd(&sb[0], t0);
-    atomicAdd(&sb[1], t1);
+    // db sums: a fixed-order LDS tree, then per-block partials (reduced in column order) or atomics
+    const int tid = threadIdx.x;
+    sb[0][tid] = t0;
+    sb[1][tid] = t1;
     __syncthreads();
-    if (threadIdx.x < 2) atomicAdd(acc + 2 * C + threadIdx.x, (double)sb[threadIdx.x]);
+#pragma unroll
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            sb[0][tid] += sb[0][tid + o];
+            sb[1][tid] += sb[1][tid + o];
+        }
+        __syncthreads();
+    }
+    if (tid < 2) {
+        if (partial) partial[(int64_t)tid * gridDim.x + xcd_remap(blockIdx.x, (int)gridDim.x)] = (double)sb[tid][0];
+        else atomicAdd(acc + 2 * C + tid, (double)sb[tid][0]);
+    }
 }
 
 // g_x[pix][c] += W[0][c] g_pre0 + W[1][c] g_pre1; dW sums (2C)
 __global__ __launch_bounds__(UNT) void k_unet_pred_bwd_x(const uint16_t* __restrict__ x, int cpitch, int C,
                                                          const float* __restrict__ wt, const float* __restrict__ gpre,
                                                          int B, int h, int w, float* __restrict__ gx, int gxp,
-                                                         double* acc, int assign) {
-    __shared__ float sw[2 * 512];
+                                                         double* acc, int assign, double* partial) {
+    __shared__ float red[2 * UNT * 4];  // [pixel row][2C] thread sums
     const int tid = threadIdx.x, CQ = C / 4;
     const int ppi = UNT / CQ, quad = tid % CQ, pr = tid / CQ, c0 = quad * 4;
-    for (int i = tid; i < 2 * C; i += UNT) sw[i] = 0.0f;
-    __syncthreads();
     const int64_t n = (int64_t)B * h * w;
     float d0[4] = {0.f, 0.f, 0.f, 0.f}, d1[4] = {0.f, 0.f, 0.f, 0.f};
     if (pr < ppi) {
@@ -1753,12 +1826,17 @@ __global__ __launch_bounds__(UNT) void k_unet_pred_bwd_x(const uint16_t* __restr
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            atomicAdd(&sw[c0 + r], d0[r]);
-            atomicAdd(&sw[C + c0 + r], d1[r]);
+            red[pr * 2 * C + c0 + r] = d0[r];
+            red[pr * 2 * C + C + c0 + r] = d1[r];
         }
     }
     __syncthreads();
-    for (int i = tid; i < 2 * C; i += UNT) atomicAdd(acc + i, (double)sw[i]);
+    for (int i = tid; i < 2 * C; i += UNT) {  // fixed order over the block's pixel rows
+        float v = 0.0f;
+        for (int q = 0; q < ppi; ++q) v += red[q * 2 * C + i];
+        if (partial) partial[(int64_t)i * gridDim.x + xcd_remap(blockIdx.x, (int)gridDim.x)] = (double)v;
+        else atomicAdd(acc + i, (double)v);
+    }
 }
 
 __global__ void k_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b) {
@@ -2202,8 +2280,8 @@ int snnflow_unet_pack(const float* src, int B, int H, int W, int C, int64_t sb, 
                       int split, uint16_t* dst, int cpitch, void* stream) {
     if (!src || !dst || B <= 0 || H <= 0 || W <= 0 || C <= 0 || cpitch % 32 != 0 || (split ? 3 * C : C) > cpitch)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_pack: bad args");
-    const int64_t n = (int64_t)B * H * W * cpitch;
-    if (n < (1LL << 31))
+    const int64_t n = (int64_t)B * H * W * (cpitch / 8);
+    if ((int64_t)B * H * W * cpitch < (1LL << 31))
         hipLaunchKernelGGL(k_unet_pack<uint32_t>, dim3(grid1d(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, src, B, H, W,
                            C, sb, sc, sh, sw, split, dst, cpitch);
     else
@@ -2216,16 +2294,13 @@ int snnflow_unet_pack(const float* src, int B, int H, int W, int C, int64_t sb, 
 int snnflow_unet_dec_in(const uint16_t* x, int cx, int px, const uint16_t* block, int cb, int pb, const float* pred, int B,
                         int h, int w, uint16_t* dst, int cpitch, void* stream) {
     if (!x || !block || !dst || B <= 0 || h <= 0 || w <= 0 || cx % 4 != 0 || cb % 4 != 0 || cpitch % 32 != 0 ||
-        cx + cb + (pred ? 6 : 0) > cpitch)
+        cx + cb + (pred ? 6 : 0) > cpitch || (int64_t)2 * w * (cpitch / 4) >= (1LL << 24))
         SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in: bad args");
-    const int64_t n = (int64_t)B * 4 * h * w * (cpitch / 4);
-    // 32-bit element indices (and pixel * pitch offsets, <= 4 n) when they fit
-    if (n < (1LL << 30))
-        hipLaunchKernelGGL(k_unet_dec_in<uint32_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, x, cx,
-                           px, block, cb, pb, pred, B, h, w, dst, cpitch);
-    else
-        hipLaunchKernelGGL(k_unet_dec_in<int64_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, x, cx,
-                           px, block, cb, pb, pred, B, h, w, dst, cpitch);
+    const int nchunk = (2 * w * (cpitch / 4) + DEC_CHUNK - 1) / DEC_CHUNK;
+    const int64_t nblk = (int64_t)B * 2 * h * nchunk;
+    if (nblk >= (1LL << 31)) SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in: too large");
+    hipLaunchKernelGGL(k_unet_dec_in, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, cx, px, block, cb, pb,
+                       pred, B, h, w, dst, cpitch, nchunk);
     SNN_CHECK_LAUNCH();
     return 0;
 }
@@ -2236,16 +2311,22 @@ int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int h
         cb % 4 != 0 || gpitch % 4 != 0 || gx_pitch % 4 != 0 || gb_pitch % 4 != 0)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: bad args");
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
-    const int64_t n = (int64_t)B * h * w * Q;
-    const int64_t offs = (int64_t)B * h * w * (gx_pitch > gb_pitch ? gx_pitch : gb_pitch);
-    if (n < (1LL << 30) && offs < (1LL << 31))
-        hipLaunchKernelGGL(k_unet_dec_in_bwd<uint32_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
-                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign);
-    else
-        hipLaunchKernelGGL(k_unet_dec_in_bwd<int64_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
-                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign);
+    if ((int64_t)w * Q >= (1LL << 24)) SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: row too long");
+    const int nchunk = (w * Q + DEC_CHUNK - 1) / DEC_CHUNK;
+    const int64_t nblk = (int64_t)B * h * nchunk;
+    if (nblk >= (1LL << 31)) SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: too large");
+    hipLaunchKernelGGL(k_unet_dec_in_bwd, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, g_up, gpitch, cx, cb,
+                       has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign, nchunk);
     SNN_CHECK_LAUNCH();
     return 0;
+}
+
+// grids of the prediction backward: g_pre (one pixel per thread) and the channel pass (>= 4 pixel
+// rounds per block, as k_unet_lif_bwd)
+static void pred_bwd_blocks(int64_t n, int C, int& ng, int& nx) {
+    ng = grid1d(n, 256, 1024);
+    const int ppi = UNT / (C / 4);
+    nx = grid1d((n + ppi - 1) / ppi, 4, 2048);
 }
 
 int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, const float* b, int B, int h, int wd,
@@ -2261,19 +2342,32 @@ int snnflow_unet_pred_fwd(const uint16_t* x, int cpitch, int C, const float* w, 
 
 int snnflow_unet_pred_bwd(const uint16_t* x, int cpitch, int C, const float* w, const float* flow, const float* g_full,
                           const float* g_extra, int B, int h, int wd, int up, float* gpre, float* g_x, int gx_pitch,
-                          double* acc, int assign, void* stream) {
+                          double* acc, int assign, double* partial, void* stream) {
     if (!x || !w || !flow || !gpre || !g_x || !acc || C <= 0 || C % 4 != 0 || C > 512 || B <= 0 || h <= 0 || wd <= 0 ||
         up < 1 || gx_pitch % 4 != 0 || (int64_t)B * h * wd >= (1LL << 31))
         SNN_FAIL(SNNFLOW_E_ARG, "unet_pred_bwd: bad args");
     const hipStream_t s = (hipStream_t)stream;
     const int64_t n = (int64_t)B * h * wd;
-    hipLaunchKernelGGL(k_unet_pred_gpre, dim3(grid1d(n, 256, 1024)), dim3(256), 0, s, flow, g_full, g_extra, B, h, wd, up,
-                       gpre, acc, C);
-    const int ppi = UNT / (C / 4);
-    hipLaunchKernelGGL(k_unet_pred_bwd_x, dim3(grid1d(n, ppi, 2048)), dim3(UNT), 0, s, x, cpitch, C, w, gpre, B, h, wd,
-                       g_x, gx_pitch, acc, assign);
+    int ng, nx;
+    pred_bwd_blocks(n, C, ng, nx);
+    double* pg = partial;
+    double* px = partial ? partial + 2 * ng : nullptr;
+    hipLaunchKernelGGL(k_unet_pred_gpre, dim3(ng), dim3(256), 0, s, flow, g_full, g_extra, B, h, wd, up, gpre, acc, C, pg);
+    hipLaunchKernelGGL(k_unet_pred_bwd_x, dim3(nx), dim3(UNT), 0, s, x, cpitch, C, w, gpre, B, h, wd, g_x, gx_pitch, acc,
+                       assign, px);
+    if (partial) {  // the blocks' sums added in column order (bit-reproducible parameter gradients)
+        hipLaunchKernelGGL(k_unet_lif_bwd_reduce, dim3(2 * C), dim3(UNT), 0, s, px, nx, 2 * C, acc);
+        hipLaunchKernelGGL(k_unet_lif_bwd_reduce, dim3(2), dim3(UNT), 0, s, pg, ng, 2, acc + 2 * C);
+    }
     SNN_CHECK_LAUNCH();
     return 0;
+}
+
+int snnflow_unet_pred_bwd_partial_doubles(int B, int h, int wd, int C) {
+    if (B <= 0 || h <= 0 || wd <= 0 || C <= 0 || C % 4 != 0 || C > 512) return 0;
+    int ng, nx;
+    pred_bwd_blocks((int64_t)B * h * wd, C, ng, nx);
+    return 2 * ng + 2 * C * nx;
 }
 
 int snnflow_unet_pred_param_grads(const double* acc, int C, int accumulate, float* g_w, float* g_b, void* stream) {

@@ -285,7 +285,7 @@ EXPORTS = {
     "snnflow_convlif_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
-    "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P]),
+    "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P, P]),
     "snnflow_iwe_scratch_floats": (I32, [I32, I32, I32]),
     "snnflow_iwe_acc_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
@@ -319,7 +319,8 @@ EXPORTS = {
     "snnflow_unet_dec_in": (I32, [P, I32, I32, P, I32, I32, P, I32, I32, I32, P, I32, P]),
     "snnflow_unet_dec_in_bwd": (I32, [P, I32, I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, I32, P]),
     "snnflow_unet_pred_fwd": (I32, [P, I32, I32, P, P, I32, I32, I32, I32, P, P, P]),
-    "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, I32, P]),
+    "snnflow_unet_pred_bwd": (I32, [P, I32, I32, P, P, P, P, I32, I32, I32, I32, P, P, I32, P, I32, P, P]),
+    "snnflow_unet_pred_bwd_partial_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
     "snnflow_firenet_fwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetFwdIo), P]),
     "snnflow_firenet_bwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), P]),

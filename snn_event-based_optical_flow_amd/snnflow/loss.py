@@ -87,7 +87,10 @@ class EventWarpingFn(torch.autograd.Function):
         B, H, W = flows_c[0].shape[0], ctx.meta["H"], ctx.meta["W"]
         gimg = torch.empty(8 * B * H * W, device=dev)
         g_flows = torch.empty(B, len(flows_c), 2, H, W, device=dev)
-        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), s)
+        # per-event flow gradients, summed per pixel in fixed point (bit-reproducible g_flows)
+        gev = torch.empty(max(2 * B * a.M, 1), device=dev)
+        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), ptr(gev),
+                  s)
         return (None, None, None, *g_flows.unbind(1))
 
 

@@ -793,9 +793,13 @@ class UNetStep(torch.autograd.Function):
             gf = g_flows[i]
             if gf is not None:
                 gf = gf.float().contiguous()
+            npart = int(lib.snnflow_unet_pred_bwd_partial_doubles(B, h2, w2, C))
+            part = d.__dict__.get("pred_part")
+            if part is None or part.numel() < npart:
+                part = d.pred_part = torch.empty(npart, dtype=torch.float64, device=dev)
             _lib.call("unet_pred_bwd", lib.snnflow_unet_pred_bwd, ptr(act), act.shape[-1], C, ptr(pw.weight),
                       ptr(S.flows_lo[i]), ptr(gf), ptr(g_extra), B, h2, w2, H // h2, ptr(gpre), ptr(gacts[f"d{i}"]),
-                      gacts[f"d{i}"].shape[-1], ptr(eng.pred_acc[i]), 1 if i == 3 else 0, s)
+                      gacts[f"d{i}"].shape[-1], ptr(eng.pred_acc[i]), 1 if i == 3 else 0, ptr(part), s)
             g3 = g3_buf(P, C)
             gp = torch.empty(1, 2, P, C, device=dev)
             st = S.states[6 + i]

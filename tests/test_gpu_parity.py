@@ -1392,8 +1392,9 @@ def test_persistent_forward_matches_slots(dev, monkeypatch, name, H, W, T):
 
 
 def test_iwe_loss_bit_reproducible(dev):
-    """The IWE splat accumulates in 64-bit fixed point (csrc/iwe_loss.hip, SNNFLOW_SPLAT_FIXED):
-    the loss is the same bits on every run even where hundreds of events pile onto a few pixels
+    """The IWE splat accumulates in 64-bit fixed point (csrc/iwe_loss.hip, SNNFLOW_SPLAT_FIXED), and so
+    do the per-pixel sums of the per-event flow gradients: the loss and dL/dflow are the same bits on
+    every run even where hundreds of events pile onto a few pixels
     (LDS atomics landing in a different order each run), and matches the oracle (fp32 sequential
     index_put_, loss/flow.py:178-303) to rtol 1e-5."""
     import snnflow
@@ -1416,13 +1417,20 @@ def test_iwe_loss_bit_reproducible(dev):
         mask[:, :, 20:26, 30:36] = 1
         flow = (torch.rand(B, 2, H, W, generator=gen) - 0.5) * 0.05
         wins.append((ev, pol, mask, flow))
-    losses = []
+    losses, grads = [], []
     for rep in range(5):
         lf = snnflow.EventWarping(cfg, dev)
-        for ev, pol, mask, flow in wins:
-            lf.event_flow_association([flow.to(dev)], ev.to(dev), pol.to(dev), mask.to(dev))
-        losses.append(lf().item())
+        fl = [flow.to(dev).requires_grad_() for _, _, _, flow in wins]
+        for (ev, pol, mask, _), f in zip(wins, fl):
+            lf.event_flow_association([f], ev.to(dev), pol.to(dev), mask.to(dev))
+        loss = lf()
+        loss.backward()
+        losses.append(loss.item())
+        grads.append(torch.cat([f.grad.flatten() for f in fl]).cpu())
     assert all(v == losses[0] for v in losses), losses
+    # the flow gradients too: the ~40 events per pixel are summed in fixed point (k_iwe_bwd_scatter)
+    for g in grads[1:]:
+        assert torch.equal(g, grads[0])
     rl = iwe_ref.EventWarpingRef([H, W])
     for ev, pol, mask, flow in wins:
         rl.event_flow_association([flow], ev, pol, mask)

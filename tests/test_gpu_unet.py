@@ -374,3 +374,34 @@ def test_convlif_variants_vs_golden(golden, dev, variant):
     print(f"\n[variant {tag}] " + ", ".join(f"{k}={v:.1e}" for k, v in errs.items()))
     for n, e in errs.items():
         assert e < 1e-4, (n, e)
+
+
+def test_unet_bit_reproducible(dev):
+    """Two identical U-Net train steps (same weights, windows and states) give bit-identical flows,
+    loss and parameter gradients: every cross-block sum of the backward (LIF / prediction parameter
+    sums, split-K and split-pixel partial tiles, the IWE splat) is reduced in a fixed order."""
+    import snnflow
+    from snnflow.synthetic import make_window
+
+    H = W = 64
+    gen = torch.Generator(device=dev).manual_seed(11)
+    wins = [make_window(2, 1000, H, W, gen, dev) for _ in range(3)]
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(7)
+        model = snnflow.SpikingRecEVFlowNet(_kw(16)).to(dev)
+        ew = snnflow.EventWarping(_cfg(H, W), dev)
+        flows = []
+        for w in wins:
+            out = model(None, w["event_cnt"])
+            flows.append(torch.cat([f.detach().flatten() for f in out["flow"]]))
+            ew.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        loss = ew()
+        loss.backward()
+        runs.append((torch.cat(flows).cpu(), loss.detach().cpu(),
+                     {n: p.grad.detach().cpu().clone() for n, p in model.named_parameters()}))
+    (f0, l0, g0), (f1, l1, g1) = runs
+    assert torch.equal(f0, f1)
+    assert torch.equal(l0, l1), (l0.item(), l1.item())
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
