@@ -1106,23 +1106,10 @@ __global__ void k_unet_wgrad_reduce(snnflow_unet_wgrad_args a, int nsplit, int K
 // every lane addressing its own pixel row, so a tap is an offset of those rows.
 // 4 waves as WK x WM, each NI x NJ 16x16 tiles of every tap (9 * NI * NJ accumulators).
 // ---------------------------------------------------------------------------------------------
-// LDS rows of the tap-fused weight gradient: 32-B chunks (16 bf16) XOR-swizzled by bits of the row
-// so that a ds_read_b64_tr_b16 half-wave (8 pixel rows {n..n+3, n+d..n+d+3}, 32 B each; d = 8 at
-// stride 1, rows doubled at stride 2) covers all 64 banks once (exhaustive search over pads and
-// row-bit XOR masks, every strip width 16..64; width 8 keeps <= 2-way).  Stride 2 pads X rows by one
-// chunk.
-template <int NCH, int S>
-__device__ __forceinline__ int wr_swz(int row) {
-    if constexpr (NCH == 2) return (row >> (S == 1 ? 3 : 4)) & 1;
-    else return ((row >> 1) & 1) | (((row >> (S == 1 ? 3 : 4)) & 1) << 1);
-}
-
 template <int NI, int NJ, int WK, int WM, int S>
 struct WrGeo {
     static constexpr int TK = 16 * NI * WK, TM = 16 * NJ * WM;
-    static constexpr int XCH = TK / 16, GCH = TM / 16;  // 32-B chunks per row
-    static_assert((XCH == 2 || XCH == 4) && (GCH == 2 || GCH == 4), "wgrad_rows: 2 or 4 chunks per row");
-    static constexpr int XS = TK + (S == 2 ? 16 : 0), GS = TM;  // bf16 per LDS pixel row
+    static constexpr int XS = TK + 8, GS = TM + 8;    // bf16 per LDS pixel row (16-B multiple)
     static constexpr int XPIX = S == 1 ? 198 : 387;   // halo pixels, largest strip shape (TW 64)
     static constexpr int XQ = TK / 8, GQ = TM / 8;     // 16-B pieces per pixel
     static constexpr int GPIECES = 3 * 64 * GQ;
@@ -1207,8 +1194,7 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             const int e = tid + r * UNT;
             if (e < xpieces) {
                 const int pix = e / G::XQ, c8 = e - pix * G::XQ;
-                *reinterpret_cast<uint4*>(&Xs[pix * XS + (((c8 >> 1) ^ wr_swz<G::XCH, S>(pix)) << 4) + 8 * (c8 & 1)]) =
-                    xr[r];
+                *reinterpret_cast<uint4*>(&Xs[pix * XS + 8 * c8]) = xr[r];
             }
         }
 #pragma unroll
@@ -1216,8 +1202,7 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             const int e = tid + r * UNT;
             if (e < G::GPIECES) {
                 const int part = e / (64 * G::GQ), rem = e - part * (64 * G::GQ), j = rem / G::GQ, c8 = rem - j * G::GQ;
-                const int row = part * 64 + j;
-                *reinterpret_cast<uint4*>(&Gs[row * GS + (((c8 >> 1) ^ wr_swz<G::GCH, 1>(row)) << 4) + 8 * (c8 & 1)]) = gr[r];
+                *reinterpret_cast<uint4*>(&Gs[(part * 64 + j) * GS + 8 * c8]) = gr[r];
             }
         }
     };
@@ -1246,9 +1231,8 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
             for (int part = 0; part < 3; ++part)
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {
-                    const int ch = (wm * (TM / WM)) / 16 + j, row0 = part * 64 + gp, row1 = row0 + 4;
-                    bgf[part][j] = tr_pair(&Gs[row0 * GS + ((ch ^ wr_swz<G::GCH, 1>(row0)) << 4) + 4 * pp],
-                                           &Gs[row1 * GS + ((ch ^ wr_swz<G::GCH, 1>(row1)) << 4) + 4 * pp]);
+                    const __bf16* r0 = &Gs[(part * 64 + gp) * GS + wm * (TM / WM) + j * 16 + 4 * pp];
+                    bgf[part][j] = tr_pair(r0, r0 + 4 * GS);
                 }
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
@@ -1256,12 +1240,10 @@ __global__ __launch_bounds__(UNT) void k_unet_wgrad_rows(snnflow_unet_wgrad_args
                 for (int kx = 0; kx < 3; ++kx) {
                     const int toff = ky * XW + kx;
                     bf16x8 axf[NI];
-                    const int xr0 = xrow[kk][0] + toff, xr1 = xrow[kk][1] + toff;
-                    const int sw0 = wr_swz<G::XCH, S>(xr0), sw1 = wr_swz<G::XCH, S>(xr1);
 #pragma unroll
                     for (int i = 0; i < NI; ++i) {
-                        const int ch = (wk * (TK / WK)) / 16 + i;
-                        axf[i] = tr_pair(&Xs[xr0 * XS + ((ch ^ sw0) << 4) + 4 * pp], &Xs[xr1 * XS + ((ch ^ sw1) << 4) + 4 * pp]);
+                        const int col = wk * (TK / WK) + i * 16 + 4 * pp;
+                        axf[i] = tr_pair(&Xs[(xrow[kk][0] + toff) * XS + col], &Xs[(xrow[kk][1] + toff) * XS + col]);
                     }
 #pragma unroll
                     for (int part = 2; part >= 0; --part)  // lo, mid, hi
@@ -1652,49 +1634,32 @@ __global__ __launch_bounds__(256) void k_unet_dec_in(const uint16_t* __restrict_
 // weight of high-res coordinate D's interpolation on low-res index i
 __device__ inline float lin_w(const Lin& l, int i) { return (l.i0 == i ? l.l0 : 0.0f) + (l.i1 == i ? l.l1 : 0.0f); }
 
-// Row-oriented (as k_unet_dec_in): block = (low-res row b*h + y, chunk of its (x, quad) elements);
-// the four high-res rows it gathers and their weights uniform, consecutive rows on one XCD (each
-// high-res row is read by two low-res rows: the second read hits that XCD's L2).
-__global__ __launch_bounds__(256) void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb,
-                                                         int has_pred, int B, int h, int w, float* __restrict__ gx,
-                                                         int gxp, float* __restrict__ gb, int gbp,
-                                                         float* __restrict__ gpred, int assign, int nchunk) {
+template <typename I>
+__global__ void k_unet_dec_in_bwd(const float* __restrict__ gup, int gpitch, int cx, int cb, int has_pred, int B, int h,
+                                  int w, float* __restrict__ gx, int gxp, float* __restrict__ gb, int gbp,
+                                  float* __restrict__ gpred, int assign) {
     const int H = 2 * h, W = 2 * w;
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
-    const int lin = xcd_remap(blockIdx.x, (int)gridDim.x);
-    const int row = lin / nchunk, chunk = lin - row * nchunk;
-    const int b = row / h, y = row - b * h;
-    float wy[4];
-    const float* gr[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int Y = 2 * y - 1 + j;
-        const bool ok = Y >= 0 && Y < H;
-        wy[j] = ok ? lin_w(lin2(Y, h), y) : 0.0f;
-        gr[j] = gup + ((int64_t)b * H + (ok ? Y : 0)) * W * gpitch;
-    }
-    const float invQ = 1.0f / (float)Q;
-    const int e1 = min((chunk + 1) * DEC_CHUNK, w * Q);
-    for (int e = chunk * DEC_CHUNK + (int)threadIdx.x; e < e1; e += 256) {
-        int x, q;
-        row_split(e, Q, invQ, x, q);
-        const int k = 4 * q;
+    const I n = (I)B * h * w * Q;
+    for (I e = (I)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (I)gridDim.x * blockDim.x) {
+        const int k = (int)(e % (I)Q) * 4;
+        const I pix = e / (I)Q;
+        const I pyy = pix / (I)w;
+        const int x = (int)(pix - pyy * (I)w), y = (int)(pyy % (I)h), b = (int)(pyy / (I)h);
         float s[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (wy[j] == 0.0f) continue;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int X = 2 * x - 1 + i;
+        for (int Y = 2 * y - 1; Y <= 2 * y + 2; ++Y) {
+            if (Y < 0 || Y >= H) continue;
+            const float wy = lin_w(lin2(Y, h), y);
+            if (wy == 0.0f) continue;
+            for (int X = 2 * x - 1; X <= 2 * x + 2; ++X) {
                 if (X < 0 || X >= W) continue;
                 const float wx = lin_w(lin2(X, w), x);
                 if (wx == 0.0f) continue;
-                const float4 g = *reinterpret_cast<const float4*>(gr[j] + (int64_t)X * gpitch + k);
-                const float ww = wy[j] * wx;
+                const float4 g = *reinterpret_cast<const float4*>(gup + (((int64_t)b * H + Y) * W + X) * gpitch + k);
+                const float ww = wy * wx;
                 s[0] += ww * g.x; s[1] += ww * g.y; s[2] += ww * g.z; s[3] += ww * g.w;
             }
         }
-        const int64_t pix = (int64_t)row * w + x;
         if (k < cx + cb) {
             const bool to_x = k < cx;
             float4* d = to_x ? reinterpret_cast<float4*>(gx + pix * gxp + k)
@@ -2311,12 +2276,14 @@ int snnflow_unet_dec_in_bwd(const float* g_up, int gpitch, int cx, int cb, int h
         cb % 4 != 0 || gpitch % 4 != 0 || gx_pitch % 4 != 0 || gb_pitch % 4 != 0)
         SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: bad args");
     const int Q = (cx + cb) / 4 + (has_pred ? 1 : 0);
-    if ((int64_t)w * Q >= (1LL << 24)) SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: row too long");
-    const int nchunk = (w * Q + DEC_CHUNK - 1) / DEC_CHUNK;
-    const int64_t nblk = (int64_t)B * h * nchunk;
-    if (nblk >= (1LL << 31)) SNN_FAIL(SNNFLOW_E_ARG, "unet_dec_in_bwd: too large");
-    hipLaunchKernelGGL(k_unet_dec_in_bwd, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, g_up, gpitch, cx, cb,
-                       has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign, nchunk);
+    const int64_t n = (int64_t)B * h * w * Q;
+    const int64_t offs = (int64_t)B * h * w * (gx_pitch > gb_pitch ? gx_pitch : gb_pitch);
+    if (n < (1LL << 30) && offs < (1LL << 31))
+        hipLaunchKernelGGL(k_unet_dec_in_bwd<uint32_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
+                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign);
+    else
+        hipLaunchKernelGGL(k_unet_dec_in_bwd<int64_t>, dim3(grid1d(n, 256, 16384)), dim3(256), 0, (hipStream_t)stream, g_up,
+                           gpitch, cx, cb, has_pred, B, h, w, g_x, gx_pitch, g_block, gb_pitch, g_pred, assign);
     SNN_CHECK_LAUNCH();
     return 0;
 }
