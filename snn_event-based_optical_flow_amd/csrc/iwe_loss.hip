@@ -519,47 +519,8 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
     }
 }
 
-// Per-pixel sums of the per-event flow gradients, windows of <= SCATTER_SMALL events: one block per
-// (sample, flow window) holds the window's event pixels and gradients in LDS; each event sums the
-// gradients of every event on its pixel in event order (a fixed order: bit-reproducible), and the
-// first event of the pixel adds the sum to g_flows.  O(N^2) LDS broadcast reads, ~1 us at N = 1000.
-constexpr int SCATTER_SMALL = 4096;
-
-__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter_small(snnflow_iwe_loss_args a, const float* __restrict__ gev,
-                                                                    float* g_flows) {
-    __shared__ int sq[SCATTER_SMALL];
-    __shared__ float2 sg[SCATTER_SMALL];
-    const int tid = threadIdx.x;
-    const int t = blockIdx.x % a.tf, b = blockIdx.x / a.tf;
-    const int64_t HWp = (int64_t)a.H * a.W;
-    const int i0 = a.tf == 1 ? 0 : a.off[t], n = (a.tf == 1 ? a.M : a.off[t + 1]) - i0;
-    for (int j = tid; j < n; j += SPLAT_NT) {
-        const EventRef r = event_ref(a, b, i0 + j);
-        sq[j] = (int)(r.ev[1] * (float)a.W + r.ev[2]);
-        sg[j] = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i0 + j));
-    }
-    __syncthreads();
-    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
-    for (int i = tid; i < n; i += SPLAT_NT) {
-        const int q = sq[i];
-        float sx = 0.0f, sy = 0.0f;
-        int first = i;
-        for (int j = 0; j < n; ++j) {
-            if (sq[j] == q) {
-                first = j < first ? j : first;
-                const float2 g = sg[j];
-                sx += g.x;
-                sy += g.y;
-            }
-        }
-        if (first == i) {
-            if (sx != 0.0f) gf[q] += sx;
-            if (sy != 0.0f) gf[HWp + q] += sy;
-        }
-    }
-}
-
-// Larger windows: one block per (sample, flow window, band of SPLAT_BAND pixels) scans the window's events, adds those of its
+// Per-pixel sums of the per-event flow gradients (an event scatters into its own pixel): one block
+// per (sample, flow window, band of SPLAT_BAND pixels) scans the window's events, adds those of its
 // band into LDS in exact two-word fixed point (SplatLdsX: integer adds, so the sum does not depend on
 // the order of the events), then adds each touched pixel's total to g_flows once.
 struct GevLds {
@@ -740,18 +701,8 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
         hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s, *a, gimg,
                            g_flows, gev);
         if (gev) {
-            int nmax = a->M;
-            if (a->tf != 1) {
-                nmax = 0;
-                for (int k = 0; k < a->T; ++k) nmax = std::max(nmax, a->off[k + 1] - a->off[k]);
-            }
-            if (nmax <= SCATTER_SMALL) {
-                hipLaunchKernelGGL(k_iwe_bwd_scatter_small, dim3(a->B * a->tf), dim3(SPLAT_NT), 0, s, *a, gev, g_flows);
-            } else {
-                const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
-                hipLaunchKernelGGL(k_iwe_bwd_scatter, dim3(a->B * a->tf * nbands), dim3(SPLAT_NT), 0, s, *a, gev, g_flows,
-                                   nbands);
-            }
+            const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
+            hipLaunchKernelGGL(k_iwe_bwd_scatter, dim3(a->B * a->tf * nbands), dim3(SPLAT_NT), 0, s, *a, gev, g_flows, nbands);
         }
     }
     SNN_CHECK_LAUNCH();
