@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 26
+#define SNNFLOW_ABI_VERSION 27
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -238,50 +238,15 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
 int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnflow_lif_bwd_args* lif,
                      void* stream);
 int snnflow_slot_supported(int c, int cin0);
+/* Tuning (ABI 27): tiles per block of the c = 8 LIF-fed tasks of the wavefront launches, forward and
+ * backward (0: one tile per block; >= 1: the tile pipelines, which overlap the next tile's halo
+ * loads by LDS-DMA with this tile's math).  Process-wide; defaults from SNNFLOW_PIPE_FWD /
+ * SNNFLOW_PIPE_BWD at load time.  Results do not depend on it beyond fp64-atomic summation order.
+ * snnflow_get_pipe(0 | 1) reads the forward / backward value. */
+int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block);
+int snnflow_get_pipe(int which);
 
-/* ---- persistent dataflow forward of a whole window (ABI 24) ---------------------------------
- * The T x (L+1) forward layer-steps of engine.FireNetSequence (what 2(T-1)+L+1 snnflow_fwd_slot
- * launches do) as ONE launch.  Every block pulls (layer-step, tile) work items in wavefront order
- * from the queue of its own XCD and starts an item once the layer-steps it reads are complete
- * (one completion counter per layer-step, agent-scope atomics): layer-step (k, t) reads (k-1, t)
- * (pre-BN current and batch sums), (k, t-1) (membrane of layer k-1) and, for a recurrent layer,
- * (k+1, t-1) (its previous spikes).  No launch boundaries, and no lockstep rounds: blocks of
- * different layer-steps overlap their load and compute phases.  Work is XCD-affine: the queue of
- * XCD x holds images [x B/8, (x+1) B/8) of every layer-step, so activations, states and the
- * running statistics (block 0 of every layer-step lives on XCD 0) are handed over inside one XCD's
- * L2 (consumers read them with sc1 loads; no fences); only the BatchNorm batch sums (fp64
- * atomics) and the counters cross XCDs.  The same arithmetic per (layer, step) as the slot path.
- * Requirements (snnflow_seq_supported): c == 8, B % 8 == 0, (B*H*W) % 512 == 0,
- * 1 <= T <= SNNFLOW_SEQ_MAX_T, 1 <= L <= SNNFLOW_MAX_LAYERS.  Tensors as FireNetSequence
- * allocates them: ys [T][L][B][H][W][c], stats [T][L][2][c], states [T][L][2][B][H][W][c],
- * facc [T][L][facc_stride doubles] (zero when the call starts).  mem0 / sprev0: the membrane /
- * previous spikes of step 0 per layer (NHWC, NULL = zeros).  sync: a work area of
- * snnflow_seq_work_bytes(T, L) bytes (16-B aligned): the first snnflow_seq_sync_ints(T, L) ints are
- * counters zeroed by the call, then every layer-step's argument structs (written by the call);
- * sync[8] != 0 after the call means a dependency wait timed out (results invalid). */
-#define SNNFLOW_SEQ_MAX_T 16
-#define SNNFLOW_MAX_LAYERS 8   /* cells of a LIFFireNet-family model (also the step driver's plan) */
-typedef struct snnflow_fwd_seq_args {
-    int T, L, B, H, W, c, cin0;
-    int rec[SNNFLOW_MAX_LAYERS];
-    int train[SNNFLOW_MAX_LAYERS];
-    snnflow_neuron n[SNNFLOW_MAX_LAYERS];
-    const float* wt_ff[SNNFLOW_MAX_LAYERS];     /* snnflow_conv_fwd_args.wt_ff of layer l   */
-    const float* wt_rec[SNNFLOW_MAX_LAYERS];
-    const float* wt_ff_t[SNNFLOW_MAX_LAYERS];   /* snnflow_conv_fwd_args.wt_ff_t of layer l */
-    const float* wt_rec_t[SNNFLOW_MAX_LAYERS];
-    const float* pred_w; const float* pred_b;
-    const float* x[SNNFLOW_SEQ_MAX_T]; int64_t xs[4];   /* step inputs (same strides) */
-    float* flow[SNNFLOW_SEQ_MAX_T];
-    float* ys; float* stats; float* states; double* facc; int64_t facc_stride;
-    const float* mem0[SNNFLOW_MAX_LAYERS]; const float* sprev0[SNNFLOW_MAX_LAYERS];
-    int* sync;
-} snnflow_fwd_seq_args;
-int snnflow_fwd_seq(const snnflow_fwd_seq_args* a, void* stream);
-int snnflow_seq_sync_ints(int T, int L);
-size_t snnflow_seq_work_bytes(int T, int L);
-int snnflow_debug_xcc(int* out, int n, void* stream);   /* diagnostics: HW_REG_XCC_ID of n blocks */
-int snnflow_seq_supported(int c, int B, int H, int W, int T, int L);
+#define SNNFLOW_MAX_LAYERS 8   /* cells of a LIFFireNet-family model (the step driver's plan) */
 
 /* ---- deferred weight gradients of one layer over many time steps ----------
  * Nothing on the backward chain depends on dW, so the weight gradients of a layer

@@ -104,7 +104,9 @@ struct SplatLdsX {  // exact two-word fixed point
         for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&hi[0][0])[j] = 0, (&lo[0][0])[j] = 0;
     }
     __device__ void add(int q, int i, float x) {
-        const double d = (double)x;
+        // corner weights (x ts) lie in [0, 1]; the clamp keeps any input inside the fixed-point range
+        // (|d| < 2^30: rint(d 2^32) fits a 64-bit word with room for 2^31 additions)
+        const double d = fmin(fmax((double)x, -0x1p30), 0x1p30);
         const double h = rint(d * 0x1p32);               // exact: x has 24 significant bits
         const double r = d - h * 0x1p-32;                // exact, |r| <= 2^-33
         const long long l = (long long)rint(r * 0x1p75);
@@ -545,7 +547,9 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_a
         const float2 g = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i));
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            const double d = (double)(c == 0 ? g.x : g.y);
+            // clamped to |d| <= 2^30 (a per-event flow gradient beyond that is not a number this sum can
+            // carry exactly in 64 bits: rint(d 2^32) must leave room for the pixel's other events)
+            const double d = fmin(fmax((double)(c == 0 ? g.x : g.y), -0x1p30), 0x1p30);
             if (d == 0.0) continue;
             const double h = rint(d * 0x1p32);
             const long long l = (long long)rint((d - h * 0x1p-32) * 0x1p75);

@@ -2573,7 +2573,8 @@ enum SlotKind : int {
     SK_HEAD1, SK_HEAD2, SK_HEAD4, SK_HEAD5,  // conv of a cin-channel input (no LIF)
     SK_PLAIN, SK_PLAIN_REC,                  // conv of a C-channel input (no LIF) [+ rec]
     SK_LIF, SK_LIF_REC,                      // LIF(l-1) on the halo + conv(l) [+ rec]
-    SK_TOP, SK_TOP_PRED                      // LIF of the last layer [+ pred]
+    SK_TOP, SK_TOP_PRED,                     // LIF of the last layer [+ pred]
+    SK_LIF_P, SK_LIF_REC_P                   // C = 8 SK_LIF / SK_LIF_REC as a tile pipeline (fwd_lif8_pipe)
 };
 
 struct FwdSlotParams {
@@ -2597,11 +2598,24 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 template <int C>
 constexpr bool kSlotAllKinds = C == 8;
 
+constexpr int kFragC8 = 3 * 3 * 256;  // bf16 entries per conv of the compact C = 8 fragments (FragC8)
+// LDS of the pipeline (bytes): raw y / m halos (680 16-B DMA slots each), the bf16 spike
+// tiles (layer l-1, and s_prev for the recurrent conv), the compact fragments.
+constexpr int kPipeRaw = 2 * HN * 16, kPipeSpk = HN * 8 * 2, kPipeFrag = kFragC8 * 2;
+template <bool REC>
+struct PipeFwdLds {
+    static constexpr int RAWY = 0, RAWM = kPipeRaw, SPK = 2 * kPipeRaw, RSPK = SPK + kPipeSpk;
+    static constexpr int FF = RSPK + (REC ? kPipeSpk : 0), FR = FF + kPipeFrag;
+    static constexpr int BYTES = FR + (REC ? kPipeFrag : 0);
+    static constexpr int FLOATS = BYTES / 4;
+};
+
 template <int C>
 struct SlotLds {
     static constexpr int FWD_ALL = cmax(cmax(ConvFwdLds<1, C, false, false, 2>::FLOATS, ConvFwdLds<5, C, false, false, 2>::FLOATS),
                                         cmax(ConvFwdLds<C, C, false, false, 2>::FLOATS, ConvFwdLds<C, C, false, true, 2>::FLOATS));
-    static constexpr int FWD = cmax(cmax(kSlotAllKinds<C> ? FWD_ALL : 0, kLifQFwdLds<C>),
+    static constexpr int FWD_P = C == 8 ? PipeFwdLds<true>::FLOATS : 0;  // the tile pipeline (C = 8)
+    static constexpr int FWD = cmax(cmax(cmax(kSlotAllKinds<C> ? FWD_ALL : 0, kLifQFwdLds<C>), FWD_P),
                                     cmax(cmax(ConvFwdLds<2, C, false, false, 2>::FLOATS, ConvFwdLds<4, C, false, false, 2>::FLOATS),
                                          cmax(ConvFwdLds<C, C, true, false, 2>::FLOATS, ConvFwdLds<C, C, true, true, 2>::FLOATS)));
     static constexpr bool BFG = C >= 16;  // LIF-fed layers: bf16 six-product input gradients from global fragments
@@ -2695,8 +2709,297 @@ __device__ inline int slot_task(const __attribute__((address_space(4))) P* pp, G
     return k;
 }
 
+// ---------------------------------------------------------------------------
+// C = 8 LIF-fed forward layer-steps as a tile pipeline (slot kinds SK_LIF_P / SK_LIF_REC_P).
+//
+// The one-tile-per-block bodies run in lockstep rounds: every block of a round issues its halo
+// loads at once (HBM busy), then computes while HBM idles, and the next round starts when the
+// whole round is done (phase trace, profiles/r03/ktrace_slot_r3_fused.json: prologue 3.2 of
+// 6.1 us per block).  Here a block owns tiles v = bid, bid + nb, ... of its layer-step and
+// overlaps tile i's math with tile i+1's loads:
+//   * the previous layer's pre-BN current y and membrane m of the next tile's halo go from
+//     global memory straight into LDS by LDS-DMA (buffer_load_dwordx4 ... lds; pixels outside
+//     the image read an offset past the buffer's range: zeros) -- no registers held in flight;
+//   * the per-block prologue (BatchNorm statistics from the batch-sum shards, running-stat
+//     update, weight fragments split into bf16 hi / mid / lo) runs once per block, not per tile;
+//   * the conv runs with the operands swapped (A = weights, B = spikes): the accumulator rows
+//     are output channels, so a lane holds four consecutive channels of one pixel, and one
+//     v_permlane32_swap per register packs the wave's two 16-pixel M-tiles into 64 lanes -- the
+//     pre-BN current leaves as one 16-B store per lane (no LDS staging, no barrier) and the
+//     batch sums stay in registers over the block's tiles (one set of fp64 atomics per block).
+// Per tile: wait(DMA) + barrier -> LIF of layer l-1 over the halo from LDS (state stores,
+// spikes as a bf16 tile) -> barrier -> DMA of the next tile -> MFMA -> store.  Two barriers per
+// tile.  Same arithmetic as conv_fwd_body<8, 8, true, REC, 2> (the conv in another summation
+// order inside the matrix core only where the hardware's k-order differs).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void;
+
+template <int N>
+__device__ inline void vm_wait() {  // s_waitcnt vmcnt(N), the other counters untouched
+    static_assert(N >= 0 && N < 64, "vmcnt");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// A value the compiler cannot treat as loop-invariant (forces per-iteration recomputation of what
+// derives from it instead of holding it in registers across the loop).
+__device__ inline int opaque_int(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// Compact C = 8 weight fragments: [chunk 0..2][part hi/mid/lo][lane group g][co 0..7][8 bf16],
+// the A operand of the swapped conv (lane (co, g) feeds W[tap 4 chunk + g][co][0..7]); rows
+// co 8..15 of the matrix core read rows 0..7 again (their outputs are never used).
+struct FragC8 {
+    float r[2];
+    __device__ inline void load(const float* __restrict__ wB) {  // wB [tap][co][ci]
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = (int)threadIdx.x + i * 2 * NT;
+            const int j = e & 7, co = (e >> 3) & 7, g = (e >> 6) & 3, ch = e >> 8, tap = 4 * ch + g;
+            r[i] = (e < 768 && tap < 9) ? wB[(tap * 8 + co) * 8 + j] : 0.0f;
+        }
+    }
+    __device__ inline void store(__bf16* f) const {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int e = (int)threadIdx.x + i * 2 * NT;
+            if (e < 768) {
+                const float w = r[i];
+                const __bf16 h = (__bf16)w;
+                const float r1 = w - (float)h;
+                const __bf16 md = (__bf16)r1;
+                __bf16* d = f + (e >> 8) * 3 * 256 + (e & 255);
+                d[0] = h;
+                d[256] = md;
+                d[512] = (__bf16)(r1 - (float)md);
+            }
+        }
+    }
+};
+
+// Tiles per block of a pipelined task (host: snnflow_set_pipe); blocks are a multiple of 8 so a
+// block's tiles v = bid + k nb stay in its XCD group of block_tile.
+__host__ __device__ inline int pipe_tiles(const Grid& g, int ntiles) {
+    return g.bid < ntiles ? (ntiles - 1 - g.bid) / g.nb + 1 : 0;
+}
+
+template <bool REC>
+__device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, float* pool) {
+    constexpr int C = 8, NTB = 2 * NT, R = Halo4<C, NTB>::R;
+    using L = PipeFwdLds<REC>;
+    char* const lds = reinterpret_cast<char*>(pool);
+    __shared__ LifCoef coef[C];
+    __shared__ double sums[2 * C];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = a.H, W = a.W, ntiles = a.B * tiles_per_image(H, W);
+    const int nt = pipe_tiles(g, ntiles);
+    const bool lead = g.bid == 0;
+    const bool has_mem = a.prev_mem != nullptr;
+    const bool has_rec = REC && a.s_prev != nullptr;
+
+    // ---- prologue (once per block): batch-sum shards, neuron parameters, fragments, first tile
+    AccGather<2 * C> gat;
+    if (a.prev.bn_train) acc_gather_load<2 * C>(a.prev_acc, 2 * C, gat);
+    const NeuronRegs nr = load_neuron(a.prev, C, lead);
+    FragC8 fz_ff, fz_rec;
+    fz_ff.load(a.wt_ff_t);
+    if (has_rec) fz_rec.load(a.wt_rec_t);
+
+    const uint32_t nbytes = (uint32_t)a.B * H * W * C * 4;  // < 2^31 (host check)
+    const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.prev_y), (short)0, (int)nbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_m =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(has_mem ? a.prev_mem : a.prev_y), (short)0, (int)nbytes, 0x00020000);
+    // the raw halo of tile t: 11 wave-loads of 64 x 16 B per tensor, wave w issues loads w, w + 8, w + 16
+    auto issue = [&](const Tile& t, int lane) {
+        const int base = ((t.b * H + t.h0 - 1) * W + (t.w0 - 1)) * (C * 4);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int k = wv + 8 * j;
+            if (k >= 22) break;
+            const bool mem = k >= 11;
+            if (mem && !has_mem) continue;
+            const int kk = mem ? k - 11 : k, ee = kk * 64 + lane, p = ee >> 1, r = p / HWD, cc = p - r * HWD;
+            const bool ok = in_image(t.h0 + r - 1, t.w0 + cc - 1, H, W);
+            const uint32_t off = ok ? (uint32_t)(base + (r * W + cc) * (C * 4) + (ee & 1) * 16) : 0x80000000u;
+            if (ee < 2 * HN)  // the last wave-load is partial: inactive lanes write no LDS
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(mem ? rs_m : rs_y, (lds_void*)(lds + (mem ? L::RAWM : L::RAWY) + kk * 1024),
+                                                         16, off, 0, 0, 0);
+        }
+    };
+    auto tile_of = [&](int k) { return block_tile(H, W, Grid{g.bid + k * g.nb, ntiles}); };
+    float4 rs[R];  // s_prev halo of the next tile (registers, issued one tile ahead)
+    auto load_sprev = [&](const Tile& t, int tid) {  // halo_load's element order, 32-bit offsets from the halo origin
+        const float4* base = reinterpret_cast<const float4*>(a.s_prev) + (((int64_t)t.b * H + (t.h0 - 1)) * W + (t.w0 - 1)) * 2;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = tid + i * NTB, p = e >> 1, r = p / HWD, cc = p - r * HWD;
+            const bool ok = e < 2 * HN && in_image(t.h0 + r - 1, t.w0 + cc - 1, H, W);
+            rs[i] = ok ? base[(r * W + cc) * 2 + (e & 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    Tile tl = tile_of(0);
+    if (nt > 0) {
+        issue(tl, lane);
+        if (has_rec) load_sprev(tl, tid);
+    }
+    if (a.prev.bn_train) acc_gather_reduce<2 * C>(gat, sums);
+    lif_prologue(a.prev, nr, sums, C, (double)a.B * H * W, a.prev_stats, coef, nullptr, lead);
+    fz_ff.store(reinterpret_cast<__bf16*>(lds + L::FF));
+    if (has_rec) fz_rec.store(reinterpret_cast<__bf16*>(lds + L::FR));
+    zero_consumed(a.zero0, a.zero1, a.zero_n, g);
+
+    const bool zr = a.prev.zero_reset != 0;
+    const int64_t plane4 = (int64_t)a.B * H * W * 2;
+    float4* st4 = reinterpret_cast<float4*>(a.prev_state);
+    float bs[4] = {0.f, 0.f, 0.f, 0.f}, bq[4] = {0.f, 0.f, 0.f, 0.f};  // this lane's batch sums
+    const __bf16* spk = reinterpret_cast<const __bf16*>(lds + L::SPK);
+    const __bf16* rspk = reinterpret_cast<const __bf16*>(lds + L::RSPK);
+
+    for (int k = 0; k < nt; ++k) {
+        vm_wait<0>();     // this wave's DMA and s_prev loads of tile k (and its stores of tile k-1)
+        __syncthreads();  // every wave's DMA landed; every wave is done with the spike tiles of k-1
+        // the lane's tile-independent index math (halo element, DMA slot, LDS addresses) is redone per
+        // tile from an opaque copy of the thread index: hoisted out of the loop it held ~30 registers
+        const int tid = opaque_int(threadIdx.x), lane = tid & 63, jj = lane & 15, gg = lane >> 4, qt = tid & 1;
+        const LifCoef kc[4] = {coef[4 * qt], coef[4 * qt + 1], coef[4 * qt + 2], coef[4 * qt + 3]};
+        // LIF of layer l-1 over the halo (element e = pixel * 2 + channel quad, e = tid + i NTB)
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < 2 * HN) {
+                const int p = e >> 1, r = p / HWD, cc = p - r * HWD;
+                const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+                const float4 yv = *reinterpret_cast<const float4*>(lds + L::RAWY + e * 16);
+                const float4 mv = has_mem ? *reinterpret_cast<const float4*>(lds + L::RAWM + e * 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+                float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (in_image(h, w, H, W)) {
+                    const Lif4 o = zr ? lif_step4(yv, mv, kc, true) : lif_step4(yv, mv, kc, false);
+                    sv = o.s;
+                    if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
+                        const int64_t q = (((int64_t)tl.b * H + h) * W + w) * 2 + qt;
+                        st_state4(st4, q, o.mout);
+                        st_state4(st4, plane4 + q, o.s);
+                    }
+                }
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<bf16x4*>(const_cast<__bf16*>(spk) + p * 8 + 4 * qt) =
+                    bf16x4{(__bf16)sv.x, (__bf16)sv.y, (__bf16)sv.z, (__bf16)sv.w};
+                if (has_rec) {
+                    const float4 s = rs[i];
+                    ok = ok && exact_bf16(s.x) && exact_bf16(s.y) && exact_bf16(s.z) && exact_bf16(s.w);
+                    *reinterpret_cast<bf16x4*>(const_cast<__bf16*>(rspk) + p * 8 + 4 * qt) =
+                        bf16x4{(__bf16)s.x, (__bf16)s.y, (__bf16)s.z, (__bf16)s.w};
+                }
+            }
+        }
+        // raw halos free, spike tiles complete (and: is s_prev exact in bf16 everywhere?)
+        const bool rec_bf = has_rec ? __syncthreads_and(ok) != 0 : (__syncthreads(), false);
+        const Tile cur = tl;
+        if (k + 1 < nt) {
+            tl = tile_of(k + 1);
+            issue(tl, lane);
+            if (has_rec) load_sprev(tl, tid);
+        }
+
+        // conv(s) of this wave's tile row: A = fragments (rows co), B = spikes (columns: pixels)
+        const bf16x8* fff = reinterpret_cast<const bf16x8*>(lds + L::FF) + gg * 8 + (jj & 7);
+        const bf16x8* ffr = reinterpret_cast<const bf16x8*>(lds + L::FR) + gg * 8 + (jj & 7);
+        f32x4 af[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, ar[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const int tap = 4 * ch + gg, ky = tap / 3, kx = tap - 3 * ky;
+            const bf16x8 fh = fff[ch * 96], fm = fff[ch * 96 + 32], fl = fff[ch * 96 + 64];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int off = ((wv + ky) * HWD + mt * 16 + jj + kx) * 8;
+                bf16x8 b = {};
+                if (tap < 9) b = *reinterpret_cast<const bf16x8*>(spk + off);
+                af[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl, b, af[mt], 0, 0, 0);
+                af[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm, b, af[mt], 0, 0, 0);
+                af[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh, b, af[mt], 0, 0, 0);
+            }
+            if (rec_bf) {
+                const bf16x8 rh = ffr[ch * 96], rm = ffr[ch * 96 + 32], rl = ffr[ch * 96 + 64];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const int off = ((wv + ky) * HWD + mt * 16 + jj + kx) * 8;
+                    bf16x8 b = {};
+                    if (tap < 9) b = *reinterpret_cast<const bf16x8*>(rspk + off);
+                    ar[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rl, b, ar[mt], 0, 0, 0);
+                    ar[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rm, b, ar[mt], 0, 0, 0);
+                    ar[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rh, b, ar[mt], 0, 0, 0);
+                }
+            }
+        }
+        // lane -> (M-tile lane >> 5, pixel column jj, channel quad (lane >> 4) & 1) after the swap
+        f32x4 yv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float y0 = rec_bf ? af[0][r] + ar[0][r] : af[0][r];  // ff + rec (:540)
+            const float y1 = rec_bf ? af[1][r] + ar[1][r] : af[1][r];
+            const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, y0), __builtin_bit_cast(unsigned, y1),
+                                                             false, false);
+            yv[r] = __builtin_bit_cast(float, sw[0]);
+        }
+        const int qd = (lane >> 4) & 1, h = cur.h0 + wv, w = cur.w0 + (lane >> 5) * 16 + jj;
+        const bool in = h < H && w < W;
+        if (has_rec && !rec_bf && in) {  // s_prev not binary: the recurrent conv on the vector ALU (exact f32)
+            const float* wr = a.wt_rec;  // [tap][ci][co]
+#pragma unroll 1
+            for (int tp = 0; tp < 9; ++tp) {
+                const int hh = h + tp / 3 - 1, ww = w + tp % 3 - 1;
+                if (!in_image(hh, ww, H, W)) continue;
+                const float* sp = a.s_prev + (((int64_t)cur.b * H + hh) * W + ww) * C;
+                for (int ci = 0; ci < C; ++ci) {
+                    const float s = sp[ci];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) yv[r] = fmaf(wr[(tp * C + ci) * C + 4 * qd + r], s, yv[r]);
+                }
+            }
+        }
+        if (in) {
+            *reinterpret_cast<float4*>(a.y + (((int64_t)cur.b * H + h) * W + w) * C + 4 * qd) =
+                make_float4(yv[0], yv[1], yv[2], yv[3]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                bs[r] += yv[r];
+                bq[r] += yv[r] * yv[r];
+            }
+        }
+    }
+
+    // ---- batch sums of the block's tiles: 16-lane rows by DPP, rows and waves through LDS, fp64 atomics
+    if (a.acc) {
+        float v[8] = {bs[0], bs[1], bs[2], bs[3], bq[0], bq[1], bq[2], bq[3]};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += dppf<0xB1>(v[j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += dppf<0x4E>(v[j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += dppf<0x141>(v[j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += dppf<0x140>(v[j]);
+        float(*red)[4][8] = reinterpret_cast<float(*)[4][8]>(sum_scratch());  // [wave][16-lane row][8 sums]
+        if ((lane & 15) == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) red[wv][lane >> 4][j] = v[j];
+        }
+        __syncthreads();
+        if (tid < 2 * C) {  // sum (tid < 8) or sum of squares of channel c
+            const int c = tid & 7, sq = tid >> 3, qd = c >> 2, j = sq * 4 + (c & 3);
+            double s = 0.0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) s += (double)red[w][qd][j] + (double)red[w][qd + 2][j];
+            atomicAdd(acc_shard(a.acc, 2 * C, g.bid) + sq * C + c, s);
+        }
+    }
+}
+
 template <int C>
-__global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
+__global__ __launch_bounds__(NT * 2, C == 8 ? 6 : 1) void k_fwd_slot(FwdSlotParams) {
     typedef const __attribute__((address_space(4))) FwdSlotParams* cptr;
     const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
     Grid g;
@@ -2721,6 +3024,15 @@ __global__ __launch_bounds__(NT * 2) void k_fwd_slot(FwdSlotParams) {
         FWD_CONV(true, SK_LIF, C, C, true, false, 2)
         FWD_CONV(true, SK_LIF_REC, C, C, true, true, 2)
 #undef FWD_CONV
+        case SK_LIF_P:
+        case SK_LIF_REC_P: {
+            if constexpr (C == 8) {
+                const snnflow_conv_fwd_args a = task_args(&pp->conv[k]);
+                if (pp->kind[k] == SK_LIF_REC_P) fwd_lif8_pipe<true>(a, g, pool);
+                else fwd_lif8_pipe<false>(a, g, pool);
+            }
+            break;
+        }
         case SK_TOP: {  // (LIFFireNet's top layer always carries the prediction: C = 8 only)
             if constexpr (kSlotAllKinds<C>) {
                 const snnflow_lif_fwd_args a = task_args(&pp->lif);
@@ -2783,257 +3095,6 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L
             break;
         }
         default: break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent dataflow forward of a window (snnflow_fwd_seq, include/snnflow.h).
-// sync: [0, 8) per-XCD queue heads, [8] timeout flag, [16 + t (L+1) + k] completion counter of
-// layer-step (k, t) (blocks done).  Items of queue x, in wavefront order (slot m = k + 2t, t
-// ascending inside a slot): for every layer-step its blocks of XCD x's images -- conv layer-steps
-// the tiles bid = x + 8 i (block_tile maps them to images [x B/8, (x+1) B/8)), the top LIF
-// layer-step the pixel blocks [x n/8, (x+1) n/8).
-// ---------------------------------------------------------------------------
-struct SeqFwdParams {
-    int T, L, nconv, ntop;  // blocks per conv / top layer-step
-    int rec[SNNFLOW_MAX_LAYERS];
-    int* sync;
-    const snnflow_conv_fwd_args* conv;  // [T][L] (k2_seq_build)
-    const snnflow_lif_fwd_args* top;    // [T]
-};
-
-#ifndef SNNFLOW_SEQ_SC1
-#define SNNFLOW_SEQ_SC1 1    // sc1 loads of handed-off bytes (A/B: 0 = plain loads)
-#endif
-#ifndef SNNFLOW_SEQ_FENCE
-#define SNNFLOW_SEQ_FENCE 0  // agent release before every completion count, acquire after every wait (A/B)
-#endif
-constexpr bool kSeqSc1 = SNNFLOW_SEQ_SC1 != 0;
-constexpr int kSeqSyncHead = 0, kSeqSyncErr = 8, kSeqSyncDone = 24;
-constexpr unsigned kSeqSpinLimit = 1u << 22;  // polls of one dependency before giving up (~0.5 s)
-
-__device__ inline int xcc_id() {
-    unsigned v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    return (int)(v & 7u);
-}
-
-__global__ void k_debug_xcc(int* out) {
-    unsigned v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-    if (threadIdx.x == 0) out[blockIdx.x] = (int)v;
-}
-
-// Lane 0: wait until counter j has reached `need` (relaxed agent-scope polls, s_sleep between);
-// on timeout raise the error flag and go on (the launch then completes with invalid results
-// instead of hanging the GPU).
-#ifndef SNNFLOW_SEQ_POLL
-#define SNNFLOW_SEQ_POLL 0  // 0: sc1 load polls; 1: atomic fetch-add(0) polls (A/B)
-#endif
-#ifndef SNNFLOW_SEQ_SLEEP
-#define SNNFLOW_SEQ_SLEEP 2  // s_sleep argument between polls (x 64 cycles), doubled up to 32x (A/B)
-#endif
-__device__ inline int seq_poll(int* c) {
-    if (SNNFLOW_SEQ_POLL) return __hip_atomic_fetch_add(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void seq_wait(int* sync, int j, int need) {
-    int* c = sync + kSeqSyncDone + j;
-    unsigned spins = 0, nap = 0;
-    while (seq_poll(c) < need) {
-        // back off: a few short naps, then longer ones (every poller is a load on this one line)
-        if (nap < 4) __builtin_amdgcn_s_sleep(SNNFLOW_SEQ_SLEEP);
-        else if (nap < 8) __builtin_amdgcn_s_sleep(4 * SNNFLOW_SEQ_SLEEP);
-        else __builtin_amdgcn_s_sleep(16 * SNNFLOW_SEQ_SLEEP > 127 ? 127 : 16 * SNNFLOW_SEQ_SLEEP);
-        ++nap;
-        if (++spins > kSeqSpinLimit) {
-            __hip_atomic_store(sync + kSeqSyncErr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-        }
-    }
-}
-
-// The slot-path argument structs of layer-step (k, t), from the window's tensors (the layout of
-// engine.FireNetSequence.forward / _fwd_conv_args / _fwd_top_args).
-__device__ inline void seq_fwd_conv_args(const snnflow_fwd_seq_args& p, int k, int t, snnflow_conv_fwd_args& a) {
-    const int L = p.L, C = p.c;
-    const int64_t ny = (int64_t)p.B * p.H * p.W * C, n1 = 2 * ny;
-    auto ys = [&](int tt, int l) { return p.ys + ((int64_t)tt * L + l) * ny; };
-    auto st = [&](int tt, int l) { return p.states + ((int64_t)tt * L + l) * n1; };
-    a = snnflow_conv_fwd_args{};
-    a.B = p.B; a.H = p.H; a.W = p.W; a.c = C;
-    if (k == 0) {
-        a.cin = p.cin0; a.lif_in = 0;
-        a.x = p.x[t]; a.xs_b = p.xs[0]; a.xs_c = p.xs[1]; a.xs_h = p.xs[2]; a.xs_w = p.xs[3];
-    } else {
-        a.cin = C; a.lif_in = 1;
-        a.prev_y = ys(t, k - 1);
-        a.prev_mem = t == 0 ? p.mem0[k - 1] : st(t - 1, k - 1);
-        a.prev_acc = p.facc + ((int64_t)t * L + k - 1) * p.facc_stride;
-        a.prev_stats = p.stats + ((int64_t)t * L + k - 1) * 2 * C;
-        a.prev = p.n[k - 1];
-        a.prev_state = st(t, k - 1);
-    }
-    a.wt_ff = p.wt_ff[k]; a.wt_rec = p.wt_rec[k]; a.wt_ff_t = p.wt_ff_t[k]; a.wt_rec_t = p.wt_rec_t[k];
-    if (p.rec[k]) a.s_prev = t == 0 ? p.sprev0[k] : st(t - 1, k) + ny;
-    a.y = ys(t, k);
-    a.acc = p.train[k] ? p.facc + ((int64_t)t * L + k) * p.facc_stride : nullptr;
-}
-
-__device__ inline void seq_fwd_top_args(const snnflow_fwd_seq_args& p, int t, snnflow_lif_fwd_args& f) {
-    const int L = p.L, C = p.c, l = L - 1;
-    const int64_t ny = (int64_t)p.B * p.H * p.W * C, n1 = 2 * ny;
-    f = snnflow_lif_fwd_args{};
-    f.B = p.B; f.H = p.H; f.W = p.W; f.c = C;
-    f.y = p.ys + ((int64_t)t * L + l) * ny;
-    f.mem = t == 0 ? p.mem0[l] : p.states + ((int64_t)(t - 1) * L + l) * n1;
-    f.acc = p.facc + ((int64_t)t * L + l) * p.facc_stride;
-    f.stats = p.stats + ((int64_t)t * L + l) * 2 * C;
-    f.n = p.n[l];
-    f.state = p.states + ((int64_t)t * L + l) * n1;
-    f.pred_w = p.pred_w; f.pred_b = p.pred_b; f.flow = p.flow[t];
-}
-
-// Every layer-step's argument structs into the work area, read by k_fwd_seq through the scalar
-// cache like kernel arguments (one thread per layer-step).
-__global__ void k_fwd_seq_build(snnflow_fwd_seq_args p, snnflow_conv_fwd_args* conv, snnflow_lif_fwd_args* top) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x, K = p.L + 1;
-    if (j >= p.T * K) return;
-    const int t = j / K, k = j - t * K;
-    if (k < p.L) {
-        snnflow_conv_fwd_args a;
-        seq_fwd_conv_args(p, k, t, a);
-        conv[t * p.L + k] = a;
-    } else {
-        snnflow_lif_fwd_args f;
-        seq_fwd_top_args(p, t, f);
-        top[t] = f;
-    }
-}
-
-// One work item (kept out of line: inlined into the item loop, the bodies' per-thread loop-invariant
-// address math would be hoisted and held across every phase of every variant, 149 VGPRs).
-template <typename T>
-__device__ inline T* uniform_ptr(T* p) {  // a wave-uniform pointer argument back into SGPRs
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (T*)(((uint64_t)hi << 32) | lo);
-}
-
-// The LDS pool of the persistent forward at namespace scope: referenced by name inside the
-// out-of-line item function, its accesses stay ds_* (a pool handed in as a pointer argument is a
-// generic pointer there: flat_* accesses, whose waits also wait for every outstanding HBM load).
-__shared__ __attribute__((aligned(16))) float g_seq_fwd_pool[SlotLds<8>::FWD];
-
-template <int C>
-__device__ __attribute__((noinline)) void seq_fwd_item(const SeqFwdParams* pg, int k, int t, int i, int q) {
-    static_assert(C == 8, "persistent forward: C = 8");
-    float* const pool = g_seq_fwd_pool;
-    typedef const __attribute__((address_space(4))) SeqFwdParams* cptr;
-    const cptr pp = (cptr)uniform_ptr(pg);
-    k = __builtin_amdgcn_readfirstlane(k);
-    t = __builtin_amdgcn_readfirstlane(t);
-    i = __builtin_amdgcn_readfirstlane(i);
-    q = __builtin_amdgcn_readfirstlane(q);
-    const int L = pp->L, nconv = pp->nconv, ntop = pp->ntop;
-#ifndef SEQV
-#define SEQV 15
-#endif
-    if (k < L) {
-        const snnflow_conv_fwd_args a =
-            task_args((const __attribute__((address_space(4))) snnflow_conv_fwd_args*)pp->conv + (t * L + k));
-        const Grid g{q + 8 * i, nconv};
-        if (k == 0) {
-            if constexpr (SEQV & 1) {
-                if (a.cin == 2) conv_fwd_body<2, C, false, false, 2, kSeqSc1>(a, g, pool);
-                else conv_fwd_body<4, C, false, false, 2, kSeqSc1>(a, g, pool);
-            }
-        } else if (pp->rec[k]) {
-            if constexpr (SEQV & 2) conv_fwd_body<C, C, true, true, 2, kSeqSc1>(a, g, pool);
-        } else {
-            if constexpr (SEQV & 4) conv_fwd_body<C, C, true, false, 2, kSeqSc1>(a, g, pool);
-        }
-    } else {
-        if constexpr (SEQV & 8) {
-            const snnflow_lif_fwd_args f =
-                task_args((const __attribute__((address_space(4))) snnflow_lif_fwd_args*)pp->top + t);
-            lif_fwd_body<C, true, NT * 2, kSeqSc1>(f, Grid{q * (ntop / 8) + i, ntop});
-        }
-    }
-}
-
-template <int C>
-__global__ __launch_bounds__(NT * 2, 6) void k_fwd_seq(SeqFwdParams) {
-    typedef const __attribute__((address_space(4))) SeqFwdParams* cptr;
-    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
-    __shared__ int s_item;
-    const int tid = threadIdx.x;
-    const int T = pp->T, L = pp->L, K = L + 1, M = K + 2 * (T - 1);
-    const int nconv = pp->nconv, ntop = pp->ntop;
-    int* const sync = (int*)pp->sync;
-    const int q = xcc_id();
-    // scan position in the queue's wavefront order (items a block takes only increase)
-    int m = 0, t = 0, base = 0;
-    auto first_t = [&](int mm) { const int lo = mm - L; return lo > 0 ? (lo + 1) / 2 : 0; };
-    t = first_t(0);
-    // timing counters (wall clock, 100 MHz): grab + dependency wait, item bodies
-    unsigned long long tw = 0, ti = 0, nitems = 0;
-    for (;;) {
-        const unsigned long long c0 = wall_clock64();
-        if (tid == 0) s_item = __hip_atomic_fetch_add(sync + kSeqSyncHead + q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const int item = __builtin_amdgcn_readfirstlane(s_item);
-        // item -> (k, t, i): advance over whole layer-steps
-        int k = 0;
-        bool found = false;
-        while (m < M) {
-            k = m - 2 * t;
-            if (k < 0 || t >= T) {  // past this slot's last layer-step
-                ++m;
-                t = first_t(m);
-                continue;
-            }
-            const int cnt = (k < L ? nconv : ntop) / 8;
-            if (item < base + cnt) { found = true; break; }
-            base += cnt;
-            ++t;
-        }
-        if (!found) break;
-        const int i = item - base;
-        const int j = t * K + k;
-        // dependencies (lane 0 polls, the barrier releases every wave's loads behind it)
-        if (tid == 0) {
-            if (k >= 1) seq_wait(sync, t * K + k - 1, k - 1 < L ? nconv : ntop);
-            if (k >= 1 && t >= 1) seq_wait(sync, (t - 1) * K + k, k < L ? nconv : ntop);
-            if (k >= 1 && k < L && pp->rec[k] && t >= 1) seq_wait(sync, (t - 1) * K + k + 1, k + 1 < L ? nconv : ntop);
-            if (SNNFLOW_SEQ_FENCE) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        __syncthreads();
-        const unsigned long long c1 = wall_clock64();
-        seq_fwd_item<C>((const SeqFwdParams*)pp, k, t, i, q);
-        tw += c1 - c0;
-        ti += wall_clock64() - c1;
-        ++nitems;
-        // completion: every wave's stores and atomics acknowledged, then one count
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            if (SNNFLOW_SEQ_FENCE) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __hip_atomic_fetch_add(sync + kSeqSyncDone + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    if (tid == 0) {  // ints [10, 18) of the sync area: (wait ticks, item ticks, blocks, items) as u64
-        unsigned long long* st = reinterpret_cast<unsigned long long*>(sync + 10);
-        __hip_atomic_fetch_add(st, tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(st + 1, ti, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(st + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(st + 3, nitems, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -3311,6 +3372,7 @@ static bool slot_c(int c) { return c == 8 || c == 16 || c == 32; }
 #endif
 static int slot_rank(int kind) {
     switch (kind) {
+        case SK_LIF_REC_P: case SK_LIF_P: return 0;
         case SK_LIF_REC: case SK_PLAIN_REC: return 0;
         case SK_LIF: case SK_PLAIN: return 1;
         default: return 2;
@@ -3341,6 +3403,23 @@ static int slot_top_blocks(int c, int B, int H, int W) {
     const int64_t items = (npix + ppb * target - 1) / (ppb * target);
     return (int)((npix + ppb * items - 1) / (ppb * items));
 }
+
+// Tiles per block of the C = 8 tile pipelines (0: the one-tile-per-block bodies).  Defaults from
+// SNNFLOW_PIPE_FWD / SNNFLOW_PIPE_BWD at load time; snnflow_set_pipe overrides (A/B, tests).
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 0);
+static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
+
+// Blocks of a pipelined task: ceil(tiles / tpb), a multiple of 8 (block_tile's XCD groups).
+static int pipe_blocks(int ntiles, int tpb) {
+    const int nb = (ntiles + tpb - 1) / tpb;
+    return (nb + 7) / 8 * 8;
+}
+// The DMA halo reads address a tensor through one buffer descriptor: 32-bit byte offsets.
+static bool pipe_fits(int B, int H, int W, int c) { return (int64_t)B * H * W * c * 4 < ((int64_t)1 << 31); }
 
 int snnflow_slot_supported(int c, int cin0) { return slot_c(c) && (cin0 == 2 || cin0 == 4) ? 1 : 0; }
 
@@ -3382,8 +3461,12 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         if (c != 8 && !(kind == SK_HEAD2 || kind == SK_HEAD4 || kind == SK_LIF || kind == SK_LIF_REC))
             SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c = 16 / 32 runs the LIFFireNet task kinds only");
         p.conv[i] = a;
-        p.kind[i] = kind;
         p.nblk[i] = snnflow_conv_blocks(B, H, W);
+        if (c == 8 && g_pipe_fwd > 0 && (kind == SK_LIF || kind == SK_LIF_REC) && pipe_fits(B, H, W, c)) {
+            kind = kind == SK_LIF ? SK_LIF_P : SK_LIF_REC_P;
+            p.nblk[i] = pipe_blocks(p.nblk[i], g_pipe_fwd);
+        }
+        p.kind[i] = kind;
     }
     if (lif) {
         if (const int e = lif_fwd_check(lif)) return e;
@@ -3396,6 +3479,7 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
     }
     if (c != 8) slot_sort(p.conv, p.kind, p.nblk, nconv);
     else if (SNNFLOW_SLOT_ORDER8) slot_sort(p.conv, p.kind, p.nblk, nconv, SNNFLOW_SLOT_ORDER8 == 2);
+    else if (g_pipe_fwd > 1) slot_sort(p.conv, p.kind, p.nblk, nconv);  // multi-tile blocks first
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
@@ -3436,6 +3520,10 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         }
         if (c != 8 && !(kind == SK_HEAD2 || kind == SK_HEAD4 || kind == SK_LIF || kind == SK_LIF_REC))
             SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c = 16 / 32 runs the LIFFireNet task kinds only");
+        // the fused weight gradients exist for the C = 8 LIF-fed tasks only: anywhere else the layer's
+        // weight gradient would be silently lost
+        if ((a.wslab_ff || a.wslab_rec) && !(c == 8 && (kind == SK_LIF || kind == SK_LIF_REC)))
+            SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: wslab_ff / wslab_rec need a c = 8 LIF-fed task");
         p.layer[i] = a;
         p.kind[i] = kind;
         p.nblk[i] = layer_bwd_blocks(a);
@@ -3462,71 +3550,13 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
     return 0;
 }
 
-int snnflow_seq_sync_ints(int T, int L) { return kSeqSyncDone + T * (L + 1); }
-
-// Diagnostics: the XCC id each of n blocks of a 512-thread launch runs on (tests only).
-int snnflow_debug_xcc(int* out, int n, void* stream) {
-    hipLaunchKernelGGL(k_debug_xcc, dim3(n), dim3(2 * NT), 0, (hipStream_t)stream, out);
-    SNN_CHECK_LAUNCH();
+int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block) {
+    if (fwd_tiles_per_block < 0 || bwd_tiles_per_block < 0) SNN_FAIL(SNNFLOW_E_ARG, "set_pipe: negative tiles per block");
+    g_pipe_fwd = fwd_tiles_per_block;
+    g_pipe_bwd = bwd_tiles_per_block;
     return 0;
 }
-
-// work area: sync ints (padded to 256 B), then the conv argument structs [T][L], then the top ones [T]
-static size_t seq_sync_bytes(int T, int L) { return ((size_t)snnflow_seq_sync_ints(T, L) * sizeof(int) + 255) / 256 * 256; }
-size_t snnflow_seq_work_bytes(int T, int L) {
-    return seq_sync_bytes(T, L) + (size_t)T * L * sizeof(snnflow_conv_fwd_args) + (size_t)T * sizeof(snnflow_lif_fwd_args) + 256;
-}
-
-int snnflow_seq_supported(int c, int B, int H, int W, int T, int L) {
-    const int64_t npix = (int64_t)B * H * W;
-    return (c == 8 && B > 0 && B % 8 == 0 && npix % (2 * NT) == 0 && T >= 1 && T <= SNNFLOW_SEQ_MAX_T && L >= 1 &&
-            L <= SNNFLOW_MAX_LAYERS) ? 1 : 0;
-}
-
-int snnflow_fwd_seq(const snnflow_fwd_seq_args* a, void* stream) {
-    if (!a || !a->sync || !a->ys || !a->stats || !a->states || !a->facc || !a->pred_w || !a->pred_b)
-        SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: bad arguments");
-    if (!snnflow_seq_supported(a->c, a->B, a->H, a->W, a->T, a->L))
-        SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: unsupported shape (c == 8, B % 8 == 0, B*H*W % 512 == 0, T <= 16)");
-    if (a->cin0 != 2 && a->cin0 != 4) SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_seq: cin0 must be 2 or 4");
-    for (int t = 0; t < a->T; ++t)
-        if (!a->x[t] || !a->flow[t]) SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: step input / flow missing");
-    for (int l = 0; l < a->L; ++l) {
-        if (!a->wt_ff[l] || !a->wt_ff_t[l] || (a->rec[l] && (!a->wt_rec[l] || !a->wt_rec_t[l])))
-            SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: weights");
-        if (l == 0 && a->rec[0]) SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: the head is feed-forward");
-    }
-    SeqFwdParams p = {};
-    p.T = a->T; p.L = a->L;
-    p.nconv = snnflow_conv_blocks(a->B, a->H, a->W);
-    p.ntop = slot_top_blocks(a->c, a->B, a->H, a->W);
-    if (p.nconv % 8 || p.ntop % 8) SNN_FAIL(SNNFLOW_E_ARG, "fwd_seq: block counts must be multiples of 8");
-    for (int l = 0; l < a->L; ++l) p.rec[l] = a->rec[l] ? 1 : 0;
-    char* work = reinterpret_cast<char*>(a->sync);
-    p.sync = a->sync;
-    snnflow_conv_fwd_args* conv = reinterpret_cast<snnflow_conv_fwd_args*>(work + seq_sync_bytes(a->T, a->L));
-    snnflow_lif_fwd_args* top = reinterpret_cast<snnflow_lif_fwd_args*>(conv + a->T * a->L);
-    p.conv = conv;
-    p.top = top;
-    const hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(a->sync, 0, sizeof(int) * snnflow_seq_sync_ints(a->T, a->L), s);
-    if (e != hipSuccess) return snnflow_set_error((int)e, "fwd_seq: memset");
-    const int ntask = a->T * (a->L + 1);
-    hipLaunchKernelGGL(k_fwd_seq_build, dim3((ntask + 63) / 64), dim3(64), 0, s, *a, conv, top);
-    // grid: every block resident (a waiting block must never keep an item's producer from a CU)
-    static int cus = 0, per_cu = 0;
-    if (!cus) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return snnflow_set_error(SNNFLOW_E_ARG, "fwd_seq: device query");
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_fwd_seq<8>, 2 * NT, 0) != hipSuccess) nb = 1;
-        per_cu = nb < 1 ? 1 : (nb > 3 ? 3 : nb);
-    }
-    hipLaunchKernelGGL(k_fwd_seq<8>, dim3(cus * per_cu), dim3(2 * NT), 0, s, p);
-    SNN_CHECK_LAUNCH();
-    return 0;
-}
+int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : g_pipe_bwd; }
 
 int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
     if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || a->nsteps <= 0 || a->nsteps > SNNFLOW_MAX_WGRAD_STEPS ||

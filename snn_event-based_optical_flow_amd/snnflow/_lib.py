@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 26
+ABI_VERSION = 27
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -224,20 +224,6 @@ class FireNetBwdIo(ctypes.Structure):
                 ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32)]
 
 
-SEQ_MAX_T = 16
-
-
-class FwdSeqArgs(ctypes.Structure):
-    """include/snnflow.h snnflow_fwd_seq_args (persistent dataflow forward of a window)."""
-    _fields_ = [("T", I32), ("L", I32), ("B", I32), ("H", I32), ("W", I32), ("c", I32), ("cin0", I32),
-                ("rec", I32 * MAX_LAYERS), ("train", I32 * MAX_LAYERS), ("n", Neuron * MAX_LAYERS),
-                ("wt_ff", PL), ("wt_rec", PL), ("wt_ff_t", PL), ("wt_rec_t", PL),
-                ("pred_w", P), ("pred_b", P),
-                ("x", P * SEQ_MAX_T), ("xs", I64 * 4), ("flow", P * SEQ_MAX_T),
-                ("ys", P), ("stats", P), ("states", P), ("facc", P), ("facc_stride", I64),
-                ("mem0", PL), ("sprev0", PL), ("sync", P)]
-
-
 class FireNetWgradStep(ctypes.Structure):
     _fields_ = [("g_cur", P), ("bnc", P), ("ys", P), ("stats", P), ("x", P), ("xs", I64 * 4), ("states", P),
                 ("s_prev", PL)]
@@ -298,13 +284,10 @@ EXPORTS = {
     "snnflow_clip_grad_norm_large": (I32, [P, I64, F32, F32, P, P, P]),
     "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),
     "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
-    "snnflow_fwd_seq": (I32, [ctypes.POINTER(FwdSeqArgs), P]),
-    "snnflow_seq_sync_ints": (I32, [I32, I32]),
-    "snnflow_seq_work_bytes": (ctypes.c_size_t, [I32, I32]),
-    "snnflow_seq_supported": (I32, [I32, I32, I32, I32, I32, I32]),
-    "snnflow_debug_xcc": (I32, [P, I32, P]),
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),
     "snnflow_slot_supported": (I32, [I32, I32]),
+    "snnflow_set_pipe": (I32, [I32, I32]),
+    "snnflow_get_pipe": (I32, [I32]),
     "snnflow_frag_halfs": (I32, [I32, I32]),
     "snnflow_unet_conv": (I32, [ctypes.POINTER(UNetConvArgs), P]),
     "snnflow_unet_conv_ksplit": (I32, [ctypes.POINTER(UNetConvArgs)]),

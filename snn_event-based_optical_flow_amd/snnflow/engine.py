@@ -883,19 +883,6 @@ def _ptr_t(t):
 # ---------------------------------------------------------------------------
 # A whole truncated-BPTT window in one autograd node, launched in wavefront order
 # ---------------------------------------------------------------------------
-def _seq_ok(eng, B, H, W, T, cin0, xs):
-    """The persistent dataflow forward (snnflow_fwd_seq) takes this window: C = 8, B % 8 == 0, whole
-    512-pixel blocks, T <= 16, a feed-forward 2- or 4-bin head, one stride set for every step's input
-    (SNNFLOW_SEQ=0 selects the wavefront launches instead)."""
-    import os
-    if os.environ.get("SNNFLOW_SEQ", "0") == "0" or eng.rec[0] or cin0 not in (2, 4):
-        return False
-    if not lib.snnflow_seq_supported(eng.C, B, H, W, T, eng.L):
-        return False
-    st = xs[0].stride()
-    return all(x.stride() == st for x in xs)
-
-
 @functools.lru_cache(maxsize=64)
 def capped_slots(T, K, rec, cap):
     """Launch order of the (kernel k < K, step t < T) grid with at most `cap` tasks per launch,
@@ -1019,43 +1006,19 @@ class FireNetSequence(torch.autograd.Function):
         neurons = eng.neurons()
         train = [bn.training or not bn.track_running_stats for bn in eng.bns]
 
-        if _seq_ok(eng, B, H, W, T, cin0, xs):
-            # one persistent dataflow launch (snnflow_fwd_seq): the same layer-steps, no wavefront rounds
-            sa = _lib.FwdSeqArgs()
-            sa.T, sa.L, sa.B, sa.H, sa.W, sa.c, sa.cin0 = T, L, B, H, W, C, cin0
-            for l in range(L):
-                sa.rec[l] = 1 if eng.rec[l] else 0
-                sa.train[l] = 1 if train[l] else 0
-                sa.n[l] = neurons[l]
-                sa.wt_ff[l], sa.wt_rec[l] = _ptr_t(wfwd[l][0]), _ptr_t(wfwd[l][1])
-                sa.wt_ff_t[l], sa.wt_rec_t[l] = _ptr_t(wbwd[l][0]), _ptr_t(wbwd[l][1])
-                sa.mem0[l] = _ptr_t(mem0[l])
-                sa.sprev0[l] = _ptr_t(sprev0[l])
-            sa.pred_w, sa.pred_b = ptr(eng.pred.weight), ptr(eng.pred.bias)
-            for t in range(T):
-                sa.x[t] = xs[t].data_ptr()
-                sa.flow[t] = flows[t].data_ptr()
-            sa.xs[0], sa.xs[1], sa.xs[2], sa.xs[3] = xs[0].stride()
-            sa.ys, sa.stats, sa.states = ys.data_ptr(), stats.data_ptr(), st_all.data_ptr()
-            sa.facc, sa.facc_stride = facc.data_ptr(), facc.stride(1)
-            work = torch.empty(int(lib.snnflow_seq_work_bytes(T, L)), dtype=torch.uint8, device=dev)
-            sa.sync = work.data_ptr()
-            _lib.call("fwd_seq", lib.snnflow_fwd_seq, ctypes.byref(sa), s)
-            eng.last_seq_work = work  # tests read the timeout flag (int 8 of the work area)
-        else:
-            frec = tuple(bool(eng.rec[k]) if k < L else False for k in range(L + 1))
-            for tasks in capped_slots(T, L + 1, frec, slot_cap()):
-                convs, top = [], None
-                for k, t in tasks:
-                    if k < L:
-                        convs.append(_fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
-                                                    s_prev[t], facc[t], neurons, train, wfwd, wbwd))
-                    else:
-                        top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons,
-                                            flows[t])
-                arr = (_lib.ConvFwdArgs * max(len(convs), 1))(*convs)
-                _lib.call("fwd_slot", lib.snnflow_fwd_slot, arr, len(convs), ctypes.byref(top) if top is not None else None,
-                          s)
+        frec = tuple(bool(eng.rec[k]) if k < L else False for k in range(L + 1))
+        for tasks in capped_slots(T, L + 1, frec, slot_cap()):
+            convs, top = [], None
+            for k, t in tasks:
+                if k < L:
+                    convs.append(_fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
+                                                s_prev[t], facc[t], neurons, train, wfwd, wbwd))
+                else:
+                    top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons,
+                                        flows[t])
+            arr = (_lib.ConvFwdArgs * max(len(convs), 1))(*convs)
+            _lib.call("fwd_slot", lib.snnflow_fwd_slot, arr, len(convs), ctypes.byref(top) if top is not None else None,
+                      s)
         _lib.timer_close()
 
         if eng.capture_states:  # tests / diagnostics: the window's pre-BN currents, statistics, batch sums

@@ -374,6 +374,9 @@ def _unet_seg(act, mode, kc0, nparts=3):
 
 _PARTIAL = {}
 _SHAPES = os.environ.get("SNNFLOW_UNET_SHAPES") == "1"  # profiling: kernel names carry the GEMM shape
+# Tests: set to a list to record every GEMM launch's split plan as (kind, M, K, P, plan) -- plan is the
+# split-K factor of a conv / input gradient, the partial-sum floats (pixel-split plan) of a weight gradient
+PLAN_LOG = None
 
 
 def _name(kind, M, K, P):
@@ -392,6 +395,8 @@ def _split_k(a, P, dev):
     """Split-K of a launch (library's choice) with the shared partial-sum workspace (stream-ordered
     reuse; sized by the largest request, which the eager warm-up steps make before any graph capture)."""
     ks = lib.snnflow_unet_conv_ksplit(ctypes.byref(a))
+    if PLAN_LOG is not None:
+        PLAN_LOG.append(("dgrad" if a.xparts == 3 else "conv", a.M, sum(a.seg[i].cpitch for i in range(a.nseg)), P, ks))
     if ks <= 1:
         a.ksplit, a.partial = 1, None
         return
@@ -456,6 +461,8 @@ def wgrad(plan, sg, g3, B, Ho, Wo, act, s):
     a.seg = _unet_seg(act, sg.mode, sg.kc0)
     a.k0, a.ktot, a.dwk = sg.k0, plan.ktot, ptr(plan.dwk)
     n = lib.snnflow_unet_wgrad_partial_floats(ctypes.byref(a))  # deterministic split sums
+    if PLAN_LOG is not None:
+        PLAN_LOG.append(("wgrad", a.M, a.seg.cpitch, B * Ho * Wo, int(n)))
     a.partial = _workspace(n, plan.dwk.device).data_ptr() if n > 0 else None
     _lib.call(_name("unet_wgrad", plan.C, a.seg.cpitch, B * Ho * Wo), lib.snnflow_unet_wgrad, ctypes.byref(a), s,
               work=2.0 * B * Ho * Wo * plan.C * sg.weight.shape[1] * plan.taps)
@@ -795,7 +802,7 @@ class UNetStep(torch.autograd.Function):
                 gf = gf.float().contiguous()
             npart = int(lib.snnflow_unet_pred_bwd_partial_doubles(B, h2, w2, C))
             part = d.__dict__.get("pred_part")
-            if part is None or part.numel() < npart:
+            if part is None or part.numel() < npart or part.device != dev:
                 part = d.pred_part = torch.empty(npart, dtype=torch.float64, device=dev)
             _lib.call("unet_pred_bwd", lib.snnflow_unet_pred_bwd, ptr(act), act.shape[-1], C, ptr(pw.weight),
                       ptr(S.flows_lo[i]), ptr(gf), ptr(g_extra), B, h2, w2, H // h2, ptr(gpre), ptr(gacts[f"d{i}"]),

@@ -46,7 +46,6 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_pointwise_args": _lib.PointwiseArgs,
         "snnflow_firenet_plan": _lib.FireNetPlan, "snnflow_firenet_fwd_io": _lib.FireNetFwdIo,
         "snnflow_firenet_bwd_io": _lib.FireNetBwdIo, "snnflow_firenet_wgrad_step": _lib.FireNetWgradStep,
-        "snnflow_fwd_seq_args": _lib.FwdSeqArgs,
     }
     lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():

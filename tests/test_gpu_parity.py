@@ -1339,14 +1339,18 @@ def test_log_activity_with_forward_hooks(dev):
     assert len(seen) == 2
 
 
-@pytest.mark.parametrize("name,H,W,T", [("LIFFireNet", 32, 32, 5), ("LIFFireNet", 64, 32, 2), ("LIFFireNet", 32, 48, 16),
-                                        ("LIFFireNet_short", 32, 32, 4), ("LIFFireFlowNet", 32, 32, 3)])
-def test_persistent_forward_matches_slots(dev, monkeypatch, name, H, W, T):
-    """The persistent dataflow forward (snnflow_fwd_seq: one launch, per-XCD work queues, per
-    layer-step completion counters) against the wavefront slot launches (SNNFLOW_SEQ=0) on the same
-    window: flows, every state, the lif.mem caches, BatchNorm running statistics and
-    num_batches_tracked, the backward's gradients; and the launch's timeout flag is clear.  Same
-    per-(layer, step) arithmetic; only the fp64 batch-sum atomics may add in another order."""
+@pytest.mark.parametrize("name,B,H,W,T,tpb", [("LIFFireNet", 8, 32, 32, 5, 2), ("LIFFireNet", 8, 64, 32, 2, 1),
+                                               ("LIFFireNet", 8, 32, 48, 6, 3), ("LIFFireNet", 3, 40, 72, 4, 2),
+                                               ("LIFFireNet_short", 8, 32, 32, 4, 4), ("LIFFireFlowNet", 8, 32, 32, 3, 2)])
+def test_pipelined_slots_match_one_tile_slots(dev, name, B, H, W, T, tpb):
+    """The C = 8 tile pipelines of the wavefront launches (fwd_lif8_pipe: several tiles per block, the
+    next tile's halo by LDS-DMA, swapped-operand convs packed by permlane32_swap) against the
+    one-tile-per-block bodies (snnflow_set_pipe(0, 0)) on the same window: flows, every state, the
+    lif.mem caches, BatchNorm running statistics and num_batches_tracked, and the backward's
+    gradients.  Shapes include partial tiles (W = 48, 40 x 72), a batch that is not a multiple of 8
+    and blocks with 1-4 tiles.  Same per-(layer, step) arithmetic; the batch sums add in another
+    order (fp32 per lane over a block's tiles, fp64 atomics), so spikes may only differ where the
+    membrane lies within rounding of the threshold."""
     import copy
 
     import snnflow
@@ -1354,41 +1358,75 @@ def test_persistent_forward_matches_slots(dev, monkeypatch, name, H, W, T):
     from snnflow import _lib
     from snnflow.synthetic import make_window
 
-    B = 8
     torch.manual_seed(21)
     kw = lif_ref.make_unet_kwargs(base_num_channels=8)
     ma = getattr(snnflow, name)(dict(kw)).to(dev).train()
     mb = copy.deepcopy(ma)
-    assert _lib.lib.snnflow_seq_supported(8, B, H, W, T, ma.engine.L)
     gen = torch.Generator(device=dev).manual_seed(22)
     wins = [make_window(B, 500, H, W, gen, dev) for _ in range(T)]
     res = {}
-    for tag, m, flag in (("seq", ma, "1"), ("slots", mb, "0")):
-        monkeypatch.setenv("SNNFLOW_SEQ", flag)
-        m.engine.last_seq_work = None
-        outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
-        loss = sum(((o["flow"][0] * (t + 1)) ** 2).sum() for t, o in enumerate(outs))
-        loss.backward()
-        torch.cuda.synchronize()
-        res[tag] = outs
-        if flag == "1":
-            work = m.engine.last_seq_work
-            assert work is not None, "the persistent path did not run"
-            assert int(work[:64].view(torch.int32)[8].item()) == 0, "dependency wait timed out"
-        else:
-            assert m.engine.last_seq_work is None
+    old = (_lib.lib.snnflow_get_pipe(0), _lib.lib.snnflow_get_pipe(1))
+    try:
+        for tag, m, fwd in (("pipe", ma, tpb), ("one", mb, 0)):
+            assert _lib.lib.snnflow_set_pipe(fwd, old[1]) == 0
+            outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+            loss = sum(((o["flow"][0] * (t + 1)) ** 2).sum() for t, o in enumerate(outs))
+            loss.backward()
+            torch.cuda.synchronize()
+            res[tag] = outs
+    finally:
+        _lib.lib.snnflow_set_pipe(*old)
     for t in range(T):
-        np.testing.assert_allclose(res["seq"][t]["flow"][0].detach().cpu().numpy(),
-                                   res["slots"][t]["flow"][0].detach().cpu().numpy(), rtol=1e-6, atol=1e-8)
+        np.testing.assert_allclose(res["pipe"][t]["flow"][0].detach().cpu().numpy(),
+                                   res["one"][t]["flow"][0].detach().cpu().numpy(), rtol=1e-5, atol=1e-6)
     for sa, sb in zip(ma.states, mb.states):
-        np.testing.assert_allclose(sa.detach().cpu().numpy(), sb.detach().cpu().numpy(), rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(sa.detach().cpu().numpy(), sb.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)
     for (n, a), (_, b) in zip(ma.named_buffers(), mb.named_buffers()):
-        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-8, err_msg=n)
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-6, atol=1e-7, err_msg=n)
     for n, _ in ma.layer_spec:
         np.testing.assert_allclose(getattr(ma, n).lif.mem.cpu().numpy(), getattr(mb, n).lif.mem.cpu().numpy(),
-                                   rtol=1e-6, atol=1e-7)
+                                   rtol=1e-5, atol=1e-5)
     for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
         assert _rel(a.grad.cpu().numpy(), b.grad.cpu().numpy()) < 1e-5, n
+
+
+def test_pipelined_forward_nonbinary_state(dev):
+    """Initial states whose spike half is not 0/1 (a caller-provided state): the recurrent conv of the
+    pipelined forward detects s_prev values that are not exact in bf16 and computes that tile's
+    recurrent conv on the vector ALU in f32; flows and states equal the one-tile bodies' (which
+    take the f32 matrix-core path there)."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow import _lib
+    from snnflow.synthetic import make_window
+
+    B, H, W, T = 8, 32, 32, 2
+    torch.manual_seed(5)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=8)
+    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    gen = torch.Generator(device=dev).manual_seed(6)
+    wins = [make_window(B, 500, H, W, gen, dev) for _ in range(T)]
+    states = [torch.rand(2, B, 8, H, W, generator=gen, device=dev) for _ in range(ma.engine.L)]
+    res = {}
+    old = (_lib.lib.snnflow_get_pipe(0), _lib.lib.snnflow_get_pipe(1))
+    try:
+        for tag, m, fwd in (("pipe", ma, 2), ("one", mb, 0)):
+            _lib.lib.snnflow_set_pipe(fwd, old[1])
+            m.states = [s.clone() for s in states]
+            with torch.no_grad():
+                outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+            torch.cuda.synchronize()
+            res[tag] = outs
+    finally:
+        _lib.lib.snnflow_set_pipe(*old)
+    for t in range(T):
+        np.testing.assert_allclose(res["pipe"][t]["flow"][0].cpu().numpy(), res["one"][t]["flow"][0].cpu().numpy(),
+                                   rtol=1e-5, atol=1e-6)
+    for sa, sb in zip(ma.states, mb.states):
+        np.testing.assert_allclose(sa.cpu().numpy(), sb.cpu().numpy(), rtol=1e-5, atol=1e-5)
 
 
 def test_iwe_loss_bit_reproducible(dev):
