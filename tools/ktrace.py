@@ -46,7 +46,7 @@ def main(C=8, R=128, B=8):
         lf().backward()
         model.detach_states()
     torch.cuda.synchronize()
-    buf = np.zeros((4, 4096, 8), dtype=np.uint64)
+    buf = np.zeros((4, 4096, 16), dtype=np.uint64)
     fn = _lib.lib.snnflow_trace_copy
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     assert fn(buf.ctypes.data, buf.nbytes) == 0

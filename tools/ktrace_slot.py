@@ -24,6 +24,15 @@ KINDS = {0: ("conv_fwd", ["prologue", "lif_halo", "conv", "store+sums"]),
          3: ("layer_bwd_rec", ["prologue", "bn_bwd_halo", "dgrad", "lif_bwd+store", "sums", "fused_wgrad"])}
 
 
+if os.environ.get("KTRACE_PIPE") == "1":  # fwd_lif8_pipe (2 tiles per block): stamps per tile
+    _P = ["gather", "coef", "frag+zero", "wait0", "lif0", "conv0", "wait1", "lif1", "conv1"]
+    KINDS[0] = ("pipe_fwd", _P)
+    KINDS[1] = ("pipe_fwd_rec", _P)
+    _B = ["prologue", "wait0", "bn_bwd0", "dgrad0", "lif_bwd0", "wgrad0", "wait1", "bn_bwd1", "dgrad1", "lif_bwd1", "wgrad1"]
+    KINDS[2] = ("pipe_bwd", _B)
+    KINDS[3] = ("pipe_bwd_rec", _B)
+
+
 def main(C=8, R=128, B=8, T=10):
     import snnflow
     from snnflow import _lib
@@ -47,7 +56,7 @@ def main(C=8, R=128, B=8, T=10):
         lf().backward()
         model.detach_states()
     torch.cuda.synchronize()
-    buf = np.zeros((4, 4096, 8), dtype=np.uint64)
+    buf = np.zeros((4, 4096, 16), dtype=np.uint64)
     fn = _lib.lib.snnflow_trace_copy
     fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     assert fn(buf.ctypes.data, buf.nbytes) == 0
