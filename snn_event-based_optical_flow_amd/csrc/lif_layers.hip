@@ -3859,7 +3859,7 @@ static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
 }
-static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 0);
+static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 2);
 static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
 // Block order of a C = 8 launch with pipelined tasks: 0 layer order, 1 pipelined tasks first, 2 last
 static int g_pipe_order = env_int("SNNFLOW_PIPE_ORDER", 1);
