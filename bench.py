@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--dist-backend", default=None,
                    help="nccl (= RCCL; the default when a GPU is present) or gloo (rehearsals, CPU, "
                         "SNNFLOW_SHARE_GPU=1)")
+    p.add_argument("--bn-broadcast", action="store_true",
+                   help="N>1: after the timed steps, broadcast rank 0's BatchNorm running statistics to every rank "
+                        "(snnflow.dp.broadcast_bn_stats; not part of the timed step)")
     p.add_argument("--dp-check", action="store_true",
                    help="N>1 correctness check of this very step path (gloo rehearsal): the all-reduced "
                         "gradient == the sum of the ranks' own gradients, parameters identical after the update")
@@ -332,6 +335,8 @@ def main():
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
+    if world > 1 and args.bn_broadcast:
+        dp.broadcast_bn_stats(model)
     ms_per_step = 1000.0 * elapsed / args.steps
     events_per_step = world * B * T * N
     value = events_per_step * args.steps / elapsed

@@ -370,6 +370,8 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     [[maybe_unused]] constexpr bool TR = LIF_IN && CIN == C;
     [[maybe_unused]] constexpr int TK = REC ? 1 : 0;
     TRACE_AT(TR, TK, 0);
+    __shared__ int rec_bad[1];
+    if (tid == 0) rec_bad[0] = 0;  // (read after the barrier that follows the exactness test)
 
     // 1. issue every global load of the tile before any use: the BN-sum replicas first (their
     //    reduction and the coefficients then overlap the halo loads), weights for LDS next
@@ -468,8 +470,8 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
             if (has_rec) fs_rec.store(reinterpret_cast<__bf16*>(wl_rec));
         }
     }
-    // previous-step spikes exact in bf16 (0/1; always so on the engine path) -> bf16 MFMA
-    bool rec_bf = false;
+    // previous-step spikes exact in bf16 (0/1; always so on the engine path) -> bf16 MFMA; a wave with an
+    // inexact value sets an LDS flag (cleared at kernel start) instead of __syncthreads_and's barriers
     if constexpr (PF_REC) {
         if (has_rec) {
             halo_store<C, NTB>(rtile, rs);
@@ -477,10 +479,11 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
 #pragma unroll
             for (int i = 0; i < Halo4<C, NTB>::R; ++i)
                 ok = ok && exact_bf16(rs[i].x) && exact_bf16(rs[i].y) && exact_bf16(rs[i].z) && exact_bf16(rs[i].w);
-            rec_bf = __syncthreads_and(ok) != 0;
+            if (__builtin_amdgcn_ballot_w64(!ok) != 0 && (tid & 63) == 0) rec_bad[0] = 1;
         }
     }
     __syncthreads();
+    const bool rec_bf = PF_REC && has_rec && rec_bad[0] == 0;
     TRACE_AT(TR, TK, 2);
 
     float y[CO];
@@ -2662,7 +2665,7 @@ __device__ inline void globalize(snnflow_conv_fwd_args& a) {
     SNN_G(a.x); SNN_G(a.prev_y); SNN_G(a.prev_mem); SNN_G(a.prev_acc); SNN_G(a.prev_stats);
     globalize(a.prev);
     SNN_G(a.prev_state); SNN_G(a.wt_ff); SNN_G(a.wt_rec); SNN_G(a.wt_ff_t); SNN_G(a.wt_rec_t); SNN_G(a.s_prev);
-    SNN_G(a.y); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1); SNN_G(a.wf_ff); SNN_G(a.wf_rec);
+    SNN_G(a.y); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1); SNN_G(a.wf_ff); SNN_G(a.wf_rec); SNN_G(a.tile_counter);
 }
 __device__ inline void globalize(snnflow_lif_fwd_args& a) {
     SNN_G(a.y); SNN_G(a.mem); SNN_G(a.acc); SNN_G(a.stats);
@@ -2784,8 +2787,41 @@ __host__ __device__ inline int pipe_tiles(const Grid& g, int ntiles) {
     return g.bid < ntiles ? (ntiles - 1 - g.bid) / g.nb + 1 : 0;
 }
 
+// The tiles of a pipelined block.  Static (no tile counter): v = bid, bid + nb, ...  Dynamic
+// (snnflow_conv_fwd_args.tile_counter): the first tile v = bid (the task's own blocks), then tiles
+// v = nfirst + atomicAdd(counter, 1) while v < ntiles, requested one tile ahead (the request of tile
+// k + 2 is issued at the top of tile k and its answer written to LDS at the end of tile k), so a
+// block that runs fast takes more tiles and the task's blocks finish together.  (Steal mode, a block
+// taking tiles of another task of the launch once its own are done, needs a second inlined body at a
+// run-time-chosen task: 49 spilled registers -- not kept; the host sizes the tasks' block counts by
+// their per-tile cost instead, snnflow_fwd_slot.)
+struct PipeSeq {
+    int* ctr;     // NULL: static
+    int nfirst;   // tiles handed out statically (v < nfirst)
+    int ntiles, bid, nb;
+    __device__ int first(bool steal, int* slot) const {
+        if (!steal) return bid < ntiles ? bid : -1;
+        if (threadIdx.x == 0) slot[0] = grab_now();
+        __syncthreads();
+        const int v = __builtin_amdgcn_readfirstlane(slot[0]);  // (block-uniform: scalar registers)
+        __syncthreads();
+        return v;
+    }
+    __device__ int grab_now() const {
+        const int v = nfirst + atomicAdd(ctr, 1);
+        return v < ntiles ? v : -1;
+    }
+    __device__ int static_next(int v) const { return v + nb < ntiles ? v + nb : -1; }
+};
+
+// Per-block scheduling state in LDS (the dynamic request's answer)
+__device__ inline int* pipe_slot() {
+    __shared__ int slot[4];
+    return slot;
+}
+
 template <bool REC>
-__device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, float* pool) {
+__device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, float* pool, bool steal = false) {
     constexpr int C = 8, NTB = 2 * NT, R = Halo4<C, NTB>::R;
     using L = PipeFwdLds<REC>;
     char* const lds = reinterpret_cast<char*>(pool);
@@ -2794,8 +2830,14 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int H = a.H, W = a.W, ntiles = a.B * tiles_per_image(H, W);
-    const int nt = pipe_tiles(g, ntiles);
-    const bool lead = g.bid == 0;
+    const PipeSeq seq{a.tile_counter, g.nb < ntiles ? g.nb : ntiles, ntiles, g.bid, g.nb};
+    const bool dyn = a.tile_counter != nullptr;
+    int* const slot = pipe_slot();
+    int v_cur = seq.first(steal, slot);
+    if (v_cur < 0) return;  // (steal mode: nothing left; block-uniform)
+    int req = -1;
+    if (dyn && tid == 0) req = seq.grab_now();
+    const bool lead = !steal && g.bid == 0;
     const bool has_mem = a.prev_mem != nullptr;
     const bool has_rec = REC && a.s_prev != nullptr;
     TRACE_AT(true, REC ? 1 : 0, 0);
@@ -2829,7 +2871,6 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
                                                          16, off, 0, 0, 0);
         }
     };
-    auto tile_of = [&](int k) { return block_tile(H, W, Grid{g.bid + k * g.nb, ntiles}); };
     float4 rs[R];  // s_prev halo of the next tile (registers, issued one tile ahead)
     auto load_sprev = [&](const Tile& t, int tid) {  // halo_load's element order, 32-bit offsets from the halo origin
         const float4* base = reinterpret_cast<const float4*>(a.s_prev) + (((int64_t)t.b * H + (t.h0 - 1)) * W + (t.w0 - 1)) * 2;
@@ -2840,18 +2881,18 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
             rs[i] = ok ? base[(r * W + cc) * 2 + (e & 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     };
-    Tile tl = tile_of(0);
-    if (nt > 0) {
-        issue(tl, lane);
-        if (has_rec) load_sprev(tl, tid);
-    }
+    Tile tl = block_tile(H, W, Grid{v_cur, ntiles});
+    issue(tl, lane);
+    if (has_rec) load_sprev(tl, tid);
     if (a.prev.bn_train) acc_gather_reduce<2 * C>(gat, sums);
     TRACE_AT(true, REC ? 1 : 0, 1);
-    lif_prologue(a.prev, nr, sums, C, (double)a.B * H * W, a.prev_stats, coef, nullptr, lead);
+    lif_prologue(a.prev, nr, sums, C, (double)a.B * H * W, steal ? nullptr : a.prev_stats, coef, nullptr, lead);
     TRACE_AT(true, REC ? 1 : 0, 2);
     fz_ff.store(reinterpret_cast<__bf16*>(lds + L::FF));
     if (has_rec) fz_rec.store(reinterpret_cast<__bf16*>(lds + L::FR));
-    zero_consumed(a.zero0, a.zero1, a.zero_n, g);
+    if (!steal) zero_consumed(a.zero0, a.zero1, a.zero_n, g);
+    if (dyn && tid == 0) slot[1] = req;
+    if (tid == 0) slot[2] = 0;  // the s_prev exactness flag of tile 0
 
     const bool zr = a.prev.zero_reset != 0;
     const int64_t plane4 = (int64_t)a.B * H * W * 2;
@@ -2861,7 +2902,7 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
     const __bf16* rspk = reinterpret_cast<const __bf16*>(lds + L::RSPK);
     TRACE_AT(true, REC ? 1 : 0, 3);
 
-    for (int k = 0; k < nt; ++k) {
+    for ([[maybe_unused]] int k = 0; v_cur >= 0; ++k) {
         vm_wait<0>();     // this wave's DMA and s_prev loads of tile k (and its stores of tile k-1)
         __syncthreads();  // every wave's DMA landed; every wave is done with the spike tiles of k-1
         TRACE_AT(k < 2, REC ? 1 : 0, 4 + 3 * k);
@@ -2900,12 +2941,20 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
                 }
             }
         }
-        // raw halos free, spike tiles complete (and: is s_prev exact in bf16 everywhere?)
-        const bool rec_bf = has_rec ? __syncthreads_and(ok) != 0 : (__syncthreads(), false);
+        // raw halos free, spike tiles complete (and: is s_prev exact in bf16 everywhere?  A wave with an
+        // inexact value sets this tile's LDS flag -- two flags alternate over the tiles, the other one
+        // is cleared here for the next tile -- instead of __syncthreads_and's three barriers)
+        int* const bad = slot + 2;  // pipe_slot()[2..3]
+        if (has_rec && __builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0) bad[k & 1] = 1;
+        if (threadIdx.x == 0) bad[(k + 1) & 1] = 0;
+        __syncthreads();
+        const bool rec_bf = has_rec && bad[k & 1] == 0;
         TRACE_AT(k < 2, REC ? 1 : 0, 5 + 3 * k);
+        const int v_nxt = dyn ? __builtin_amdgcn_readfirstlane(slot[1]) : seq.static_next(v_cur);
+        if (dyn && tid == 0 && v_nxt >= 0) req = seq.grab_now();
         const Tile cur = tl;
-        if (k + 1 < nt) {
-            tl = tile_of(k + 1);
+        if (v_nxt >= 0) {
+            tl = block_tile(H, W, Grid{v_nxt, ntiles});
             issue(tl, lane);
             if (has_rec) load_sprev(tl, tid);
         }
@@ -2976,6 +3025,8 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
             }
         }
         TRACE_AT(k < 2, REC ? 1 : 0, 6 + 3 * k);
+        if (dyn && tid == 0) slot[1] = v_nxt >= 0 ? req : -1;
+        v_cur = v_nxt;
     }
 
     // ---- batch sums of the block's tiles: 16-lane rows by DPP, rows and waves through LDS, fp64 atomics
@@ -3034,9 +3085,11 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? 6 : 1) void k_fwd_slot(FwdSlotPara
         case SK_LIF_P:
         case SK_LIF_REC_P: {
             if constexpr (C == 8) {
-                const snnflow_conv_fwd_args a = task_args(&pp->conv[k]);
-                if (pp->kind[k] == SK_LIF_REC_P) fwd_lif8_pipe<true>(a, g, pool);
-                else fwd_lif8_pipe<false>(a, g, pool);
+                {
+                    const snnflow_conv_fwd_args a = task_args(&pp->conv[k]);
+                    if (pp->kind[k] == SK_LIF_REC_P) fwd_lif8_pipe<true>(a, g, pool);
+                    else fwd_lif8_pipe<false>(a, g, pool);
+                }
             }
             break;
         }
@@ -3863,6 +3916,8 @@ static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 2);
 static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
 // Block order of a C = 8 launch with pipelined tasks: 0 layer order, 1 pipelined tasks first, 2 last
 static int g_pipe_order = env_int("SNNFLOW_PIPE_ORDER", 1);
+// Blocks of a recurrent pipelined task relative to a feed-forward one, percent (dynamic tiles only)
+static int g_pipe_recw = env_int("SNNFLOW_PIPE_RECW", 150);
 
 // Blocks of a pipelined task: ceil(tiles / tpb), a multiple of 8 (block_tile's XCD groups).
 static int pipe_blocks(int ntiles, int tpb) {
@@ -3914,8 +3969,13 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         p.conv[i] = a;
         p.nblk[i] = snnflow_conv_blocks(B, H, W);
         if (c == 8 && g_pipe_fwd > 0 && (kind == SK_LIF || kind == SK_LIF_REC) && pipe_fits(B, H, W, c)) {
+            // a recurrent tile costs ~1.5x a feed-forward one (two convs, the s_prev halo): its task
+            // gets g_pipe_recw percent of the blocks, so that with dynamic tiles both finish together
+            const int nt = p.nblk[i];
+            p.nblk[i] = kind == SK_LIF_REC && a.tile_counter ? pipe_blocks((int)((int64_t)nt * g_pipe_recw / 100), g_pipe_fwd)
+                                                             : pipe_blocks(nt, g_pipe_fwd);
+            if (p.nblk[i] > (nt + 7) / 8 * 8) p.nblk[i] = (nt + 7) / 8 * 8;
             kind = kind == SK_LIF ? SK_LIF_P : SK_LIF_REC_P;
-            p.nblk[i] = pipe_blocks(p.nblk[i], g_pipe_fwd);
         }
         p.kind[i] = kind;
     }

@@ -79,6 +79,37 @@ class GradAllReduce:
             off += g.numel()
 
 
+def bn_buffers(model):
+    """The BatchNorm running statistics of `model` (running_mean, running_var, num_batches_tracked
+    of every BatchNorm module, in module order)."""
+    out = []
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and m.track_running_stats:
+            out += [m.running_mean, m.running_var, m.num_batches_tracked]
+    return [b for b in out if b is not None]
+
+
+def broadcast_bn_stats(model, src=0, group=None):
+    """Opt-in: overwrite every rank's BatchNorm running statistics with rank
+    `src`'s, so that an evaluation after data-parallel training sees one set (the batch statistics
+    of the train step itself stay rank-local either way).  One flat broadcast of the float buffers
+    (running means and variances) and one of the int64 counters; a no-op without a process group
+    or with one rank."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    bufs = bn_buffers(model)
+    for dtype in (torch.float32, torch.int64):
+        part = [b for b in bufs if b.dtype == dtype]
+        if not part:
+            continue
+        flat = torch.cat([b.reshape(-1) for b in part])
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        for b in part:
+            b.copy_(flat[off:off + b.numel()].view_as(b))
+            off += b.numel()
+
+
 _CLIP_SCRATCH = {}
 
 

@@ -923,6 +923,15 @@ def capped_slots(T, K, rec, cap):
     return launches
 
 
+def _pipe_dynamic():
+    """Dynamic tile hand-out for the C = 8 tile pipelines (snnflow_conv_fwd_args.tile_counter), opt-in
+    with SNNFLOW_PIPE_DYN=1.  Measured slower (cfg2 fwd slot 19.4 -> 25.3 us, step 1.45 -> 1.60 ms,
+    profiles/r04/ab_pipe_dynamic.txt): the ~512 returning atomics per task on one counter word
+    serialise (~90 per us per word) and stall the requesting wave."""
+    import os
+    return os.environ.get("SNNFLOW_PIPE_DYN", "0") == "1"
+
+
 def slot_cap():
     """Tasks per slot launch (SNNFLOW_SLOT_CAP; 0, the default: the plain wavefront order).  Measured
     (profiles/r03/ab_slot_cap.txt): cap 3 is slower at cfg2 (1.545-1.552 vs 1.491-1.504 ms: a
@@ -1007,12 +1016,19 @@ class FireNetSequence(torch.autograd.Function):
         train = [bn.training or not bn.track_running_stats for bn in eng.bns]
 
         frec = tuple(bool(eng.rec[k]) if k < L else False for k in range(L + 1))
-        for tasks in capped_slots(T, L + 1, frec, slot_cap()):
+        launches = capped_slots(T, L + 1, frec, slot_cap())
+        # dynamic tile hand-out of the C = 8 tile pipelines: one zeroed counter per task and launch
+        ctr = (torch.zeros(len(launches) * _lib.MAX_SLOT_TASKS, dtype=torch.int32, device=dev)
+               if C == 8 and _pipe_dynamic() else None)
+        for li, tasks in enumerate(launches):
             convs, top = [], None
             for k, t in tasks:
                 if k < L:
-                    convs.append(_fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
-                                                s_prev[t], facc[t], neurons, train, wfwd, wbwd))
+                    a = _fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
+                                       s_prev[t], facc[t], neurons, train, wfwd, wbwd)
+                    if ctr is not None and k >= 1:
+                        a.tile_counter = ctr.data_ptr() + 4 * (li * _lib.MAX_SLOT_TASKS + len(convs))
+                    convs.append(a)
                 else:
                     top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons,
                                         flows[t])

@@ -155,3 +155,38 @@ def test_bench_gpus_flag_spawns_ranks(monkeypatch):
     assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
     assert cmd[-4:] == ["--gpus", "2", "--steps", "3"]
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def _bn_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Conv2d(2, 4, 3), torch.nn.BatchNorm2d(4), torch.nn.BatchNorm2d(4))
+        model.train()
+        torch.manual_seed(10 + rank)  # rank-local batches: rank-local running statistics
+        for _ in range(3 + rank):
+            model(torch.randn(2, 2, 8, 8))
+        before = [b.clone() for b in dp.bn_buffers(model)]
+        dp.broadcast_bn_stats(model, src=0)
+        after = [b.clone() for b in dp.bn_buffers(model)]
+        q.put((rank, [b.tolist() for b in before], [b.tolist() for b in after]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_bn_stats_gloo_world2():
+    """dp.broadcast_bn_stats: after the broadcast every rank holds rank 0's running mean / var and
+    num_batches_tracked (which differed before: rank-local batches and step counts)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bn_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (b, a)) for r, b, a in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][0] != res[1][0]  # rank-local before
+    assert res[1][1] == res[0][0] and res[0][1] == res[0][0]  # rank 0's everywhere after

@@ -4,7 +4,7 @@
 set -u -o pipefail
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${TESTS:-} > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread ${KSEL:+-k "$KSEL"} > gpurun_out/gpu_tests.log 2>&1
   rc=$?
   tail -25 gpurun_out/gpu_tests.log
   [ $rc -ne 0 ] && { echo "pytest rc=$rc -> stop"; exit $rc; }
