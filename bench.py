@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--bn-broadcast", action="store_true",
                    help="N>1: after the timed steps, broadcast rank 0's BatchNorm running statistics to every rank "
                         "(snnflow.dp.broadcast_bn_stats; not part of the timed step)")
+    p.add_argument("--eval", action="store_true",
+                   help="LIFFireNet evaluation pass instead of the train step (eval_flow.py:208-338): model.eval(), "
+                        "no autograd, T windows forward + rounded per-polarity IWE + AEE per window")
     p.add_argument("--dp-check", action="store_true",
                    help="N>1 correctness check of this very step path (gloo rehearsal): the all-reduced "
                         "gradient == the sum of the ranks' own gradients, parameters identical after the update")
@@ -169,6 +172,10 @@ def main():
         backend = resolve_backend(args.dist_backend, torch.cuda.device_count(), share)
         dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
+    if args.eval:
+        if args.model != "LIFFireNet":
+            raise SystemExit("bench.py --eval: LIFFireNet only")
+        return eval_main(args, world, rank, dev, backend)
 
     import snnflow
     from snnflow import _lib
@@ -196,10 +203,6 @@ def main():
     def load_batch(i):  # eager steps: one device copy of the next resident batch into the input buffer
         static_flat.copy_(pool[i % len(pool)][0], non_blocking=True)
         cur["views"] = static_views
-
-    # persistent state buffers: detach_states() == copy into them (the reference clones)
-    state_bufs = None
-    state_flat = None
 
     unet = args.model == "SpikingRecEVFlowNet"
 
@@ -230,30 +233,15 @@ def main():
 
     sync_grads = dp.GradAllReduce(params)  # one SUM all-reduce over the engine's flat gradient buffer
 
+    handover = StateHandover(dev, get_states, set_states)
+
     def update():
         dp.clip_grad_norm_(params, 1.0)
         opt.step()
         if args.no_graph:  # the reference loop's hand-over (train_flow.py:262-279)
             model.detach_states()
             return
-        nonlocal state_bufs, state_flat
-        states = get_states()
-        if state_bufs is None:
-            src = _flat_span(states)
-            if src is not None:  # persistent buffers with the same back-to-back layout
-                state_flat = src.clone()
-                base = src.data_ptr()
-                state_bufs = [torch.empty(0, device=dev).set_(state_flat.untyped_storage(),
-                                                              (s.data_ptr() - base) // 4, s.shape, s.stride())
-                              for s in states]
-            else:
-                state_bufs = [s.detach().clone() for s in states]
-        src = _flat_span(states)
-        if src is not None and state_flat is not None:
-            state_flat.copy_(src)  # the engine's states are back to back: one contiguous copy
-        else:
-            torch._foreach_copy_(state_bufs, [s.detach() for s in states])
-        set_states(list(state_bufs))
+        handover()
 
     def step_eager():
         opt.zero_grad(set_to_none=True)
@@ -421,6 +409,178 @@ def _dp_check(world, rank, step_parts, params):
               flush=True)
 
 
+def perturb_running_stats(model, seed=3):
+    """Seeded BatchNorm running statistics away from (0, 1), as a trained model carries them: the
+    eval-mode BatchNorm is then not the identity (the same perturbation as
+    tests/test_gpu_fullsize.py::test_cfg2_eval_vs_oracle)."""
+    g = torch.Generator().manual_seed(seed)
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.running_mean.copy_(0.2 * torch.randn(m.running_mean.shape, generator=g))
+            m.running_var.copy_(0.5 + torch.rand(m.running_var.shape, generator=g))
+
+
+def eval_main(args, world, rank, dev, backend):
+    """`--eval`: the reference's evaluation loop (eval_flow.py:208-338) on synthetic windows.  One
+    step = T windows of B sequences: model.eval() forward (BatchNorm on running statistics, no
+    autograd; forward_sequence's wavefront launches), then per window the rounded per-polarity IWE
+    (compute_pol_iwe, eval_flow.py:227-235) and AEE against a synthetic ground-truth flow
+    (loss/flow.py:597-649), the per-sample AEE / outlier percentage accumulated on the device (the
+    reference moves them to the host per window for its result table).  Visualisation is not part
+    of the step.  HIP graphs as the train bench: one per resident batch, the state hand-over inside.
+    A second, smaller measurement covers configs[0] of BASELINE.json (T=5, B=1, forward only) on
+    the GPU and with the CPU oracle."""
+    import snnflow
+    from snnflow import _lib, dp
+    from snnflow.iwe import compute_pol_iwe
+    from snnflow.parser import train_snn_model_kwargs
+    from snnflow.synthetic import make_window
+
+    R, B, T, N = args.res, args.batch, args.T, args.events
+    kw = train_snn_model_kwargs(args.model, base_num_channels=args.channels)
+
+    def new_model():
+        torch.manual_seed(0)
+        m = snnflow.LIFFireNet(kw)
+        perturb_running_stats(m)
+        return m.to(dev).eval()
+
+    model = new_model()
+    gen = torch.Generator(device=dev).manual_seed(dp.stream_seed(1, rank))
+    pool = [_pack([make_window(B, N, R, R, gen, dev) for _ in range(T)]) for _ in range(args.pool)]
+    gts = [[(torch.rand(B, 2, R, R, generator=gen, device=dev) - 0.5) * 8.0 for _ in range(T)]
+           for _ in range(args.pool)]
+    one = torch.ones(1, device=dev)
+    metric = snnflow.AEE({"loader": {"resolution": [R, R]}, "loss": {"overwrite_intermediate": False}}, dev,
+                         flow_scaling=128)
+    acc = torch.zeros(2, B, dtype=torch.float64, device=dev)  # sum over windows of AEE, outlier %
+
+    def set_states(st):
+        model._states = st
+
+    handover = StateHandover(dev, lambda: model._states, set_states)
+
+    def eval_pass(j):
+        views, gt = pool[j % len(pool)][1], gts[j % len(pool)]
+        outs = model.forward_sequence([w["event_voxel"] for w in views], [w["event_cnt"] for w in views])
+        for t, w in enumerate(views):
+            pol = w["event_list_pol_mask"]
+            compute_pol_iwe(outs[t]["flow"][-1], w["event_list"], (R, R), pol[:, :, 0:1], pol[:, :, 1:2],
+                            flow_scaling=128, round_idx=True)
+            metric.event_flow_association(outs[t]["flow"], {"event_list": w["event_list"], "event_list_pol_mask": pol,
+                                                            "event_mask": w["event_mask"], "gtflow": gt[t],
+                                                            "dt_input": one, "dt_gt": one})
+            aee, pct = metric()
+            metric.reset()
+            acc[0].add_(aee)
+            acc[1].add_(pct)
+        handover()
+
+    graphs, elapsed = _timed_passes(args, dev, world, eval_pass, reset=acc.zero_)
+    aee_mean = (acc[0] / (args.steps * T)).tolist()
+    events_per_step = world * B * T * N
+    value = events_per_step * args.steps / elapsed
+
+    timer = _lib.KernelTimer()
+    _lib.TIMER = timer
+    torch.cuda._sleep(100_000_000)
+    with torch.no_grad():
+        eval_pass(0)
+    _lib.TIMER = None
+    roofline, kernels = _firenet_roofline(timer.summary(), model, args, B, R, T)
+
+    # configs[0]: T = 5 windows of one sequence, forward only, GPU and CPU oracle
+    cfg1 = None
+    if rank == 0 and world == 1:
+        m1 = new_model()
+        g1 = torch.Generator(device=dev).manual_seed(11)
+        wins1 = [make_window(1, N, R, R, g1, dev) for _ in range(5)]
+        h1 = StateHandover(dev, lambda: m1._states, lambda st: setattr(m1, "_states", st))
+
+        def fwd1(j):
+            m1.forward_sequence([w["event_voxel"] for w in wins1], [w["event_cnt"] for w in wins1])
+            h1()
+
+        a1 = argparse.Namespace(**vars(args))
+        a1.steps, a1.pool = max(args.steps, 50), 1
+        _, el1 = _timed_passes(a1, dev, 1, fwd1)
+        cfg1 = {"workload": f"configs[0]: LIFFireNet {R}x{R}, T=5, batch 1, forward only (eval mode)",
+                "gpu": {"value": round(5 * N * a1.steps / el1, 1), "unit": "events/s",
+                        "ms_per_pass": round(1000.0 * el1 / a1.steps, 4)}}
+        if not args.no_cpu_baseline:
+            cfg1["cpu"] = cpu_baseline_forward(args, wins1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_eval(args, pool[0][1], gts[0])
+
+    if rank == 0:
+        line = {
+            "metric": f"events/sec (eval: forward + IWE + AEE) LIFFireNet T={T} {R}x{R}",
+            "value": round(value, 1), "unit": "events/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000.0 * elapsed / args.steps, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+            "config": {"workload": f"LIFFireNet eval pass: T={T} x {N}-event windows, {R}x{R}, batch {B}/GPU, "
+                                   f"base_num_channels {args.channels}, model.eval() (running statistics), "
+                                   "rounded per-polarity IWE + AEE per window",
+                       "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "none",
+                       "collective": backend, "hip_graph": not args.no_graph, "launch_order": "wavefront"},
+            "aee_mean_per_sample": [round(v, 6) for v in aee_mean],
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu, "configs0": cfg1,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _timed_passes(args, dev, world, run, reset=None):
+    """Warm-up (eager, side stream), one HIP graph per resident batch (unless --no-graph), then
+    args.steps timed passes bracketed by barrier + synchronize; returns (graphs, max-over-ranks
+    seconds).  `run(j)` enqueues pass j; it runs under torch.no_grad()."""
+    s_side = torch.cuda.Stream(dev)
+    s_side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.no_grad(), torch.cuda.stream(s_side):
+        for i in range(max(args.warmup, 3)):
+            run(i)
+    torch.cuda.current_stream(dev).wait_stream(s_side)
+    torch.cuda.synchronize(dev)
+    graphs = []
+    if not args.no_graph:
+        for j in range(args.pool):
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(g):
+                run(j)
+            graphs.append(g)
+
+    def step(i):
+        if graphs:
+            graphs[i % len(graphs)].replay()
+        else:
+            with torch.no_grad():
+                run(i)
+
+    for i in range(2):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    if reset is not None:  # accumulators count the timed passes only
+        reset()
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    return graphs, elapsed
+
+
 def _firenet_roofline(kern, model, args, B, R, T):
     """HBM roofline of the dominant LIFFireNet kernel class (algorithmic bytes / HIP-event time)."""
     rec_layers = {i for i, (_, r) in enumerate(model.layer_spec) if r}
@@ -490,6 +650,36 @@ def _flat_span(tensors):
     flat = torch.empty(0, device=tensors[0].device)
     flat.set_(st, base, (off - base,), (1,))
     return flat
+
+
+class StateHandover:
+    """The reference loop's state hand-over (detach_states, train_flow.py:262-279) for HIP-graph
+    replays: persistent state buffers, and detach == one copy of the step's final states into them
+    (one contiguous copy when the engine's states lie back to back), so that every replay of a
+    captured step reads the states the previous replay left."""
+
+    def __init__(self, dev, get_states, set_states):
+        self.dev, self.get, self.set = dev, get_states, set_states
+        self.bufs = None
+        self.flat = None
+
+    def __call__(self):
+        states = self.get()
+        src = _flat_span(states)
+        if self.bufs is None:
+            if src is not None:  # persistent buffers with the same back-to-back layout
+                self.flat = src.clone()
+                base = src.data_ptr()
+                self.bufs = [torch.empty(0, device=self.dev).set_(self.flat.untyped_storage(),
+                                                                  (s.data_ptr() - base) // 4, s.shape, s.stride())
+                             for s in states]
+            else:
+                self.bufs = [s.detach().clone() for s in states]
+        if src is not None and self.flat is not None:
+            self.flat.copy_(src)
+        else:
+            torch._foreach_copy_(self.bufs, [s.detach() for s in states])
+        self.set(list(self.bufs))
 
 
 def _pack(windows):
@@ -598,6 +788,77 @@ def cpu_baseline(args, windows):
             "sample": f"{n} timed train steps (after 1 warm-up) of the same workload: {args.batch}x{args.T} windows "
                       f"of {args.events} events, {R}x{R}, C={args.channels}, Adam; oracle/ pure-PyTorch CPU "
                       f"restatement of the reference path, {threads} threads", "seconds": round(dt, 3)}
+
+
+def _oracle_eval_model(args):
+    from oracle import lif_ref
+
+    torch.manual_seed(0)
+    model = lif_ref.LIFFireNetRef(lif_ref.make_unet_kwargs(base_num_channels=args.channels), args.model)
+    perturb_running_stats(model)
+    return model.eval()
+
+
+def _bounded(run, seconds):
+    """run() once as warm-up, then until `seconds` of CPU work have passed (>= 1 run)."""
+    run()
+    n, t0 = 0, time.perf_counter()
+    while n == 0 or time.perf_counter() - t0 < seconds:
+        run()
+        n += 1
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline_eval(args, windows, gts):
+    """The CPU oracle's evaluation pass of the --eval workload: eval-mode forward of every window,
+    rounded per-polarity IWE (oracle/iwe_ref.py compute_pol_iwe_t) and AEE (oracle/metrics_ref.py),
+    whole T-window passes until ~10 s of CPU work."""
+    from oracle import iwe_ref
+    from oracle.metrics_ref import flow_metrics_ref
+
+    threads = _cpu_threads()
+    torch.set_num_threads(threads)
+    model = _oracle_eval_model(args)
+    R = args.res
+    cpu_w = [{k: v.cpu() for k, v in w.items()} for w in windows]
+    cpu_gt = [g.cpu() for g in gts]
+    one = torch.ones(1)
+
+    def one_pass():
+        with torch.no_grad():
+            for w, gt in zip(cpu_w, cpu_gt):
+                flow = model(None, w["event_cnt"])["flow"][-1]
+                pol = w["event_list_pol_mask"]
+                iwe_ref.compute_pol_iwe_t(flow, w["event_list"], [R, R], pol[:, :, 0:1], pol[:, :, 1:2], 128, True)
+                flow_metrics_ref(flow, gt, w["event_mask"], one, one, 128)
+
+    n, dt = _bounded(one_pass, 10.0)
+    ev = n * args.batch * args.T * args.events
+    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "cpu_model": _cpu_model(),
+            "threads_note": _THREADS_NOTE, "kind": "port",
+            "sample": f"{n} timed eval passes (after 1 warm-up) of the same workload: {args.batch}x{args.T} windows "
+                      f"of {args.events} events, {R}x{R}, C={args.channels}; oracle/ CPU restatement (eval-mode "
+                      f"forward, rounded IWE, AEE), {threads} threads", "seconds": round(dt, 3)}
+
+
+def cpu_baseline_forward(args, windows):
+    """configs[0] of BASELINE.json on the CPU oracle: T = len(windows) eval-mode forwards of one
+    sequence (batch 1), repeated until ~5 s of CPU work."""
+    threads = _cpu_threads()
+    torch.set_num_threads(threads)
+    model = _oracle_eval_model(args)
+    cpu_w = [w["event_cnt"].cpu() for w in windows]
+
+    def one_pass():
+        with torch.no_grad():
+            for x in cpu_w:
+                model(None, x)
+
+    n, dt = _bounded(one_pass, 5.0)
+    ev = n * len(cpu_w) * args.events
+    return {"value": round(ev / dt, 1), "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"{n} timed passes of {len(cpu_w)} windows x 1 sequence, forward only (oracle/lif_ref.py)",
+            "seconds": round(dt, 3)}
 
 
 def cpu_baseline_unet(args, windows):

@@ -8,7 +8,8 @@ Two restatements:
     (``utils/iwe.py:20-71``).
   * ``get_interpolation_t`` / ``interpolate_t`` / ``EventWarpingRef``: torch fp32
     restatements with autograd, the oracle for IWE images, the loss value and
-    dL/dflow (``utils/iwe.py:4-93``, ``loss/flow.py:28-303``).
+    dL/dflow (``utils/iwe.py:4-93``, ``loss/flow.py:28-303``); ``deblur_events_t`` /
+    ``compute_pol_iwe_t`` the evaluation images (``utils/iwe.py:96-154``).
 """
 import numpy as np
 import torch
@@ -106,6 +107,25 @@ def interpolate_t(idx, weights, res, polarity_mask=None):
     img = torch.zeros((idx.shape[0], res[0] * res[1], 1), dtype=weights.dtype)
     img = img.scatter_add_(1, idx.long(), weights)
     return img.view(idx.shape[0], 1, res[0], res[1])
+
+
+def deblur_events_t(flow, event_list, res, flow_scaling=128, round_idx=True, polarity_mask=None):
+    """``utils/iwe.py:96-130``: the flow vector at each event's pixel (gather; channel 1 = y,
+    channel 0 = x), events warped to tref = 1, splatted into [B,1,H,W]."""
+    B = flow.shape[0]
+    pix = (event_list[:, :, 1] * res[1] + event_list[:, :, 2]).long()
+    fl = flow.reshape(B, 2, -1)
+    ev_flow = torch.stack([torch.gather(fl[:, 1], 1, pix), torch.gather(fl[:, 0], 1, pix)], dim=2)
+    idx, w = get_interpolation_t(event_list, ev_flow, 1, res, flow_scaling, round_idx=round_idx)
+    if not round_idx and polarity_mask is not None:
+        polarity_mask = torch.cat([polarity_mask] * 4, dim=1)
+    return interpolate_t(idx, w, res, polarity_mask)
+
+
+def compute_pol_iwe_t(flow, event_list, res, pos_mask, neg_mask, flow_scaling=128, round_idx=True):
+    """``utils/iwe.py:133-154``: [B,2,H,W] per-polarity images of warped events."""
+    return torch.cat([deblur_events_t(flow, event_list, res, flow_scaling, round_idx, m) for m in (pos_mask, neg_mask)],
+                     dim=1)
 
 
 def _charbonnier(d):

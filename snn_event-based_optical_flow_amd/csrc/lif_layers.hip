@@ -1251,16 +1251,68 @@ __device__ void fused_wgrad_stage(const snnflow_layer_bwd_args& a, const float* 
     }
 }
 
+// The recurrent cell's two weight gradients in one matrix-core pass: the tile holds x and s_prev side
+// by side ([256 pixels][x 0..7 | s 8..15] bf16 in wl_x), so the B operand's columns 0..7 are x and
+// 8..15 are s_prev -- D[co][n] is dW_ff for n < 8 and dW_rec for n >= 8 (the one-conv form leaves
+// columns 8..15 unused).  Results: dW_ff's R / tap-8 partials at wl_r, dW_rec's at wl_r + kWgfR + kWgfP.
+__device__ void fused_wgrad_stage_pk(const float* G, float* wl_x, float* wl_r, const float (&xsp)[4], const float4& sp,
+                                     int pt, int ci0) {
+    constexpr int C = 8, PART = HN * C, XS = 16;
+    static_assert(FragFloats<true, 8, 2 * NT>::v >= NT * XS / 2 && FragFloats<true, 8, 2 * NT>::v >= 2 * (kWgfR + kWgfP),
+                  "packed x|s tile in wl_x, both result sets in wl_r");
+    const int tid = threadIdx.x;
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    __bf16* X = reinterpret_cast<__bf16*>(wl_x);
+    __syncthreads();  // every wave is done with the staged input-gradient results: the regions are free
+    *reinterpret_cast<bf16x4*>(X + pt * XS + ci0) = bf16x4{(__bf16)xsp[0], (__bf16)xsp[1], (__bf16)xsp[2], (__bf16)xsp[3]};
+    *reinterpret_cast<bf16x4*>(X + pt * XS + C + ci0) = bf16x4{(__bf16)sp.x, (__bf16)sp.y, (__bf16)sp.z, (__bf16)sp.w};
+    __syncthreads();
+
+    const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+    const __bf16* G3 = reinterpret_cast<const __bf16*>(G);
+    const int j0 = 8 * g4 + qq;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc8 = acc;
+    auto kstep = [&](int tap, int row, f32x4& d) {
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        const int hp = (row + 2 - ky) * HWD + (j0 + 2 - kx);
+        const __bf16* ga = G3 + hp * C + 4 * pp;
+        const bf16x8 ah = tr8(ga, ga + 4 * C);
+        const bf16x8 am = tr8(ga + PART, ga + PART + 4 * C);
+        const bf16x8 al = tr8(ga + 2 * PART, ga + 2 * PART + 4 * C);
+        const __bf16* xb = X + (row * TW + j0) * XS + 4 * pp;
+        const bf16x8 b = tr8(xb, xb + 4 * XS);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, d, 0, 0, 0);
+    };
+#pragma unroll 2
+    for (int row = 0; row < TH; ++row) kstep(wv, row, acc);
+    kstep(8, wv, acc8);
+    const int n = lane & 15;
+    if (g4 < 2) {  // co = 4 g4 + j < 8
+        float* R = wl_r + (n < C ? 0 : kWgfR + kWgfP);
+        float* P8 = R + kWgfR;
+        const int ci = n & 7;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = 4 * g4 + j;
+            R[(co * C + ci) * 9 + wv] = acc[j];
+            P8[wv * 64 + co * C + ci] = acc8[j];
+        }
+    }
+}
+
 // The block's slab rows: element e of [c][cin][9] = R[e] (taps 0..7) or the tap-8 partials of the
 // 8 waves summed in wave order; written or added to the old value (fixed order over the steps).
+// rx / rr: the R arrays of the two convs (the tap-8 partials follow each).
 template <bool REC>
-__device__ void fused_wgrad_store(const snnflow_layer_bwd_args& a, const Grid& g, const float* wl_x,
-                                  const float* wl_r, const float (&wold)[4]) {
+__device__ void fused_wgrad_store(const snnflow_layer_bwd_args& a, const Grid& g, const float* rx,
+                                  const float* rr, const float (&wold)[4]) {
     const int tid = threadIdx.x;
     const bool acc_in = a.wslab_accumulate != 0;
     const bool has_s = REC && a.s_prev != nullptr && a.wslab_rec != nullptr;
-    auto value = [&](const float* base, int e) {
-        const float* R = base + kWgfX;
+    auto value = [&](const float* R, int e) {
         const int tap = e % 9;
         if (tap < 8) return R[e];
         const float* P8 = R + kWgfR;
@@ -1274,10 +1326,10 @@ __device__ void fused_wgrad_store(const snnflow_layer_bwd_args& a, const Grid& g
     for (int i = 0; i < 2; ++i) {
         const int e = tid + i * 2 * NT;
         if (e < kWgfR) {
-            a.wslab_ff[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[i] + value(wl_x, e) : value(wl_x, e);
+            a.wslab_ff[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[i] + value(rx, e) : value(rx, e);
             if constexpr (REC) {
                 if (a.wslab_rec) {
-                    if (has_s) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[2 + i] + value(wl_r, e) : value(wl_r, e);
+                    if (has_s) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[2 + i] + value(rr, e) : value(rr, e);
                     else if (!acc_in) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = 0.0f;
                 }
             }
@@ -1353,10 +1405,20 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (a.g_state_prev) sw_r.load(a.wt_fwd_rec);
         }
     }
+    // C = 8 recurrent cells: both input gradients in one pass (the recurrent conv's fragments in the
+    // unused columns 8..15 of the ff conv's B operand): half the input-gradient MFMAs
+    constexpr bool PKC = FLDS && REC && CIN == 8 && C == 8;
+    [[maybe_unused]] const bool pkr = PKC && a.wt_bwd_ff != nullptr && a.g_state_prev != nullptr;
     if constexpr (FLDS) {
-        if (a.wt_bwd_ff) fs_x.load(a.wt_fwd_ff);
-        if constexpr (REC) {
-            if (a.g_state_prev) fs_r.load(a.wt_fwd_rec);
+        if constexpr (PKC) {
+            if (pkr) fs_x.load2(a.wt_fwd_ff, a.wt_fwd_rec);
+            else if (a.wt_bwd_ff) fs_x.load(a.wt_fwd_ff);
+            if (!pkr && a.g_state_prev) fs_r.load(a.wt_fwd_rec);
+        } else {
+            if (a.wt_bwd_ff) fs_x.load(a.wt_fwd_ff);
+            if constexpr (REC) {
+                if (a.g_state_prev) fs_r.load(a.wt_fwd_rec);
+            }
         }
     }
     float4 rg[PF ? Halo4<C, NTB>::R : 1], ry[PF ? Halo4<C, NTB>::R : 1];
@@ -1470,7 +1532,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     if constexpr (FLDS) {
         if (a.wt_bwd_ff) fs_x.store(reinterpret_cast<__bf16*>(wl_x));
         if constexpr (REC) {
-            if (a.g_state_prev) fs_r.store(reinterpret_cast<__bf16*>(wl_r));
+            if (a.g_state_prev && !pkr) fs_r.store(reinterpret_cast<__bf16*>(wl_r));
         }
     }
     __syncthreads();
@@ -1501,7 +1563,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             }
         }
         if constexpr (REC) {
-            if (do_r) {
+            if (do_r && !pkr) {
                 arr.zero();
                 if constexpr (FLDS) {
                     if (!PROBE_OFF(1)) mfma_dgrad_bf6<C, C, NW>(g3, reinterpret_cast<const __bf16*>(wl_r), arr);
@@ -1517,7 +1579,29 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         // results staged through LDS: the gradient tile G, or (fused weight gradients, which still
         // read G) the weight-fragment regions wl_x.. (free now; the slot pool holds both of them)
         float* const dgo = (WGF && wgf) ? wl_x : G;
-        if (do_x) {
+        if constexpr (PKC) {
+            if (pkr) {  // columns n < 8: gx -> wl_x [NT][8]; n >= 8: the recurrent gradient -> wl_r [NT][8]
+                const int lane = tid & 63, n = lane & 15, g4 = lane >> 4;
+                const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+                float* out = (n < 8 ? wl_x : wl_r) + (n & 7);
+#pragma unroll
+                for (int mt = 0; mt < MfmaAcc<C, CIN, NW, NG>::MT; ++mt) {
+                    const int T = MfmaAcc<C, CIN, NW, NG>::mt0(wv) + mt, row = T >> 1, c0 = (T & 1) * 16;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) out[(row * TW + c0 + g4 * 4 + r) * 8] = ax.v[mt][0][r];
+                }
+                __syncthreads();
+                const float4 gv4 = *reinterpret_cast<const float4*>(wl_x + pt * 8 + ci0);
+                gx[0] = gv4.x; gx[1] = gv4.y; gx[2] = gv4.z; gx[3] = gv4.w;
+                if (in) {
+                    const int64_t plane = (int64_t)a.B * H * W * C;
+                    float* gsp = a.g_state_prev + pix * C + cr0;
+                    if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp) = z4;
+                    *reinterpret_cast<float4*>(gsp + plane) = *reinterpret_cast<const float4*>(wl_r + pt * 8 + cr0);
+                }
+            }
+        }
+        if (do_x && !pkr) {
             mfma_store<false>(ax, ax, dgo);
             __syncthreads();
             const float* gl = dgo + pt * Pad<CIN>::v + ci0;
@@ -1525,7 +1609,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             for (int ci = 0; ci < CI; ++ci) gx[ci] = gl[ci];
         }
         if constexpr (REC) {
-            if (do_r) {
+            if (do_r && !pkr) {
                 __syncthreads();
                 mfma_store<false>(arr, arr, dgo);
                 __syncthreads();
@@ -1610,9 +1694,15 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
         TRACE_AT(TR, TK, 5);
         if constexpr (WGF) {
             if (wgf) {
-                fused_wgrad_stage<REC>(a, G, wl_x, wl_r, xsp, wsp, pt, ci0);
-                __syncthreads();
-                fused_wgrad_store<REC>(a, g, wl_x, wl_r, wold);
+                if (REC && a.s_prev != nullptr && a.wslab_rec != nullptr) {  // dW_ff and dW_rec in one pass
+                    fused_wgrad_stage_pk(G, wl_x, wl_r, xsp, wsp, pt, ci0);
+                    __syncthreads();
+                    fused_wgrad_store<REC>(a, g, wl_r, wl_r + kWgfR + kWgfP, wold);
+                } else {
+                    fused_wgrad_stage<REC>(a, G, wl_x, wl_r, xsp, wsp, pt, ci0);
+                    __syncthreads();
+                    fused_wgrad_store<REC>(a, g, wl_x + kWgfX, wl_r + kWgfX, wold);
+                }
             }
         }
         TRACE_AT(TR, TK, 6);

@@ -385,6 +385,21 @@ struct FragStage {
             r[i] = (e < E && tap < 9 && n < NOUT) ? wB[(tap * NOUT + n) * KIN + c0 + j] : 0.0f;
         }
     }
+    // Two convs sharing the A operand in one B operand (NOUT <= 8, one n-tile): columns n < 8 from wB0,
+    // columns 8 <= n < 8 + NOUT from wB1 (the recurrent input gradient packed beside the ff one)
+    __device__ inline void load2(const float* __restrict__ wB0, const float* __restrict__ wB1) {
+        static_assert(NOUT <= 8 && G::NNT == 1, "packed fragments: two convs of <= 8 outputs");
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = (int)threadIdx.x + i * NTH;
+            const int j = e & 7, lane = (e >> 3) & 63, ch = e >> 9, n = lane & 15;
+            int tap, c0;
+            bf3_k<KIN>(ch, lane >> 4, tap, c0);
+            const float* w = n < 8 ? wB0 : wB1;
+            const int nn = n & 7;
+            r[i] = (e < E && tap < 9 && nn < NOUT) ? w[(tap * NOUT + nn) * KIN + c0 + j] : 0.0f;
+        }
+    }
     __device__ inline void store(__bf16* lds) const {
 #pragma unroll
         for (int i = 0; i < R; ++i) {

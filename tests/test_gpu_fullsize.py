@@ -312,3 +312,55 @@ def test_clip_grad_norm_large_vs_torch(dev):
     coef = np.float32(1.0) / (np.float32(total.item()) + np.float32(1e-6))
     for p, v in zip(ps, vals):
         np.testing.assert_allclose(p.grad.cpu().numpy(), v.numpy() * coef, rtol=1e-6, atol=1e-12)
+
+
+def test_cfg2_eval_vs_oracle(dev):
+    """The evaluation path at cfg2's shape (eval_flow.py:208-338: model.eval(), BatchNorm on its
+    running statistics, forward only, AEE per window): T = 10 windows of 1000 events at 128 x 128,
+    B = 8, through forward_sequence (the wavefront launches the bench's --eval line times) against
+    the oracle in eval mode, flip-corrected like the train step (a differing spike must lie within
+    1e-4 of the threshold).  Running statistics are perturbed away from (0, 1) so that the eval
+    BatchNorm is not the identity.  Flows within 1e-4, AEE of a synthetic ground truth per window
+    within 1e-4 (north star)."""
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    B, H, T, N, C = 8, 128, 10, 1000, 8
+    gen = torch.Generator(device=dev).manual_seed(7)
+    wins = [make_window(B, N, H, H, gen, dev) for _ in range(T)]
+    cpu_wins = [{k: v.cpu() for k, v in w.items()} for w in wins]
+    model = _new_model(C)
+    g = torch.Generator().manual_seed(3)
+    for m in model.modules():
+        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            m.running_mean.copy_(0.2 * torch.randn(m.running_mean.shape, generator=g))
+            m.running_var.copy_(0.5 + torch.rand(m.running_var.shape, generator=g))
+    init = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    model = model.to(dev).eval()
+    model.engine.capture_states = True
+    with torch.no_grad():
+        outs = model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+    flows = [o["flow"][0].detach() for o in outs]
+    states = [[s.detach().cpu() for s in sts] for sts in model.engine.seq_states]
+    model.engine.seq_states = None
+
+    ref = lif_ref.LIFFireNetRef(lif_ref.make_unet_kwargs(base_num_channels=C), "LIFFireNet").eval()
+    ref.load_state_dict(init)
+    rflows, flips, hard = [], 0, 0
+    with torch.no_grad():
+        for t, w in enumerate(cpu_wins):
+            f, fl, hd = _oracle_step(ref, w["event_cnt"], states[t], 1e-4)
+            rflows.append(f)
+            flips += sum(fl)
+            hard += hd
+    gtg = torch.Generator().manual_seed(2)
+    worst_flow, worst_aee = 0.0, 0.0
+    for t in range(T):
+        worst_flow = max(worst_flow, float((flows[t].cpu() - rflows[t]).abs().max()))
+        gt = (torch.rand(B, 2, H, H, generator=gtg) - 0.5) * 8.0
+        ours, theirs = _aee_pair(flows[t], rflows[t], gt, cpu_wins[t]["event_mask"], dev)
+        worst_aee = max(worst_aee, float(np.abs(ours - theirs).max()))
+    print(f"\n[cfg2 eval] spike flips {flips} (away from the threshold: {hard}); max|dflow| {worst_flow:.2e}; "
+          f"max|dAEE| over {T} windows {worst_aee:.2e}")
+    assert hard == 0
+    assert worst_flow <= 1e-4 and worst_aee <= 1e-4
