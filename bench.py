@@ -57,6 +57,9 @@ def parse():
     p.add_argument("--bn-broadcast", action="store_true",
                    help="N>1: after the timed steps, broadcast rank 0's BatchNorm running statistics to every rank "
                         "(snnflow.dp.broadcast_bn_stats; not part of the timed step)")
+    p.add_argument("--torch-adam", action="store_true",
+                   help="LIFFireNet: snnflow's clip + torch's fused Adam (two launches + torch's) instead of "
+                        "snnflow.ClipAdam (one launch)")
     p.add_argument("--eval", action="store_true",
                    help="LIFFireNet evaluation pass instead of the train step (eval_flow.py:208-338): model.eval(), "
                         "no autograd, T windows forward + rounded per-polarity IWE + AEE per window")
@@ -191,8 +194,13 @@ def main():
            "model": {"mask_output": True}}
     loss_fn = snnflow.EventWarping(cfg, dev)
     params = list(model.parameters())
-    # fused Adam: one multi-tensor launch per step (torch's own implementation)
-    opt = torch.optim.Adam(params, lr=2e-4, capturable=not args.no_graph, fused=True)
+    # LIFFireNet: clip_grad_norm_ + Adam in one launch (snnflow.ClipAdam over the engine's flat
+    # gradient buffer); the U-Net (and --torch-adam): torch's fused Adam after snnflow's clip
+    fused_opt = args.model != "SpikingRecEVFlowNet" and not args.torch_adam
+    if fused_opt:
+        opt = snnflow.ClipAdam(params, lr=2e-4, max_norm=1.0)
+    else:
+        opt = torch.optim.Adam(params, lr=2e-4, capturable=not args.no_graph, fused=True)
 
     # synthetic data, resident in HBM; per-rank stream seeded by (seed, rank)
     gen = torch.Generator(device=dev).manual_seed(dp.stream_seed(1, rank))
@@ -215,6 +223,8 @@ def main():
         else:
             model._states = st
 
+    seed = torch.ones((), device=dev)
+
     def fwd_bwd():
         static = cur["views"]
         loss_fn.reset()
@@ -228,20 +238,23 @@ def main():
             w = static[t]
             loss_fn.event_flow_association(outs[t]["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
         loss = loss_fn()
-        loss.backward()
+        loss.backward(seed)  # == loss.backward(): the unit seed is a persistent tensor, not a fill per step
         return loss
 
     sync_grads = dp.GradAllReduce(params)  # one SUM all-reduce over the engine's flat gradient buffer
 
     handover = StateHandover(dev, get_states, set_states)
+    pingpong = None  # graph replays of forward_sequence: copy-free hand-over (StatePingPong)
 
     def update():
-        dp.clip_grad_norm_(params, 1.0)
+        if not fused_opt:
+            dp.clip_grad_norm_(params, 1.0)
         opt.step()
         if args.no_graph:  # the reference loop's hand-over (train_flow.py:262-279)
             model.detach_states()
             return
-        handover()
+        if pingpong is None:
+            handover()
 
     def step_eager():
         opt.zero_grad(set_to_none=True)
@@ -268,9 +281,15 @@ def main():
     g_upd = None
     multi = world == 1
     if not args.no_graph:
-        for j in range(len(pool) if multi else 1):
+        n_graphs = len(pool) if multi else 1
+        if multi and not unet and not args.per_step:
+            pingpong = StatePingPong(dev, get_states())
+            n_graphs = pingpong.cycle(len(pool))
+        for j in range(n_graphs):
             opt.zero_grad(set_to_none=True)
-            cur["views"] = pool[j][1] if multi else static_views
+            cur["views"] = pool[j % len(pool)][1] if multi else static_views
+            if pingpong is not None:
+                pingpong.arm(model, j)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 fwd_bwd()
@@ -335,6 +354,8 @@ def main():
     timer = _lib.KernelTimer()
     _lib.TIMER = timer
     load_batch(0)
+    if pingpong is not None:  # the states the graphs hand over (detached views), not a capture's outputs
+        set_states(list(pingpong.views[0]))
     torch.cuda._sleep(100_000_000)
     step_eager()
     _lib.TIMER = None
@@ -455,6 +476,8 @@ def eval_main(args, world, rank, dev, backend):
                          flow_scaling=128)
     acc = torch.zeros(2, B, dtype=torch.float64, device=dev)  # sum over windows of AEE, outlier %
 
+    pingpong = []  # set after the warm-up: graph replays hand the states over copy-free
+
     def set_states(st):
         model._states = st
 
@@ -474,9 +497,15 @@ def eval_main(args, world, rank, dev, backend):
             metric.reset()
             acc[0].add_(aee)
             acc[1].add_(pct)
-        handover()
+        if not pingpong:
+            handover()
 
-    graphs, elapsed = _timed_passes(args, dev, world, eval_pass, reset=acc.zero_)
+    def arm(j):
+        if not pingpong:
+            pingpong.append(StatePingPong(dev, model._states))
+        pingpong[0].arm(model, j)
+
+    graphs, elapsed = _timed_passes(args, dev, world, eval_pass, reset=acc.zero_, arm=arm)
     aee_mean = (acc[0] / (args.steps * T)).tolist()
     events_per_step = world * B * T * N
     value = events_per_step * args.steps / elapsed
@@ -496,14 +525,21 @@ def eval_main(args, world, rank, dev, backend):
         g1 = torch.Generator(device=dev).manual_seed(11)
         wins1 = [make_window(1, N, R, R, g1, dev) for _ in range(5)]
         h1 = StateHandover(dev, lambda: m1._states, lambda st: setattr(m1, "_states", st))
+        pp1 = []
 
         def fwd1(j):
             m1.forward_sequence([w["event_voxel"] for w in wins1], [w["event_cnt"] for w in wins1])
-            h1()
+            if not pp1:
+                h1()
+
+        def arm1(j):
+            if not pp1:
+                pp1.append(StatePingPong(dev, m1._states))
+            pp1[0].arm(m1, j)
 
         a1 = argparse.Namespace(**vars(args))
         a1.steps, a1.pool = max(args.steps, 50), 1
-        _, el1 = _timed_passes(a1, dev, 1, fwd1)
+        _, el1 = _timed_passes(a1, dev, 1, fwd1, arm=arm1)
         cfg1 = {"workload": f"configs[0]: LIFFireNet {R}x{R}, T=5, batch 1, forward only (eval mode)",
                 "gpu": {"value": round(5 * N * a1.steps / el1, 1), "unit": "events/s",
                         "ms_per_pass": round(1000.0 * el1 / a1.steps, 4)}}
@@ -533,10 +569,11 @@ def eval_main(args, world, rank, dev, backend):
         dist.destroy_process_group()
 
 
-def _timed_passes(args, dev, world, run, reset=None):
-    """Warm-up (eager, side stream), one HIP graph per resident batch (unless --no-graph), then
-    args.steps timed passes bracketed by barrier + synchronize; returns (graphs, max-over-ranks
-    seconds).  `run(j)` enqueues pass j; it runs under torch.no_grad()."""
+def _timed_passes(args, dev, world, run, reset=None, arm=None):
+    """Warm-up (eager, side stream), one HIP graph per resident batch (unless --no-graph; with
+    `arm(j)`, called before capture j, StatePingPong.cycle(pool) graphs), then args.steps timed
+    passes bracketed by barrier + synchronize; returns (graphs, max-over-ranks seconds).  `run(j)`
+    enqueues pass j; it runs under torch.no_grad()."""
     s_side = torch.cuda.Stream(dev)
     s_side.wait_stream(torch.cuda.current_stream(dev))
     with torch.no_grad(), torch.cuda.stream(s_side):
@@ -546,7 +583,9 @@ def _timed_passes(args, dev, world, run, reset=None):
     torch.cuda.synchronize(dev)
     graphs = []
     if not args.no_graph:
-        for j in range(args.pool):
+        for j in range(args.pool if arm is None else StatePingPong.cycle(args.pool)):
+            if arm is not None:
+                arm(j)
             g = torch.cuda.CUDAGraph()
             with torch.no_grad(), torch.cuda.graph(g):
                 run(j)
@@ -680,6 +719,31 @@ class StateHandover:
         else:
             torch._foreach_copy_(self.bufs, [s.detach() for s in states])
         self.set(list(self.bufs))
+
+
+class StatePingPong:
+    """Copy-free state hand-over for HIP-graph replays of forward_sequence: two persistent state
+    buffers; the graph of replay j reads buffer j % 2 as its initial states while the engine writes
+    the final step's states straight into buffer (j + 1) % 2 (FireNetEngine.final_state_out), so the
+    reference's detach (a clone, train_flow.py:262-279) costs nothing.  Replays must alternate
+    parity: `cycle(n)` is the number of graphs to capture for n resident batches (2n when n is odd)."""
+
+    def __init__(self, dev, states):
+        src = _flat_span(states)
+        if src is None:
+            raise RuntimeError("StatePingPong: the engine's states are not one flat row")
+        base = src.data_ptr()
+        self.bufs = [src.clone(), src.clone()]
+        self.views = [[torch.empty(0, device=dev).set_(b.untyped_storage(), (s.data_ptr() - base) // 4, s.shape,
+                                                       s.stride()) for s in states] for b in self.bufs]
+
+    @staticmethod
+    def cycle(n):
+        return n if n % 2 == 0 else 2 * n
+
+    def arm(self, model, j):
+        model._states = list(self.views[j % 2])
+        model.engine.final_state_out = self.bufs[(j + 1) % 2]
 
 
 def _pack(windows):

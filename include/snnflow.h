@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 28
+#define SNNFLOW_ABI_VERSION 29
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -73,6 +73,10 @@ typedef struct snnflow_prep_desc {
      * input-gradient conv (snnflow_layer_bwd_args.wd_ff / wd_rec); snnflow_frag_halfs(c, cin)
      * bf16 values (uint16 bit patterns) each */
     uint16_t* frag_fwd; uint16_t* frag_bwd;
+    /* ABI 29, optional: zero_n doubles at `zero` are set to 0 (the batch-sum accumulators of the
+     * following forward / backward pass ride along with the weight preparation: one launch fewer
+     * than a separate fill).  A descriptor may carry only this (w = threshold = NULL). */
+    double* zero; int64_t zero_n;
 } snnflow_prep_desc;
 int snnflow_frag_halfs(int c, int cin);
 #define SNNFLOW_MAX_BATCH 16
@@ -432,10 +436,15 @@ typedef struct snnflow_aee_args {
     const float* event_mask;    /* [B][H][W] event mask of the last window */
     const float* dt_ratio;      /* [B] dt_gt / dt_input */
     float flow_scaling;
-    double* acc;                /* scratch [2B + 1], zeroed by the call */
+    double* acc;                /* ABI 29: scratch of snnflow_aee_acc_doubles(B, H, W) doubles; acc[0] (a
+                                 * completion counter) must be zero before the first call on it and every
+                                 * call leaves it zero -- allocate zeroed once and reuse */
     float* aee; float* percent; /* out [B] */
 } snnflow_aee_args;
+/* One launch: per-block partial sums (fp64 rows), the last block to finish reduces them in a fixed
+ * order (deterministic) and writes aee / percent. */
 int snnflow_aee(const snnflow_aee_args* a, void* stream);
+int snnflow_aee_acc_doubles(int B, int H, int W);
 
 /* Every flow-vs-ground-truth metric of loss/flow.py in one pass over the pixels
  * (flow' = flow*flow_scaling*dt_ratio[b], valid = event_mask && gt != (0,0)):
@@ -497,6 +506,38 @@ int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float
 #define SNNFLOW_CLIP_SCRATCH 513
 int snnflow_clip_grad_norm_large(float* g, int64_t n, float max_norm, float eps, float* total_out,
                                  double* scratch, void* stream);
+
+/* clip_grad_norm_ + Adam in one launch (train_flow.py:265-267: clip_grad_norm_(params, max_norm),
+ * optimizer.step() of torch.optim.Adam, configs/train_SNN.yml:45-47), over the engine's flat gradient
+ * buffer (snnflow.optim.ClipAdam).  total = ||grad||_2 (fp64), grad *= min(max_norm / (total +
+ * clip_eps), 1) in place (skipped when max_norm <= 0), *step += 1, then per element the reference's
+ * Adam (torch _single_tensor_adam: weight decay, exp_avg.lerp_(g, 1 - beta1), exp_avg_sq =
+ * exp_avg_sq * beta2 + (1 - beta2) g^2, bias corrections in fp64, denom = sqrt(exp_avg_sq) /
+ * sqrt(bc2) + eps, param -= lr / bc1 * exp_avg / denom).  t[i] maps parameter tensor i to
+ * grad[offset .. offset + numel) and to exp_avg / exp_avg_sq[state_offset .. state_offset + numel)
+ * (persistent moment buffers: the gradient buffer may move between steps, the moments do not).  One
+ * block: n <= SNNFLOW_CLIP_ADAM_MAX_N.  Replaces snnflow_clip_grad_norm + torch's Adam kernels. */
+#define SNNFLOW_ADAM_MAX_TENSORS 64
+#define SNNFLOW_CLIP_ADAM_MAX_N (1 << 20)
+typedef struct {
+    float* param;
+    int64_t offset;        /* into grad */
+    int64_t state_offset;  /* into exp_avg / exp_avg_sq */
+    int64_t numel;
+} snnflow_adam_tensor;
+typedef struct {
+    float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    float* step;       /* device scalar (fp32, as torch's capturable Adam state) */
+    float* total_out;  /* device scalar or NULL: the pre-clip norm */
+    int64_t n;
+    double lr, beta1, beta2, eps, weight_decay;
+    float max_norm, clip_eps;
+    int ntensors;
+    snnflow_adam_tensor t[SNNFLOW_ADAM_MAX_TENSORS];
+} snnflow_clip_adam_args;
+int snnflow_clip_adam(const snnflow_clip_adam_args* a, void* stream);
 
 /* Activity log of LIFFireNet.forward(log=True) (models/model.py:188-205: per tensor
  * `l.detach().ne(0).float().mean()`): counts[i] = number of non-zero elements (NaN counts, -0 does

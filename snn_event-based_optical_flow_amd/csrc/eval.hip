@@ -59,10 +59,15 @@ __global__ __launch_bounds__(NT) void k_pol_iwe(const float* __restrict__ events
     }
 }
 
-// per pixel: endpoint error and validity; per-sample sums (fp64 atomics): acc[2b] = sum err,
-// acc[2b+1] = sum valid, acc[2B] = outliers over the batch.  blocks: B * chunks.
+// AEE in one launch.  Per pixel: endpoint error, validity, outlier; per (sample, chunk of NT pixels)
+// block one fp64 row {sum err, sum valid, outliers} at acc[1 + 3 blk]; the last block to finish
+// (completion counter acc[0]) sums every sample's rows in chunk order, writes aee / percent (the
+// outliers counted over the whole batch, loss/flow.py:647) and resets the counter: deterministic,
+// and no zero / finalize launches.
 __global__ __launch_bounds__(NT) void k_aee(snnflow_aee_args a, int chunks) {
     __shared__ float red[NT / 64][3];
+    __shared__ double smp[NT][3];  // B <= NT (host check)
+    __shared__ int last;
     const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
     const int64_t HWp = (int64_t)a.H * a.W;
     const int64_t p = (int64_t)chunk * NT + tid;
@@ -91,16 +96,38 @@ __global__ __launch_bounds__(NT) void k_aee(snnflow_aee_args a, int chunks) {
     if (tid < 3) {
         double t = 0.0;
         for (int w = 0; w < NT / 64; ++w) t += (double)red[w][tid];
-        atomicAdd(tid < 2 ? a.acc + 2 * b + tid : a.acc + 2 * a.B, t);
+        a.acc[1 + 3 * (int64_t)blockIdx.x + tid] = t;
     }
-}
-
-__global__ void k_aee_finalize(snnflow_aee_args a) {
-    const int b = threadIdx.x;
-    if (b >= a.B) return;
-    const float nvalid = (float)a.acc[2 * b + 1];
-    a.aee[b] = (float)a.acc[2 * b] / (nvalid + 1e-9f);
-    a.percent[b] = (float)a.acc[2 * a.B] / (nvalid + 1e-9f);
+    __threadfence();  // the row is visible device-wide before the block counts as done
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long done = atomicAdd(reinterpret_cast<unsigned long long*>(a.acc), 1ull);
+        last = done == (unsigned long long)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (tid < a.B) {
+        double e = 0.0, v = 0.0, o = 0.0;
+        const double* r = a.acc + 1 + 3 * (int64_t)tid * chunks;
+        for (int c = 0; c < chunks; ++c) {
+            e += r[3 * c];
+            v += r[3 * c + 1];
+            o += r[3 * c + 2];
+        }
+        smp[tid][0] = e;
+        smp[tid][1] = v;
+        smp[tid][2] = o;
+    }
+    __syncthreads();
+    if (tid < a.B) {
+        double outl = 0.0;
+        for (int bb = 0; bb < a.B; ++bb) outl += smp[bb][2];
+        const float nvalid = (float)smp[tid][1];
+        a.aee[tid] = (float)smp[tid][0] / (nvalid + 1e-9f);
+        a.percent[tid] = (float)outl / (nvalid + 1e-9f);
+    }
+    if (tid == 0) *reinterpret_cast<unsigned long long*>(a.acc) = 0ull;
 }
 
 // All flow metrics (snnflow.h, snnflow_flow_metrics): one row of FM_NV per-block sums per
@@ -224,10 +251,6 @@ __global__ __launch_bounds__(NT) void k_flow_metrics_finalize(snnflow_flow_metri
     o[SNNFLOW_M_AAE_FILTERED] = (float)s[14] / ((float)s[15] + 1e-9f);
 }
 
-__global__ void k_zero_f64(double* p, int n) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) p[i] = 0.0;
-}
-
 }  // namespace
 
 extern "C" {
@@ -255,12 +278,14 @@ int snnflow_aee(const snnflow_aee_args* a, void* stream) {
         !a->dt_ratio || !a->acc || !a->aee || !a->percent)
         SNN_FAIL(SNNFLOW_E_ARG, "aee: bad args");
     const hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_zero_f64, dim3(1), dim3(NT), 0, s, a->acc, 2 * a->B + 1);
     const int chunks = (int)(((int64_t)a->H * a->W + NT - 1) / NT);
     hipLaunchKernelGGL(k_aee, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
-    hipLaunchKernelGGL(k_aee_finalize, dim3(1), dim3(NT), 0, s, *a);
     SNN_CHECK_LAUNCH();
     return 0;
+}
+
+int snnflow_aee_acc_doubles(int B, int H, int W) {
+    return (int)(1 + 3 * (int64_t)B * (((int64_t)H * W + NT - 1) / NT));
 }
 
 int snnflow_flow_metrics_rows(int B, int H, int W) {

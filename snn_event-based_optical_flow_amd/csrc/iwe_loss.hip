@@ -35,11 +35,6 @@ __device__ inline int xcd_block() {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
 }
 
-__device__ inline int pass_of(const int32_t* off, int T, int i) {
-    int k = 0;
-    while (k + 1 < T && i >= off[k + 1]) ++k;
-    return k;
-}
 
 // d/dz of max(0, z) as torch.maximum(zeros, z) backward: 1 above, 1/2 on the tie, 0 below.
 __device__ inline float relu_tie(float z) { return z > 0.0f ? 1.0f : (z == 0.0f ? 0.5f : 0.0f); }
@@ -48,15 +43,59 @@ __device__ inline float sgnf(float d) { return d > 0.0f ? 1.0f : (d < 0.0f ? -1.
 // Event e = (sample b, concatenated index i) of window k: its 4 floats and 2 pol floats.
 struct EventRef { const float* ev; const float* pol; int k; };
 
-__device__ inline EventRef event_ref(const snnflow_iwe_loss_args& a, int b, int i) {
-    const int k = pass_of(a.off, a.T, i);
-    const int64_t nk = a.off[k + 1] - a.off[k], j = (int64_t)b * nk + (i - a.off[k]);
+// The window tables of the argument block (pass offsets; event, polarity and flow pointers), copied
+// once per block into LDS: the per-event lookups index them with a per-lane window index, which on
+// the argument block itself is a chain of dependent scalar-memory-missing vector loads (the pass
+// search alone up to T of them) ahead of every event load.  n0: events per window and sample when
+// every window holds the same count (the pass is then one division), else 0.
+struct WinTab {
+    int32_t off[SNNFLOW_MAX_WINDOWS + 1];
+    const float* ev[SNNFLOW_MAX_WINDOWS];
+    const float* pol[SNNFLOW_MAX_WINDOWS];
+    const float* fl[SNNFLOW_MAX_WINDOWS];
+    int n0;
+};
+
+// Called by every thread of the block before its first lookup (contains a barrier).
+__device__ inline void wintab_load(const snnflow_iwe_loss_args& a, WinTab& w) {
+    const int t = threadIdx.x;
+    if (t <= a.T) w.off[t] = a.off[t];
+    if (t < a.T) {
+        w.ev[t] = a.events[t];
+        w.pol[t] = a.pol[t];
+    }
+    if (t < a.tf) w.fl[t] = a.flows[t];
+    if (t == 0) {
+        int n0 = a.off[1] - a.off[0];
+        if (a.off[0] != 0 || n0 <= 0) n0 = 0;
+        for (int k = 1; k < a.T && n0 > 0; ++k)
+            if (a.off[k + 1] - a.off[k] != n0) n0 = 0;
+        w.n0 = n0;
+    }
+    __syncthreads();
+}
+
+__device__ inline int pass_of(const WinTab& w, int T, int i) {
+    if (w.n0 > 0) {
+        const int k = i / w.n0;
+        return k < T ? k : T - 1;
+    }
+    int k = 0;
+    while (k + 1 < T && i >= w.off[k + 1]) ++k;
+    return k;
+}
+
+__device__ inline EventRef event_ref(const WinTab& w, int T, int b, int i) {
+    const int k = pass_of(w, T, i);
+    const int o = w.off[k];
+    const int64_t nk = w.off[k + 1] - o, j = (int64_t)b * nk + (i - o);
     EventRef r;
-    r.ev = a.events[k] + j * 4;
-    r.pol = a.pol[k] + j * 2;
+    r.ev = w.ev[k] + j * 4;
+    r.pol = w.pol[k] + j * 2;
     r.k = k;
     return r;
 }
+
 
 __device__ inline const float* flow_of(const snnflow_iwe_loss_args& a, int b, int t) {
     return a.flows[t] + (int64_t)b * 2 * a.H * a.W;
@@ -132,7 +171,9 @@ __host__ __device__ inline int splat_nsplit(int B, int nbands) {
 
 __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands, int nsplit) {
     __shared__ SplatLds img;
+    __shared__ WinTab wt;
     const int tid = threadIdx.x;
+    wintab_load(a, wt);
     const int blk = xcd_block();
     const int split = blk % nsplit, rest = blk / nsplit;
     const int band = rest % nbands, d = (rest / nbands) % 2, b = rest / (2 * nbands);
@@ -152,7 +193,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
             const int i = i0 + u * stride;
             kk[u] = -1;
             if (i < a.M) {
-                const EventRef r = event_ref(a, b, i);
+                const EventRef r = event_ref(wt, a.T, b, i);
                 ev[u] = *reinterpret_cast<const float4*>(r.ev);
                 pm[u] = *reinterpret_cast<const float2*>(r.pol);
                 kk[u] = r.k;
@@ -163,7 +204,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
         for (int u = 0; u < SPLAT_U; ++u) {
             if (kk[u] < 0) continue;
             const int pix = (int)(ev[u].y * (float)a.W + ev[u].z);
-            const float* fl = flow_of(a, b, a.tf == 1 ? 0 : kk[u]);
+            const float* fl = wt.fl[a.tf == 1 ? 0 : kk[u]] + (int64_t)b * 2 * HWp;
             fy[u] = fl[HWp + pix];
             fx[u] = fl[pix];
         }
@@ -469,16 +510,18 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
     const int64_t n = (int64_t)a.B * a.M;
     const int64_t img = (int64_t)a.B * HWp;
     const int sub = threadIdx.x & (kBwdLanes - 1), d = sub >> 2, q = sub & 3;
+    __shared__ WinTab wt;
+    wintab_load(a, wt);
     // XCD-ordered blocks: a sample's events (and so its image gathers) on one XCD's L2; an event's
     // eight lanes are consecutive lanes of one wave and leave the loop together
     for (int64_t t = (int64_t)xcd_block() * NT + threadIdx.x; t < n * kBwdLanes; t += (int64_t)gridDim.x * NT) {
         const int64_t e = t / kBwdLanes;
         const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
-        const EventRef r = event_ref(a, b, i);
+        const EventRef r = event_ref(wt, a.T, b, i);
         const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
         const int pix = (int)(y * (float)a.W + x);
         const int kf = a.tf == 1 ? 0 : r.k;
-        const float* fl = flow_of(a, b, kf);
+        const float* fl = wt.fl[kf] + (int64_t)b * 2 * HWp;
         const float fy = fl[HWp + pix], fx = fl[pix];
         const float pm0 = r.pol[0], pm1 = r.pol[1];
         const float tref = d == 0 ? (float)a.T : 0.0f;
@@ -532,7 +575,9 @@ struct GevLds {
 __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_args a, const float* __restrict__ gev,
                                                               float* g_flows, int nbands) {
     __shared__ GevLds img;
+    __shared__ WinTab wt;
     const int tid = threadIdx.x;
+    wintab_load(a, wt);
     const int band = blockIdx.x % nbands, rest = blockIdx.x / nbands, t = rest % a.tf, b = rest / a.tf;
     const int64_t HWp = (int64_t)a.H * a.W;
     const int p0 = band * SPLAT_BAND;
@@ -541,7 +586,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_a
     __syncthreads();
     const int i0 = a.tf == 1 ? 0 : a.off[t], i1 = a.tf == 1 ? a.M : a.off[t + 1];
     for (int i = i0 + tid; i < i1; i += SPLAT_NT) {
-        const EventRef r = event_ref(a, b, i);
+        const EventRef r = event_ref(wt, a.T, b, i);
         const int q = (int)(r.ev[1] * (float)a.W + r.ev[2]) - p0;
         if (q < 0 || q >= np) continue;
         const float2 g = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i));

@@ -297,6 +297,9 @@ __global__ void k_prep_weights(DescBatch<snnflow_prep_desc> batch) {
         const float t = d.threshold[e];
         d.threshold[e] = (t < 0.01f) ? 0.01f : t;
     }
+    if (d.zero) {
+        for (int64_t i = e; i < d.zero_n; i += (int64_t)gridDim.x * blockDim.x) d.zero[i] = 0.0;
+    }
 }
 
 // The C x C conv layers (C = 8, 16, 32) run their convolutions on the matrix cores.
@@ -2643,6 +2646,80 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
     for (; j < n; j += CLIP_NT) g[j] = g[j] * c;
 }
 
+// clip_grad_norm_ + Adam (snnflow_clip_adam): one block; the norm pass as k_clip_grad_norm, then
+// every parameter tensor's elements with the reference's Adam arithmetic (fp64 bias corrections).
+__global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a) {
+    __shared__ double part[CLIP_NT / 64];
+    __shared__ float coef_s, step_s;
+    float c = 1.0f;
+    if (a.max_norm > 0.0f) {
+        double s = 0.0;
+        int64_t i = threadIdx.x;
+        for (; i + 7 * CLIP_NT < a.n; i += 8 * CLIP_NT) {
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = a.grad[i + k * CLIP_NT];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += (double)v[k] * (double)v[k];
+        }
+        for (; i < a.n; i += CLIP_NT) {
+            const double v = a.grad[i];
+            s += v * v;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (a.max_norm > 0.0f) {
+            double t = 0.0;
+            for (int w = 0; w < CLIP_NT / 64; ++w) t += part[w];
+            const float total = (float)sqrt(t);
+            const float cc = a.max_norm / (total + a.clip_eps);
+            coef_s = cc < 1.0f ? cc : 1.0f;
+            if (a.total_out) a.total_out[0] = total;
+        } else {
+            coef_s = 1.0f;
+        }
+        const float st = a.step[0] + 1.0f;
+        step_s = st;
+        a.step[0] = st;
+    }
+    __syncthreads();
+    c = coef_s;
+    const double step = (double)step_s;
+    const double bc1 = 1.0 - pow(a.beta1, step), bc2 = 1.0 - pow(a.beta2, step);
+    const float neg_step_size = (float)(-(a.lr / bc1));
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2);
+    const float eps = (float)a.eps, wd = (float)a.weight_decay;
+    const bool clip = a.max_norm > 0.0f;
+    for (int k = 0; k < a.ntensors; ++k) {
+        const snnflow_adam_tensor tk = a.t[k];
+        float* gk = a.grad + tk.offset;
+        float* mk = a.exp_avg + tk.state_offset;
+        float* vk = a.exp_avg_sq + tk.state_offset;
+        for (int64_t i = threadIdx.x; i < tk.numel; i += CLIP_NT) {
+            float g = gk[i];
+            if (clip) {
+                g = g * c;
+                gk[i] = g;  // clip_grad_norm_ scales the gradients in place
+            }
+            float p = tk.param[i];
+            if (wd != 0.0f) g = g + wd * p;
+            float m = mk[i];
+            m = m + w1 * (g - m);  // lerp, weight < 0.5
+            const float v = vk[i] * b2 + w2 * g * g;
+            const float denom = sqrtf(v) / bc2_sqrt + eps;
+            p = p + neg_step_size * (m / denom);
+            mk[i] = m;
+            vk[i] = v;
+            tk.param[i] = p;
+        }
+    }
+}
+
 __global__ void k_lif_export(const float* __restrict__ x, const float* __restrict__ mem, const float* __restrict__ beta,
                              const float* __restrict__ thr, int64_t total, int C, int HW, float* spk, float* mout) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -3786,8 +3863,8 @@ int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream) 
     int maxe = 1;
     for (int i = 0; i < n; ++i) {
         const snnflow_prep_desc& x = d[i];
-        if ((x.w && (x.c <= 0 || x.cin <= 0 || !x.wt_fwd || !x.wt_bwd)) || (!x.w && !x.threshold) ||
-            (x.threshold && x.thr_n <= 0))
+        if ((x.w && (x.c <= 0 || x.cin <= 0 || !x.wt_fwd || !x.wt_bwd)) || (!x.w && !x.threshold && !x.zero) ||
+            (x.threshold && x.thr_n <= 0) || (x.zero && x.zero_n < 0))
             SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: bad descriptor");
         if ((x.frag_fwd || x.frag_bwd) && (!x.w || snnflow_frag_halfs(x.c, x.cin) == 0))
             SNN_FAIL(SNNFLOW_E_ARG, "prep_weights_batch: fragments need cin == c, c % 8 == 0");
@@ -3798,6 +3875,7 @@ int snnflow_prep_weights_batch(const snnflow_prep_desc* d, int n, void* stream) 
             if (fe > maxe) maxe = fe;
         }
         if (x.threshold && x.thr_n > maxe) maxe = x.thr_n;
+        if (x.zero) maxe = std::max(maxe, (int)std::min<int64_t>(x.zero_n, 65536));  // grid-stride beyond
     }
     hipLaunchKernelGGL(k_prep_weights, dim3((maxe + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, batch);
     SNN_CHECK_LAUNCH();
@@ -3808,7 +3886,7 @@ int snnflow_prep_weights(const float* w, int c, int cin, float* wt_fwd, float* w
                          void* stream) {
     if (c <= 0 || cin <= 0 || (w && (!wt_fwd || !wt_bwd)) || (!w && !threshold))
         SNN_FAIL(SNNFLOW_E_ARG, "prep_weights: bad args");
-    snnflow_prep_desc d = {w, c, cin, wt_fwd, wt_bwd, threshold, c, nullptr, nullptr};
+    snnflow_prep_desc d = {w, c, cin, wt_fwd, wt_bwd, threshold, c, nullptr, nullptr, nullptr, 0};
     return snnflow_prep_weights_batch(&d, 1, stream);
 }
 
@@ -4309,6 +4387,20 @@ int snnflow_clip_grad_norm_large(float* g, int64_t n, float max_norm, float eps,
     if (gs > 4096) gs = 4096;
     if (gs < 1) gs = 1;
     hipLaunchKernelGGL(k_clip_scale, dim3((unsigned)gs), dim3(256), 0, s, g, n, coef);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
+int snnflow_clip_adam(const snnflow_clip_adam_args* a, void* stream) {
+    if (!a || !a->grad || !a->exp_avg || !a->exp_avg_sq || !a->step || a->n < 0 || a->n > SNNFLOW_CLIP_ADAM_MAX_N ||
+        a->ntensors < 0 || a->ntensors > SNNFLOW_ADAM_MAX_TENSORS)
+        SNN_FAIL(SNNFLOW_E_ARG, "clip_adam: bad args (n <= SNNFLOW_CLIP_ADAM_MAX_N, ntensors <= SNNFLOW_ADAM_MAX_TENSORS)");
+    for (int k = 0; k < a->ntensors; ++k) {
+        const snnflow_adam_tensor& t = a->t[k];
+        if (!t.param || t.offset < 0 || t.state_offset < 0 || t.numel < 0 || t.offset + t.numel > a->n)
+            SNN_FAIL(SNNFLOW_E_ARG, "clip_adam: tensor range outside the flat buffer");
+    }
+    hipLaunchKernelGGL(k_clip_adam, dim3(1), dim3(CLIP_NT), 0, (hipStream_t)stream, *a);
     SNN_CHECK_LAUNCH();
     return 0;
 }

@@ -11,6 +11,7 @@ from .convlif import ConvLIF, ConvLIFRecurrent
 from . import checkpoint, encodings  # noqa: F401  (checkpoint interchange, on-device event encodings)
 from .loss import EventWarping
 from .metrics import AAE, AAE_Filtered, AAE_Weighted, AE_ofMeans, AEE, NAAE, NEE
+from .optim import ClipAdam
 from .model import LIFFireFlowNet, LIFFireFlowNet_short, LIFFireNet, LIFFireNet_short
 from .unet import (SpikingMultiResUNetRecurrent, SpikingRecEVFlowNet, SpikingRecurrentConvLayer,
                    SpikingResidualBlock, SpikingUpsampleConvLayer)
@@ -18,4 +19,5 @@ from .unet import (SpikingMultiResUNetRecurrent, SpikingRecEVFlowNet, SpikingRec
 __all__ = ["LIFFireNet", "LIFFireNet_short", "LIFFireFlowNet", "LIFFireFlowNet_short", "SNNtorch_ConvLIF",
            "SNNtorch_ConvLIFRecurrent", "ConvLIF", "ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping", "AEE",
            "NEE", "AAE", "NAAE", "AE_ofMeans", "AAE_Weighted", "AAE_Filtered", "SpikingRecEVFlowNet",
-           "SpikingMultiResUNetRecurrent", "SpikingRecurrentConvLayer", "SpikingResidualBlock", "SpikingUpsampleConvLayer"]
+           "SpikingMultiResUNetRecurrent", "SpikingRecurrentConvLayer", "SpikingResidualBlock", "SpikingUpsampleConvLayer",
+           "ClipAdam"]

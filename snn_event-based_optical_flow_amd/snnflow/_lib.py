@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 28
+ABI_VERSION = 29
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -124,6 +124,20 @@ class FlowMetricsArgs(ctypes.Structure):
                 ("dt_ratio", P), ("flow_scaling", F32), ("mag_threshold", F32), ("rows", P), ("out", P)]
 
 
+ADAM_MAX_TENSORS = 64  # SNNFLOW_ADAM_MAX_TENSORS
+CLIP_ADAM_MAX_N = 1 << 20  # SNNFLOW_CLIP_ADAM_MAX_N
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", P), ("offset", I64), ("state_offset", I64), ("numel", I64)]
+
+
+class ClipAdamArgs(ctypes.Structure):
+    _fields_ = [("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("step", P), ("total_out", P), ("n", I64),
+                ("lr", F64), ("beta1", F64), ("beta2", F64), ("eps", F64), ("weight_decay", F64),
+                ("max_norm", F32), ("clip_eps", F32), ("ntensors", I32), ("t", AdamTensor * ADAM_MAX_TENSORS)]
+
+
 # SNNFLOW_M_* output columns of snnflow_flow_metrics
 METRICS = ("aee", "aee_pct", "nee", "nee_pct", "aae", "aae_pct", "naae", "ae_of_means", "aae_weighted",
            "aae_filtered")
@@ -147,7 +161,7 @@ class SlabDesc(ctypes.Structure):
 
 class PrepDesc(ctypes.Structure):
     _fields_ = [("w", P), ("c", I32), ("cin", I32), ("wt_fwd", P), ("wt_bwd", P),
-                ("threshold", P), ("thr_n", I32), ("frag_fwd", P), ("frag_bwd", P)]
+                ("threshold", P), ("thr_n", I32), ("frag_fwd", P), ("frag_bwd", P), ("zero", P), ("zero_n", I64)]
 
 
 MAX_BATCH = 16
@@ -265,6 +279,7 @@ EXPORTS = {
     "snnflow_encode_events": (I32, [ctypes.POINTER(EncodeArgs), P]),
     "snnflow_pol_iwe": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, F32, F32, I32, P, P]),
     "snnflow_aee": (I32, [ctypes.POINTER(AeeArgs), P]),
+    "snnflow_aee_acc_doubles": (I32, [I32, I32, I32]),
     "snnflow_flow_metrics": (I32, [ctypes.POINTER(FlowMetricsArgs), P]),
     "snnflow_flow_metrics_rows": (I32, [I32, I32, I32]),
     "snnflow_convlif_bwd": (I32, [ctypes.POINTER(ConvLifBwdArgs), P]),
@@ -282,6 +297,7 @@ EXPORTS = {
     "snnflow_lif_theta_subtract": (I32, [P, P, P, I64, I32, P, P, P]),
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
     "snnflow_clip_grad_norm_large": (I32, [P, I64, F32, F32, P, P, P]),
+    "snnflow_clip_adam": (I32, [P, P]),
     "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),
     "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),

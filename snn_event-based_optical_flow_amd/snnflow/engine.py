@@ -119,9 +119,10 @@ class PreppedWeights:
         self.key = None
         self.gen = 0  # bumped whenever the buffers are re-allocated
 
-    def ensure(self, weights, thresholds, stream, refresh=True):
+    def ensure(self, weights, thresholds, stream, refresh=True, zero=None):
         """`weights` / `thresholds` are the engine's cached lists (re-built when a parameter is replaced
-        or moved): a new list re-checks pointers and buffers, the same list only the version counters."""
+        or moved): a new list re-checks pointers and buffers, the same list only the version counters.
+        `zero`: an fp64 tensor zeroed by the same launch (a zero-only launch if nothing is re-prepared)."""
         ver = sum(w._version for w in weights) + sum(t._version for t in thresholds)
         same = self.__dict__.get("src") is weights
         if not same:
@@ -149,6 +150,10 @@ class PreppedWeights:
         if fresh:
             self.gen += 1
         if not (refresh or fresh):
+            if zero is not None:
+                d = _lib.PrepDesc()
+                d.zero, d.zero_n = zero.data_ptr(), zero.numel()
+                _lib.call("prep_weights", lib.snnflow_prep_weights_batch, (_lib.PrepDesc * 1)(d), 1, stream)
             return
         descs = []
         for i, w in enumerate(weights):
@@ -162,6 +167,10 @@ class PreppedWeights:
                 descs[i].threshold, descs[i].thr_n = ptr(t), t.numel()
             else:
                 descs.append(_lib.PrepDesc(None, 0, 0, None, None, ptr(t), t.numel()))
+        if zero is not None:
+            if not descs:
+                descs.append(_lib.PrepDesc())
+            descs[0].zero, descs[0].zero_n = zero.data_ptr(), zero.numel()
         for i0 in range(0, len(descs), _lib.MAX_BATCH):
             chunk = descs[i0:i0 + _lib.MAX_BATCH]
             _lib.call("prep_weights", lib.snnflow_prep_weights_batch, (_lib.PrepDesc * len(chunk))(*chunk),
@@ -191,6 +200,11 @@ class FireNetEngine:
         self.fuse_wgrad = self.C == 8          # wavefront backward computes layers >= 1's dW in place
         self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
         self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
+        # forward_sequence, one-shot: a flat fp32 buffer of L x 2BHWC floats that receives the final
+        # step's states (the states the call returns are views into it) instead of a fresh
+        # allocation.  A graph-replay loop that alternates two such buffers hands the states from
+        # one step to the next with no copy; the buffer must not alias the states passed in.
+        self.final_state_out = None
         self.seq_states = None
         self.prep_stale = True  # re-prepare weights at the next forward (set after each backward)
         self.lifs = [c.lif for c in self.cells]
@@ -295,7 +309,7 @@ class FireNetEngine:
         self.ws.slabs([(c.input_size, r) for c, r in zip(self.cells, self.rec)])
         return self.ws
 
-    def prep_weights(self, stream, refresh=True):
+    def prep_weights(self, stream, refresh=True, zero=None):
         ws = self.__dict__.get("_prep_ws")
         if ws is None or self._plist is None:  # conv weights in PreppedWeights order (param_list validates)
             ws = []
@@ -306,7 +320,7 @@ class FireNetEngine:
             self._prep_ws = ws
             self._prep_th = [c.lif.threshold for c in self.cells]
             self._prep_map = None
-        self.prep.ensure(ws, self._prep_th, stream, refresh)
+        self.prep.ensure(ws, self._prep_th, stream, refresh, zero)
         m = self._prep_map
         if m is not None and m[0] == self.prep.gen:
             return m[1], m[2]
@@ -954,6 +968,13 @@ def wavefront_slots(T, K):
     return slots
 
 
+def _state_rows(st_all, fin, T):
+    """Flat per-step state rows of a FireNetSequence call: st_all's rows, the last one replaced by
+    the caller's final_state_out buffer when there is one (st_all then has T - 1 rows)."""
+    rows = [st_all[t] for t in range(st_all.shape[0])]
+    return rows + [fin] if fin is not None else rows
+
+
 class FireNetSequence(torch.autograd.Function):
     """T fused time steps of the network as one autograd node (``forward_sequence``).
 
@@ -978,18 +999,33 @@ class FireNetSequence(torch.autograd.Function):
                 raise _lib.SnnflowError("forward_sequence: every step's input must have the same shape")
         s = _lib.stream_ptr(dev)
         ws = eng.workspace(B, H, W, dev)
-        wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale)
+        # the batch-sum accumulators of this forward (facc) and of its backward (bacc), one fp64
+        # allocation zeroed by the weight-preparation launch
+        nf, nb = T * L * _lib.acc_storage(2 * C), T * L * _lib.acc_storage(_lib.bwd_acc_len(C))
+        accs = torch.empty(nf + nb, dtype=torch.float64, device=dev)
+        facc = accs[:nf].view(T, L, -1)
+        ctx.bacc = accs[nf:].view(T, L, -1)
+        wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale, zero=accs)
         eng.prep_stale = False
         cells = eng.cells
 
         ys = torch.empty(T, L, B, H, W, C, device=dev)
         stats = torch.empty(T, L, 2, C, device=dev)
         n1 = 2 * B * H * W * C
-        st_all = torch.empty(T, L * n1, device=dev)
-        states = [[st_all[t, l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
+        fin = eng.final_state_out
+        eng.final_state_out = None
+        if fin is not None:
+            if (fin.device != dev or fin.dtype != torch.float32 or fin.numel() != L * n1 or not fin.is_contiguous()
+                    or any(p is not None and p.untyped_storage().data_ptr() == fin.untyped_storage().data_ptr()
+                           for p in prev)):
+                raise _lib.SnnflowError("final_state_out: a contiguous fp32 buffer of L*2*B*H*W*C floats on the "
+                                        "input's device, not aliasing the initial states")
+            fin = fin.view(L * n1)
+        st_all = torch.empty(T - (fin is not None), L * n1, device=dev)
+        rows = _state_rows(st_all, fin, T)
+        states = [[rows[t][l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
                    for l in range(L)] for t in range(T)]
         flows = [torch.empty(B, 2, H, W, device=dev) for _ in range(T)]
-        facc = torch.zeros(T, L, _lib.acc_storage(2 * C), dtype=torch.float64, device=dev)
 
         # step 0 reads the initial states (as FireNetStep); step t > 0 the states of step t-1
         mem0, sprev0 = [], []
@@ -1052,6 +1088,9 @@ class FireNetSequence(torch.autograd.Function):
         ctx.has_prev = [p is not None for p in prev]
         ctx.has_mem = [m is not None for m in mem0]
         saved = xs + flows + [ys, stats, st_all]
+        ctx.has_fin = fin is not None
+        if fin is not None:
+            saved.append(fin)
         saved += [m for m in mem0 if m is not None]
         saved += [sp for sp in sprev0 if sp is not None]
         ctx.save_for_backward(*saved)
@@ -1068,8 +1107,10 @@ class FireNetSequence(torch.autograd.Function):
         xs, flows = saved[:T], saved[T:2 * T]
         ys, stats, st_all = saved[2 * T:2 * T + 3]
         rest = saved[2 * T + 3:]
+        fin = rest.pop(0) if ctx.has_fin else None
+        rows = _state_rows(st_all, fin, T)
         n1 = 2 * B * H * W * C
-        states = [[st_all[t, l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
+        states = [[rows[t][l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), nhwc_state_strides(B, C, H, W))
                    for l in range(L)] for t in range(T)]
         mem0 = [rest.pop(0) if ctx.has_mem[l] else None for l in range(L)]
         sprev0 = [rest.pop(0) if (ctx.has_prev[l] and eng.rec[l]) else None for l in range(L)]
@@ -1086,7 +1127,8 @@ class FireNetSequence(torch.autograd.Function):
             eng.open_chain(dev)
         glayers, gpw, gpb = eng.grad_views()
         neurons = eng.neurons()
-        bacc = torch.zeros(T, L, _lib.acc_storage(_lib.bwd_acc_len(C)), dtype=torch.float64, device=dev)
+        bacc = ctx.bacc  # zeroed in the forward (prep launch)
+        ctx.bacc = None
         gcur = torch.empty(T, L, B, H, W, C, device=dev)
         bnc = torch.empty(T, L, 2, C, device=dev)
 

@@ -104,7 +104,11 @@ class AEE(BaseValidationLoss):
         ratio = torch.as_tensor(self._dt_gt, dtype=torch.float32, device=flow.device) / torch.as_tensor(
             self._dt_input, dtype=torch.float32, device=flow.device)
         ratio = ratio.reshape(-1).expand(B).contiguous() if ratio.numel() == 1 else ratio.reshape(B).contiguous()
-        acc = torch.empty(2 * B + 1, dtype=torch.float64, device=flow.device)
+        n = lib.snnflow_aee_acc_doubles(B, H, W)
+        acc = self.__dict__.get("_aee_acc")
+        if acc is None or acc.numel() < n or acc.device != flow.device:
+            acc = torch.zeros(n, dtype=torch.float64, device=flow.device)  # counter acc[0]: zero, kept zero
+            self._aee_acc = acc
         aee = torch.empty(B, device=flow.device)
         pct = torch.empty(B, device=flow.device)
         a = _lib.AeeArgs()

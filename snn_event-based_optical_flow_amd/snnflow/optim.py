@@ -1,0 +1,103 @@
+"""The reference loop's clip + optimizer step as one HIP launch.
+
+train_flow.py:265-267 runs ``torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)`` and then
+``optimizer.step()`` of ``torch.optim.Adam`` (configs/train_SNN.yml:45-47: Adam, lr 2e-4).
+``ClipAdam`` is that pair: ``torch.optim.Adam``'s constructor and per-parameter state
+(``step``, ``exp_avg``, ``exp_avg_sq``) with an optional ``max_norm``; ``step()`` clips the gradients
+in place and applies Adam with the reference's arithmetic (``_single_tensor_adam``: ``lerp_`` for the
+first moment, fp64 bias corrections) in ``snnflow_clip_adam``, one block over the engine's flat
+gradient buffer (FireNetEngine hands every parameter's gradient out as a view of one buffer).  The
+moments live in two persistent flat buffers (parameter order; the gradient buffer may move between
+steps, e.g. one per captured HIP graph); ``self.state[p]`` holds views of them, so ``state_dict()``
+/ ``load_state_dict()`` round-trip like torch's Adam (loaded states are copied back into the flat
+buffers on the next step).  No CPU path: gradients must be the engine's
+flat CUDA buffer (``snnflow.dp.flat_grad_buffer``)."""
+import ctypes
+
+import torch
+
+from . import _lib
+from .dp import flat_grad_buffer
+
+
+class ClipAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, max_norm=None,
+                 clip_eps=1e-6):
+        if lr < 0.0 or eps < 0.0 or not 0.0 <= betas[0] < 1.0 or not 0.0 <= betas[1] < 1.0 or weight_decay < 0.0:
+            raise ValueError("ClipAdam: invalid hyper-parameter")
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, max_norm=max_norm,
+                        clip_eps=clip_eps)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise ValueError("ClipAdam: one parameter group (the clip norm spans all parameters)")
+        self._moments = None     # (parameter ids, exp_avg, exp_avg_sq, step, state offsets)
+        self.last_total_norm = None
+
+    def _state(self, params):
+        """Persistent flat moment buffers (parameter order) and the device step counter; the
+        per-parameter state entries are views of them.  Rebuilt only when the parameter set
+        changes or a loaded state dict replaced the views (values copied over)."""
+        ids = tuple(id(p) for p in params)
+        m = self._moments
+        if m is not None and m[0] == ids and all(self.state[p].get("exp_avg") is not None and
+                                                 self.state[p]["exp_avg"].data_ptr() == m[1].data_ptr() + 4 * o
+                                                 for p, o in zip(params, m[4])):
+            return m
+        dev = params[0].device
+        offs, total = [], 0
+        for p in params:
+            offs.append(total)
+            total += p.numel()
+        ea = torch.zeros(total, device=dev)
+        es = torch.zeros(total, device=dev)
+        step = torch.zeros((), dtype=torch.float32, device=dev)
+        for p, o in zip(params, offs):
+            st, n = self.state[p], p.numel()
+            if "exp_avg" in st:  # carried over (another parameter set, or a loaded state dict)
+                ea[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                es[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                step.copy_(torch.as_tensor(st["step"], dtype=torch.float32))
+            st["exp_avg"] = ea[o:o + n].view_as(p)
+            st["exp_avg_sq"] = es[o:o + n].view_as(p)
+            st["step"] = step
+        self._moments = (ids, ea, es, step, offs)
+        return self._moments
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        group = self.param_groups[0]
+        params = [p for p in group["params"] if p.grad is not None]
+        if not params:
+            return loss
+        if len(params) > _lib.ADAM_MAX_TENSORS:
+            raise _lib.SnnflowError(f"ClipAdam: at most {_lib.ADAM_MAX_TENSORS} parameter tensors")
+        grad = flat_grad_buffer(params)
+        if grad is None or not grad.is_cuda or grad.dtype != torch.float32:
+            raise _lib.SnnflowError("ClipAdam: the gradients must be the engine's flat fp32 CUDA buffer")
+        if grad.numel() > _lib.CLIP_ADAM_MAX_N:
+            raise _lib.SnnflowError("ClipAdam: more than SNNFLOW_CLIP_ADAM_MAX_N parameters")
+        for p in params:
+            if p.dtype != torch.float32 or not p.is_contiguous() or p.device != grad.device:
+                raise _lib.SnnflowError("ClipAdam: fp32 contiguous parameters on the gradients' device")
+        _, ea, es, step, offs = self._state(params)
+        if self.last_total_norm is None or self.last_total_norm.device != grad.device:
+            self.last_total_norm = torch.zeros((), device=grad.device)
+        a = _lib.ClipAdamArgs()
+        a.grad, a.exp_avg, a.exp_avg_sq, a.step = grad.data_ptr(), ea.data_ptr(), es.data_ptr(), step.data_ptr()
+        a.total_out, a.n = self.last_total_norm.data_ptr(), grad.numel()
+        a.lr = float(group["lr"])
+        a.beta1, a.beta2 = float(group["betas"][0]), float(group["betas"][1])
+        a.eps, a.weight_decay = float(group["eps"]), float(group["weight_decay"])
+        mn = group["max_norm"]
+        a.max_norm, a.clip_eps = (float(mn) if mn is not None else 0.0), float(group["clip_eps"])
+        a.ntensors = len(params)
+        base = grad.data_ptr()
+        for i, (p, o) in enumerate(zip(params, offs)):
+            t = a.t[i]
+            t.param, t.offset, t.state_offset, t.numel = p.data_ptr(), (p.grad.data_ptr() - base) // 4, o, p.numel()
+        _lib.call("clip_adam", _lib.lib.snnflow_clip_adam, ctypes.byref(a), _lib.stream_ptr(grad.device))
+        return loss

@@ -40,6 +40,7 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_wgrad_step": _lib.WgradStep, "snnflow_aee_args": _lib.AeeArgs, "snnflow_encode_args": _lib.EncodeArgs, "snnflow_convlif_params": _lib.ConvLifParams,
         "snnflow_convlif_fwd_args": _lib.ConvLifFwdArgs, "snnflow_convlif_bwd_args": _lib.ConvLifBwdArgs, "snnflow_wgrad_args": _lib.WgradArgs, "snnflow_iwe_loss_args": _lib.IweLossArgs,
         "snnflow_flow_metrics_args": _lib.FlowMetricsArgs,
+        "snnflow_adam_tensor": _lib.AdamTensor, "snnflow_clip_adam_args": _lib.ClipAdamArgs,
         "snnflow_unet_seg": _lib.UNetSeg, "snnflow_unet_conv_args": _lib.UNetConvArgs,
         "snnflow_unet_wgrad_args": _lib.UNetWgradArgs, "snnflow_unet_lif_bwd_args": _lib.UNetLifBwdArgs,
         "snnflow_bn_fwd_args": _lib.BnFwdArgs, "snnflow_bn_bwd_args": _lib.BnBwdArgs,
@@ -95,6 +96,13 @@ def test_argument_validation_without_gpu():
     sizes[0] = 4
     assert lib.snnflow_count_nonzero(ptrs, sizes, 1, 1, None) == -1    # NULL data, non-empty
     assert b"count_nonzero" in lib.snnflow_last_error()
+    ca = _lib.ClipAdamArgs()
+    assert lib.snnflow_clip_adam(ctypes.byref(ca), None) == -1          # NULL buffers
+    ca.grad = ca.exp_avg = ca.exp_avg_sq = ca.step = 1
+    ca.n, ca.ntensors = 16, 1
+    ca.t[0].param, ca.t[0].offset, ca.t[0].numel = 1, 8, 9             # range past n
+    assert lib.snnflow_clip_adam(ctypes.byref(ca), None) == -1
+    assert b"clip_adam" in lib.snnflow_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

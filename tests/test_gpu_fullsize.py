@@ -364,3 +364,64 @@ def test_cfg2_eval_vs_oracle(dev):
           f"max|dAEE| over {T} windows {worst_aee:.2e}")
     assert hard == 0
     assert worst_flow <= 1e-4 and worst_aee <= 1e-4
+
+
+def test_clip_adam_matches_torch(dev):
+    """snnflow.ClipAdam (one launch: clip_grad_norm_ + Adam, train_flow.py:265-267) against the
+    reference's pair -- torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (single-tensor, the
+    reference's CPU arithmetic) -- over 4 train steps of LIFFireNet at C = 8 with large gradients
+    (so that the clip is active), plus weight decay on a second run.  Both copies see the same
+    gradients at every step (the torch copy's gradients are copied from ours before clipping), so
+    the comparison isolates the optimizer: clipped gradients and the reported norm within 1e-6 /
+    1e-5 relative; moments within 1e-6 of their scale; parameters within 1e-6 relative or 1e-4 of
+    the largest Adam step."""
+    import copy
+
+    import snnflow
+    from snnflow.parser import train_snn_model_kwargs
+    from snnflow.synthetic import make_window
+
+    for wd in (0.0, 1e-2):
+        torch.manual_seed(0)
+        model = snnflow.LIFFireNet(train_snn_model_kwargs(base_num_channels=8)).to(dev).train()
+        twin = [p.detach().clone() for p in model.parameters()]
+        opt = snnflow.ClipAdam(model.parameters(), lr=2e-4, weight_decay=wd, max_norm=1.0)
+        tw = [torch.nn.Parameter(t) for t in twin]
+        topt = torch.optim.Adam(tw, lr=2e-4, weight_decay=wd, foreach=False)
+        cfg = {"loader": {"resolution": [64, 64]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+               "model": {"mask_output": True}}
+        lf = snnflow.EventWarping(cfg, dev)
+        gen = torch.Generator(device=dev).manual_seed(5)
+        for it in range(4):
+            wins = [make_window(2, 500, 64, 64, gen, dev) for _ in range(3)]
+            lf.reset()
+            outs = model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+            for w, o in zip(wins, outs):
+                lf.event_flow_association(o["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            (lf() * 1e3).backward()
+            for t, p in zip(tw, model.parameters()):
+                t.grad = p.grad.detach().clone()
+            want_norm = torch.nn.utils.clip_grad_norm_(tw, 1.0)
+            opt.step()
+            topt.step()
+            assert abs(float(opt.last_total_norm) - float(want_norm)) <= 1e-5 * float(want_norm)
+            assert float(want_norm) > 1.0  # the clip is active
+            for p, t in zip(model.parameters(), tw):
+                # the largest Adam step is lr / bc1 = 2e-3 (step 1); near-zero first moments round
+                # differently in the two lerps: 1e-4 of that step
+                np.testing.assert_allclose(p.detach().cpu().numpy(), t.detach().cpu().numpy(), rtol=1e-6, atol=2e-7)
+                np.testing.assert_allclose(p.grad.cpu().numpy(), t.grad.cpu().numpy(), rtol=1e-6, atol=1e-12)
+                so, st = opt.state[p], topt.state[t]
+                for k in ("exp_avg", "exp_avg_sq"):  # lerp / fma rounding: relative to the tensor's scale
+                    want = st[k].cpu().numpy()
+                    np.testing.assert_allclose(so[k].cpu().numpy(), want, rtol=1e-6, atol=1e-6 * np.abs(want).max())
+                assert float(so["step"]) == float(st["step"]) == it + 1
+            opt.zero_grad(set_to_none=True)
+            model.detach_states()
+        # state dict round trip: a fresh optimizer continues from the saved moments
+        sd = copy.deepcopy(opt.state_dict())
+        opt2 = snnflow.ClipAdam(model.parameters(), lr=2e-4, weight_decay=wd, max_norm=1.0)
+        opt2.load_state_dict(sd)
+        m = opt2._state([p for p in model.parameters()])
+        assert float(m[3]) == 4.0
+        np.testing.assert_array_equal(m[1].cpu().numpy(), opt._moments[1].cpu().numpy())

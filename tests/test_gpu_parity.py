@@ -767,6 +767,11 @@ def test_eval_vs_golden(golden, dev, B):
     aee, pct = m()
     np.testing.assert_allclose(aee.cpu().numpy(), g[f"b{B}_aee"], rtol=1e-5)
     np.testing.assert_allclose(pct.cpu().numpy(), g[f"b{B}_pct"], rtol=1e-6)
+    # one launch with a self-resetting completion counter and fixed-order sums: repeated calls on
+    # the same scratch give the same bits
+    for _ in range(3):
+        a2, p2 = m()
+        assert torch.equal(a2, aee) and torch.equal(p2, pct)
 
 
 _METRIC_CLASSES = {"NEE": ("nee", "nee_pct"), "AAE": ("aae", "aae_pct"), "NAAE": ("naae",),
@@ -1023,6 +1028,57 @@ def test_forward_sequence_input_and_state_grads(dev):
             assert _rel(b, a) < 1e-5
     for a, b in zip(res["step"][2], res["seq"][2]):
         assert _rel(b, a) < 1e-5
+
+
+def test_forward_sequence_final_state_out(dev):
+    """FireNetEngine.final_state_out (the bench's copy-free state hand-over): two chained train
+    sequences with the final states written into alternating caller buffers give the same flows,
+    parameter gradients and states, bit for bit, as fresh allocations + detach; the returned states
+    are views into the buffer; a buffer aliasing the initial states is refused."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow import _lib
+
+    torch.manual_seed(8)
+    H = W = 32
+    T, B, C = 3, 2, 8
+    ma = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=C)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    gen = torch.Generator(device=dev).manual_seed(4)
+    xs = [(torch.rand(B, 2, H, W, generator=gen, device=dev) < 0.2).float() * 3 for _ in range(2 * T)]
+    n = mb.engine.L * 2 * B * C * H * W
+    bufs = [torch.full((n,), float("nan"), device=dev), torch.full((n,), float("nan"), device=dev)]
+    out = {}
+    for tag, m in (("alloc", ma), ("buf", mb)):
+        flows, grads = [], []
+        for k in range(2):
+            if tag == "buf":
+                m.engine.final_state_out = bufs[k % 2]
+            outs = m.forward_sequence(None, xs[k * T:(k + 1) * T])
+            if tag == "buf":
+                base = bufs[k % 2].data_ptr()
+                assert all(base <= s.data_ptr() < base + 4 * n for s in m._states)
+            sum(o["flow"][0].square().sum() for o in outs).backward()
+            flows += [o["flow"][0].detach().cpu() for o in outs]
+            grads.append([p.grad.detach().cpu().clone() for p in m.parameters()])
+            m.zero_grad(set_to_none=True)
+            m.detach_states()
+        out[tag] = (flows, grads, [s.detach().cpu() for s in m._states])
+    for a, b in zip(out["alloc"][0], out["buf"][0]):
+        assert torch.equal(a, b)
+    for ga, gb in zip(out["alloc"][1], out["buf"][1]):
+        for a, b in zip(ga, gb):
+            assert torch.equal(a, b)
+    for a, b in zip(out["alloc"][2], out["buf"][2]):
+        assert torch.equal(a, b)
+    with torch.no_grad():
+        mb.engine.final_state_out = bufs[0]
+        mb.forward_sequence(None, xs[:T])  # mb's states are now views of bufs[0]
+        mb.engine.final_state_out = bufs[0]
+        with pytest.raises(_lib.SnnflowError):
+            mb.forward_sequence(None, xs[:T])
 
 
 def test_forward_sequence_eval_mode_and_fallbacks(dev):
