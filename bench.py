@@ -107,6 +107,18 @@ def slot_pass_bytes(kind, C, P, cin0, T, layer_spec):
     return T * sum(algorithmic_bytes(n, C, P, cin0) for n in names)
 
 
+def eval_pass_bytes(C, P, cin0, T, layer_spec):
+    """Algorithmic bytes of the fused evaluation launches over T steps (snnflow_eval_slot): per
+    layer-step the input (event tensor, or layer l-1's spikes), the layer's membrane at t-1 (and its
+    spikes at t-1 for a recurrent cell) in, its state (membrane, spikes) out; the flow out once per
+    step."""
+    f = 4 * P
+    per = f * (cin0 + C + 2 * C)
+    for _, r in layer_spec[1:]:
+        per += f * (C + C + (C if r else 0) + 2 * C)
+    return T * (per + f * 2)
+
+
 def classify(name, rec_layers):
     """Map engine launch names to kernel classes with one byte formula each."""
     if name.startswith("conv_fwd["):
@@ -635,6 +647,8 @@ def _firenet_roofline(kern, model, args, B, R, T):
     abytes = algorithmic_bytes(dominant, args.channels, P, 2)
     if dominant in ("fwd_slot", "bwd_slot"):  # wavefront launches: the pass's layer-step bytes / its launches
         abytes = slot_pass_bytes(dominant, args.channels, P, 2, T, model.layer_spec) / n_dom
+    elif dominant == "eval_slot":
+        abytes = eval_pass_bytes(args.channels, P, 2, T, model.layer_spec) / n_dom
     achieved = abytes / (avg_us * 1e-6) / 1e9 if abytes else None
     kernels = {k: {"launches": n, "avg_us": round(1000.0 * t / n, 2), "share": round(t / sum(x[1] for x in classes.values()), 3)}
                for k, (n, t) in sorted(classes.items(), key=lambda kv: -kv[1][1])}

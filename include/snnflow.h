@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 29
+#define SNNFLOW_ABI_VERSION 30
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -507,6 +507,30 @@ int snnflow_clip_grad_norm(float* g, int64_t n, float max_norm, float eps, float
 int snnflow_clip_grad_norm_large(float* g, int64_t n, float max_norm, float eps, float* total_out,
                                  double* scratch, void* stream);
 
+/* ---- evaluation forward (eval_flow.py:208-338: model.eval(), BatchNorm on running statistics)
+ * One layer-step with conv + BatchNorm + LIF fused, and for the last layer also the prediction
+ * ConvLayer(C->2, 1x1) + tanh (models/model.py:182): with running statistics a layer's spikes can
+ * leave the kernel that computes its conv, so task (l, t) reads the spikes of layer l-1 at step t
+ * (or the event tensor, l = 0) and layer l's own state at t-1, and writes layer l's state at t.  The
+ * T x L layer-steps then run in T + L - 1 wavefront launches (task (l, t) in launch l + t) instead of
+ * the train path's 2(T-1) + L + 1 split conv / LIF launches.  c = 8; the same per-element LIF
+ * arithmetic as the train-path kernels (snnflow_lif_fwd / the LIF-fed conv tasks). */
+typedef struct snnflow_eval_fwd_args {
+    int B, H, W, cin, c;
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;  /* cin != c (2 or 4): the event tensor, any strides */
+    const float* s_in;        /* cin == c: spikes of layer l-1 at this step, NHWC [B][H][W][c] (its state's
+                               * spike half) */
+    const float* mem_prev;    /* NHWC [B][H][W][c] membrane of this layer at t-1 (NULL: zero) */
+    const float* s_prev;      /* recurrent cells: NHWC spikes of this layer at t-1 (NULL: no recurrent input) */
+    const float* wt_ff; const float* wt_rec;      /* [tap][cin][c] (snnflow_prep_desc.wt_fwd) */
+    const float* wt_ff_t; const float* wt_rec_t;  /* [tap][c][cin] (wt_bwd): the c = 8 matrix-core fragments */
+    snnflow_neuron n;         /* this layer's BatchNorm (bn_train must be 0) + LIF */
+    float* state;             /* out [2][B][H][W][c]: membrane, spikes */
+    const float* pred_w; const float* pred_b; float* flow;  /* optional (last layer): flow [B][2][H][W] */
+} snnflow_eval_fwd_args;
+#define SNNFLOW_EVAL_MAX_TASKS 8
+int snnflow_eval_slot(const snnflow_eval_fwd_args* tasks, int n, void* stream);
+
 /* clip_grad_norm_ + Adam in one launch (train_flow.py:265-267: clip_grad_norm_(params, max_norm),
  * optimizer.step() of torch.optim.Adam, configs/train_SNN.yml:45-47), over the engine's flat gradient
  * buffer (snnflow.optim.ClipAdam).  total = ||grad||_2 (fp64), grad *= min(max_norm / (total +
@@ -515,8 +539,8 @@ int snnflow_clip_grad_norm_large(float* g, int64_t n, float max_norm, float eps,
  * exp_avg_sq * beta2 + (1 - beta2) g^2, bias corrections in fp64, denom = sqrt(exp_avg_sq) /
  * sqrt(bc2) + eps, param -= lr / bc1 * exp_avg / denom).  t[i] maps parameter tensor i to
  * grad[offset .. offset + numel) and to exp_avg / exp_avg_sq[state_offset .. state_offset + numel)
- * (persistent moment buffers: the gradient buffer may move between steps, the moments do not).  One
- * block: n <= SNNFLOW_CLIP_ADAM_MAX_N.  Replaces snnflow_clip_grad_norm + torch's Adam kernels. */
+ * (persistent moment buffers: the gradient buffer may move between steps, the moments do not); the
+ * t[] in ascending, non-overlapping gradient order.  One block: n <= SNNFLOW_CLIP_ADAM_MAX_N.  Replaces snnflow_clip_grad_norm + torch's Adam kernels. */
 #define SNNFLOW_ADAM_MAX_TENSORS 64
 #define SNNFLOW_CLIP_ADAM_MAX_N (1 << 20)
 typedef struct {

@@ -59,34 +59,53 @@ __global__ __launch_bounds__(NT) void k_pol_iwe(const float* __restrict__ events
     }
 }
 
-// AEE in one launch.  Per pixel: endpoint error, validity, outlier; per (sample, chunk of NT pixels)
-// block one fp64 row {sum err, sum valid, outliers} at acc[1 + 3 blk]; the last block to finish
-// (completion counter acc[0]) sums every sample's rows in chunk order, writes aee / percent (the
-// outliers counted over the whole batch, loss/flow.py:647) and resets the counter: deterministic,
-// and no zero / finalize launches.
-__global__ __launch_bounds__(NT) void k_aee(snnflow_aee_args a, int chunks) {
-    __shared__ float red[NT / 64][3];
-    __shared__ double smp[NT][3];  // B <= NT (host check)
+// AEE in one launch.  Per pixel: endpoint error, validity, outlier; per (sample, slice of
+// AEE_NT * AEE_PPT pixels) block one fp64 row {sum err, sum valid, outliers} at acc[1 + 3 blk]; the
+// last block to finish (completion counter acc[0]) sums every sample's rows in slice order, writes
+// aee / percent (the outliers counted over the whole batch, loss/flow.py:647) and resets the
+// counter: deterministic, no zero / finalize launches.  Few large blocks: each block's release
+// fence writes its XCD's L2 back, so the block count is kept near one per sample.
+constexpr int AEE_NT = 1024, AEE_PPT = 16;
+
+__host__ __device__ inline int aee_slices(int64_t HWp) {
+    return (int)((HWp + (int64_t)AEE_NT * AEE_PPT - 1) / ((int64_t)AEE_NT * AEE_PPT));
+}
+
+__global__ __launch_bounds__(AEE_NT) void k_aee(snnflow_aee_args a, int slices) {
+    __shared__ double red[AEE_NT / 64][3];
+    __shared__ double smp[AEE_NT][3];  // B <= AEE_NT (host check)
     __shared__ int last;
-    const int tid = threadIdx.x, b = blockIdx.x / chunks, chunk = blockIdx.x - b * chunks;
+    const int tid = threadIdx.x, b = blockIdx.x / slices, sl = blockIdx.x - b * slices;
     const int64_t HWp = (int64_t)a.H * a.W;
-    const int64_t p = (int64_t)chunk * NT + tid;
+    const int64_t p0 = (int64_t)sl * AEE_NT * AEE_PPT;
+    const int64_t p1 = p0 + (int64_t)AEE_NT * AEE_PPT < HWp ? p0 + (int64_t)AEE_NT * AEE_PPT : HWp;
+    const float r = a.dt_ratio[b];
+    const float* f = a.flow + (int64_t)b * 2 * HWp;
+    const float* g = a.gtflow + (int64_t)b * 2 * HWp;
+    const float* em = a.event_mask + (int64_t)b * HWp;
     float err = 0.0f, val = 0.0f, out = 0.0f;
-    if (p < HWp) {
-        const float r = a.dt_ratio[b];
-        const float* f = a.flow + (int64_t)b * 2 * HWp + p;
-        const float* g = a.gtflow + (int64_t)b * 2 * HWp + p;
-        const float fx = (f[0] * a.flow_scaling) * r, fy = (f[HWp] * a.flow_scaling) * r;
+#pragma unroll 4
+    for (int64_t p = p0 + tid; p < p1; p += AEE_NT) {
+        const float fx = (f[p] * a.flow_scaling) * r, fy = (f[HWp + p] * a.flow_scaling) * r;
+        const float gx = g[p], gy = g[HWp + p];
         const float mag = sqrtf(fx * fx + fy * fy);
-        const float dx = fx - g[0], dy = fy - g[HWp];
+        const float dx = fx - gx, dy = fy - gy;
         const float e = sqrtf(dx * dx + dy * dy);
-        const bool valid = a.event_mask[(int64_t)b * HWp + p] != 0.0f && !(g[0] == 0.0f && g[HWp] == 0.0f);
+        const bool valid = em[p] != 0.0f && !(gx == 0.0f && gy == 0.0f);
         const float mk = valid ? 1.0f : 0.0f;
-        err = e * mk;
-        val = mk;
-        out = (err > 3.0f && err > 0.05f * (mag * mk)) ? 1.0f : 0.0f;
+        const float ae = e * mk;
+        err += ae;
+        val += mk;
+        out += (ae > 3.0f && ae > 0.05f * (mag * mk)) ? 1.0f : 0.0f;
     }
-    const float s0 = wave_total(err), s1 = wave_total(val), s2 = wave_total(out);
+    // per-thread sums of <= AEE_PPT pixels in fp32 (counts exact), across threads in fp64
+    double s0 = err, s1 = val, s2 = out;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s0 += __shfl_xor(s0, off, 64);
+        s1 += __shfl_xor(s1, off, 64);
+        s2 += __shfl_xor(s2, off, 64);
+    }
     if ((tid & 63) == 0) {
         red[tid >> 6][0] = s0;
         red[tid >> 6][1] = s1;
@@ -95,7 +114,7 @@ __global__ __launch_bounds__(NT) void k_aee(snnflow_aee_args a, int chunks) {
     __syncthreads();
     if (tid < 3) {
         double t = 0.0;
-        for (int w = 0; w < NT / 64; ++w) t += (double)red[w][tid];
+        for (int w = 0; w < AEE_NT / 64; ++w) t += red[w][tid];
         a.acc[1 + 3 * (int64_t)blockIdx.x + tid] = t;
     }
     __threadfence();  // the row is visible device-wide before the block counts as done
@@ -109,11 +128,11 @@ __global__ __launch_bounds__(NT) void k_aee(snnflow_aee_args a, int chunks) {
     __threadfence();
     if (tid < a.B) {
         double e = 0.0, v = 0.0, o = 0.0;
-        const double* r = a.acc + 1 + 3 * (int64_t)tid * chunks;
-        for (int c = 0; c < chunks; ++c) {
-            e += r[3 * c];
-            v += r[3 * c + 1];
-            o += r[3 * c + 2];
+        const double* rr = a.acc + 1 + 3 * (int64_t)tid * slices;
+        for (int c = 0; c < slices; ++c) {
+            e += rr[3 * c];
+            v += rr[3 * c + 1];
+            o += rr[3 * c + 2];
         }
         smp[tid][0] = e;
         smp[tid][1] = v;
@@ -274,18 +293,18 @@ int snnflow_pol_iwe(const float* events, const float* flow, const float* pol, in
 }
 
 int snnflow_aee(const snnflow_aee_args* a, void* stream) {
-    if (!a || a->B <= 0 || a->B > NT || a->H <= 0 || a->W <= 0 || !a->flow || !a->gtflow || !a->event_mask ||
+    if (!a || a->B <= 0 || a->B > AEE_NT || a->H <= 0 || a->W <= 0 || !a->flow || !a->gtflow || !a->event_mask ||
         !a->dt_ratio || !a->acc || !a->aee || !a->percent)
         SNN_FAIL(SNNFLOW_E_ARG, "aee: bad args");
     const hipStream_t s = (hipStream_t)stream;
-    const int chunks = (int)(((int64_t)a->H * a->W + NT - 1) / NT);
-    hipLaunchKernelGGL(k_aee, dim3(a->B * chunks), dim3(NT), 0, s, *a, chunks);
+    const int slices = aee_slices((int64_t)a->H * a->W);
+    hipLaunchKernelGGL(k_aee, dim3(a->B * slices), dim3(AEE_NT), 0, s, *a, slices);
     SNN_CHECK_LAUNCH();
     return 0;
 }
 
 int snnflow_aee_acc_doubles(int B, int H, int W) {
-    return (int)(1 + 3 * (int64_t)B * (((int64_t)H * W + NT - 1) / NT));
+    return (int)(1 + 3 * (int64_t)B * aee_slices((int64_t)H * W));
 }
 
 int snnflow_flow_metrics_rows(int B, int H, int W) {

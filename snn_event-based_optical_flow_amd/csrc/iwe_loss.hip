@@ -128,6 +128,9 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 #ifndef SNNFLOW_SPLAT_SPLIT
 #define SNNFLOW_SPLAT_SPLIT 4
 #endif
+#ifndef SNNFLOW_SPLAT_PROBE
+#define SNNFLOW_SPLAT_PROBE 0  // timing attribution only: 1 = no LDS adds, 2 = no event loop
+#endif
 constexpr bool kSplatFixed = SNNFLOW_SPLAT_FIXED != 0;
 constexpr int SPLAT_NT = 1024, SPLAT_BAND = kSplatFixed ? 2048 : 4096, SPLAT_SPLIT = SNNFLOW_SPLAT_SPLIT;
 
@@ -184,7 +187,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
     __syncthreads();
     const float tref = d == 0 ? (float)a.T : 0.0f;
     const int stride = nsplit * SPLAT_NT;
-    for (int i0 = split * SPLAT_NT + tid; i0 < a.M; i0 += SPLAT_U * stride) {
+    for (int i0 = split * SPLAT_NT + tid; i0 < ((SNNFLOW_SPLAT_PROBE & 2) ? 0 : a.M); i0 += SPLAT_U * stride) {
         float4 ev[SPLAT_U];
         float2 pm[SPLAT_U];
         int kk[SPLAT_U];
@@ -223,6 +226,10 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
                 const int li = c[q].idx - p0;
                 if (wt == 0.0f || li < 0 || li >= np) continue;
                 const float wts = wt * tsw;
+                if (SNNFLOW_SPLAT_PROBE & 1) {
+                    if (wts == 12345.0f) img.add(0, li, wt);  // (keeps the math alive)
+                    continue;
+                }
                 if (pm0 != 0.0f) {
                     img.add(0, li, wt * pm0);
                     img.add(2, li, wts * pm0);

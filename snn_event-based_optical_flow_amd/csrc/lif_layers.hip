@@ -2607,19 +2607,15 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
                                                           float* total_out) {
     __shared__ double part[CLIP_NT / 64];
     __shared__ float coef_s;
-    // 8 loads in flight per thread (one block: the vector is small, ~5e3..1e5 floats)
+    // 8 guarded loads in flight per thread and round (one block: the vector is small, ~5e3..1e5
+    // floats; a serial tail loop waited one memory latency per element)
     double s = 0.0;
-    int64_t i = threadIdx.x;
-    for (; i + 7 * CLIP_NT < n; i += 8 * CLIP_NT) {
+    for (int64_t i = threadIdx.x; i < n; i += 8 * CLIP_NT) {
         float v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = g[i + k * CLIP_NT];
+        for (int k = 0; k < 8; ++k) v[k] = i + k * CLIP_NT < n ? g[i + k * CLIP_NT] : 0.0f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) s += (double)v[k] * (double)v[k];
-    }
-    for (; i < n; i += CLIP_NT) {
-        const double v = g[i];
-        s += v * v;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -2635,15 +2631,14 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
     }
     __syncthreads();
     const float c = coef_s;
-    int64_t j = threadIdx.x;
-    for (; j + 7 * CLIP_NT < n; j += 8 * CLIP_NT) {
+    for (int64_t j = threadIdx.x; j < n; j += 8 * CLIP_NT) {
         float v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = g[j + k * CLIP_NT];
+        for (int k = 0; k < 8; ++k) v[k] = j + k * CLIP_NT < n ? g[j + k * CLIP_NT] : 0.0f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) g[j + k * CLIP_NT] = v[k] * c;
+        for (int k = 0; k < 8; ++k)
+            if (j + k * CLIP_NT < n) g[j + k * CLIP_NT] = v[k] * c;
     }
-    for (; j < n; j += CLIP_NT) g[j] = g[j] * c;
 }
 
 // clip_grad_norm_ + Adam (snnflow_clip_adam): one block; the norm pass as k_clip_grad_norm, then
@@ -2651,20 +2646,19 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
 __global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a) {
     __shared__ double part[CLIP_NT / 64];
     __shared__ float coef_s, step_s;
+    __shared__ snnflow_adam_tensor tab[SNNFLOW_ADAM_MAX_TENSORS];  // the argument table, for lookups
+    if (threadIdx.x < a.ntensors) tab[threadIdx.x] = a.t[threadIdx.x];
     float c = 1.0f;
     if (a.max_norm > 0.0f) {
         double s = 0.0;
-        int64_t i = threadIdx.x;
-        for (; i + 7 * CLIP_NT < a.n; i += 8 * CLIP_NT) {
+        // 8 guarded loads in flight per thread and round (the vector is ~5e3..1e6 floats: for the
+        // small ones a serial tail loop would wait one memory latency per element)
+        for (int64_t i0 = threadIdx.x; i0 < a.n; i0 += 8 * CLIP_NT) {
             float v[8];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = a.grad[i + k * CLIP_NT];
+            for (int k = 0; k < 8; ++k) v[k] = i0 + k * CLIP_NT < a.n ? a.grad[i0 + k * CLIP_NT] : 0.0f;
 #pragma unroll
             for (int k = 0; k < 8; ++k) s += (double)v[k] * (double)v[k];
-        }
-        for (; i < a.n; i += CLIP_NT) {
-            const double v = a.grad[i];
-            s += v * v;
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
@@ -2695,27 +2689,52 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a)
     const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2);
     const float eps = (float)a.eps, wd = (float)a.weight_decay;
     const bool clip = a.max_norm > 0.0f;
-    for (int k = 0; k < a.ntensors; ++k) {
-        const snnflow_adam_tensor tk = a.t[k];
-        float* gk = a.grad + tk.offset;
-        float* mk = a.exp_avg + tk.state_offset;
-        float* vk = a.exp_avg_sq + tk.state_offset;
-        for (int64_t i = threadIdx.x; i < tk.numel; i += CLIP_NT) {
-            float g = gk[i];
+    // flat over the gradient buffer: element i belongs to the tensor with the largest offset <= i
+    // (offsets ascending, host-checked), found by a binary search over the LDS copy of the table.
+    // CLIP_PER elements per thread and round with every load issued before any math: one memory
+    // latency per round instead of one per element (or, looping over tensors, one per tensor).
+    constexpr int CLIP_PER = 8;
+    for (int64_t i0 = threadIdx.x; i0 < a.n; i0 += (int64_t)CLIP_PER * CLIP_NT) {
+        float gv[CLIP_PER], pv[CLIP_PER], mv[CLIP_PER], vv[CLIP_PER];
+        float *pp[CLIP_PER], *mp[CLIP_PER], *vp[CLIP_PER];
+#pragma unroll
+        for (int u = 0; u < CLIP_PER; ++u) {
+            const int64_t i = i0 + (int64_t)u * CLIP_NT;
+            pp[u] = nullptr;
+            if (i >= a.n) continue;
+            int lo = 0, hi = a.ntensors - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (tab[mid].offset <= i) lo = mid;
+                else hi = mid - 1;
+            }
+            const int64_t j = i - tab[lo].offset;
+            if (j < 0 || j >= tab[lo].numel) continue;  // a gap between tensors (not written by the engine)
+            pp[u] = tab[lo].param + j;
+            mp[u] = a.exp_avg + tab[lo].state_offset + j;
+            vp[u] = a.exp_avg_sq + tab[lo].state_offset + j;
+            gv[u] = a.grad[i];
+            pv[u] = *pp[u];
+            mv[u] = *mp[u];
+            vv[u] = *vp[u];
+        }
+#pragma unroll
+        for (int u = 0; u < CLIP_PER; ++u) {
+            if (!pp[u]) continue;
+            float g = gv[u];
             if (clip) {
                 g = g * c;
-                gk[i] = g;  // clip_grad_norm_ scales the gradients in place
+                a.grad[i0 + (int64_t)u * CLIP_NT] = g;  // clip_grad_norm_ scales the gradients in place
             }
-            float p = tk.param[i];
+            float p = pv[u];
             if (wd != 0.0f) g = g + wd * p;
-            float m = mk[i];
-            m = m + w1 * (g - m);  // lerp, weight < 0.5
-            const float v = vk[i] * b2 + w2 * g * g;
+            const float m = mv[u] + w1 * (g - mv[u]);  // lerp, weight < 0.5
+            const float v = vv[u] * b2 + w2 * g * g;
             const float denom = sqrtf(v) / bc2_sqrt + eps;
             p = p + neg_step_size * (m / denom);
-            mk[i] = m;
-            vk[i] = v;
-            tk.param[i] = p;
+            *mp[u] = m;
+            *vp[u] = v;
+            *pp[u] = p;
         }
     }
 }
@@ -2855,6 +2874,12 @@ __device__ inline void globalize(snnflow_layer_bwd_args& a) {
     globalize(a.prev);
     SNN_G(a.prev_g_state); SNN_G(a.prev_g_cur); SNN_G(a.prev_g_mem); SNN_G(a.acc_out); SNN_G(a.zero0);
     SNN_G(a.zero1); SNN_G(a.wd_ff); SNN_G(a.wd_rec); SNN_G(a.wslab_ff); SNN_G(a.wslab_rec); SNN_G(a.s_prev);
+}
+__device__ inline void globalize(snnflow_eval_fwd_args& a) {
+    SNN_G(a.x); SNN_G(a.s_in); SNN_G(a.mem_prev); SNN_G(a.s_prev); SNN_G(a.wt_ff); SNN_G(a.wt_rec);
+    SNN_G(a.wt_ff_t); SNN_G(a.wt_rec_t);
+    globalize(a.n);
+    SNN_G(a.state); SNN_G(a.pred_w); SNN_G(a.pred_b); SNN_G(a.flow);
 }
 #undef SNN_G
 
@@ -3273,6 +3298,270 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? 6 : 1) void k_fwd_slot(FwdSlotPara
             else lif_fwd_body<C, true, NT * 2>(a, g);
             break;
         }
+        default: break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Evaluation forward (snnflow_eval_slot): conv + BatchNorm (running statistics) + LIF of one layer
+// in one task, the prediction fused into the last layer's.  C = 8 LIF-fed layers as a tile pipeline
+// organised like fwd_lif8_pipe (2 tiles per block, the next tile's spike halo by LDS-DMA while this
+// tile's convs run, swapped-operand convs packed by v_permlane32_swap); the head (event-tensor input,
+// real-valued: vector-ALU conv in conv_fwd_body's order) one tile per block.
+// ---------------------------------------------------------------------------
+constexpr int kEvalTasks = SNNFLOW_EVAL_MAX_TASKS;
+enum EvalKind : int { EK_HEAD2, EK_HEAD4, EK_FF, EK_REC };
+
+struct EvalSlotParams {
+    snnflow_eval_fwd_args t[kEvalTasks];
+    int kind[kEvalTasks], blk0[kEvalTasks], nblk[kEvalTasks];
+    int ntask;
+};
+
+template <bool REC>
+struct EvalLds {  // bytes: raw fp32 spike halo (DMA), bf16 spike tiles, compact fragments
+    static constexpr int RAW = 0, SPK = kPipeRaw, RSPK = SPK + kPipeSpk;
+    static constexpr int FF = RSPK + (REC ? kPipeSpk : 0), FR = FF + kPipeFrag;
+    static constexpr int BYTES = FR + (REC ? kPipeFrag : 0);
+    static constexpr int FLOATS = BYTES / 4;
+};
+constexpr int kEvalLdsFloats = cmax(EvalLds<true>::FLOATS, ConvFwdLds<4, 8, false, false, 2>::FLOATS);
+
+// LIF of 4 channels of one pixel from the pre-BN current (layer's own coefficients) and the
+// incoming membrane; writes the state (membrane, spike planes) and returns the spikes.
+__device__ inline float4 eval_lif_store(const float4& y, const float4& m, const LifCoef* kc, bool zr, float4* st4,
+                                        int64_t q, int64_t plane4) {
+    const Lif4 o = zr ? lif_step4(y, m, kc, true) : lif_step4(y, m, kc, false);
+    st_state4(st4, q, o.mout);
+    st_state4(st4, plane4 + q, o.s);
+    return o.s;
+}
+
+// Head task: conv of the cin-channel event tensor (conv_fwd_body<CIN, 8, false, false, 2>'s staging
+// and per-pixel summation order) -> BN + LIF -> state.  One tile per block.
+template <int CIN>
+__device__ void eval_head_body(const snnflow_eval_fwd_args& a, const Grid g, float* lds) {
+    constexpr int C = 8, NTB = 2 * NT, CO = 4;
+    __shared__ LifCoef coef[C];
+    const int tid = threadIdx.x, pt = tid % NT, ty = pt / TW, tx = pt - ty * TW;
+    const int part = thread_part(), co0 = part * CO;
+    const int H = a.H, W = a.W;
+    const Tile tl = block_tile(H, W, g);
+    const NeuronRegs nr = load_neuron(a.n, C, false);
+    const int h = tl.h0 + ty, w = tl.w0 + tx;
+    const bool in = h < H && w < W;
+    const int64_t q = (((int64_t)tl.b * H + (in ? h : 0)) * W + (in ? w : 0)) * 2 + part;
+    const float4 mv = (a.mem_prev && in) ? reinterpret_cast<const float4*>(a.mem_prev)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    stage_strided<CIN, NTB>(a.x, a.xs_b, a.xs_c, a.xs_h, a.xs_w, tl, H, W, lds);
+    lif_prologue(a.n, nr, nullptr, C, (double)a.B * H * W, nullptr, coef, nullptr, false);
+    __syncthreads();
+    float y[CO] = {0.f, 0.f, 0.f, 0.f};
+    conv_acc<CIN, C, CO>(lds, a.wt_ff, ty, tx, co0, y);
+    if (in)
+        eval_lif_store(make_float4(y[0], y[1], y[2], y[3]), mv, coef + co0, a.n.zero_reset != 0,
+                       reinterpret_cast<float4*>(a.state), q, (int64_t)a.B * H * W * 2);
+}
+
+template <bool REC>
+__device__ void eval8_pipe(const snnflow_eval_fwd_args& a, const Grid g, float* pool) {
+    constexpr int C = 8, NTB = 2 * NT, R = Halo4<C, NTB>::R;
+    using L = EvalLds<REC>;
+    char* const lds = reinterpret_cast<char*>(pool);
+    __shared__ LifCoef coef[C];
+    __shared__ int bad[2];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int H = a.H, W = a.W, ntiles = a.B * tiles_per_image(H, W);
+    int v_cur = g.bid < ntiles ? g.bid : -1;
+    if (v_cur < 0) return;
+    const bool has_mem = a.mem_prev != nullptr;
+    const bool has_rec = REC && a.s_prev != nullptr;
+    const bool pred = a.flow != nullptr;
+
+    // ---- prologue (once per block): neuron parameters (running statistics), fragments, first tile
+    const NeuronRegs nr = load_neuron(a.n, C, false);
+    FragC8 fz_ff, fz_rec;
+    fz_ff.load(a.wt_ff_t);
+    if (has_rec) fz_rec.load(a.wt_rec_t);
+    const uint32_t nbytes = (uint32_t)a.B * H * W * C * 4;  // < 2^31 (host check)
+    const __amdgpu_buffer_rsrc_t rs_s = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.s_in), (short)0, (int)nbytes, 0x00020000);
+    // the raw spike halo of tile t: 11 wave-loads of 64 x 16 B, wave w issues loads w, w + 8
+    auto issue = [&](const Tile& t, int lane) {
+        const int base = ((t.b * H + t.h0 - 1) * W + (t.w0 - 1)) * (C * 4);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = wv + 8 * j;
+            if (k >= 11) break;
+            const int ee = k * 64 + lane, p = ee >> 1, r = p / HWD, cc = p - r * HWD;
+            const bool ok = in_image(t.h0 + r - 1, t.w0 + cc - 1, H, W);
+            const uint32_t off = ok ? (uint32_t)(base + (r * W + cc) * (C * 4) + (ee & 1) * 16) : 0x80000000u;
+            if (ee < 2 * HN)  // the last wave-load is partial: inactive lanes write no LDS
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs_s, (lds_void*)(lds + L::RAW + k * 1024), 16, off, 0, 0, 0);
+        }
+    };
+    float4 rs[R];  // s_prev halo of the next tile (registers, issued one tile ahead)
+    auto load_sprev = [&](const Tile& t, int tid) {
+        const float4* base = reinterpret_cast<const float4*>(a.s_prev) + (((int64_t)t.b * H + (t.h0 - 1)) * W + (t.w0 - 1)) * 2;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = tid + i * NTB, p = e >> 1, r = p / HWD, cc = p - r * HWD;
+            const bool ok = e < 2 * HN && in_image(t.h0 + r - 1, t.w0 + cc - 1, H, W);
+            rs[i] = ok ? base[(r * W + cc) * 2 + (e & 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    Tile tl = block_tile(H, W, Grid{v_cur, ntiles});
+    issue(tl, lane);
+    if (has_rec) load_sprev(tl, tid);
+    lif_prologue(a.n, nr, nullptr, C, (double)a.B * H * W, nullptr, coef, nullptr, false);
+    fz_ff.store(reinterpret_cast<__bf16*>(lds + L::FF));
+    if (has_rec) fz_rec.store(reinterpret_cast<__bf16*>(lds + L::FR));
+    if (tid == 0) bad[0] = 0;
+
+    const bool zr = a.n.zero_reset != 0;
+    const int64_t plane4 = (int64_t)a.B * H * W * 2;
+    float4* st4 = reinterpret_cast<float4*>(a.state);
+    const float4* mem4 = reinterpret_cast<const float4*>(a.mem_prev);
+    const __bf16* spk = reinterpret_cast<const __bf16*>(lds + L::SPK);
+    const __bf16* rspk = reinterpret_cast<const __bf16*>(lds + L::RSPK);
+    const int64_t HWp = (int64_t)H * W;
+
+    for (int k = 0; v_cur >= 0; ++k) {
+        vm_wait<0>();     // this wave's DMA and s_prev loads of tile k (and its stores of tile k-1)
+        __syncthreads();  // every wave's DMA landed; every wave is done with the spike tiles of k-1
+        const int tid = opaque_int(threadIdx.x), lane = tid & 63, jj = lane & 15, gg = lane >> 4, qt = tid & 1;
+        // the spike halo as a bf16 tile (pixels outside the image: the DMA read zeros); s_prev likewise
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < 2 * HN) {
+                const int p = e >> 1;
+                const float4 sv = *reinterpret_cast<const float4*>(lds + L::RAW + e * 16);
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<bf16x4*>(const_cast<__bf16*>(spk) + p * 8 + 4 * qt) =
+                    bf16x4{(__bf16)sv.x, (__bf16)sv.y, (__bf16)sv.z, (__bf16)sv.w};
+                if (has_rec) {
+                    const float4 s = rs[i];
+                    ok = ok && exact_bf16(s.x) && exact_bf16(s.y) && exact_bf16(s.z) && exact_bf16(s.w);
+                    *reinterpret_cast<bf16x4*>(const_cast<__bf16*>(rspk) + p * 8 + 4 * qt) =
+                        bf16x4{(__bf16)s.x, (__bf16)s.y, (__bf16)s.z, (__bf16)s.w};
+                }
+            }
+        }
+        if (has_rec && __builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0) bad[k & 1] = 1;
+        if (threadIdx.x == 0) bad[(k + 1) & 1] = 0;
+        __syncthreads();
+        const bool rec_bf = has_rec && bad[k & 1] == 0;
+        const int v_nxt = v_cur + g.nb < ntiles ? v_cur + g.nb : -1;
+        const Tile cur = tl;
+        if (v_nxt >= 0) {
+            tl = block_tile(H, W, Grid{v_nxt, ntiles});
+            issue(tl, lane);
+            if (has_rec) load_sprev(tl, tid);
+        }
+        // this lane's output: row wv, column (lane >> 5) * 16 + jj, channel quad (lane >> 4) & 1
+        const int qd = (lane >> 4) & 1, h = cur.h0 + wv, w = cur.w0 + (lane >> 5) * 16 + jj;
+        const bool in = h < H && w < W;
+        const int64_t pix = ((int64_t)cur.b * H + (in ? h : 0)) * W + (in ? w : 0);
+        const float4 mv = (has_mem && in) ? mem4[pix * 2 + qd] : make_float4(0.f, 0.f, 0.f, 0.f);
+
+        const bf16x8* fff = reinterpret_cast<const bf16x8*>(lds + L::FF) + gg * 8 + (jj & 7);
+        const bf16x8* ffr = reinterpret_cast<const bf16x8*>(lds + L::FR) + gg * 8 + (jj & 7);
+        f32x4 af[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, ar[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const int tap = 4 * ch + gg, ky = tap / 3, kx = tap - 3 * ky;
+            const bf16x8 fh = fff[ch * 96], fm = fff[ch * 96 + 32], fl = fff[ch * 96 + 64];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int off = ((wv + ky) * HWD + mt * 16 + jj + kx) * 8;
+                bf16x8 b = {};
+                if (tap < 9) b = *reinterpret_cast<const bf16x8*>(spk + off);
+                af[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl, b, af[mt], 0, 0, 0);
+                af[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm, b, af[mt], 0, 0, 0);
+                af[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh, b, af[mt], 0, 0, 0);
+            }
+            if (rec_bf) {
+                const bf16x8 rh = ffr[ch * 96], rm = ffr[ch * 96 + 32], rl = ffr[ch * 96 + 64];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    const int off = ((wv + ky) * HWD + mt * 16 + jj + kx) * 8;
+                    bf16x8 b = {};
+                    if (tap < 9) b = *reinterpret_cast<const bf16x8*>(rspk + off);
+                    ar[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rl, b, ar[mt], 0, 0, 0);
+                    ar[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rm, b, ar[mt], 0, 0, 0);
+                    ar[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rh, b, ar[mt], 0, 0, 0);
+                }
+            }
+        }
+        f32x4 yv;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float y0 = rec_bf ? af[0][r] + ar[0][r] : af[0][r];  // ff + rec (:540)
+            const float y1 = rec_bf ? af[1][r] + ar[1][r] : af[1][r];
+            const auto sw = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, y0), __builtin_bit_cast(unsigned, y1),
+                                                             false, false);
+            yv[r] = __builtin_bit_cast(float, sw[0]);
+        }
+        if (has_rec && !rec_bf && in) {  // s_prev not binary: the recurrent conv on the vector ALU (exact f32)
+            const float* wr = a.wt_rec;  // [tap][ci][co]
+#pragma unroll 1
+            for (int tp = 0; tp < 9; ++tp) {
+                const int hh = h + tp / 3 - 1, ww = w + tp % 3 - 1;
+                if (!in_image(hh, ww, H, W)) continue;
+                const float* sp = a.s_prev + (((int64_t)cur.b * H + hh) * W + ww) * C;
+                for (int ci = 0; ci < C; ++ci) {
+                    const float s = sp[ci];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) yv[r] = fmaf(wr[(tp * C + ci) * C + 4 * qd + r], s, yv[r]);
+                }
+            }
+        }
+        // BatchNorm (running statistics) + LIF of this layer; state out
+        const LifCoef kc[4] = {coef[4 * qd], coef[4 * qd + 1], coef[4 * qd + 2], coef[4 * qd + 3]};
+        const Lif4 o = zr ? lif_step4(make_float4(yv[0], yv[1], yv[2], yv[3]), mv, kc, true)
+                          : lif_step4(make_float4(yv[0], yv[1], yv[2], yv[3]), mv, kc, false);
+        if (in) {
+            st_state4(st4, pix * 2 + qd, o.mout);
+            st_state4(st4, plane4 + pix * 2 + qd, o.s);
+        }
+        if (pred) {  // ConvLayer(C -> 2, 1x1) + tanh: the pixel's other channel quad from lane ^ 16,
+                     // summed in channel order as lif_fwd_body does; lane qd writes output qd
+            const float p0 = __shfl_xor(o.s.x, 16, 64), p1 = __shfl_xor(o.s.y, 16, 64);
+            const float p2 = __shfl_xor(o.s.z, 16, 64), p3 = __shfl_xor(o.s.w, 16, 64);
+            const float s8[8] = {qd ? p0 : o.s.x, qd ? p1 : o.s.y, qd ? p2 : o.s.z, qd ? p3 : o.s.w,
+                                 qd ? o.s.x : p0, qd ? o.s.y : p1, qd ? o.s.z : p2, qd ? o.s.w : p3};
+            if (in) {
+                const float* pw = a.pred_w + qd * C;
+                float acc = 0.0f;
+#pragma unroll
+                for (int c = 0; c < C; ++c) acc = fmaf(pw[c], s8[c], acc);
+                a.flow[((int64_t)cur.b * 2 + qd) * HWp + (int64_t)h * W + w] = tanhf(acc + a.pred_b[qd]);
+            }
+        }
+        v_cur = v_nxt;
+    }
+}
+
+__global__ __launch_bounds__(NT * 2, 6) void k_eval_slot(EvalSlotParams) {
+    typedef const __attribute__((address_space(4))) EvalSlotParams* cptr;
+    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+    const int bid = blockIdx.x, nt = pp->ntask;
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < kEvalTasks; ++i)
+        if (i < nt && bid >= pp->blk0[i]) k = i;
+    Grid g;
+    g.bid = bid - pp->blk0[k];
+    g.nb = pp->nblk[k];
+    if (g.bid >= g.nb) return;  // padding block of a range
+    __shared__ __attribute__((aligned(16))) float pool[kEvalLdsFloats];
+    const snnflow_eval_fwd_args a = task_args(&pp->t[k]);
+    switch (pp->kind[k]) {
+        case EK_HEAD2: eval_head_body<2>(a, g, pool); break;
+        case EK_HEAD4: eval_head_body<4>(a, g, pool); break;
+        case EK_FF: eval8_pipe<false>(a, g, pool); break;
+        case EK_REC: eval8_pipe<true>(a, g, pool); break;
         default: break;
     }
 }
@@ -4169,6 +4458,43 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
     return 0;
 }
 
+int snnflow_eval_slot(const snnflow_eval_fwd_args* tasks, int n, void* stream) {
+    if (!tasks || n <= 0 || n > kEvalTasks) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: task count");
+    EvalSlotParams p = {};
+    const int B = tasks[0].B, H = tasks[0].H, W = tasks[0].W;
+    for (int i = 0; i < n; ++i) {
+        const snnflow_eval_fwd_args& a = tasks[i];
+        if (a.c != 8) SNN_FAIL(SNNFLOW_E_CHANNELS, "eval_slot: c must be 8");
+        if (a.B != B || a.H != H || a.W != W || B <= 0 || H <= 0 || W <= 0)
+            SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: tasks of different or empty shapes");
+        if (a.n.bn_train) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: BatchNorm in train mode needs batch statistics (snnflow_fwd_slot)");
+        if (!a.state || !a.wt_ff || !a.n.bn_weight || !a.n.bn_bias || !a.n.running_mean || !a.n.running_var ||
+            !a.n.beta || !a.n.threshold)
+            SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: missing state, weights or neuron parameters");
+        if (a.flow && (!a.pred_w || !a.pred_b)) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: prediction without weights");
+        if (!pipe_fits(B, H, W, 8)) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: tensors of 2^31 bytes or more");
+        const int ntiles = snnflow_conv_blocks(B, H, W);
+        if (a.cin == a.c) {
+            if (!a.s_in || !a.wt_ff_t) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: spike input / fragment weights missing");
+            if (a.s_prev && (!a.wt_rec || !a.wt_rec_t)) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: recurrent weights missing");
+            p.kind[i] = a.s_prev ? EK_REC : EK_FF;
+            p.nblk[i] = pipe_blocks(ntiles, 2);
+        } else if (a.cin == 2 || a.cin == 4) {
+            if (!a.x || a.s_prev || a.flow) SNN_FAIL(SNNFLOW_E_ARG, "eval_slot: head task takes the event tensor only");
+            p.kind[i] = a.cin == 2 ? EK_HEAD2 : EK_HEAD4;
+            p.nblk[i] = ntiles;
+        } else {
+            SNN_FAIL(SNNFLOW_E_CHANNELS, "eval_slot: cin must be 2, 4 or c");
+        }
+        p.t[i] = a;
+    }
+    p.ntask = n;
+    const int nb = slot_ranges(p.nblk, n, p.blk0);
+    hipLaunchKernelGGL(k_eval_slot, dim3(nb), dim3(2 * NT), 0, (hipStream_t)stream, p);
+    SNN_CHECK_LAUNCH();
+    return 0;
+}
+
 int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnflow_lif_bwd_args* lif,
                      void* stream) {
     const int nt = nlayer + (lif ? 1 : 0);
@@ -4399,6 +4725,8 @@ int snnflow_clip_adam(const snnflow_clip_adam_args* a, void* stream) {
         const snnflow_adam_tensor& t = a->t[k];
         if (!t.param || t.offset < 0 || t.state_offset < 0 || t.numel < 0 || t.offset + t.numel > a->n)
             SNN_FAIL(SNNFLOW_E_ARG, "clip_adam: tensor range outside the flat buffer");
+        if (k > 0 && t.offset < a->t[k - 1].offset + a->t[k - 1].numel)
+            SNN_FAIL(SNNFLOW_E_ARG, "clip_adam: tensors must be in ascending, non-overlapping gradient order");
     }
     hipLaunchKernelGGL(k_clip_adam, dim3(1), dim3(CLIP_NT), 0, (hipStream_t)stream, *a);
     SNN_CHECK_LAUNCH();

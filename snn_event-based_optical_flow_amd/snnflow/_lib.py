@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 29
+ABI_VERSION = 30
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -40,6 +40,16 @@ class ConvFwdArgs(ctypes.Structure):
                 ("wt_ff", P), ("wt_rec", P), ("wt_ff_t", P), ("wt_rec_t", P), ("s_prev", P),
                 ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32),
                 ("wf_ff", P), ("wf_rec", P), ("tile_counter", P)]
+
+
+class EvalFwdArgs(ctypes.Structure):
+    _fields_ = [("B", I32), ("H", I32), ("W", I32), ("cin", I32), ("c", I32),
+                ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
+                ("s_in", P), ("mem_prev", P), ("s_prev", P), ("wt_ff", P), ("wt_rec", P), ("wt_ff_t", P),
+                ("wt_rec_t", P), ("n", Neuron), ("state", P), ("pred_w", P), ("pred_b", P), ("flow", P)]
+
+
+EVAL_MAX_TASKS = 8  # SNNFLOW_EVAL_MAX_TASKS
 
 
 class LifFwdArgs(ctypes.Structure):
@@ -298,6 +308,7 @@ EXPORTS = {
     "snnflow_clip_grad_norm": (I32, [P, I64, F32, F32, P, P]),
     "snnflow_clip_grad_norm_large": (I32, [P, I64, F32, F32, P, P, P]),
     "snnflow_clip_adam": (I32, [P, P]),
+    "snnflow_eval_slot": (I32, [P, I32, P]),
     "snnflow_count_nonzero": (I32, [P, P, I32, P, P]),
     "snnflow_fwd_slot": (I32, [ctypes.POINTER(ConvFwdArgs), I32, ctypes.POINTER(LifFwdArgs), P]),
     "snnflow_bwd_slot": (I32, [ctypes.POINTER(LayerBwdArgs), I32, ctypes.POINTER(LifBwdArgs), P]),

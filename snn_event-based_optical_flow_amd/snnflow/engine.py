@@ -1218,3 +1218,101 @@ class FireNetSequence(torch.autograd.Function):
             eng.last_flat = eng.flat
             eng.prep_stale = True
         return (None, None, *gxs, *g0, *pgrads)
+
+
+def eval_fused_ok(eng, x):
+    """True if forward_sequence may take the fused evaluation launches (eval_sequence): C = 8, every
+    BatchNorm on running statistics, no autograd needed, 2- or 4-bin input on the GPU, and not
+    disabled by SNNFLOW_EVAL_FUSED=0 (the train-path split launches then run in eval mode too)."""
+    import os
+    if os.environ.get("SNNFLOW_EVAL_FUSED", "1") == "0" or eng.C != 8 or not x.is_cuda or x.shape[1] not in (2, 4):
+        return False
+    if any(bn.training or not bn.track_running_stats for bn in eng.bns):
+        return False
+    return not (torch.is_grad_enabled() and any(p.requires_grad for p in eng.param_list()))
+
+
+def eval_sequence(eng, xs, prev):
+    """T steps of the network in evaluation mode (eval_flow.py:208-338 under torch.no_grad(),
+    BatchNorm on running statistics) through snnflow_eval_slot: task (l, t) = conv + BatchNorm + LIF
+    of layer l at step t (+ the prediction for the last layer) reads layer l-1's spikes at t and its
+    own state at t-1, so the T x L tasks run in T + L - 1 wavefront launches.  Same results as the
+    train-path kernels in eval mode (forward_sequence with SNNFLOW_EVAL_FUSED=0) up to the conv's
+    summation order.  Returns (flows [T], final states [L]); no autograd."""
+    L, C = eng.L, eng.C
+    T = len(xs)
+    B, cin0, H, W = xs[0].shape
+    dev = xs[0].device
+    for x in xs:
+        _lib.require_device(x, "event tensor")
+        if tuple(x.shape) != (B, cin0, H, W):
+            raise _lib.SnnflowError("forward_sequence: every step's input must have the same shape")
+    s = _lib.stream_ptr(dev)
+    wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale)
+    eng.prep_stale = False
+    neurons = eng.neurons()
+    n1 = 2 * B * H * W * C
+    fin = eng.final_state_out
+    eng.final_state_out = None
+    if fin is not None:
+        if (fin.device != dev or fin.dtype != torch.float32 or fin.numel() != L * n1 or not fin.is_contiguous()
+                or any(p is not None and p.untyped_storage().data_ptr() == fin.untyped_storage().data_ptr()
+                       for p in prev)):
+            raise _lib.SnnflowError("final_state_out: a contiguous fp32 buffer of L*2*B*H*W*C floats on the "
+                                    "input's device, not aliasing the initial states")
+        fin = fin.view(L * n1)
+    st_all = torch.empty(T - (fin is not None), L * n1, device=dev)
+    rows = _state_rows(st_all, fin, T)
+    sst = nhwc_state_strides(B, C, H, W)
+    states = [[rows[t][l * n1:(l + 1) * n1].as_strided((2, B, C, H, W), sst) for l in range(L)] for t in range(T)]
+    flows = [torch.empty(B, 2, H, W, device=dev) for _ in range(T)]
+    half = 4 * (n1 // 2)
+    keep, mem0, sp0 = [], [], []
+    for l in range(L):
+        p = prev[l]
+        if p is None:
+            cache = eng.lifs[l].mem
+            ok = cache is not None and tuple(cache.shape) == (B, C, H, W) and cache.device == dev
+            if ok and cache.stride() != (H * W * C, 1, W * C, C):
+                cache = cache.permute(0, 2, 3, 1).contiguous().permute(0, 3, 1, 2)
+            mem0.append(cache.data_ptr() if ok else None)
+            sp0.append(None)
+            keep.append(cache if ok else None)
+        else:
+            pn = as_nhwc_state(p.detach())
+            mem0.append(pn.data_ptr())
+            sp0.append(pn.data_ptr() + half if eng.rec[l] else None)
+            keep.append(pn)
+    base = [r.data_ptr() for r in rows]
+
+    def targs(l, t):
+        a = _lib.EvalFwdArgs()
+        a.B, a.H, a.W, a.c = B, H, W, C
+        if l == 0:
+            x = xs[t]
+            a.cin, a.x = cin0, x.data_ptr()
+            a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(x)
+        else:
+            a.cin, a.s_in = C, base[t] + 4 * (l - 1) * n1 + half
+        a.mem_prev = mem0[l] if t == 0 else base[t - 1] + 4 * l * n1
+        if eng.rec[l]:
+            a.s_prev = sp0[l] if t == 0 else base[t - 1] + 4 * l * n1 + half
+        a.wt_ff, a.wt_rec = ptr(wfwd[l][0]), _ptr_t(wfwd[l][1])
+        a.wt_ff_t, a.wt_rec_t = ptr(wbwd[l][0]), _ptr_t(wbwd[l][1])
+        a.n = neurons[l]
+        a.state = base[t] + 4 * l * n1
+        if l == L - 1:
+            a.pred_w, a.pred_b, a.flow = ptr(eng.pred.weight), ptr(eng.pred.bias), flows[t].data_ptr()
+        return a
+
+    for d in range(T + L - 1):  # wavefront: task (l, t) in launch l + t
+        tasks = [(l, d - l) for l in range(L) if 0 <= d - l < T]
+        for i0 in range(0, len(tasks), _lib.EVAL_MAX_TASKS):
+            chunk = [targs(l, t) for l, t in tasks[i0:i0 + _lib.EVAL_MAX_TASKS]]
+            _lib.call("eval_slot", lib.snnflow_eval_slot, (_lib.EvalFwdArgs * len(chunk))(*chunk), len(chunk), s)
+    _lib.timer_close()
+    del keep  # (the initial states are read by the launches above: stream-ordered)
+    for l in range(L):
+        eng.cells[l].lif.mem = states[T - 1][l][0]
+    eng.seq_states = [list(sts) for sts in states] if eng.keep_seq_states else None
+    return flows, states[T - 1]

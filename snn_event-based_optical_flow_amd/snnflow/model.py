@@ -18,7 +18,7 @@ import torch.nn as nn
 
 from . import _lib
 from .cells import ConvLayer, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
-from .engine import FireNetEngine, FireNetSequence, FireNetStep
+from .engine import FireNetEngine, FireNetSequence, FireNetStep, eval_fused_ok, eval_sequence
 
 
 class BaseModel(nn.Module):
@@ -176,9 +176,12 @@ class _FireNetBase(BaseModel):
         """T consecutive time steps in one call (not in the reference; its training loop calls
         ``forward`` once per window, ``train_flow.py:232-279``).  Same results, states and
         ``lif.mem`` caches as T ``forward`` calls -- returns their T result dicts -- with the
-        steps' kernels issued as wavefront launches (engine.FireNetSequence).  With ``log`` the T
-        activity dicts come from one count launch per 16 tensors and one read-back.  Falls back to
-        T ``forward`` calls where those launches do not apply (hooks, TEBN/MPBN, C = 4)."""
+        steps' kernels issued as wavefront launches (engine.FireNetSequence).  In eval mode without
+        autograd (eval_flow.py's loop under torch.no_grad()) at C = 8 the fused evaluation launches
+        run instead (engine.eval_sequence: conv + BatchNorm + LIF per task, T + L - 1 launches).  With
+        ``log`` the T activity dicts come from one count launch per 16 tensors and one read-back.
+        Falls back to T ``forward`` calls where those launches do not apply (hooks, TEBN/MPBN,
+        C = 4)."""
         seq = event_voxels if self.encoding == "voxel" else event_cnts
         T = len(seq)
         none = [None] * T
@@ -195,7 +198,11 @@ class _FireNetBase(BaseModel):
         logging = isinstance(log, bool) and log and not self.exporting
         eng.keep_seq_states = logging or eng.capture_states
         try:
-            res = FireNetSequence.apply(eng, T, *xs, *self._states, *eng.param_list())
+            if eval_fused_ok(eng, xs[0]):  # eval mode, no autograd: conv + BN + LIF fused per task
+                flows, fin = eval_sequence(eng, xs, list(self._states))
+                res = list(flows) + list(fin)
+            else:
+                res = FireNetSequence.apply(eng, T, *xs, *self._states, *eng.param_list())
         finally:
             eng.keep_seq_states = False
         self._states = list(res[T:])

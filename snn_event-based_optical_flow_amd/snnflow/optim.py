@@ -96,8 +96,9 @@ class ClipAdam(torch.optim.Optimizer):
         a.max_norm, a.clip_eps = (float(mn) if mn is not None else 0.0), float(group["clip_eps"])
         a.ntensors = len(params)
         base = grad.data_ptr()
-        for i, (p, o) in enumerate(zip(params, offs)):
-            t = a.t[i]
-            t.param, t.offset, t.state_offset, t.numel = p.data_ptr(), (p.grad.data_ptr() - base) // 4, o, p.numel()
+        order = sorted(range(len(params)), key=lambda k: params[k].grad.data_ptr())  # gradient order
+        for i, k in enumerate(order):
+            p, t = params[k], a.t[i]
+            t.param, t.offset, t.state_offset, t.numel = p.data_ptr(), (p.grad.data_ptr() - base) // 4, offs[k], p.numel()
         _lib.call("clip_adam", _lib.lib.snnflow_clip_adam, ctypes.byref(a), _lib.stream_ptr(grad.device))
         return loss

@@ -41,6 +41,7 @@ def test_struct_layouts_match_c(tmp_path):
         "snnflow_convlif_fwd_args": _lib.ConvLifFwdArgs, "snnflow_convlif_bwd_args": _lib.ConvLifBwdArgs, "snnflow_wgrad_args": _lib.WgradArgs, "snnflow_iwe_loss_args": _lib.IweLossArgs,
         "snnflow_flow_metrics_args": _lib.FlowMetricsArgs,
         "snnflow_adam_tensor": _lib.AdamTensor, "snnflow_clip_adam_args": _lib.ClipAdamArgs,
+        "snnflow_eval_fwd_args": _lib.EvalFwdArgs,
         "snnflow_unet_seg": _lib.UNetSeg, "snnflow_unet_conv_args": _lib.UNetConvArgs,
         "snnflow_unet_wgrad_args": _lib.UNetWgradArgs, "snnflow_unet_lif_bwd_args": _lib.UNetLifBwdArgs,
         "snnflow_bn_fwd_args": _lib.BnFwdArgs, "snnflow_bn_bwd_args": _lib.BnBwdArgs,
@@ -103,6 +104,12 @@ def test_argument_validation_without_gpu():
     ca.t[0].param, ca.t[0].offset, ca.t[0].numel = 1, 8, 9             # range past n
     assert lib.snnflow_clip_adam(ctypes.byref(ca), None) == -1
     assert b"clip_adam" in lib.snnflow_last_error()
+    ev = (_lib.EvalFwdArgs * 1)()
+    assert lib.snnflow_eval_slot(ev, 0, None) == -1                    # no task
+    ev[0].B, ev[0].H, ev[0].W, ev[0].c, ev[0].cin = 1, 8, 8, 8, 8
+    ev[0].n.bn_train = 1
+    assert lib.snnflow_eval_slot(ev, 1, None) == -1                    # train-mode BatchNorm refused
+    assert b"eval_slot" in lib.snnflow_last_error()
 
 
 def test_product_path_refuses_cpu_tensors():

@@ -1532,3 +1532,86 @@ def test_iwe_loss_bit_reproducible(dev):
     for ev, pol, mask, flow in wins:
         rl.event_flow_association([flow], ev, pol, mask)
     np.testing.assert_allclose(losses[0], rl().item(), rtol=1e-5)
+
+
+def _eval_model(C=8, seed=0):
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(seed)
+    m = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=C))
+    g = torch.Generator().manual_seed(seed + 3)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.modules.batchnorm._BatchNorm):
+            mod.running_mean.copy_(0.2 * torch.randn(mod.running_mean.shape, generator=g))
+            mod.running_var.copy_(0.5 + torch.rand(mod.running_var.shape, generator=g))
+    return m
+
+
+@pytest.mark.parametrize("B,H,W,T", [(2, 40, 72, 4), (8, 128, 128, 10)])
+def test_eval_fused_matches_split(dev, monkeypatch, B, H, W, T):
+    """The fused evaluation launches (engine.eval_sequence: conv + BN + LIF per task, T + L - 1
+    launches) against the train-path split launches in eval mode (SNNFLOW_EVAL_FUSED=0), two chained
+    calls (states carried), on a ragged shape (tiles past the image edge) and at cfg2's size: flows
+    within 1e-5, spikes identical except where the membrane lies within 1e-4 of the threshold,
+    membranes within 1e-5; the final states and every lif.mem cache likewise."""
+    import copy
+
+    from snnflow.synthetic import make_window
+
+    ma = _eval_model().to(dev).eval()
+    mb = copy.deepcopy(ma)
+    ma.engine.capture_states = mb.engine.capture_states = True
+    gen = torch.Generator(device=dev).manual_seed(9)
+    wins = [make_window(B, 600, H, W, gen, dev) for _ in range(2 * T)]
+    out = {}
+    for tag, m, fused in (("split", ma, "0"), ("fused", mb, "1")):
+        monkeypatch.setenv("SNNFLOW_EVAL_FUSED", fused)
+        flows, sts = [], []
+        with torch.no_grad():
+            for k in range(2):
+                o = m.forward_sequence(None, [w["event_cnt"] for w in wins[k * T:(k + 1) * T]])
+                flows += [x["flow"][0].cpu() for x in o]
+                sts += [[s.cpu() for s in st] for st in m.engine.seq_states]
+        out[tag] = (flows, sts, [s.cpu() for s in m._states], [c.lif.mem.cpu() for c in m.engine.cells])
+    worst = max(float((a - b).abs().max()) for a, b in zip(out["split"][0], out["fused"][0]))
+    flips = 0
+    for sa, sb in zip(out["split"][1], out["fused"][1]):
+        for a, b in zip(sa, sb):
+            d = (a[1] != b[1])
+            flips += int(d.sum())
+            assert float((a[0] - b[0]).abs()[~d].max()) <= 1e-5
+    print(f"\n[eval fused {B}x{H}x{W} T={T}] max|dflow| {worst:.2e}, spike flips {flips}")
+    assert worst <= 1e-5 or flips > 0
+    assert flips <= 4
+    for a, b in zip(out["split"][2] + out["split"][3], out["fused"][2] + out["fused"][3]):
+        assert float((a - b).abs().max()) <= 1e-5 or flips > 0
+
+
+def test_eval_fused_nonbinary_state_and_final_out(dev, monkeypatch):
+    """Initial states with non-binary spike halves (the recurrent conv's vector-ALU fallback) and
+    FireNetEngine.final_state_out on the fused evaluation path, against the split launches."""
+    import copy
+
+    ma = _eval_model(seed=2).to(dev).eval()
+    mb = copy.deepcopy(ma)
+    B, H, W, T, C = 2, 24, 40, 3, 8
+    gen = torch.Generator(device=dev).manual_seed(5)
+    xs = [(torch.rand(B, 2, H, W, generator=gen, device=dev) < 0.2).float() * 2 for _ in range(T)]
+    st0 = [torch.rand(2, B, C, H, W, generator=gen, device=dev) * 0.7 for _ in range(7)]
+    n = mb.engine.L * 2 * B * C * H * W
+    fin = torch.full((n,), float("nan"), device=dev)
+    res = {}
+    for tag, m, fused in (("split", ma, "0"), ("fused", mb, "1")):
+        monkeypatch.setenv("SNNFLOW_EVAL_FUSED", fused)
+        m.states = [s.clone() for s in st0]
+        if fused == "1":
+            m.engine.final_state_out = fin
+        with torch.no_grad():
+            o = m.forward_sequence(None, xs)
+        res[tag] = ([x["flow"][0].cpu() for x in o], [s.cpu() for s in m._states])
+    if True:
+        base = fin.data_ptr()
+        assert all(base <= s.data_ptr() < base + 4 * n for s in mb._states)
+    for a, b in zip(res["split"][0] + res["split"][1], res["fused"][0] + res["fused"][1]):
+        assert float((a - b).abs().max()) <= 1e-5
