@@ -458,8 +458,9 @@ def eval_main(args, world, rank, dev, backend):
     step = T windows of B sequences: model.eval() forward (BatchNorm on running statistics, no
     autograd; forward_sequence's wavefront launches), then per window the rounded per-polarity IWE
     (compute_pol_iwe, eval_flow.py:227-235) and AEE against a synthetic ground-truth flow
-    (loss/flow.py:597-649), the per-sample AEE / outlier percentage accumulated on the device (the
-    reference moves them to the host per window for its result table).  Visualisation is not part
+    (loss/flow.py:597-649), the per-sample AEE / outlier percentage left on the device (the
+    reference moves them to the host per window for its result table; the line reports the last
+    pass's mean).  Visualisation is not part
     of the step.  HIP graphs as the train bench: one per resident batch, the state hand-over inside.
     A second, smaller measurement covers configs[0] of BASELINE.json (T=5, B=1, forward only) on
     the GPU and with the CPU oracle."""
@@ -486,7 +487,7 @@ def eval_main(args, world, rank, dev, backend):
     one = torch.ones(1, device=dev)
     metric = snnflow.AEE({"loader": {"resolution": [R, R]}, "loss": {"overwrite_intermediate": False}}, dev,
                          flow_scaling=128)
-    acc = torch.zeros(2, B, dtype=torch.float64, device=dev)  # sum over windows of AEE, outlier %
+    last = {}  # the last pass's per-window AEE / outlier % (device tensors; read after timing)
 
     pingpong = []  # set after the warm-up: graph replays hand the states over copy-free
 
@@ -505,10 +506,8 @@ def eval_main(args, world, rank, dev, backend):
             metric.event_flow_association(outs[t]["flow"], {"event_list": w["event_list"], "event_list_pol_mask": pol,
                                                             "event_mask": w["event_mask"], "gtflow": gt[t],
                                                             "dt_input": one, "dt_gt": one})
-            aee, pct = metric()
+            last[t] = metric()
             metric.reset()
-            acc[0].add_(aee)
-            acc[1].add_(pct)
         if not pingpong:
             handover()
 
@@ -517,8 +516,8 @@ def eval_main(args, world, rank, dev, backend):
             pingpong.append(StatePingPong(dev, model._states))
         pingpong[0].arm(model, j)
 
-    graphs, elapsed = _timed_passes(args, dev, world, eval_pass, reset=acc.zero_, arm=arm)
-    aee_mean = (acc[0] / (args.steps * T)).tolist()
+    graphs, elapsed = _timed_passes(args, dev, world, eval_pass, arm=arm)
+    aee_mean = (torch.stack([last[t][0] for t in range(T)]).mean(0)).tolist()  # the last timed pass
     events_per_step = world * B * T * N
     value = events_per_step * args.steps / elapsed
 
@@ -573,7 +572,7 @@ def eval_main(args, world, rank, dev, backend):
                                    "rounded per-polarity IWE + AEE per window",
                        "global_batch": B * world, "parallelism": f"dp{world}" if world > 1 else "none",
                        "collective": backend, "hip_graph": not args.no_graph, "launch_order": "wavefront"},
-            "aee_mean_per_sample": [round(v, 6) for v in aee_mean],
+            "aee_last_pass_mean_per_sample": [round(v, 6) for v in aee_mean],
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu, "configs0": cfg1,
         }
         print(json.dumps(line), flush=True)

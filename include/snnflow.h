@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 30
+#define SNNFLOW_ABI_VERSION 31
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -434,12 +434,15 @@ typedef struct snnflow_aee_args {
     const float* flow;          /* [B][2][H][W] network flow (before scaling) */
     const float* gtflow;        /* [B][2][H][W] */
     const float* event_mask;    /* [B][H][W] event mask of the last window */
-    const float* dt_ratio;      /* [B] dt_gt / dt_input */
+    const float* dt_ratio;      /* [B] dt_gt / dt_input, or NULL: the ratio of dt_gt / dt_input below */
     float flow_scaling;
     double* acc;                /* ABI 29: scratch of snnflow_aee_acc_doubles(B, H, W) doubles; acc[0] (a
                                  * completion counter) must be zero before the first call on it and every
                                  * call leaves it zero -- allocate zeroed once and reuse */
     float* aee; float* percent; /* out [B] */
+    /* ABI 31 (dt_ratio NULL): dt_gt[b] / dt_input[b] formed in the kernel, each of dt_gt_n / dt_input_n
+     * (1: one value for the batch, or B) entries -- no separate division launch per window */
+    const float* dt_gt; const float* dt_input; int dt_gt_n, dt_input_n;
 } snnflow_aee_args;
 /* One launch: per-block partial sums (fp64 rows), the last block to finish reduces them in a fixed
  * order (deterministic) and writes aee / percent. */

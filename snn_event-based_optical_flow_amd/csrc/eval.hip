@@ -59,13 +59,73 @@ __global__ __launch_bounds__(NT) void k_pol_iwe(const float* __restrict__ events
     }
 }
 
+// Banded form (snnflow_pol_iwe): one block per (sample, band of POLB_BAND pixels) holds the band's
+// nimg images in LDS, scans the sample's events, adds the contributions that land in the band with
+// LDS atomics, and writes the whole band once -- no memset launch, no global atomics.  Rounded
+// warps with 0/1 masks add exact integers (order-free); bilinear weights add in LDS-atomic order,
+// as the global atomics of k_pol_iwe did.
+constexpr int POLB_NT = 1024, POLB_BAND = 4096;  // ~1 event per thread at 1000-event windows: one load chain
+
+__global__ __launch_bounds__(POLB_NT) void k_pol_iwe_band(const float* __restrict__ events, const float* __restrict__ flow,
+                                                         const float* __restrict__ pol, int64_t pol_stride, int nimg,
+                                                         int N, int H, int W, float tref, float s, int round_idx,
+                                                         int nbands, float* out) {
+    __shared__ float img[2][POLB_BAND];
+    const int tid = threadIdx.x, band = blockIdx.x % nbands, b = blockIdx.x / nbands;
+    const int64_t HWp = (int64_t)H * W;
+    const int p0 = band * POLB_BAND;
+    const int np = (int)(HWp - p0 < POLB_BAND ? HWp - p0 : POLB_BAND);
+    for (int j = tid; j < 2 * POLB_BAND; j += POLB_NT) (&img[0][0])[j] = 0.0f;
+    __syncthreads();
+    const float* fl = flow + (int64_t)b * 2 * HWp;
+    for (int i = tid; i < N; i += POLB_NT) {
+        const int64_t e = (int64_t)b * N + i;
+        const float* ev = events + e * 4;  // (event views need not be 16-B aligned)
+        const float ts = ev[0], y = ev[1], x = ev[2];
+        const int64_t fpix = (int64_t)(y * (float)W + x);  // deblur_events: flow_idx.long()
+        const float fy = fl[HWp + fpix], fx = fl[fpix];
+        float m[2] = {1.0f, 1.0f};
+        if (pol)
+            for (int k = 0; k < nimg; ++k) m[k] = pol[e * pol_stride + k];
+        if (round_idx) {
+            const float dt = tref - ts;
+            const float wy = y + (dt * fy) * s, wx = x + (dt * fx) * s;
+            const float cy = rintf(wy), cx = rintf(wx);  // torch.round: half to even
+            const bool inb = cy >= 0.0f && cy < (float)H && cx >= 0.0f && cx < (float)W;
+            const float mk = inb ? 1.0f : 0.0f;
+            const int li = (int)((cy * mk) * (float)W + cx * mk) - p0;
+            if (li >= 0 && li < np)
+                for (int k = 0; k < nimg; ++k) {
+                    const float v = mk * m[k];
+                    if (v != 0.0f) atomicAdd(&img[k][li], v);
+                }
+        } else {
+            Corner c[4];
+            float wy, wx;
+            warp4(ts, y, x, fy, fx, tref, s, H, W, c, wy, wx);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int li = c[q].idx - p0;
+                if (li < 0 || li >= np) continue;
+                for (int k = 0; k < nimg; ++k) {
+                    const float v = c[q].wt * m[k];
+                    if (v != 0.0f) atomicAdd(&img[k][li], v);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    for (int k = 0; k < nimg; ++k)
+        for (int j = tid; j < np; j += POLB_NT) out[((int64_t)b * nimg + k) * HWp + p0 + j] = img[k][j];
+}
+
 // AEE in one launch.  Per pixel: endpoint error, validity, outlier; per (sample, slice of
 // AEE_NT * AEE_PPT pixels) block one fp64 row {sum err, sum valid, outliers} at acc[1 + 3 blk]; the
 // last block to finish (completion counter acc[0]) sums every sample's rows in slice order, writes
 // aee / percent (the outliers counted over the whole batch, loss/flow.py:647) and resets the
 // counter: deterministic, no zero / finalize launches.  Few large blocks: each block's release
 // fence writes its XCD's L2 back, so the block count is kept near one per sample.
-constexpr int AEE_NT = 1024, AEE_PPT = 16;
+constexpr int AEE_NT = 1024, AEE_PPT = 4;
 
 __host__ __device__ inline int aee_slices(int64_t HWp) {
     return (int)((HWp + (int64_t)AEE_NT * AEE_PPT - 1) / ((int64_t)AEE_NT * AEE_PPT));
@@ -77,21 +137,32 @@ __global__ __launch_bounds__(AEE_NT) void k_aee(snnflow_aee_args a, int slices) 
     __shared__ int last;
     const int tid = threadIdx.x, b = blockIdx.x / slices, sl = blockIdx.x - b * slices;
     const int64_t HWp = (int64_t)a.H * a.W;
-    const int64_t p0 = (int64_t)sl * AEE_NT * AEE_PPT;
-    const int64_t p1 = p0 + (int64_t)AEE_NT * AEE_PPT < HWp ? p0 + (int64_t)AEE_NT * AEE_PPT : HWp;
-    const float r = a.dt_ratio[b];
+    const int64_t p0 = (int64_t)sl * AEE_NT * AEE_PPT + tid;
+    const float r = a.dt_ratio ? a.dt_ratio[b] : a.dt_gt[a.dt_gt_n == 1 ? 0 : b] / a.dt_input[a.dt_input_n == 1 ? 0 : b];
     const float* f = a.flow + (int64_t)b * 2 * HWp;
     const float* g = a.gtflow + (int64_t)b * 2 * HWp;
     const float* em = a.event_mask + (int64_t)b * HWp;
+    // every load of the thread's AEE_PPT pixels first (one memory latency), then the math
+    float fx_[AEE_PPT], fy_[AEE_PPT], gx_[AEE_PPT], gy_[AEE_PPT], m_[AEE_PPT];
+#pragma unroll
+    for (int u = 0; u < AEE_PPT; ++u) {
+        const int64_t p = p0 + (int64_t)u * AEE_NT;
+        const bool ok = p < HWp;
+        fx_[u] = ok ? f[p] : 0.0f;
+        fy_[u] = ok ? f[HWp + p] : 0.0f;
+        gx_[u] = ok ? g[p] : 0.0f;
+        gy_[u] = ok ? g[HWp + p] : 0.0f;
+        m_[u] = ok ? em[p] : 0.0f;
+    }
     float err = 0.0f, val = 0.0f, out = 0.0f;
-#pragma unroll 4
-    for (int64_t p = p0 + tid; p < p1; p += AEE_NT) {
-        const float fx = (f[p] * a.flow_scaling) * r, fy = (f[HWp + p] * a.flow_scaling) * r;
-        const float gx = g[p], gy = g[HWp + p];
+#pragma unroll
+    for (int u = 0; u < AEE_PPT; ++u) {
+        const float fx = (fx_[u] * a.flow_scaling) * r, fy = (fy_[u] * a.flow_scaling) * r;
+        const float gx = gx_[u], gy = gy_[u];
         const float mag = sqrtf(fx * fx + fy * fy);
         const float dx = fx - gx, dy = fy - gy;
         const float e = sqrtf(dx * dx + dy * dy);
-        const bool valid = em[p] != 0.0f && !(gx == 0.0f && gy == 0.0f);
+        const bool valid = m_[u] != 0.0f && !(gx == 0.0f && gy == 0.0f);  // (m_ = 0 past the image)
         const float mk = valid ? 1.0f : 0.0f;
         const float ae = e * mk;
         err += ae;
@@ -112,20 +183,24 @@ __global__ __launch_bounds__(AEE_NT) void k_aee(snnflow_aee_args a, int slices) 
         red[tid >> 6][2] = s2;
     }
     __syncthreads();
-    if (tid < 3) {
-        double t = 0.0;
-        for (int w = 0; w < AEE_NT / 64; ++w) t += red[w][tid];
-        a.acc[1 + 3 * (int64_t)blockIdx.x + tid] = t;
-    }
-    __threadfence();  // the row is visible device-wide before the block counts as done
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned long long done = atomicAdd(reinterpret_cast<unsigned long long*>(a.acc), 1ull);
-        last = done == (unsigned long long)gridDim.x - 1;
+    // wave 0 writes the block's row, fences it device-wide (one wave per block: a fence is an L2
+    // write-back + invalidate, and every wave of every block fencing cost ~15 us here), then counts
+    // the block as done; the last block's wave 0 fences again (acquire) before the rows are read
+    if (tid < 64) {
+        if (tid < 3) {
+            double t = 0.0;
+            for (int w = 0; w < AEE_NT / 64; ++w) t += red[w][tid];
+            a.acc[1 + 3 * (int64_t)blockIdx.x + tid] = t;
+        }
+        __threadfence();
+        if (tid == 0) {
+            const unsigned long long done = atomicAdd(reinterpret_cast<unsigned long long*>(a.acc), 1ull);
+            last = done == (unsigned long long)gridDim.x - 1;
+            if (last) __threadfence();
+        }
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();
     if (tid < a.B) {
         double e = 0.0, v = 0.0, o = 0.0;
         const double* rr = a.acc + 1 + 3 * (int64_t)tid * slices;
@@ -280,6 +355,13 @@ int snnflow_pol_iwe(const float* events, const float* flow, const float* pol, in
         (nimg == 2 && !pol))
         SNN_FAIL(SNNFLOW_E_ARG, "pol_iwe: bad args");
     const hipStream_t s = (hipStream_t)stream;
+    const int64_t HWp = (int64_t)H * W, nbands = (HWp + POLB_BAND - 1) / POLB_BAND;
+    if ((int64_t)B * nbands <= 65535 * 64 && N <= 65536) {  // banded: every block scans its sample's events
+        hipLaunchKernelGGL(k_pol_iwe_band, dim3((unsigned)(B * nbands)), dim3(POLB_NT), 0, s, events, flow, pol, pol_stride,
+                           nimg, N, H, W, tref, flow_scaling, round_idx, (int)nbands, out);
+        SNN_CHECK_LAUNCH();
+        return 0;
+    }
     hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * (size_t)B * nimg * H * W, s);
     if (e != hipSuccess) SNN_FAIL((int)e, hipGetErrorString(e));
     const int64_t n = (int64_t)B * N;
@@ -294,8 +376,11 @@ int snnflow_pol_iwe(const float* events, const float* flow, const float* pol, in
 
 int snnflow_aee(const snnflow_aee_args* a, void* stream) {
     if (!a || a->B <= 0 || a->B > AEE_NT || a->H <= 0 || a->W <= 0 || !a->flow || !a->gtflow || !a->event_mask ||
-        !a->dt_ratio || !a->acc || !a->aee || !a->percent)
+        !a->acc || !a->aee || !a->percent)
         SNN_FAIL(SNNFLOW_E_ARG, "aee: bad args");
+    if (!a->dt_ratio && (!a->dt_gt || !a->dt_input || (a->dt_gt_n != 1 && a->dt_gt_n != a->B) ||
+                         (a->dt_input_n != 1 && a->dt_input_n != a->B)))
+        SNN_FAIL(SNNFLOW_E_ARG, "aee: dt_ratio, or dt_gt / dt_input of 1 or B entries");
     const hipStream_t s = (hipStream_t)stream;
     const int slices = aee_slices((int64_t)a->H * a->W);
     hipLaunchKernelGGL(k_aee, dim3(a->B * slices), dim3(AEE_NT), 0, s, *a, slices);

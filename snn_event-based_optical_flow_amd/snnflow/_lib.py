@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 30
+ABI_VERSION = 31
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -126,7 +126,8 @@ class EncodeArgs(ctypes.Structure):
 
 class AeeArgs(ctypes.Structure):
     _fields_ = [("B", I32), ("H", I32), ("W", I32), ("flow", P), ("gtflow", P), ("event_mask", P),
-                ("dt_ratio", P), ("flow_scaling", F32), ("acc", P), ("aee", P), ("percent", P)]
+                ("dt_ratio", P), ("flow_scaling", F32), ("acc", P), ("aee", P), ("percent", P),
+                ("dt_gt", P), ("dt_input", P), ("dt_gt_n", I32), ("dt_input_n", I32)]
 
 
 class FlowMetricsArgs(ctypes.Structure):

@@ -116,8 +116,14 @@ def _pol_iwe(flow, event_list, res, masks, flow_scaling, round_idx, tref=1.0):
         raise ValueError("flow map and resolution disagree")
     pol, stride, nimg = None, 0, 1
     if masks is not None:
-        pol = torch.cat([m.reshape(B, N, 1).float() for m in masks], dim=2).contiguous()
-        stride, nimg = pol.shape[2], pol.shape[2]
+        m0 = masks[0]
+        if (len(masks) == 2 and all(m.dtype == torch.float32 and m.device == ev.device and tuple(m.shape) == (B, N, 1)
+                                    and m.stride()[:2] == (2 * N, 2) for m in masks)
+                and masks[1].data_ptr() == m0.data_ptr() + 4):
+            pol, stride, nimg = m0, 2, 2  # the two columns of one [B][N][2] mask tensor: read in place
+        else:
+            pol = torch.cat([m.reshape(B, N, 1).float() for m in masks], dim=2).contiguous()
+            stride, nimg = pol.shape[2], pol.shape[2]
     out = torch.empty(B, nimg, H, W, device=ev.device)
     check(lib.snnflow_pol_iwe(ptr(ev), ptr(fl), ptr(pol), stride, nimg, B, N, H, W, float(tref), float(flow_scaling),
                               int(bool(round_idx)), ptr(out), _lib.stream_ptr(ev.device)), "pol_iwe")

@@ -101,9 +101,9 @@ class AEE(BaseValidationLoss):
         B, _, H, W = flow.shape
         gt = self._gtflow.float().contiguous()
         mask = self._event_mask[:, -1, :, :].float().contiguous()
-        ratio = torch.as_tensor(self._dt_gt, dtype=torch.float32, device=flow.device) / torch.as_tensor(
-            self._dt_input, dtype=torch.float32, device=flow.device)
-        ratio = ratio.reshape(-1).expand(B).contiguous() if ratio.numel() == 1 else ratio.reshape(B).contiguous()
+        # dt_gt / dt_input (one value for the batch, or B) divided in the kernel
+        dtg = torch.as_tensor(self._dt_gt, dtype=torch.float32, device=flow.device).reshape(-1).contiguous()
+        dti = torch.as_tensor(self._dt_input, dtype=torch.float32, device=flow.device).reshape(-1).contiguous()
         n = lib.snnflow_aee_acc_doubles(B, H, W)
         acc = self.__dict__.get("_aee_acc")
         if acc is None or acc.numel() < n or acc.device != flow.device:
@@ -113,7 +113,8 @@ class AEE(BaseValidationLoss):
         pct = torch.empty(B, device=flow.device)
         a = _lib.AeeArgs()
         a.B, a.H, a.W = B, H, W
-        a.flow, a.gtflow, a.event_mask, a.dt_ratio = ptr(flow), ptr(gt), ptr(mask), ptr(ratio)
+        a.flow, a.gtflow, a.event_mask, a.dt_ratio = ptr(flow), ptr(gt), ptr(mask), None
+        a.dt_gt, a.dt_input, a.dt_gt_n, a.dt_input_n = ptr(dtg), ptr(dti), dtg.numel(), dti.numel()
         a.flow_scaling = float(self.flow_scaling)
         a.acc, a.aee, a.percent = ptr(acc), ptr(aee), ptr(pct)
         _lib.call("aee", lib.snnflow_aee, ctypes.byref(a), _lib.stream_ptr(flow.device))
