@@ -33,6 +33,11 @@ def main(C=8, R=128, B=8, T=10, steps=3):
         opt.step()
         opt.zero_grad()
         model.detach_states()
+    # evaluation passes (model.eval() under no_grad: the fused eval_slot launches at C = 8)
+    model.eval()
+    with torch.no_grad():
+        for _ in range(2):
+            model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
     torch.cuda.synchronize()
 
 
