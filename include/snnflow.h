@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 31
+#define SNNFLOW_ABI_VERSION 32
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -543,9 +543,13 @@ int snnflow_eval_slot(const snnflow_eval_fwd_args* tasks, int n, void* stream);
  * sqrt(bc2) + eps, param -= lr / bc1 * exp_avg / denom).  t[i] maps parameter tensor i to
  * grad[offset .. offset + numel) and to exp_avg / exp_avg_sq[state_offset .. state_offset + numel)
  * (persistent moment buffers: the gradient buffer may move between steps, the moments do not); the
- * t[] in ascending, non-overlapping gradient order.  One block: n <= SNNFLOW_CLIP_ADAM_MAX_N.  Replaces snnflow_clip_grad_norm + torch's Adam kernels. */
+ * t[] in ascending, non-overlapping gradient order.  n <= SNNFLOW_CLIP_ADAM_MAX_N; up to
+ * SNNFLOW_CLIP_ADAM_ONE_BLOCK elements one launch of one block, above that (ABI 32) two launches of
+ * one block per SNNFLOW_CLIP_ADAM_ONE_BLOCK elements (per-block norm partials in `scratch`,
+ * SNNFLOW_CLIP_SCRATCH doubles, summed by every block in the same order: deterministic).  Replaces snnflow_clip_grad_norm + torch's Adam kernels. */
 #define SNNFLOW_ADAM_MAX_TENSORS 64
 #define SNNFLOW_CLIP_ADAM_MAX_N (1 << 20)
+#define SNNFLOW_CLIP_ADAM_ONE_BLOCK 8192
 typedef struct {
     float* param;
     int64_t offset;        /* into grad */
@@ -563,6 +567,7 @@ typedef struct {
     float max_norm, clip_eps;
     int ntensors;
     snnflow_adam_tensor t[SNNFLOW_ADAM_MAX_TENSORS];
+    double* scratch;   /* ABI 32: SNNFLOW_CLIP_SCRATCH doubles when n > SNNFLOW_CLIP_ADAM_ONE_BLOCK (else may be NULL) */
 } snnflow_clip_adam_args;
 int snnflow_clip_adam(const snnflow_clip_adam_args* a, void* stream);
 

@@ -2641,67 +2641,96 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_grad_norm(float* g, int64_t n,
     }
 }
 
-// clip_grad_norm_ + Adam (snnflow_clip_adam): one block; the norm pass as k_clip_grad_norm, then
-// every parameter tensor's elements with the reference's Adam arithmetic (fp64 bias corrections).
-__global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a) {
+// clip_grad_norm_ + Adam (snnflow_clip_adam).  Block b owns elements [b S, (b+1) S), S =
+// CLIP_PER * CLIP_NT, one round with every load issued before any math.  One block (n <= S): the norm
+// pass and the step increment in the same launch.  Several blocks: k_clip_adam_norm writes per-block
+// norm partials and increments the step first; every block of k_clip_adam then sums all partials in
+// block order (the same value everywhere, deterministic).  Elements find their parameter tensor by a
+// binary search over the LDS copy of the table (offsets ascending, host-checked); Adam as the reference
+// (torch _single_tensor_adam: lerp first moment, fp64 bias corrections).
+constexpr int CLIP_PER = 8, CLIP_SLICE = CLIP_PER * CLIP_NT;
+static_assert(CLIP_SLICE == SNNFLOW_CLIP_ADAM_ONE_BLOCK, "one-block size");
+
+__device__ inline double clip_sq_slice(const float* g, int64_t n, int64_t i0, int64_t i1) {
+    double s = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += (int64_t)CLIP_SLICE) {
+        float v[CLIP_PER];
+#pragma unroll
+        for (int k = 0; k < CLIP_PER; ++k) v[k] = i + k * CLIP_NT < i1 ? g[i + k * CLIP_NT] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < CLIP_PER; ++k) s += (double)v[k] * (double)v[k];
+    }
+    return s;
+}
+
+// block total of a per-thread double (all threads; result valid in thread 0)
+__device__ inline double clip_block_sum(double s, double* part) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    double t = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < CLIP_NT / 64; ++w) t += part[w];
+    return t;
+}
+
+__global__ __launch_bounds__(CLIP_NT) void k_clip_adam_norm(snnflow_clip_adam_args a) {
+    __shared__ double part[CLIP_NT / 64];
+    const int64_t i0 = (int64_t)blockIdx.x * CLIP_SLICE, i1 = i0 + CLIP_SLICE < a.n ? i0 + CLIP_SLICE : a.n;
+    const double t = clip_block_sum(a.max_norm > 0.0f ? clip_sq_slice(a.grad, a.n, i0, i1) : 0.0, part);
+    if (threadIdx.x == 0) {
+        a.scratch[blockIdx.x] = t;
+        if (blockIdx.x == 0) a.step[0] = a.step[0] + 1.0f;
+    }
+}
+
+__global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a, int nparts) {
     __shared__ double part[CLIP_NT / 64];
     __shared__ float coef_s, step_s;
     __shared__ snnflow_adam_tensor tab[SNNFLOW_ADAM_MAX_TENSORS];  // the argument table, for lookups
     if (threadIdx.x < a.ntensors) tab[threadIdx.x] = a.t[threadIdx.x];
-    float c = 1.0f;
-    if (a.max_norm > 0.0f) {
-        double s = 0.0;
-        // 8 guarded loads in flight per thread and round (the vector is ~5e3..1e6 floats: for the
-        // small ones a serial tail loop would wait one memory latency per element)
-        for (int64_t i0 = threadIdx.x; i0 < a.n; i0 += 8 * CLIP_NT) {
-            float v[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = i0 + k * CLIP_NT < a.n ? a.grad[i0 + k * CLIP_NT] : 0.0f;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += (double)v[k] * (double)v[k];
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    const bool clip = a.max_norm > 0.0f;
+    double tot = 0.0;
+    if (nparts == 0) {  // one block: the norm over all n here
+        tot = clip_block_sum(clip ? clip_sq_slice(a.grad, a.n, 0, a.n) : 0.0, part);
+    } else if (threadIdx.x == 0 && clip) {
+        for (int j = 0; j < nparts; ++j) tot += a.scratch[j];
     }
-    __syncthreads();
     if (threadIdx.x == 0) {
-        if (a.max_norm > 0.0f) {
-            double t = 0.0;
-            for (int w = 0; w < CLIP_NT / 64; ++w) t += part[w];
-            const float total = (float)sqrt(t);
+        if (clip) {
+            const float total = (float)sqrt(tot);
             const float cc = a.max_norm / (total + a.clip_eps);
             coef_s = cc < 1.0f ? cc : 1.0f;
-            if (a.total_out) a.total_out[0] = total;
+            if (a.total_out && blockIdx.x == 0) a.total_out[0] = total;
         } else {
             coef_s = 1.0f;
         }
-        const float st = a.step[0] + 1.0f;
+        float st = a.step[0];
+        if (nparts == 0) {
+            st += 1.0f;
+            a.step[0] = st;
+        }
         step_s = st;
-        a.step[0] = st;
     }
     __syncthreads();
-    c = coef_s;
+    const float c = coef_s;
     const double step = (double)step_s;
     const double bc1 = 1.0 - pow(a.beta1, step), bc2 = 1.0 - pow(a.beta2, step);
     const float neg_step_size = (float)(-(a.lr / bc1));
     const float bc2_sqrt = (float)sqrt(bc2);
     const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2);
     const float eps = (float)a.eps, wd = (float)a.weight_decay;
-    const bool clip = a.max_norm > 0.0f;
-    // flat over the gradient buffer: element i belongs to the tensor with the largest offset <= i
-    // (offsets ascending, host-checked), found by a binary search over the LDS copy of the table.
-    // CLIP_PER elements per thread and round with every load issued before any math: one memory
-    // latency per round instead of one per element (or, looping over tensors, one per tensor).
-    constexpr int CLIP_PER = 8;
-    for (int64_t i0 = threadIdx.x; i0 < a.n; i0 += (int64_t)CLIP_PER * CLIP_NT) {
+    const int64_t lo_i = nparts ? (int64_t)blockIdx.x * CLIP_SLICE : 0;
+    const int64_t hi_i = nparts ? (lo_i + CLIP_SLICE < a.n ? lo_i + CLIP_SLICE : a.n) : a.n;
+    for (int64_t i0 = lo_i + threadIdx.x; i0 < hi_i; i0 += (int64_t)CLIP_SLICE) {
         float gv[CLIP_PER], pv[CLIP_PER], mv[CLIP_PER], vv[CLIP_PER];
         float *pp[CLIP_PER], *mp[CLIP_PER], *vp[CLIP_PER];
 #pragma unroll
         for (int u = 0; u < CLIP_PER; ++u) {
             const int64_t i = i0 + (int64_t)u * CLIP_NT;
             pp[u] = nullptr;
-            if (i >= a.n) continue;
+            if (i >= hi_i) continue;
             int lo = 0, hi = a.ntensors - 1;
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
@@ -4728,7 +4757,15 @@ int snnflow_clip_adam(const snnflow_clip_adam_args* a, void* stream) {
         if (k > 0 && t.offset < a->t[k - 1].offset + a->t[k - 1].numel)
             SNN_FAIL(SNNFLOW_E_ARG, "clip_adam: tensors must be in ascending, non-overlapping gradient order");
     }
-    hipLaunchKernelGGL(k_clip_adam, dim3(1), dim3(CLIP_NT), 0, (hipStream_t)stream, *a);
+    const hipStream_t s = (hipStream_t)stream;
+    if (a->n <= CLIP_SLICE) {
+        hipLaunchKernelGGL(k_clip_adam, dim3(1), dim3(CLIP_NT), 0, s, *a, 0);
+    } else {
+        const int nb = (int)((a->n + CLIP_SLICE - 1) / CLIP_SLICE);
+        if (!a->scratch || nb > SNNFLOW_CLIP_SCRATCH) SNN_FAIL(SNNFLOW_E_ARG, "clip_adam: scratch needed above SNNFLOW_CLIP_ADAM_ONE_BLOCK");
+        hipLaunchKernelGGL(k_clip_adam_norm, dim3(nb), dim3(CLIP_NT), 0, s, *a);
+        hipLaunchKernelGGL(k_clip_adam, dim3(nb), dim3(CLIP_NT), 0, s, *a, nb);
+    }
     SNN_CHECK_LAUNCH();
     return 0;
 }

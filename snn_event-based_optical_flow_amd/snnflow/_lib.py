@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 31
+ABI_VERSION = 32
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -146,7 +146,8 @@ class AdamTensor(ctypes.Structure):
 class ClipAdamArgs(ctypes.Structure):
     _fields_ = [("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("step", P), ("total_out", P), ("n", I64),
                 ("lr", F64), ("beta1", F64), ("beta2", F64), ("eps", F64), ("weight_decay", F64),
-                ("max_norm", F32), ("clip_eps", F32), ("ntensors", I32), ("t", AdamTensor * ADAM_MAX_TENSORS)]
+                ("max_norm", F32), ("clip_eps", F32), ("ntensors", I32), ("t", AdamTensor * ADAM_MAX_TENSORS),
+                ("scratch", P)]
 
 
 # SNNFLOW_M_* output columns of snnflow_flow_metrics

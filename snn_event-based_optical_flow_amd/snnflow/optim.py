@@ -86,6 +86,7 @@ class ClipAdam(torch.optim.Optimizer):
         _, ea, es, step, offs = self._state(params)
         if self.last_total_norm is None or self.last_total_norm.device != grad.device:
             self.last_total_norm = torch.zeros((), device=grad.device)
+            self._scratch = torch.empty(513, dtype=torch.float64, device=grad.device)  # SNNFLOW_CLIP_SCRATCH
         a = _lib.ClipAdamArgs()
         a.grad, a.exp_avg, a.exp_avg_sq, a.step = grad.data_ptr(), ea.data_ptr(), es.data_ptr(), step.data_ptr()
         a.total_out, a.n = self.last_total_norm.data_ptr(), grad.numel()
@@ -95,6 +96,7 @@ class ClipAdam(torch.optim.Optimizer):
         mn = group["max_norm"]
         a.max_norm, a.clip_eps = (float(mn) if mn is not None else 0.0), float(group["clip_eps"])
         a.ntensors = len(params)
+        a.scratch = self._scratch.data_ptr()
         base = grad.data_ptr()
         order = sorted(range(len(params)), key=lambda k: params[k].grad.data_ptr())  # gradient order
         for i, k in enumerate(order):

@@ -366,10 +366,12 @@ def test_cfg2_eval_vs_oracle(dev):
     assert worst_flow <= 1e-4 and worst_aee <= 1e-4
 
 
-def test_clip_adam_matches_torch(dev):
+@pytest.mark.parametrize("C", [8, 32])
+def test_clip_adam_matches_torch(dev, C):
     """snnflow.ClipAdam (one launch: clip_grad_norm_ + Adam, train_flow.py:265-267) against the
     reference's pair -- torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (single-tensor, the
-    reference's CPU arithmetic) -- over 4 train steps of LIFFireNet at C = 8 with large gradients
+    reference's CPU arithmetic) -- over 4 train steps of LIFFireNet at C = 8 (4,994 parameters: one
+    block) and C = 32 (75,266: the two-launch multi-block form) with large gradients
     (so that the clip is active), plus weight decay on a second run.  Both copies see the same
     gradients at every step (the torch copy's gradients are copied from ours before clipping), so
     the comparison isolates the optimizer: clipped gradients and the reported norm within 1e-6 /
@@ -383,7 +385,7 @@ def test_clip_adam_matches_torch(dev):
 
     for wd in (0.0, 1e-2):
         torch.manual_seed(0)
-        model = snnflow.LIFFireNet(train_snn_model_kwargs(base_num_channels=8)).to(dev).train()
+        model = snnflow.LIFFireNet(train_snn_model_kwargs(base_num_channels=C)).to(dev).train()
         twin = [p.detach().clone() for p in model.parameters()]
         opt = snnflow.ClipAdam(model.parameters(), lr=2e-4, weight_decay=wd, max_norm=1.0)
         tw = [torch.nn.Parameter(t) for t in twin]
@@ -392,8 +394,13 @@ def test_clip_adam_matches_torch(dev):
                "model": {"mask_output": True}}
         lf = snnflow.EventWarping(cfg, dev)
         gen = torch.Generator(device=dev).manual_seed(5)
+        is_thr = [n.endswith("threshold") for n, _ in model.named_parameters()]
         for it in range(4):
             wins = [make_window(2, 500, 64, 64, gen, dev) for _ in range(3)]
+            with torch.no_grad():  # the forward clamps thresholds at 0.01 in place (weight preparation)
+                for t, th in zip(tw, is_thr):
+                    if th:
+                        t.clamp_(min=0.01)
             lf.reset()
             outs = model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
             for w, o in zip(wins, outs):
