@@ -128,7 +128,10 @@ class _FireNetBase(BaseModel):
         self._states = states
 
     def detach_states(self):
-        self.states = [s.detach() if s is not None else None for s in self.states]
+        # models/model.py:126-130 detaches copies of the states; the kernels never write a state in
+        # place (every step's states are new buffers), so detaching the states themselves gives the
+        # same values without one clone launch per state
+        self._states = [s.detach() if s is not None else None for s in self._states]
 
     def reset_states(self):
         self._states = [None] * self.num_recurrent_units
