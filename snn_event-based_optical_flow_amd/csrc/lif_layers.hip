@@ -1378,8 +1378,19 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     //    the BN-sum replicas first, so that their reduction overlaps the halo loads
     //    (C <= 16; at C = 32 the 12 extra live registers spill: gathered in place there)
     constexpr bool EARLY_G = C <= 16 && !(REC && C == 8 && !SNNFLOW_EARLY_G_REC8);
-    AccGather<SNNFLOW_BWD_ACC(C)> gat;
-    if constexpr (EARLY_G) acc_gather_load<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), gat);
+    // every block needs only the 2C BatchNorm sums (sum g, sum (y - mean) g) of the replicas; the
+    // other neuron-gradient sums only block 0 (a third of the loads and of the reduction elsewhere)
+    // (C = 32: one gather of all sums -- the second reduction array would take the slot kernel's LDS
+    // past two blocks per CU)
+    constexpr int NSUM = SNNFLOW_BWD_ACC(C), NBN = C <= 16 ? 2 * C : NSUM;
+    const bool lead = g.bid == 0;
+    constexpr int NL = NSUM - NBN > 0 ? NSUM - NBN : 1;
+    AccGather<NBN> gat;
+    AccGather<NL> gat_l;
+    if constexpr (EARLY_G) {
+        acc_gather_load<NBN>(a.acc_in, NSUM, gat);
+        if (NBN < NSUM && lead) acc_gather_load<NL>(a.acc_in + NBN, NSUM, gat_l);
+    }
     // per-channel parameters, also ahead of the halo loads
     float st_mean = 0.f, st_inv = 0.f, gamma = 0.f;
     if (tid < C) {
@@ -1462,10 +1473,15 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
 
     // 2. per-channel constants; block 0 finishes layer l's neuron gradients and stores the
     //    BN backward coefficients for the deferred weight gradient
-    __shared__ double sums[SNNFLOW_BWD_ACC(C)];
-    if constexpr (EARLY_G) acc_gather_reduce<SNNFLOW_BWD_ACC(C)>(gat, sums);
-    else acc_gather<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), sums);
-    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
+    __shared__ double sums[NSUM];
+    if constexpr (EARLY_G) {
+        acc_gather_reduce<NBN>(gat, sums);
+        if (NBN < NSUM && lead) acc_gather_reduce<NL>(gat_l, sums + NBN);  // (block-uniform: barriers inside)
+    } else {
+        acc_gather<NBN>(a.acc_in, NSUM, sums);
+        if (NBN < NSUM && lead) acc_gather<NL>(a.acc_in + NBN, NSUM, sums + NBN);
+    }
+    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b, lead);
     if (tid < C) {
         const float mean = st_mean, inv = st_inv;
         BnBwdLds c;
