@@ -6,8 +6,9 @@ SUM all-reduce of gradients across ranks (data parallel, weak scaling), clip_gra
 (1.0), Adam (lr 2e-4), truncated-BPTT state detach, loss reset.  Synthetic seeded
 event windows resident in HBM (configs/train_SNN.yml shapes: 128x128, batch 8 per
 GPU, base_num_channels 8).  The whole step is captured into a HIP graph (torch.cuda.graph),
-one graph per resident batch of the pool, each reading its batch in place, and the graphs are
-replayed in turn; every kernel on the path is in libsnnflow.so.
+one graph per resident batch of the pool and state parity, each reading its batch in place, and the
+graphs are replayed in turn (N > 1: per batch a forward + backward graph, the SUM all-reduce of its
+gradient buffer, an update graph); every kernel on the path is in libsnnflow.so.
 
     python bench.py [--gpus N --steps K --warmup W --channels C --res R --batch B]
     torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU, RCCL)
@@ -284,22 +285,21 @@ def main():
     torch.cuda.current_stream(dev).wait_stream(s_side)
     torch.cuda.synchronize(dev)
 
-    # HIP graphs.  N = 1: one graph per resident batch of the pool (forward, backward, clip, Adam,
-    # state hand-over), each reading its batch in place: no per-step input copy.  Every capture starts
-    # from set_to_none gradients, so each graph owns its gradient buffer and everything that reads it
-    # (clip, Adam) is inside the same graph.  N > 1: one forward + backward graph over a fixed input
-    # buffer (refilled by load_batch), the eager all-reduce, then the update graph.
-    graphs = []
-    g_upd = None
+    # HIP graphs, one per resident batch of the pool (and state parity: StatePingPong), each reading
+    # its batch in place.  N = 1: forward, backward, clip, Adam and the state hand-over in one graph.
+    # N > 1: the same forward + backward graph per batch, the eager SUM all-reduce of that graph's
+    # flat gradient buffer, then that batch's update graph (clip + Adam read the graph's gradients).
+    # Every capture starts from set_to_none gradients, so each graph owns its gradient buffer.
+    graphs, upds, flats = [], [], []
     multi = world == 1
     if not args.no_graph:
-        n_graphs = len(pool) if multi else 1
-        if multi and not unet and not args.per_step:
+        n_graphs = len(pool)
+        if not unet and not args.per_step:
             pingpong = StatePingPong(dev, get_states())
             n_graphs = pingpong.cycle(len(pool))
         for j in range(n_graphs):
             opt.zero_grad(set_to_none=True)
-            cur["views"] = pool[j % len(pool)][1] if multi else static_views
+            cur["views"] = pool[j % len(pool)][1]
             if pingpong is not None:
                 pingpong.arm(model, j)
             g = torch.cuda.CUDAGraph()
@@ -308,10 +308,12 @@ def main():
                 if multi:
                     update()
             graphs.append(g)
-        if not multi:
-            g_upd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_upd, pool=graphs[0].pool()):
-                update()
+            if not multi:
+                flats.append(dp.flat_grad_buffer(params))
+                u = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(u, pool=g.pool()):
+                    update()
+                upds.append(u)
 
     def step(i):
         if not graphs:
@@ -320,15 +322,18 @@ def main():
         elif multi:
             graphs[i % len(graphs)].replay()
         else:
-            load_batch(i)
-            graphs[0].replay()
-            sync_grads()
-            g_upd.replay()
+            j = i % len(graphs)
+            graphs[j].replay()
+            if flats[j] is not None:
+                dist.all_reduce(flats[j], op=dist.ReduceOp.SUM)
+            else:
+                sync_grads()
+            upds[j].replay()
 
     for i in range(2):  # graph warm replays
         step(i)
     if args.dp_check:
-        _dp_check(world, rank, step_parts=(load_batch, graphs, g_upd, fwd_bwd, sync_grads, update, opt), params=params)
+        _dp_check(world, rank, step_parts=(graphs, upds, flats, fwd_bwd, sync_grads, update, opt), params=params)
         dist.destroy_process_group()
         return
     if world > 1:
@@ -401,23 +406,31 @@ def main():
 
 
 def _dp_check(world, rank, step_parts, params):
-    """One step of the N>1 path exactly as timed (graph 1: forward + backward; eager all-reduce;
-    graph 2: clip + Adam + state hand-over), checked: the all-reduced flat gradient equals the
-    SUM of every rank's own gradient (gathered through the host), and after the update every
-    rank holds the same parameters.  Rank 0 prints one JSON line."""
-    load_batch, graphs, g_upd, fwd_bwd, sync_grads, update, opt = step_parts
-    load_batch(1)
-    if graphs:
-        graphs[0].replay()
+    """One step of the N>1 path exactly as timed (batch 1's forward + backward graph; the eager
+    all-reduce of that graph's flat gradient buffer; its update graph: clip + Adam), checked: the
+    all-reduced flat gradient equals the SUM of every rank's own gradient (gathered through the
+    host), and after the update every rank holds the same parameters.  Rank 0 prints one JSON line."""
+    from snnflow import dp
+
+    graphs, upds, flats, fwd_bwd, sync_grads, update, opt = step_parts
+    if graphs:  # batch 1's graphs (the gradients of a replay live in that graph's own flat buffer)
+        graphs[1 % len(graphs)].replay()
+        flat = flats[1 % len(graphs)]
     else:
         opt.zero_grad(set_to_none=True)
         fwd_bwd()
+        flat = dp.flat_grad_buffer(params)
     torch.cuda.synchronize()
+
     def grads():
-        return torch.cat([p.grad.detach().reshape(-1).cpu() for p in params])
+        return flat.detach().cpu().clone() if flat is not None else torch.cat(
+            [p.grad.detach().reshape(-1).cpu() for p in params])
 
     local = grads()
-    sync_grads()
+    if flat is not None:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    else:
+        sync_grads()
     torch.cuda.synchronize()
     reduced = grads()
     locals_ = [torch.empty_like(local) for _ in range(world)]
@@ -428,7 +441,7 @@ def _dp_check(world, rank, step_parts, params):
     err = float((reduced.double() - want).abs().max() / max(float(want.abs().max()), 1e-30))
     distinct = float(max((t - locals_[0]).abs().max() for t in locals_[1:]))
     if graphs:
-        g_upd.replay()
+        upds[1 % len(graphs)].replay()
     else:
         update()
     torch.cuda.synchronize()
@@ -663,15 +676,26 @@ BF16_PEAK_TFLOPS = 2500.0
 BF16X3_PEAK_TFLOPS = BF16_PEAK_TFLOPS / 3
 
 
+# bf16 matrix-core products each U-Net GEMM class issues per exact fp32 product: the forward conv and
+# the weight gradient multiply an exact-in-bf16 operand (spikes, spike sums) by a 3-part split, the
+# input gradient multiplies two 3-part splits (six products above 2^-24 relative)
+UNET_PRODUCTS = {"unet_conv": 3, "unet_wgrad": 3, "unet_dgrad": 6}
+
+
 def _unet_roofline(kern):
     """MFMA roofline of the dominant U-Net GEMM class: algorithmic (reference fp32 conv) FLOPs per
-    launch / HIP-event time, against the bf16x3 peak; every class listed with its own rate."""
+    launch / HIP-event time, against the bf16x3 peak; every class listed with its own rate, and with
+    its issued rate (algorithmic x the bf16 products it issues) against the dense bf16 peak."""
     kernels = {}
     total = sum(v["total_ms"] for v in kern.values())
     for k, v in sorted(kern.items(), key=lambda kv: -kv[1]["total_ms"]):
         e = {"launches": v["launches"], "avg_us": round(v["avg_us"], 2), "share": round(v["total_ms"] / total, 3)}
         if v["work"]:
-            e["tflops"] = round(v["work"] / (v["total_ms"] * 1e-3) / 1e12, 1)
+            tf = v["work"] / (v["total_ms"] * 1e-3) / 1e12
+            e["tflops"] = round(tf, 1)
+            if k in UNET_PRODUCTS:
+                e["issued_tflops"] = round(tf * UNET_PRODUCTS[k], 1)
+                e["issued_frac"] = round(tf * UNET_PRODUCTS[k] / BF16_PEAK_TFLOPS, 4)
         kernels[k] = e
     gemm = {k: v for k, v in kern.items() if v["work"]}
     dominant = max(gemm, key=lambda k: gemm[k]["total_ms"])
@@ -680,7 +704,8 @@ def _unet_roofline(kern):
     roofline = {"bound": "mfma", "kernel": dominant, "achieved": round(achieved, 1), "peak": round(BF16X3_PEAK_TFLOPS, 1),
                 "unit": "TFLOP/s", "frac": round(achieved / BF16X3_PEAK_TFLOPS, 4), "traffic": None,
                 "flops_per_launch": d["work"] / d["launches"], "avg_us": round(d["avg_us"], 2),
-                "peak_note": "bf16 dense 2.5 PF / 3 (hi/mid/lo weight products per exact fp32 product)"}
+                "peak_note": "bf16 dense 2.5 PF / 3 (hi/mid/lo weight products per exact fp32 product)",
+                "issued_frac": kernels.get(dominant, {}).get("issued_frac")}
     return roofline, kernels
 
 

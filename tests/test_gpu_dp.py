@@ -1,5 +1,5 @@
-"""The N>1 bench step path on the GPU (two graphs per step with the SUM all-reduce of the flat
-gradient buffer between them, bench.py step()), rehearsed with 2 fresh ranks sharing the box's
+"""The N>1 bench step path on the GPU (per resident batch a forward + backward graph, the SUM
+all-reduce of that graph's flat gradient buffer, and its update graph, bench.py step()), rehearsed with 2 fresh ranks sharing the box's
 one GPU over gloo (SNNFLOW_SHARE_GPU=1).  bench.py --dp-check replays one step exactly as timed
 and checks that the all-reduced gradient is the sum of the two ranks' own gradients (each rank
 draws its own synthetic stream, so they differ) and that after clip + Adam both ranks hold the
@@ -55,3 +55,19 @@ def test_bench_gpus_flag_launches_its_ranks():
     assert res["world"] == 2
     assert res["allreduce_rel_err"] < 1e-6
     assert res["param_max_diff_after_update"] == 0.0
+
+
+def test_bench_two_ranks_timed_line():
+    """The timed N = 2 path end to end (gloo rehearsal on the shared GPU, 3 resident batches, so 6
+    graph pairs with the state ping-pong): one JSON line with n_gpus 2 and a positive rate."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(SNNFLOW_SHARE_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--batch", "2", "--dist-backend", "gloo"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert lines, r.stdout[-2000:]
+    res = json.loads(lines[-1])
+    print("\n[N=2 timed]", res["value"], res["ms_per_step"])
+    assert res["n_gpus"] == 2 and res["value"] > 0 and res["config"]["parallelism"] == "dp2"
