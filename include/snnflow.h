@@ -445,7 +445,8 @@ typedef struct snnflow_aee_args {
     const float* dt_gt; const float* dt_input; int dt_gt_n, dt_input_n;
 } snnflow_aee_args;
 /* One launch: per-block partial sums (fp64 rows), the last block to finish reduces them in a fixed
- * order (deterministic) and writes aee / percent. */
+ * order (deterministic) and writes aee / percent.  The scratch carries the completion counter from
+ * call to call: one stream at a time per scratch (concurrent calls need their own scratch). */
 int snnflow_aee(const snnflow_aee_args* a, void* stream);
 int snnflow_aee_acc_doubles(int B, int H, int W);
 
