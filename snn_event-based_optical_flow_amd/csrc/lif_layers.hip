@@ -2702,17 +2702,58 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_adam_norm(snnflow_clip_adam_ar
 }
 
 __global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a, int nparts) {
+    // Every load of the block (step counter, gradients, parameters, both moments) is issued in one
+    // round ahead of the norm reduction: the update needs nothing from the norm but the clip factor,
+    // so the kernel waits for one memory latency, not three (norm pass, step counter, update).
     __shared__ double part[CLIP_NT / 64];
-    __shared__ float coef_s, step_s;
+    __shared__ float coef_s;
     __shared__ snnflow_adam_tensor tab[SNNFLOW_ADAM_MAX_TENSORS];  // the argument table, for lookups
     if (threadIdx.x < a.ntensors) tab[threadIdx.x] = a.t[threadIdx.x];
     const bool clip = a.max_norm > 0.0f;
+    const float st_in = a.step[0];
+    __syncthreads();
+    const int64_t lo_i = nparts ? (int64_t)blockIdx.x * CLIP_SLICE : 0;
+    const int64_t hi_i = lo_i + CLIP_SLICE < a.n ? lo_i + CLIP_SLICE : a.n;  // (one block: n <= CLIP_SLICE)
+    float gv[CLIP_PER], pv[CLIP_PER], mv[CLIP_PER], vv[CLIP_PER];
+    float *pp[CLIP_PER], *mp[CLIP_PER], *vp[CLIP_PER];
+#pragma unroll
+    for (int u = 0; u < CLIP_PER; ++u) {  // gradients first: the norm waits only for them
+        const int64_t i = lo_i + threadIdx.x + (int64_t)u * CLIP_NT;
+        gv[u] = i < hi_i ? a.grad[i] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < CLIP_PER; ++u) {
+        const int64_t i = lo_i + threadIdx.x + (int64_t)u * CLIP_NT;
+        pp[u] = nullptr;
+        if (i >= hi_i) continue;
+        int lo = 0, hi = a.ntensors - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (tab[mid].offset <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t j = i - tab[lo].offset;
+        if (j < 0 || j >= tab[lo].numel) continue;  // a gap between tensors (not written by the engine)
+        pp[u] = tab[lo].param + j;
+        mp[u] = a.exp_avg + tab[lo].state_offset + j;
+        vp[u] = a.exp_avg_sq + tab[lo].state_offset + j;
+        pv[u] = *pp[u];
+        mv[u] = *mp[u];
+        vv[u] = *vp[u];
+    }
     double tot = 0.0;
-    if (nparts == 0) {  // one block: the norm over all n here
-        tot = clip_block_sum(clip ? clip_sq_slice(a.grad, a.n, 0, a.n) : 0.0, part);
+    if (nparts == 0) {  // one block: the norm over all n here (the same squares, the same order)
+        double sq = 0.0;
+        if (clip) {
+#pragma unroll
+            for (int u = 0; u < CLIP_PER; ++u) sq += (double)gv[u] * (double)gv[u];
+        }
+        tot = clip_block_sum(sq, part);
     } else if (threadIdx.x == 0 && clip) {
         for (int j = 0; j < nparts; ++j) tot += a.scratch[j];
     }
+    // the step counter: incremented here (one block) or by k_clip_adam_norm (several)
+    const float st = nparts == 0 ? st_in + 1.0f : st_in;
     if (threadIdx.x == 0) {
         if (clip) {
             const float total = (float)sqrt(tot);
@@ -2722,65 +2763,33 @@ __global__ __launch_bounds__(CLIP_NT) void k_clip_adam(snnflow_clip_adam_args a,
         } else {
             coef_s = 1.0f;
         }
-        float st = a.step[0];
-        if (nparts == 0) {
-            st += 1.0f;
-            a.step[0] = st;
-        }
-        step_s = st;
+        if (nparts == 0) a.step[0] = st;
     }
+    const double step = (double)st;
+    const double bc1 = 1.0 - pow(a.beta1, step), bc2 = 1.0 - pow(a.beta2, step);  // (overlaps the barrier wait)
     __syncthreads();
     const float c = coef_s;
-    const double step = (double)step_s;
-    const double bc1 = 1.0 - pow(a.beta1, step), bc2 = 1.0 - pow(a.beta2, step);
     const float neg_step_size = (float)(-(a.lr / bc1));
     const float bc2_sqrt = (float)sqrt(bc2);
     const float w1 = (float)(1.0 - a.beta1), b2 = (float)a.beta2, w2 = (float)(1.0 - a.beta2);
     const float eps = (float)a.eps, wd = (float)a.weight_decay;
-    const int64_t lo_i = nparts ? (int64_t)blockIdx.x * CLIP_SLICE : 0;
-    const int64_t hi_i = nparts ? (lo_i + CLIP_SLICE < a.n ? lo_i + CLIP_SLICE : a.n) : a.n;
-    for (int64_t i0 = lo_i + threadIdx.x; i0 < hi_i; i0 += (int64_t)CLIP_SLICE) {
-        float gv[CLIP_PER], pv[CLIP_PER], mv[CLIP_PER], vv[CLIP_PER];
-        float *pp[CLIP_PER], *mp[CLIP_PER], *vp[CLIP_PER];
 #pragma unroll
-        for (int u = 0; u < CLIP_PER; ++u) {
-            const int64_t i = i0 + (int64_t)u * CLIP_NT;
-            pp[u] = nullptr;
-            if (i >= hi_i) continue;
-            int lo = 0, hi = a.ntensors - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (tab[mid].offset <= i) lo = mid;
-                else hi = mid - 1;
-            }
-            const int64_t j = i - tab[lo].offset;
-            if (j < 0 || j >= tab[lo].numel) continue;  // a gap between tensors (not written by the engine)
-            pp[u] = tab[lo].param + j;
-            mp[u] = a.exp_avg + tab[lo].state_offset + j;
-            vp[u] = a.exp_avg_sq + tab[lo].state_offset + j;
-            gv[u] = a.grad[i];
-            pv[u] = *pp[u];
-            mv[u] = *mp[u];
-            vv[u] = *vp[u];
+    for (int u = 0; u < CLIP_PER; ++u) {
+        if (!pp[u]) continue;
+        float g = gv[u];
+        if (clip) {
+            g = g * c;
+            a.grad[lo_i + threadIdx.x + (int64_t)u * CLIP_NT] = g;  // clip_grad_norm_ scales the gradients in place
         }
-#pragma unroll
-        for (int u = 0; u < CLIP_PER; ++u) {
-            if (!pp[u]) continue;
-            float g = gv[u];
-            if (clip) {
-                g = g * c;
-                a.grad[i0 + (int64_t)u * CLIP_NT] = g;  // clip_grad_norm_ scales the gradients in place
-            }
-            float p = pv[u];
-            if (wd != 0.0f) g = g + wd * p;
-            const float m = mv[u] + w1 * (g - mv[u]);  // lerp, weight < 0.5
-            const float v = vv[u] * b2 + w2 * g * g;
-            const float denom = sqrtf(v) / bc2_sqrt + eps;
-            p = p + neg_step_size * (m / denom);
-            *mp[u] = m;
-            *vp[u] = v;
-            *pp[u] = p;
-        }
+        float p = pv[u];
+        if (wd != 0.0f) g = g + wd * p;
+        const float m = mv[u] + w1 * (g - mv[u]);  // lerp, weight < 0.5
+        const float v = vv[u] * b2 + w2 * g * g;
+        const float denom = sqrtf(v) / bc2_sqrt + eps;
+        p = p + neg_step_size * (m / denom);
+        *mp[u] = m;
+        *vp[u] = v;
+        *pp[u] = p;
     }
 }
 
