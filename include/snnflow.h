@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 32
+#define SNNFLOW_ABI_VERSION 33
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -130,6 +130,9 @@ typedef struct snnflow_conv_fwd_args {
      * blocks of the launch's other such tasks take the rest once theirs are done); the call leaves it
      * nonzero, so every launch needs a fresh zeroed counter.  NULL: a static tile assignment. */
     int* tile_counter;
+    /* ABI 33: 1 = store only the membrane half of prev_state (a caller whose spike half is never read:
+     * a feed-forward layer's intermediate time steps in a window -- the backward recomputes the spikes) */
+    int state_spk_skip;
 } snnflow_conv_fwd_args;
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream);
 int snnflow_conv_blocks(int B, int H, int W);
@@ -147,6 +150,7 @@ typedef struct snnflow_lif_fwd_args {
     const float* pred_b;        /* [2] */
     float* flow;                /* NCHW [B][2][H][W] */
     double* zero0; double* zero1; int zero_n;
+    int state_spk_skip;         /* ABI 33: 1 = store only the membrane half of state (as snnflow_conv_fwd_args) */
 } snnflow_lif_fwd_args;
 int snnflow_lif_fwd(const snnflow_lif_fwd_args* a, void* stream);
 

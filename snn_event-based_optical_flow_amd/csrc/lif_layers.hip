@@ -442,7 +442,7 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                             const int64_t k = (((int64_t)tl.b * H + h) * W + w) * Q + qt;
                             // write-through: read again only at the next time step (measured -1 us per launch)
                             st_state4(st4, k, o.mout);
-                            st_state4(st4, plane4 + k, o.s);
+                            if (!a.state_spk_skip) st_state4(st4, plane4 + k, o.s);
                         }
                     }
                     if constexpr (L::BT) {
@@ -638,7 +638,7 @@ __device__ void lif_fwd_body(const snnflow_lif_fwd_args& a, const Grid g) {
     for (int q = 0; q < Q; ++q) {
         const Lif4 o = lif_step4(yv[q], mv[q], coef + 4 * q, zr);
         st4[p * Q + q] = o.mout;  // plain: write-through measured slower in this streaming kernel
-        st4[plane4 + p * Q + q] = o.s;
+        if (!a.state_spk_skip) st4[plane4 + p * Q + q] = o.s;
         s[4 * q] = o.s.x; s[4 * q + 1] = o.s.y; s[4 * q + 2] = o.s.z; s[4 * q + 3] = o.s.w;
     }
     if constexpr (PRED) {
@@ -881,7 +881,7 @@ __device__ void lif_fwd_q_body(const snnflow_lif_fwd_args& a, const Grid g, floa
         const Lif4 o = lif_step4(yv, mv, kc, zr);
         if (act) {
             st4[p * Q + q] = o.mout;
-            st4[plane4 + p * Q + q] = o.s;
+            if (!a.state_spk_skip) st4[plane4 + p * Q + q] = o.s;
         }
         if constexpr (PRED) {
             // the pixel's C spikes as a bit mask on each of its lanes; the 1x1 conv then runs in
@@ -3140,7 +3140,7 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
     if (dyn && tid == 0) slot[1] = req;
     if (tid == 0) slot[2] = 0;  // the s_prev exactness flag of tile 0
 
-    const bool zr = a.prev.zero_reset != 0;
+    const bool zr = a.prev.zero_reset != 0, spk_skip = a.state_spk_skip != 0;
     const int64_t plane4 = (int64_t)a.B * H * W * 2;
     float4* st4 = reinterpret_cast<float4*>(a.prev_state);
     float bs[4] = {0.f, 0.f, 0.f, 0.f}, bq[4] = {0.f, 0.f, 0.f, 0.f};  // this lane's batch sums
@@ -3173,7 +3173,7 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
                     if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
                         const int64_t q = (((int64_t)tl.b * H + h) * W + w) * 2 + qt;
                         st_state4(st4, q, o.mout);
-                        st_state4(st4, plane4 + q, o.s);
+                        if (!spk_skip) st_state4(st4, plane4 + q, o.s);
                     }
                 }
                 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

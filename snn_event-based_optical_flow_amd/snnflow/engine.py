@@ -1052,6 +1052,13 @@ class FireNetSequence(torch.autograd.Function):
         train = [bn.training or not bn.track_running_stats for bn in eng.bns]
 
         frec = tuple(bool(eng.rec[k]) if k < L else False for k in range(L + 1))
+        # with the weight gradients fused into the backward (C = 8) the spike half of a feed-forward
+        # layer's state at steps t < T-1 is never read (the next step's LIF reads the membrane half,
+        # the backward recomputes the spikes, only recurrent layers read s_prev; the deferred weight
+        # gradients of the other widths read the spikes), so it is not stored unless the caller
+        # keeps every step's states
+        def spk_skip(l, t):
+            return eng.fuse_wgrad and t < T - 1 and not eng.rec[l] and not eng.keep_seq_states
         launches = capped_slots(T, L + 1, frec, slot_cap())
         # dynamic tile hand-out of the C = 8 tile pipelines: one zeroed counter per task and launch
         ctr = (torch.zeros(len(launches) * _lib.MAX_SLOT_TASKS, dtype=torch.int32, device=dev)
@@ -1064,10 +1071,14 @@ class FireNetSequence(torch.autograd.Function):
                                        s_prev[t], facc[t], neurons, train, wfwd, wbwd)
                     if ctr is not None and k >= 1:
                         a.tile_counter = ctr.data_ptr() + 4 * (li * _lib.MAX_SLOT_TASKS + len(convs))
+                    if k >= 1 and spk_skip(k - 1, t):
+                        a.state_spk_skip = 1
                     convs.append(a)
                 else:
                     top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons,
                                         flows[t])
+                    if spk_skip(L - 1, t):
+                        top.state_spk_skip = 1
             arr = (_lib.ConvFwdArgs * max(len(convs), 1))(*convs)
             _lib.call("fwd_slot", lib.snnflow_fwd_slot, arr, len(convs), ctypes.byref(top) if top is not None else None,
                       s)
@@ -1186,6 +1197,12 @@ class FireNetSequence(torch.autograd.Function):
                         a = _bwd_layer_args(eng, l, B, H, W, cin0, ys[t], stats[t], mem_in[t], neurons,
                                             g_into[t], gcur[t], gmem[t], bacc[t], bnc[t], glayers, gpw, gpb,
                                             acc, wfwd, wbwd, g_out[t], ext[t], gxs[t] if l == 0 else None)
+                        if t > 0:
+                            # g_out[t] (t >= 1) stays inside the chain, and its membrane half is never
+                            # read (the engine's cells detach the reset: step t-1's kernels read only
+                            # the spike half of g_into), so that plane is not zero-filled; step 0's is
+                            # returned to autograd and is
+                            a.zero_mem_half = 0
                         if fuse and l > 0:
                             a.wslab_ff = ws.slab_ff[l].data_ptr()
                             if eng.rec[l]:
