@@ -97,15 +97,29 @@ def algorithmic_bytes(name, C, P, cin0):
     return None
 
 
-def slot_pass_bytes(kind, C, P, cin0, T, layer_spec):
+def slot_pass_bytes(kind, C, P, cin0, T, layer_spec, g0=False):
     """Algorithmic bytes of all T x (L+1) layer-steps of a forward (fwd_slot) or backward
-    (bwd_slot) pass: the per-kernel formulas of algorithmic_bytes, summed."""
+    (bwd_slot) pass: the per-kernel formulas of algorithmic_bytes, summed, less the writes the
+    sequence path leaves out: at C = 8 (weight gradients fused into the backward) the spike half of
+    a feed-forward layer's state at steps t < T-1 (state_spk_skip), at every width the membrane half
+    of the recurrent state gradients of steps t >= 1 (never read); step 0 of the backward writes no state
+    gradient at all when the initial states need none (g0=False: the bench's detached hand-over)."""
     rec = [r for _, r in layer_spec]
+    L, f = len(rec), 4 * P
     if kind == "fwd_slot":
         names = ["conv_fwd[0]"] + ["conv_fwd_rec" if r else "conv_fwd" for r in rec[1:]] + ["lif_fwd"]
-    else:  # the head's backward reads no pixels without an input gradient (one block: neuron grads only)
-        names = ["lif_bwd"] + ["layer_bwd_rec" if r else "layer_bwd" for r in rec[1:]]
-    return T * sum(algorithmic_bytes(n, C, P, cin0) for n in names)
+        total = T * sum(algorithmic_bytes(n, C, P, cin0) for n in names)
+        if C == 8:  # task l >= 1 writes layer l-1's state, the top task layer L-1's
+            total -= (T - 1) * sum(f * C for l in range(L) if not rec[l])
+        return total
+    # the head's backward reads no pixels without an input gradient (one block: neuron grads only)
+    names = ["lif_bwd"] + ["layer_bwd_rec" if r else "layer_bwd" for r in rec[1:]]
+    total = T * sum(algorithmic_bytes(n, C, P, cin0) for n in names)
+    nrec = sum(1 for l in range(1, L) if rec[l])
+    total -= (T - 1) * nrec * f * C
+    if not g0:
+        total -= nrec * f * 2 * C
+    return total
 
 
 def eval_pass_bytes(C, P, cin0, T, layer_spec):
