@@ -276,6 +276,31 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
     for (int j = 0; j < LOSS_NV; ++j) v[j] = 0.0f;
     const int p = chunk * NT + tid;
     if (p < HWp) {
+        const int h = p / a.W, w = p - h * a.W;
+        const bool right = w + 1 < a.W, down = h + 1 < a.H, up = h >= 1, sm = a.smoothing_mask != 0;
+        const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
+        // neighbours right, down, down-right, up-right (a neighbour outside the image reads this pixel:
+        // address always valid, term skipped), loaded a window ahead of their use
+        const int Wd = a.W;
+        const int off[4] = {1, Wd, Wd + 1, -Wd + 1};
+        const bool ok[4] = {right, down, down && right, up && right};
+        auto load_nb = [&](int t, float (&X)[4], float (&Y)[4], float (&M)[4]) {
+            const float* fx = flow_of(a, b, t);
+            const float* m = mask_of(a, b, t);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int pq = ok[q] ? p + off[q] : p;
+                X[q] = fx[pq];
+                Y[q] = fx[HWp + pq];
+                M[q] = m[pq];
+            }
+        };
+        float X[4], Y[4], M[4];
+        load_nb(t0, X, Y, M);
+        const float* f0 = flow_of(a, b, t0);
+        float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
+        // (the images after the first window's loads are issued: their in-place stores would
+        // otherwise hold those loads back)
         if (tg == 0) {
             const float T = (float)a.T;
 #pragma unroll
@@ -299,32 +324,39 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
                 v[3 * d + 2] += (cp + cn > 0.0f) ? 1.0f : 0.0f;
             }
         }
-        const int h = p / a.W, w = p - h * a.W;
-        const bool right = w + 1 < a.W, down = h + 1 < a.H, up = h >= 1, sm = a.smoothing_mask != 0;
-        const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
-        const float* f0 = flow_of(a, b, t0);
-        float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
         for (int t = t0; t < t1; ++t) {
-            const float* fx = flow_of(a, b, t);
-            const float* fy = fx + HWp;
-            const float* m = mask_of(a, b, t);
+            float nX[4], nY[4], nM[4];
+            const bool more = t + 1 < t1;
+            if (more) load_nb(t + 1, nX, nY, nM);
+            float nx = 0.0f, ny = 0.0f, nm = 0.0f;
+            if (t + 1 < a.tf) {
+                const float* f2 = flow_of(a, b, t + 1);
+                nx = f2[p];
+                ny = f2[HWp + p];
+                nm = mask_of(a, b, t + 1)[p];
+            }
             // pair ('a' = centre of window t, 'b' = (bx, by, bm)): masked Charbonnier term
             auto term = [&](float bx, float by, float bm) {
                 const float dd = (cx - bx) + (cy - by);
                 const float c = charb(dd);
                 return sm ? (cm * bm) * c : c;
             };
-            if (right) v[6] += term(fx[p + 1], fy[p + 1], m[p + 1]);                        // dx
-            if (down) v[7] += term(fx[p + a.W], fy[p + a.W], m[p + a.W]);                   // dy
-            if (down && right) v[8] += term(fx[p + a.W + 1], fy[p + a.W + 1], m[p + a.W + 1]);  // dxdy_dr
-            if (up && right) v[9] += term(fx[p - a.W + 1], fy[p - a.W + 1], m[p - a.W + 1]);    // dxdy_ur
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // dx, dy, dxdy_dr, dxdy_ur
+                if (ok[q]) v[6 + q] += term(X[q], Y[q], M[q]);
             if (t + 1 < a.tf) {
-                const float* f2 = flow_of(a, b, t + 1);
-                const float nx = f2[p], ny = f2[HWp + p], nm = mask_of(a, b, t + 1)[p];
-                if (!a.overwrite_intermediate) v[10] += term(nx, ny, nm);                    // dt
+                if (!a.overwrite_intermediate) v[10] += term(nx, ny, nm);  // dt
                 cx = nx;
                 cy = ny;
                 cm = nm;
+            }
+            if (more) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    X[q] = nX[q];
+                    Y[q] = nY[q];
+                    M[q] = nM[q];
+                }
             }
         }
     }
@@ -418,6 +450,45 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
     const int p = chunk * NT + tid;
     if (p >= HWp) return;
     const float g = g_loss[0];
+    // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
+    const int comps = a.overwrite_intermediate ? 4 : 5;
+    const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
+    const int h = p / a.W, w = p - h * a.W;
+    const bool sm = a.smoothing_mask != 0, dt_terms = !a.overwrite_intermediate;
+    // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
+    auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
+        const float dd = (ax - bx) + (ay - by);
+        const float c = charb(dd);
+        const float mk = sm ? am * bm : 1.0f;
+        return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
+    };
+    const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
+    // the 8 neighbours in the order their terms are summed (right, left, down, up, down-right,
+    // up-left, up-right, down-left; odd q: this pixel is the pair's 'b'); a neighbour outside the
+    // image reads this pixel (address always valid) and contributes nothing
+    const int Wd = a.W;
+    const int off[8] = {1, -1, Wd, -Wd, Wd + 1, -Wd - 1, -Wd + 1, Wd - 1};
+    const bool vr = w + 1 < a.W, vl = w >= 1, vd = h + 1 < a.H, vu = h >= 1;
+    const bool ok[8] = {vr, vl, vd, vu, vd && vr, vu && vl, vu && vr, vd && vl};
+    // one window's neighbour values, loaded a window ahead of their use (the loads no longer wait
+    // behind the previous window's g_flows stores)
+    auto load_nb = [&](int t, float (&X)[8], float (&Y)[8], float (&M)[8]) {
+        const float* fx = flow_of(a, b, t);
+        const float* m = mask_of(a, b, t);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int pq = ok[q] ? p + off[q] : p;
+            X[q] = fx[pq];
+            Y[q] = fx[HWp + pq];
+            M[q] = m[pq];
+        }
+    };
+    float X[8], Y[8], M[8];
+    load_nb(t0, X, Y, M);
+    const float* f0 = flow_of(a, b, t0);
+    float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
+    // (the image gradients after the first window's loads are issued: their stores would
+    // otherwise hold those loads back)
     if (tg == 0) {
         const float T = (float)a.T;
 #pragma unroll
@@ -444,52 +515,34 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
             gb[3 * img] = gqn / dn;
         }
     }
-    // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
-    const int comps = a.overwrite_intermediate ? 4 : 5;
-    const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
-    const int h = p / a.W, w = p - h * a.W;
-    const bool sm = a.smoothing_mask != 0, dt_terms = !a.overwrite_intermediate;
-    // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
-    auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
-        const float dd = (ax - bx) + (ay - by);
-        const float c = charb(dd);
-        const float mk = sm ? am * bm : 1.0f;
-        return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
-    };
-    const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
-    const float* f0 = flow_of(a, b, t0);
-    float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
     float gprev = 0.0f;  // gradient of the dt pair (t-1, t) w.r.t. window t-1
     if (dt_terms && t0 >= 1) {
         const float* fp = flow_of(a, b, t0 - 1);
         gprev = pg(fp[p], fp[HWp + p], mask_of(a, b, t0 - 1)[p], cx, cy, cm);
     }
     for (int t = t0; t < t1; ++t) {
-        const float* fx = flow_of(a, b, t);
-        const float* fy = fx + HWp;
-        const float* m = mask_of(a, b, t);
-        float acc = 0.0f;
-        // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
-        auto fwd = [&](int q) { return pg(cx, cy, cm, fx[q], fy[q], m[q]); };
-        auto bwd = [&](int q) { return pg(fx[q], fy[q], m[q], cx, cy, cm); };
-        if (w + 1 < a.W) acc += fwd(p + 1);
-        if (w >= 1) acc -= bwd(p - 1);
-        if (h + 1 < a.H) acc += fwd(p + a.W);
-        if (h >= 1) acc -= bwd(p - a.W);
-        if (h + 1 < a.H && w + 1 < a.W) acc += fwd(p + a.W + 1);
-        if (h >= 1 && w >= 1) acc -= bwd(p - a.W - 1);
-        if (h >= 1 && w + 1 < a.W) acc += fwd(p - a.W + 1);
-        if (h + 1 < a.H && w >= 1) acc -= bwd(p + a.W - 1);
-        float nx = 0.0f, ny = 0.0f, nm = 0.0f, gnext = 0.0f;
+        float nX[8], nY[8], nM[8];
+        const bool more = t + 1 < t1;
+        if (more) load_nb(t + 1, nX, nY, nM);
+        float nx = 0.0f, ny = 0.0f, nm = 0.0f;
         if (t + 1 < a.tf) {
             const float* f2 = flow_of(a, b, t + 1);
             nx = f2[p];
             ny = f2[HWp + p];
             nm = mask_of(a, b, t + 1)[p];
-            if (dt_terms) {
-                gnext = pg(cx, cy, cm, nx, ny, nm);
-                acc += gnext;
-            }
+        }
+        float acc = 0.0f;
+        // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            if (!ok[q]) continue;
+            if (q % 2 == 0) acc += pg(cx, cy, cm, X[q], Y[q], M[q]);
+            else acc -= pg(X[q], Y[q], M[q], cx, cy, cm);
+        }
+        float gnext = 0.0f;
+        if (t + 1 < a.tf && dt_terms) {
+            gnext = pg(cx, cy, cm, nx, ny, nm);
+            acc += gnext;
         }
         if (dt_terms && t >= 1) acc -= gprev;
         float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
@@ -499,6 +552,14 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
         cx = nx;
         cy = ny;
         cm = nm;
+        if (more) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                X[q] = nX[q];
+                Y[q] = nY[q];
+                M[q] = nM[q];
+            }
+        }
     }
 }
 
