@@ -164,7 +164,7 @@ typedef std::conditional_t<kSplatFixed, SplatLdsX, SplatLdsF> SplatLds;
 // Events per thread and pass: their loads (event, polarity, then the flow gather) are all issued
 // before any of them is splatted, so a thread waits for one chain of dependent loads per SPLAT_U
 // events instead of per event.
-constexpr int SPLAT_U = 4;
+constexpr int SPLAT_U = 4;  // (8, one round of dependent loads per thread at cfg2: measured no faster)
 
 // Partial image sets per band: enough blocks for one per CU (256), at most SPLAT_SPLIT.
 __host__ __device__ inline int splat_nsplit(int B, int nbands) {
@@ -651,13 +651,23 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_a
     const int p0 = band * SPLAT_BAND;
     const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
     for (int j = tid; j < 2 * SPLAT_BAND; j += SPLAT_NT) (&img.hi[0][0])[j] = 0, (&img.lo[0][0])[j] = 0;
+    // the band's current g_flows values (the pixel backward's), read ahead of the event loop
+    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
+    constexpr int GFR = 2 * SPLAT_BAND / SPLAT_NT;
+    float gold[GFR];
+#pragma unroll
+    for (int k = 0; k < GFR; ++k) {
+        const int j = tid + k * SPLAT_NT, c = j / SPLAT_BAND, q = j - c * SPLAT_BAND;
+        gold[k] = q < np ? gf[c * HWp + q] : 0.0f;
+    }
     __syncthreads();
     const int i0 = a.tf == 1 ? 0 : a.off[t], i1 = a.tf == 1 ? a.M : a.off[t + 1];
     for (int i = i0 + tid; i < i1; i += SPLAT_NT) {
         const EventRef r = event_ref(wt, a.T, b, i);
+        // the event's flow gradients load alongside its position (one round trip, not two)
+        const float2 g = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i));
         const int q = (int)(r.ev[1] * (float)a.W + r.ev[2]) - p0;
         if (q < 0 || q >= np) continue;
-        const float2 g = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i));
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             // clamped to |d| <= 2^30 (a per-event flow gradient beyond that is not a number this sum can
@@ -671,11 +681,12 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_a
         }
     }
     __syncthreads();
-    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
-    for (int j = tid; j < 2 * np; j += SPLAT_NT) {
-        const int c = j / np, q = j - c * np;
+#pragma unroll
+    for (int k = 0; k < GFR; ++k) {
+        const int j = tid + k * SPLAT_NT, c = j / SPLAT_BAND, q = j - c * SPLAT_BAND;
+        if (q >= np) continue;
         const unsigned long long h = img.hi[c][q], l = img.lo[c][q];
-        if (h | l) gf[c * HWp + q] += (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75);
+        if (h | l) gf[c * HWp + q] = gold[k] + (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75);
     }
 }
 
