@@ -1081,6 +1081,48 @@ def test_forward_sequence_final_state_out(dev):
             mb.forward_sequence(None, xs[:T])
 
 
+def test_forward_sequence_unread_state_writes(dev):
+    """The window leaves out the spike half of the feed-forward layers' intermediate states
+    (state_spk_skip, C = 8) and the membrane half of the internal state gradients; a run that keeps
+    every step's states (capture_states: nothing skipped) gives the same flows, parameter gradients
+    and final states bit for bit, and its per-step states are complete (finite) everywhere."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(9)
+    H = W = 32
+    T, B, C = 4, 2, 8
+    ma = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=C)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    mb.engine.capture_states = True
+    gen = torch.Generator(device=dev).manual_seed(5)
+    xs = [(torch.rand(B, 2, H, W, generator=gen, device=dev) < 0.2).float() * 3 for _ in range(2 * T)]
+    out = {}
+    for tag, m in (("skip", ma), ("keep", mb)):
+        flows, grads = [], []
+        for k in range(2):
+            outs = m.forward_sequence(None, xs[k * T:(k + 1) * T])
+            if tag == "keep":
+                for sts in m.engine.seq_states:
+                    assert all(bool(torch.isfinite(s).all()) for s in sts)
+                m.engine.seq_states = None
+            sum(o["flow"][0].square().sum() for o in outs).backward()
+            flows += [o["flow"][0].detach().cpu() for o in outs]
+            grads.append([p.grad.detach().cpu().clone() for p in m.parameters()])
+            m.zero_grad(set_to_none=True)
+            m.detach_states()
+        out[tag] = (flows, grads, [s.detach().cpu() for s in m._states])
+    for a, b in zip(out["skip"][0], out["keep"][0]):
+        assert torch.equal(a, b)
+    for ga, gb in zip(out["skip"][1], out["keep"][1]):
+        for a, b in zip(ga, gb):
+            assert torch.equal(a, b)
+    for a, b in zip(out["skip"][2], out["keep"][2]):
+        assert torch.equal(a, b)
+
+
 def test_forward_sequence_eval_mode_and_fallbacks(dev):
     """Eval mode (running statistics, no running-stat update) through the wavefront launches
     matches per-step eval; T = 1 and log=True take the per-step path with the same results."""
