@@ -403,7 +403,8 @@ def main():
     if rank == 0:
         line = {
             "metric": (f"events/sec (train step) SpikingRecEVFlowNet T={T} {R}x{R}" if unet
-                       else "events/sec (train step) LIFFireNet T=10 128x128"),
+                       else f"events/sec (train step) LIFFireNet T={T} {R}x{R}"
+                       + (f" C={args.channels}" if args.channels != 8 else "")),
             "value": round(value, 1), "unit": "events/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
@@ -680,7 +681,9 @@ def _firenet_roofline(kern, model, args, B, R, T):
                for k, (n, t) in sorted(classes.items(), key=lambda kv: -kv[1][1])}
     roofline = {"bound": "hbm", "kernel": dominant, "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": _pmc_traffic(dominant, args), "bytes_per_launch": abytes, "avg_us": round(avg_us, 2)}
+                "traffic": _pmc_traffic(dominant, args),
+                "traffic_source": "committed PMC (profiles/pmc_traffic.json, separate rocprofv3 --pmc passes), not live",
+                "bytes_per_launch": abytes, "avg_us": round(avg_us, 2)}
     return roofline, kernels
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 33
+#define SNNFLOW_ABI_VERSION 34
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -125,11 +125,6 @@ typedef struct snnflow_conv_fwd_args {
     /* ABI 15, optional: bf16 fragments of wt_ff_t / wt_rec_t (snnflow_prep_desc.frag_fwd) for the
      * spike convs of the cin == c kernels at c = 16, 32 (else split in the kernel) */
     const uint16_t* wf_ff; const uint16_t* wf_rec;
-    /* ABI 28, optional (wavefront launches, c = 8 LIF-fed tasks): a zero-initialised int through which
-     * the task's blocks hand out its tiles dynamically (blocks that finish early take more tiles, and
-     * blocks of the launch's other such tasks take the rest once theirs are done); the call leaves it
-     * nonzero, so every launch needs a fresh zeroed counter.  NULL: a static tile assignment. */
-    int* tile_counter;
     /* ABI 33: 1 = store only the membrane half of prev_state (a caller whose spike half is never read:
      * a feed-forward layer's intermediate time steps in a window -- the backward recomputes the spikes) */
     int state_spk_skip;

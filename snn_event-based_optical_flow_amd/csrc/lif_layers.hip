@@ -2905,7 +2905,7 @@ __device__ inline void globalize(snnflow_conv_fwd_args& a) {
     SNN_G(a.x); SNN_G(a.prev_y); SNN_G(a.prev_mem); SNN_G(a.prev_acc); SNN_G(a.prev_stats);
     globalize(a.prev);
     SNN_G(a.prev_state); SNN_G(a.wt_ff); SNN_G(a.wt_rec); SNN_G(a.wt_ff_t); SNN_G(a.wt_rec_t); SNN_G(a.s_prev);
-    SNN_G(a.y); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1); SNN_G(a.wf_ff); SNN_G(a.wf_rec); SNN_G(a.tile_counter);
+    SNN_G(a.y); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1); SNN_G(a.wf_ff); SNN_G(a.wf_rec);
 }
 __device__ inline void globalize(snnflow_lif_fwd_args& a) {
     SNN_G(a.y); SNN_G(a.mem); SNN_G(a.acc); SNN_G(a.stats);
@@ -3033,41 +3033,14 @@ __host__ __device__ inline int pipe_tiles(const Grid& g, int ntiles) {
     return g.bid < ntiles ? (ntiles - 1 - g.bid) / g.nb + 1 : 0;
 }
 
-// The tiles of a pipelined block.  Static (no tile counter): v = bid, bid + nb, ...  Dynamic
-// (snnflow_conv_fwd_args.tile_counter): the first tile v = bid (the task's own blocks), then tiles
-// v = nfirst + atomicAdd(counter, 1) while v < ntiles, requested one tile ahead (the request of tile
-// k + 2 is issued at the top of tile k and its answer written to LDS at the end of tile k), so a
-// block that runs fast takes more tiles and the task's blocks finish together.  (Steal mode, a block
-// taking tiles of another task of the launch once its own are done, needs a second inlined body at a
-// run-time-chosen task: 49 spilled registers -- not kept; the host sizes the tasks' block counts by
-// their per-tile cost instead, snnflow_fwd_slot.)
-struct PipeSeq {
-    int* ctr;     // NULL: static
-    int nfirst;   // tiles handed out statically (v < nfirst)
-    int ntiles, bid, nb;
-    __device__ int first(bool steal, int* slot) const {
-        if (!steal) return bid < ntiles ? bid : -1;
-        if (threadIdx.x == 0) slot[0] = grab_now();
-        __syncthreads();
-        const int v = __builtin_amdgcn_readfirstlane(slot[0]);  // (block-uniform: scalar registers)
-        __syncthreads();
-        return v;
-    }
-    __device__ int grab_now() const {
-        const int v = nfirst + atomicAdd(ctr, 1);
-        return v < ntiles ? v : -1;
-    }
-    __device__ int static_next(int v) const { return v + nb < ntiles ? v + nb : -1; }
-};
-
-// Per-block scheduling state in LDS (the dynamic request's answer)
+// Per-block scheduling state in LDS (the recurrent input's two alternating exactness flags)
 __device__ inline int* pipe_slot() {
     __shared__ int slot[4];
     return slot;
 }
 
 template <bool REC>
-__device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, float* pool, bool steal = false) {
+__device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, float* pool) {
     constexpr int C = 8, NTB = 2 * NT, R = Halo4<C, NTB>::R;
     using L = PipeFwdLds<REC>;
     char* const lds = reinterpret_cast<char*>(pool);
@@ -3076,14 +3049,10 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int H = a.H, W = a.W, ntiles = a.B * tiles_per_image(H, W);
-    const PipeSeq seq{a.tile_counter, g.nb < ntiles ? g.nb : ntiles, ntiles, g.bid, g.nb};
-    const bool dyn = a.tile_counter != nullptr;
     int* const slot = pipe_slot();
-    int v_cur = seq.first(steal, slot);
-    if (v_cur < 0) return;  // (steal mode: nothing left; block-uniform)
-    int req = -1;
-    if (dyn && tid == 0) req = seq.grab_now();
-    const bool lead = !steal && g.bid == 0;
+    int v_cur = g.bid < ntiles ? g.bid : -1;  // tiles v = bid, bid + nb, ...
+    if (v_cur < 0) return;
+    const bool lead = g.bid == 0;
     const bool has_mem = a.prev_mem != nullptr;
     const bool has_rec = REC && a.s_prev != nullptr;
     TRACE_AT(true, REC ? 1 : 0, 0);
@@ -3132,12 +3101,11 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
     if (has_rec) load_sprev(tl, tid);
     if (a.prev.bn_train) acc_gather_reduce<2 * C>(gat, sums);
     TRACE_AT(true, REC ? 1 : 0, 1);
-    lif_prologue(a.prev, nr, sums, C, (double)a.B * H * W, steal ? nullptr : a.prev_stats, coef, nullptr, lead);
+    lif_prologue(a.prev, nr, sums, C, (double)a.B * H * W, a.prev_stats, coef, nullptr, lead);
     TRACE_AT(true, REC ? 1 : 0, 2);
     fz_ff.store(reinterpret_cast<__bf16*>(lds + L::FF));
     if (has_rec) fz_rec.store(reinterpret_cast<__bf16*>(lds + L::FR));
-    if (!steal) zero_consumed(a.zero0, a.zero1, a.zero_n, g);
-    if (dyn && tid == 0) slot[1] = req;
+    zero_consumed(a.zero0, a.zero1, a.zero_n, g);
     if (tid == 0) slot[2] = 0;  // the s_prev exactness flag of tile 0
 
     const bool zr = a.prev.zero_reset != 0, spk_skip = a.state_spk_skip != 0;
@@ -3196,8 +3164,7 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
         __syncthreads();
         const bool rec_bf = has_rec && bad[k & 1] == 0;
         TRACE_AT(k < 2, REC ? 1 : 0, 5 + 3 * k);
-        const int v_nxt = dyn ? __builtin_amdgcn_readfirstlane(slot[1]) : seq.static_next(v_cur);
-        if (dyn && tid == 0 && v_nxt >= 0) req = seq.grab_now();
+        const int v_nxt = v_cur + g.nb < ntiles ? v_cur + g.nb : -1;
         const Tile cur = tl;
         if (v_nxt >= 0) {
             tl = block_tile(H, W, Grid{v_nxt, ntiles});
@@ -3271,7 +3238,6 @@ __device__ void fwd_lif8_pipe(const snnflow_conv_fwd_args& a, const Grid g, floa
             }
         }
         TRACE_AT(k < 2, REC ? 1 : 0, 6 + 3 * k);
-        if (dyn && tid == 0) slot[1] = v_nxt >= 0 ? req : -1;
         v_cur = v_nxt;
     }
 
@@ -4427,8 +4393,6 @@ static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 2);
 static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
 // Block order of a C = 8 launch with pipelined tasks: 0 layer order, 1 pipelined tasks first, 2 last
 static int g_pipe_order = env_int("SNNFLOW_PIPE_ORDER", 1);
-// Blocks of a recurrent pipelined task relative to a feed-forward one, percent (dynamic tiles only)
-static int g_pipe_recw = env_int("SNNFLOW_PIPE_RECW", 150);
 
 // Blocks of a pipelined task: ceil(tiles / tpb), a multiple of 8 (block_tile's XCD groups).
 static int pipe_blocks(int ntiles, int tpb) {
@@ -4480,11 +4444,8 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
         p.conv[i] = a;
         p.nblk[i] = snnflow_conv_blocks(B, H, W);
         if (c == 8 && g_pipe_fwd > 0 && (kind == SK_LIF || kind == SK_LIF_REC) && pipe_fits(B, H, W, c)) {
-            // a recurrent tile costs ~1.5x a feed-forward one (two convs, the s_prev halo): its task
-            // gets g_pipe_recw percent of the blocks, so that with dynamic tiles both finish together
             const int nt = p.nblk[i];
-            p.nblk[i] = kind == SK_LIF_REC && a.tile_counter ? pipe_blocks((int)((int64_t)nt * g_pipe_recw / 100), g_pipe_fwd)
-                                                             : pipe_blocks(nt, g_pipe_fwd);
+            p.nblk[i] = pipe_blocks(nt, g_pipe_fwd);
             if (p.nblk[i] > (nt + 7) / 8 * 8) p.nblk[i] = (nt + 7) / 8 * 8;
             kind = kind == SK_LIF ? SK_LIF_P : SK_LIF_REC_P;
         }

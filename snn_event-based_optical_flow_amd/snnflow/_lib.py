@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 33
+ABI_VERSION = 34
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -39,7 +39,7 @@ class ConvFwdArgs(ctypes.Structure):
                 ("prev", Neuron), ("prev_state", P),
                 ("wt_ff", P), ("wt_rec", P), ("wt_ff_t", P), ("wt_rec_t", P), ("s_prev", P),
                 ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32),
-                ("wf_ff", P), ("wf_rec", P), ("tile_counter", P), ("state_spk_skip", I32)]
+                ("wf_ff", P), ("wf_rec", P), ("state_spk_skip", I32)]
 
 
 class EvalFwdArgs(ctypes.Structure):

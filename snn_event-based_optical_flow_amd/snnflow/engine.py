@@ -16,7 +16,6 @@ by the first step of the window ("root"), so autograd performs no per-step
 gradient additions.
 """
 import ctypes
-import functools
 import operator
 
 import torch
@@ -897,64 +896,6 @@ def _ptr_t(t):
 # ---------------------------------------------------------------------------
 # A whole truncated-BPTT window in one autograd node, launched in wavefront order
 # ---------------------------------------------------------------------------
-@functools.lru_cache(maxsize=64)
-def capped_slots(T, K, rec, cap):
-    """Launch order of the (kernel k < K, step t < T) grid with at most `cap` tasks per launch,
-    from its exact dependencies: (k-1, t), (k, t-1), and (k+1, t-1) where rec[k] (a recurrent
-    layer reads spikes the next kernel of the previous step wrote).  List scheduling, longest
-    remaining dependency chain first.  A task is one 512-block layer-step at cfg2 and a launch
-    runs in rounds of 768 resident blocks: three tasks are exactly two rounds, four take a
-    third, 2/3-full round -- wavefront_slots' 26 launches are 62 rounds, this schedule (cap 3)
-    29 launches and 56 rounds (measured slower all the same: see slot_cap).
-    Returns [[(k, t), ...] per launch]."""
-    if cap <= 0:
-        return wavefront_slots(T, K)
-
-    def deps(k, t):
-        d = []
-        if k >= 1:
-            d.append((k - 1, t))
-        if t >= 1:
-            d.append((k, t - 1))
-            if k + 1 < K and rec[k]:
-                d.append((k + 1, t - 1))
-        return d
-    tasks = [(k, t) for t in range(T) for k in range(K)]
-    succ = {x: [] for x in tasks}
-    for x in tasks:
-        for d in deps(*x):
-            succ[d].append(x)
-    chain = {}
-    for x in reversed(tasks):  # successors come later in (t, k) order
-        chain[x] = 1 + max((chain[y] for y in succ[x]), default=0)
-    done, launches = set(), []
-    while len(done) < len(tasks):
-        ready = [x for x in tasks if x not in done and all(d in done for d in deps(*x))]
-        ready.sort(key=lambda x: (-chain[x], x[1], x[0]))
-        pick = ready[:cap]
-        launches.append(pick)
-        done.update(pick)
-    return launches
-
-
-def _pipe_dynamic():
-    """Dynamic tile hand-out for the C = 8 tile pipelines (snnflow_conv_fwd_args.tile_counter), opt-in
-    with SNNFLOW_PIPE_DYN=1.  Measured slower (cfg2 fwd slot 19.4 -> 25.3 us, step 1.45 -> 1.60 ms,
-    profiles/r04/ab_pipe_dynamic.txt): the ~512 returning atomics per task on one counter word
-    serialise (~90 per us per word) and stall the requesting wave."""
-    import os
-    return os.environ.get("SNNFLOW_PIPE_DYN", "0") == "1"
-
-
-def slot_cap():
-    """Tasks per slot launch (SNNFLOW_SLOT_CAP; 0, the default: the plain wavefront order).  Measured
-    (profiles/r03/ab_slot_cap.txt): cap 3 is slower at cfg2 (1.545-1.552 vs 1.491-1.504 ms: a
-    3-task launch takes 28.4 / 20.1 us against 30.5 / 21.3 us for 4 tasks, so the time follows the
-    work, not the block rounds) and at C = 32 (6.56 vs 6.50 ms)."""
-    import os
-    return int(os.environ.get("SNNFLOW_SLOT_CAP", "0"))
-
-
 def wavefront_slots(T, K):
     """Launch order of a (kernel k < K, step t < T) grid whose task (k, t) reads the outputs of
     (k-1, t), (k, t-1) and (k+1, t-1) (the spikes of a recurrent layer come out of the next
@@ -1051,26 +992,21 @@ class FireNetSequence(torch.autograd.Function):
         neurons = eng.neurons()
         train = [bn.training or not bn.track_running_stats for bn in eng.bns]
 
-        frec = tuple(bool(eng.rec[k]) if k < L else False for k in range(L + 1))
         # with the weight gradients fused into the backward (C = 8) the spike half of a feed-forward
         # layer's state at steps t < T-1 is never read (the next step's LIF reads the membrane half,
         # the backward recomputes the spikes, only recurrent layers read s_prev; the deferred weight
         # gradients of the other widths read the spikes), so it is not stored unless the caller
         # keeps every step's states
+        fuse = bool(eng.fuse_wgrad)  # decided once: the backward must see the same choice (ctx.fuse)
+
         def spk_skip(l, t):
-            return eng.fuse_wgrad and t < T - 1 and not eng.rec[l] and not eng.keep_seq_states
-        launches = capped_slots(T, L + 1, frec, slot_cap())
-        # dynamic tile hand-out of the C = 8 tile pipelines: one zeroed counter per task and launch
-        ctr = (torch.zeros(len(launches) * _lib.MAX_SLOT_TASKS, dtype=torch.int32, device=dev)
-               if C == 8 and _pipe_dynamic() else None)
-        for li, tasks in enumerate(launches):
+            return fuse and t < T - 1 and not eng.rec[l] and not eng.keep_seq_states
+        for tasks in wavefront_slots(T, L + 1):
             convs, top = [], None
             for k, t in tasks:
                 if k < L:
                     a = _fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
                                        s_prev[t], facc[t], neurons, train, wfwd, wbwd)
-                    if ctr is not None and k >= 1:
-                        a.tile_counter = ctr.data_ptr() + 4 * (li * _lib.MAX_SLOT_TASKS + len(convs))
                     if k >= 1 and spk_skip(k - 1, t):
                         a.state_spk_skip = 1
                     convs.append(a)
@@ -1093,6 +1029,7 @@ class FireNetSequence(torch.autograd.Function):
 
         ctx.eng = eng
         ctx.T = T
+        ctx.fuse = fuse
         ctx.root = root
         ctx.ext = ext
         ctx.shape = (B, H, W, cin0)
@@ -1138,8 +1075,10 @@ class FireNetSequence(torch.autograd.Function):
             eng.open_chain(dev)
         glayers, gpw, gpb = eng.grad_views()
         neurons = eng.neurons()
-        bacc = ctx.bacc  # zeroed in the forward (prep launch)
+        bacc = ctx.bacc  # zeroed in the forward (prep launch); a second backward (retain_graph) gets a fresh one
         ctx.bacc = None
+        if bacc is None:
+            bacc = torch.zeros(T, L, _lib.acc_storage(_lib.bwd_acc_len(C)), dtype=torch.float64, device=dev)
         gcur = torch.empty(T, L, B, H, W, C, device=dev)
         bnc = torch.empty(T, L, 2, C, device=dev)
 
@@ -1172,7 +1111,9 @@ class FireNetSequence(torch.autograd.Function):
             gfl.append(g)
 
         # the deferred weight gradients see the steps in the per-step path's order (last first)
-        fuse = eng.fuse_wgrad  # layers >= 1: dW inside the backward slot tasks (wslab_*)
+        # layers >= 1: dW inside the backward slot tasks (wslab_*); the forward's choice (it skipped the
+        # spike planes the fused form never reads), not the engine flag's value now
+        fuse = ctx.fuse
         for t in range(T - 1, -1, -1):
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys[t]), _Rows(stats[t]), xs[t], states[t], s_prev[t],
                                 (gcur, bnc, ys, stats)))
@@ -1183,8 +1124,7 @@ class FireNetSequence(torch.autograd.Function):
             # (the BN-backward sums of layer L-j), (j, tau-1) (the membrane gradient from step t+1),
             # and (j+1, tau-1) where layer L-j-1 is recurrent (its spikes' gradient from the
             # recurrent dgrad of step t+1)
-            brec = tuple(bool(eng.rec[L - 1 - j]) if j < L else False for j in range(L + 1))
-            for tasks in capped_slots(T, L + 1, brec, slot_cap()):
+            for tasks in wavefront_slots(T, L + 1):
                 layers, top = [], None
                 for j, tau in tasks:
                     t = T - 1 - tau
@@ -1237,16 +1177,22 @@ class FireNetSequence(torch.autograd.Function):
         return (None, None, *gxs, *g0, *pgrads)
 
 
-def eval_fused_ok(eng, x):
+def eval_fused_ok(eng, xs, prev=()):
     """True if forward_sequence may take the fused evaluation launches (eval_sequence): C = 8, every
-    BatchNorm on running statistics, no autograd needed, 2- or 4-bin input on the GPU, and not
-    disabled by SNNFLOW_EVAL_FUSED=0 (the train-path split launches then run in eval mode too)."""
+    BatchNorm on running statistics, no autograd needed -- neither the parameters nor any input or
+    initial state require grad while grad mode is on (saliency / adversarial evaluation keeps the
+    autograd path) --, 2- or 4-bin input on the GPU, and not disabled by SNNFLOW_EVAL_FUSED=0 (the
+    train-path split launches then run in eval mode too)."""
     import os
+    x = xs[0]
     if os.environ.get("SNNFLOW_EVAL_FUSED", "1") == "0" or eng.C != 8 or not x.is_cuda or x.shape[1] not in (2, 4):
         return False
     if any(bn.training or not bn.track_running_stats for bn in eng.bns):
         return False
-    return not (torch.is_grad_enabled() and any(p.requires_grad for p in eng.param_list()))
+    if not torch.is_grad_enabled():
+        return True
+    return not (any(p.requires_grad for p in eng.param_list()) or any(t.requires_grad for t in xs)
+                or any(p is not None and p.requires_grad for p in prev))
 
 
 def eval_sequence(eng, xs, prev):

@@ -105,10 +105,16 @@ class AEE(BaseValidationLoss):
         dtg = torch.as_tensor(self._dt_gt, dtype=torch.float32, device=flow.device).reshape(-1).contiguous()
         dti = torch.as_tensor(self._dt_input, dtype=torch.float32, device=flow.device).reshape(-1).contiguous()
         n = lib.snnflow_aee_acc_doubles(B, H, W)
-        acc = self.__dict__.get("_aee_acc")
-        if acc is None or acc.numel() < n or acc.device != flow.device:
+        # the scratch carries the kernel's completion counter acc[0] (zero between calls: the last
+        # block resets it), so it must never be shared by launches that can overlap: one scratch per
+        # stream (a graph replays on the stream it was captured on, in order with eager calls there)
+        stream = _lib.stream_ptr(flow.device)
+        scratch = self.__dict__.setdefault("_aee_acc", {})
+        key = (flow.device, stream)
+        acc = scratch.get(key)
+        if acc is None or acc.numel() < n:
             acc = torch.zeros(n, dtype=torch.float64, device=flow.device)  # counter acc[0]: zero, kept zero
-            self._aee_acc = acc
+            scratch[key] = acc
         aee = torch.empty(B, device=flow.device)
         pct = torch.empty(B, device=flow.device)
         a = _lib.AeeArgs()
@@ -117,7 +123,11 @@ class AEE(BaseValidationLoss):
         a.dt_gt, a.dt_input, a.dt_gt_n, a.dt_input_n = ptr(dtg), ptr(dti), dtg.numel(), dti.numel()
         a.flow_scaling = float(self.flow_scaling)
         a.acc, a.aee, a.percent = ptr(acc), ptr(aee), ptr(pct)
-        _lib.call("aee", lib.snnflow_aee, ctypes.byref(a), _lib.stream_ptr(flow.device))
+        try:
+            _lib.call("aee", lib.snnflow_aee, ctypes.byref(a), stream)
+        except Exception:
+            scratch.pop(key, None)  # a refused or failed launch may leave the counter nonzero: fresh scratch next time
+            raise
         return aee, pct
 
 

@@ -201,7 +201,7 @@ class _FireNetBase(BaseModel):
         logging = isinstance(log, bool) and log and not self.exporting
         eng.keep_seq_states = logging or eng.capture_states
         try:
-            if eval_fused_ok(eng, xs[0]):  # eval mode, no autograd: conv + BN + LIF fused per task
+            if eval_fused_ok(eng, xs, self._states):  # eval mode, no autograd: conv + BN + LIF fused per task
                 flows, fin = eval_sequence(eng, xs, list(self._states))
                 res = list(flows) + list(fin)
             else:

@@ -92,6 +92,21 @@ class ClipAdam(torch.optim.Optimizer):
             return None
         return c[3], base
 
+    def state_dict(self):
+        """torch.optim.Adam's state-dict form: every parameter's ``step`` is its own CPU float32
+        tensor (a copy of the shared device counter, which stays internal).  A shared tensor would
+        be incremented once per parameter by torch's Adam after ``load_state_dict`` (the reference
+        saves ``optimizer.state_dict()`` in its checkpoints, train_flow.py:131-150)."""
+        sd = super().state_dict()
+        state = {}
+        for k, st in sd["state"].items():
+            st = dict(st)  # super() hands out this optimizer's own per-parameter dicts
+            if isinstance(st.get("step"), torch.Tensor):
+                st["step"] = st["step"].detach().to("cpu", torch.float32, copy=True)
+            state[k] = st
+        sd["state"] = state
+        return sd
+
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._args_cache = None  # the loaded moments replace the flat buffers' views (re-read by _state)

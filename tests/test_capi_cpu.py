@@ -275,3 +275,39 @@ def test_tebn_mpbn_model_loads_reference_state_dict_strict():
     model.load_state_dict({k[3:]: torch.from_numpy(np.asarray(v)) for k, v in g.items() if k.startswith("p0.")},
                           strict=True)
     assert model.G1.tebn_enabled and model.G1.mpbn_enabled and model._cellwise()
+
+
+def test_clip_adam_state_dict_loads_into_torch_adam():
+    """ClipAdam keeps ONE device step counter for all parameters internally; its state dict must
+    still be torch.optim.Adam's form (one step tensor per parameter), so that the reference's
+    optimizer continues correctly from a saved optimizer_state_dict (train_flow.py:131-150):
+    after one torch Adam step every parameter's step is n + 1 (a shared tensor would be n + P)."""
+    import torch
+
+    import snnflow
+
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(s)) for s in ((3, 4), (5,), (2, 2, 3))]
+    opt = snnflow.ClipAdam(params, lr=1e-3, max_norm=1.0)
+    _, ea, es, step, _ = opt._state(params)  # the persistent flat moments (no kernel runs)
+    ea.normal_()
+    es.uniform_(0.1, 1.0)
+    step.fill_(4.0)
+    sd = opt.state_dict()
+    steps = [sd["state"][i]["step"] for i in range(len(params))]
+    assert all(s.device.type == "cpu" and s.dtype == torch.float32 and float(s) == 4.0 for s in steps)
+    assert len({id(s) for s in steps}) == len(params)
+    assert float(step) == 4.0 and opt.state[params[0]]["step"] is step  # the internal counter untouched
+    twin = [torch.nn.Parameter(p.detach().clone()) for p in params]
+    topt = torch.optim.Adam(twin, lr=1e-3, foreach=False)
+    topt.load_state_dict(sd)
+    for t in twin:
+        t.grad = torch.ones_like(t)
+    topt.step()
+    assert [float(topt.state[t]["step"]) for t in twin] == [5.0] * len(params)
+    # and back: a fresh ClipAdam picks the counter up from the per-parameter entries
+    opt2 = snnflow.ClipAdam(params, lr=1e-3, max_norm=1.0)
+    opt2.load_state_dict(topt.state_dict())
+    m = opt2._state(params)
+    assert float(m[3]) == 5.0
+    assert torch.equal(m[1][:12], topt.state[twin[0]]["exp_avg"].reshape(-1))

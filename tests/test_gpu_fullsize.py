@@ -432,3 +432,143 @@ def test_clip_adam_matches_torch(dev, C):
         m = opt2._state([p for p in model.parameters()])
         assert float(m[3]) == 4.0
         np.testing.assert_array_equal(m[1].cpu().numpy(), opt._moments[1].cpu().numpy())
+
+
+def _window_run(dev, wins, C, keep):
+    """forward_sequence + EventWarping + backward of one window at full size, with the engine either
+    keeping every step's states (capture_states: nothing skipped, as test_cfg2_train_step_vs_oracle
+    runs it) or not (the bench: the unread spike planes and state-gradient halves are skipped)."""
+    import snnflow
+
+    model = _new_model(C).to(dev).train()
+    B, _, H, W = wins[0]["event_cnt"].shape
+    model.engine.capture_states = keep
+    outs = model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+    if keep:
+        model.engine.seq_states = None
+    ew = snnflow.EventWarping(_cfg(H, W), dev)
+    for o, w in zip(outs, wins):
+        ew.event_flow_association(o["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+    loss = ew()
+    loss.backward()
+    return ([o["flow"][0].detach().cpu() for o in outs], loss.item(),
+            [p.grad.detach().cpu().clone() for p in model.parameters()], [s.detach().cpu() for s in model._states])
+
+
+@pytest.mark.parametrize("tag,B,H", [("cfg2", 8, 128), ("cfg3", 4, 256)], ids=["cfg2", "cfg3"])
+def test_bench_window_skips_bit_identical(dev, tag, B, H):
+    """The bench's exact window at full size: test_cfg2_train_step_vs_oracle runs forward_sequence with
+    capture_states on, which keeps every write; the bench runs it off, which skips the spike half of the
+    feed-forward layers' intermediate states (state_spk_skip) and the membrane half of the internal
+    state gradients.  Same windows as the oracle test (seed 1, T = 10 x 1000 events, C = 8): flows, loss,
+    every parameter gradient and the final states must be the same bits.  (Run-to-run, the fp64
+    batch-sum atomics could reorder; the sums round to fp32 identically in practice -- a mismatch here
+    names the tensor.)"""
+    from snnflow.synthetic import make_window
+
+    T, N, C = 10, 1000, 8
+    gen = torch.Generator(device=dev).manual_seed(1)
+    wins = [make_window(B, N, H, H, gen, dev) for _ in range(T)]
+    keep = _window_run(dev, wins, C, True)
+    skip = _window_run(dev, wins, C, False)
+    for t, (a, b) in enumerate(zip(keep[0], skip[0])):
+        assert torch.equal(a, b), f"flow of step {t}"
+    assert keep[1] == skip[1], (keep[1], skip[1])
+    names = [n for n, _ in _new_model(C).named_parameters()]
+    for n, a, b in zip(names, keep[2], skip[2]):
+        assert torch.equal(a, b), f"gradient of {n}: max |d| {float((a - b).abs().max()):.3e}"
+    for l, (a, b) in enumerate(zip(keep[3], skip[3])):
+        assert torch.equal(a, b), f"final state of layer {l}"
+    print(f"\n[{tag}] capture on / off: loss {keep[1]:.9g}, {len(names)} gradients, {len(keep[3])} final states identical")
+
+
+def test_bench_graph_pingpong_matches_eager(dev):
+    """The bench's timed step itself (bench.py main, N = 1): one HIP graph per resident batch and state
+    parity holding forward_sequence + EventWarping + backward + ClipAdam, the states handed over
+    copy-free through bench.StatePingPong -- replayed twice at cfg2 (128x128, B = 8, T = 10 x 1000
+    events, C = 8) against the same two steps run eagerly (forward_sequence, loss, backward,
+    ClipAdam.step, detach_states) from the same initial parameters, moments and (zero) states.  Loss,
+    every parameter, the Adam moments and the handed-over states must be the same bits after each step."""
+    import bench
+    import snnflow
+    from snnflow.parser import train_snn_model_kwargs
+    from snnflow.synthetic import make_window
+
+    B, R, T, N = 8, 128, 10, 1000
+    gen = torch.Generator(device=dev).manual_seed(11)
+    pool = [bench._pack([make_window(B, N, R, R, gen, dev) for _ in range(T)]) for _ in range(2)]
+    seed = torch.ones((), device=dev)
+
+    def build():
+        torch.manual_seed(0)
+        m = snnflow.LIFFireNet(train_snn_model_kwargs("LIFFireNet", base_num_channels=8)).to(dev).train()
+        return m, snnflow.EventWarping(_cfg(R, R), dev), snnflow.ClipAdam(list(m.parameters()), lr=2e-4, max_norm=1.0)
+
+    def fwd_bwd(m, lf, views):
+        lf.reset()
+        outs = m.forward_sequence([w["event_voxel"] for w in views], [w["event_cnt"] for w in views])
+        for t in range(T):
+            w = views[t]
+            lf.event_flow_association(outs[t]["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+        loss = lf()
+        loss.backward(seed)
+        return loss
+
+    def snap(m, opt):
+        _, ea, es, _, _ = opt._moments
+        return [p.detach().cpu().clone() for p in m.parameters()], ea.cpu().clone(), es.cpu().clone()
+
+    # eager reference: two steps from the fresh model (zero initial states)
+    me, lfe, oe = build()
+    want = []
+    for j in range(2):
+        oe.zero_grad(set_to_none=True)
+        loss = fwd_bwd(me, lfe, pool[j][1])
+        oe.step()
+        want.append((loss.item(), snap(me, oe), [s.detach().cpu() for s in me._states]))
+        me.detach_states()
+
+    # the bench's graphs: warm up eagerly (workspaces, optimizer state), capture, then restore the
+    # initial parameters / buffers / moments in place and zero both ping-pong buffers
+    mg, lfg, og = build()
+    init = {k: v.detach().clone() for k, v in mg.state_dict().items()}
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for j in range(3):
+            og.zero_grad(set_to_none=True)
+            fwd_bwd(mg, lfg, pool[j % 2][1])
+            og.step()
+            mg.detach_states()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    torch.cuda.synchronize(dev)
+    pingpong = bench.StatePingPong(dev, mg._states)
+    graphs, losses = [], []
+    for j in range(pingpong.cycle(len(pool))):
+        og.zero_grad(set_to_none=True)
+        pingpong.arm(mg, j)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            losses.append(fwd_bwd(mg, lfg, pool[j % len(pool)][1]))
+            og.step()
+        graphs.append(g)
+    with torch.no_grad():
+        for k, v in mg.state_dict().items():
+            v.copy_(init[k])
+        for t in og._moments[1:4]:
+            t.zero_()
+        for b in pingpong.bufs:
+            b.zero_()
+    torch.cuda.synchronize(dev)
+    for j in range(2):
+        graphs[j].replay()
+        torch.cuda.synchronize(dev)
+        wl, (wp, wea, wes), wst = want[j]
+        assert losses[j].item() == wl, (j, losses[j].item(), wl)
+        gp, gea, ges = snap(mg, og)
+        for (n, _), a, b in zip(mg.named_parameters(), gp, wp):
+            assert torch.equal(a, b), f"step {j}: parameter {n}"
+        assert torch.equal(gea, wea) and torch.equal(ges, wes), f"step {j}: Adam moments"
+        for l, (v, w) in enumerate(zip(pingpong.views[(j + 1) % 2], wst)):
+            assert torch.equal(v.detach().cpu(), w), f"step {j}: handed-over state of layer {l}"
+    print(f"\n[cfg2 graph ping-pong] 2 replays == 2 eager steps: losses {[w[0] for w in want]}")

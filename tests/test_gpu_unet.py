@@ -465,3 +465,56 @@ def test_unet_bit_reproducible(dev):
     assert torch.equal(l0, l1), (l0.item(), l1.item())
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+
+
+def test_unet_cfg5_b16_gradients_equal_sum_of_b2_pairs(dev):
+    """cfg5's bench batch with the loss on ALL 16 samples: the U-Net has no BatchNorm and the
+    EventWarping loss is a sum of per-sample terms (loss/flow.py:178-303: per-sample IWE terms summed,
+    the smoothness term a sum over pixels), so the B = 16 parameter gradients must equal the sum of
+    eight B = 2 runs on the same sample pairs.  B = 16 runs other split-K and pixel-split plans than
+    B = 2 (test_unet_cfg5_shapes_vs_oracle lists them) and B = 2 is pinned to the oracle, so a B = 16
+    plan that dropped or mis-indexed the pixels of samples 2..15 fails here.  256 x 256, base 32, T = 2
+    windows of 1000 events.  The spikes must agree exactly (the two batch sizes sum the convs in
+    different orders; a near-threshold flip at this seed would need another seed); then loss rtol 1e-5
+    and every gradient within rel-L2 1e-5 (fp32 summation order)."""
+    import snnflow
+    from snnflow.synthetic import make_window
+
+    base, H, B, T = 32, 256, 16, 2
+    torch.manual_seed(5)
+    model = snnflow.SpikingRecEVFlowNet(_kw(base)).to(dev)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    wins = [make_window(B, 1000, H, H, gen, dev) for _ in range(T)]
+
+    def run(sl):
+        model.reset_states()
+        model.zero_grad(set_to_none=True)
+        ew = snnflow.EventWarping(_cfg(H, H), dev)
+        spikes = []
+        for w in wins:
+            out = model(None, w["event_cnt"][sl])
+            ew.event_flow_association(out["flow"], w["event_list"][sl], w["event_list_pol_mask"][sl], w["event_mask"][sl])
+            spikes.append([_spk(st) for st in model.states])
+        loss = ew()
+        loss.backward()
+        return loss.item(), {n: p.grad.detach().double().cpu() for n, p in model.named_parameters()}, spikes
+
+    l16, g16, s16 = run(slice(0, B))
+    lsum, gsum, flips = 0.0, None, 0
+    for k in range(B // 2):
+        sl = slice(2 * k, 2 * k + 2)
+        l2, g2, s2 = run(sl)
+        lsum += l2
+        gsum = g2 if gsum is None else {n: gsum[n] + g2[n] for n in gsum}
+        for t in range(T):
+            for a, b in zip(s16[t], s2[t]):
+                a = a[:, sl] if a.dim() == 5 else a[sl]
+                flips += int((a != b).sum())
+    print(f"\n[unet cfg5 B=16 vs 8 x B=2] spike differences {flips}; loss {l16:.9g} vs {lsum:.9g}")
+    assert flips == 0, f"{flips} near-threshold spike flips between the batch sizes: change the seed"
+    np.testing.assert_allclose(l16, lsum, rtol=1e-5)
+    errs = {n: _rel(g16[n].numpy(), gsum[n].numpy()) for n in g16}
+    worst = max(errs.items(), key=lambda kv: kv[1])
+    print(f"[unet cfg5 B=16 vs 8 x B=2] gradient rel-L2 worst {worst[0]} {worst[1]:.2e} over {len(errs)} tensors")
+    for n, e in errs.items():
+        assert e <= 1e-5, (n, e)
