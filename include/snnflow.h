@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 34
+#define SNNFLOW_ABI_VERSION 35
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -390,11 +390,14 @@ typedef struct snnflow_iwe_loss_args {
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
 /* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch
- * [2][4][B][H*W].  gev (ABI 26, optional): scratch [B][M][2] floats; with it the per-event flow
- * gradients are stored, then summed per pixel in exact two-word fixed point (order-independent:
- * bit-reproducible g_flows); NULL: fp32 atomics into g_flows (order-dependent rounding). */
+ * [2][4][B][H*W].  bin (ABI 35, optional): int scratch of snnflow_iwe_bwd_scratch_ints(B, M, H, W, tf);
+ * with it every (sample, flow window)'s events are binned by the pixel band of their own pixel and one
+ * block per band forms their flow gradients and sums them per pixel in exact two-word fixed point
+ * (order-independent: bit-reproducible g_flows); NULL: fp32 atomics into g_flows (order-dependent
+ * rounding).  H * W <= 2^21. */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
-                         float* g_flows, float* gev, void* stream);
+                         float* g_flows, int* bin, void* stream);
+int snnflow_iwe_bwd_scratch_ints(int B, int M, int H, int W, int tf);
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf);
 int snnflow_iwe_scratch_floats(int B, int H, int W);  /* floats of the images scratch */
 

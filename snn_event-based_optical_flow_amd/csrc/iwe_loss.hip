@@ -573,7 +573,7 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
 constexpr int kBwdLanes = 8;
 
 __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
-                                                      float* g_flows, float* gev) {
+                                                      float* g_flows) {
     const int64_t HWp = (int64_t)a.H * a.W;
     const int64_t n = (int64_t)a.B * a.M;
     const int64_t img = (int64_t)a.B * HWp;
@@ -621,36 +621,98 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
         gfy += __shfl_xor(gfy, 4, 64);
         gfx += __shfl_xor(gfx, 4, 64);
         if (sub == 0) {
-            if (gev) {  // summed per pixel by k_iwe_bwd_scatter
-                *reinterpret_cast<float2*>(gev + 2 * e) = make_float2(gfx, gfy);
-            } else {
-                float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
-                if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
-                if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
-            }
+            float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
+            if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
+            if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
         }
     }
 }
 
-// Per-pixel sums of the per-event flow gradients (an event scatters into its own pixel): one block
-// per (sample, flow window, band of SPLAT_BAND pixels) scans the window's events, adds those of its
-// band into LDS in exact two-word fixed point (SplatLdsX: integer adds, so the sum does not depend on
-// the order of the events), then adds each touched pixel's total to g_flows once.
+// The events of every (sample, flow window) binned by the pixel band (SPLAT_BAND pixels) of the event's
+// own pixel -- the pixel its flow gradient lands in.  The binning depends on the event lists only.
+// perm [B][M]: for flow window t (events [i0, i1) of the concatenation: window t, or all of them when
+// tf == 1) the region [b M + i0, b M + i1) lists the events' concatenated indices band by band;
+// bins [B][tf][nbands + 1]: each band's start in that region (the last entry: the window's count).  The
+// order inside a band follows the LDS atomics (it does not matter: the consumer sums in exact fixed
+// point).  One block per (sample, flow window): a band histogram, a wave-0 prefix scan, the placement.
+constexpr int kMaxBands = 1024;  // H W <= kMaxBands SPLAT_BAND pixels (host check)
+
+__device__ inline void flow_window_events(const snnflow_iwe_loss_args& a, int t, int& i0, int& i1) {
+    i0 = a.tf == 1 ? 0 : a.off[t];
+    i1 = a.tf == 1 ? a.M : a.off[t + 1];
+}
+
+__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int nbands, int* perm, int* bins) {
+    __shared__ int cnt[kMaxBands], cur[kMaxBands];
+    __shared__ WinTab wt;
+    const int tid = threadIdx.x;
+    wintab_load(a, wt);
+    const int t = blockIdx.x % a.tf, b = blockIdx.x / a.tf;
+    int i0, i1;
+    flow_window_events(a, t, i0, i1);
+    for (int k = tid; k < nbands; k += SPLAT_NT) cnt[k] = 0;
+    __syncthreads();
+    auto band_of = [&](int i) {
+        const EventRef r = event_ref(wt, a.T, b, i);
+        const int pix = (int)(r.ev[1] * (float)a.W + r.ev[2]);
+        const int k = pix / SPLAT_BAND;
+        return k < 0 ? 0 : (k >= nbands ? nbands - 1 : k);
+    };
+    for (int i = i0 + tid; i < i1; i += SPLAT_NT) atomicAdd(&cnt[band_of(i)], 1);
+    __syncthreads();
+    int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
+    if (tid < 64) {  // exclusive prefix over the bands, 64 at a time
+        int carry = 0;
+        for (int k0 = 0; k0 < nbands; k0 += 64) {
+            const int k = k0 + tid;
+            const int c = k < nbands ? cnt[k] : 0;
+            int x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
+                if (tid >= o) x += y;
+            }
+            if (k < nbands) {
+                cur[k] = carry + x - c;
+                bo[k] = carry + x - c;
+            }
+            carry += __shfl(x, 63, 64);
+        }
+        if (tid == 0) bo[nbands] = carry;
+    }
+    __syncthreads();
+    int* pr = perm + (int64_t)b * a.M + i0;
+    for (int i = i0 + tid; i < i1; i += SPLAT_NT) pr[atomicAdd(&cur[band_of(i)], 1)] = i;
+}
+
+// The loss backward's per-event part, per (sample, flow window, band): each event of the band's bin
+// gathers dL/d(images) at the 4 corners of both warps and chains them through the bilinear weights to
+// its flow (eight lanes per event as in k_iwe_bwd_event), and the band's per-pixel sums of those flow
+// gradients are formed in LDS in exact two-word fixed point (SplatLdsX's split: integer adds, so the
+// sums do not depend on the order of the events) and added to g_flows once per touched pixel.  No
+// block reads an event outside its bin (the former scan of the whole window per band is gone).
 struct GevLds {
     unsigned long long hi[2][SPLAT_BAND], lo[2][SPLAT_BAND];
 };
 
-__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_args a, const float* __restrict__ gev,
-                                                              float* g_flows, int nbands) {
-    __shared__ GevLds img;
+__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
+                                                           float* g_flows, const int* __restrict__ perm,
+                                                           const int* __restrict__ bins, int nbands) {
+    __shared__ GevLds acc;
     __shared__ WinTab wt;
     const int tid = threadIdx.x;
     wintab_load(a, wt);
-    const int band = blockIdx.x % nbands, rest = blockIdx.x / nbands, t = rest % a.tf, b = rest / a.tf;
-    const int64_t HWp = (int64_t)a.H * a.W;
+    const int blk = xcd_block();  // a sample's windows and bands on one XCD: its flows / image gradients in one L2
+    const int band = blk % nbands, rest = blk / nbands, t = rest % a.tf, b = rest / a.tf;
+    const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p0 = band * SPLAT_BAND;
     const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
-    for (int j = tid; j < 2 * SPLAT_BAND; j += SPLAT_NT) (&img.hi[0][0])[j] = 0, (&img.lo[0][0])[j] = 0;
+    const int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
+    int i0, i1;
+    flow_window_events(a, t, i0, i1);
+    const int e0 = bo[band], e1 = bo[band + 1];
+    const int* pr = perm + (int64_t)b * a.M + i0;
+    for (int j = tid; j < 2 * SPLAT_BAND; j += SPLAT_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
     // the band's current g_flows values (the pixel backward's), read ahead of the event loop
     float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
     constexpr int GFR = 2 * SPLAT_BAND / SPLAT_NT;
@@ -661,23 +723,62 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_a
         gold[k] = q < np ? gf[c * HWp + q] : 0.0f;
     }
     __syncthreads();
-    const int i0 = a.tf == 1 ? 0 : a.off[t], i1 = a.tf == 1 ? a.M : a.off[t + 1];
-    for (int i = i0 + tid; i < i1; i += SPLAT_NT) {
-        const EventRef r = event_ref(wt, a.T, b, i);
-        // the event's flow gradients load alongside its position (one round trip, not two)
-        const float2 g = *reinterpret_cast<const float2*>(gev + 2 * ((int64_t)b * a.M + i));
-        const int q = (int)(r.ev[1] * (float)a.W + r.ev[2]) - p0;
-        if (q < 0 || q >= np) continue;
+    const int sub = tid & (kBwdLanes - 1), d = sub >> 2, qc = sub & 3;
+    const float tref = d == 0 ? (float)a.T : 0.0f;
+    const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
+    // every lane runs every round (the lane exchanges need the whole 8-lane group): a slot past the bin
+    // contributes zeros
+    for (int s0 = e0; s0 < e1; s0 += SPLAT_NT / kBwdLanes) {
+        const int slot = s0 + tid / kBwdLanes;
+        const bool on = slot < e1;
+        float gwy = 0.0f, gwx = 0.0f, dt = 0.0f;
+        int q = -1;
+        if (on) {
+            const int i = pr[slot];
+            const EventRef r = event_ref(wt, a.T, b, i);
+            const float4 ev = *reinterpret_cast<const float4*>(r.ev);
+            const float2 pm = *reinterpret_cast<const float2*>(r.pol);
+            const float ts = ev.x + (float)r.k, y = ev.y, x = ev.z;
+            const int pix = (int)(y * (float)a.W + x);
+            q = pix - p0;
+            const float* fl = wt.fl[a.tf == 1 ? 0 : r.k] + (int64_t)b * 2 * HWp;
+            const float fy = fl[HWp + pix], fx = fl[pix];
+            const float tsw = d == 0 ? ts : (float)a.T - ts;
+            Corner c[4];
+            float wy, wx;
+            warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
+            Corner cq = c[0];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            // clamped to |d| <= 2^30 (a per-event flow gradient beyond that is not a number this sum can
-            // carry exactly in 64 bits: rint(d 2^32) must leave room for the pixel's other events)
-            const double d = fmin(fmax((double)(c == 0 ? g.x : g.y), -0x1p30), 0x1p30);
-            if (d == 0.0) continue;
-            const double h = rint(d * 0x1p32);
-            const long long l = (long long)rint((d - h * 0x1p-32) * 0x1p75);
-            atomicAdd(&img.hi[c][q], (unsigned long long)(long long)h);
-            if (l != 0) atomicAdd(&img.lo[c][q], (unsigned long long)l);
+            for (int k = 1; k < 4; ++k)
+                if (qc == k) cq = c[k];
+            if (cq.inb) {
+                const int id = cq.idx;
+                const float gwt = (gb[id] * pm.x + gb[img + id] * pm.y) +
+                                  (gb[2 * img + id] * (tsw * pm.x) + gb[3 * img + id] * (tsw * pm.y));
+                // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
+                const float gay = gwt * cq.ax, gax = gwt * cq.ay;
+                gwy = -(gay * relu_tie(1.0f - fabsf(cq.dy))) * sgnf(cq.dy);
+                gwx = -(gax * relu_tie(1.0f - fabsf(cq.dx))) * sgnf(cq.dx);
+            }
+            dt = tref - ts;
+        }
+        gwy += __shfl_xor(gwy, 1, 64);
+        gwx += __shfl_xor(gwx, 1, 64);
+        gwy += __shfl_xor(gwy, 2, 64);
+        gwx += __shfl_xor(gwx, 2, 64);
+        float gfy = (gwy * a.flow_scaling) * dt, gfx = (gwx * a.flow_scaling) * dt;
+        gfy += __shfl_xor(gfy, 4, 64);
+        gfx += __shfl_xor(gfx, 4, 64);
+        if (on && sub < 2 && q >= 0 && q < np) {  // lane 0: the x component, lane 1: y
+            // clamped to |v| <= 2^30 (a per-event flow gradient beyond that is not a number this sum can
+            // carry exactly in 64 bits: rint(v 2^32) must leave room for the pixel's other events)
+            const double v = fmin(fmax((double)(sub == 0 ? gfx : gfy), -0x1p30), 0x1p30);
+            if (v != 0.0) {
+                const double h = rint(v * 0x1p32);
+                const long long l = (long long)rint((v - h * 0x1p-32) * 0x1p75);
+                atomicAdd(&acc.hi[sub][q], (unsigned long long)(long long)h);
+                if (l != 0) atomicAdd(&acc.lo[sub][q], (unsigned long long)l);
+            }
         }
     }
     __syncthreads();
@@ -685,7 +786,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_scatter(snnflow_iwe_loss_a
     for (int k = 0; k < GFR; ++k) {
         const int j = tid + k * SPLAT_NT, c = j / SPLAT_BAND, q = j - c * SPLAT_BAND;
         if (q >= np) continue;
-        const unsigned long long h = img.hi[c][q], l = img.lo[c][q];
+        const unsigned long long h = acc.hi[c][q], l = acc.lo[c][q];
         if (h | l) gf[c * HWp + q] = gold[k] + (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75);
     }
 }
@@ -797,6 +898,12 @@ extern "C" {
 
 int snnflow_iwe_scratch_floats(int B, int H, int W) { return SPLAT_SPLIT * 8 * B * H * W; }
 
+int snnflow_iwe_bwd_scratch_ints(int B, int M, int H, int W, int tf) {
+    const int64_t HWp = (int64_t)H * W;
+    const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
+    return (int)((int64_t)B * M + (int64_t)B * tf * (nbands + 1));
+}
+
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
     const int64_t HWp = (int64_t)H * W;
     return (int)((int64_t)B * loss_tsplit(B, HWp, tf) * loss_chunks(HWp) * LOSS_NV);
@@ -816,7 +923,7 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     return 0;
 }
 
-int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows, float* gev,
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows, int* bin,
                          void* stream) {
     if (int rc = check_loss_args(a)) return rc;
     if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
@@ -826,11 +933,17 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
                        chunks, tsplit);
     if (a->M > 0) {
-        hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s, *a, gimg,
-                           g_flows, gev);
-        if (gev) {
+        if (bin) {  // events binned by pixel band, then per band: event gradients + exact per-pixel sums
             const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
-            hipLaunchKernelGGL(k_iwe_bwd_scatter, dim3(a->B * a->tf * nbands), dim3(SPLAT_NT), 0, s, *a, gev, g_flows, nbands);
+            if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
+            int* perm = bin;
+            int* bins = bin + (int64_t)a->B * a->M;
+            hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(SPLAT_NT), 0, s, *a, nbands, perm, bins);
+            hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(SPLAT_NT), 0, s, *a, gimg, g_flows, perm,
+                               bins, nbands);
+        } else {
+            hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s,
+                               *a, gimg, g_flows);
         }
     }
     SNN_CHECK_LAUNCH();

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 34
+ABI_VERSION = 35
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -300,6 +300,7 @@ EXPORTS = {
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
     "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P, P]),
     "snnflow_iwe_scratch_floats": (I32, [I32, I32, I32]),
+    "snnflow_iwe_bwd_scratch_ints": (I32, [I32, I32, I32, I32, I32]),
     "snnflow_iwe_acc_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
     "snnflow_iwe_interpolate": (I32, [P, P, P, I64, I32, I32, I32, I32, P, P]),

@@ -6,9 +6,10 @@ in place through per-window pointer tables (nothing is concatenated).  ``forward
 three kernels: the warp + bilinear splat of every event into the 8 IWEs (forward/backward
 warp x {count, timestamp} x polarity) with LDS-privatised image bands; per (pixel,
 window) loss and Charbonnier smoothness terms reduced to per-block rows; a fixed-order
-fp64 reduction of the rows into the loss.  The backward runs two more: per (pixel,
-window) image and smoothness gradients, then the per-event gradient gathered from the 4
-corners of both warps and scattered onto the flow maps.
+fp64 reduction of the rows into the loss.  The backward runs three more: per (pixel,
+window) image and smoothness gradients; the events of every (sample, window) binned by
+the pixel band of their own pixel; per band, each event's gradient gathered from the 4
+corners of both warps and summed onto its pixel's flow in exact fixed point.
 """
 import ctypes
 
@@ -87,9 +88,11 @@ class EventWarpingFn(torch.autograd.Function):
         B, H, W = flows_c[0].shape[0], ctx.meta["H"], ctx.meta["W"]
         gimg = torch.empty(8 * B * H * W, device=dev)
         g_flows = torch.empty(B, len(flows_c), 2, H, W, device=dev)
-        # per-event flow gradients, summed per pixel in fixed point (bit-reproducible g_flows)
-        gev = torch.empty(max(2 * B * a.M, 1), device=dev)
-        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), ptr(gev),
+        # the events binned by pixel band; per band the flow gradients summed per pixel in fixed point
+        # (bit-reproducible g_flows)
+        nbin = lib.snnflow_iwe_bwd_scratch_ints(B, a.M, H, W, len(flows_c))
+        bins = torch.empty(max(nbin, 1), dtype=torch.int32, device=dev)
+        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), ptr(bins),
                   s)
         return (None, None, None, *g_flows.unbind(1))
 

@@ -1567,7 +1567,7 @@ def test_iwe_loss_bit_reproducible(dev):
         losses.append(loss.item())
         grads.append(torch.cat([f.grad.flatten() for f in fl]).cpu())
     assert all(v == losses[0] for v in losses), losses
-    # the flow gradients too: the ~40 events per pixel are summed in fixed point (k_iwe_bwd_scatter)
+    # the flow gradients too: the ~40 events per pixel are summed in fixed point (k_iwe_bwd_band)
     for g in grads[1:]:
         assert torch.equal(g, grads[0])
     rl = iwe_ref.EventWarpingRef([H, W])
