@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 35
+ABI_VERSION = 36
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -247,7 +247,8 @@ class FireNetBwdIo(ctypes.Structure):
     _fields_ = [("ys", P), ("stats", P), ("flow", P), ("mem_in", PL), ("g_state", PL),
                 ("g_flow", P), ("gflow_sb", I64), ("gflow_sc", I64), ("g_cur", P), ("bnc", P),
                 ("g_prev", PL), ("ext", I32 * MAX_LAYERS), ("g_x", P), ("gxs", I64 * 4),
-                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32)]
+                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32),
+                ("s_prev", PL)]
 
 
 class FireNetWgradStep(ctypes.Structure):
@@ -337,6 +338,8 @@ EXPORTS = {
     "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
     "snnflow_firenet_fwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetFwdIo), P]),
     "snnflow_firenet_bwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), P]),
+    "snnflow_firenet_bwd_seq": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), I32, P, I64, I32,
+                                      ctypes.POINTER(I32), P]),
     "snnflow_firenet_wgrad": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetWgradStep), I32, P, P, P]),
     "snnflow_bn_fwd": (I32, [ctypes.POINTER(BnFwdArgs), P]),
     "snnflow_bn_bwd": (I32, [ctypes.POINTER(BnBwdArgs), P]),

@@ -197,6 +197,11 @@ class FireNetEngine:
         self.pending_layers = []  # per pending step: the layers whose weight gradients are still deferred
         self.slab_live = [False] * self.L      # slab rows of layer l hold partial sums of this chain
         self.fuse_wgrad = self.C == 8          # wavefront backward computes layers >= 1's dW in place
+        # per-step autograd nodes of one BPTT chain (the reference loop's T model() calls): their backwards
+        # are collected and issued at the chain's first step as wavefront launches (FireNetStep, _Chain);
+        # SNNFLOW_DEFER_BWD=0: every node runs its own step's backward
+        import os
+        self.defer_backward = os.environ.get("SNNFLOW_DEFER_BWD", "1") != "0"
         self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
         self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
         # forward_sequence, one-shot: a flat fp32 buffer of L x 2BHWC floats that receives the final
@@ -724,6 +729,7 @@ class FireNetStep(torch.autograd.Function):
         mem_in, s_prev, keep = [], [], []
         half = 4 * (n1 // 2)
         root = True
+        chain = None
         ext = [False] * L  # prev state requiring grad that this engine did not produce
         for l in range(L):
             p = prev[l]
@@ -742,7 +748,16 @@ class FireNetStep(torch.autograd.Function):
                 ours = getattr(p.grad_fn, "eng", None) is eng
                 if eng.rec[l] and p.requires_grad and ours:
                     root = False
+                    chain = chain or getattr(p.grad_fn, "chain", None)
                 ext[l] = p.requires_grad and not ours
+        # the BPTT chain of this step: a new one at its first step (root); the chain's backwards can be
+        # batched if no step needs an event-tensor gradient and only the first step sees external states
+        if root:
+            chain = _Chain(eng.defer_backward and not x.requires_grad and eng.sequence_ok(cin0))
+        elif chain is None:  # continues a forward_sequence window: per-step backwards
+            chain = _Chain(False)
+        elif x.requires_grad or any(ext):
+            chain.defer = False
         ys_t, stats_t = ys, stats
         plan = None if _lib.TIMER is not None else eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
         try:
@@ -767,6 +782,7 @@ class FireNetStep(torch.autograd.Function):
 
         ctx.eng = eng
         ctx.root = root
+        ctx.chain = chain
         ctx.ext = ext
         ctx.shape = (B, H, W, cin0)
         ctx.has_prev = [p is not None for p in prev]
@@ -780,110 +796,265 @@ class FireNetStep(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_flow, *g_states):
-        eng = ctx.eng
-        L, C = eng.L, eng.C
-        B, H, W, cin0 = ctx.shape
-        saved = list(ctx.saved_tensors)
-        x, ys, stats, flow = saved[:4]
-        states = saved[4:4 + L]
-        keep = saved[4 + L:]  # tensors behind the mem_in / s_prev pointers (alive while saved here)
-        mem_in, s_prev = ctx.ptrs
+        eng, chain = ctx.eng, ctx.chain
+        st = _StepBwd(ctx, g_flow, g_states)
+        if chain.defer:
+            if not ctx.root:  # collected; the chain's first step (the last node autograd calls) runs them
+                chain.steps.append(st)
+                return (None,) * (3 + eng.L)
+            steps = [st] + chain.steps[::-1]  # time order
+            chain.steps = []
+            if len(steps) > 1:
+                return _chain_backward(eng, steps)
+        return _step_backward(eng, st)
 
-        dev = x.device
-        s = _lib.stream_ptr(dev)
-        ws = eng.workspace(B, H, W, dev)
-        wfwd, wbwd = eng.prepped()  # the buffers of the forward (same weights)
-        if not eng.bwd_open:
-            eng.open_chain(dev)
-            acc = 0
-        else:
-            acc = 1
-        glayers, gpw, gpb = eng.grad_views()
-        neurons = eng.neurons()
-        bacc = _Rows(ws.bwd_acc)
-        zn = ws.bwd_acc.shape[1]
-        gst = [as_nhwc_state(g) if g is not None else None for g in g_states]
-        # gradients of the previous states: the spike half of recurrent cells (rec dgrad);
-        # for states that did not come from this engine also the membrane half
-        # (v depends on the incoming membrane, SNNtorch_spiking_submodules.py:305 / snn.Leaky).
-        g_prev = [None] * L
+
+class _Chain:
+    """The BPTT chain of FireNetStep nodes linked by this engine's recurrent states (one truncated
+    window of the reference loop, train_flow.py:232-262: T model() calls, one loss.backward()).  With
+    ``defer`` the later steps' nodes only record their backward inputs (``steps``) and the chain's first
+    step -- the last node autograd calls -- issues every step's backward at once (_chain_backward)."""
+    __slots__ = ("defer", "steps")
+
+    def __init__(self, defer):
+        self.defer = defer
+        self.steps = []
+
+
+class _StepBwd:
+    """One FireNetStep's backward inputs, unpacked from its ctx (autograd frees a node's saved tensors
+    once its backward returns; these references keep them for the chain's first step)."""
+    __slots__ = ("saved", "ptrs", "shape", "root", "ext", "has_prev", "needs", "g_flow", "g_states")
+
+    def __init__(self, ctx, g_flow, g_states):
+        self.saved = list(ctx.saved_tensors)
+        self.ptrs, self.shape, self.root, self.ext = ctx.ptrs, ctx.shape, ctx.root, ctx.ext
+        self.has_prev, self.needs = ctx.has_prev, ctx.needs_input_grad
+        self.g_flow, self.g_states = g_flow, g_states
+
+
+def _chain_backward(eng, steps):
+    """The backwards of a chain's steps (time order; steps[0] is the chain's first step), issued by the
+    first step's node.  Without external gradients on intermediate states, one snnflow_firenet_bwd_seq
+    call: the T x (L+1) layer-steps as 2(T-1)+L+1 wavefront launches (FireNetSequence's schedule and
+    kernels, the per-step tensors read in place).  Otherwise, or under per-kernel timing, the steps'
+    backwards one after the other (last first), each step's state-input gradient added to the external
+    gradient of the previous step's states -- what autograd would have summed.  Returns the first
+    step's input gradients."""
+    L = eng.L
+    T = len(steps)
+    if _lib.TIMER is None and all(g is None for st in steps[:-1] for g in st.g_states):
+        return _chain_backward_batched(eng, steps)
+    nxt = None
+    for t in range(T - 1, -1, -1):
+        st = steps[t]
+        gs = list(st.g_states)
+        if nxt is not None:
+            gs = [a if b is None else (b if a is None else a + b) for a, b in zip(gs, nxt)]
+        res = _step_backward(eng, st, gs)
+        nxt = res[2:2 + L]
+    return res
+
+
+def _chain_backward_batched(eng, steps):
+    L, C = eng.L, eng.C
+    T = len(steps)
+    first = steps[0]
+    B, H, W, cin0 = first.shape
+    dev = first.saved[0].device
+    s = _lib.stream_ptr(dev)
+    ws = eng.workspace(B, H, W, dev)
+    wfwd, wbwd = eng.prepped()
+    plan = eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
+    fresh = not eng.bwd_open
+    if fresh:
+        eng.open_chain(dev)
+    glayers, gpw, gpb = eng.grad_views()
+    gcur = torch.empty(T, L, B, H, W, C, device=dev)
+    bnc = torch.empty(T, L, 2, C, device=dev)
+    nacc = _lib.acc_storage(_lib.bwd_acc_len(C))
+    bacc = torch.zeros(T * L * nacc, dtype=torch.float64, device=dev)
+    # gradients of each step's incoming states: inside the chain the spike half of recurrent cells
+    # (steps t >= 1), at the first step what its node returns (FireNetSequence's g0)
+    g_out = [[empty_state(B, C, H, W, dev) if eng.rec[l] else None for l in range(L)] for _ in range(T)]
+    g0 = [None] * L
+    for l in range(L):
+        if not (first.has_prev[l] and first.needs[2 + l]):
+            continue
+        if first.ext[l]:
+            g0[l] = torch.zeros((2, B, C, H, W), device=dev).as_strided(
+                (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
+        elif eng.rec[l]:
+            g0[l] = empty_state(B, C, H, W, dev)
+    g_out[0] = g0
+    g_last = [as_nhwc_state(g) if g is not None else None for g in steps[-1].g_states]
+    ios = (_lib.FireNetBwdIo * T)()
+    gfl = []
+    for t, st in enumerate(steps):
+        io = ios[t]
+        ys, stats, flow = st.saved[1:4]
+        mem_in, s_prev = st.ptrs
+        io.ys, io.stats, io.flow = ys.data_ptr(), stats.data_ptr(), flow.data_ptr()
+        g_into = g_last if t == T - 1 else g_out[t + 1]
         for l in range(L):
-            if not (ctx.has_prev[l] and ctx.needs_input_grad[2 + l]):
-                continue
-            if ctx.ext[l]:
-                g_prev[l] = torch.zeros((2, B, C, H, W), device=dev).as_strided(
-                    (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
-            elif eng.rec[l]:
-                g_prev[l] = empty_state(B, C, H, W, dev)
-        gmem = [g_prev[l] if (g_prev[l] is not None and ctx.ext[l]) else None for l in range(L)]
-
-        # per-step buffers kept until the deferred weight gradients run (root step)
-        gcur_t = torch.empty(L, B, H, W, C, device=dev)   # dL/d BN-output of every layer
-        bnc_t = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
-        gcur, bnc, ys, stats = _Rows(gcur_t), _Rows(bnc_t), _Rows(ys), _Rows(stats)
-        # pending: row pointers for the deferred wgrad + the tensors behind them (kept alive)
-        eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev, (keep, gcur_t, bnc_t, saved)))
-        eng.pending_layers.append(tuple(range(L)))
-        # (the deferred weight gradients stay on this stream after the chain: a side stream
-        # overlapping them with the root step's chain measured slower under graph replay,
-        # 2.48 -> 2.72 ms per cfg2 train step)
-        try:
-            if g_flow is not None and (g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32):
-                g_flow = g_flow.contiguous().float()
-            gx = None
-            if ctx.needs_input_grad[1]:
-                gx = torch.empty_like(x)
-            plan = None if _lib.TIMER is not None else eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
-            if plan is not None:  # one call of the C step driver
-                io = _lib.FireNetBwdIo()
-                io.ys, io.stats, io.flow = ys.base, stats.base, flow.data_ptr()
+            io.mem_in[l] = mem_in[l]
+            io.s_prev[l] = s_prev[l]
+            io.g_state[l] = _ptr_t(g_into[l])
+            io.g_prev[l] = _ptr_t(g_out[t][l])
+            io.ext[l] = 1 if (t == 0 and first.ext[l]) else 0
+            io.ng[l] = glayers[l][2]
+        g = st.g_flow
+        if g is not None:
+            if g.stride(3) != 1 or g.stride(2) != W or g.dtype != torch.float32:
+                g = g.contiguous().float()
+            io.g_flow, io.gflow_sb, io.gflow_sc = g.data_ptr(), g.stride(0), g.stride(1)
+        gfl.append(g)
+        io.g_cur, io.bnc = gcur[t].data_ptr(), bnc[t].data_ptr()
+        io.g_pred_w, io.g_pred_b = gpw, gpb
+        io.accumulate = 0 if (fresh and t == T - 1) else 1
+    fuse = bool(eng.fuse_wgrad) and C == 8
+    live = (ctypes.c_int * L)(*[1 if v else 0 for v in eng.slab_live])
+    try:
+        _lib.call("firenet_bwd_seq", lib.snnflow_firenet_bwd_seq, ctypes.byref(plan), ios, T, bacc.data_ptr(), nacc,
+                  1 if fuse else 0, live, s)
+        eng.slab_live = [bool(v) for v in live]
+        if eng.any_subtract():
+            for t, st in enumerate(steps):
                 for l in range(L):
-                    io.mem_in[l] = mem_in[l]
-                    io.g_state[l] = _ptr_t(gst[l])
-                    io.g_prev[l] = _ptr_t(g_prev[l])
-                    io.ext[l] = 1 if ctx.ext[l] else 0
-                    io.ng[l] = glayers[l][2]
-                if g_flow is not None:
-                    io.g_flow, io.gflow_sb, io.gflow_sc = g_flow.data_ptr(), g_flow.stride(0), g_flow.stride(1)
-                io.g_cur, io.bnc = gcur.base, bnc.base
-                if gx is not None:
-                    io.g_x = gx.data_ptr()
-                    io.gxs[0], io.gxs[1], io.gxs[2], io.gxs[3] = gx.stride()
-                io.g_pred_w, io.g_pred_b, io.accumulate = gpw, gpb, acc
-                _lib.call("firenet_bwd", lib.snnflow_firenet_bwd, ctypes.byref(plan), ctypes.byref(io), s)
-            else:  # per-kernel launches (KernelTimer attribution): the same kernels and arguments
-                # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
-                b = _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, gcur, gmem, bacc)
-                b.zero0, b.zero_n = bacc[0], zn
-                _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
-                for l in range(L - 1, -1, -1):
-                    a = _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur, gmem, bacc, bnc,
-                                        glayers, gpw, gpb, acc, wfwd, wbwd, g_prev, ctx.ext, gx)
-                    if l + 1 <= L - 1:
-                        a.zero0, a.zero_n = bacc[l + 1], zn
-                    _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
-            if eng.any_subtract():
-                for l in range(L):
-                    theta_subtract(eng.cells[l], gcur[l], mem_in[l], B * H * W, glayers[l][2].threshold, s)
-            if ctx.root:
-                eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
-        except Exception:
-            ws.reset_acc()
-            eng.bwd_open = False
-            eng.pending, eng.pending_layers = [], []
-            eng.prep_stale = True
-            raise
+                    theta_subtract(eng.cells[l], gcur[t][l].data_ptr(), st.ptrs[0][l], B * H * W,
+                                   glayers[l][2].threshold, s)
+        # the deferred weight gradients (layer 0 with the fused form) see the steps last first
+        for t in range(T - 1, -1, -1):
+            st = steps[t]
+            x, ys, stats = st.saved[:3]
+            eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys), _Rows(stats), x, st.saved[4:4 + L],
+                                st.ptrs[1], (st.saved, gcur, bnc)))
+            eng.pending_layers.append((0,) if fuse else tuple(range(L)))
+        eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
+    except Exception:
+        eng.ws.reset_acc()
+        eng.bwd_open = False
+        eng.pending, eng.pending_layers = [], []
+        eng.prep_stale = True
+        raise
+    g_anchor = eng.flat if first.needs[2 + L] else None
+    eng.flat_views = None
+    eng.bwd_open = False
+    eng.last_flat = eng.flat
+    eng.prep_stale = True
+    del gfl
+    return (None, None, *g0, g_anchor)
 
-        g_anchor = None
+
+def _step_backward(eng, ctx, g_states=None):
+    """One step's backward (snnflow_firenet_bwd), ``ctx`` a _StepBwd; g_states overrides its state
+    gradients (the chain's sequential form)."""
+    g_flow = ctx.g_flow
+    if g_states is None:
+        g_states = ctx.g_states
+    L, C = eng.L, eng.C
+    B, H, W, cin0 = ctx.shape
+    saved = ctx.saved
+    x, ys, stats, flow = saved[:4]
+    states = saved[4:4 + L]
+    keep = saved[4 + L:]  # tensors behind the mem_in / s_prev pointers (alive while saved here)
+    mem_in, s_prev = ctx.ptrs
+
+    dev = x.device
+    s = _lib.stream_ptr(dev)
+    ws = eng.workspace(B, H, W, dev)
+    wfwd, wbwd = eng.prepped()  # the buffers of the forward (same weights)
+    if not eng.bwd_open:
+        eng.open_chain(dev)
+        acc = 0
+    else:
+        acc = 1
+    glayers, gpw, gpb = eng.grad_views()
+    neurons = eng.neurons()
+    bacc = _Rows(ws.bwd_acc)
+    zn = ws.bwd_acc.shape[1]
+    gst = [as_nhwc_state(g) if g is not None else None for g in g_states]
+    # gradients of the previous states: the spike half of recurrent cells (rec dgrad);
+    # for states that did not come from this engine also the membrane half
+    # (v depends on the incoming membrane, SNNtorch_spiking_submodules.py:305 / snn.Leaky).
+    g_prev = [None] * L
+    for l in range(L):
+        if not (ctx.has_prev[l] and ctx.needs[2 + l]):
+            continue
+        if ctx.ext[l]:
+            g_prev[l] = torch.zeros((2, B, C, H, W), device=dev).as_strided(
+                (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
+        elif eng.rec[l]:
+            g_prev[l] = empty_state(B, C, H, W, dev)
+    gmem = [g_prev[l] if (g_prev[l] is not None and ctx.ext[l]) else None for l in range(L)]
+
+    # per-step buffers kept until the deferred weight gradients run (root step)
+    gcur_t = torch.empty(L, B, H, W, C, device=dev)   # dL/d BN-output of every layer
+    bnc_t = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
+    gcur, bnc, ys, stats = _Rows(gcur_t), _Rows(bnc_t), _Rows(ys), _Rows(stats)
+    # pending: row pointers for the deferred wgrad + the tensors behind them (kept alive)
+    eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev, (keep, gcur_t, bnc_t, saved)))
+    eng.pending_layers.append(tuple(range(L)))
+    # (the deferred weight gradients stay on this stream after the chain: a side stream
+    # overlapping them with the root step's chain measured slower under graph replay,
+    # 2.48 -> 2.72 ms per cfg2 train step)
+    try:
+        if g_flow is not None and (g_flow.stride(3) != 1 or g_flow.stride(2) != W or g_flow.dtype != torch.float32):
+            g_flow = g_flow.contiguous().float()
+        gx = None
+        if ctx.needs[1]:
+            gx = torch.empty_like(x)
+        plan = None if _lib.TIMER is not None else eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
+        if plan is not None:  # one call of the C step driver
+            io = _lib.FireNetBwdIo()
+            io.ys, io.stats, io.flow = ys.base, stats.base, flow.data_ptr()
+            for l in range(L):
+                io.mem_in[l] = mem_in[l]
+                io.g_state[l] = _ptr_t(gst[l])
+                io.g_prev[l] = _ptr_t(g_prev[l])
+                io.ext[l] = 1 if ctx.ext[l] else 0
+                io.ng[l] = glayers[l][2]
+            if g_flow is not None:
+                io.g_flow, io.gflow_sb, io.gflow_sc = g_flow.data_ptr(), g_flow.stride(0), g_flow.stride(1)
+            io.g_cur, io.bnc = gcur.base, bnc.base
+            if gx is not None:
+                io.g_x = gx.data_ptr()
+                io.gxs[0], io.gxs[1], io.gxs[2], io.gxs[3] = gx.stride()
+            io.g_pred_w, io.g_pred_b, io.accumulate = gpw, gpb, acc
+            _lib.call("firenet_bwd", lib.snnflow_firenet_bwd, ctypes.byref(plan), ctypes.byref(io), s)
+        else:  # per-kernel launches (KernelTimer attribution): the same kernels and arguments
+            # top: pred backward + LIF backward of layer L-1  (zeroes bwd_acc[0])
+            b = _bwd_top_args(eng, B, H, W, ys, stats, mem_in, neurons, gst, g_flow, flow, gcur, gmem, bacc)
+            b.zero0, b.zero_n = bacc[0], zn
+            _lib.call("lif_bwd", lib.snnflow_lif_bwd, ctypes.byref(b), s)
+            for l in range(L - 1, -1, -1):
+                a = _bwd_layer_args(eng, l, B, H, W, cin0, ys, stats, mem_in, neurons, gst, gcur, gmem, bacc, bnc,
+                                    glayers, gpw, gpb, acc, wfwd, wbwd, g_prev, ctx.ext, gx)
+                if l + 1 <= L - 1:
+                    a.zero0, a.zero_n = bacc[l + 1], zn
+                _lib.call(f"layer_bwd[{l}]", lib.snnflow_layer_bwd, ctypes.byref(a), s)
+        if eng.any_subtract():
+            for l in range(L):
+                theta_subtract(eng.cells[l], gcur[l], mem_in[l], B * H * W, glayers[l][2].threshold, s)
         if ctx.root:
-            # the whole flat gradient buffer to the chain's parameter anchor (ParamAnchor splits it
-            # into per-parameter views once every step of the chain is done)
-            g_anchor = eng.flat if ctx.needs_input_grad[2 + L] else None
-            eng.flat_views = None
-            eng.bwd_open = False
-            eng.last_flat = eng.flat
-            eng.prep_stale = True
-        return (None, gx, *g_prev, g_anchor)
+            eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
+    except Exception:
+        ws.reset_acc()
+        eng.bwd_open = False
+        eng.pending, eng.pending_layers = [], []
+        eng.prep_stale = True
+        raise
+
+    g_anchor = None
+    if ctx.root:
+        # the whole flat gradient buffer to the chain's parameter anchor (ParamAnchor splits it
+        # into per-parameter views once every step of the chain is done)
+        g_anchor = eng.flat if ctx.needs[2 + L] else None
+        eng.flat_views = None
+        eng.bwd_open = False
+        eng.last_flat = eng.flat
+        eng.prep_stale = True
+    return (None, gx, *g_prev, g_anchor)
 
 
 def _ptr_t(t):

@@ -1657,3 +1657,65 @@ def test_eval_fused_nonbinary_state_and_final_out(dev, monkeypatch):
         assert all(base <= s.data_ptr() < base + 4 * n for s in mb._states)
     for a, b in zip(res["split"][0] + res["split"][1], res["fused"][0] + res["fused"][1]):
         assert float((a - b).abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize("case", ["all_flows", "partial_loss", "state_grad", "two_windows"])
+def test_per_step_chain_backward_batched(dev, case):
+    """The reference loop's per-window calls (train_flow.py:232-262: T model() calls, one
+    loss.backward()) are T autograd nodes; with FireNetEngine.defer_backward the later nodes only record
+    their inputs and the chain's first step issues every step's backward as wavefront launches
+    (snnflow_firenet_bwd_seq).  Against the same loop with every node running its own step
+    (defer_backward = False), same weights and windows: flows identical (same forward), loss
+    identical, parameter gradients within rel-L2 1e-5 (fp64 batch-sum atomics and the fused weight
+    gradients sum in another order).  Cases: every flow in the loss; a loss on the first half of the
+    windows only (the later nodes are never called); an extra loss term on an intermediate state
+    (external state gradient: the chain falls back to the steps one after the other); two windows
+    with a detach between them (two chains in two backward calls)."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(21)
+    B, H, W, T = 2, 64, 96, 5
+    base = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8)).to(dev).train()
+    gen = torch.Generator(device=dev).manual_seed(4)
+    wins = [make_window(B, 600, H, W, gen, dev) for _ in range(2 * T)]
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    res = {}
+    for defer in (False, True):
+        m = copy.deepcopy(base)
+        m.engine.defer_backward = defer
+        lf = snnflow.EventWarping(cfg, dev)
+        flows, losses, grads = [], [], []
+        for k in range(2 if case == "two_windows" else 1):
+            lf.reset()
+            extra = 0.0
+            for t in range(T):
+                w = wins[k * T + t]
+                out = m(w["event_voxel"], w["event_cnt"])
+                flows.append(out["flow"][0].detach().cpu())
+                if case != "partial_loss" or t < T // 2 + 1:
+                    lf.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+                if case == "state_grad" and t == 2:
+                    extra = m._states[1][1].sum() * 1e-3 + m._states[4][0].square().sum() * 1e-4
+            loss = lf() + extra
+            loss.backward()
+            losses.append(loss.item())
+            grads.append([p.grad.detach().cpu().clone() for p in m.parameters()])
+            m.zero_grad(set_to_none=True)
+            m.detach_states()
+        res[defer] = (flows, losses, grads)
+    for a, b in zip(res[False][0], res[True][0]):
+        assert torch.equal(a, b)
+    assert res[False][1] == res[True][1]
+    names = [n for n, _ in base.named_parameters()]
+    worst = 0.0
+    for ga, gb in zip(res[False][2], res[True][2]):
+        for n, a, b in zip(names, ga, gb):
+            e = float((a - b).double().norm() / max(float(b.double().norm()), 1e-30))
+            worst = max(worst, e)
+            assert e <= 1e-5, (case, n, e)
+    print(f"\n[{case}] batched chain backward vs per-node: worst gradient rel-L2 {worst:.2e}")
