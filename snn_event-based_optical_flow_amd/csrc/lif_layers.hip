@@ -44,6 +44,9 @@
 #ifndef SNNFLOW_TRACE
 #define SNNFLOW_TRACE 0
 #endif
+#ifndef SNNFLOW_SWZ
+#define SNNFLOW_SWZ 1  // C = 8 recurrent backward: bank-conflict-free LDS layouts of the packed x|s tile and dgrad staging
+#endif
 #ifndef SNNFLOW_TRACE_MINGRID
 #define SNNFLOW_TRACE_MINGRID 0  // stamp only launches of at least this many blocks (slot launches: 4 tasks)
 #endif
@@ -1254,6 +1257,16 @@ __device__ void fused_wgrad_stage(const snnflow_layer_bwd_args& a, const float* 
     }
 }
 
+// LDS slot of tile pixel q in the packed [256][16] bf16 x|s tile (32 B per pixel): the transposed reads
+// of one 32-lane half-wave fetch pixels j0..j0+3 (lanes 0-15) and j0+8..j0+11 (lanes 16-31), 256 B
+// apart -- the same 64 banks; swapping the two 4-pixel halves of every odd 8-pixel group puts the
+// second set 128 B further (SQ_LDS_BANK_CONFLICT: 2-way -> none).
+__device__ inline int pk_slot(int q) { return SNNFLOW_SWZ ? q ^ (((q >> 3) & 1) << 2) : q; }
+// Channel-quad slot of tile pixel q in the packed dgrad staging ([256][8] f32, 32 B per pixel): the
+// 16-lane groups of a ds_read_b128 over consecutive pixels would meet pixels 8 apart on one bank set;
+// odd 8-pixel groups swap their two quads.
+__device__ inline int pk_quad(int q, int quad) { return SNNFLOW_SWZ ? quad ^ ((q >> 3) & 1) : quad; }
+
 // The recurrent cell's two weight gradients in one matrix-core pass: the tile holds x and s_prev side
 // by side ([256 pixels][x 0..7 | s 8..15] bf16 in wl_x), so the B operand's columns 0..7 are x and
 // 8..15 are s_prev -- D[co][n] is dW_ff for n < 8 and dW_rec for n >= 8 (the one-conv form leaves
@@ -1267,8 +1280,9 @@ __device__ void fused_wgrad_stage_pk(const float* G, float* wl_x, float* wl_r, c
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     __bf16* X = reinterpret_cast<__bf16*>(wl_x);
     __syncthreads();  // every wave is done with the staged input-gradient results: the regions are free
-    *reinterpret_cast<bf16x4*>(X + pt * XS + ci0) = bf16x4{(__bf16)xsp[0], (__bf16)xsp[1], (__bf16)xsp[2], (__bf16)xsp[3]};
-    *reinterpret_cast<bf16x4*>(X + pt * XS + C + ci0) = bf16x4{(__bf16)sp.x, (__bf16)sp.y, (__bf16)sp.z, (__bf16)sp.w};
+    const int ps = pk_slot(pt);
+    *reinterpret_cast<bf16x4*>(X + ps * XS + ci0) = bf16x4{(__bf16)xsp[0], (__bf16)xsp[1], (__bf16)xsp[2], (__bf16)xsp[3]};
+    *reinterpret_cast<bf16x4*>(X + ps * XS + C + ci0) = bf16x4{(__bf16)sp.x, (__bf16)sp.y, (__bf16)sp.z, (__bf16)sp.w};
     __syncthreads();
 
     const int lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1283,8 +1297,8 @@ __device__ void fused_wgrad_stage_pk(const float* G, float* wl_x, float* wl_r, c
         const bf16x8 ah = tr8(ga, ga + 4 * C);
         const bf16x8 am = tr8(ga + PART, ga + PART + 4 * C);
         const bf16x8 al = tr8(ga + 2 * PART, ga + 2 * PART + 4 * C);
-        const __bf16* xb = X + (row * TW + j0) * XS + 4 * pp;
-        const bf16x8 b = tr8(xb, xb + 4 * XS);
+        const int q = row * TW + j0;
+        const bf16x8 b = tr8(X + pk_slot(q) * XS + 4 * pp, X + pk_slot(q + 4) * XS + 4 * pp);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, d, 0, 0, 0);
         d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, d, 0, 0, 0);
@@ -1602,21 +1616,24 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (pkr) {  // columns n < 8: gx -> wl_x [NT][8]; n >= 8: the recurrent gradient -> wl_r [NT][8]
                 const int lane = tid & 63, n = lane & 15, g4 = lane >> 4;
                 const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-                float* out = (n < 8 ? wl_x : wl_r) + (n & 7);
+                float* out = (n < 8 ? wl_x : wl_r) + (n & 3);
 #pragma unroll
                 for (int mt = 0; mt < MfmaAcc<C, CIN, NW, NG>::MT; ++mt) {
                     const int T = MfmaAcc<C, CIN, NW, NG>::mt0(wv) + mt, row = T >> 1, c0 = (T & 1) * 16;
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) out[(row * TW + c0 + g4 * 4 + r) * 8] = ax.v[mt][0][r];
+                    for (int r = 0; r < 4; ++r) {
+                        const int q = row * TW + c0 + g4 * 4 + r;
+                        out[q * 8 + 4 * pk_quad(q, (n >> 2) & 1)] = ax.v[mt][0][r];
+                    }
                 }
                 __syncthreads();
-                const float4 gv4 = *reinterpret_cast<const float4*>(wl_x + pt * 8 + ci0);
+                const float4 gv4 = *reinterpret_cast<const float4*>(wl_x + pt * 8 + 4 * pk_quad(pt, ci0 >> 2));
                 gx[0] = gv4.x; gx[1] = gv4.y; gx[2] = gv4.z; gx[3] = gv4.w;
                 if (in) {
                     const int64_t plane = (int64_t)a.B * H * W * C;
                     float* gsp = a.g_state_prev + pix * C + cr0;
                     if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp) = z4;
-                    *reinterpret_cast<float4*>(gsp + plane) = *reinterpret_cast<const float4*>(wl_r + pt * 8 + cr0);
+                    *reinterpret_cast<float4*>(gsp + plane) = *reinterpret_cast<const float4*>(wl_r + pt * 8 + 4 * pk_quad(pt, cr0 >> 2));
                 }
             }
         }
