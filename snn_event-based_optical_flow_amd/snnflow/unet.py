@@ -377,6 +377,9 @@ _SHAPES = os.environ.get("SNNFLOW_UNET_SHAPES") == "1"  # profiling: kernel name
 # Tests: set to a list to record every GEMM launch's split plan as (kind, M, K, P, plan) -- plan is the
 # split-K factor of a conv / input gradient, the partial-sum floats (pixel-split plan) of a weight gradient
 PLAN_LOG = None
+# Tests: an upper bound on the split-K factor of convs and input gradients (1: none), so that runs at
+# different batch sizes sum every conv in the same order (split-K partitions K, not pixels)
+KSPLIT_MAX = None
 
 
 def _name(kind, M, K, P):
@@ -395,6 +398,8 @@ def _split_k(a, P, dev):
     """Split-K of a launch (library's choice) with the shared partial-sum workspace (stream-ordered
     reuse; sized by the largest request, which the eager warm-up steps make before any graph capture)."""
     ks = lib.snnflow_unet_conv_ksplit(ctypes.byref(a))
+    if KSPLIT_MAX is not None:
+        ks = min(ks, KSPLIT_MAX)
     if PLAN_LOG is not None:
         PLAN_LOG.append(("dgrad" if a.xparts == 3 else "conv", a.M, sum(a.seg[i].cpitch for i in range(a.nseg)), P, ks))
     if ks <= 1:
