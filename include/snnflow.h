@@ -390,9 +390,10 @@ typedef struct snnflow_iwe_loss_args {
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
 /* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch
- * [2][4][B][H*W].  bin (ABI 35, optional): int scratch of snnflow_iwe_bwd_scratch_ints(B, M, H, W, tf);
- * with it every (sample, flow window)'s events are binned by the pixel band of their own pixel and one
- * block per band forms their flow gradients and sums them per pixel in exact two-word fixed point
+ * [2][4][B][H*W].  bin (ABI 35, optional): 16-B aligned scratch of snnflow_iwe_bwd_scratch_ints(B, M, H,
+ * W, tf) 32-bit words; with it every (sample, flow window)'s events are copied into bins by the pixel band
+ * of their own pixel and one block per band forms their flow gradients and sums them per pixel in exact
+ * two-word fixed point
  * (order-independent: bit-reproducible g_flows); NULL: fp32 atomics into g_flows (order-dependent
  * rounding).  H * W <= 2^21. */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,

@@ -628,21 +628,24 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
     }
 }
 
-// The events of every (sample, flow window) binned by the pixel band (SPLAT_BAND pixels) of the event's
-// own pixel -- the pixel its flow gradient lands in.  The binning depends on the event lists only.
-// perm [B][M]: for flow window t (events [i0, i1) of the concatenation: window t, or all of them when
-// tf == 1) the region [b M + i0, b M + i1) lists the events' concatenated indices band by band;
-// bins [B][tf][nbands + 1]: each band's start in that region (the last entry: the window's count).  The
-// order inside a band follows the LDS atomics (it does not matter: the consumer sums in exact fixed
-// point).  One block per (sample, flow window): a band histogram, a wave-0 prefix scan, the placement.
-constexpr int kMaxBands = 1024;  // H W <= kMaxBands SPLAT_BAND pixels (host check)
+// The events of every (sample, flow window) binned by the pixel band (GB_BAND pixels) of the event's own
+// pixel -- the pixel its flow gradient lands in.  The binning depends on the event lists only.  Each
+// event is copied into its bin as a record: rec4 = (ts + window, y, x, polarity mask 0) and rec1 =
+// polarity mask 1, so that a band's block reads its events contiguously with no index indirection.
+// The region of flow window t (events [i0, i1) of the concatenation: window t, or all of them when
+// tf == 1) is [b M + i0, b M + i1) of rec4 / rec1, band by band; bins [B][tf][nbands + 1]: each band's
+// start in that region (the last entry: the window's count).  The order inside a band follows the LDS
+// atomics (it does not matter: the consumer sums in exact fixed point).  One block per (sample, flow
+// window): a band histogram, a wave-0 prefix scan, the placement.
+constexpr int GB_NT = 256, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
 
 __device__ inline void flow_window_events(const snnflow_iwe_loss_args& a, int t, int& i0, int& i1) {
     i0 = a.tf == 1 ? 0 : a.off[t];
     i1 = a.tf == 1 ? a.M : a.off[t + 1];
 }
 
-__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int nbands, int* perm, int* bins) {
+__global__ __launch_bounds__(GB_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int nbands, float4* rec4, float* rec1,
+                                                   int* bins) {
     __shared__ int cnt[kMaxBands], cur[kMaxBands];
     __shared__ WinTab wt;
     const int tid = threadIdx.x;
@@ -650,15 +653,14 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bin(snnflow_iwe_loss_args a, i
     const int t = blockIdx.x % a.tf, b = blockIdx.x / a.tf;
     int i0, i1;
     flow_window_events(a, t, i0, i1);
-    for (int k = tid; k < nbands; k += SPLAT_NT) cnt[k] = 0;
+    for (int k = tid; k < nbands; k += GB_NT) cnt[k] = 0;
     __syncthreads();
-    auto band_of = [&](int i) {
-        const EventRef r = event_ref(wt, a.T, b, i);
-        const int pix = (int)(r.ev[1] * (float)a.W + r.ev[2]);
-        const int k = pix / SPLAT_BAND;
+    auto band_of = [&](const float* ev) {
+        const int pix = (int)(ev[1] * (float)a.W + ev[2]);
+        const int k = pix / GB_BAND;
         return k < 0 ? 0 : (k >= nbands ? nbands - 1 : k);
     };
-    for (int i = i0 + tid; i < i1; i += SPLAT_NT) atomicAdd(&cnt[band_of(i)], 1);
+    for (int i = i0 + tid; i < i1; i += GB_NT) atomicAdd(&cnt[band_of(event_ref(wt, a.T, b, i).ev)], 1);
     __syncthreads();
     int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
     if (tid < 64) {  // exclusive prefix over the bands, 64 at a time
@@ -681,67 +683,71 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bin(snnflow_iwe_loss_args a, i
         if (tid == 0) bo[nbands] = carry;
     }
     __syncthreads();
-    int* pr = perm + (int64_t)b * a.M + i0;
-    for (int i = i0 + tid; i < i1; i += SPLAT_NT) pr[atomicAdd(&cur[band_of(i)], 1)] = i;
+    const int64_t base = (int64_t)b * a.M + i0;
+    for (int i = i0 + tid; i < i1; i += GB_NT) {
+        const EventRef r = event_ref(wt, a.T, b, i);
+        const float4 ev = *reinterpret_cast<const float4*>(r.ev);
+        const float2 pm = *reinterpret_cast<const float2*>(r.pol);
+        const int slot = atomicAdd(&cur[band_of(r.ev)], 1);
+        rec4[base + slot] = make_float4(ev.x + (float)r.k, ev.y, ev.z, pm.x);
+        rec1[base + slot] = pm.y;
+    }
 }
 
-// The loss backward's per-event part, per (sample, flow window, band): each event of the band's bin
-// gathers dL/d(images) at the 4 corners of both warps and chains them through the bilinear weights to
-// its flow (eight lanes per event as in k_iwe_bwd_event), and the band's per-pixel sums of those flow
-// gradients are formed in LDS in exact two-word fixed point (SplatLdsX's split: integer adds, so the
-// sums do not depend on the order of the events) and added to g_flows once per touched pixel.  No
-// block reads an event outside its bin (the former scan of the whole window per band is gone).
+// The loss backward's per-event part, per (sample, flow window, band of GB_BAND pixels): each event of
+// the band's bin gathers dL/d(images) at the 4 corners of both warps and chains them through the
+// bilinear weights to its flow (eight lanes per event as in k_iwe_bwd_event), and the band's
+// per-pixel sums of those flow gradients are formed in LDS in exact two-word fixed point (SplatLdsX's
+// split: integer adds, so the sums do not depend on the order of the events) and added to g_flows once
+// per touched pixel.  No block reads an event outside its bin.
 struct GevLds {
-    unsigned long long hi[2][SPLAT_BAND], lo[2][SPLAT_BAND];
+    unsigned long long hi[2][GB_BAND], lo[2][GB_BAND];
 };
 
-__global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
-                                                           float* g_flows, const int* __restrict__ perm,
-                                                           const int* __restrict__ bins, int nbands) {
+__global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
+                                                        float* g_flows, const float4* __restrict__ rec4,
+                                                        const float* __restrict__ rec1, const int* __restrict__ bins,
+                                                        int nbands) {
     __shared__ GevLds acc;
-    __shared__ WinTab wt;
     const int tid = threadIdx.x;
-    wintab_load(a, wt);
     const int blk = xcd_block();  // a sample's windows and bands on one XCD: its flows / image gradients in one L2
     const int band = blk % nbands, rest = blk / nbands, t = rest % a.tf, b = rest / a.tf;
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
-    const int p0 = band * SPLAT_BAND;
-    const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
+    const int p0 = band * GB_BAND;
+    const int np = (int)((HWp - p0) < GB_BAND ? (HWp - p0) : GB_BAND);
     const int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
     int i0, i1;
     flow_window_events(a, t, i0, i1);
     const int e0 = bo[band], e1 = bo[band + 1];
-    const int* pr = perm + (int64_t)b * a.M + i0;
-    for (int j = tid; j < 2 * SPLAT_BAND; j += SPLAT_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
+    const int64_t base = (int64_t)b * a.M + i0;
+    for (int j = tid; j < 2 * GB_BAND; j += GB_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
     // the band's current g_flows values (the pixel backward's), read ahead of the event loop
     float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
-    constexpr int GFR = 2 * SPLAT_BAND / SPLAT_NT;
+    constexpr int GFR = 2 * GB_BAND / GB_NT;
     float gold[GFR];
 #pragma unroll
     for (int k = 0; k < GFR; ++k) {
-        const int j = tid + k * SPLAT_NT, c = j / SPLAT_BAND, q = j - c * SPLAT_BAND;
+        const int j = tid + k * GB_NT, c = j / GB_BAND, q = j - c * GB_BAND;
         gold[k] = q < np ? gf[c * HWp + q] : 0.0f;
     }
+    const float* fl = a.flows[a.tf == 1 ? 0 : t] + (int64_t)b * 2 * HWp;
     __syncthreads();
     const int sub = tid & (kBwdLanes - 1), d = sub >> 2, qc = sub & 3;
     const float tref = d == 0 ? (float)a.T : 0.0f;
     const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
     // every lane runs every round (the lane exchanges need the whole 8-lane group): a slot past the bin
     // contributes zeros
-    for (int s0 = e0; s0 < e1; s0 += SPLAT_NT / kBwdLanes) {
+    for (int s0 = e0; s0 < e1; s0 += GB_NT / kBwdLanes) {
         const int slot = s0 + tid / kBwdLanes;
         const bool on = slot < e1;
         float gwy = 0.0f, gwx = 0.0f, dt = 0.0f;
         int q = -1;
         if (on) {
-            const int i = pr[slot];
-            const EventRef r = event_ref(wt, a.T, b, i);
-            const float4 ev = *reinterpret_cast<const float4*>(r.ev);
-            const float2 pm = *reinterpret_cast<const float2*>(r.pol);
-            const float ts = ev.x + (float)r.k, y = ev.y, x = ev.z;
+            const float4 ev = rec4[base + slot];
+            const float pm1 = rec1[base + slot];
+            const float ts = ev.x, y = ev.y, x = ev.z, pm0 = ev.w;
             const int pix = (int)(y * (float)a.W + x);
             q = pix - p0;
-            const float* fl = wt.fl[a.tf == 1 ? 0 : r.k] + (int64_t)b * 2 * HWp;
             const float fy = fl[HWp + pix], fx = fl[pix];
             const float tsw = d == 0 ? ts : (float)a.T - ts;
             Corner c[4];
@@ -753,8 +759,8 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args
                 if (qc == k) cq = c[k];
             if (cq.inb) {
                 const int id = cq.idx;
-                const float gwt = (gb[id] * pm.x + gb[img + id] * pm.y) +
-                                  (gb[2 * img + id] * (tsw * pm.x) + gb[3 * img + id] * (tsw * pm.y));
+                const float gwt = (gb[id] * pm0 + gb[img + id] * pm1) +
+                                  (gb[2 * img + id] * (tsw * pm0) + gb[3 * img + id] * (tsw * pm1));
                 // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
                 const float gay = gwt * cq.ax, gax = gwt * cq.ay;
                 gwy = -(gay * relu_tie(1.0f - fabsf(cq.dy))) * sgnf(cq.dy);
@@ -784,7 +790,7 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < GFR; ++k) {
-        const int j = tid + k * SPLAT_NT, c = j / SPLAT_BAND, q = j - c * SPLAT_BAND;
+        const int j = tid + k * GB_NT, c = j / GB_BAND, q = j - c * GB_BAND;
         if (q >= np) continue;
         const unsigned long long h = acc.hi[c][q], l = acc.lo[c][q];
         if (h | l) gf[c * HWp + q] = gold[k] + (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75);
@@ -900,8 +906,8 @@ int snnflow_iwe_scratch_floats(int B, int H, int W) { return SPLAT_SPLIT * 8 * B
 
 int snnflow_iwe_bwd_scratch_ints(int B, int M, int H, int W, int tf) {
     const int64_t HWp = (int64_t)H * W;
-    const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
-    return (int)((int64_t)B * M + (int64_t)B * tf * (nbands + 1));
+    const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
+    return (int)((int64_t)B * M * 5 + (int64_t)B * tf * (nbands + 1));  // rec4, rec1, bins
 }
 
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
@@ -934,12 +940,15 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
                        chunks, tsplit);
     if (a->M > 0) {
         if (bin) {  // events binned by pixel band, then per band: event gradients + exact per-pixel sums
-            const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
+            const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
             if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
-            int* perm = bin;
-            int* bins = bin + (int64_t)a->B * a->M;
-            hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(SPLAT_NT), 0, s, *a, nbands, perm, bins);
-            hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(SPLAT_NT), 0, s, *a, gimg, g_flows, perm,
+            if ((reinterpret_cast<uintptr_t>(bin) & 15) != 0) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: bin scratch not 16-B aligned");
+            const int64_t n = (int64_t)a->B * a->M;
+            float4* rec4 = reinterpret_cast<float4*>(bin);  // 16-B aligned: the caller's allocation
+            float* rec1 = reinterpret_cast<float*>(bin) + 4 * n;
+            int* bins = bin + 5 * n;
+            hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(GB_NT), 0, s, *a, nbands, rec4, rec1, bins);
+            hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), 0, s, *a, gimg, g_flows, rec4, rec1,
                                bins, nbands);
         } else {
             hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s,

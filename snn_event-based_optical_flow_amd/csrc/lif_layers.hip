@@ -1267,6 +1267,10 @@ __device__ inline int pk_slot(int q) { return SNNFLOW_SWZ ? q ^ (((q >> 3) & 1) 
 // odd 8-pixel groups swap their two quads.
 __device__ inline int pk_quad(int q, int quad) { return SNNFLOW_SWZ ? quad ^ ((q >> 3) & 1) : quad; }
 
+// The recurrent conv's results (weight-gradient set, dgrad staging) 16 floats further than a bank-row
+// multiple from the feed-forward conv's: lanes n and n + 8 then write different banks.
+constexpr int kPkRecOff = SNNFLOW_SWZ ? 16 : 0;
+
 // The recurrent cell's two weight gradients in one matrix-core pass: the tile holds x and s_prev side
 // by side ([256 pixels][x 0..7 | s 8..15] bf16 in wl_x), so the B operand's columns 0..7 are x and
 // 8..15 are s_prev -- D[co][n] is dW_ff for n < 8 and dW_rec for n >= 8 (the one-conv form leaves
@@ -1274,7 +1278,7 @@ __device__ inline int pk_quad(int q, int quad) { return SNNFLOW_SWZ ? quad ^ ((q
 __device__ void fused_wgrad_stage_pk(const float* G, float* wl_x, float* wl_r, const float (&xsp)[4], const float4& sp,
                                      int pt, int ci0) {
     constexpr int C = 8, PART = HN * C, XS = 16;
-    static_assert(FragFloats<true, 8, 2 * NT>::v >= NT * XS / 2 && FragFloats<true, 8, 2 * NT>::v >= 2 * (kWgfR + kWgfP),
+    static_assert(FragFloats<true, 8, 2 * NT>::v >= NT * XS / 2 && FragFloats<true, 8, 2 * NT>::v >= 2 * (kWgfR + kWgfP) + kPkRecOff,
                   "packed x|s tile in wl_x, both result sets in wl_r");
     const int tid = threadIdx.x;
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -1308,7 +1312,7 @@ __device__ void fused_wgrad_stage_pk(const float* G, float* wl_x, float* wl_r, c
     kstep(8, wv, acc8);
     const int n = lane & 15;
     if (g4 < 2) {  // co = 4 g4 + j < 8
-        float* R = wl_r + (n < C ? 0 : kWgfR + kWgfP);
+        float* R = wl_r + (n < C ? 0 : kWgfR + kWgfP + kPkRecOff);
         float* P8 = R + kWgfR;
         const int ci = n & 7;
 #pragma unroll
@@ -1616,7 +1620,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (pkr) {  // columns n < 8: gx -> wl_x [NT][8]; n >= 8: the recurrent gradient -> wl_r [NT][8]
                 const int lane = tid & 63, n = lane & 15, g4 = lane >> 4;
                 const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-                float* out = (n < 8 ? wl_x : wl_r) + (n & 3);
+                float* out = (n < 8 ? wl_x : wl_r + kPkRecOff) + (n & 3);
 #pragma unroll
                 for (int mt = 0; mt < MfmaAcc<C, CIN, NW, NG>::MT; ++mt) {
                     const int T = MfmaAcc<C, CIN, NW, NG>::mt0(wv) + mt, row = T >> 1, c0 = (T & 1) * 16;
@@ -1633,7 +1637,8 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                     const int64_t plane = (int64_t)a.B * H * W * C;
                     float* gsp = a.g_state_prev + pix * C + cr0;
                     if (a.zero_mem_half) *reinterpret_cast<float4*>(gsp) = z4;
-                    *reinterpret_cast<float4*>(gsp + plane) = *reinterpret_cast<const float4*>(wl_r + pt * 8 + 4 * pk_quad(pt, cr0 >> 2));
+                    *reinterpret_cast<float4*>(gsp + plane) =
+                        *reinterpret_cast<const float4*>(wl_r + kPkRecOff + pt * 8 + 4 * pk_quad(pt, cr0 >> 2));
                 }
             }
         }
@@ -1733,7 +1738,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
                 if (REC && a.s_prev != nullptr && a.wslab_rec != nullptr) {  // dW_ff and dW_rec in one pass
                     fused_wgrad_stage_pk(G, wl_x, wl_r, xsp, wsp, pt, ci0);
                     __syncthreads();
-                    fused_wgrad_store<REC>(a, g, wl_r, wl_r + kWgfR + kWgfP, wold);
+                    fused_wgrad_store<REC>(a, g, wl_r, wl_r + kWgfR + kWgfP + kPkRecOff, wold);
                 } else {
                     fused_wgrad_stage<REC>(a, G, wl_x, wl_r, xsp, wsp, pt, ci0);
                     __syncthreads();
