@@ -381,19 +381,26 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
 constexpr int FIN_NT = 1024;
 
 __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int rows_b) {
+    constexpr int NW = FIN_NT / 64;
     __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
     __shared__ double smp[64][5];          // per-sample smoothness sums
+    __shared__ double part[NW][LOSS_NV];   // per-wave partial sums (several waves per sample when B < 16)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // wave w reduces samples w, w + 16, ...: lane-strided rows, all 11 columns at once
-    for (int b = wv; b < a.B; b += FIN_NT / 64) {
+    // wps waves per sample (B <= 16), each summing a lane-strided share of the sample's rows, all 11
+    // columns at once; B > 16: wave w reduces samples w, w + 16, ...
+    const int wps = a.B <= NW ? NW / a.B : 1;
+    for (int b0 = 0; b0 < a.B; b0 += NW / wps) {
+        const int b = b0 + wv / wps, sub = wv % wps;
         double s[LOSS_NV];
 #pragma unroll
         for (int j = 0; j < LOSS_NV; ++j) s[j] = 0.0;
-        const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
+        if (b < a.B) {
+            const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
 #pragma unroll 4
-        for (int c = lane; c < rows_b; c += 64) {
+            for (int c = sub * 64 + lane; c < rows_b; c += 64 * wps) {
 #pragma unroll
-            for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
+                for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
+            }
         }
 #pragma unroll
         for (int j = 0; j < LOSS_NV; ++j) {
@@ -402,12 +409,20 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
         }
         if (lane == 0) {
 #pragma unroll
-            for (int j = 0; j < 6; ++j) outv[6 * b + j] = s[j];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) smp[b][j] = s[6 + j];
+            for (int j = 0; j < LOSS_NV; ++j) part[wv][j] = s[j];
         }
+        __syncthreads();
+        if (threadIdx.x < (NW / wps) * LOSS_NV) {  // the sample's waves in a fixed order
+            const int bl = threadIdx.x / LOSS_NV, j = threadIdx.x - bl * LOSS_NV, bb = b0 + bl;
+            if (bb < a.B) {
+                double t = 0.0;
+                for (int w = 0; w < wps; ++w) t += part[bl * wps + w][j];
+                if (j < 6) outv[6 * bb + j] = t;
+                else smp[bb][j - 6] = t;
+            }
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (threadIdx.x < 5) {
         double t = 0.0;
         for (int b = 0; b < a.B; ++b) t += smp[b][threadIdx.x];
@@ -637,15 +652,15 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
 // start in that region (the last entry: the window's count).  The order inside a band follows the LDS
 // atomics (it does not matter: the consumer sums in exact fixed point).  One block per (sample, flow
 // window): a band histogram, a wave-0 prefix scan, the placement.
-constexpr int GB_NT = 256, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
+constexpr int GB_NT = 256, BIN_NT = 1024, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
 
 __device__ inline void flow_window_events(const snnflow_iwe_loss_args& a, int t, int& i0, int& i1) {
     i0 = a.tf == 1 ? 0 : a.off[t];
     i1 = a.tf == 1 ? a.M : a.off[t + 1];
 }
 
-__global__ __launch_bounds__(GB_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int nbands, float4* rec4, float* rec1,
-                                                   int* bins) {
+__global__ __launch_bounds__(BIN_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int nbands, float4* rec4, float* rec1,
+                                                    int* bins) {
     __shared__ int cnt[kMaxBands], cur[kMaxBands];
     __shared__ WinTab wt;
     const int tid = threadIdx.x;
@@ -653,14 +668,14 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int 
     const int t = blockIdx.x % a.tf, b = blockIdx.x / a.tf;
     int i0, i1;
     flow_window_events(a, t, i0, i1);
-    for (int k = tid; k < nbands; k += GB_NT) cnt[k] = 0;
+    for (int k = tid; k < nbands; k += BIN_NT) cnt[k] = 0;
     __syncthreads();
     auto band_of = [&](const float* ev) {
         const int pix = (int)(ev[1] * (float)a.W + ev[2]);
         const int k = pix / GB_BAND;
         return k < 0 ? 0 : (k >= nbands ? nbands - 1 : k);
     };
-    for (int i = i0 + tid; i < i1; i += GB_NT) atomicAdd(&cnt[band_of(event_ref(wt, a.T, b, i).ev)], 1);
+    for (int i = i0 + tid; i < i1; i += BIN_NT) atomicAdd(&cnt[band_of(event_ref(wt, a.T, b, i).ev)], 1);
     __syncthreads();
     int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
     if (tid < 64) {  // exclusive prefix over the bands, 64 at a time
@@ -684,7 +699,7 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int 
     }
     __syncthreads();
     const int64_t base = (int64_t)b * a.M + i0;
-    for (int i = i0 + tid; i < i1; i += GB_NT) {
+    for (int i = i0 + tid; i < i1; i += BIN_NT) {
         const EventRef r = event_ref(wt, a.T, b, i);
         const float4 ev = *reinterpret_cast<const float4*>(r.ev);
         const float2 pm = *reinterpret_cast<const float2*>(r.pol);
@@ -947,7 +962,7 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
             float4* rec4 = reinterpret_cast<float4*>(bin);  // 16-B aligned: the caller's allocation
             float* rec1 = reinterpret_cast<float*>(bin) + 4 * n;
             int* bins = bin + 5 * n;
-            hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(GB_NT), 0, s, *a, nbands, rec4, rec1, bins);
+            hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
             hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), 0, s, *a, gimg, g_flows, rec4, rec1,
                                bins, nbands);
         } else {
