@@ -381,26 +381,19 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
 constexpr int FIN_NT = 1024;
 
 __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int rows_b) {
-    constexpr int NW = FIN_NT / 64;
     __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
     __shared__ double smp[64][5];          // per-sample smoothness sums
-    __shared__ double part[NW][LOSS_NV];   // per-wave partial sums (several waves per sample when B < 16)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    // wps waves per sample (B <= 16), each summing a lane-strided share of the sample's rows, all 11
-    // columns at once; B > 16: wave w reduces samples w, w + 16, ...
-    const int wps = a.B <= NW ? NW / a.B : 1;
-    for (int b0 = 0; b0 < a.B; b0 += NW / wps) {
-        const int b = b0 + wv / wps, sub = wv % wps;
+    // wave w reduces samples w, w + 16, ...: lane-strided rows, all 11 columns at once
+    for (int b = wv; b < a.B; b += FIN_NT / 64) {
         double s[LOSS_NV];
 #pragma unroll
         for (int j = 0; j < LOSS_NV; ++j) s[j] = 0.0;
-        if (b < a.B) {
-            const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
+        const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
 #pragma unroll 4
-            for (int c = sub * 64 + lane; c < rows_b; c += 64 * wps) {
+        for (int c = lane; c < rows_b; c += 64) {
 #pragma unroll
-                for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
-            }
+            for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
         }
 #pragma unroll
         for (int j = 0; j < LOSS_NV; ++j) {
@@ -409,20 +402,12 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
         }
         if (lane == 0) {
 #pragma unroll
-            for (int j = 0; j < LOSS_NV; ++j) part[wv][j] = s[j];
+            for (int j = 0; j < 6; ++j) outv[6 * b + j] = s[j];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) smp[b][j] = s[6 + j];
         }
-        __syncthreads();
-        if (threadIdx.x < (NW / wps) * LOSS_NV) {  // the sample's waves in a fixed order
-            const int bl = threadIdx.x / LOSS_NV, j = threadIdx.x - bl * LOSS_NV, bb = b0 + bl;
-            if (bb < a.B) {
-                double t = 0.0;
-                for (int w = 0; w < wps; ++w) t += part[bl * wps + w][j];
-                if (j < 6) outv[6 * bb + j] = t;
-                else smp[bb][j - 6] = t;
-            }
-        }
-        __syncthreads();
     }
+    __syncthreads();
     if (threadIdx.x < 5) {
         double t = 0.0;
         for (int b = 0; b < a.B; ++b) t += smp[b][threadIdx.x];

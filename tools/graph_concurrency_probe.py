@@ -31,6 +31,8 @@ def timed(fn, reps=5):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
+timed(lambda: torch.cuda._sleep(N))  # warm-up
+timed(branches)
 one = timed(lambda: torch.cuda._sleep(N))
 eager = timed(branches)
 g = torch.cuda.CUDAGraph()
