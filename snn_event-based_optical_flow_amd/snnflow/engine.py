@@ -1079,9 +1079,11 @@ class _SlotStreams:
     launch is (HIP graphs run the captured branches concurrently).  The streams fork from and join
     back into the caller's stream; the engine keeps them across calls."""
 
-    def __init__(self, streams, main, K, rec):
+    def __init__(self, streams, main, K, rec, keep):
         self.streams, self.main, self.K, self.rec = streams, main, K, rec
         self.done = {}
+        self.capturing = torch.cuda.is_current_stream_capturing()
+        self.keep = keep
 
     @staticmethod
     def open(eng, dev, K, rec):
@@ -1095,7 +1097,8 @@ class _SlotStreams:
         main = torch.cuda.current_stream(dev)
         for st in ss:
             st.wait_stream(main)
-        return _SlotStreams(ss, main, K, rec)
+        keep = eng.__dict__.setdefault("_slot_stream_events", [])  # the captured graphs' events
+        return _SlotStreams(ss, main, K, rec, keep)
 
     def stream(self, k):
         return self.streams[(k // 2) % len(self.streams)]
@@ -1112,6 +1115,8 @@ class _SlotStreams:
         ev = torch.cuda.Event()
         ev.record(st)
         self.done[key] = ev
+        if self.capturing:  # an event recorded into a graph capture must outlive the capture
+            self.keep.append(ev)
 
     def join(self):
         for st in self.streams:
