@@ -202,9 +202,6 @@ class FireNetEngine:
         # SNNFLOW_DEFER_BWD=0: every node runs its own step's backward
         import os
         self.defer_backward = os.environ.get("SNNFLOW_DEFER_BWD", "1") != "0"
-        # forward_sequence: wavefront tasks as separate launches on this many streams (0: one launch per
-        # wavefront step), _SlotStreams
-        self.slot_streams = int(os.environ.get("SNNFLOW_SLOT_STREAMS", "0"))
         self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
         self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
         # forward_sequence, one-shot: a flat fp32 buffer of L x 2BHWC floats that receives the final
@@ -1070,59 +1067,6 @@ def _ptr_t(t):
 # ---------------------------------------------------------------------------
 # A whole truncated-BPTT window in one autograd node, launched in wavefront order
 # ---------------------------------------------------------------------------
-class _SlotStreams:
-    """Multi-stream form of the wavefront launches (FireNetEngine.slot_streams = n > 0): every
-    (kernel k, step) task of a FireNetSequence pass is its own slot launch on stream (k // 2) % n
-    (the tasks of one wavefront launch, k = d, d-2, ..., land on distinct streams), ordered after the
-    events of the tasks it reads that ran on other streams -- (k-1, t), (k, t-1) and, where rec(k),
-    (k+1, t-1).  A task then starts when its own inputs are done, not when the whole previous
-    launch is (HIP graphs run the captured branches concurrently).  The streams fork from and join
-    back into the caller's stream; the engine keeps them across calls."""
-
-    def __init__(self, streams, main, K, rec, keep):
-        self.streams, self.main, self.K, self.rec = streams, main, K, rec
-        self.done = {}
-        self.capturing = torch.cuda.is_current_stream_capturing()
-        self.keep = keep
-
-    @staticmethod
-    def open(eng, dev, K, rec):
-        n = getattr(eng, "slot_streams", 0)
-        if n <= 0 or _lib.TIMER is not None:
-            return None
-        ss = eng.__dict__.get("_slot_stream_objs")
-        if ss is None or len(ss) != n or ss[0].device != dev:
-            ss = [torch.cuda.Stream(dev) for _ in range(n)]
-            eng._slot_stream_objs = ss
-        main = torch.cuda.current_stream(dev)
-        for st in ss:
-            st.wait_stream(main)
-        keep = eng.__dict__.setdefault("_slot_stream_events", [])  # the captured graphs' events
-        return _SlotStreams(ss, main, K, rec, keep)
-
-    def stream(self, k):
-        return self.streams[(k // 2) % len(self.streams)]
-
-    def launch(self, key, fn):
-        k, t = key
-        st = self.stream(k)
-        for dk, dt in ((k - 1, t), (k, t - 1), (k + 1, t - 1)):
-            if dk < 0 or dk >= self.K or dt < 0 or (dk == k + 1 and not self.rec(k)):
-                continue
-            if self.stream(dk) is not st:
-                st.wait_event(self.done[(dk, dt)])
-        fn(st.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(st)
-        self.done[key] = ev
-        if self.capturing:  # an event recorded into a graph capture must outlive the capture
-            self.keep.append(ev)
-
-    def join(self):
-        for st in self.streams:
-            self.main.wait_stream(st)
-
-
 def wavefront_slots(T, K):
     """Launch order of a (kernel k < K, step t < T) grid whose task (k, t) reads the outputs of
     (k-1, t), (k, t-1) and (k+1, t-1) (the spikes of a recurrent layer come out of the next
@@ -1228,11 +1172,8 @@ class FireNetSequence(torch.autograd.Function):
 
         def spk_skip(l, t):
             return fuse and t < T - 1 and not eng.rec[l] and not eng.keep_seq_states
-        # kernel k of step t reads (k-1, t), (k, t-1) and, for a recurrent layer k, (k+1, t-1) (the spikes
-        # of layer k come out of kernel k+1)
-        ms = _SlotStreams.open(eng, dev, L + 1, lambda k: k < L and bool(eng.rec[k]))
         for tasks in wavefront_slots(T, L + 1):
-            convs, top, keys = [], None, []
+            convs, top = [], None
             for k, t in tasks:
                 if k < L:
                     a = _fwd_conv_args(eng, k, B, H, W, cin0, xs[t], ys[t], stats[t], states[t], mem_in[t],
@@ -1240,24 +1181,14 @@ class FireNetSequence(torch.autograd.Function):
                     if k >= 1 and spk_skip(k - 1, t):
                         a.state_spk_skip = 1
                     convs.append(a)
-                    keys.append((k, t))
                 else:
                     top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons,
                                         flows[t])
                     if spk_skip(L - 1, t):
                         top.state_spk_skip = 1
-                    ktop = (k, t)
-            if ms is not None:  # one launch per task, each on its layer's stream after its inputs' events
-                for a, key in zip(convs, keys):
-                    ms.launch(key, lambda st, a=a: _lib.call("fwd_slot", lib.snnflow_fwd_slot, ctypes.byref(a), 1, None, st))
-                if top is not None:
-                    ms.launch(ktop, lambda st: _lib.call("fwd_slot", lib.snnflow_fwd_slot, None, 0, ctypes.byref(top), st))
-                continue
             arr = (_lib.ConvFwdArgs * max(len(convs), 1))(*convs)
             _lib.call("fwd_slot", lib.snnflow_fwd_slot, arr, len(convs), ctypes.byref(top) if top is not None else None,
                       s)
-        if ms is not None:
-            ms.join()
         _lib.timer_close()
 
         if eng.capture_states:  # tests / diagnostics: the window's pre-BN currents, statistics, batch sums
@@ -1364,16 +1295,14 @@ class FireNetSequence(torch.autograd.Function):
             # (the BN-backward sums of layer L-j), (j, tau-1) (the membrane gradient from step t+1),
             # and (j+1, tau-1) where layer L-j-1 is recurrent (its spikes' gradient from the
             # recurrent dgrad of step t+1)
-            ms = _SlotStreams.open(eng, dev, L + 1, lambda j: j < L and bool(eng.rec[L - 1 - j]))
             for tasks in wavefront_slots(T, L + 1):
-                layers, top, keys = [], None, []
+                layers, top = [], None
                 for j, tau in tasks:
                     t = T - 1 - tau
                     acc = 0 if (fresh and t == T - 1) else 1
                     if j == 0:
                         top = _bwd_top_args(eng, B, H, W, ys[t], stats[t], mem_in[t], neurons, g_into[t], gfl[t],
                                             flows[t], gcur[t], gmem[t], bacc[t])
-                        ktop = (j, tau)
                     else:
                         l = L - j
                         a = _bwd_layer_args(eng, l, B, H, W, cin0, ys[t], stats[t], mem_in[t], neurons,
@@ -1393,19 +1322,9 @@ class FireNetSequence(torch.autograd.Function):
                             a.wslab_accumulate = 1 if eng.slab_live[l] else 0
                             eng.slab_live[l] = True
                         layers.append(a)
-                        keys.append((j, tau))
-                if ms is not None:
-                    for a, key in zip(layers, keys):
-                        ms.launch(key, lambda st, a=a: _lib.call("bwd_slot", lib.snnflow_bwd_slot, ctypes.byref(a), 1, None,
-                                                                 st))
-                    if top is not None:
-                        ms.launch(ktop, lambda st: _lib.call("bwd_slot", lib.snnflow_bwd_slot, None, 0, ctypes.byref(top), st))
-                    continue
                 arr = (_lib.LayerBwdArgs * max(len(layers), 1))(*layers)
                 _lib.call("bwd_slot", lib.snnflow_bwd_slot, arr, len(layers),
                           ctypes.byref(top) if top is not None else None, s)
-            if ms is not None:
-                ms.join()
             _lib.timer_close()
             for l in range(L):
                 for t in range(T):

@@ -1719,46 +1719,3 @@ def test_per_step_chain_backward_batched(dev, case):
             worst = max(worst, e)
             assert e <= 1e-5, (case, n, e)
     print(f"\n[{case}] batched chain backward vs per-node: worst gradient rel-L2 {worst:.2e}")
-
-
-@pytest.mark.parametrize("nstreams", [2, 4])
-def test_forward_sequence_multistream_matches(dev, nstreams):
-    """FireNetEngine.slot_streams: every wavefront task as its own launch on its layer's stream, ordered
-    by events on the tasks it reads (engine._SlotStreams), against the one-launch-per-wavefront-step
-    form on the same window: flows, final states and every parameter gradient (the weight gradients'
-    slab accumulation keeps its order: a layer's tasks share a stream); the fp64 batch-sum atomics may
-    add in another order, so gradients within rel 1e-6 and spikes identical (loss within rtol 1e-6)."""
-    import copy
-
-    import snnflow
-    from oracle import lif_ref
-    from snnflow.synthetic import make_window
-
-    torch.manual_seed(13)
-    B, H, W, T = 4, 64, 64, 6
-    base = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8)).to(dev).train()
-    gen = torch.Generator(device=dev).manual_seed(6)
-    wins = [make_window(B, 700, H, W, gen, dev) for _ in range(T)]
-    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
-           "model": {"mask_output": True}}
-    res = {}
-    for n in (0, nstreams):
-        m = copy.deepcopy(base)
-        m.engine.slot_streams = n
-        lf = snnflow.EventWarping(cfg, dev)
-        outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
-        for o, w in zip(outs, wins):
-            lf.event_flow_association(o["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
-        loss = lf()
-        loss.backward()
-        res[n] = ([o["flow"][0].detach().cpu() for o in outs], loss.item(),
-                  [p.grad.detach().cpu().clone() for p in m.parameters()], [s.detach().cpu() for s in m._states])
-    a, b = res[0], res[nstreams]
-    for fa, fb in zip(a[0], b[0]):
-        np.testing.assert_allclose(fa.numpy(), fb.numpy(), rtol=1e-6, atol=1e-7)
-    for sa, sb in zip(a[3], b[3]):
-        assert torch.equal(sa[1], sb[1])  # spikes
-    np.testing.assert_allclose(a[1], b[1], rtol=1e-6)
-    for ga, gb in zip(a[2], b[2]):
-        e = float((ga - gb).double().norm() / max(float(gb.double().norm()), 1e-30))
-        assert e <= 1e-6, e

@@ -31,11 +31,14 @@ def wave(T=4, K=8):
                         st.wait_event(done[(dk, dt)])
             with torch.cuda.stream(st):
                 torch.cuda._sleep(1000)
-            ev = torch.cuda.Event()
-            ev.record(st)
-            done[(k, t)] = ev
-            if mode == "keep":
-                KEEP.append(ev)
+            # "needed": record only the events some task on another stream will wait for
+            readers = [(k + 1, t), (k, t + 1), (k - 1, t + 1)]
+            if mode != "needed" or any(0 <= rk < K and rt < T and stream(rk) is not st for rk, rt in readers):
+                ev = torch.cuda.Event()
+                ev.record(st)
+                done[(k, t)] = ev
+                if mode in ("keep", "needed"):
+                    KEEP.append(ev)
     for st in ss:
         main.wait_stream(st)
 
