@@ -4413,22 +4413,6 @@ static int env_int(const char* name, int dflt) {
 }
 static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 2);
 static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
-static int g_pipe_fwd_auto = env_int("SNNFLOW_PIPE_FWD_AUTO", 0);
-// Resident blocks of k_fwd_slot<8> on the device (occupancy x CUs), queried once.
-static int fwd_slot8_resident() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_fwd_slot<8>, 2 * NT, 0) != hipSuccess || cus * per <= 0)
-            return 768;
-        n = cus * per;
-    }
-    return n;
-}
-// Block order of a C = 8 launch with pipelined tasks: 0 layer order, 1 pipelined tasks first, 2 last
-static int g_pipe_order = env_int("SNNFLOW_PIPE_ORDER", 1);
-
 // Blocks of a pipelined task: ceil(tiles / tpb), a multiple of 8 (block_tile's XCD groups).
 static int pipe_blocks(int ntiles, int tpb) {
     const int nb = (ntiles + tpb - 1) / tpb;
@@ -4482,22 +4466,7 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
             kind = kind == SK_LIF ? SK_LIF_P : SK_LIF_REC_P;
         p.kind[i] = kind;
     }
-    // tiles per block of the pipelined tasks: g_pipe_fwd, or (SNNFLOW_PIPE_FWD_AUTO) as many as put every
-    // block of the launch into one round of resident blocks
-    int tpb = g_pipe_fwd;
-    if (g_pipe_fwd_auto && c == 8) {
-        int ptiles = 0, other = 0;
-        for (int i = 0; i < nconv; ++i) {
-            if (p.kind[i] == SK_LIF_P || p.kind[i] == SK_LIF_REC_P) ptiles += p.nblk[i];
-            else other += (p.nblk[i] + 7) / 8 * 8;
-        }
-        if (lif) other += slot_top_blocks(c, B, H, W);
-        const int room = fwd_slot8_resident() - other;
-        if (ptiles > 0 && room > 0) {
-            const int need = (ptiles + room - 1) / room;
-            tpb = need > tpb ? (need < 4 ? need : 4) : tpb;
-        }
-    }
+    const int tpb = g_pipe_fwd;
     for (int i = 0; i < nconv; ++i) {
         if (p.kind[i] != SK_LIF_P && p.kind[i] != SK_LIF_REC_P) continue;
         const int nt = p.nblk[i];
