@@ -4413,6 +4413,9 @@ static int env_int(const char* name, int dflt) {
 }
 static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 2);
 static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
+// Block order of a C = 8 launch with pipelined tasks: 0 layer order, 1 pipelined tasks first, 2 last
+static int g_pipe_order = env_int("SNNFLOW_PIPE_ORDER", 1);
+
 // Blocks of a pipelined task: ceil(tiles / tpb), a multiple of 8 (block_tile's XCD groups).
 static int pipe_blocks(int ntiles, int tpb) {
     const int nb = (ntiles + tpb - 1) / tpb;
