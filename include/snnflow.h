@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 36
+#define SNNFLOW_ABI_VERSION 37
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -806,25 +806,47 @@ typedef struct snnflow_firenet_bwd_io {
     snnflow_neuron_grad ng[SNNFLOW_MAX_LAYERS];
     float* g_pred_w; float* g_pred_b;
     int accumulate;                              /* add into the neuron / pred gradients */
-    /* ABI 36, snnflow_firenet_bwd_seq only: the step's previous spikes of recurrent layers (the recurrent
-     * conv's input, for its fused weight gradient) or NULL */
-    const float* s_prev[SNNFLOW_MAX_LAYERS];
 } snnflow_firenet_bwd_io;
 int snnflow_firenet_bwd(const snnflow_firenet_plan* p, const snnflow_firenet_bwd_io* io, void* stream);
 
-/* ABI 36: the backwards of T consecutive time steps of one BPTT chain in wavefront launches
+/* ABI 37: the backwards of T consecutive time steps of one BPTT chain in wavefront launches
  * (snnflow_bwd_slot: task (kernel j, reversed step tau) in launch j + 2 tau, as engine.FireNetSequence),
  * for the per-window drop-in loop whose T model() calls are T autograd nodes: the chain's first step
- * (the last node autograd calls) issues every step's backward in one call.  io[0..T-1] in time order,
- * each as for snnflow_firenet_bwd except: io[t].g_state must be io[t+1].g_prev for t < T-1 (the
- * caller's buffers: the spike half is written, the membrane half only for t = 0); ext[] may be set for
- * t = 0 only; g_x must be NULL.  bwd_acc: T*L backward accumulators (step-major, acc_stride doubles
- * apart, SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC(c)) each), zero on entry.  fused = 1 (c = 8): the weight
- * gradients of layers >= 1 go into plan->slab_* inside the backward tasks, slab_live[l] in/out
- * (0: the layer's slab rows are written, 1: added to); layer 0's (and, with fused = 0, every
- * layer's) stay for snnflow_firenet_wgrad.  c = 8, 16 or 32 (snnflow_slot_supported). */
-int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet_bwd_io* io, int T,
-                            double* bwd_acc, int64_t acc_stride, int fused, int* slab_live, void* stream);
+ * (the last node autograd calls) issues every step's backward in one call.  Steps in time order; each
+ * step t's tensors as snnflow_firenet_fwd wrote them (ys, stats, flow, states [L][2][B][H][W][c]); its
+ * incoming states are step t-1's (step 0: mem_in0 / s_prev0).  Gradients: g_flow[t] (NULL: none) with
+ * element strides (batch, channel); g_state_last = dL/d(the last step's output states) or NULL;
+ * inside the chain the spike halves of the recurrent layers' state gradients live in g_out ((T-1) x
+ * (recurrent layers) buffers of 2BHWc floats, step-major, layer order; the membrane half is never
+ * read); g_prev0[l]: dL/d(step 0's incoming state l) (written when non-NULL: spike half for a recurrent
+ * layer, plus the zero-filled / ext0 membrane half).  g_cur / bnc: [T][L] x the per-step outputs of
+ * snnflow_firenet_bwd.  bwd_acc: T*L backward accumulators (step-major, acc_stride doubles apart,
+ * SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC(c)) each), zero on entry.  fresh = 1: the first task of every
+ * layer writes (does not add to) the neuron / pred gradients.  fused = 1 (c = 8): the weight
+ * gradients of layers >= 1 go into plan->slab_* inside the backward tasks, slab_live[l] in/out (0: the
+ * layer's slab rows are written, 1: added to); layer 0's (and, with fused = 0, every layer's) stay for
+ * snnflow_firenet_wgrad.  c = 8, 16 or 32 (snnflow_slot_supported); 1 <= T <= SNNFLOW_MAX_WINDOWS. */
+typedef struct snnflow_firenet_seq_bwd {
+    int T, fresh, fused;
+    const float* ys[SNNFLOW_MAX_WINDOWS];
+    const float* stats[SNNFLOW_MAX_WINDOWS];
+    const float* flow[SNNFLOW_MAX_WINDOWS];
+    const float* states[SNNFLOW_MAX_WINDOWS];
+    const float* g_flow[SNNFLOW_MAX_WINDOWS];
+    int64_t gflow_sb[SNNFLOW_MAX_WINDOWS], gflow_sc[SNNFLOW_MAX_WINDOWS];
+    const float* mem_in0[SNNFLOW_MAX_LAYERS];
+    const float* s_prev0[SNNFLOW_MAX_LAYERS];
+    float* g_prev0[SNNFLOW_MAX_LAYERS];
+    int ext0[SNNFLOW_MAX_LAYERS];
+    const float* g_state_last[SNNFLOW_MAX_LAYERS];
+    float* g_out;
+    float* g_cur; float* bnc;
+    double* bwd_acc; int64_t acc_stride;
+    snnflow_neuron_grad ng[SNNFLOW_MAX_LAYERS];
+    float* g_pred_w; float* g_pred_b;
+} snnflow_firenet_seq_bwd;
+int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet_seq_bwd* q, int* slab_live,
+                            void* stream);
 
 /* One time step's tensors for the deferred weight gradients (the backward's g_cur / bnc and the
  * forward's ys / stats / states, the step's input and the previous spikes). */

@@ -159,24 +159,33 @@ int snnflow_firenet_bwd(const snnflow_firenet_plan* p, const snnflow_firenet_bwd
     return 0;
 }
 
-int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet_bwd_io* io, int T, double* bwd_acc,
-                            int64_t acc_stride, int fused, int* slab_live, void* stream) {
-    if (check_plan(p) || !io || T < 1 || !bwd_acc || acc_stride < SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC(p->c)) || !slab_live)
+int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet_seq_bwd* q, int* slab_live,
+                            void* stream) {
+    if (check_plan(p) || !q || q->T < 1 || q->T > SNNFLOW_MAX_WINDOWS || !q->bwd_acc || !q->g_cur || !q->bnc ||
+        q->acc_stride < SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC(p->c)) || !slab_live)
         SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: bad arguments");
-    const int L = p->L, C = p->c, top = L - 1, K = L + 1;
-    for (int t = 0; t < T; ++t) {
-        const snnflow_firenet_bwd_io& s = io[t];
-        if (!s.ys || !s.stats || !s.flow || !s.g_cur || !s.bnc || s.g_x)
-            SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: incomplete step (or an input gradient)");
-        for (int l = 0; l < L; ++l) {
-            if (t > 0 && s.ext[l]) SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: external states only at step 0");
-            if (t + 1 < T && s.g_state[l] != io[t + 1].g_prev[l])
-                SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: io[t].g_state must be io[t + 1].g_prev");
-        }
-    }
-    if (fused && C != 8) SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: fused weight gradients need c = 8");
-    const int64_t ny = (int64_t)p->B * p->H * p->W * C;
-    auto acc_of = [&](int t, int l) { return bwd_acc + ((int64_t)t * L + l) * acc_stride; };
+    const int L = p->L, C = p->c, top = L - 1, K = L + 1, T = q->T;
+    if (q->fused && C != 8) SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: fused weight gradients need c = 8");
+    const int64_t npix = (int64_t)p->B * p->H * p->W;
+    const int64_t ny = npix * C, nst = 2 * ny;
+    int rslot[SNNFLOW_MAX_LAYERS], nrec = 0;  // recurrent layer -> its g_out slot within a step
+    for (int l = 0; l < L; ++l) rslot[l] = p->rec[l] ? nrec++ : -1;
+    if (T > 1 && nrec && !q->g_out) SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: g_out missing");
+    for (int t = 0; t < T; ++t)
+        if (!q->ys[t] || !q->stats[t] || !q->flow[t] || !q->states[t])
+            SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: incomplete step");
+    // gradient of step t's incoming state of layer l (t >= 1: inside the chain, recurrent layers only)
+    auto g_in = [&](int t, int l) -> float* {
+        if (t == 0) return q->g_prev0[l];
+        return rslot[l] >= 0 ? q->g_out + ((int64_t)(t - 1) * nrec + rslot[l]) * nst : nullptr;
+    };
+    // gradient flowing into step t's output state of layer l
+    auto g_st = [&](int t, int l) -> const float* { return t == T - 1 ? q->g_state_last[l] : g_in(t + 1, l); };
+    auto mem_in = [&](int t, int l) -> const float* { return t == 0 ? q->mem_in0[l] : q->states[t - 1] + l * nst; };
+    auto s_prev = [&](int t, int l) -> const float* {
+        return t == 0 ? q->s_prev0[l] : (p->rec[l] ? q->states[t - 1] + l * nst + ny : nullptr);
+    };
+    auto acc_of = [&](int t, int l) { return q->bwd_acc + ((int64_t)t * L + l) * q->acc_stride; };
     for (int d = 0; d < K + 2 * (T - 1); ++d) {
         snnflow_layer_bwd_args la[SNNFLOW_MAX_SLOT_TASKS];
         snnflow_lif_bwd_args tb;
@@ -185,20 +194,21 @@ int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet
         for (int j = 0; j < K; ++j) {
             if ((d - j) % 2 || (d - j) < 0 || (d - j) / 2 >= T) continue;
             const int t = T - 1 - (d - j) / 2;
-            const snnflow_firenet_bwd_io& s = io[t];
-            float* g_mem[SNNFLOW_MAX_LAYERS];
-            for (int l = 0; l < L; ++l) g_mem[l] = (s.g_prev[l] && s.ext[l]) ? s.g_prev[l] : nullptr;
+            const float* ys = q->ys[t];
+            const float* stats = q->stats[t];
+            float* gcur = q->g_cur + (int64_t)t * L * ny;
+            auto g_mem = [&](int l) -> float* { return (t == 0 && q->ext0[l] && q->g_prev0[l]) ? q->g_prev0[l] : nullptr; };
             if (j == 0) {  // pred backward + LIF backward of layer L-1
                 snnflow_lif_bwd_args& b = tb;
                 memset(&b, 0, sizeof(b));
                 b.B = p->B; b.H = p->H; b.W = p->W; b.c = C;
-                b.y = s.ys + top * ny; b.mem = s.mem_in[top]; b.stats = s.stats + (int64_t)top * 2 * C; b.n = p->n[top];
-                b.g_state = s.g_state[top];
-                b.pred_w = p->pred_w; b.flow = s.flow;
-                if (s.g_flow) {
-                    b.g_flow = s.g_flow; b.gflow_sb = s.gflow_sb; b.gflow_sc = s.gflow_sc;
+                b.y = ys + top * ny; b.mem = mem_in(t, top); b.stats = stats + (int64_t)top * 2 * C; b.n = p->n[top];
+                b.g_state = g_st(t, top);
+                b.pred_w = p->pred_w; b.flow = q->flow[t];
+                if (q->g_flow[t]) {
+                    b.g_flow = q->g_flow[t]; b.gflow_sb = q->gflow_sb[t]; b.gflow_sc = q->gflow_sc[t];
                 }
-                b.g_cur = s.g_cur + top * ny; b.g_mem = g_mem[top];
+                b.g_cur = gcur + top * ny; b.g_mem = g_mem(top);
                 b.acc = acc_of(t, top);
                 has_top = true;
                 continue;
@@ -208,38 +218,38 @@ int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet
             snnflow_layer_bwd_args& a = la[nl++];
             memset(&a, 0, sizeof(a));
             a.B = p->B; a.H = p->H; a.W = p->W; a.c = C;
-            a.y = s.ys + l * ny; a.stats = s.stats + (int64_t)l * 2 * C; a.g_cur = s.g_cur + l * ny;
+            a.y = ys + l * ny; a.stats = stats + (int64_t)l * 2 * C; a.g_cur = gcur + l * ny;
             a.acc_in = acc_of(t, l);
             a.n = p->n[l];
-            a.ng = s.ng[l];
-            a.accumulate = s.accumulate;
-            a.bnc_out = s.bnc + (int64_t)l * 2 * C;
+            a.ng = q->ng[l];
+            a.accumulate = (q->fresh && t == T - 1) ? 0 : 1;
+            a.bnc_out = q->bnc + ((int64_t)t * L + l) * 2 * C;
             if (l == L - 1) {
-                a.has_pred = 1; a.g_pred_w = s.g_pred_w; a.g_pred_b = s.g_pred_b;
+                a.has_pred = 1; a.g_pred_w = q->g_pred_w; a.g_pred_b = q->g_pred_b;
             }
             if (p->rec[l]) {
                 a.wt_bwd_rec = p->wt_bwd_rec[l]; a.wt_fwd_rec = p->wt_fwd_rec[l];
-                if (s.g_prev[l]) {
-                    a.g_state_prev = s.g_prev[l];
+                if (float* gp = g_in(t, l)) {
+                    a.g_state_prev = gp;
                     // steps t >= 1: the gradient stays inside the chain and its membrane half is never
                     // read (the cells detach the reset); step 0's leaves the chain zero-filled
-                    a.zero_mem_half = (t == 0 && !s.ext[l]) ? 1 : 0;
+                    a.zero_mem_half = (t == 0 && !q->ext0[l]) ? 1 : 0;
                 }
             }
             a.wd_ff = p->wd_ff[l]; a.wd_rec = p->wd_rec[l];
             if (l > 0) {
                 a.cin = C; a.lif_in = 1;
                 a.wt_bwd_ff = p->wt_bwd_ff[l]; a.wt_fwd_ff = p->wt_fwd_ff[l];
-                a.prev_y = s.ys + (l - 1) * ny; a.prev_mem = s.mem_in[l - 1];
-                a.prev_stats = s.stats + (int64_t)(l - 1) * 2 * C; a.prev = p->n[l - 1];
-                a.prev_g_state = s.g_state[l - 1];
-                a.prev_g_cur = s.g_cur + (l - 1) * ny; a.prev_g_mem = g_mem[l - 1];
+                a.prev_y = ys + (l - 1) * ny; a.prev_mem = mem_in(t, l - 1);
+                a.prev_stats = stats + (int64_t)(l - 1) * 2 * C; a.prev = p->n[l - 1];
+                a.prev_g_state = g_st(t, l - 1);
+                a.prev_g_cur = gcur + (l - 1) * ny; a.prev_g_mem = g_mem(l - 1);
                 a.acc_out = acc_of(t, l - 1);
-                if (fused) {
+                if (q->fused) {
                     a.wslab_ff = p->slab_ff[l];
                     if (p->rec[l]) {
                         a.wslab_rec = p->slab_rec[l];
-                        a.s_prev = s.s_prev[l];
+                        a.s_prev = s_prev(t, l);
                     }
                     a.wslab_accumulate = slab_live[l] ? 1 : 0;
                     slab_live[l] = 1;

@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 36
+ABI_VERSION = 37
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -247,8 +247,17 @@ class FireNetBwdIo(ctypes.Structure):
     _fields_ = [("ys", P), ("stats", P), ("flow", P), ("mem_in", PL), ("g_state", PL),
                 ("g_flow", P), ("gflow_sb", I64), ("gflow_sc", I64), ("g_cur", P), ("bnc", P),
                 ("g_prev", PL), ("ext", I32 * MAX_LAYERS), ("g_x", P), ("gxs", I64 * 4),
-                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32),
-                ("s_prev", PL)]
+                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P), ("accumulate", I32)]
+
+
+class FireNetSeqBwd(ctypes.Structure):
+    _fields_ = [("T", I32), ("fresh", I32), ("fused", I32),
+                ("ys", P * MAX_WINDOWS), ("stats", P * MAX_WINDOWS), ("flow", P * MAX_WINDOWS),
+                ("states", P * MAX_WINDOWS), ("g_flow", P * MAX_WINDOWS),
+                ("gflow_sb", I64 * MAX_WINDOWS), ("gflow_sc", I64 * MAX_WINDOWS),
+                ("mem_in0", PL), ("s_prev0", PL), ("g_prev0", PL), ("ext0", I32 * MAX_LAYERS), ("g_state_last", PL),
+                ("g_out", P), ("g_cur", P), ("bnc", P), ("bwd_acc", P), ("acc_stride", I64),
+                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P)]
 
 
 class FireNetWgradStep(ctypes.Structure):
@@ -338,8 +347,7 @@ EXPORTS = {
     "snnflow_unet_pred_param_grads": (I32, [P, I32, I32, P, P, P]),
     "snnflow_firenet_fwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetFwdIo), P]),
     "snnflow_firenet_bwd": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), P]),
-    "snnflow_firenet_bwd_seq": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetBwdIo), I32, P, I64, I32,
-                                      ctypes.POINTER(I32), P]),
+    "snnflow_firenet_bwd_seq": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetSeqBwd), ctypes.POINTER(I32), P]),
     "snnflow_firenet_wgrad": (I32, [ctypes.POINTER(FireNetPlan), ctypes.POINTER(FireNetWgradStep), I32, P, P, P]),
     "snnflow_bn_fwd": (I32, [ctypes.POINTER(BnFwdArgs), P]),
     "snnflow_bn_bwd": (I32, [ctypes.POINTER(BnBwdArgs), P]),

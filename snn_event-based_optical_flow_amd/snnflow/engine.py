@@ -756,7 +756,9 @@ class FireNetStep(torch.autograd.Function):
             chain = _Chain(eng.defer_backward and not x.requires_grad and eng.sequence_ok(cin0))
         elif chain is None:  # continues a forward_sequence window: per-step backwards
             chain = _Chain(False)
-        elif x.requires_grad or any(ext):
+        elif x.requires_grad or any(ext) or chain.last is None or any(
+                p is None or mem_in[l] != chain.last + 4 * l * n1 for l, p in enumerate(prev)):
+            # the batched form reads step t's incoming states as step t-1's output states
             chain.defer = False
         ys_t, stats_t = ys, stats
         plan = None if _lib.TIMER is not None else eng.plan(B, H, W, cin0, ws, wfwd, wbwd)
@@ -780,6 +782,7 @@ class FireNetStep(torch.autograd.Function):
         for l in range(L):  # snn.Leaky's membrane cache, materialised on first read (cells.Leaky.mem)
             eng.lifs[l].__dict__["_mem_lazy"] = (st_all, (B, C, H, W), mst, l * n1)
 
+        chain.last = st_all.data_ptr()
         ctx.eng = eng
         ctx.root = root
         ctx.chain = chain
@@ -814,11 +817,12 @@ class _Chain:
     window of the reference loop, train_flow.py:232-262: T model() calls, one loss.backward()).  With
     ``defer`` the later steps' nodes only record their backward inputs (``steps``) and the chain's first
     step -- the last node autograd calls -- issues every step's backward at once (_chain_backward)."""
-    __slots__ = ("defer", "steps")
+    __slots__ = ("defer", "steps", "last")
 
     def __init__(self, defer):
         self.defer = defer
         self.steps = []
+        self.last = None  # the latest step's state allocation (its L output states back to back)
 
 
 class _StepBwd:
@@ -870,13 +874,15 @@ def _chain_backward_batched(eng, steps):
     if fresh:
         eng.open_chain(dev)
     glayers, gpw, gpb = eng.grad_views()
-    gcur = torch.empty(T, L, B, H, W, C, device=dev)
-    bnc = torch.empty(T, L, 2, C, device=dev)
+    npix = B * H * W
+    nrec = sum(1 for r in eng.rec if r)
     nacc = _lib.acc_storage(_lib.bwd_acc_len(C))
+    # one allocation: [T][L] g_cur, [T][L][2][C] bnc, (T-1) x recurrent-layer state gradients (spike half
+    # written, the membrane half never read inside the chain)
+    ng_, nb_, no_ = T * L * npix * C, T * L * 2 * C, (T - 1) * nrec * 2 * npix * C
+    buf = torch.empty(ng_ + nb_ + no_, device=dev)
+    gcur, bnc = buf[:ng_].view(T, L, B, H, W, C), buf[ng_:ng_ + nb_].view(T, L, 2, C)
     bacc = torch.zeros(T * L * nacc, dtype=torch.float64, device=dev)
-    # gradients of each step's incoming states: inside the chain the spike half of recurrent cells
-    # (steps t >= 1), at the first step what its node returns (FireNetSequence's g0)
-    g_out = [[empty_state(B, C, H, W, dev) if eng.rec[l] else None for l in range(L)] for _ in range(T)]
     g0 = [None] * L
     for l in range(L):
         if not (first.has_prev[l] and first.needs[2 + l]):
@@ -886,37 +892,36 @@ def _chain_backward_batched(eng, steps):
                 (2, B, C, H, W), (B * H * W * C, H * W * C, 1, W * C, C))
         elif eng.rec[l]:
             g0[l] = empty_state(B, C, H, W, dev)
-    g_out[0] = g0
-    g_last = [as_nhwc_state(g) if g is not None else None for g in steps[-1].g_states]
-    ios = (_lib.FireNetBwdIo * T)()
+    q = _lib.FireNetSeqBwd()
+    q.T, q.fresh = T, 1 if fresh else 0
+    fuse = bool(eng.fuse_wgrad) and C == 8
+    q.fused = 1 if fuse else 0
+    q.ys[:T] = [st.saved[1].data_ptr() for st in steps]
+    q.stats[:T] = [st.saved[2].data_ptr() for st in steps]
+    q.flow[:T] = [st.saved[3].data_ptr() for st in steps]
+    q.states[:T] = [st.saved[4].data_ptr() for st in steps]  # (the step's L states: one allocation)
     gfl = []
     for t, st in enumerate(steps):
-        io = ios[t]
-        ys, stats, flow = st.saved[1:4]
-        mem_in, s_prev = st.ptrs
-        io.ys, io.stats, io.flow = ys.data_ptr(), stats.data_ptr(), flow.data_ptr()
-        g_into = g_last if t == T - 1 else g_out[t + 1]
-        for l in range(L):
-            io.mem_in[l] = mem_in[l]
-            io.s_prev[l] = s_prev[l]
-            io.g_state[l] = _ptr_t(g_into[l])
-            io.g_prev[l] = _ptr_t(g_out[t][l])
-            io.ext[l] = 1 if (t == 0 and first.ext[l]) else 0
-            io.ng[l] = glayers[l][2]
         g = st.g_flow
         if g is not None:
             if g.stride(3) != 1 or g.stride(2) != W or g.dtype != torch.float32:
                 g = g.contiguous().float()
-            io.g_flow, io.gflow_sb, io.gflow_sc = g.data_ptr(), g.stride(0), g.stride(1)
+            q.g_flow[t], q.gflow_sb[t], q.gflow_sc[t] = g.data_ptr(), g.stride(0), g.stride(1)
         gfl.append(g)
-        io.g_cur, io.bnc = gcur[t].data_ptr(), bnc[t].data_ptr()
-        io.g_pred_w, io.g_pred_b = gpw, gpb
-        io.accumulate = 0 if (fresh and t == T - 1) else 1
-    fuse = bool(eng.fuse_wgrad) and C == 8
+    mem0, sp0 = first.ptrs
+    gl = [as_nhwc_state(g) if g is not None else None for g in steps[-1].g_states]
+    for l in range(L):
+        q.mem_in0[l], q.s_prev0[l], q.g_prev0[l] = mem0[l], sp0[l], _ptr_t(g0[l])
+        q.ext0[l] = 1 if first.ext[l] else 0
+        q.g_state_last[l] = _ptr_t(gl[l])
+        q.ng[l] = glayers[l][2]
+    q.g_out = buf.data_ptr() + 4 * (ng_ + nb_) if no_ else None
+    q.g_cur, q.bnc = gcur.data_ptr(), bnc.data_ptr()
+    q.bwd_acc, q.acc_stride = bacc.data_ptr(), nacc
+    q.g_pred_w, q.g_pred_b = gpw, gpb
     live = (ctypes.c_int * L)(*[1 if v else 0 for v in eng.slab_live])
     try:
-        _lib.call("firenet_bwd_seq", lib.snnflow_firenet_bwd_seq, ctypes.byref(plan), ios, T, bacc.data_ptr(), nacc,
-                  1 if fuse else 0, live, s)
+        _lib.call("firenet_bwd_seq", lib.snnflow_firenet_bwd_seq, ctypes.byref(plan), ctypes.byref(q), live, s)
         eng.slab_live = [bool(v) for v in live]
         if eng.any_subtract():
             for t, st in enumerate(steps):
@@ -928,7 +933,7 @@ def _chain_backward_batched(eng, steps):
             st = steps[t]
             x, ys, stats = st.saved[:3]
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys), _Rows(stats), x, st.saved[4:4 + L],
-                                st.ptrs[1], (st.saved, gcur, bnc)))
+                                st.ptrs[1], (st.saved, buf)))
             eng.pending_layers.append((0,) if fuse else tuple(range(L)))
         eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
     except Exception:

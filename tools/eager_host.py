@@ -35,6 +35,8 @@ def timed(name, fn):
 def main(steps=20, C=8, R=128, B=8, T=10):
     engine.FireNetStep.forward = staticmethod(timed("step.forward", engine.FireNetStep.forward))
     engine.FireNetStep.backward = staticmethod(timed("step.backward", engine.FireNetStep.backward))
+    engine._chain_backward_batched = timed("chain_backward_batched", engine._chain_backward_batched)
+    engine.FireNetEngine.flush_weight_grads = timed("flush_weight_grads", engine.FireNetEngine.flush_weight_grads)
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
     model = snnflow.LIFFireNet(train_snn_model_kwargs(base_num_channels=C)).to(dev).train()
