@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 37
+#define SNNFLOW_ABI_VERSION 38
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -253,6 +253,11 @@ int snnflow_slot_supported(int c, int cin0);
  * snnflow_get_pipe(0 | 1) reads the forward / backward value. */
 int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block);
 int snnflow_get_pipe(int which);
+/* (ABI 38) the c = 8 LIF-fed backward tasks through the one-tile body with swapped-operand input
+ * gradients (1) or the generic layer body (0); process-wide, default from SNNFLOW_BWD_TILE.  A set
+ * tile pipeline (snnflow_set_pipe, backward > 0) takes precedence. */
+int snnflow_set_bwd_tile(int on);
+int snnflow_get_bwd_tile(void);
 
 #define SNNFLOW_MAX_LAYERS 8   /* cells of a LIFFireNet-family model (the step driver's plan) */
 

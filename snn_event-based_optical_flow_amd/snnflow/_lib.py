@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 37
+ABI_VERSION = 38
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -328,6 +328,8 @@ EXPORTS = {
     "snnflow_slot_supported": (I32, [I32, I32]),
     "snnflow_set_pipe": (I32, [I32, I32]),
     "snnflow_get_pipe": (I32, [I32]),
+    "snnflow_set_bwd_tile": (I32, [I32]),
+    "snnflow_get_bwd_tile": (I32, []),
     "snnflow_frag_halfs": (I32, [I32, I32]),
     "snnflow_unet_conv": (I32, [ctypes.POINTER(UNetConvArgs), P]),
     "snnflow_unet_conv_ksplit": (I32, [ctypes.POINTER(UNetConvArgs)]),

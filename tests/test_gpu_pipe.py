@@ -52,22 +52,30 @@ def _weights(dev, gen, C):
     return wt_fwd, wt_bwd
 
 
-def _run(lib_, fn, tasks, n, tf, tb):
+def _run(lib_, fn, tasks, n, tf, tb, tile=0):
     old = (lib_.lib.snnflow_get_pipe(0), lib_.lib.snnflow_get_pipe(1))
+    old_tile = lib_.lib.snnflow_get_bwd_tile()
     try:
         assert lib_.lib.snnflow_set_pipe(tf, tb) == 0
+        assert lib_.lib.snnflow_set_bwd_tile(tile) == 0
         arr = (type(tasks[0]) * len(tasks))(*tasks)
         lib_.check(fn(arr, n, None, lib_.stream_ptr(torch.device("cuda:0"))), "slot")
         torch.cuda.synchronize()
     finally:
         lib_.lib.snnflow_set_pipe(*old)
+        lib_.lib.snnflow_set_bwd_tile(old_tile)
 
 
-@pytest.mark.parametrize("rec,B,H,W,tb,zr", [(False, 8, 32, 32, 2, True), (True, 8, 32, 32, 2, True),
-                                            (True, 3, 40, 72, 3, False), (False, 2, 24, 96, 1, True)])
-def test_bwd_pipe_task_vs_one_tile(dev, rec, B, H, W, tb, zr):
+@pytest.mark.parametrize("rec,B,H,W,tb,zr,acc", [(False, 8, 32, 32, 2, True, 0), (True, 8, 32, 32, 2, True, 0),
+                                                (True, 3, 40, 72, 3, False, 0), (False, 2, 24, 96, 1, True, 0),
+                                                (True, 8, 32, 32, "tile", True, 0), (False, 8, 32, 32, "tile", True, 1),
+                                                (True, 3, 40, 72, "tile", False, 1), (False, 2, 24, 96, "tile", True, 0),
+                                                (True, 1, 13, 50, "tile", True, 1)])
+def test_bwd_pipe_task_vs_one_tile(dev, rec, B, H, W, tb, zr, acc):
     """One LIF-fed backward task (fused weight gradients, prev_g_state given, recurrent input gradient
-    when rec) through k_bwd_slot<8> and through k_bwd_slot_p8 (bwd_lif8_pipe, tb tiles per block)."""
+    when rec) through k_bwd_slot<8> (layer_bwd_body) and through k_bwd_slot_p8 (bwd_lif8_pipe, tb
+    tiles per block) or, tb = "tile", k_bwd_slot_t8 (bwd_lif8_tile: one tile per block, swapped-operand
+    input gradients); acc: the weight-gradient slabs accumulate onto their old values."""
     from snnflow import _lib
 
     C = 8
@@ -94,6 +102,7 @@ def test_bwd_pipe_task_vs_one_tile(dev, rec, B, H, W, tb, zr):
     pn, kp = _neuron(_lib, dev, gen, C, zero_reset=zr)
     ntiles = _lib.lib.snnflow_conv_blocks(B, H, W)
 
+    slab0 = torch.randn(ntiles, C * C * 9, device=dev, generator=gen)
     outs = {}
     for tag, tbb in (("one", 0), ("pipe", tb)):
         o = {"g_cur": torch.full((P, C), 7.0, device=dev), "g_mem": torch.full((P, C), 7.0, device=dev),
@@ -117,8 +126,14 @@ def test_bwd_pipe_task_vs_one_tile(dev, rec, B, H, W, tb, zr):
         a.prev_y, a.prev_mem, a.prev_stats, a.prev = prev_y.data_ptr(), prev_mem.data_ptr(), prev_stats.data_ptr(), pn
         a.prev_g_state, a.prev_g_cur, a.prev_g_mem = prev_gs.data_ptr(), o["g_cur"].data_ptr(), o["g_mem"].data_ptr()
         a.acc_out = o["acc_out"].data_ptr()
-        a.wslab_ff, a.wslab_accumulate = o["slab_ff"].data_ptr(), 0
-        _run(_lib, _lib.lib.snnflow_bwd_slot, [a], 1, 0, tbb)
+        if acc:
+            o["slab_ff"].copy_(slab0)
+            o["slab_rec"].copy_(slab0.flip(0))
+        a.wslab_ff, a.wslab_accumulate = o["slab_ff"].data_ptr(), acc
+        if tbb == "tile":
+            _run(_lib, _lib.lib.snnflow_bwd_slot, [a], 1, 0, 0, tile=1)
+        else:
+            _run(_lib, _lib.lib.snnflow_bwd_slot, [a], 1, 0, tbb)
         outs[tag] = o
     errs = {}
     for k in ("g_cur", "g_mem", "ng", "bnc") + (("gsp",) if rec else ()):
@@ -126,23 +141,34 @@ def test_bwd_pipe_task_vs_one_tile(dev, rec, B, H, W, tb, zr):
     sums = [outs[x]["acc_out"].view(32, -1)[:, :3 * C].sum(0).cpu().numpy() for x in ("pipe", "one")]
     errs["acc_out"] = _rel(*sums)
     for k in ("slab_ff",) + (("slab_rec",) if rec else ()):
-        errs[k] = _rel(outs["pipe"][k].sum(0).cpu().numpy(), outs["one"][k].sum(0).cpu().numpy())
+        if tb == "tile":  # one slab row per tile in both: row by row
+            errs[k] = _rel(outs["pipe"][k].cpu().numpy(), outs["one"][k].cpu().numpy())
+        else:
+            errs[k] = _rel(outs["pipe"][k].sum(0).cpu().numpy(), outs["one"][k].sum(0).cpu().numpy())
+    if tb == "tile":  # the recomputed spikes: g_cur is zero exactly where no surrogate gradient flows
+        errs["g_cur_max"] = float((outs["pipe"]["g_cur"] - outs["one"]["g_cur"]).abs().max() /
+                                  outs["one"]["g_cur"].abs().max())
     print(f"\n[bwd pipe rec={rec} {B}x{H}x{W} tb={tb}] " + ", ".join(f"{k} {v:.1e}" for k, v in errs.items()))
     for k, v in errs.items():
         assert v < 1e-5, (k, v)
 
 
 def test_bwd_pipe_set_get():
-    """snnflow_set_pipe / snnflow_get_pipe round trip; negative values are refused."""
+    """snnflow_set_pipe / snnflow_get_pipe and snnflow_set_bwd_tile / get round trips; negative tile
+    counts are refused."""
     from snnflow import _lib
 
     old = (_lib.lib.snnflow_get_pipe(0), _lib.lib.snnflow_get_pipe(1))
+    old_tile = _lib.lib.snnflow_get_bwd_tile()
     try:
         assert _lib.lib.snnflow_set_pipe(3, 2) == 0
         assert (_lib.lib.snnflow_get_pipe(0), _lib.lib.snnflow_get_pipe(1)) == (3, 2)
         assert _lib.lib.snnflow_set_pipe(-1, 0) != 0
+        assert _lib.lib.snnflow_set_bwd_tile(5) == 0 and _lib.lib.snnflow_get_bwd_tile() == 1
+        assert _lib.lib.snnflow_set_bwd_tile(0) == 0 and _lib.lib.snnflow_get_bwd_tile() == 0
     finally:
         _lib.lib.snnflow_set_pipe(*old)
+        _lib.lib.snnflow_set_bwd_tile(old_tile)
 
 
 def test_bwd_pipe_debug_dgrad(dev):

@@ -35,6 +35,19 @@ if os.environ.get("SNNFLOW_PIPE_BWD", "0") != "0":
     KINDS[2] = ("pipe_bwd", _B)
     KINDS[3] = ("pipe_bwd_rec", _B)
 
+if os.environ.get("SNNFLOW_BWD_TILE", "0") != "0":  # bwd_lif8_tile (k_bwd_slot_t8)
+    _T = ["prologue", "bn_bwd", "dgrad", "lif_bwd+red", "sums+wgrad"]
+    KINDS[2] = ("tile_bwd", _T)
+    KINDS[3] = ("tile_bwd_rec", _T)
+
+
+def residency(rows, t0, step_us=1.0):
+    """Blocks resident (started, not finished) at each step_us of the launch, over the traced kinds."""
+    st = np.concatenate([(t[:, 0] - t0) * 0.01 for t, _ in rows.values()])
+    en = np.concatenate([(t[:, -1] - t0) * 0.01 for t, _ in rows.values()])
+    grid = np.arange(0.0, float(en.max()) + step_us, step_us)
+    return [int(((st <= x) & (en > x)).sum()) for x in grid]
+
 
 def main(C=8, R=128, B=8, T=10):
     import snnflow
@@ -76,7 +89,7 @@ def main(C=8, R=128, B=8, T=10):
             continue
         t0 = min(t[:, 0].min() for t, _ in rows.values())
         t1 = max(t[:, -1].max() for t, _ in rows.values())
-        out = {"launch_span_us": round(float(t1 - t0) * 0.01, 2)}
+        out = {"launch_span_us": round(float(t1 - t0) * 0.01, 2), "resident_blocks_per_us": residency(rows, t0)}
         for name, (t, phases) in rows.items():
             rel = (t - t0) * 0.01
             d = np.diff(rel, axis=1)

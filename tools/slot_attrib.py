@@ -82,7 +82,11 @@ def main():
     T = int(sys.argv[3]) if len(sys.argv) > 3 else 10
     kinds, A1 = mix(direction, T)
     n = A1.shape[0]
-    vals = dispatch_values(path, f"k_{direction}_slot<8>(")
+    vals = {}
+    for kname in (f"k_{direction}_slot<8>(", f"k_{direction}_slot_t8(", f"k_{direction}_slot_p8("):
+        vals = dispatch_values(path, kname)  # (the C = 8 slot kernel the run launched)
+        if vals:
+            break
     out = {"direction": direction, "T": T, "launches_per_pass": n, "kinds": kinds,
            "tasks_per_launch": A1.tolist(), "quantities": {}}
     for q, v in vals.items():
