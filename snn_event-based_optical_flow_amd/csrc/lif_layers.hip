@@ -3863,11 +3863,15 @@ __device__ void bwd_lif8_tile(const snnflow_layer_bwd_args& a, const Grid g, flo
     }
     const int q = wv * TW + (lane >> 5) * 16 + jj;  // tile pixel
     __bf16* const X = reinterpret_cast<__bf16*>(lds + L::X);
-    __bf16* const S = reinterpret_cast<__bf16*>(lds + L::S);
     if (wgf) {
-        *reinterpret_cast<bf16x4*>(X + q * C + 4 * qd) = bf16x4{(__bf16)xs[0], (__bf16)xs[1], (__bf16)xs[2], (__bf16)xs[3]};
-        if (has_s)
-            *reinterpret_cast<bf16x4*>(S + q * C + 4 * qd) = bf16x4{(__bf16)cs.x, (__bf16)cs.y, (__bf16)cs.z, (__bf16)cs.w};
+        const bf16x4 xv = {(__bf16)xs[0], (__bf16)xs[1], (__bf16)xs[2], (__bf16)xs[3]};
+        if constexpr (REC) {  // x | s_prev side by side ([256][16], pk_slot order): one matrix-core pass for both
+            const int ps = pk_slot(q);
+            *reinterpret_cast<bf16x4*>(X + ps * 16 + 4 * qd) = xv;
+            *reinterpret_cast<bf16x4*>(X + ps * 16 + C + 4 * qd) = bf16x4{(__bf16)cs.x, (__bf16)cs.y, (__bf16)cs.z, (__bf16)cs.w};
+        } else {
+            *reinterpret_cast<bf16x4*>(X + q * C + 4 * qd) = xv;
+        }
     }
     // layer l-1's sums of this block: 16-lane row totals by DPP into LDS (one barrier with the x / s tiles)
 #pragma unroll
@@ -3898,8 +3902,8 @@ __device__ void bwd_lif8_tile(const snnflow_layer_bwd_args& a, const Grid g, flo
     if (wgf) {
         const int g4 = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
         const int j0 = 8 * g4 + qq;
-        f32x4 wacc = {0.f, 0.f, 0.f, 0.f}, wacc8 = wacc, waccr = wacc, wacc8r = wacc;
-        auto kstep = [&](int tap, int row, f32x4& d, f32x4& dr) {
+        f32x4 wacc = {0.f, 0.f, 0.f, 0.f}, wacc8 = wacc;
+        auto kstep = [&](int tap, int row, f32x4& d) {
             const int ky = tap / 3, kx = tap - 3 * ky;
             const int hp = (row + 2 - ky) * HWD + (j0 + 2 - kx);
             const __bf16* ga = G3 + hp * C + 4 * p4;
@@ -3907,36 +3911,29 @@ __device__ void bwd_lif8_tile(const snnflow_layer_bwd_args& a, const Grid g, flo
             const bf16x8 am = tr8(ga + PART, ga + PART + 4 * C);
             const bf16x8 al = tr8(ga + 2 * PART, ga + 2 * PART + 4 * C);
             const int qq2 = row * TW + j0;
-            const __bf16* xb = X + qq2 * C + 4 * p4;
-            const bf16x8 b = tr8(xb, xb + 4 * C);
+            bf16x8 b;
+            if constexpr (REC) b = tr8(X + pk_slot(qq2) * 16 + 4 * p4, X + pk_slot(qq2 + 4) * 16 + 4 * p4);
+            else b = tr8(X + qq2 * C + 4 * p4, X + (qq2 + 4) * C + 4 * p4);
             d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, d, 0, 0, 0);
             d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, d, 0, 0, 0);
             d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, d, 0, 0, 0);
-            if (has_s) {
-                const __bf16* sb = S + qq2 * C + 4 * p4;
-                const bf16x8 bs = tr8(sb, sb + 4 * C);
-                dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bs, dr, 0, 0, 0);
-                dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs, dr, 0, 0, 0);
-                dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs, dr, 0, 0, 0);
-            }
         };
 #pragma unroll 2
-        for (int row = 0; row < TH; ++row) kstep(wv, row, wacc, waccr);
-        kstep(8, wv, wacc8, wacc8r);
-        // results over the (dead) fragments: lane D[co = 4 g4 + j][ci = lane & 15], co, ci < 8 the layer's
+        for (int row = 0; row < TH; ++row) kstep(wv, row, wacc);
+        kstep(8, wv, wacc8);
+        // results over the (dead) fragments: lane D[co = 4 g4 + j][n = lane & 15]; n < 8: dW_ff[co][ci = n],
+        // (REC) n >= 8: dW_rec[co][ci = n - 8]
         float* Rx = reinterpret_cast<float*>(lds + L::FX);  // [kWgfR] taps 0..7, then the tap-8 partials [8][64]
         float* Rr = Rx + kWgfR + kWgfP + kPkRecOff;
-        const int ci = lane & 15;
-        if (ci < C && g4 < 2) {
+        const int n = lane & 15;
+        if ((REC || n < C) && g4 < 2) {
+            float* R = n < C ? Rx : Rr;
+            const int ci = n & 7;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int co = 4 * g4 + j;
-                Rx[(co * C + ci) * 9 + wv] = wacc[j];
-                Rx[kWgfR + wv * 64 + co * C + ci] = wacc8[j];
-                if (has_s) {
-                    Rr[(co * C + ci) * 9 + wv] = waccr[j];
-                    Rr[kWgfR + wv * 64 + co * C + ci] = wacc8r[j];
-                }
+                R[(co * C + ci) * 9 + wv] = wacc[j];
+                R[kWgfR + wv * 64 + co * C + ci] = wacc8[j];
             }
         }
         __syncthreads();
