@@ -246,18 +246,14 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
 int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnflow_lif_bwd_args* lif,
                      void* stream);
 int snnflow_slot_supported(int c, int cin0);
-/* Tuning (ABI 27): tiles per block of the c = 8 LIF-fed tasks of the wavefront launches, forward and
- * backward (0: one tile per block; >= 1: the tile pipelines, which overlap the next tile's halo
- * loads by LDS-DMA with this tile's math).  Process-wide; defaults from SNNFLOW_PIPE_FWD /
- * SNNFLOW_PIPE_BWD at load time.  Results do not depend on it beyond fp64-atomic summation order.
- * snnflow_get_pipe(0 | 1) reads the forward / backward value. */
+/* Tuning (ABI 27): tiles per block of the c = 8 LIF-fed forward tasks of the wavefront launches
+ * (0: one tile per block; >= 1: the tile pipeline, which overlaps the next tile's halo loads by
+ * LDS-DMA with this tile's math).  Process-wide; default from SNNFLOW_PIPE_FWD at load time.  Results
+ * do not depend on it beyond fp64-atomic summation order.  ABI 38: the backward runs one tile per
+ * block only -- bwd_tiles_per_block must be 0 (its tile pipeline measured slower and was removed);
+ * snnflow_get_pipe(0) reads the forward value, snnflow_get_pipe(1) is 0. */
 int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block);
 int snnflow_get_pipe(int which);
-/* (ABI 38) the c = 8 LIF-fed backward tasks through the one-tile body with swapped-operand input
- * gradients (1) or the generic layer body (0); process-wide, default from SNNFLOW_BWD_TILE.  A set
- * tile pipeline (snnflow_set_pipe, backward > 0) takes precedence. */
-int snnflow_set_bwd_tile(int on);
-int snnflow_get_bwd_tile(void);
 
 #define SNNFLOW_MAX_LAYERS 8   /* cells of a LIFFireNet-family model (the step driver's plan) */
 

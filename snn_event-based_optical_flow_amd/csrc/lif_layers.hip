@@ -48,7 +48,9 @@
 #define SNNFLOW_SWZ 1  // C = 8 recurrent backward: bank-conflict-free LDS layouts of the packed x|s tile and dgrad staging
 #endif
 #ifndef SNNFLOW_TRACE_LAYER
-#define SNNFLOW_TRACE_LAYER 1  // stamp layer_bwd_body too (0: the trace build of k_bwd_slot_t8 alone)
+// layer_bwd_body's stamps: off (with them k_bwd_slot<8> fails to compile on ROCm 7.2, "illegal VGPR to
+// SGPR copy": the trace build stamps the forward slot kinds only)
+#define SNNFLOW_TRACE_LAYER 0
 #endif
 #ifndef SNNFLOW_TRACE_MINGRID
 #define SNNFLOW_TRACE_MINGRID 0  // stamp only launches of at least this many blocks (slot launches: 4 tasks)
@@ -2842,8 +2844,7 @@ enum SlotKind : int {
     SK_PLAIN, SK_PLAIN_REC,                  // conv of a C-channel input (no LIF) [+ rec]
     SK_LIF, SK_LIF_REC,                      // LIF(l-1) on the halo + conv(l) [+ rec]
     SK_TOP, SK_TOP_PRED,                     // LIF of the last layer [+ pred]
-    SK_LIF_P, SK_LIF_REC_P,                  // C = 8 SK_LIF / SK_LIF_REC as a tile pipeline (fwd_lif8_pipe)
-    SK_LIF_T, SK_LIF_REC_T                   // C = 8 backward SK_LIF / SK_LIF_REC, one tile per block (bwd_lif8_tile)
+    SK_LIF_P, SK_LIF_REC_P                   // C = 8 forward SK_LIF / SK_LIF_REC as a tile pipeline (fwd_lif8_pipe)
 };
 
 struct FwdSlotParams {
@@ -2871,20 +2872,6 @@ constexpr int kFragC8 = 3 * 3 * 256;  // bf16 entries per conv of the compact C 
 // LDS of the pipeline (bytes): raw y / m halos (680 16-B DMA slots each), the bf16 spike
 // tiles (layer l-1, and s_prev for the recurrent conv), the compact fragments.
 constexpr int kPipeRaw = 2 * HN * 16, kPipeSpk = HN * 8 * 2, kPipeFrag = kFragC8 * 2;
-// LDS of the one-tile C = 8 backward (bwd_lif8_tile)
-template <bool REC>
-struct TileBwdLds {  // bytes
-    // after the weight-gradient MFMAs the result sets (taps 0..7, then the tap-8 partials of the 8 waves)
-    // are staged over FX.. (the fragments are dead by then, the x / s tiles may still be read): the
-    // recurrent set kPkRecOff further
-    static constexpr int STAGE = 4 * ((REC ? 2 : 1) * (kWgfR + kWgfP) + (REC ? kPkRecOff : 0));
-    static constexpr int G3 = 0, FX = 3 * kPipeSpk, FR = FX + kPipeFrag;
-    static constexpr int X = FX + cmax((REC ? 2 : 1) * kPipeFrag, STAGE), S = X + NT * 8 * 2;
-    static constexpr int RED = S + (REC ? NT * 8 * 2 : 0);  // [wave 8][16-lane row 4][12 sums] floats
-    static constexpr int BYTES = RED + 8 * 4 * 12 * 4;
-    static constexpr int FLOATS = BYTES / 4;
-    static_assert(X % 16 == 0 && RED % 16 == 0, "16-B aligned tiles");
-};
 template <bool REC>
 struct PipeFwdLds {
     static constexpr int RAWY = 0, RAWM = kPipeRaw, SPK = 2 * kPipeRaw, RSPK = SPK + kPipeSpk;
@@ -3626,322 +3613,6 @@ __global__ __launch_bounds__(NT * 2, 6) void k_eval_slot(EvalSlotParams) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// C = 8 LIF-fed backward layer-step, one 8x32 tile per block (slot kinds SK_LIF_T / SK_LIF_REC_T):
-// the arithmetic of layer_bwd_body<8, 8, true, REC, 2, false, true> with the per-tile organisation of
-// bwd_lif8_pipe and no state carried between tiles:
-//   * the halos of g_cur and y in registers (issued at kernel start), BN backward of layer l on them
-//     into the three bf16 planes of G;
-//   * input gradients with swapped operands (A = compact weight fragments, rows = input channels;
-//     B = the G planes, six products): after one permlane32_swap per register a lane holds four
-//     channels of one pixel -- the input of the LIF backward of that pixel, no LDS staging, no barrier;
-//   * LIF backward of layer l-1 (stores), the spikes x (and s_prev) to LDS; layer l-1's sums by DPP
-//     row totals into LDS, one barrier for both; then the fp64 sum atomics beside the fused
-//     weight-gradient MFMAs (wave w: tap w over the 8 tile rows and row w of tap 8), one barrier, the
-//     block's slab row.
-// Four barriers (the one-tile body: nine).  LDS: G planes, fragments, x / s tiles, sum rows.
-// ---------------------------------------------------------------------------
-
-#ifndef SNNFLOW_TILE_EARLY
-#define SNNFLOW_TILE_EARLY 1  // the per-pixel loads with the halos (0: after the input-gradient MFMAs)
-#endif
-template <bool REC>
-__device__ void bwd_lif8_tile(const snnflow_layer_bwd_args& a, const Grid g, float* pool) {
-    constexpr int C = 8, NTB = 2 * NT, R = Halo4<C, NTB>::R, PART = HN * C;
-    constexpr int NSUM = SNNFLOW_BWD_ACC(C), NBN = 2 * C, NL = NSUM - NBN;
-    using L = TileBwdLds<REC>;
-    char* const lds = reinterpret_cast<char*>(pool);
-    __shared__ BnBwdLds bnp[C];
-    __shared__ LifCoef pcoef[C];
-    __shared__ float pmean[C];
-    __shared__ double sums[NSUM];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int H = a.H, W = a.W;
-    const Tile tl = block_tile(H, W, g);
-    const bool lead = g.bid == 0;
-    const double N = (double)a.B * H * W;
-    const float nf = (float)N;
-    const bool do_r = REC && a.g_state_prev != nullptr;
-    const bool wgf = a.wslab_ff != nullptr;
-    const bool has_s = REC && wgf && a.s_prev != nullptr && a.wslab_rec != nullptr;
-    const bool zr = a.prev.zero_reset != 0;
-    const bool acc_in = a.wslab_accumulate != 0;
-    TRACE_AT(true, REC ? 3 : 2, 0);
-
-    // 1. every load of the prologue: BN-sum replicas (2C sums; block 0 all), per-channel parameters,
-    //    the weight fragments, the halos of g_cur and y
-    AccGather<NBN> gat;
-    AccGather<NL> gat_l;
-    acc_gather_load<NBN>(a.acc_in, NSUM, gat);
-    if (lead) acc_gather_load<NL>(a.acc_in + NBN, NSUM, gat_l);
-    float st_mean = 0.f, st_inv = 0.f, gamma = 0.f, pmu = 0.f;
-    LifCoef pk = {0.f, 0.f, 0.f, 0.f};
-    if (tid < C) {
-        st_mean = a.stats[tid];
-        st_inv = a.stats[C + tid];
-        gamma = a.n.bn_weight[tid];
-        pk = lif_coef(a.prev, a.prev_stats, C, tid);
-        pmu = a.prev_stats[tid];
-    }
-    const NeuronGradRegs ngr = load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b, lead);
-    FragC8 fz_x, fz_r;
-    fz_x.load(a.wt_fwd_ff);
-    if (do_r) fz_r.load(a.wt_fwd_rec);
-    float4 rg[R], ry[R];
-    halo_load<C, NTB>(a.g_cur, tl, H, W, rg);
-    halo_load<C, NTB>(a.y, tl, H, W, ry);
-    // this lane's pixel: tile row wv, column 16 (lane >> 5) + (lane & 15), channels 4 qd .. 4 qd + 3
-    const int jj = lane & 15, gg = lane >> 4, qd = (lane >> 4) & 1;
-    const int h = tl.h0 + wv, w = tl.w0 + (lane >> 5) * 16 + jj;
-    const bool in = h < H && w < W;
-    const int64_t pix = ((int64_t)tl.b * H + (h < H ? h : H - 1)) * W + (w < W ? w : W - 1);
-    const int64_t plane4 = (int64_t)a.B * H * W * 2;
-    // the LIF backward's per-pixel inputs, in flight with the halos (SNNFLOW_TILE_EARLY)
-    const float4* y4 = reinterpret_cast<const float4*>(a.prev_y);
-    const int64_t q4 = pix * 2 + qd;
-#if SNNFLOW_TILE_EARLY
-    const float4 cy = y4[q4];
-    const float4 cm = ld4_or_zero(reinterpret_cast<const float4*>(a.prev_mem), y4, q4);
-    const float4 cg = ld4_or_zero(a.prev_g_state ? reinterpret_cast<const float4*>(a.prev_g_state) + plane4 : nullptr, y4, q4);
-#endif
-
-    // 2. layer l's neuron gradients (block 0), BN-backward coefficients, layer l-1's LIF coefficients
-    acc_gather_reduce<NBN>(gat, sums);
-    if (lead) acc_gather_reduce<NL>(gat_l, sums + NBN);  // (block-uniform: barriers inside)
-    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b, lead);
-    if (tid < C) {
-        BnBwdLds c;
-        c.mean = st_mean;
-        c.inv = st_inv;
-        c.w = gamma;
-        if (a.n.bn_train) {  // torch batch_norm_cpu_backward: k = dotp*invstd*invstd/n, grad_mean = sum/n
-            c.k = (float)sums[C + tid] * st_inv * st_inv / nf;
-            c.gm = (float)(sums[tid] / N);
-        } else {
-            c.k = 0.0f;
-            c.gm = 0.0f;
-        }
-        bnp[tid] = c;
-        if (lead && a.bnc_out) {
-            a.bnc_out[tid] = c.gm;
-            a.bnc_out[C + tid] = c.k;
-        }
-        pcoef[tid] = pk;
-        pmean[tid] = pmu;
-    }
-    fz_x.store(reinterpret_cast<__bf16*>(lds + L::FX));
-    if (do_r) fz_r.store(reinterpret_cast<__bf16*>(lds + L::FR));
-    __syncthreads();
-    TRACE_AT(true, REC ? 3 : 2, 1);
-    zero_consumed(a.zero0, a.zero1, a.zero_n, g);  // after the gather (vmcnt counts stores)
-
-    // 3. BN backward of layer l over the halo -> G = dL/dy as hi / mid / lo bf16 planes
-    __bf16* const G3 = reinterpret_cast<__bf16*>(lds + L::G3);
-    {
-        const int qt = tid & 1;
-        const BnBwdLds kb[4] = {bnp[4 * qt], bnp[4 * qt + 1], bnp[4 * qt + 2], bnp[4 * qt + 3]};
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            const int e = tid + i * NTB;
-            if (e < 2 * HN) {
-                const int p = e >> 1, r = p / HWD, cc = p - r * HWD;
-                const bool img = in_image(tl.h0 + r - 1, tl.w0 + cc - 1, H, W);
-                const float4 gv = img ? bn_bwd4(rg[i], ry[i], kb) : make_float4(0.f, 0.f, 0.f, 0.f);
-                split3_store4(G3 + p * C + 4 * qt, PART, gv);
-            }
-        }
-    }
-    __syncthreads();
-    TRACE_AT(true, REC ? 3 : 2, 2);
-
-    // 4. input gradients: A = fragments (rows ci), B = G at the flipped tap; six bf16 products
-    f32x4 ax[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, ar[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    {
-        const bf16x8* fx = reinterpret_cast<const bf16x8*>(lds + L::FX) + gg * 8 + (jj & 7);
-        const bf16x8* fr = reinterpret_cast<const bf16x8*>(lds + L::FR) + gg * 8 + (jj & 7);
-#pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            const int tap = 4 * ch + gg, ky = tap / 3, kx = tap - 3 * ky;
-            const bf16x8 wh = fx[ch * 96], wm = fx[ch * 96 + 32], wl = fx[ch * 96 + 64];
-            bf16x8 rh = {}, rm = {}, rl = {};
-            if (do_r) {
-                rh = fr[ch * 96];
-                rm = fr[ch * 96 + 32];
-                rl = fr[ch * 96 + 64];
-            }
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {  // (one column tile's B operands at a time: registers)
-                const int hp = ((wv + 2 - ky) * HWD + mt * 16 + jj + 2 - kx) * C;
-                bf16x8 bh = {}, bm = {}, bl = {};
-                if (tap < 9) {
-                    bh = *reinterpret_cast<const bf16x8*>(G3 + hp);
-                    bm = *reinterpret_cast<const bf16x8*>(G3 + PART + hp);
-                    bl = *reinterpret_cast<const bf16x8*>(G3 + 2 * PART + hp);
-                }
-                f32x4 c = ax[mt];
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bm, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bm, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bh, c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh, c, 0, 0, 0);
-                ax[mt] = c;
-                if (do_r) {
-                    f32x4 d = ar[mt];
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rm, bm, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rh, bl, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rl, bh, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rh, bm, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rm, bh, d, 0, 0, 0);
-                    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rh, bh, d, 0, 0, 0);
-                    ar[mt] = d;
-                }
-            }
-        }
-    }
-#if !SNNFLOW_TILE_EARLY
-    const float4 cy = y4[q4];
-    const float4 cm = ld4_or_zero(reinterpret_cast<const float4*>(a.prev_mem), y4, q4);
-    const float4 cg = ld4_or_zero(a.prev_g_state ? reinterpret_cast<const float4*>(a.prev_g_state) + plane4 : nullptr, y4, q4);
-#endif
-    // s_prev (for the weight gradient only) and the slab rows' old values: after the matrix-core loop
-    const float4 cs = (has_s && in) ? reinterpret_cast<const float4*>(a.s_prev)[q4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float wold[4] = {0.f, 0.f, 0.f, 0.f};  // (e = tid, tid + 512)
-    if (wgf && acc_in) {
-        const float* sf = a.wslab_ff + (int64_t)g.bid * kWgfR;
-        wold[0] = sf[tid];
-        if (tid + 2 * NT < kWgfR) wold[1] = sf[tid + 2 * NT];
-        if (has_s) {
-            const float* sr = a.wslab_rec + (int64_t)g.bid * kWgfR;
-            wold[2] = sr[tid];
-            if (tid + 2 * NT < kWgfR) wold[3] = sr[tid + 2 * NT];
-        }
-    }
-    float gx[4], grc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        // (element values into scalars first: __builtin_bit_cast of an ext_vector element lvalue reads
-        // element 0 of the vector -- ROCm 7.2 clang)
-        const float x0 = ax[0][r], x1 = ax[1][r], r0 = ar[0][r], r1 = ar[1][r];
-        const auto sx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x0), __builtin_bit_cast(unsigned, x1),
-                                                         false, false);
-        gx[r] = __builtin_bit_cast(float, sx[0]);
-        const auto sr = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, r0), __builtin_bit_cast(unsigned, r1),
-                                                         false, false);
-        grc[r] = __builtin_bit_cast(float, sr[0]);
-    }
-    TRACE_AT(true, REC ? 3 : 2, 3);
-
-    // 5. LIF backward of layer l-1 at this lane's pixel
-    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    float sv[12] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (g, (y - mean) g, g m') x 4
-    float xs[4] = {0.f, 0.f, 0.f, 0.f};
-    if (in) {
-        const float yi[4] = {cy.x, cy.y, cy.z, cy.w}, mi[4] = {cm.x, cm.y, cm.z, cm.w}, gi[4] = {cg.x, cg.y, cg.z, cg.w};
-        float go[4], gmo[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const LifCoef kc = pcoef[4 * qd + j];
-            const float gs = gx[j] + gi[j];
-            const LifOut o = lif_step(yi[j], mi[j], kc, zr);
-            const float gv = atan_sg(o.v - kc.theta) * gs;
-            xs[j] = o.s;
-            go[j] = gv;
-            gmo[j] = mem_grad(gv, mi[j], kc, zr);
-            sv[j] = gv;
-            sv[4 + j] = (yi[j] - pmean[4 * qd + j]) * gv;
-            sv[8 + j] = gv * o.mprime;
-        }
-        reinterpret_cast<float4*>(a.prev_g_cur)[q4] = make_float4(go[0], go[1], go[2], go[3]);
-        if (a.prev_g_mem) reinterpret_cast<float4*>(a.prev_g_mem)[q4] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
-        if (do_r) {
-            float4* gsp = reinterpret_cast<float4*>(a.g_state_prev) + q4;
-            if (a.zero_mem_half) gsp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-            gsp[plane4] = make_float4(grc[0], grc[1], grc[2], grc[3]);
-        }
-    }
-    const int q = wv * TW + (lane >> 5) * 16 + jj;  // tile pixel
-    __bf16* const X = reinterpret_cast<__bf16*>(lds + L::X);
-    if (wgf) {
-        const bf16x4 xv = {(__bf16)xs[0], (__bf16)xs[1], (__bf16)xs[2], (__bf16)xs[3]};
-        if constexpr (REC) {  // x | s_prev side by side ([256][16], pk_slot order): one matrix-core pass for both
-            const int ps = pk_slot(q);
-            *reinterpret_cast<bf16x4*>(X + ps * 16 + 4 * qd) = xv;
-            *reinterpret_cast<bf16x4*>(X + ps * 16 + C + 4 * qd) = bf16x4{(__bf16)cs.x, (__bf16)cs.y, (__bf16)cs.z, (__bf16)cs.w};
-        } else {
-            *reinterpret_cast<bf16x4*>(X + q * C + 4 * qd) = xv;
-        }
-    }
-    // layer l-1's sums of this block: 16-lane row totals by DPP into LDS (one barrier with the x / s tiles)
-#pragma unroll
-    for (int j = 0; j < 12; ++j) sv[j] += dppf<0xB1>(sv[j]);
-#pragma unroll
-    for (int j = 0; j < 12; ++j) sv[j] += dppf<0x4E>(sv[j]);
-#pragma unroll
-    for (int j = 0; j < 12; ++j) sv[j] += dppf<0x141>(sv[j]);
-#pragma unroll
-    for (int j = 0; j < 12; ++j) sv[j] += dppf<0x140>(sv[j]);
-    float(*red)[4][12] = reinterpret_cast<float(*)[4][12]>(lds + L::RED);  // [wave][16-lane row][12 sums]
-    if ((lane & 15) == 0) {
-#pragma unroll
-        for (int j = 0; j < 12; ++j) red[wv][lane >> 4][j] = sv[j];
-    }
-    __syncthreads();
-    TRACE_AT(true, REC ? 3 : 2, 4);
-    if (tid < 3 * C) {  // sum kind kk of channel c, fp64, rows and waves in a fixed order
-        const int c = tid & 7, kk = tid >> 3, cq = c >> 2, j = kk * 4 + (c & 3);
-        double sacc = 0.0;
-#pragma unroll
-        for (int w8 = 0; w8 < 8; ++w8) sacc += (double)red[w8][cq][j] + (double)red[w8][cq + 2][j];
-        atomicAdd(acc_shard(a.acc_out, NSUM, g.bid) + kk * C + c, sacc);
-    }
-
-    // 6. fused weight gradients: dW[co][ci][tap] += sum_q G[q - tap][co] X[q][ci]; wave wv owns tap wv over
-    //    the 8 tile rows and row wv of tap 8 (A = G through the transposed reads, B = X; exact products)
-    if (wgf) {
-        const int g4 = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
-        const int j0 = 8 * g4 + qq;
-        f32x4 wacc = {0.f, 0.f, 0.f, 0.f}, wacc8 = wacc;
-        auto kstep = [&](int tap, int row, f32x4& d) {
-            const int ky = tap / 3, kx = tap - 3 * ky;
-            const int hp = (row + 2 - ky) * HWD + (j0 + 2 - kx);
-            const __bf16* ga = G3 + hp * C + 4 * p4;
-            const bf16x8 ah = tr8(ga, ga + 4 * C);
-            const bf16x8 am = tr8(ga + PART, ga + PART + 4 * C);
-            const bf16x8 al = tr8(ga + 2 * PART, ga + 2 * PART + 4 * C);
-            const int qq2 = row * TW + j0;
-            bf16x8 b;
-            if constexpr (REC) b = tr8(X + pk_slot(qq2) * 16 + 4 * p4, X + pk_slot(qq2 + 4) * 16 + 4 * p4);
-            else b = tr8(X + qq2 * C + 4 * p4, X + (qq2 + 4) * C + 4 * p4);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, d, 0, 0, 0);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, d, 0, 0, 0);
-        };
-#pragma unroll 2
-        for (int row = 0; row < TH; ++row) kstep(wv, row, wacc);
-        kstep(8, wv, wacc8);
-        // results over the (dead) fragments: lane D[co = 4 g4 + j][n = lane & 15]; n < 8: dW_ff[co][ci = n],
-        // (REC) n >= 8: dW_rec[co][ci = n - 8]
-        float* Rx = reinterpret_cast<float*>(lds + L::FX);  // [kWgfR] taps 0..7, then the tap-8 partials [8][64]
-        float* Rr = Rx + kWgfR + kWgfP + kPkRecOff;
-        const int n = lane & 15;
-        if ((REC || n < C) && g4 < 2) {
-            float* R = n < C ? Rx : Rr;
-            const int ci = n & 7;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int co = 4 * g4 + j;
-                R[(co * C + ci) * 9 + wv] = wacc[j];
-                R[kWgfR + wv * 64 + co * C + ci] = wacc8[j];
-            }
-        }
-        __syncthreads();
-        fused_wgrad_store<REC>(a, g, Rx, Rr, wold);
-    }
-    TRACE_AT(true, REC ? 3 : 2, 5);
-}
-
 #ifndef SNNFLOW_BWD_SLOT_WAVES
 #define SNNFLOW_BWD_SLOT_WAVES 6  // min waves per SIMD: 3 blocks per CU (measured: 2 per CU is 15 % slower)
 #endif
@@ -3984,491 +3655,6 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L
             const snnflow_lif_bwd_args a = task_args(&pp->lif);
             if constexpr (C >= 16) lif_bwd_q_body<C, true, NT * 2>(a, g, pool);
             else lif_bwd_body<C, true, NT * 2>(a, g);
-            break;
-        }
-        default: break;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// C = 8 LIF-fed backward layer-steps as a tile pipeline (bwd_lif8_pipe; kinds SK_LIF_P /
-// SK_LIF_REC_P of k_bwd_slot_p8).  The same per-tile arithmetic as layer_bwd_body<8, 8, true, REC, 2,
-// false, true> (BN backward of layer l on the halo, input gradients of the ff / rec convs, LIF
-// backward of layer l-1, fused weight gradients), organised like fwd_lif8_pipe:
-//   * once per block: batch-sum shards -> layer l's neuron gradients (block 0), BN-backward
-//     coefficients, layer l-1's LIF coefficients, the transposed-conv weight fragments;
-//   * per tile: the halos of g_cur and y arrive by LDS-DMA one tile ahead, the per-pixel inputs of
-//     the LIF backward (prev_y, prev_mem, prev_g_state, s_prev) in registers one tile ahead;
-//   * the input gradients run with swapped operands (A = weight fragments, rows = input channels;
-//     B = the gradient tile's hi / mid / lo planes, six products), so after one permlane32_swap per
-//     register a lane holds four channels of one pixel -- exactly what the LIF backward of that pixel
-//     needs (no LDS staging of the results);
-//   * the weight gradients accumulate in registers over the block's tiles (fixed tile order), one
-//     slab row per block (the rows of its other tiles are zeroed on the first step); the layer l-1
-//     sums stay in registers over the tiles (one set of fp64 atomics per block).
-// Per tile: wait + barrier -> BN backward (G as three bf16 planes) -> barrier -> next tile's DMA ->
-// input-gradient MFMAs -> LIF backward + stores (spikes x, s_prev to LDS) -> barrier -> weight-gradient
-// MFMAs.  Three barriers per tile.
-// ---------------------------------------------------------------------------
-template <bool REC>
-struct PipeBwdLds {  // bytes
-    static constexpr int RAWG = 0, RAWY = kPipeRaw, G3 = 2 * kPipeRaw;
-    static constexpr int FX = G3 + 3 * kPipeSpk, FR = FX + kPipeFrag;
-    static constexpr int X = FR + (REC ? kPipeFrag : 0), S = X + NT * 8 * 2;
-    static constexpr int BYTES = S + (REC ? NT * 8 * 2 : 0);
-    static constexpr int FLOATS = BYTES / 4;
-    static_assert(2 * kPipeRaw >= 4 * (2 * (kWgfR + kWgfP)), "weight-gradient results staged in the raw halos");
-};
-
-template <bool REC>
-__device__ void bwd_lif8_pipe(const snnflow_layer_bwd_args& a, const Grid g, float* pool) {
-    constexpr int C = 8, NTB = 2 * NT, R = Halo4<C, NTB>::R, PART = HN * C;
-    using L = PipeBwdLds<REC>;
-    char* const lds = reinterpret_cast<char*>(pool);
-    __shared__ BnBwdLds bnp[C];
-    __shared__ LifCoef pcoef[C];
-    __shared__ float pmean[C];
-    __shared__ double sums[SNNFLOW_BWD_ACC(C)];
-    const int tid0 = threadIdx.x, lane0 = tid0 & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid0 >> 6);
-    const int H = a.H, W = a.W, ntiles = a.B * tiles_per_image(H, W);
-    const int nt = pipe_tiles(g, ntiles);
-    const bool lead = g.bid == 0;
-    const double N = (double)a.B * H * W;
-    const float nf = (float)N;
-    const bool do_x = a.wt_bwd_ff != nullptr;
-    const bool do_r = REC && a.g_state_prev != nullptr;
-    const bool wgf = a.wslab_ff != nullptr;
-    const bool has_s = REC && wgf && a.s_prev != nullptr && a.wslab_rec != nullptr;
-    const bool zr = a.prev.zero_reset != 0;
-    TRACE_AT(true, REC ? 3 : 2, 0);
-
-    // ---- prologue: batch sums of layer l, per-channel constants, fragments, the first tile's loads
-    AccGather<SNNFLOW_BWD_ACC(C)> gat;
-    acc_gather_load<SNNFLOW_BWD_ACC(C)>(a.acc_in, SNNFLOW_BWD_ACC(C), gat);
-    float st_mean = 0.f, st_inv = 0.f, gamma = 0.f;
-    LifCoef pk = {0.f, 0.f, 0.f, 0.f};
-    float pmu = 0.f;
-    if (tid0 < C) {
-        st_mean = a.stats[tid0];
-        st_inv = a.stats[C + tid0];
-        gamma = a.n.bn_weight[tid0];
-        pk = lif_coef(a.prev, a.prev_stats, C, tid0);
-        pmu = a.prev_stats[tid0];
-    }
-    const NeuronGradRegs ngr = load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b, lead);
-    FragC8 fz_x, fz_r;
-    if (do_x) fz_x.load(a.wt_fwd_ff);
-    if (do_r) fz_r.load(a.wt_fwd_rec);
-
-    const uint32_t nbytes = (uint32_t)a.B * H * W * C * 4;  // < 2^31 (host check)
-    const __amdgpu_buffer_rsrc_t rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.g_cur), (short)0, (int)nbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.y), (short)0, (int)nbytes, 0x00020000);
-    auto issue = [&](const Tile& t, int lane) {  // halos of g_cur and y: 11 wave-loads each
-        const int base = ((t.b * H + t.h0 - 1) * W + (t.w0 - 1)) * (C * 4);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int k = wv + 8 * j;
-            if (k >= 22) break;
-            const bool isy = k >= 11;
-            const int kk = isy ? k - 11 : k, ee = kk * 64 + lane, p = ee >> 1, r = p / HWD, cc = p - r * HWD;
-            const bool ok = in_image(t.h0 + r - 1, t.w0 + cc - 1, H, W);
-            const uint32_t off = ok ? (uint32_t)(base + (r * W + cc) * (C * 4) + (ee & 1) * 16) : 0x80000000u;
-            if (ee < 2 * HN)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(isy ? rs_y : rs_g, (lds_void*)(lds + (isy ? L::RAWY : L::RAWG) + kk * 1024),
-                                                         16, off, 0, 0, 0);
-        }
-    };
-    auto tile_of = [&](int k) { return block_tile(H, W, Grid{g.bid + k * g.nb, ntiles}); };
-    // this lane's pixel of a tile (the packed dgrad layout): row wv, column 16 (lane >> 5) + (lane & 15),
-    // channels 4 ((lane >> 4) & 1) .. + 3
-    const int64_t plane4 = (int64_t)a.B * H * W * 2;
-    float4 py, pm, pg, ps;  // layer l-1's pre-BN current, membrane, spike-state gradient; s_prev (next tile)
-    auto load_pix = [&](const Tile& t, int lane) {
-        const int h = t.h0 + wv, w = t.w0 + (lane >> 5) * 16 + (lane & 15), qd = (lane >> 4) & 1;
-        const int64_t q = (((int64_t)t.b * H + (h < H ? h : H - 1)) * W + (w < W ? w : W - 1)) * 2 + qd;
-        const float4* y4 = reinterpret_cast<const float4*>(a.prev_y);
-        py = y4[q];
-        pm = ld4_or_zero(reinterpret_cast<const float4*>(a.prev_mem), y4, q);
-        pg = ld4_or_zero(a.prev_g_state ? reinterpret_cast<const float4*>(a.prev_g_state) + plane4 : nullptr, y4, q);
-        ps = has_s ? reinterpret_cast<const float4*>(a.s_prev)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-    Tile tl = tile_of(0);
-    if (nt > 0) {
-        issue(tl, lane0);
-        load_pix(tl, lane0);
-    }
-
-    acc_gather_reduce<SNNFLOW_BWD_ACC(C)>(gat, sums);
-    neuron_grads(ngr, sums, C, a.ng, a.has_pred, a.g_pred_w, a.g_pred_b, lead);
-    if (tid0 < C) {
-        BnBwdLds c;
-        c.mean = st_mean;
-        c.inv = st_inv;
-        c.w = gamma;
-        if (a.n.bn_train) {  // torch batch_norm_cpu_backward: k = dotp*invstd*invstd/n, grad_mean = sum/n
-            c.k = (float)sums[C + tid0] * st_inv * st_inv / nf;
-            c.gm = (float)(sums[tid0] / N);
-        } else {
-            c.k = 0.0f;
-            c.gm = 0.0f;
-        }
-        bnp[tid0] = c;
-        if (lead && a.bnc_out) {
-            a.bnc_out[tid0] = c.gm;
-            a.bnc_out[C + tid0] = c.k;
-        }
-        pcoef[tid0] = pk;
-        pmean[tid0] = pmu;
-    }
-    if (do_x) fz_x.store(reinterpret_cast<__bf16*>(lds + L::FX));
-    if (do_r) fz_r.store(reinterpret_cast<__bf16*>(lds + L::FR));
-    zero_consumed(a.zero0, a.zero1, a.zero_n, g);
-    TRACE_AT(true, REC ? 3 : 2, 1);
-
-    float sv[12] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // (g, (y - mean) g, g m') x 4 channels
-    f32x4 wacc = {0.f, 0.f, 0.f, 0.f}, wacc8 = wacc, waccr = wacc, wacc8r = wacc;  // weight gradients over the tiles
-    float wold[4] = {0.f, 0.f, 0.f, 0.f};  // the slab row's old values (accumulate), loaded with the last tile
-    const bool acc_in = a.wslab_accumulate != 0;
-    __bf16* const G3 = reinterpret_cast<__bf16*>(lds + L::G3);
-    __bf16* const X = reinterpret_cast<__bf16*>(lds + L::X);
-    __bf16* const S = reinterpret_cast<__bf16*>(lds + L::S);
-
-    for (int k = 0; k < nt; ++k) {
-        vm_wait<0>();
-        __syncthreads();  // the halos landed; every wave is done with G3 / X / S of tile k-1
-        const int tid = opaque_int(threadIdx.x), lane = tid & 63, jj = lane & 15, gg = lane >> 4, qt = tid & 1;
-        TRACE_AT(k < 2, REC ? 3 : 2, 2 + 5 * k);
-        // BN backward of layer l over the halo -> G = dL/dy as hi / mid / lo bf16 planes
-        {
-            const BnBwdLds kb[4] = {bnp[4 * qt], bnp[4 * qt + 1], bnp[4 * qt + 2], bnp[4 * qt + 3]};
-#pragma unroll
-            for (int i = 0; i < R; ++i) {
-                const int e = tid + i * NTB;
-                if (e < 2 * HN) {
-                    const int p = e >> 1, r = p / HWD, cc = p - r * HWD;
-                    const bool img = in_image(tl.h0 + r - 1, tl.w0 + cc - 1, H, W);
-                    const float4 gr = *reinterpret_cast<const float4*>(lds + L::RAWG + e * 16);
-                    const float4 yr = *reinterpret_cast<const float4*>(lds + L::RAWY + e * 16);
-                    const float4 gv = img ? bn_bwd4(gr, yr, kb) : make_float4(0.f, 0.f, 0.f, 0.f);
-                    split3_store4(G3 + p * C + 4 * qt, PART, gv);
-                }
-            }
-        }
-        __syncthreads();  // G3 complete; the raw halos are free
-        TRACE_AT(k < 2, REC ? 3 : 2, 3 + 5 * k);
-        const Tile cur = tl;
-        const float4 cy = py, cm = pm, cg = pg, cs = ps;
-        if (k + 1 < nt) {
-            tl = tile_of(k + 1);
-            issue(tl, lane);
-        }
-        if (wgf && acc_in && k + 1 == nt) {  // old slab values, in flight during this tile's math
-            const float* sf = a.wslab_ff + (int64_t)g.bid * kWgfR;
-            wold[0] = sf[tid];
-            if (tid + 2 * NT < kWgfR) wold[1] = sf[tid + 2 * NT];
-            if (has_s) {
-                const float* sr = a.wslab_rec + (int64_t)g.bid * kWgfR;
-                wold[2] = sr[tid];
-                if (tid + 2 * NT < kWgfR) wold[3] = sr[tid + 2 * NT];
-            }
-        }
-
-        // input gradients: A = fragments (rows ci), B = G at the flipped tap; six bf16 products
-        f32x4 ax[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, ar[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-        {
-            const bf16x8* fx = reinterpret_cast<const bf16x8*>(lds + L::FX) + gg * 8 + (jj & 7);
-            const bf16x8* fr = reinterpret_cast<const bf16x8*>(lds + L::FR) + gg * 8 + (jj & 7);
-#pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                const int tap = 4 * ch + gg, ky = tap / 3, kx = tap - 3 * ky;
-                bf16x8 bh[2], bm[2], bl[2];
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    const int hp = ((wv + 2 - ky) * HWD + mt * 16 + jj + 2 - kx) * C;
-                    bh[mt] = bm[mt] = bl[mt] = bf16x8{};
-                    if (tap < 9) {
-                        bh[mt] = *reinterpret_cast<const bf16x8*>(G3 + hp);
-                        bm[mt] = *reinterpret_cast<const bf16x8*>(G3 + PART + hp);
-                        bl[mt] = *reinterpret_cast<const bf16x8*>(G3 + 2 * PART + hp);
-                    }
-                }
-                if (do_x) {
-                    const bf16x8 wh = fx[ch * 96], wm = fx[ch * 96 + 32], wl = fx[ch * 96 + 64];
-#pragma unroll
-                    for (int mt = 0; mt < 2; ++mt) {
-                        f32x4 c = ax[mt];
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bm[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bm[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bh[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh[mt], c, 0, 0, 0);
-                        ax[mt] = c;
-                    }
-                }
-                if (do_r) {
-                    const bf16x8 wh = fr[ch * 96], wm = fr[ch * 96 + 32], wl = fr[ch * 96 + 64];
-#pragma unroll
-                    for (int mt = 0; mt < 2; ++mt) {
-                        f32x4 c = ar[mt];
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bm[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bl[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, bh[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bm[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wm, bh[mt], c, 0, 0, 0);
-                        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, bh[mt], c, 0, 0, 0);
-                        ar[mt] = c;
-                    }
-                }
-            }
-        }
-        float gx[4], grc[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            // (element values into scalars first: __builtin_bit_cast of an ext_vector element lvalue reads
-            // element 0 of the vector -- ROCm 7.2 clang)
-            const float x0 = ax[0][r], x1 = ax[1][r], r0 = ar[0][r], r1 = ar[1][r];
-            const auto sx = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, x0), __builtin_bit_cast(unsigned, x1),
-                                                             false, false);
-            gx[r] = __builtin_bit_cast(float, sx[0]);
-            const auto sr = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, r0), __builtin_bit_cast(unsigned, r1),
-                                                             false, false);
-            grc[r] = __builtin_bit_cast(float, sr[0]);
-        }
-        if (k + 1 < nt) load_pix(tl, lane);  // the next tile's per-pixel inputs (cy.. hold this tile's)
-        TRACE_AT(k < 2, REC ? 3 : 2, 4 + 5 * k);
-
-        // LIF backward of layer l-1 at this lane's pixel and channels 4 qd .. 4 qd + 3
-        const int qd = (lane >> 4) & 1, h = cur.h0 + wv, w = cur.w0 + (lane >> 5) * 16 + jj;
-        const bool in = h < H && w < W;
-        const int64_t pix = ((int64_t)cur.b * H + h) * W + w;
-        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-        float xs[4] = {0.f, 0.f, 0.f, 0.f};
-        if (in) {
-            const float yi[4] = {cy.x, cy.y, cy.z, cy.w}, mi[4] = {cm.x, cm.y, cm.z, cm.w}, gi[4] = {cg.x, cg.y, cg.z, cg.w};
-            float go[4], gmo[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const LifCoef kc = pcoef[4 * qd + j];
-                const float gs = gx[j] + gi[j];
-                const LifOut o = lif_step(yi[j], mi[j], kc, zr);
-                const float gv = atan_sg(o.v - kc.theta) * gs;
-                xs[j] = o.s;
-                go[j] = gv;
-                gmo[j] = mem_grad(gv, mi[j], kc, zr);
-                sv[j] += gv;
-                sv[4 + j] += (yi[j] - pmean[4 * qd + j]) * gv;
-                sv[8 + j] += gv * o.mprime;
-            }
-#ifdef SNNFLOW_PIPE_DEBUG_GX
-            reinterpret_cast<float4*>(a.prev_g_cur)[pix * 2 + qd] = make_float4(gx[0], gx[1], gx[2], gx[3]);
-#else
-            reinterpret_cast<float4*>(a.prev_g_cur)[pix * 2 + qd] = make_float4(go[0], go[1], go[2], go[3]);
-#endif
-            if (a.prev_g_mem) reinterpret_cast<float4*>(a.prev_g_mem)[pix * 2 + qd] = make_float4(gmo[0], gmo[1], gmo[2], gmo[3]);
-            if (do_r) {
-                float4* gsp = reinterpret_cast<float4*>(a.g_state_prev) + pix * 2 + qd;
-                if (a.zero_mem_half) gsp[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-                gsp[plane4] = make_float4(grc[0], grc[1], grc[2], grc[3]);
-            }
-        }
-        const int q = wv * TW + (lane >> 5) * 16 + jj;  // tile pixel
-        if (wgf) {
-            *reinterpret_cast<bf16x4*>(X + q * C + 4 * qd) = bf16x4{(__bf16)xs[0], (__bf16)xs[1], (__bf16)xs[2], (__bf16)xs[3]};
-            if (has_s) {
-                const float4 s4 = in ? cs : make_float4(0.f, 0.f, 0.f, 0.f);
-                *reinterpret_cast<bf16x4*>(S + q * C + 4 * qd) = bf16x4{(__bf16)s4.x, (__bf16)s4.y, (__bf16)s4.z, (__bf16)s4.w};
-            }
-        }
-        TRACE_AT(k < 2, REC ? 3 : 2, 5 + 5 * k);
-        if (wgf) {
-            __syncthreads();  // X / S complete
-            // dW[co][ci][tap] += sum_q G[q - tap][co] X[q][ci]: wave wv owns tap wv over the 8 tile rows and
-            // row wv of tap 8 (A = G through the transposed reads, B = X; exact products, f32 sums)
-            const int g4 = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
-            const int j0 = 8 * g4 + qq;
-            auto kstep = [&](int tap, int row, f32x4& d, f32x4& dr) {
-                const int ky = tap / 3, kx = tap - 3 * ky;
-                const int hp = (row + 2 - ky) * HWD + (j0 + 2 - kx);
-                const __bf16* ga = G3 + hp * C + 4 * p4;
-                const bf16x8 ah = tr8(ga, ga + 4 * C);
-                const bf16x8 am = tr8(ga + PART, ga + PART + 4 * C);
-                const bf16x8 al = tr8(ga + 2 * PART, ga + 2 * PART + 4 * C);
-                const int qq2 = row * TW + j0;
-                const __bf16* xb = X + qq2 * C + 4 * p4;
-                const bf16x8 b = tr8(xb, xb + 4 * C);
-                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, b, d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, b, d, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, b, d, 0, 0, 0);
-                if (has_s) {
-                    const __bf16* sb = S + qq2 * C + 4 * p4;
-                    const bf16x8 bs = tr8(sb, sb + 4 * C);
-                    dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bs, dr, 0, 0, 0);
-                    dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bs, dr, 0, 0, 0);
-                    dr = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bs, dr, 0, 0, 0);
-                }
-            };
-#pragma unroll 2
-            for (int row = 0; row < TH; ++row) kstep(wv, row, wacc, waccr);
-            kstep(8, wv, wacc8, wacc8r);
-        }
-        TRACE_AT(k < 2, REC ? 3 : 2, 6 + 5 * k);
-    }
-
-    // ---- layer l-1's sums of the block's tiles: 16-lane rows by DPP, rows and waves through LDS, fp64 atomics
-    {
-        const int lane = lane0;
-#pragma unroll
-        for (int j = 0; j < 12; ++j) sv[j] += dppf<0xB1>(sv[j]);
-#pragma unroll
-        for (int j = 0; j < 12; ++j) sv[j] += dppf<0x4E>(sv[j]);
-#pragma unroll
-        for (int j = 0; j < 12; ++j) sv[j] += dppf<0x141>(sv[j]);
-#pragma unroll
-        for (int j = 0; j < 12; ++j) sv[j] += dppf<0x140>(sv[j]);
-        __syncthreads();  // (the last tile's weight-gradient reads of G3 / X / S are done: LDS reuse below)
-        float(*red)[4][12] = reinterpret_cast<float(*)[4][12]>(sum_scratch());  // [wave][16-lane row][12 sums]
-        if ((lane & 15) == 0) {
-#pragma unroll
-            for (int j = 0; j < 12; ++j) red[wv][lane >> 4][j] = sv[j];
-        }
-        // weight-gradient results of the waves: lane D[co = 4 g4 + j][ci = lane & 15] (co, ci < 8 are the layer's)
-        float* Rx = reinterpret_cast<float*>(lds + L::RAWG);  // [kWgfR] taps 0..7, then the tap-8 partials [8][64]
-        float* Rr = Rx + kWgfR + kWgfP;
-        const int ci = lane & 15, g4 = lane >> 4;
-        if (wgf && ci < C && g4 < 2) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int co = 4 * g4 + j;
-                Rx[(co * C + ci) * 9 + wv] = wacc[j];
-                Rx[kWgfR + wv * 64 + co * C + ci] = wacc8[j];
-                if (has_s) {
-                    Rr[(co * C + ci) * 9 + wv] = waccr[j];
-                    Rr[kWgfR + wv * 64 + co * C + ci] = wacc8r[j];
-                }
-            }
-        }
-        __syncthreads();
-        const int tid = tid0;
-        if (tid < 3 * C) {  // sum kind kk of channel c
-            const int c = tid & 7, kk = tid >> 3, qd = c >> 2, j = kk * 4 + (c & 3);
-            double s = 0.0;
-#pragma unroll
-            for (int w8 = 0; w8 < 8; ++w8) s += (double)red[w8][qd][j] + (double)red[w8][qd + 2][j];
-            atomicAdd(acc_shard(a.acc_out, SNNFLOW_BWD_ACC(C), g.bid) + kk * C + c, s);
-        }
-        if (wgf && nt > 0) {
-            auto value = [&](const float* base, int e) {
-                const int tap = e % 9;
-                if (tap < 8) return base[e];
-                const float* P8 = base + kWgfR;
-                const int kq = e / 9;
-                float v = P8[kq];
-#pragma unroll
-                for (int w8 = 1; w8 < 8; ++w8) v += P8[w8 * 64 + kq];
-                return v;
-            };
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int e = tid + i * 2 * NT;
-                if (e < kWgfR) {
-                    a.wslab_ff[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[i] + value(Rx, e) : value(Rx, e);
-                    if (REC && a.wslab_rec) {
-                        if (has_s) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = acc_in ? wold[2 + i] + value(Rr, e) : value(Rr, e);
-                        else if (!acc_in) a.wslab_rec[(int64_t)g.bid * kWgfR + e] = 0.0f;
-                    }
-                    if (!acc_in) {  // the rows of the block's other tiles: zero (the block's sum sits in row bid)
-                        for (int kt = 1; kt < nt; ++kt) {
-                            a.wslab_ff[(int64_t)(g.bid + kt * g.nb) * kWgfR + e] = 0.0f;
-                            if (REC && a.wslab_rec) a.wslab_rec[(int64_t)(g.bid + kt * g.nb) * kWgfR + e] = 0.0f;
-                        }
-                    }
-                }
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(NT * 2, 4) void k_bwd_slot_p8(BwdSlotParams) {
-    typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
-    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
-    Grid g;
-    const int k = slot_task(pp, g);
-    if (g.bid >= g.nb) return;
-    __shared__ __attribute__((aligned(16))) float pool[cmax(PipeBwdLds<true>::FLOATS, LayerBwdLds<4, 8, false, false, 2>::FLOATS)];
-    switch (pp->kind[k]) {
-        case SK_HEAD2: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            layer_bwd_body<2, 8, false, false, 2>(a, g, pool);
-            break;
-        }
-        case SK_HEAD4: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            layer_bwd_body<4, 8, false, false, 2>(a, g, pool);
-            break;
-        }
-        case SK_LIF_P: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            bwd_lif8_pipe<false>(a, g, pool);
-            break;
-        }
-        case SK_LIF_REC_P: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            bwd_lif8_pipe<true>(a, g, pool);
-            break;
-        }
-        case SK_TOP: {
-            const snnflow_lif_bwd_args a = task_args(&pp->lif);
-            lif_bwd_body<8, false, NT * 2>(a, g);
-            break;
-        }
-        case SK_TOP_PRED: {
-            const snnflow_lif_bwd_args a = task_args(&pp->lif);
-            lif_bwd_body<8, true, NT * 2>(a, g);
-            break;
-        }
-        default: break;
-    }
-}
-
-// The C = 8 backward slot with the LIF-fed tasks one tile per block (bwd_lif8_tile), the heads and the top
-__global__ __launch_bounds__(NT * 2, SNNFLOW_BWD_SLOT_WAVES) void k_bwd_slot_t8(BwdSlotParams) {
-    typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
-    const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
-    Grid g;
-    const int k = slot_task(pp, g);
-    if (g.bid >= g.nb) return;
-    __shared__ __attribute__((aligned(16))) float pool[cmax(TileBwdLds<true>::FLOATS, LayerBwdLds<4, 8, false, false, 2>::FLOATS)];
-    switch (pp->kind[k]) {
-        case SK_HEAD2: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            layer_bwd_body<2, 8, false, false, 2>(a, g, pool);
-            break;
-        }
-        case SK_HEAD4: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            layer_bwd_body<4, 8, false, false, 2>(a, g, pool);
-            break;
-        }
-        case SK_LIF_T: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            bwd_lif8_tile<false>(a, g, pool);
-            break;
-        }
-        case SK_LIF_REC_T: {
-            const snnflow_layer_bwd_args a = task_args(&pp->layer[k]);
-            bwd_lif8_tile<true>(a, g, pool);
-            break;
-        }
-        case SK_TOP: {
-            const snnflow_lif_bwd_args a = task_args(&pp->lif);
-            lif_bwd_body<8, false, NT * 2>(a, g);
-            break;
-        }
-        case SK_TOP_PRED: {
-            const snnflow_lif_bwd_args a = task_args(&pp->lif);
-            lif_bwd_body<8, true, NT * 2>(a, g);
             break;
         }
         default: break;
@@ -4789,8 +3975,6 @@ static int env_int(const char* name, int dflt) {
     return v && *v ? atoi(v) : dflt;
 }
 static int g_pipe_fwd = env_int("SNNFLOW_PIPE_FWD", 2);
-static int g_pipe_bwd = env_int("SNNFLOW_PIPE_BWD", 0);
-static int g_bwd_tile = env_int("SNNFLOW_BWD_TILE", 0);
 // Block order of a C = 8 launch with pipelined tasks: 0 layer order, 1 pipelined tasks first, 2 last
 static int g_pipe_order = env_int("SNNFLOW_PIPE_ORDER", 1);
 
@@ -4961,25 +4145,7 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
         p.kind[nlayer] = lif->pred_w ? SK_TOP_PRED : SK_TOP;
         p.nblk[nlayer] = slot_top_blocks(c, B, H, W);
     }
-    // C = 8 LIF-fed tasks one tile per block (k_bwd_slot_t8: these, the heads and the top; SNNFLOW_BWD_TILE)
-    bool tile = c == 8 && g_bwd_tile > 0;
-    for (int i = 0; i < nlayer && tile; ++i)
-        tile = p.kind[i] == SK_LIF || p.kind[i] == SK_LIF_REC || p.kind[i] == SK_HEAD2 || p.kind[i] == SK_HEAD4;
-    if (tile)
-        for (int i = 0; i < nlayer; ++i)
-            if (p.kind[i] == SK_LIF || p.kind[i] == SK_LIF_REC) p.kind[i] = p.kind[i] == SK_LIF ? SK_LIF_T : SK_LIF_REC_T;
-    // C = 8 with every LIF-fed task pipelined (k_bwd_slot_p8 holds the pipelines, the heads and the top)
-    bool pipe = c == 8 && g_pipe_bwd > 0 && pipe_fits(B, H, W, c);
-    for (int i = 0; i < nlayer && pipe; ++i)
-        pipe = p.kind[i] == SK_LIF || p.kind[i] == SK_LIF_REC || p.kind[i] == SK_HEAD2 || p.kind[i] == SK_HEAD4;
-    if (pipe) {
-        for (int i = 0; i < nlayer; ++i)
-            if (p.kind[i] == SK_LIF || p.kind[i] == SK_LIF_REC) {
-                p.kind[i] = p.kind[i] == SK_LIF ? SK_LIF_P : SK_LIF_REC_P;
-                p.nblk[i] = pipe_blocks(p.nblk[i], g_pipe_bwd);
-            }
-        if (g_pipe_order) slot_sort(p.layer, p.kind, p.nblk, nlayer, g_pipe_order == 2);
-    } else if (c != 8) {
+    if (c != 8) {
         slot_sort(p.layer, p.kind, p.nblk, nlayer);
     } else if (SNNFLOW_SLOT_ORDER8) {
         slot_sort(p.layer, p.kind, p.nblk, nlayer, SNNFLOW_SLOT_ORDER8 == 2);
@@ -4987,9 +4153,7 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
     p.ntask = nt;
     const int nb = slot_ranges(p.nblk, nt, p.blk0);
     const hipStream_t s = (hipStream_t)stream;
-    if (pipe) hipLaunchKernelGGL(k_bwd_slot_p8, dim3(nb), dim3(2 * NT), 0, s, p);
-    else if (tile) hipLaunchKernelGGL(k_bwd_slot_t8, dim3(nb), dim3(2 * NT), 0, s, p);
-    else if (c == 8) hipLaunchKernelGGL(k_bwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
+    if (c == 8) hipLaunchKernelGGL(k_bwd_slot<8>, dim3(nb), dim3(2 * NT), 0, s, p);
     else if (c == 16) hipLaunchKernelGGL(k_bwd_slot<16>, dim3(nb), dim3(2 * NT), 0, s, p);
     else hipLaunchKernelGGL(k_bwd_slot<32>, dim3(nb), dim3(2 * NT), 0, s, p);
     SNN_CHECK_LAUNCH();
@@ -4997,17 +4161,12 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
 }
 
 int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block) {
-    if (fwd_tiles_per_block < 0 || bwd_tiles_per_block < 0) SNN_FAIL(SNNFLOW_E_ARG, "set_pipe: negative tiles per block");
+    if (fwd_tiles_per_block < 0) SNN_FAIL(SNNFLOW_E_ARG, "set_pipe: negative tiles per block");
+    if (bwd_tiles_per_block != 0) SNN_FAIL(SNNFLOW_E_ARG, "set_pipe: the backward runs one tile per block (ABI 38)");
     g_pipe_fwd = fwd_tiles_per_block;
-    g_pipe_bwd = bwd_tiles_per_block;
     return 0;
 }
-int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : g_pipe_bwd; }
-int snnflow_set_bwd_tile(int on) {
-    g_bwd_tile = on != 0;
-    return 0;
-}
-int snnflow_get_bwd_tile(void) { return g_bwd_tile; }
+int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : 0; }
 
 int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
     if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || a->nsteps <= 0 || a->nsteps > SNNFLOW_MAX_WGRAD_STEPS ||

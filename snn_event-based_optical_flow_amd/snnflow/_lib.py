@@ -328,8 +328,6 @@ EXPORTS = {
     "snnflow_slot_supported": (I32, [I32, I32]),
     "snnflow_set_pipe": (I32, [I32, I32]),
     "snnflow_get_pipe": (I32, [I32]),
-    "snnflow_set_bwd_tile": (I32, [I32]),
-    "snnflow_get_bwd_tile": (I32, []),
     "snnflow_frag_halfs": (I32, [I32, I32]),
     "snnflow_unet_conv": (I32, [ctypes.POINTER(UNetConvArgs), P]),
     "snnflow_unet_conv_ksplit": (I32, [ctypes.POINTER(UNetConvArgs)]),

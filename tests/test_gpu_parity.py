@@ -1437,21 +1437,19 @@ def test_log_activity_with_forward_hooks(dev):
     assert len(seen) == 2
 
 
-@pytest.mark.parametrize("name,B,H,W,T,tf,tb", [("LIFFireNet", 8, 32, 32, 5, 2, 0), ("LIFFireNet", 8, 32, 32, 5, 0, 2),
-                                                 ("LIFFireNet", 8, 32, 32, 5, 2, 2), ("LIFFireNet", 8, 64, 32, 2, 1, 1),
-                                                 ("LIFFireNet", 8, 32, 48, 6, 3, 3), ("LIFFireNet", 3, 40, 72, 4, 2, 2),
-                                                 ("LIFFireNet_short", 8, 32, 32, 4, 4, 4), ("LIFFireFlowNet", 8, 32, 32, 3, 2, 3)])
-def test_pipelined_slots_match_one_tile_slots(dev, name, B, H, W, T, tf, tb):
-    """The C = 8 tile pipelines of the wavefront launches (fwd_lif8_pipe / bwd_lif8_pipe: several tiles
-    per block, the next tile's halos by LDS-DMA, swapped-operand convs packed by permlane32_swap, the
-    weight gradients and batch sums accumulated over a block's tiles) against the one-tile-per-block
-    bodies (snnflow_set_pipe(0, 0)) on the same window: flows, every state, the lif.mem caches,
-    BatchNorm running statistics and num_batches_tracked, and the backward's gradients.  tf / tb:
-    tiles per block of the forward / backward pipelines (0 = the one-tile bodies).  Shapes include
-    partial tiles (W = 48, 40 x 72), a batch that is not a multiple of 8 and blocks with 1-4 tiles.
-    Same per-(layer, step) arithmetic; the batch sums add in another order (fp32 per lane over a
-    block's tiles, fp64 atomics), so spikes may only differ where the membrane lies within rounding of
-    the threshold."""
+@pytest.mark.parametrize("name,B,H,W,T,tf", [("LIFFireNet", 8, 32, 32, 5, 2), ("LIFFireNet", 8, 64, 32, 2, 1),
+                                              ("LIFFireNet", 8, 32, 48, 6, 3), ("LIFFireNet", 3, 40, 72, 4, 2),
+                                              ("LIFFireNet_short", 8, 32, 32, 4, 4), ("LIFFireFlowNet", 8, 32, 32, 3, 2)])
+def test_pipelined_slots_match_one_tile_slots(dev, name, B, H, W, T, tf):
+    """The C = 8 forward tile pipeline of the wavefront launches (fwd_lif8_pipe: several tiles per
+    block, the next tile's halos by LDS-DMA, swapped-operand convs packed by permlane32_swap, the batch
+    sums accumulated over a block's tiles) against the one-tile-per-block bodies (snnflow_set_pipe(0,
+    0)) on the same window: flows, every state, the lif.mem caches, BatchNorm running statistics and
+    num_batches_tracked, and the backward's gradients.  tf: tiles per block of the forward pipeline.
+    Shapes include partial tiles (W = 48, 40 x 72), a batch that is not a multiple of 8 and blocks with
+    1-4 tiles.  Same per-(layer, step) arithmetic; the batch sums add in another order (fp32 per lane
+    over a block's tiles, fp64 atomics), so spikes may only differ where the membrane lies within
+    rounding of the threshold."""
     import copy
 
     import snnflow
@@ -1468,8 +1466,8 @@ def test_pipelined_slots_match_one_tile_slots(dev, name, B, H, W, T, tf, tb):
     res = {}
     old = (_lib.lib.snnflow_get_pipe(0), _lib.lib.snnflow_get_pipe(1))
     try:
-        for tag, m, fwd, bwd in (("pipe", ma, tf, tb), ("one", mb, 0, 0)):
-            assert _lib.lib.snnflow_set_pipe(fwd, bwd) == 0
+        for tag, m, fwd in (("pipe", ma, tf), ("one", mb, 0)):
+            assert _lib.lib.snnflow_set_pipe(fwd, 0) == 0
             outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
             loss = sum(((o["flow"][0] * (t + 1)) ** 2).sum() for t, o in enumerate(outs))
             loss.backward()
@@ -1515,7 +1513,7 @@ def test_pipelined_forward_nonbinary_state(dev):
     old = (_lib.lib.snnflow_get_pipe(0), _lib.lib.snnflow_get_pipe(1))
     try:
         for tag, m, fwd in (("pipe", ma, 2), ("one", mb, 0)):
-            _lib.lib.snnflow_set_pipe(fwd, old[1])
+            _lib.lib.snnflow_set_pipe(fwd, 0)
             m.states = [s.clone() for s in states]
             with torch.no_grad():
                 outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])

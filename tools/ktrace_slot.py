@@ -24,21 +24,12 @@ KINDS = {0: ("conv_fwd", ["prologue", "lif_halo", "conv", "store+sums"]),
          3: ("layer_bwd_rec", ["prologue", "bn_bwd_halo", "dgrad", "lif_bwd+store", "sums", "fused_wgrad"])}
 
 
-# the tile pipelines (fwd_lif8_pipe / bwd_lif8_pipe, 2 tiles per block) stamp per tile; which ones
-# run follows the library's defaults / SNNFLOW_PIPE_FWD / SNNFLOW_PIPE_BWD (0 = one tile per block)
+# the forward tile pipeline (fwd_lif8_pipe, 2 tiles per block) stamps per tile; whether it runs
+# follows the library's default / SNNFLOW_PIPE_FWD (0 = one tile per block)
 if os.environ.get("SNNFLOW_PIPE_FWD", "2") != "0":
     _P = ["gather", "coef", "frag+zero", "wait0", "lif0", "conv0", "wait1", "lif1", "conv1"]
     KINDS[0] = ("pipe_fwd", _P)
     KINDS[1] = ("pipe_fwd_rec", _P)
-if os.environ.get("SNNFLOW_PIPE_BWD", "0") != "0":
-    _B = ["prologue", "wait0", "bn_bwd0", "dgrad0", "lif_bwd0", "wgrad0", "wait1", "bn_bwd1", "dgrad1", "lif_bwd1", "wgrad1"]
-    KINDS[2] = ("pipe_bwd", _B)
-    KINDS[3] = ("pipe_bwd_rec", _B)
-
-if os.environ.get("SNNFLOW_BWD_TILE", "0") != "0":  # bwd_lif8_tile (k_bwd_slot_t8)
-    _T = ["prologue", "bn_bwd", "dgrad", "lif_bwd+red", "sums+wgrad"]
-    KINDS[2] = ("tile_bwd", _T)
-    KINDS[3] = ("tile_bwd_rec", _T)
 
 
 def residency(rows, t0, step_us=1.0):
