@@ -380,9 +380,10 @@ typedef struct snnflow_iwe_loss_args {
     int32_t off[SNNFLOW_MAX_WINDOWS + 1];  /* pass offsets off[0..T], by value */
     float flow_scaling, weight;
     int smoothing_mask, overwrite_intermediate, loss_scaling;
-    float* images;              /* scratch snnflow_iwe_scratch_floats(B, H, W): per-split partial
-                                   IWEs; after the forward its first [2 dir][4 img][B][H*W]
-                                   (cnt+, cnt-, ts+, ts-) hold the totals the backward reads */
+    float* images;              /* 16-B aligned scratch of snnflow_iwe_scratch_floats(B, M, T, tf, H, W)
+                                   floats: the IWEs [2 dir][4 img][B][H*W] (cnt+, cnt-, ts+, ts-),
+                                   then the events binned by warped band (forward) and by own-pixel
+                                   band (backward) -- ABI 38; kept from the forward to the backward */
     double* acc;                /* scratch snnflow_iwe_acc_doubles(B, H, W, tf): per-block partial
                                    sums, reduced in a fixed order (deterministic loss) */
     float* persample;           /* scratch [2 dir][B][4]: S+, S-, nz, loss_b          */
@@ -390,18 +391,16 @@ typedef struct snnflow_iwe_loss_args {
     float* loss;                /* out [1]                                             */
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
-/* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch
- * [2][4][B][H*W].  bin (ABI 35, optional): 16-B aligned scratch of snnflow_iwe_bwd_scratch_ints(B, M, H,
- * W, tf) 32-bit words; with it every (sample, flow window)'s events are copied into bins by the pixel band
- * of their own pixel and one block per band forms their flow gradients and sums them per pixel in exact
- * two-word fixed point
- * (order-independent: bit-reproducible g_flows); NULL: fp32 atomics into g_flows (order-dependent
- * rounding).  H * W <= 2^21. */
+/* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch [2][4][B][H*W].
+ * Reads the forward's images scratch (the IWEs and, ABI 38, the events binned by the pixel band of
+ * their own pixel -- formed by the forward when tf == T, here otherwise); one block per band forms the
+ * events' flow gradients and sums them per pixel in exact two-word fixed point (order-independent:
+ * bit-reproducible g_flows).  H * W <= 2^21. */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
-                         float* g_flows, int* bin, void* stream);
-int snnflow_iwe_bwd_scratch_ints(int B, int M, int H, int W, int tf);
+                         float* g_flows, void* stream);
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf);
-int snnflow_iwe_scratch_floats(int B, int H, int W);  /* floats of the images scratch */
+/* floats of the images scratch (ABI 38: the IWEs and both binnings of the events; H * W <= 2^21) */
+int64_t snnflow_iwe_scratch_floats(int B, int M, int T, int tf, int H, int W);
 
 /* utils/iwe.py:20-71 get_interpolation (+ purge_unfeasible :4-17) for one pass:
  * idx out [B][K*M] int32 (corner-major, K=4 bilinear / 1 rounded), w out [B][K*M]. */

@@ -104,19 +104,23 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
     return a.masks[t] + (int64_t)b * a.H * a.W;
 }
 
-// IWE splat with LDS-privatised images.  One block per (sample, warp direction, band of
-// SPLAT_BAND pixels) owns the four images (cnt+, cnt-, ts+, ts-) of its band in LDS, scans
-// every event of its sample, adds the bilinear corners that fall into the band with LDS
-// atomics, then writes the band once (no memset, no global atomics).
-// images layout: [dir 2][img 4][B][HW].
-// Events of a sample are dealt to nsplit <= SPLAT_SPLIT blocks per band (splat_nsplit: as many as
-// fill the chip once); each writes its own partial image set (images + split * 8*B*HW), summed in
-// fixed order by k_iwe_loss.
+// IWE splat with LDS-privatised images over events binned by the band of their warped corners.
+// k_iwe_wbin, one block per (sample b, event window k): gathers every event's flow at its pixel,
+// warps it to both reference times (warp4: tref = T for direction 0, 0 for direction 1) and files one
+// record per (event, direction, band of SB_BAND pixels touched by a corner of non-zero weight) --
+// rec = (ts + k, y, x, pol mask 0 | flow y, flow x, pol mask 1, 0), 32 B -- into the (b, k) region of
+// the record scratch, direction-major and band by band (a band histogram in LDS, a wave-0 prefix scan,
+// the placement; bins [B][T][2 nbands + 1]: each (direction, band)'s start in the region).
+// k_iwe_splat, one block per (sample, direction, band): owns the four images (cnt+, cnt-, ts+, ts-) of
+// its band in LDS, reads the band's records of the T windows (contiguous, no rescan of the event
+// lists: every record is read once), re-warps them (the same warp4 on the same inputs: the same
+// corners and weights) and adds the corners inside the band, then writes the band once (no memset, no
+// global atomics).  images layout: [dir 2][img 4][B][HW].
 // Deterministic accumulation (SNNFLOW_SPLAT_FIXED, default): every corner contribution v is split
 // exactly into two 64-bit fixed-point integers, v = H 2^-32 + L 2^-75 (H = rint(v 2^32) in double,
 // L = rint((v - H 2^-32) 2^75): exact for |v| >= 2^-51), and the two are added with integer LDS
 // atomics.  Integer addition is associative, so the band totals -- the whole IWE -- are the same
-// bits on every run whatever order the events' atomics land in, and they are the exact sums of the
+// bits on every run whatever order the records' atomics land in, and they are the exact sums of the
 // fp32 contributions (rounded once to fp32 at the end).  Two words because the loss reads ratios
 // (ts image / count image, loss/flow.py:219-233) that do not shrink with the weights: a pixel hit
 // only by a 1e-7 corner still contributes ts^2 to the loss, so the fraction needs relative, not
@@ -125,25 +129,21 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 #ifndef SNNFLOW_SPLAT_FIXED
 #define SNNFLOW_SPLAT_FIXED 1
 #endif
-#ifndef SNNFLOW_SPLAT_SPLIT
-#define SNNFLOW_SPLAT_SPLIT 4
-#endif
-#ifndef SNNFLOW_SPLAT_PROBE
-#define SNNFLOW_SPLAT_PROBE 0  // timing attribution only: 1 = no LDS adds, 2 = no event loop
-#endif
 constexpr bool kSplatFixed = SNNFLOW_SPLAT_FIXED != 0;
-constexpr int SPLAT_NT = 1024, SPLAT_BAND = kSplatFixed ? 2048 : 4096, SPLAT_SPLIT = SNNFLOW_SPLAT_SPLIT;
+constexpr int SPLAT_NT = 1024, SB_BAND = 1024, WB_NT = 1024, WB_U = 2, kMaxSBands = 2048;  // H W <= 2^21 pixels
+// the loss backward's bins (k_iwe_bin / k_iwe_wbin, k_iwe_bwd_band): bands of GB_BAND pixels
+constexpr int GB_NT = 256, BIN_NT = 1024, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
 
 struct SplatLdsF {  // fp32 images
-    float v[4][SPLAT_BAND];
-    __device__ void zero(int tid) { for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&v[0][0])[j] = 0.0f; }
+    float v[4][SB_BAND];
+    __device__ void zero(int tid) { for (int j = tid; j < 4 * SB_BAND; j += SPLAT_NT) (&v[0][0])[j] = 0.0f; }
     __device__ void add(int q, int i, float x) { atomicAdd(&v[q][i], x); }
     __device__ float get(int q, int i) const { return v[q][i]; }
 };
 struct SplatLdsX {  // exact two-word fixed point
-    unsigned long long hi[4][SPLAT_BAND], lo[4][SPLAT_BAND];
+    unsigned long long hi[4][SB_BAND], lo[4][SB_BAND];
     __device__ void zero(int tid) {
-        for (int j = tid; j < 4 * SPLAT_BAND; j += SPLAT_NT) (&hi[0][0])[j] = 0, (&lo[0][0])[j] = 0;
+        for (int j = tid; j < 4 * SB_BAND; j += SPLAT_NT) (&hi[0][0])[j] = 0, (&lo[0][0])[j] = 0;
     }
     __device__ void add(int q, int i, float x) {
         // corner weights (x ts) lie in [0, 1]; the clamp keeps any input inside the fixed-point range
@@ -161,91 +161,276 @@ struct SplatLdsX {  // exact two-word fixed point
 };
 typedef std::conditional_t<kSplatFixed, SplatLdsX, SplatLdsF> SplatLds;
 
-// Events per thread and pass: their loads (event, polarity, then the flow gather) are all issued
-// before any of them is splatted, so a thread waits for one chain of dependent loads per SPLAT_U
-// events instead of per event.
-constexpr int SPLAT_U = 4;  // (8, one round of dependent loads per thread at cfg2: measured no faster)
+// Records per (event, direction) at most: the non-zero corners of a warp lie within 2 W + 2 pixels
+// (y1 = floor(wy + 1) may exceed floor(wy) + 1 by one under rounding, likewise x1).
+__host__ __device__ inline int splat_rec_per_event(int W) { return (2 * W + 2) / SB_BAND + 2; }
+__host__ __device__ inline int splat_bands(int64_t HWp) { return (int)((HWp + SB_BAND - 1) / SB_BAND); }
 
-// Partial image sets per band: enough blocks for one per CU (256), at most SPLAT_SPLIT.
-__host__ __device__ inline int splat_nsplit(int B, int nbands) {
-    const int base = B * 2 * nbands, s = (256 + base - 1) / base;
-    return s < 1 ? 1 : (s > SPLAT_SPLIT ? SPLAT_SPLIT : s);
+// The record scratch after the images: [B M R 2] records of 32 B ((b, k) region at R 2 (b M + off[k]))
+// and the bin table [B][T][2 nbands + 1] ints.
+__host__ __device__ inline int64_t splat_img_floats(int B, int64_t HWp) { return 8 * (int64_t)B * HWp; }
+__host__ __device__ inline int64_t splat_rec_floats(int B, int M, int W) { return (int64_t)B * M * splat_rec_per_event(W) * 2 * 8; }
+
+// The loss scratch (snnflow_iwe_scratch_floats), float offsets, each region 16-B aligned: the IWEs, the
+// forward's records and bin table, the backward's records (rec4 = (ts + window, y, x, pol mask 0),
+// rec1 = pol mask 1) and bin table [B][tf][nbands_g + 1].
+struct LossScratch {
+    int64_t rec, bins, rec4, rec1, gbins, total;
+    __host__ __device__ LossScratch(int B, int M, int T, int tf, int H, int W) {
+        const int64_t HWp = (int64_t)H * W;
+        auto up4 = [](int64_t x) { return (x + 3) / 4 * 4; };
+        rec = splat_img_floats(B, HWp);
+        bins = rec + splat_rec_floats(B, M, W);
+        rec4 = up4(bins + (int64_t)B * T * (2 * ((HWp + SB_BAND - 1) / SB_BAND) + 1));
+        rec1 = rec4 + 4 * (int64_t)B * M;
+        gbins = rec1 + (int64_t)B * M;
+        total = gbins + (int64_t)B * tf * ((HWp + GB_BAND - 1) / GB_BAND + 1);
+    }
+};
+
+// The bands (ascending, distinct) that the non-zero corners of one warp touch, as a count and the
+// first band; corners are idx-ordered (c0 <= c1 <= c2 <= c3 for in-image corners).
+template <typename F>
+__device__ inline void corner_bands(const Corner (&c)[4], F&& visit) {
+    int prev = -1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (c[q].wt == 0.0f) continue;
+        const int band = c[q].idx / SB_BAND;
+        if (band != prev) visit(band);
+        prev = band;
+    }
 }
 
-__global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands, int nsplit) {
-    __shared__ SplatLds img;
+__global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int nbands, float4* rec, int* bins, int nbg,
+                                                     float4* rec4, float* rec1, int* gbins) {
+    __shared__ int cnt[2 * kMaxSBands], cur[2 * kMaxSBands];
+    __shared__ int gcnt[kMaxBands], gcur[kMaxBands];  // the backward's bins (own-pixel bands; tf == T)
     __shared__ WinTab wt;
     const int tid = threadIdx.x;
     wintab_load(a, wt);
+    const int k = blockIdx.x % a.T, b = blockIdx.x / a.T;
+    const int i0 = a.off[k], i1 = a.off[k + 1];
+    const int64_t HWp = (int64_t)a.H * a.W;
+    const int R = splat_rec_per_event(a.W), nb2 = 2 * nbands;
+    // with one flow per event window the backward's (sample, flow window) regions are this block's:
+    // its bins by the band of the event's own pixel are formed here too (else k_iwe_bin, in the backward)
+    const bool gb = a.tf == a.T;
+    for (int j = tid; j < nb2; j += WB_NT) cnt[j] = 0;
+    if (gb)
+        for (int j = tid; j < nbg; j += WB_NT) gcnt[j] = 0;
+    __syncthreads();
+    const float* fl = wt.fl[a.tf == 1 ? 0 : k] + (int64_t)b * 2 * HWp;
+    auto gband = [&](const float4& r0) {
+        const int pix = (int)(r0.y * (float)a.W + r0.z);
+        const int q = pix / GB_BAND;
+        return q < 0 ? 0 : (q >= nbg ? nbg - 1 : q);
+    };
+    // one event: its record halves and the corners of both warps
+    auto warp_event = [&](int i, float4& r0, float4& r1, Corner (&c0)[4], Corner (&c1)[4]) {
+        const EventRef r = event_ref(wt, a.T, b, i);
+        const float4 ev = *reinterpret_cast<const float4*>(r.ev);
+        const float2 pm = *reinterpret_cast<const float2*>(r.pol);
+        const int pix = (int)(ev.y * (float)a.W + ev.z);
+        const float fy = fl[HWp + pix], fx = fl[pix];
+        const float ts = ev.x + (float)k;
+        r0 = make_float4(ts, ev.y, ev.z, pm.x);
+        r1 = make_float4(fy, fx, pm.y, 0.0f);
+        float wy, wx;
+        warp4(ts, ev.y, ev.z, fy, fx, (float)a.T, a.flow_scaling, a.H, a.W, c0, wy, wx);
+        warp4(ts, ev.y, ev.z, fy, fx, 0.0f, a.flow_scaling, a.H, a.W, c1, wy, wx);
+    };
+    // the window's first WB_U * WB_NT events stay in registers between the histogram and the placement
+    // (their loads and flow gathers issued together: one chain of dependent loads per thread); any
+    // further events are loaded again for the placement
+    float4 kr0[WB_U], kr1[WB_U];
+#pragma unroll
+    for (int u = 0; u < WB_U; ++u) {
+        const int i = i0 + tid + u * WB_NT;
+        kr0[u] = kr1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < i1) {
+            const EventRef r = event_ref(wt, a.T, b, i);
+            const float4 ev = *reinterpret_cast<const float4*>(r.ev);
+            const float2 pm = *reinterpret_cast<const float2*>(r.pol);
+            kr0[u] = make_float4(ev.x + (float)k, ev.y, ev.z, pm.x);
+            kr1[u] = make_float4(0.f, 0.f, pm.y, 0.f);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < WB_U; ++u) {
+        const int i = i0 + tid + u * WB_NT;
+        if (i < i1) {
+            const int pix = (int)(kr0[u].y * (float)a.W + kr0[u].z);
+            kr1[u].x = fl[HWp + pix];
+            kr1[u].y = fl[pix];
+        }
+    }
+    auto warps = [&](const float4& r0, const float4& r1, Corner (&c0)[4], Corner (&c1)[4]) {
+        float wy, wx;
+        warp4(r0.x, r0.y, r0.z, r1.x, r1.y, (float)a.T, a.flow_scaling, a.H, a.W, c0, wy, wx);
+        warp4(r0.x, r0.y, r0.z, r1.x, r1.y, 0.0f, a.flow_scaling, a.H, a.W, c1, wy, wx);
+    };
+#pragma unroll
+    for (int u = 0; u < WB_U; ++u) {
+        if (i0 + tid + u * WB_NT >= i1) continue;
+        Corner c0[4], c1[4];
+        warps(kr0[u], kr1[u], c0, c1);
+        corner_bands(c0, [&](int band) { atomicAdd(&cnt[band], 1); });
+        corner_bands(c1, [&](int band) { atomicAdd(&cnt[nbands + band], 1); });
+        if (gb) atomicAdd(&gcnt[gband(kr0[u])], 1);
+    }
+    for (int i = i0 + tid + WB_U * WB_NT; i < i1; i += WB_NT) {
+        float4 r0, r1;
+        Corner c0[4], c1[4];
+        warp_event(i, r0, r1, c0, c1);
+        corner_bands(c0, [&](int band) { atomicAdd(&cnt[band], 1); });
+        corner_bands(c1, [&](int band) { atomicAdd(&cnt[nbands + band], 1); });
+        if (gb) atomicAdd(&gcnt[gband(r0)], 1);
+    }
+    __syncthreads();
+    int* bo = bins + ((int64_t)b * a.T + k) * (nb2 + 1);
+    if (tid < 64) {  // exclusive prefix over (direction, band), 64 at a time
+        int carry = 0;
+        for (int j0 = 0; j0 < nb2; j0 += 64) {
+            const int j = j0 + tid;
+            const int c = j < nb2 ? cnt[j] : 0;
+            int x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
+                if (tid >= o) x += y;
+            }
+            if (j < nb2) {
+                cur[j] = carry + x - c;
+                bo[j] = carry + x - c;
+            }
+            carry += __shfl(x, 63, 64);
+        }
+        if (tid == 0) bo[nb2] = carry;
+    } else if (gb && tid < 128) {  // (wave 1) the same over the own-pixel bands
+        const int l = tid - 64;
+        int* go = gbins + ((int64_t)b * a.tf + k) * (nbg + 1);
+        int carry = 0;
+        for (int j0 = 0; j0 < nbg; j0 += 64) {
+            const int j = j0 + l;
+            const int c = j < nbg ? gcnt[j] : 0;
+            int x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
+                if (l >= o) x += y;
+            }
+            if (j < nbg) {
+                gcur[j] = carry + x - c;
+                go[j] = carry + x - c;
+            }
+            carry += __shfl(x, 63, 64);
+        }
+        if (l == 0) go[nbg] = carry;
+    }
+    __syncthreads();
+    float4* rg = rec + (int64_t)R * 2 * ((int64_t)b * a.M + i0) * 2;  // (two float4 per record)
+    const int64_t gbase = (int64_t)b * a.M + i0;
+    auto gplace = [&](const float4& r0, const float4& r1) {
+        if (!gb) return;
+        const int slot = atomicAdd(&gcur[gband(r0)], 1);
+        rec4[gbase + slot] = r0;
+        rec1[gbase + slot] = r1.z;
+    };
+    auto place = [&](const float4& r0, const float4& r1, const Corner (&c0)[4], const Corner (&c1)[4]) {
+        auto put = [&](int j) {
+            const int slot = atomicAdd(&cur[j], 1);
+            rg[2 * slot] = r0;
+            rg[2 * slot + 1] = r1;
+        };
+        corner_bands(c0, [&](int band) { put(band); });
+        corner_bands(c1, [&](int band) { put(nbands + band); });
+    };
+#pragma unroll
+    for (int u = 0; u < WB_U; ++u) {
+        if (i0 + tid + u * WB_NT >= i1) continue;
+        Corner c0[4], c1[4];
+        warps(kr0[u], kr1[u], c0, c1);
+        place(kr0[u], kr1[u], c0, c1);
+        gplace(kr0[u], kr1[u]);
+    }
+    for (int i = i0 + tid + WB_U * WB_NT; i < i1; i += WB_NT) {
+        float4 r0, r1;
+        Corner c0[4], c1[4];
+        warp_event(i, r0, r1, c0, c1);
+        place(r0, r1, c0, c1);
+        gplace(r0, r1);
+    }
+}
+
+__global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands, const float4* __restrict__ rec,
+                                                        const int* __restrict__ bins) {
+    __shared__ SplatLds img;
+    __shared__ int64_t seg0[SNNFLOW_MAX_WINDOWS];
+    __shared__ int pre[SNNFLOW_MAX_WINDOWS + 1];
+    const int tid = threadIdx.x;
     const int blk = xcd_block();
-    const int split = blk % nsplit, rest = blk / nsplit;
-    const int band = rest % nbands, d = (rest / nbands) % 2, b = rest / (2 * nbands);
+    const int band = blk % nbands, d = (blk / nbands) % 2, b = blk / (2 * nbands);
     const int64_t HWp = (int64_t)a.H * a.W, imgsz = (int64_t)a.B * HWp;
-    const int p0 = band * SPLAT_BAND;
-    const int np = (int)((HWp - p0) < SPLAT_BAND ? (HWp - p0) : SPLAT_BAND);
+    const int p0 = band * SB_BAND;
+    const int np = (int)((HWp - p0) < SB_BAND ? (HWp - p0) : SB_BAND);
+    const int R = splat_rec_per_event(a.W), nb2 = 2 * nbands, j = d * nbands + band;
+    if (tid < 64) {  // the band's segment in every window's region, and their prefix
+        int len = 0;
+        if (tid < a.T) {
+            const int* bo = bins + ((int64_t)b * a.T + tid) * (nb2 + 1);
+            const int s0 = bo[j];
+            len = bo[j + 1] - s0;
+            seg0[tid] = (int64_t)R * 2 * ((int64_t)b * a.M + a.off[tid]) + s0;  // record index of the segment's start
+        }
+        int x = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (tid >= o) x += y;
+        }
+        if (tid < a.T) pre[tid + 1] = x;
+        if (tid == 0) pre[0] = 0;
+    }
     img.zero(tid);
     __syncthreads();
+    const int total = pre[a.T];
     const float tref = d == 0 ? (float)a.T : 0.0f;
-    const int stride = nsplit * SPLAT_NT;
-    for (int i0 = split * SPLAT_NT + tid; i0 < ((SNNFLOW_SPLAT_PROBE & 2) ? 0 : a.M); i0 += SPLAT_U * stride) {
-        float4 ev[SPLAT_U];
-        float2 pm[SPLAT_U];
-        int kk[SPLAT_U];
+    for (int f = tid; f < total; f += SPLAT_NT) {
+        int lo = 0, hi = a.T - 1;  // the window holding flat record f: last k with pre[k] <= f
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pre[mid] <= f) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t ri = (int64_t)seg0[lo] + (f - pre[lo]);
+        const float4 r0 = rec[2 * ri], r1 = rec[2 * ri + 1];
+        const float ts = r0.x, pm0 = r0.w, pm1 = r1.z;
+        const float tsw = d == 0 ? ts : (float)a.T - ts;
+        Corner c[4];
+        float wy, wx;
+        warp4(ts, r0.y, r0.z, r1.x, r1.y, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
 #pragma unroll
-        for (int u = 0; u < SPLAT_U; ++u) {
-            const int i = i0 + u * stride;
-            kk[u] = -1;
-            if (i < a.M) {
-                const EventRef r = event_ref(wt, a.T, b, i);
-                ev[u] = *reinterpret_cast<const float4*>(r.ev);
-                pm[u] = *reinterpret_cast<const float2*>(r.pol);
-                kk[u] = r.k;
+        for (int q = 0; q < 4; ++q) {
+            const float w = c[q].wt;
+            const int li = c[q].idx - p0;
+            if (w == 0.0f || li < 0 || li >= np) continue;
+            const float wts = w * tsw;
+            if (pm0 != 0.0f) {
+                img.add(0, li, w * pm0);
+                img.add(2, li, wts * pm0);
             }
-        }
-        float fy[SPLAT_U], fx[SPLAT_U];
-#pragma unroll
-        for (int u = 0; u < SPLAT_U; ++u) {
-            if (kk[u] < 0) continue;
-            const int pix = (int)(ev[u].y * (float)a.W + ev[u].z);
-            const float* fl = wt.fl[a.tf == 1 ? 0 : kk[u]] + (int64_t)b * 2 * HWp;
-            fy[u] = fl[HWp + pix];
-            fx[u] = fl[pix];
-        }
-#pragma unroll
-        for (int u = 0; u < SPLAT_U; ++u) {
-            if (kk[u] < 0) continue;
-            const float ts = ev[u].x + (float)kk[u], y = ev[u].y, x = ev[u].z;
-            const float pm0 = pm[u].x, pm1 = pm[u].y;
-            const float tsw = d == 0 ? ts : (float)a.T - ts;
-            Corner c[4];
-            float wy, wx;
-            warp4(ts, y, x, fy[u], fx[u], tref, a.flow_scaling, a.H, a.W, c, wy, wx);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float wt = c[q].wt;
-                const int li = c[q].idx - p0;
-                if (wt == 0.0f || li < 0 || li >= np) continue;
-                const float wts = wt * tsw;
-                if (SNNFLOW_SPLAT_PROBE & 1) {
-                    if (wts == 12345.0f) img.add(0, li, wt);  // (keeps the math alive)
-                    continue;
-                }
-                if (pm0 != 0.0f) {
-                    img.add(0, li, wt * pm0);
-                    img.add(2, li, wts * pm0);
-                }
-                if (pm1 != 0.0f) {
-                    img.add(1, li, wt * pm1);
-                    img.add(3, li, wts * pm1);
-                }
+            if (pm1 != 0.0f) {
+                img.add(1, li, w * pm1);
+                img.add(3, li, wts * pm1);
             }
         }
     }
     __syncthreads();
-    float* out = a.images + (int64_t)split * 8 * imgsz + (int64_t)d * 4 * imgsz + (int64_t)b * HWp + p0;
+    float* out = a.images + (int64_t)d * 4 * imgsz + (int64_t)b * HWp + p0;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-        for (int j = tid; j < np; j += SPLAT_NT) out[(int64_t)q * imgsz + j] = img.get(q, j);
+        for (int jj = tid; jj < np; jj += SPLAT_NT) out[(int64_t)q * imgsz + jj] = img.get(q, jj);
 }
 
 __device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
@@ -266,7 +451,7 @@ __host__ __device__ inline int loss_tsplit(int B, int64_t HWp, int tf) {
     return s < 1 ? 1 : (s > tf ? tf : (int)s);
 }
 
-__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit, int nsplit) {
+__global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit) {
     __shared__ float red[NT / 64][LOSS_NV];
     const int blk = xcd_block();
     const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
@@ -305,17 +490,10 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
             const float T = (float)a.T;
 #pragma unroll
             for (int d = 0; d < 2; ++d) {
-                // sum the splat's partial images (fixed order) and keep the total in partial 0
-                float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+                const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
                 float q4[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    float v0 = base[q * img];
-                    for (int sp = 1; sp < nsplit; ++sp) v0 += base[(int64_t)sp * 8 * img + q * img];
-                    q4[q] = v0;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) base[q * img] = q4[q];
+                for (int q = 0; q < 4; ++q) q4[q] = base[q * img];
                 const float cp = q4[0], cn = q4[1], tp = q4[2], tn = q4[3];
                 const float A = (tp / (cp + 1e-9f)) / T;
                 const float Bv = (tn / (cn + 1e-9f)) / T;
@@ -563,70 +741,12 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
     }
 }
 
-// Per event: gather dL/d(images) at the 4 corners of both warps, chain through the
-// bilinear weights to the warped position and the per-event flow, scatter into g_flows.
-// Eight lanes per event, one per (direction d, corner q): the event / flow loads are shared
-// (same addresses), each lane gathers its corner's four image gradients, the corners are summed by
-// lane exchange before the (flow_scaling, dt) factor of their direction, the directions after it,
-// and lane 0 of the group adds to g_flows.  (One thread per event left ~5 waves per CU with a
-// chain of 2 x 16 dependent-address gathers each: latency-bound.)
+// Eight lanes per event in the per-event backward (k_iwe_bwd_band), one per (direction d, corner q): the
+// event / flow loads are shared (same addresses), each lane gathers its corner's four image gradients,
+// the corners are summed by lane exchange before the (flow_scaling, dt) factor of their direction, the
+// directions after it.  (One thread per event left ~5 waves per CU with a chain of 2 x 16
+// dependent-address gathers each: latency-bound.)
 constexpr int kBwdLanes = 8;
-
-__global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
-                                                      float* g_flows) {
-    const int64_t HWp = (int64_t)a.H * a.W;
-    const int64_t n = (int64_t)a.B * a.M;
-    const int64_t img = (int64_t)a.B * HWp;
-    const int sub = threadIdx.x & (kBwdLanes - 1), d = sub >> 2, q = sub & 3;
-    __shared__ WinTab wt;
-    wintab_load(a, wt);
-    // XCD-ordered blocks: a sample's events (and so its image gathers) on one XCD's L2; an event's
-    // eight lanes are consecutive lanes of one wave and leave the loop together
-    for (int64_t t = (int64_t)xcd_block() * NT + threadIdx.x; t < n * kBwdLanes; t += (int64_t)gridDim.x * NT) {
-        const int64_t e = t / kBwdLanes;
-        const int b = (int)(e / a.M), i = (int)(e - (int64_t)b * a.M);
-        const EventRef r = event_ref(wt, a.T, b, i);
-        const float ts = r.ev[0] + (float)r.k, y = r.ev[1], x = r.ev[2];
-        const int pix = (int)(y * (float)a.W + x);
-        const int kf = a.tf == 1 ? 0 : r.k;
-        const float* fl = wt.fl[kf] + (int64_t)b * 2 * HWp;
-        const float fy = fl[HWp + pix], fx = fl[pix];
-        const float pm0 = r.pol[0], pm1 = r.pol[1];
-        const float tref = d == 0 ? (float)a.T : 0.0f;
-        const float tsw = d == 0 ? ts : (float)a.T - ts;
-        Corner c[4];
-        float wy, wx;
-        warp4(ts, y, x, fy, fx, tref, a.flow_scaling, a.H, a.W, c, wy, wx);
-        Corner cq = c[0];
-#pragma unroll
-        for (int k = 1; k < 4; ++k)
-            if (q == k) cq = c[k];
-        float gwy = 0.0f, gwx = 0.0f;
-        if (cq.inb) {
-            const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
-            const int id = cq.idx;
-            const float gwt = (gb[id] * pm0 + gb[img + id] * pm1) +
-                              (gb[2 * img + id] * (tsw * pm0) + gb[3 * img + id] * (tsw * pm1));
-            // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
-            const float gay = gwt * cq.ax, gax = gwt * cq.ay;
-            gwy = -(gay * relu_tie(1.0f - fabsf(cq.dy))) * sgnf(cq.dy);
-            gwx = -(gax * relu_tie(1.0f - fabsf(cq.dx))) * sgnf(cq.dx);
-        }
-        gwy += __shfl_xor(gwy, 1, 64);
-        gwx += __shfl_xor(gwx, 1, 64);
-        gwy += __shfl_xor(gwy, 2, 64);
-        gwx += __shfl_xor(gwx, 2, 64);
-        const float dt = tref - ts;
-        float gfy = (gwy * a.flow_scaling) * dt, gfx = (gwx * a.flow_scaling) * dt;
-        gfy += __shfl_xor(gfy, 4, 64);
-        gfx += __shfl_xor(gfx, 4, 64);
-        if (sub == 0) {
-            float* gf = g_flows + (((int64_t)b * a.tf + kf) * 2) * HWp;
-            if (gfx != 0.0f) atomicAdd(gf + pix, gfx);
-            if (gfy != 0.0f) atomicAdd(gf + HWp + pix, gfy);
-        }
-    }
-}
 
 // The events of every (sample, flow window) binned by the pixel band (GB_BAND pixels) of the event's own
 // pixel -- the pixel its flow gradient lands in.  The binning depends on the event lists only.  Each
@@ -637,7 +757,6 @@ __global__ __launch_bounds__(NT) void k_iwe_bwd_event(snnflow_iwe_loss_args a, c
 // start in that region (the last entry: the window's count).  The order inside a band follows the LDS
 // atomics (it does not matter: the consumer sums in exact fixed point).  One block per (sample, flow
 // window): a band histogram, a wave-0 prefix scan, the placement.
-constexpr int GB_NT = 256, BIN_NT = 1024, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
 
 __device__ inline void flow_window_events(const snnflow_iwe_loss_args& a, int t, int& i0, int& i1) {
     i0 = a.tf == 1 ? 0 : a.off[t];
@@ -696,7 +815,7 @@ __global__ __launch_bounds__(BIN_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int
 
 // The loss backward's per-event part, per (sample, flow window, band of GB_BAND pixels): each event of
 // the band's bin gathers dL/d(images) at the 4 corners of both warps and chains them through the
-// bilinear weights to its flow (eight lanes per event as in k_iwe_bwd_event), and the band's
+// bilinear weights to its flow (eight lanes per event, kBwdLanes), and the band's
 // per-pixel sums of those flow gradients are formed in LDS in exact two-word fixed point (SplatLdsX's
 // split: integer adds, so the sums do not depend on the order of the events) and added to g_flows once
 // per touched pixel.  No block reads an event outside its bin.
@@ -838,7 +957,7 @@ __global__ void k_iwe_interpolate(const int32_t* __restrict__ idx, const float* 
 
 // Backward of get_interpolation (utils/iwe.py:37-65) w.r.t. the per-event flow: the gradients
 // of the 4 corner weights [B][4][M] -> dL/dflow_ev [B][M][2] (y, x).  weights = prod(max(0,
-// 1 - |w - c|), -1) * mask, w = pos + ((tref - ts) * f) * s: the same chain as k_iwe_bwd_event.
+// 1 - |w - c|), -1) * mask, w = pos + ((tref - ts) * f) * s: the same chain as k_iwe_bwd_band.
 __global__ void k_iwe_corners_bwd(const float* __restrict__ events, const float* __restrict__ flow_ev, int B, int M,
                                   float tref, int H, int W, float s, const float* __restrict__ g_w,
                                   float* __restrict__ g_flow_ev) {
@@ -902,12 +1021,8 @@ int check_loss_args(const snnflow_iwe_loss_args* a) {
 
 extern "C" {
 
-int snnflow_iwe_scratch_floats(int B, int H, int W) { return SPLAT_SPLIT * 8 * B * H * W; }
-
-int snnflow_iwe_bwd_scratch_ints(int B, int M, int H, int W, int tf) {
-    const int64_t HWp = (int64_t)H * W;
-    const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
-    return (int)((int64_t)B * M * 5 + (int64_t)B * tf * (nbands + 1));  // rec4, rec1, bins
+int64_t snnflow_iwe_scratch_floats(int B, int M, int T, int tf, int H, int W) {
+    return LossScratch(B, M, T, tf, H, W).total;
 }
 
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
@@ -919,18 +1034,24 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     if (int rc = check_loss_args(a)) return rc;
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
-    const int nbands = (int)((HWp + SPLAT_BAND - 1) / SPLAT_BAND);
-    const int nsplit = splat_nsplit(a->B, nbands);
-    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands * nsplit), dim3(SPLAT_NT), 0, s, *a, nbands, nsplit);
+    const int nbands = splat_bands(HWp), nbg = (int)((HWp + GB_BAND - 1) / GB_BAND);
+    if (nbands > kMaxSBands || nbg > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: H * W above 2^21 pixels");
+    if ((reinterpret_cast<uintptr_t>(a->images) & 15) != 0) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss: images scratch not 16-B aligned");
+    const LossScratch ls(a->B, a->M, a->T, a->tf, a->H, a->W);
+    float4* rec = reinterpret_cast<float4*>(a->images + ls.rec);
+    int* bins = reinterpret_cast<int*>(a->images + ls.bins);
+    hipLaunchKernelGGL(k_iwe_wbin, dim3(a->B * a->T), dim3(WB_NT), 0, s, *a, nbands, rec, bins, nbg,
+                       reinterpret_cast<float4*>(a->images + ls.rec4), a->images + ls.rec1,
+                       reinterpret_cast<int*>(a->images + ls.gbins));
+    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands), dim3(SPLAT_NT), 0, s, *a, nbands, rec, bins);
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
-    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit, nsplit);
+    hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit);
     hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, tsplit * chunks);
     SNN_CHECK_LAUNCH();
     return 0;
 }
 
-int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows, int* bin,
-                         void* stream) {
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows, void* stream) {
     if (int rc = check_loss_args(a)) return rc;
     if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
     const hipStream_t s = (hipStream_t)stream;
@@ -938,22 +1059,18 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
     hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
                        chunks, tsplit);
-    if (a->M > 0) {
-        if (bin) {  // events binned by pixel band, then per band: event gradients + exact per-pixel sums
-            const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
-            if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
-            if ((reinterpret_cast<uintptr_t>(bin) & 15) != 0) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: bin scratch not 16-B aligned");
-            const int64_t n = (int64_t)a->B * a->M;
-            float4* rec4 = reinterpret_cast<float4*>(bin);  // 16-B aligned: the caller's allocation
-            float* rec1 = reinterpret_cast<float*>(bin) + 4 * n;
-            int* bins = bin + 5 * n;
+    if (a->M > 0) {  // the events binned by own-pixel band, then per band: event gradients + exact per-pixel sums
+        const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
+        if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
+        const LossScratch ls(a->B, a->M, a->T, a->tf, a->H, a->W);
+        float4* rec4 = reinterpret_cast<float4*>(a->images + ls.rec4);
+        float* rec1 = a->images + ls.rec1;
+        int* bins = reinterpret_cast<int*>(a->images + ls.gbins);
+        // (tf == T: the forward's k_iwe_wbin formed these bins)
+        if (a->tf != a->T)
             hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
-            hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), 0, s, *a, gimg, g_flows, rec4, rec1,
-                               bins, nbands);
-        } else {
-            hipLaunchKernelGGL(k_iwe_bwd_event, dim3(grid_for((int64_t)a->B * a->M * kBwdLanes, NT, 65536)), dim3(NT), 0, s,
-                               *a, gimg, g_flows);
-        }
+        hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), 0, s, *a, gimg, g_flows, rec4, rec1,
+                           bins, nbands);
     }
     SNN_CHECK_LAUNCH();
     return 0;

@@ -66,7 +66,7 @@ class EventWarpingFn(torch.autograd.Function):
             _lib.require_device(f, "flow")
         B, H, W = evs[0].shape[0], meta["H"], meta["W"]
         scr = scr.get(B, H, W, len(flows_c), dev)
-        images = torch.empty(lib.snnflow_iwe_scratch_floats(B, H, W), device=dev)
+        images = torch.empty(lib.snnflow_iwe_scratch_floats(B, meta["off"][-1], meta["T"], len(flows_c), H, W), device=dev)
         persample = torch.empty(2 * B * 4, device=dev)
         smooth = torch.empty(8, device=dev)
         loss = torch.empty((), device=dev)
@@ -88,12 +88,9 @@ class EventWarpingFn(torch.autograd.Function):
         B, H, W = flows_c[0].shape[0], ctx.meta["H"], ctx.meta["W"]
         gimg = torch.empty(8 * B * H * W, device=dev)
         g_flows = torch.empty(B, len(flows_c), 2, H, W, device=dev)
-        # the events binned by pixel band; per band the flow gradients summed per pixel in fixed point
-        # (bit-reproducible g_flows)
-        nbin = lib.snnflow_iwe_bwd_scratch_ints(B, a.M, H, W, len(flows_c))
-        bins = torch.empty(max(nbin, 1), dtype=torch.int32, device=dev)
-        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), ptr(bins),
-                  s)
+        # (the events binned by pixel band in the images scratch; per band the flow gradients summed per
+        # pixel in fixed point: bit-reproducible g_flows)
+        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), s)
         return (None, None, None, *g_flows.unbind(1))
 
 
