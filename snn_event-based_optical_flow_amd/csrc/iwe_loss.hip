@@ -188,45 +188,18 @@ struct LossScratch {
     }
 };
 
-// The r-th distinct band (ascending) that the non-zero corners of one warp touch, -1 past the last;
-// corners are idx-ordered (c0 <= c1 <= c2 <= c3 for in-image corners).
-__device__ inline int nth_band(const Corner (&c)[4], int r) {
-    int prev = -1, n = 0;
+// The bands (ascending, distinct) that the non-zero corners of one warp touch, as a count and the
+// first band; corners are idx-ordered (c0 <= c1 <= c2 <= c3 for in-image corners).
+template <typename F>
+__device__ inline void corner_bands(const Corner (&c)[4], F&& visit) {
+    int prev = -1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (c[q].wt == 0.0f) continue;
         const int band = c[q].idx / SB_BAND;
-        if (band != prev) {
-            if (n == r) return band;
-            ++n;
-        }
+        if (band != prev) visit(band);
         prev = band;
     }
-    return -1;
-}
-
-// Wave-aggregated LDS counter: every active lane adds one to ctr[key]; the lanes of one key take
-// consecutive values in lane order, the wave's first lane of each key making one atomic for all of them
-// (the events of a wave fall into few bands: one LDS atomic per (wave, band) instead of one per lane,
-// each of which serialised on the band's word).  Returns the lane's old value (ret), else 0.
-// Wave-uniform call (all lanes, active or not).
-__device__ inline int wave_count_add(int* ctr, int key, bool active) {
-    const int lane = threadIdx.x & 63;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    unsigned long long pending = __ballot(active);
-    int res = 0;
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int v = __shfl(key, leader, 64);
-        const bool mine = active && key == v;
-        const unsigned long long m = __ballot(mine);
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&ctr[v], __popcll(m));
-        base = __shfl(base, leader, 64);
-        if (mine) res = base + __popcll(m & below);
-        pending &= ~m;
-    }
-    return res;
 }
 
 __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int nbands, float4* rec, int* bins, int nbg,
@@ -253,60 +226,66 @@ __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int
         const int q = pix / GB_BAND;
         return q < 0 ? 0 : (q >= nbg ? nbg - 1 : q);
     };
-    // one event's record halves (ts + k, y, x, pol 0 | flow y, flow x, pol 1, 0)
-    auto load_event = [&](int i, float4& r0, float4& r1) {
+    // one event: its record halves and the corners of both warps
+    auto warp_event = [&](int i, float4& r0, float4& r1, Corner (&c0)[4], Corner (&c1)[4]) {
         const EventRef r = event_ref(wt, a.T, b, i);
         const float4 ev = *reinterpret_cast<const float4*>(r.ev);
         const float2 pm = *reinterpret_cast<const float2*>(r.pol);
-        r0 = make_float4(ev.x + (float)k, ev.y, ev.z, pm.x);
-        r1 = make_float4(0.f, 0.f, pm.y, 0.f);
+        const int pix = (int)(ev.y * (float)a.W + ev.z);
+        const float fy = fl[HWp + pix], fx = fl[pix];
+        const float ts = ev.x + (float)k;
+        r0 = make_float4(ts, ev.y, ev.z, pm.x);
+        r1 = make_float4(fy, fx, pm.y, 0.0f);
+        float wy, wx;
+        warp4(ts, ev.y, ev.z, fy, fx, (float)a.T, a.flow_scaling, a.H, a.W, c0, wy, wx);
+        warp4(ts, ev.y, ev.z, fy, fx, 0.0f, a.flow_scaling, a.H, a.W, c1, wy, wx);
     };
-    auto gather_flow = [&](const float4& r0, float4& r1) {
-        const int pix = (int)(r0.y * (float)a.W + r0.z);
-        r1.x = fl[HWp + pix];
-        r1.y = fl[pix];
-    };
+    // the window's first WB_U * WB_NT events stay in registers between the histogram and the placement
+    // (their loads and flow gathers issued together: one chain of dependent loads per thread); any
+    // further events are loaded again for the placement
+    float4 kr0[WB_U], kr1[WB_U];
+#pragma unroll
+    for (int u = 0; u < WB_U; ++u) {
+        const int i = i0 + tid + u * WB_NT;
+        kr0[u] = kr1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < i1) {
+            const EventRef r = event_ref(wt, a.T, b, i);
+            const float4 ev = *reinterpret_cast<const float4*>(r.ev);
+            const float2 pm = *reinterpret_cast<const float2*>(r.pol);
+            kr0[u] = make_float4(ev.x + (float)k, ev.y, ev.z, pm.x);
+            kr1[u] = make_float4(0.f, 0.f, pm.y, 0.f);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < WB_U; ++u) {
+        const int i = i0 + tid + u * WB_NT;
+        if (i < i1) {
+            const int pix = (int)(kr0[u].y * (float)a.W + kr0[u].z);
+            kr1[u].x = fl[HWp + pix];
+            kr1[u].y = fl[pix];
+        }
+    }
     auto warps = [&](const float4& r0, const float4& r1, Corner (&c0)[4], Corner (&c1)[4]) {
         float wy, wx;
         warp4(r0.x, r0.y, r0.z, r1.x, r1.y, (float)a.T, a.flow_scaling, a.H, a.W, c0, wy, wx);
         warp4(r0.x, r0.y, r0.z, r1.x, r1.y, 0.0f, a.flow_scaling, a.H, a.W, c1, wy, wx);
     };
-    // the window's first WB_U * WB_NT events stay in registers between the histogram and the placement
-    // (their loads and flow gathers issued together: one chain of dependent loads per thread); any
-    // further events are loaded again for the placement.  Loops are wave-uniform (the aggregated
-    // counters need every lane).
-    float4 kr0[WB_U], kr1[WB_U];
 #pragma unroll
     for (int u = 0; u < WB_U; ++u) {
-        kr0[u] = kr1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (i0 + tid + u * WB_NT < i1) load_event(i0 + tid + u * WB_NT, kr0[u], kr1[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < WB_U; ++u)
-        if (i0 + tid + u * WB_NT < i1) gather_flow(kr0[u], kr1[u]);
-    const int iw = i0 + (tid & ~63);  // this wave's first event of a pass
-    auto count = [&](bool on, const float4& r0, const float4& r1) {
+        if (i0 + tid + u * WB_NT >= i1) continue;
         Corner c0[4], c1[4];
-        if (on) warps(r0, r1, c0, c1);
-        for (int r = 0; r < R; ++r) {
-            const int b0 = on ? nth_band(c0, r) : -1, b1 = on ? nth_band(c1, r) : -1;
-            if (!__ballot(b0 >= 0 || b1 >= 0)) break;
-            wave_count_add(cnt, b0, b0 >= 0);
-            wave_count_add(cnt, nbands + b1, b1 >= 0);
-        }
-        if (gb) wave_count_add(gcnt, on ? gband(r0) : 0, on);
-    };
-#pragma unroll
-    for (int u = 0; u < WB_U; ++u)
-        if (iw + u * WB_NT < i1) count(i0 + tid + u * WB_NT < i1, kr0[u], kr1[u]);
-    for (int base = i0 + WB_U * WB_NT; base + (tid & ~63) < i1; base += WB_NT) {
-        const int i = base + tid;
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-        if (i < i1) {
-            load_event(i, r0, r1);
-            gather_flow(r0, r1);
-        }
-        count(i < i1, r0, r1);
+        warps(kr0[u], kr1[u], c0, c1);
+        corner_bands(c0, [&](int band) { atomicAdd(&cnt[band], 1); });
+        corner_bands(c1, [&](int band) { atomicAdd(&cnt[nbands + band], 1); });
+        if (gb) atomicAdd(&gcnt[gband(kr0[u])], 1);
+    }
+    for (int i = i0 + tid + WB_U * WB_NT; i < i1; i += WB_NT) {
+        float4 r0, r1;
+        Corner c0[4], c1[4];
+        warp_event(i, r0, r1, c0, c1);
+        corner_bands(c0, [&](int band) { atomicAdd(&cnt[band], 1); });
+        corner_bands(c1, [&](int band) { atomicAdd(&cnt[nbands + band], 1); });
+        if (gb) atomicAdd(&gcnt[gband(r0)], 1);
     }
     __syncthreads();
     int* bo = bins + ((int64_t)b * a.T + k) * (nb2 + 1);
@@ -352,42 +331,35 @@ __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int
     __syncthreads();
     float4* rg = rec + (int64_t)R * 2 * ((int64_t)b * a.M + i0) * 2;  // (two float4 per record)
     const int64_t gbase = (int64_t)b * a.M + i0;
-    auto place = [&](bool on, const float4& r0, const float4& r1) {
-        Corner c0[4], c1[4];
-        if (on) warps(r0, r1, c0, c1);
-        for (int r = 0; r < R; ++r) {
-            const int b0 = on ? nth_band(c0, r) : -1, b1 = on ? nth_band(c1, r) : -1;
-            if (!__ballot(b0 >= 0 || b1 >= 0)) break;
-            const int s0 = wave_count_add(cur, b0, b0 >= 0);
-            const int s1 = wave_count_add(cur, nbands + b1, b1 >= 0);
-            if (b0 >= 0) {
-                rg[2 * s0] = r0;
-                rg[2 * s0 + 1] = r1;
-            }
-            if (b1 >= 0) {
-                rg[2 * s1] = r0;
-                rg[2 * s1 + 1] = r1;
-            }
-        }
-        if (gb) {
-            const int sg = wave_count_add(gcur, on ? gband(r0) : 0, on);
-            if (on) {
-                rec4[gbase + sg] = r0;
-                rec1[gbase + sg] = r1.z;
-            }
-        }
+    auto gplace = [&](const float4& r0, const float4& r1) {
+        if (!gb) return;
+        const int slot = atomicAdd(&gcur[gband(r0)], 1);
+        rec4[gbase + slot] = r0;
+        rec1[gbase + slot] = r1.z;
+    };
+    auto place = [&](const float4& r0, const float4& r1, const Corner (&c0)[4], const Corner (&c1)[4]) {
+        auto put = [&](int j) {
+            const int slot = atomicAdd(&cur[j], 1);
+            rg[2 * slot] = r0;
+            rg[2 * slot + 1] = r1;
+        };
+        corner_bands(c0, [&](int band) { put(band); });
+        corner_bands(c1, [&](int band) { put(nbands + band); });
     };
 #pragma unroll
-    for (int u = 0; u < WB_U; ++u)
-        if (iw + u * WB_NT < i1) place(i0 + tid + u * WB_NT < i1, kr0[u], kr1[u]);
-    for (int base = i0 + WB_U * WB_NT; base + (tid & ~63) < i1; base += WB_NT) {
-        const int i = base + tid;
-        float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
-        if (i < i1) {
-            load_event(i, r0, r1);
-            gather_flow(r0, r1);
-        }
-        place(i < i1, r0, r1);
+    for (int u = 0; u < WB_U; ++u) {
+        if (i0 + tid + u * WB_NT >= i1) continue;
+        Corner c0[4], c1[4];
+        warps(kr0[u], kr1[u], c0, c1);
+        place(kr0[u], kr1[u], c0, c1);
+        gplace(kr0[u], kr1[u]);
+    }
+    for (int i = i0 + tid + WB_U * WB_NT; i < i1; i += WB_NT) {
+        float4 r0, r1;
+        Corner c0[4], c1[4];
+        warp_event(i, r0, r1, c0, c1);
+        place(r0, r1, c0, c1);
+        gplace(r0, r1);
     }
 }
 
