@@ -873,42 +873,23 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
     const int sub = tid & (kBwdLanes - 1), d = sub >> 2, qc = sub & 3;
     const float tref = d == 0 ? (float)a.T : 0.0f;
     const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
-    // the window's P parts (regions at their first event): this band's bins of all parts as one flat
-    // range of slots (every round fills all 8-lane groups); every lane runs every round (the lane
-    // exchanges need the whole 8-lane group): a slot past the bins contributes zeros
-    int64_t sbase[WB_PMAX];  // record index of flat slot 0 of each part's bin, minus that part's flat start
-    int fend[WB_PMAX];       // flat end of each part's bin
-    int ftot = 0;
-#pragma unroll
-    for (int pt = 0; pt < WB_PMAX; ++pt) {
-        sbase[pt] = 0;
-        fend[pt] = ftot;
-        if (pt < P) {
-            int ps, pe;
-            part_range(i0, i1, P, pt, ps, pe);
-            const int* bo = bins + (((int64_t)b * a.tf + t) * P + pt) * (nbands + 1);
-            const int e0 = bo[band], e1 = bo[band + 1];
-            sbase[pt] = (int64_t)b * a.M + ps + e0 - ftot;
-            ftot += e1 - e0;
-            fend[pt] = ftot;
-        }
-    }
-    for (int s0 = 0; s0 < ftot; s0 += GB_NT / kBwdLanes) {
-        const int fs = s0 + tid / kBwdLanes;
-        const bool on = fs < ftot;
+    // the window's P parts (regions at their first event), each part's bin of this band in turn; every
+    // lane runs every round (the lane exchanges need the whole 8-lane group): a slot past the bin
+    // contributes zeros
+    for (int pt = 0; pt < P; ++pt) {
+    int ps, pe;
+    part_range(i0, i1, P, pt, ps, pe);
+    const int* bo = bins + (((int64_t)b * a.tf + t) * P + pt) * (nbands + 1);
+    const int e0 = bo[band], e1 = bo[band + 1];
+    const int64_t base = (int64_t)b * a.M + ps;
+    for (int s0 = e0; s0 < e1; s0 += GB_NT / kBwdLanes) {
+        const int slot = s0 + tid / kBwdLanes;
+        const bool on = slot < e1;
         float gwy = 0.0f, gwx = 0.0f, dt = 0.0f;
         int q = -1;
         if (on) {
-            int pt = 0;
-#pragma unroll
-            for (int u = 0; u < WB_PMAX - 1; ++u)
-                if (fs >= fend[u]) pt = u + 1;
-            int64_t ri = sbase[0] + fs;
-#pragma unroll
-            for (int u = 1; u < WB_PMAX; ++u)
-                if (pt == u) ri = sbase[u] + fs;
-            const float4 ev = rec4[ri];
-            const float pm1 = rec1[ri];
+            const float4 ev = rec4[base + slot];
+            const float pm1 = rec1[base + slot];
             const float ts = ev.x, y = ev.y, x = ev.z, pm0 = ev.w;
             const int pix = (int)(y * (float)a.W + x);
             q = pix - p0;
@@ -950,6 +931,7 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
                 if (l != 0) atomicAdd(&acc.lo[sub][q], (unsigned long long)l);
             }
         }
+    }
     }
     __syncthreads();
 #pragma unroll
