@@ -105,15 +105,14 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 }
 
 // IWE splat with LDS-privatised images over events binned by the band of their warped corners.
-// k_iwe_wbin, one block per (sample b, event window k, part p of wbin_parts: a contiguous share of the
-// window's events, so that the grid fills the chip): gathers every event's flow at its pixel,
+// k_iwe_wbin, one block per (sample b, event window k): gathers every event's flow at its pixel,
 // warps it to both reference times (warp4: tref = T for direction 0, 0 for direction 1) and files one
 // record per (event, direction, band of SB_BAND pixels touched by a corner of non-zero weight) --
 // rec = (ts + k, y, x, pol mask 0 | flow y, flow x, pol mask 1, 0), 32 B -- into the (b, k) region of
 // the record scratch, direction-major and band by band (a band histogram in LDS, a wave-0 prefix scan,
-// the placement; bins [B][T][parts][2 nbands + 1]: each (direction, band)'s start in the part's region).
+// the placement; bins [B][T][2 nbands + 1]: each (direction, band)'s start in the region).
 // k_iwe_splat, one block per (sample, direction, band): owns the four images (cnt+, cnt-, ts+, ts-) of
-// its band in LDS, reads the band's records of the T windows' parts (contiguous, no rescan of the event
+// its band in LDS, reads the band's records of the T windows (contiguous, no rescan of the event
 // lists: every record is read once), re-warps them (the same warp4 on the same inputs: the same
 // corners and weights) and adds the corners inside the band, then writes the band once (no memset, no
 // global atomics).  images layout: [dir 2][img 4][B][HW].
@@ -131,7 +130,7 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 #define SNNFLOW_SPLAT_FIXED 1
 #endif
 constexpr bool kSplatFixed = SNNFLOW_SPLAT_FIXED != 0;
-constexpr int SPLAT_NT = 1024, SB_BAND = 1024, WB_NT = 256, WB_U = 2, WB_PMAX = 8, kMaxSBands = 2048;  // H W <= 2^21 pixels
+constexpr int SPLAT_NT = 1024, SB_BAND = 1024, WB_NT = 1024, WB_U = 2, kMaxSBands = 2048;  // H W <= 2^21 pixels
 // the loss backward's bins (k_iwe_bin / k_iwe_wbin, k_iwe_bwd_band): bands of GB_BAND pixels
 constexpr int GB_NT = 256, BIN_NT = 1024, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
 
@@ -166,17 +165,6 @@ typedef std::conditional_t<kSplatFixed, SplatLdsX, SplatLdsF> SplatLds;
 // (y1 = floor(wy + 1) may exceed floor(wy) + 1 by one under rounding, likewise x1).
 __host__ __device__ inline int splat_rec_per_event(int W) { return (2 * W + 2) / SB_BAND + 2; }
 __host__ __device__ inline int splat_bands(int64_t HWp) { return (int)((HWp + SB_BAND - 1) / SB_BAND); }
-// Blocks (parts) per (sample, event window) of the binning: enough for one per CU, at most WB_PMAX.
-__host__ __device__ inline int wbin_parts(int B, int T) {
-    const int n = B * T, p = (256 + n - 1) / n;
-    return p < 1 ? 1 : (p > WB_PMAX ? WB_PMAX : p);
-}
-// Part p of P of the events [i0, i1): [s, e), contiguous, in order.
-__host__ __device__ inline void part_range(int i0, int i1, int P, int p, int& s, int& e) {
-    const int n = i1 - i0, ch = (n + P - 1) / P;
-    s = i0 + (p * ch < n ? p * ch : n);
-    e = i0 + ((p + 1) * ch < n ? (p + 1) * ch : n);
-}
 
 // The record scratch after the images: [B M R 2] records of 32 B ((b, k) region at R 2 (b M + off[k]))
 // and the bin table [B][T][2 nbands + 1] ints.
@@ -193,10 +181,10 @@ struct LossScratch {
         auto up4 = [](int64_t x) { return (x + 3) / 4 * 4; };
         rec = splat_img_floats(B, HWp);
         bins = rec + splat_rec_floats(B, M, W);
-        rec4 = up4(bins + (int64_t)B * T * WB_PMAX * (2 * ((HWp + SB_BAND - 1) / SB_BAND) + 1));
+        rec4 = up4(bins + (int64_t)B * T * (2 * ((HWp + SB_BAND - 1) / SB_BAND) + 1));
         rec1 = rec4 + 4 * (int64_t)B * M;
         gbins = rec1 + (int64_t)B * M;
-        total = gbins + (int64_t)B * tf * WB_PMAX * ((HWp + GB_BAND - 1) / GB_BAND + 1);
+        total = gbins + (int64_t)B * tf * ((HWp + GB_BAND - 1) / GB_BAND + 1);
     }
 };
 
@@ -215,20 +203,18 @@ __device__ inline void corner_bands(const Corner (&c)[4], F&& visit) {
 }
 
 __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int nbands, float4* rec, int* bins, int nbg,
-                                                     float4* rec4, float* rec1, int* gbins, int P) {
+                                                     float4* rec4, float* rec1, int* gbins) {
     __shared__ int cnt[2 * kMaxSBands], cur[2 * kMaxSBands];
     __shared__ int gcnt[kMaxBands], gcur[kMaxBands];  // the backward's bins (own-pixel bands; tf == T)
     __shared__ WinTab wt;
     const int tid = threadIdx.x;
     wintab_load(a, wt);
-    const int pt = blockIdx.x % P, k = (blockIdx.x / P) % a.T, b = blockIdx.x / (P * a.T);
-    int i0, i1;  // this part's events; its record regions start at event i0
-    part_range(a.off[k], a.off[k + 1], P, pt, i0, i1);
+    const int k = blockIdx.x % a.T, b = blockIdx.x / a.T;
+    const int i0 = a.off[k], i1 = a.off[k + 1];
     const int64_t HWp = (int64_t)a.H * a.W;
     const int R = splat_rec_per_event(a.W), nb2 = 2 * nbands;
-    // with one flow per event window the backward's (sample, flow window) regions are this window's:
-    // its bins by the band of the event's own pixel are formed here too, per part (else k_iwe_bin, in
-    // the backward, one part)
+    // with one flow per event window the backward's (sample, flow window) regions are this block's:
+    // its bins by the band of the event's own pixel are formed here too (else k_iwe_bin, in the backward)
     const bool gb = a.tf == a.T;
     for (int j = tid; j < nb2; j += WB_NT) cnt[j] = 0;
     if (gb)
@@ -302,7 +288,7 @@ __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int
         if (gb) atomicAdd(&gcnt[gband(r0)], 1);
     }
     __syncthreads();
-    int* bo = bins + (((int64_t)b * a.T + k) * P + pt) * (nb2 + 1);
+    int* bo = bins + ((int64_t)b * a.T + k) * (nb2 + 1);
     if (tid < 64) {  // exclusive prefix over (direction, band), 64 at a time
         int carry = 0;
         for (int j0 = 0; j0 < nb2; j0 += 64) {
@@ -323,7 +309,7 @@ __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int
         if (tid == 0) bo[nb2] = carry;
     } else if (gb && tid < 128) {  // (wave 1) the same over the own-pixel bands
         const int l = tid - 64;
-        int* go = gbins + (((int64_t)b * a.tf + k) * P + pt) * (nbg + 1);
+        int* go = gbins + ((int64_t)b * a.tf + k) * (nbg + 1);
         int carry = 0;
         for (int j0 = 0; j0 < nbg; j0 += 64) {
             const int j = j0 + l;
@@ -378,48 +364,40 @@ __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int
 }
 
 __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands, const float4* __restrict__ rec,
-                                                        const int* __restrict__ bins, int P) {
+                                                        const int* __restrict__ bins) {
     __shared__ SplatLds img;
-    __shared__ int64_t seg0[SNNFLOW_MAX_WINDOWS * WB_PMAX];
-    __shared__ int pre[SNNFLOW_MAX_WINDOWS * WB_PMAX + 1];
+    __shared__ int64_t seg0[SNNFLOW_MAX_WINDOWS];
+    __shared__ int pre[SNNFLOW_MAX_WINDOWS + 1];
     const int tid = threadIdx.x;
     const int blk = xcd_block();
     const int band = blk % nbands, d = (blk / nbands) % 2, b = blk / (2 * nbands);
     const int64_t HWp = (int64_t)a.H * a.W, imgsz = (int64_t)a.B * HWp;
     const int p0 = band * SB_BAND;
     const int np = (int)((HWp - p0) < SB_BAND ? (HWp - p0) : SB_BAND);
-    const int R = splat_rec_per_event(a.W), nb2 = 2 * nbands, j = d * nbands + band, nseg = a.T * P;
-    if (tid < 64) {  // the band's segment in every (window, part) region, and their prefix
-        int carry = 0;
-        for (int q0 = 0; q0 < nseg; q0 += 64) {
-            const int q = q0 + tid;
-            int len = 0;
-            if (q < nseg) {
-                const int k = q / P, pt = q - k * P;
-                int s0, e0;
-                part_range(a.off[k], a.off[k + 1], P, pt, s0, e0);
-                const int* bo = bins + ((int64_t)b * a.T * P + q) * (nb2 + 1);
-                const int st = bo[j];
-                len = bo[j + 1] - st;
-                seg0[q] = (int64_t)R * 2 * ((int64_t)b * a.M + s0) + st;  // record index of the segment's start
-            }
-            int x = len;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int y = __shfl_up(x, o, 64);
-                if (tid >= o) x += y;
-            }
-            if (q < nseg) pre[q + 1] = carry + x;
-            carry += __shfl(x, 63, 64);
+    const int R = splat_rec_per_event(a.W), nb2 = 2 * nbands, j = d * nbands + band;
+    if (tid < 64) {  // the band's segment in every window's region, and their prefix
+        int len = 0;
+        if (tid < a.T) {
+            const int* bo = bins + ((int64_t)b * a.T + tid) * (nb2 + 1);
+            const int s0 = bo[j];
+            len = bo[j + 1] - s0;
+            seg0[tid] = (int64_t)R * 2 * ((int64_t)b * a.M + a.off[tid]) + s0;  // record index of the segment's start
         }
+        int x = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (tid >= o) x += y;
+        }
+        if (tid < a.T) pre[tid + 1] = x;
         if (tid == 0) pre[0] = 0;
     }
     img.zero(tid);
     __syncthreads();
-    const int total = pre[nseg];
+    const int total = pre[a.T];
     const float tref = d == 0 ? (float)a.T : 0.0f;
     for (int f = tid; f < total; f += SPLAT_NT) {
-        int lo = 0, hi = nseg - 1;  // the segment holding flat record f: last q with pre[q] <= f
+        int lo = 0, hi = a.T - 1;  // the window holding flat record f: last k with pre[k] <= f
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
             if (pre[mid] <= f) lo = mid;
@@ -848,7 +826,7 @@ struct GevLds {
 __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
                                                         float* g_flows, const float4* __restrict__ rec4,
                                                         const float* __restrict__ rec1, const int* __restrict__ bins,
-                                                        int nbands, int P) {
+                                                        int nbands) {
     __shared__ GevLds acc;
     const int tid = threadIdx.x;
     const int blk = xcd_block();  // a sample's windows and bands on one XCD: its flows / image gradients in one L2
@@ -856,8 +834,11 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p0 = band * GB_BAND;
     const int np = (int)((HWp - p0) < GB_BAND ? (HWp - p0) : GB_BAND);
+    const int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
     int i0, i1;
     flow_window_events(a, t, i0, i1);
+    const int e0 = bo[band], e1 = bo[band + 1];
+    const int64_t base = (int64_t)b * a.M + i0;
     for (int j = tid; j < 2 * GB_BAND; j += GB_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
     // the band's current g_flows values (the pixel backward's), read ahead of the event loop
     float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
@@ -873,15 +854,8 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
     const int sub = tid & (kBwdLanes - 1), d = sub >> 2, qc = sub & 3;
     const float tref = d == 0 ? (float)a.T : 0.0f;
     const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
-    // the window's P parts (regions at their first event), each part's bin of this band in turn; every
-    // lane runs every round (the lane exchanges need the whole 8-lane group): a slot past the bin
+    // every lane runs every round (the lane exchanges need the whole 8-lane group): a slot past the bin
     // contributes zeros
-    for (int pt = 0; pt < P; ++pt) {
-    int ps, pe;
-    part_range(i0, i1, P, pt, ps, pe);
-    const int* bo = bins + (((int64_t)b * a.tf + t) * P + pt) * (nbands + 1);
-    const int e0 = bo[band], e1 = bo[band + 1];
-    const int64_t base = (int64_t)b * a.M + ps;
     for (int s0 = e0; s0 < e1; s0 += GB_NT / kBwdLanes) {
         const int slot = s0 + tid / kBwdLanes;
         const bool on = slot < e1;
@@ -931,7 +905,6 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
                 if (l != 0) atomicAdd(&acc.lo[sub][q], (unsigned long long)l);
             }
         }
-    }
     }
     __syncthreads();
 #pragma unroll
@@ -1067,11 +1040,10 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     const LossScratch ls(a->B, a->M, a->T, a->tf, a->H, a->W);
     float4* rec = reinterpret_cast<float4*>(a->images + ls.rec);
     int* bins = reinterpret_cast<int*>(a->images + ls.bins);
-    const int P = wbin_parts(a->B, a->T);
-    hipLaunchKernelGGL(k_iwe_wbin, dim3(a->B * a->T * P), dim3(WB_NT), 0, s, *a, nbands, rec, bins, nbg,
+    hipLaunchKernelGGL(k_iwe_wbin, dim3(a->B * a->T), dim3(WB_NT), 0, s, *a, nbands, rec, bins, nbg,
                        reinterpret_cast<float4*>(a->images + ls.rec4), a->images + ls.rec1,
-                       reinterpret_cast<int*>(a->images + ls.gbins), P);
-    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands), dim3(SPLAT_NT), 0, s, *a, nbands, rec, bins, P);
+                       reinterpret_cast<int*>(a->images + ls.gbins));
+    hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands), dim3(SPLAT_NT), 0, s, *a, nbands, rec, bins);
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
     hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit);
     hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, tsplit * chunks);
@@ -1094,12 +1066,11 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
         float4* rec4 = reinterpret_cast<float4*>(a->images + ls.rec4);
         float* rec1 = a->images + ls.rec1;
         int* bins = reinterpret_cast<int*>(a->images + ls.gbins);
-        // (tf == T: the forward's k_iwe_wbin formed these bins, in its parts)
-        const int P = a->tf == a->T ? wbin_parts(a->B, a->T) : 1;
+        // (tf == T: the forward's k_iwe_wbin formed these bins)
         if (a->tf != a->T)
             hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
         hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), 0, s, *a, gimg, g_flows, rec4, rec1,
-                           bins, nbands, P);
+                           bins, nbands);
     }
     SNN_CHECK_LAUNCH();
     return 0;
