@@ -442,7 +442,10 @@ __device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
 // The window loop carries the centre pixel of window t+1 (needed by the dt term) into the next
 // iteration, so every flow / mask map is read once per pixel instead of twice.
 constexpr int LOSS_NV = 11;
-constexpr int LOSS_MIN_BLOCKS = 2048;  // split the window loop until the grid has this many blocks
+#ifndef SNNFLOW_LOSS_MIN_BLOCKS
+#define SNNFLOW_LOSS_MIN_BLOCKS 2048
+#endif
+constexpr int LOSS_MIN_BLOCKS = SNNFLOW_LOSS_MIN_BLOCKS;  // split the window loop until the grid has this many blocks
 
 __host__ __device__ inline int loss_chunks(int64_t HWp) { return (int)((HWp + NT - 1) / NT); }
 __host__ __device__ inline int loss_tsplit(int B, int64_t HWp, int tf) {
