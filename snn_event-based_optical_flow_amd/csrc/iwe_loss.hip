@@ -443,7 +443,7 @@ __device__ inline float charb(float d) { return sqrtf(d * d + 1e-6f); }
 // iteration, so every flow / mask map is read once per pixel instead of twice.
 constexpr int LOSS_NV = 11;
 #ifndef SNNFLOW_LOSS_MIN_BLOCKS
-#define SNNFLOW_LOSS_MIN_BLOCKS 2048
+#define SNNFLOW_LOSS_MIN_BLOCKS 1024  // (2048: +1.7 us over the three kernels, 4096 / 8192: slower still)
 #endif
 constexpr int LOSS_MIN_BLOCKS = SNNFLOW_LOSS_MIN_BLOCKS;  // split the window loop until the grid has this many blocks
 
@@ -619,22 +619,32 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
     a.loss[0] = total + a.weight * sm;
 }
 
-// Per (sample, range of windows, pixel): dL/d(images) for both directions (first-range blocks)
-// and the smoothness part of dL/dflow_t (plain stores: g_flows is fully written here; the
-// events add into it afterwards).  As in k_iwe_loss the window loop carries the centre pixel
-// of window t+1, and the dt pair (t, t+1) is differentiated once: +g for window t, -g for t+1.
+// Per (sample, range of windows, chunk of NT pixels): dL/d(images) for both directions (first-range
+// blocks) and the smoothness part of dL/dflow_t (plain stores: g_flows is fully written here; the
+// events add into it afterwards).  Per window the flow (x, y) and mask values of the chunk and its
+// neighbour rows, [p0 - W - 1, p0 + NT + W + 1), are staged in LDS by coalesced loads (each value
+// loaded once, not by each of its 8 neighbours); the centre of window t+1 (the dt pair) comes straight
+// from memory.  As in k_iwe_loss the dt pair (t, t+1) is differentiated once: +g for window t, -g for
+// t+1.  Dynamic LDS: 3 (NT + 2 W + 2) floats.
+__host__ __device__ inline int px_stage_floats(int W) { return 3 * (NT + 2 * W + 2); }
+
 __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
                                                         float* g_flows, int chunks, int tsplit) {
+    extern __shared__ float nbs[];  // [3][S]: flow x, flow y, mask of the current window
     const int blk = xcd_block();
     const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
-    if (p >= HWp) return;
+    const bool valid = p < HWp;  // (no early return: the staging has barriers)
+    const int S = NT + 2 * a.W + 2, lo = chunk * NT - a.W - 1;
+    float* const sx = nbs;
+    float* const sy = nbs + S;
+    float* const smk = nbs + 2 * S;
     const float g = g_loss[0];
     // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
     const int comps = a.overwrite_intermediate ? 4 : 5;
     const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
-    const int h = p / a.W, w = p - h * a.W;
+    const int h = valid ? p / a.W : 0, w = valid ? p - h * a.W : 0;
     const bool sm = a.smoothing_mask != 0, dt_terms = !a.overwrite_intermediate;
     // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
     auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
@@ -646,31 +656,25 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
     const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
     // the 8 neighbours in the order their terms are summed (right, left, down, up, down-right,
     // up-left, up-right, down-left; odd q: this pixel is the pair's 'b'); a neighbour outside the
-    // image reads this pixel (address always valid) and contributes nothing
+    // image contributes nothing
     const int Wd = a.W;
     const int off[8] = {1, -1, Wd, -Wd, Wd + 1, -Wd - 1, -Wd + 1, Wd - 1};
     const bool vr = w + 1 < a.W, vl = w >= 1, vd = h + 1 < a.H, vu = h >= 1;
     const bool ok[8] = {vr, vl, vd, vu, vd && vr, vu && vl, vu && vr, vd && vl};
-    // one window's neighbour values, loaded a window ahead of their use (the loads no longer wait
-    // behind the previous window's g_flows stores)
-    auto load_nb = [&](int t, float (&X)[8], float (&Y)[8], float (&M)[8]) {
+    auto stage = [&](int t) {
         const float* fx = flow_of(a, b, t);
         const float* m = mask_of(a, b, t);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int pq = ok[q] ? p + off[q] : p;
-            X[q] = fx[pq];
-            Y[q] = fx[HWp + pq];
-            M[q] = m[pq];
+        for (int e = tid; e < S; e += NT) {
+            const int64_t q = (int64_t)lo + e;
+            const bool in = q >= 0 && q < HWp;
+            sx[e] = in ? fx[q] : 0.0f;
+            sy[e] = in ? fx[HWp + q] : 0.0f;
+            smk[e] = in ? m[q] : 0.0f;
         }
     };
-    float X[8], Y[8], M[8];
-    load_nb(t0, X, Y, M);
-    const float* f0 = flow_of(a, b, t0);
-    float cx = f0[p], cy = f0[HWp + p], cm = mask_of(a, b, t0)[p];
-    // (the image gradients after the first window's loads are issued: their stores would
-    // otherwise hold those loads back)
-    if (tg == 0) {
+    stage(t0);
+    // (the image gradients while the first window's staging loads are in flight)
+    if (tg == 0 && valid) {
         const float T = (float)a.T;
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
@@ -696,17 +700,17 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
             gb[3 * img] = gqn / dn;
         }
     }
-    float gprev = 0.0f;  // gradient of the dt pair (t-1, t) w.r.t. window t-1
-    if (dt_terms && t0 >= 1) {
+    const int c0 = p - lo;  // this pixel's staging index
+    float gprev = 0.0f;     // gradient of the dt pair (t-1, t) w.r.t. window t-1
+    __syncthreads();
+    float cx = sx[c0], cy = sy[c0], cm = smk[c0];
+    if (dt_terms && t0 >= 1 && valid) {
         const float* fp = flow_of(a, b, t0 - 1);
         gprev = pg(fp[p], fp[HWp + p], mask_of(a, b, t0 - 1)[p], cx, cy, cm);
     }
     for (int t = t0; t < t1; ++t) {
-        float nX[8], nY[8], nM[8];
-        const bool more = t + 1 < t1;
-        if (more) load_nb(t + 1, nX, nY, nM);
         float nx = 0.0f, ny = 0.0f, nm = 0.0f;
-        if (t + 1 < a.tf) {
+        if (t + 1 < a.tf && valid) {
             const float* f2 = flow_of(a, b, t + 1);
             nx = f2[p];
             ny = f2[HWp + p];
@@ -717,8 +721,9 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             if (!ok[q]) continue;
-            if (q % 2 == 0) acc += pg(cx, cy, cm, X[q], Y[q], M[q]);
-            else acc -= pg(X[q], Y[q], M[q], cx, cy, cm);
+            const int e = c0 + off[q];
+            if (q % 2 == 0) acc += pg(cx, cy, cm, sx[e], sy[e], smk[e]);
+            else acc -= pg(sx[e], sy[e], smk[e], cx, cy, cm);
         }
         float gnext = 0.0f;
         if (t + 1 < a.tf && dt_terms) {
@@ -726,20 +731,19 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
             acc += gnext;
         }
         if (dt_terms && t >= 1) acc -= gprev;
-        float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
-        gf[p] = acc;
-        gf[HWp + p] = acc;
+        if (valid) {
+            float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
+            gf[p] = acc;
+            gf[HWp + p] = acc;
+        }
         gprev = gnext;
         cx = nx;
         cy = ny;
         cm = nm;
-        if (more) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                X[q] = nX[q];
-                Y[q] = nY[q];
-                M[q] = nM[q];
-            }
+        if (t + 1 < t1) {
+            __syncthreads();  // every thread is done with window t's staging
+            stage(t + 1);
+            __syncthreads();
         }
     }
 }
@@ -1060,7 +1064,9 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
-    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, g_loss, gimg, g_flows,
+    const size_t px_lds = (size_t)px_stage_floats(a->W) * sizeof(float);
+    if (px_lds > 64 * 1024) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: W above 2600 pixels");
+    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), px_lds, s, *a, g_loss, gimg, g_flows,
                        chunks, tsplit);
     if (a->M > 0) {  // the events binned by own-pixel band, then per band: event gradients + exact per-pixel sums
         const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
