@@ -625,21 +625,24 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
 // neighbour rows, [p0 - W - 1, p0 + NT + W + 1), are staged in LDS by coalesced loads (each value
 // loaded once, not by each of its 8 neighbours); the centre of window t+1 (the dt pair) comes straight
 // from memory.  As in k_iwe_loss the dt pair (t, t+1) is differentiated once: +g for window t, -g for
-// t+1.  Dynamic LDS: 3 (NT + 2 W + 2) floats.
-__host__ __device__ inline int px_stage_floats(int W) { return 3 * (NT + 2 * W + 2); }
+// t+1.  The next window's staging loads are issued into registers before this window's math (two LDS
+// buffers, one barrier per window).  Dynamic LDS: 2 x 3 (NT + 2 W + 2) floats.
+// PX_SR: staged values per thread and array held in registers, NT + 2 W + 2 <= PX_SR NT (3: W <= 255, 8: W <= 895)
+__host__ __device__ inline int px_stage_floats(int W) { return 2 * 3 * (NT + 2 * W + 2); }
 
+template <int PX_SR>
 __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
                                                         float* g_flows, int chunks, int tsplit) {
-    extern __shared__ float nbs[];  // [3][S]: flow x, flow y, mask of the current window
+    extern __shared__ float nbs[];  // [2][3][S]: flow x, flow y, mask of the current and the next window
     const int blk = xcd_block();
     const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p = chunk * NT + tid;
     const bool valid = p < HWp;  // (no early return: the staging has barriers)
     const int S = NT + 2 * a.W + 2, lo = chunk * NT - a.W - 1;
-    float* const sx = nbs;
-    float* const sy = nbs + S;
-    float* const smk = nbs + 2 * S;
+    float* sx = nbs;
+    float* sy = nbs + S;
+    float* smk = nbs + 2 * S;
     const float g = g_loss[0];
     // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
     const int comps = a.overwrite_intermediate ? 4 : 5;
@@ -661,18 +664,33 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
     const int off[8] = {1, -1, Wd, -Wd, Wd + 1, -Wd - 1, -Wd + 1, Wd - 1};
     const bool vr = w + 1 < a.W, vl = w >= 1, vd = h + 1 < a.H, vu = h >= 1;
     const bool ok[8] = {vr, vl, vd, vu, vd && vr, vu && vl, vu && vr, vd && vl};
-    auto stage = [&](int t) {
+    float rx[PX_SR], ry[PX_SR], rm[PX_SR];
+    auto stage_load = [&](int t) {
         const float* fx = flow_of(a, b, t);
         const float* m = mask_of(a, b, t);
-        for (int e = tid; e < S; e += NT) {
+#pragma unroll
+        for (int k = 0; k < PX_SR; ++k) {
+            const int e = tid + k * NT;
             const int64_t q = (int64_t)lo + e;
-            const bool in = q >= 0 && q < HWp;
-            sx[e] = in ? fx[q] : 0.0f;
-            sy[e] = in ? fx[HWp + q] : 0.0f;
-            smk[e] = in ? m[q] : 0.0f;
+            const bool in = e < S && q >= 0 && q < HWp;
+            rx[k] = in ? fx[q] : 0.0f;
+            ry[k] = in ? fx[HWp + q] : 0.0f;
+            rm[k] = in ? m[q] : 0.0f;
         }
     };
-    stage(t0);
+    auto stage_store = [&](float* dx, float* dy, float* dm) {
+#pragma unroll
+        for (int k = 0; k < PX_SR; ++k) {
+            const int e = tid + k * NT;
+            if (e < S) {
+                dx[e] = rx[k];
+                dy[e] = ry[k];
+                dm[e] = rm[k];
+            }
+        }
+    };
+    stage_load(t0);
+    stage_store(sx, sy, smk);
     // (the image gradients while the first window's staging loads are in flight)
     if (tg == 0 && valid) {
         const float T = (float)a.T;
@@ -709,6 +727,7 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
         gprev = pg(fp[p], fp[HWp + p], mask_of(a, b, t0 - 1)[p], cx, cy, cm);
     }
     for (int t = t0; t < t1; ++t) {
+        if (t + 1 < t1) stage_load(t + 1);  // in flight during this window's math
         float nx = 0.0f, ny = 0.0f, nm = 0.0f;
         if (t + 1 < a.tf && valid) {
             const float* f2 = flow_of(a, b, t + 1);
@@ -740,9 +759,12 @@ __global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a,
         cx = nx;
         cy = ny;
         cm = nm;
-        if (t + 1 < t1) {
-            __syncthreads();  // every thread is done with window t's staging
-            stage(t + 1);
+        if (t + 1 < t1) {  // the other buffer (last read in window t - 1, before the previous barrier)
+            float* nb = sx == nbs ? nbs + 3 * S : nbs;
+            sx = nb;
+            sy = nb + S;
+            smk = nb + 2 * S;
+            stage_store(sx, sy, smk);
             __syncthreads();
         }
     }
@@ -1065,9 +1087,13 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     const int64_t HWp = (int64_t)a->H * a->W;
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
     const size_t px_lds = (size_t)px_stage_floats(a->W) * sizeof(float);
-    if (px_lds > 64 * 1024) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: W above 2600 pixels");
-    hipLaunchKernelGGL(k_iwe_loss_bwd_px, dim3(a->B * tsplit * chunks), dim3(NT), px_lds, s, *a, g_loss, gimg, g_flows,
-                       chunks, tsplit);
+    if (NT + 2 * a->W + 2 > 8 * NT) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: W above 895 pixels");
+    if (NT + 2 * a->W + 2 <= 3 * NT)
+        hipLaunchKernelGGL(k_iwe_loss_bwd_px<3>, dim3(a->B * tsplit * chunks), dim3(NT), px_lds, s, *a, g_loss, gimg,
+                           g_flows, chunks, tsplit);
+    else
+        hipLaunchKernelGGL(k_iwe_loss_bwd_px<8>, dim3(a->B * tsplit * chunks), dim3(NT), px_lds, s, *a, g_loss, gimg,
+                           g_flows, chunks, tsplit);
     if (a->M > 0) {  // the events binned by own-pixel band, then per band: event gradients + exact per-pixel sums
         const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
         if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
