@@ -1085,7 +1085,11 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
-    const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
+    const int chunks = loss_chunks(HWp);
+#ifndef SNNFLOW_PX_TSPLIT
+#define SNNFLOW_PX_TSPLIT 0  // windows split over blocks in the pixel backward: 0 = as the loss rows (loss_tsplit)
+#endif
+    const int tsplit = SNNFLOW_PX_TSPLIT > 0 ? (SNNFLOW_PX_TSPLIT < a->tf ? SNNFLOW_PX_TSPLIT : a->tf) : loss_tsplit(a->B, HWp, a->tf);
     const size_t px_lds = (size_t)px_stage_floats(a->W) * sizeof(float);
     if (NT + 2 * a->W + 2 > 8 * NT) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: W above 895 pixels");
     if (NT + 2 * a->W + 2 <= 3 * NT)
