@@ -12,4 +12,4 @@ for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
   timeout -k 10 300 rocprofv3 --pmc $ctrs -d $OUT/p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/prof_step.py ${PMC_ARGS:-} > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 ls -R $OUT | head -30
-python3 $GRAFT_REPO_ROOT/tools/pmc_traffic.py $OUT ${PMC_KEY:-C8_R128_B8}
+python3 $GRAFT_REPO_ROOT/tools/pmc_traffic.py $OUT ${PMC_KEY:-C8_R128_B8} $GRAFT_REPO_ROOT/gpurun_out/pmc_counters.json

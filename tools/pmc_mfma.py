@@ -35,7 +35,7 @@ def main():
     out = {"note": "rocprofv3 --pmc (tools/pmc_mfma.sh), per-dispatch averages per kernel class; mfma_busy_frac = "
                    "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs)",
            "workloads": {"c8": "LIFFireNet C=8 128^2 B=8 T=10 wavefront (eager)",
-                         "c32": "LIFFireNet C=32 128^2 B=8 T=10 per-step (eager)",
+                         "c32": "LIFFireNet C=32 128^2 B=8 T=10 wavefront (eager)",
                          "unet": "SpikingRecEVFlowNet base 32, 256^2 B=16 T=20 (eager)"},
            "kernels": res}
     path = os.path.join(root, "pmc_mfma.json")  # copied to profiles/r02/

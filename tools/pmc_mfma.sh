@@ -24,7 +24,11 @@ run() {  # name, args...
     timeout -k 10 300 rocprofv3 --pmc $ctrs -d $OUT/$name/p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/prof_step.py "$@" > $OUT/$name.p$i.log 2>&1 || { echo "$name pass $i failed"; tail -5 $OUT/$name.p$i.log; exit 1; }
   done
 }
-run c8 8 128 8 10 2 || exit 1
-SNNFLOW_PER_STEP=1 run c32 32 128 8 10 2 || exit 1
-run unet unet 256 16 20 32 1 || exit 1
+for w in ${WL:-c8 c32 unet}; do
+  case $w in
+    c8) run c8 8 128 8 10 2 || exit 1 ;;
+    c32) run c32 32 128 8 10 2 || exit 1 ;;
+    unet) run unet unet 256 16 20 32 1 || exit 1 ;;
+  esac
+done
 python3 $GRAFT_REPO_ROOT/tools/pmc_mfma.py $OUT
