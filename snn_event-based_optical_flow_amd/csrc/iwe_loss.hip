@@ -619,154 +619,39 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
     a.loss[0] = total + a.weight * sm;
 }
 
-// Per (sample, range of windows, chunk of NT pixels): dL/d(images) for both directions (first-range
-// blocks) and the smoothness part of dL/dflow_t (plain stores: g_flows is fully written here; the
-// events add into it afterwards).  Per window the flow (x, y) and mask values of the chunk and its
-// neighbour rows, [p0 - W - 1, p0 + NT + W + 1), are staged in LDS by coalesced loads (each value
-// loaded once, not by each of its 8 neighbours); the centre of window t+1 (the dt pair) comes straight
-// from memory.  As in k_iwe_loss the dt pair (t, t+1) is differentiated once: +g for window t, -g for
-// t+1.  The next window's staging loads are issued into registers before this window's math (two LDS
-// buffers, one barrier per window).  Dynamic LDS: 2 x 3 (NT + 2 W + 2) floats.
-// PX_SR: staged values per thread and array held in registers, NT + 2 W + 2 <= PX_SR NT (3: W <= 255, 8: W <= 895)
-__host__ __device__ inline int px_stage_floats(int W) { return 2 * 3 * (NT + 2 * W + 2); }
-
-template <int PX_SR>
-__global__ __launch_bounds__(NT) void k_iwe_loss_bwd_px(snnflow_iwe_loss_args a, const float* g_loss, float* gimg,
-                                                        float* g_flows, int chunks, int tsplit) {
-    extern __shared__ float nbs[];  // [2][3][S]: flow x, flow y, mask of the current and the next window
+// Per (sample, pixel): dL/d(images) for both directions (loss/flow.py:219-261 differentiated; the
+// smoothness part of dL/dflow is formed by k_iwe_bwd_band with the events' part, so g_flows is written
+// once).
+__global__ __launch_bounds__(NT) void k_iwe_img_bwd(snnflow_iwe_loss_args a, const float* g_loss, float* gimg, int chunks) {
     const int blk = xcd_block();
-    const int tid = threadIdx.x, chunk = blk % chunks, tg = (blk / chunks) % tsplit, b = blk / (chunks * tsplit);
+    const int chunk = blk % chunks, b = blk / chunks;
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
-    const int p = chunk * NT + tid;
-    const bool valid = p < HWp;  // (no early return: the staging has barriers)
-    const int S = NT + 2 * a.W + 2, lo = chunk * NT - a.W - 1;
-    float* sx = nbs;
-    float* sy = nbs + S;
-    float* smk = nbs + 2 * S;
+    const int p = chunk * NT + threadIdx.x;
+    if (p >= HWp) return;
     const float g = g_loss[0];
-    // smoothness: loss += weight * (sum of masked charbonnier terms) / comps / T
-    const int comps = a.overwrite_intermediate ? 4 : 5;
-    const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
-    const int h = valid ? p / a.W : 0, w = valid ? p - h * a.W : 0;
-    const bool sm = a.smoothing_mask != 0, dt_terms = !a.overwrite_intermediate;
-    // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
-    auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
-        const float dd = (ax - bx) + (ay - by);
-        const float c = charb(dd);
-        const float mk = sm ? am * bm : 1.0f;
-        return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
-    };
-    const int t0 = tg * a.tf / tsplit, t1 = (tg + 1) * a.tf / tsplit;
-    // the 8 neighbours in the order their terms are summed (right, left, down, up, down-right,
-    // up-left, up-right, down-left; odd q: this pixel is the pair's 'b'); a neighbour outside the
-    // image contributes nothing
-    const int Wd = a.W;
-    const int off[8] = {1, -1, Wd, -Wd, Wd + 1, -Wd - 1, -Wd + 1, Wd - 1};
-    const bool vr = w + 1 < a.W, vl = w >= 1, vd = h + 1 < a.H, vu = h >= 1;
-    const bool ok[8] = {vr, vl, vd, vu, vd && vr, vu && vl, vu && vr, vd && vl};
-    float rx[PX_SR], ry[PX_SR], rm[PX_SR];
-    auto stage_load = [&](int t) {
-        const float* fx = flow_of(a, b, t);
-        const float* m = mask_of(a, b, t);
+    const float T = (float)a.T;
 #pragma unroll
-        for (int k = 0; k < PX_SR; ++k) {
-            const int e = tid + k * NT;
-            const int64_t q = (int64_t)lo + e;
-            const bool in = e < S && q >= 0 && q < HWp;
-            rx[k] = in ? fx[q] : 0.0f;
-            ry[k] = in ? fx[HWp + q] : 0.0f;
-            rm[k] = in ? m[q] : 0.0f;
+    for (int d = 0; d < 2; ++d) {
+        const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
+        const float nz = ps[2], lb = ps[3];
+        const float gS = a.loss_scaling ? g / nz : g;
+        const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+        float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
+        const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
+        const float dp = cp + 1e-9f, dn = cn + 1e-9f;
+        const float qp = tp / dp, qn = tn / dn;
+        const float Ap = qp / T, An = qn / T;
+        const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
+        float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
+        if (a.loss_scaling && !(cp + cn > 0.0f)) {
+            const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
+            gcp += gz;
+            gcn += gz;
         }
-    };
-    auto stage_store = [&](float* dx, float* dy, float* dm) {
-#pragma unroll
-        for (int k = 0; k < PX_SR; ++k) {
-            const int e = tid + k * NT;
-            if (e < S) {
-                dx[e] = rx[k];
-                dy[e] = ry[k];
-                dm[e] = rm[k];
-            }
-        }
-    };
-    stage_load(t0);
-    stage_store(sx, sy, smk);
-    // (the image gradients while the first window's staging loads are in flight)
-    if (tg == 0 && valid) {
-        const float T = (float)a.T;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-            const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
-            const float nz = ps[2], lb = ps[3];
-            const float gS = a.loss_scaling ? g / nz : g;
-            const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-            float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-            const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
-            const float dp = cp + 1e-9f, dn = cn + 1e-9f;
-            const float qp = tp / dp, qn = tn / dn;
-            const float Ap = qp / T, An = qn / T;
-            const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
-            float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
-            if (a.loss_scaling && !(cp + cn > 0.0f)) {
-                const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
-                gcp += gz;
-                gcn += gz;
-            }
-            gb[0] = gcp;
-            gb[img] = gcn;
-            gb[2 * img] = gqp / dp;
-            gb[3 * img] = gqn / dn;
-        }
-    }
-    const int c0 = p - lo;  // this pixel's staging index
-    float gprev = 0.0f;     // gradient of the dt pair (t-1, t) w.r.t. window t-1
-    __syncthreads();
-    float cx = sx[c0], cy = sy[c0], cm = smk[c0];
-    if (dt_terms && t0 >= 1 && valid) {
-        const float* fp = flow_of(a, b, t0 - 1);
-        gprev = pg(fp[p], fp[HWp + p], mask_of(a, b, t0 - 1)[p], cx, cy, cm);
-    }
-    for (int t = t0; t < t1; ++t) {
-        if (t + 1 < t1) stage_load(t + 1);  // in flight during this window's math
-        float nx = 0.0f, ny = 0.0f, nm = 0.0f;
-        if (t + 1 < a.tf && valid) {
-            const float* f2 = flow_of(a, b, t + 1);
-            nx = f2[p];
-            ny = f2[HWp + p];
-            nm = mask_of(a, b, t + 1)[p];
-        }
-        float acc = 0.0f;
-        // term with 'a' = (t,h,w), 'b' = neighbour: +dc/dd;  term with 'b' = (t,h,w): -dc/dd
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            if (!ok[q]) continue;
-            const int e = c0 + off[q];
-            if (q % 2 == 0) acc += pg(cx, cy, cm, sx[e], sy[e], smk[e]);
-            else acc -= pg(sx[e], sy[e], smk[e], cx, cy, cm);
-        }
-        float gnext = 0.0f;
-        if (t + 1 < a.tf && dt_terms) {
-            gnext = pg(cx, cy, cm, nx, ny, nm);
-            acc += gnext;
-        }
-        if (dt_terms && t >= 1) acc -= gprev;
-        if (valid) {
-            float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp;
-            gf[p] = acc;
-            gf[HWp + p] = acc;
-        }
-        gprev = gnext;
-        cx = nx;
-        cy = ny;
-        cm = nm;
-        if (t + 1 < t1) {  // the other buffer (last read in window t - 1, before the previous barrier)
-            float* nb = sx == nbs ? nbs + 3 * S : nbs;
-            sx = nb;
-            sy = nb + S;
-            smk = nb + 2 * S;
-            stage_store(sx, sy, smk);
-            __syncthreads();
-        }
+        gb[0] = gcp;
+        gb[img] = gcn;
+        gb[2 * img] = gqp / dp;
+        gb[3 * img] = gqn / dn;
     }
 }
 
@@ -842,44 +727,123 @@ __global__ __launch_bounds__(BIN_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int
     }
 }
 
-// The loss backward's per-event part, per (sample, flow window, band of GB_BAND pixels): each event of
-// the band's bin gathers dL/d(images) at the 4 corners of both warps and chains them through the
-// bilinear weights to its flow (eight lanes per event, kBwdLanes), and the band's
-// per-pixel sums of those flow gradients are formed in LDS in exact two-word fixed point (SplatLdsX's
-// split: integer adds, so the sums do not depend on the order of the events) and added to g_flows once
-// per touched pixel.  No block reads an event outside its bin.
+// dL/dflow of one (sample, flow window t, band of GB_BAND pixels), written once:
+//  * the smoothness part (loss/flow.py:263-303 differentiated): per pixel the 8 neighbour pairs of
+//    window t (the flow / mask values of the band and its neighbour rows, [p0 - W - 1, p0 + GB_BAND + W
+//    + 1), staged in LDS by coalesced loads) and the dt pairs (t-1, t), (t, t+1) (centres straight from
+//    memory; each pair's term is the one its other window computes, the same floats);
+//  * the events' part: each event of the band's bin (events binned by the band of their own pixel --
+//    the pixel their flow gradient lands in) gathers dL/d(images) at the 4 corners of both warps and
+//    chains them through the bilinear weights to its flow (eight lanes per event, kBwdLanes); the
+//    band's per-pixel sums of those are formed in LDS in exact two-word fixed point (integer adds: the
+//    sums do not depend on the order of the events; SplatLdsX's split).  No block reads an event
+//    outside its bin.
+//  g_flows = smoothness + the event sum (where a pixel has events), the same floats as a separate
+//  smoothness pass followed by adding the sums.  Dynamic LDS: 3 (GB_BAND + 2 W + 2) floats.
 struct GevLds {
     unsigned long long hi[2][GB_BAND], lo[2][GB_BAND];
 };
+__host__ __device__ inline int gb_stage_floats(int W) { return 3 * (GB_BAND + 2 * W + 2); }
 
-__global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* __restrict__ gimg,
-                                                        float* g_flows, const float4* __restrict__ rec4,
-                                                        const float* __restrict__ rec1, const int* __restrict__ bins,
-                                                        int nbands) {
+__global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* g_loss,
+                                                        const float* __restrict__ gimg, float* g_flows,
+                                                        const float4* __restrict__ rec4, const float* __restrict__ rec1,
+                                                        const int* __restrict__ bins, int nbands, int has_events) {
     __shared__ GevLds acc;
+    extern __shared__ float nbs[];  // [3][S]: flow x, flow y, mask of window t around the band
     const int tid = threadIdx.x;
     const int blk = xcd_block();  // a sample's windows and bands on one XCD: its flows / image gradients in one L2
     const int band = blk % nbands, rest = blk / nbands, t = rest % a.tf, b = rest / a.tf;
     const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
     const int p0 = band * GB_BAND;
     const int np = (int)((HWp - p0) < GB_BAND ? (HWp - p0) : GB_BAND);
-    const int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
-    int i0, i1;
-    flow_window_events(a, t, i0, i1);
-    const int e0 = bo[band], e1 = bo[band + 1];
-    const int64_t base = (int64_t)b * a.M + i0;
-    for (int j = tid; j < 2 * GB_BAND; j += GB_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
-    // the band's current g_flows values (the pixel backward's), read ahead of the event loop
-    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
-    constexpr int GFR = 2 * GB_BAND / GB_NT;
-    float gold[GFR];
-#pragma unroll
-    for (int k = 0; k < GFR; ++k) {
-        const int j = tid + k * GB_NT, c = j / GB_BAND, q = j - c * GB_BAND;
-        gold[k] = q < np ? gf[c * HWp + q] : 0.0f;
+    const int S = GB_BAND + 2 * a.W + 2, lo = p0 - a.W - 1;
+    float* const sx = nbs;
+    float* const sy = nbs + S;
+    float* const smk = nbs + 2 * S;
+    // smoothness inputs: window t around the band (LDS), the centres of windows t-1 and t+1 (registers)
+    constexpr int PPT = GB_BAND / GB_NT;  // band pixels per thread
+    const bool sm = a.smoothing_mask != 0, dt_terms = !a.overwrite_intermediate;
+    const float* f1 = flow_of(a, b, t);
+    const float* m1 = mask_of(a, b, t);
+    for (int e = tid; e < S; e += GB_NT) {
+        const int64_t q = (int64_t)lo + e;
+        const bool in = q >= 0 && q < HWp;
+        sx[e] = in ? f1[q] : 0.0f;
+        sy[e] = in ? f1[HWp + q] : 0.0f;
+        smk[e] = in ? m1[q] : 0.0f;
     }
+    float px_[PPT], py_[PPT], pm_[PPT], nx_[PPT], ny_[PPT], nm_[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+        const int j = tid + k * GB_NT;
+        const int64_t p = p0 + j;
+        px_[k] = py_[k] = pm_[k] = nx_[k] = ny_[k] = nm_[k] = 0.0f;
+        if (j < np && dt_terms && t >= 1) {
+            const float* fp = flow_of(a, b, t - 1);
+            px_[k] = fp[p];
+            py_[k] = fp[HWp + p];
+            pm_[k] = mask_of(a, b, t - 1)[p];
+        }
+        if (j < np && dt_terms && t + 1 < a.tf) {
+            const float* fn = flow_of(a, b, t + 1);
+            nx_[k] = fn[p];
+            ny_[k] = fn[HWp + p];
+            nm_[k] = mask_of(a, b, t + 1)[p];
+        }
+    }
+    int e0 = 0, e1 = 0;
+    int64_t base = 0;
+    if (has_events) {
+        const int* bo = bins + ((int64_t)b * a.tf + t) * (nbands + 1);
+        int i0, i1;
+        flow_window_events(a, t, i0, i1);
+        e0 = bo[band];
+        e1 = bo[band + 1];
+        base = (int64_t)b * a.M + i0;
+    }
+    for (int j = tid; j < 2 * GB_BAND; j += GB_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
     const float* fl = a.flows[a.tf == 1 ? 0 : t] + (int64_t)b * 2 * HWp;
     __syncthreads();
+    // the smoothness gradient of this thread's pixels (the sum order of the per-pixel form: the 8
+    // neighbours -- right, left, down, up, down-right, up-left, up-right, down-left; odd q: this pixel
+    // is the pair's 'b' -- then +(t, t+1), then -(t-1, t))
+    float smooth[PPT];
+    {
+        const float g = g_loss[0];
+        const int comps = a.overwrite_intermediate ? 4 : 5;
+        const float gsm = ((g * a.weight) / (float)comps) / (float)a.tf;
+        // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
+        auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
+            const float dd = (ax - bx) + (ay - by);
+            const float c = charb(dd);
+            const float mk = sm ? am * bm : 1.0f;
+            return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
+        };
+        const int Wd = a.W;
+        const int off[8] = {1, -1, Wd, -Wd, Wd + 1, -Wd - 1, -Wd + 1, Wd - 1};
+#pragma unroll
+        for (int k = 0; k < PPT; ++k) {
+            const int j = tid + k * GB_NT;
+            const int p = p0 + (j < np ? j : 0);
+            const int h = p / a.W, w = p - h * a.W;
+            const bool vr = w + 1 < a.W, vl = w >= 1, vd = h + 1 < a.H, vu = h >= 1;
+            const bool ok[8] = {vr, vl, vd, vu, vd && vr, vu && vl, vu && vr, vd && vl};
+            const int c0 = p - lo;
+            const float cx = sx[c0], cy = sy[c0], cm = smk[c0];
+            float v = 0.0f;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                if (!ok[q]) continue;
+                const int e = c0 + off[q];
+                if (q % 2 == 0) v += pg(cx, cy, cm, sx[e], sy[e], smk[e]);
+                else v -= pg(sx[e], sy[e], smk[e], cx, cy, cm);
+            }
+            if (t + 1 < a.tf && dt_terms) v += pg(cx, cy, cm, nx_[k], ny_[k], nm_[k]);
+            if (dt_terms && t >= 1) v -= pg(px_[k], py_[k], pm_[k], cx, cy, cm);
+            smooth[k] = v;
+        }
+    }
     const int sub = tid & (kBwdLanes - 1), d = sub >> 2, qc = sub & 3;
     const float tref = d == 0 ? (float)a.T : 0.0f;
     const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
@@ -936,12 +900,17 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
         }
     }
     __syncthreads();
+    float* gf = g_flows + (((int64_t)b * a.tf + t) * 2) * HWp + p0;
 #pragma unroll
-    for (int k = 0; k < GFR; ++k) {
-        const int j = tid + k * GB_NT, c = j / GB_BAND, q = j - c * GB_BAND;
+    for (int k = 0; k < PPT; ++k) {
+        const int q = tid + k * GB_NT;
         if (q >= np) continue;
-        const unsigned long long h = acc.hi[c][q], l = acc.lo[c][q];
-        if (h | l) gf[c * HWp + q] = gold[k] + (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {  // plane 0: x, 1: y
+            const unsigned long long h = acc.hi[c][q], l = acc.lo[c][q];
+            gf[c * HWp + q] =
+                (h | l) ? smooth[k] + (float)((double)(long long)h * 0x1p-32 + (double)(long long)l * 0x1p-75) : smooth[k];
+        }
     }
 }
 
@@ -1086,31 +1055,21 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
     const int chunks = loss_chunks(HWp);
-#ifndef SNNFLOW_PX_TSPLIT
-#define SNNFLOW_PX_TSPLIT 0  // windows split over blocks in the pixel backward: 0 = as the loss rows (loss_tsplit)
-#endif
-    const int tsplit = SNNFLOW_PX_TSPLIT > 0 ? (SNNFLOW_PX_TSPLIT < a->tf ? SNNFLOW_PX_TSPLIT : a->tf) : loss_tsplit(a->B, HWp, a->tf);
-    const size_t px_lds = (size_t)px_stage_floats(a->W) * sizeof(float);
-    if (NT + 2 * a->W + 2 > 8 * NT) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: W above 895 pixels");
-    if (NT + 2 * a->W + 2 <= 3 * NT)
-        hipLaunchKernelGGL(k_iwe_loss_bwd_px<3>, dim3(a->B * tsplit * chunks), dim3(NT), px_lds, s, *a, g_loss, gimg,
-                           g_flows, chunks, tsplit);
-    else
-        hipLaunchKernelGGL(k_iwe_loss_bwd_px<8>, dim3(a->B * tsplit * chunks), dim3(NT), px_lds, s, *a, g_loss, gimg,
-                           g_flows, chunks, tsplit);
-    if (a->M > 0) {  // the events binned by own-pixel band, then per band: event gradients + exact per-pixel sums
-        const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
-        if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
-        const LossScratch ls(a->B, a->M, a->T, a->tf, a->H, a->W);
-        float4* rec4 = reinterpret_cast<float4*>(a->images + ls.rec4);
-        float* rec1 = a->images + ls.rec1;
-        int* bins = reinterpret_cast<int*>(a->images + ls.gbins);
-        // (tf == T: the forward's k_iwe_wbin formed these bins)
-        if (a->tf != a->T)
-            hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
-        hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), 0, s, *a, gimg, g_flows, rec4, rec1,
-                           bins, nbands);
-    }
+    hipLaunchKernelGGL(k_iwe_img_bwd, dim3(a->B * chunks), dim3(NT), 0, s, *a, g_loss, gimg, chunks);
+    // the events binned by own-pixel band (tf == T: the forward's k_iwe_wbin formed these bins), then per
+    // band: the smoothness gradient + the events' gradients summed per pixel in exact fixed point
+    const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
+    if (nbands > kMaxBands) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: H * W above 2^21 pixels");
+    const size_t gb_lds = (size_t)gb_stage_floats(a->W) * sizeof(float);
+    if (gb_lds > 48 * 1024) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: W above 1791 pixels");
+    const LossScratch ls(a->B, a->M, a->T, a->tf, a->H, a->W);
+    float4* rec4 = reinterpret_cast<float4*>(a->images + ls.rec4);
+    float* rec1 = a->images + ls.rec1;
+    int* bins = reinterpret_cast<int*>(a->images + ls.gbins);
+    if (a->M > 0 && a->tf != a->T)
+        hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
+    hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), gb_lds, s, *a, g_loss, gimg, g_flows,
+                       rec4, rec1, bins, nbands, a->M > 0 ? 1 : 0);
     SNN_CHECK_LAUNCH();
     return 0;
 }
