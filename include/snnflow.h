@@ -391,13 +391,13 @@ typedef struct snnflow_iwe_loss_args {
     float* loss;                /* out [1]                                             */
 } snnflow_iwe_loss_args;
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
-/* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written). gimg scratch [2][4][B][H*W].
- * Reads the forward's images scratch (the IWEs and, ABI 38, the events binned by the pixel band of
- * their own pixel -- formed by the forward when tf == T, here otherwise); one block per band forms the
- * events' flow gradients and sums them per pixel in exact two-word fixed point (order-independent:
- * bit-reproducible g_flows).  H * W <= 2^21. */
-int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg,
-                         float* g_flows, void* stream);
+/* g_loss: device scalar; g_flows out [B][tf][2][H][W] (fully written).  Reads the forward's images
+ * scratch (the IWEs and, ABI 38, the events binned by the pixel band of their own pixel -- formed by the
+ * forward when tf == T, here otherwise); one block per (sample, flow window, band) forms the smoothness
+ * gradient of its pixels and the events' flow gradients (the image gradients formed at their warped
+ * corners), summed per pixel in exact two-word fixed point (order-independent: bit-reproducible
+ * g_flows), and writes the band once.  H * W <= 2^21, W <= 1791. */
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* g_flows, void* stream);
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf);
 /* floats of the images scratch (ABI 38: the IWEs and both binnings of the events; H * W <= 2^21) */
 int64_t snnflow_iwe_scratch_floats(int B, int M, int T, int tf, int H, int W);

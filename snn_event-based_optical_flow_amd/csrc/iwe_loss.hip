@@ -619,40 +619,24 @@ __global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a
     a.loss[0] = total + a.weight * sm;
 }
 
-// Per (sample, pixel): dL/d(images) for both directions (loss/flow.py:219-261 differentiated; the
-// smoothness part of dL/dflow is formed by k_iwe_bwd_band with the events' part, so g_flows is written
-// once).
-__global__ __launch_bounds__(NT) void k_iwe_img_bwd(snnflow_iwe_loss_args a, const float* g_loss, float* gimg, int chunks) {
-    const int blk = xcd_block();
-    const int chunk = blk % chunks, b = blk / chunks;
-    const int64_t HWp = (int64_t)a.H * a.W, img = (int64_t)a.B * HWp;
-    const int p = chunk * NT + threadIdx.x;
-    if (p >= HWp) return;
-    const float g = g_loss[0];
-    const float T = (float)a.T;
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-        const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
-        const float nz = ps[2], lb = ps[3];
-        const float gS = a.loss_scaling ? g / nz : g;
-        const float* base = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-        float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp + p;
-        const float cp = base[0], cn = base[img], tp = base[2 * img], tn = base[3 * img];
-        const float dp = cp + 1e-9f, dn = cn + 1e-9f;
-        const float qp = tp / dp, qn = tn / dn;
-        const float Ap = qp / T, An = qn / T;
-        const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
-        float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
-        if (a.loss_scaling && !(cp + cn > 0.0f)) {
-            const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
-            gcp += gz;
-            gcn += gz;
-        }
-        gb[0] = gcp;
-        gb[img] = gcn;
-        gb[2 * img] = gqp / dp;
-        gb[3 * img] = gqn / dn;
+// dL/d(images) at one pixel of one direction (loss/flow.py:219-261 differentiated): (d/dcnt+, d/dcnt-,
+// d/dts+, d/dts-) from the pixel's four IWE values, its sample's loss row (nz, loss_b) and the loss
+// gradient g.  Formed where it is gathered (k_iwe_bwd_band: at the events' warped corners), so no
+// per-pixel image-gradient pass and no buffer.
+__device__ inline float4 img_grad(const float* __restrict__ im, int64_t img, int64_t id, float g, float gS, float nz,
+                                  float lb, float T, bool loss_scaling) {
+    const float cp = im[id], cn = im[img + id], tp = im[2 * img + id], tn = im[3 * img + id];
+    const float dp = cp + 1e-9f, dn = cn + 1e-9f;
+    const float qp = tp / dp, qn = tn / dn;
+    const float Ap = qp / T, An = qn / T;
+    const float gqp = ((2.0f * Ap) * gS) / T, gqn = ((2.0f * An) * gS) / T;
+    float gcp = -gqp * (qp / dp), gcn = -gqn * (qn / dn);
+    if (loss_scaling && !(cp + cn > 0.0f)) {
+        const float gz = -(lb / nz) * g;  // d(sum/nz)/dnz on pixels the nonzero mask did not overwrite
+        gcp += gz;
+        gcn += gz;
     }
+    return make_float4(gcp, gcn, gqp / dp, gqn / dn);
 }
 
 // Eight lanes per event in the per-event backward (k_iwe_bwd_band), one per (direction d, corner q): the
@@ -733,7 +717,8 @@ __global__ __launch_bounds__(BIN_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int
 //    + 1), staged in LDS by coalesced loads) and the dt pairs (t-1, t), (t, t+1) (centres straight from
 //    memory; each pair's term is the one its other window computes, the same floats);
 //  * the events' part: each event of the band's bin (events binned by the band of their own pixel --
-//    the pixel their flow gradient lands in) gathers dL/d(images) at the 4 corners of both warps and
+//    the pixel their flow gradient lands in) forms dL/d(images) at the 4 corners of both warps from the
+//    IWE values there (img_grad) and
 //    chains them through the bilinear weights to its flow (eight lanes per event, kBwdLanes); the
 //    band's per-pixel sums of those are formed in LDS in exact two-word fixed point (integer adds: the
 //    sums do not depend on the order of the events; SplatLdsX's split).  No block reads an event
@@ -745,8 +730,7 @@ struct GevLds {
 };
 __host__ __device__ inline int gb_stage_floats(int W) { return 3 * (GB_BAND + 2 * W + 2); }
 
-__global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* g_loss,
-                                                        const float* __restrict__ gimg, float* g_flows,
+__global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* g_loss, float* g_flows,
                                                         const float4* __restrict__ rec4, const float* __restrict__ rec1,
                                                         const int* __restrict__ bins, int nbands, int has_events) {
     __shared__ GevLds acc;
@@ -846,7 +830,12 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
     }
     const int sub = tid & (kBwdLanes - 1), d = sub >> 2, qc = sub & 3;
     const float tref = d == 0 ? (float)a.T : 0.0f;
-    const float* gb = gimg + (int64_t)d * 4 * img + (int64_t)b * HWp;
+    const float* im = a.images + (int64_t)d * 4 * img + (int64_t)b * HWp;
+    const float gl = g_loss[0];
+    const float* ps = a.persample + ((int64_t)d * a.B + b) * 4;
+    const float nz = ps[2], lb = ps[3];
+    const float gS = a.loss_scaling ? gl / nz : gl;
+    const bool lsc = a.loss_scaling != 0;
     // every lane runs every round (the lane exchanges need the whole 8-lane group): a slot past the bin
     // contributes zeros
     for (int s0 = e0; s0 < e1; s0 += GB_NT / kBwdLanes) {
@@ -870,9 +859,8 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
             for (int k = 1; k < 4; ++k)
                 if (qc == k) cq = c[k];
             if (cq.inb) {
-                const int id = cq.idx;
-                const float gwt = (gb[id] * pm0 + gb[img + id] * pm1) +
-                                  (gb[2 * img + id] * (tsw * pm0) + gb[3 * img + id] * (tsw * pm1));
+                const float4 G = img_grad(im, img, cq.idx, gl, gS, nz, lb, (float)a.T, lsc);
+                const float gwt = (G.x * pm0 + G.y * pm1) + (G.z * (tsw * pm0) + G.w * (tsw * pm1));
                 // wt = ay * ax * mask: d/day = ax, d/dax = ay; ay = max(0, 1 - |dy|)
                 const float gay = gwt * cq.ax, gax = gwt * cq.ay;
                 gwy = -(gay * relu_tie(1.0f - fabsf(cq.dy))) * sgnf(cq.dy);
@@ -1049,13 +1037,11 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     return 0;
 }
 
-int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* gimg, float* g_flows, void* stream) {
+int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* g_flows, void* stream) {
     if (int rc = check_loss_args(a)) return rc;
-    if (!g_loss || !gimg || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
+    if (!g_loss || !g_flows) SNN_FAIL(SNNFLOW_E_ARG, "iwe_loss_bwd: missing buffer");
     const hipStream_t s = (hipStream_t)stream;
     const int64_t HWp = (int64_t)a->H * a->W;
-    const int chunks = loss_chunks(HWp);
-    hipLaunchKernelGGL(k_iwe_img_bwd, dim3(a->B * chunks), dim3(NT), 0, s, *a, g_loss, gimg, chunks);
     // the events binned by own-pixel band (tf == T: the forward's k_iwe_wbin formed these bins), then per
     // band: the smoothness gradient + the events' gradients summed per pixel in exact fixed point
     const int nbands = (int)((HWp + GB_BAND - 1) / GB_BAND);
@@ -1068,7 +1054,7 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     int* bins = reinterpret_cast<int*>(a->images + ls.gbins);
     if (a->M > 0 && a->tf != a->T)
         hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
-    hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), gb_lds, s, *a, g_loss, gimg, g_flows,
+    hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), gb_lds, s, *a, g_loss, g_flows,
                        rec4, rec1, bins, nbands, a->M > 0 ? 1 : 0);
     SNN_CHECK_LAUNCH();
     return 0;

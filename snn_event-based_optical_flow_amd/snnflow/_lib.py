@@ -308,7 +308,7 @@ EXPORTS = {
     "snnflow_convlif_param_grads": (I32, [P, P, P, I32, I32, P, P, P]),
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
-    "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P, P]),
+    "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P]),
     "snnflow_iwe_scratch_floats": (I64, [I32, I32, I32, I32, I32, I32]),
     "snnflow_iwe_acc_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),

@@ -86,11 +86,10 @@ class EventWarpingFn(torch.autograd.Function):
         a = _fill_args(ctx.meta, ctx.windows, flows_c, images, persample, smooth, loss, ctx.scr)
         g = g.contiguous().float()
         B, H, W = flows_c[0].shape[0], ctx.meta["H"], ctx.meta["W"]
-        gimg = torch.empty(8 * B * H * W, device=dev)
         g_flows = torch.empty(B, len(flows_c), 2, H, W, device=dev)
         # (the events binned by pixel band in the images scratch; per band the flow gradients summed per
         # pixel in fixed point: bit-reproducible g_flows)
-        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(gimg), ptr(g_flows), s)
+        _lib.call("iwe_loss_bwd", lib.snnflow_iwe_loss_bwd, ctypes.byref(a), ptr(g), ptr(g_flows), s)
         return (None, None, None, *g_flows.unbind(1))
 
 
