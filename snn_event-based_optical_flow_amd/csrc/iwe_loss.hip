@@ -132,7 +132,13 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 constexpr bool kSplatFixed = SNNFLOW_SPLAT_FIXED != 0;
 constexpr int SPLAT_NT = 1024, SB_BAND = 1024, WB_NT = 1024, WB_U = 2, kMaxSBands = 2048;  // H W <= 2^21 pixels
 // the loss backward's bins (k_iwe_bin / k_iwe_wbin, k_iwe_bwd_band): bands of GB_BAND pixels
-constexpr int GB_NT = 256, BIN_NT = 1024, GB_BAND = 512, kMaxBands = 4096;  // H W <= kMaxBands GB_BAND = 2^21 pixels
+#ifndef SNNFLOW_GB_BAND
+#define SNNFLOW_GB_BAND 512
+#endif
+#ifndef SNNFLOW_GB_NT
+#define SNNFLOW_GB_NT 256
+#endif
+constexpr int GB_NT = SNNFLOW_GB_NT, BIN_NT = 1024, GB_BAND = SNNFLOW_GB_BAND, kMaxBands = (1 << 21) / GB_BAND;  // H W <= 2^21 pixels
 
 struct SplatLdsF {  // fp32 images
     float v[4][SB_BAND];
