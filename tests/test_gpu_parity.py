@@ -860,11 +860,14 @@ def test_clip_grad_norm_flat_vs_torch(dev, scale):
         np.testing.assert_allclose(p.grad.cpu().numpy(), q.grad.numpy(), rtol=1e-5, atol=1e-8)
 
 
-@pytest.mark.parametrize("H,W,Ns", [(256, 256, (3000, 2500, 3000)), (100, 130, (700, 0, 500))])
+@pytest.mark.parametrize("H,W,Ns", [(256, 256, (3000, 2500, 3000)), (100, 130, (700, 0, 500)),
+                                    (48, 640, (800, 600))])
 def test_event_warping_bands_and_empty_windows_vs_oracle(dev, H, W, Ns):
-    """The LDS-privatised IWE splat at 256x256 (16 bands of 4096 pixels), a ragged image
-    (100x130: partial last band and pixel chunk) and an empty event window (N_k = 0) against
-    the CPU oracle: loss rtol 2e-5, per-window flow gradients relative-L2 1e-4."""
+    """The binned IWE splat and the banded backward at 256x256 (64 splat bands of 1024 pixels), a
+    ragged image (100x130: partial last band and pixel chunk), an empty event window (N_k = 0) and a
+    wide image (48x640: warps up to +-16 pixels, corners in a neighbouring band, the backward's LDS
+    neighbourhood of 2 W + 2 extra pixels) against the CPU oracle: loss rtol 2e-5, per-window flow
+    gradients relative-L2 1e-4."""
     import snnflow
     from oracle import iwe_ref
     from snnflow.synthetic import make_window
