@@ -385,9 +385,7 @@ typedef struct snnflow_iwe_loss_args {
                                    then the events binned by warped band (forward) and by own-pixel
                                    band (backward) -- ABI 38; kept from the forward to the backward */
     double* acc;                /* scratch snnflow_iwe_acc_doubles(B, H, W, tf): per-block partial
-                                   sums, reduced in a fixed order (deterministic loss), then a
-                                   completion counter: zero it once before the first call (ABI 38;
-                                   every call leaves it zero) */
+                                   sums, reduced in a fixed order (deterministic loss) */
     float* persample;           /* scratch [2 dir][B][4]: S+, S-, nz, loss_b          */
     float* smooth;              /* scratch [8]                                         */
     float* loss;                /* out [1]                                             */

@@ -460,74 +460,6 @@ __host__ __device__ inline int loss_tsplit(int B, int64_t HWp, int tf) {
     return s < 1 ? 1 : (s > tf ? tf : (int)s);
 }
 
-// Fixed-order fp64 reduction of the partial rows, then loss = sum_b (S+ + S-)_fw / nz_fw
-// + ... (loss/flow.py:219-261) + weight * smoothness.  Run by the last block of k_iwe_loss to finish:
-// wave w reduces the rows of samples w, w + NW, ... (all 11 columns; a sample's rows in one wave, in
-// lane order: the same sums whatever the block size), then the smoothness sums add up over samples.
-template <int NTH>
-__device__ void iwe_finalize(const snnflow_iwe_loss_args& a, int rows_b) {
-    __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
-    __shared__ double smp[64][5];          // per-sample smoothness sums
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int b = wv; b < a.B; b += NTH / 64) {
-        double s[LOSS_NV];
-#pragma unroll
-        for (int j = 0; j < LOSS_NV; ++j) s[j] = 0.0;
-        const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
-#pragma unroll 4
-        for (int c = lane; c < rows_b; c += 64) {
-#pragma unroll
-            for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
-        }
-#pragma unroll
-        for (int j = 0; j < LOSS_NV; ++j) {
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) s[j] += __shfl_xor(s[j], off, 64);
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < 6; ++j) outv[6 * b + j] = s[j];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) smp[b][j] = s[6 + j];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 5) {
-        double t = 0.0;
-        for (int b = 0; b < a.B; ++b) t += smp[b][threadIdx.x];
-        outv[6 * a.B + threadIdx.x] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    float total = 0.0f;
-    for (int d = 0; d < 2; ++d) {
-        float dir = 0.0f;
-        for (int bb = 0; bb < a.B; ++bb) {
-            const float sp = (float)outv[6 * bb + 3 * d], sn = (float)outv[6 * bb + 3 * d + 1];
-            const float nz = (float)outv[6 * bb + 3 * d + 2];
-            float lb = sp + sn;
-            if (a.loss_scaling) lb = lb / nz;
-            float* ps = a.persample + ((int64_t)d * a.B + bb) * 4;
-            ps[0] = sp; ps[1] = sn; ps[2] = nz; ps[3] = lb;
-            dir += lb;
-        }
-        total += dir;
-    }
-    const int comps = a.overwrite_intermediate ? 4 : 5;
-    float sm = (float)outv[6 * a.B + 0];
-    for (int j = 1; j < comps; ++j) sm += (float)outv[6 * a.B + j];
-    sm = sm / (float)comps / (float)a.tf;
-    for (int j = 0; j < 5; ++j) a.smooth[j] = (float)outv[6 * a.B + j];
-    a.smooth[5] = sm;
-    a.loss[0] = total + a.weight * sm;
-}
-
-// The loss rows' completion counter: one 32-bit word in the double after the rows (zeroed by the caller
-// once, reset by the block that finishes).
-__device__ inline unsigned int* loss_done_counter(const snnflow_iwe_loss_args& a, int nrows) {
-    return reinterpret_cast<unsigned int*>(a.acc + (int64_t)nrows * LOSS_NV);
-}
-
 __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int chunks, int tsplit) {
     __shared__ float red[NT / 64][LOSS_NV];
     const int blk = xcd_block();
@@ -622,30 +554,76 @@ __global__ __launch_bounds__(NT) void k_iwe_loss(snnflow_iwe_loss_args a, int ch
         if (lane == 0) red[wv][j] = s;
     }
     __syncthreads();
-    // wave 0 writes the block's row, fences it device-wide and counts the block as done (one wave per
-    // block: a fence is an L2 write-back); the last block to finish fences again (acquire) and reduces
-    // every row in a fixed order (iwe_finalize) -- no separate launch
-    __shared__ int last;
-    if (tid < 64) {
-        if (tid < LOSS_NV) {
-            double s = 0.0;
+    if (tid < LOSS_NV) {
+        double s = 0.0;
 #pragma unroll
-            for (int w2 = 0; w2 < NT / 64; ++w2) s += (double)red[w2][tid];
-            a.acc[(int64_t)blk * LOSS_NV + tid] = s;
+        for (int w2 = 0; w2 < NT / 64; ++w2) s += (double)red[w2][tid];
+        a.acc[(int64_t)blk * LOSS_NV + tid] = s;
+    }
+}
+
+// Fixed-order fp64 reduction of the partial rows, then loss = sum_b (S+ + S-)_fw / nz_fw
+// + ... (loss/flow.py:219-261) + weight * smoothness.  One block: wave w reduces the rows
+// of samples w, w + 16, ... (all 11 columns), then the smoothness sums add up over samples.
+constexpr int FIN_NT = 1024;
+
+__global__ __launch_bounds__(FIN_NT) void k_iwe_finalize(snnflow_iwe_loss_args a, int rows_b) {
+    __shared__ double outv[6 * 64 + 5];    // B <= 64 (checked by the host)
+    __shared__ double smp[64][5];          // per-sample smoothness sums
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // wave w reduces samples w, w + 16, ...: lane-strided rows, all 11 columns at once
+    for (int b = wv; b < a.B; b += FIN_NT / 64) {
+        double s[LOSS_NV];
+#pragma unroll
+        for (int j = 0; j < LOSS_NV; ++j) s[j] = 0.0;
+        const double* r = a.acc + (int64_t)b * rows_b * LOSS_NV;
+#pragma unroll 4
+        for (int c = lane; c < rows_b; c += 64) {
+#pragma unroll
+            for (int j = 0; j < LOSS_NV; ++j) s[j] += r[(int64_t)c * LOSS_NV + j];
         }
-        __threadfence();
-        if (tid == 0) {
-            const unsigned int done = atomicAdd(loss_done_counter(a, (int)gridDim.x), 1u);
-            last = done == gridDim.x - 1;
-            if (last) __threadfence();
+#pragma unroll
+        for (int j = 0; j < LOSS_NV; ++j) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) s[j] += __shfl_xor(s[j], off, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int j = 0; j < 6; ++j) outv[6 * b + j] = s[j];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) smp[b][j] = s[6 + j];
         }
     }
     __syncthreads();
-    if (!last) return;
-    iwe_finalize<NT>(a, chunks * tsplit);
-    if (tid == 0) *loss_done_counter(a, (int)gridDim.x) = 0u;
+    if (threadIdx.x < 5) {
+        double t = 0.0;
+        for (int b = 0; b < a.B; ++b) t += smp[b][threadIdx.x];
+        outv[6 * a.B + threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    float total = 0.0f;
+    for (int d = 0; d < 2; ++d) {
+        float dir = 0.0f;
+        for (int bb = 0; bb < a.B; ++bb) {
+            const float sp = (float)outv[6 * bb + 3 * d], sn = (float)outv[6 * bb + 3 * d + 1];
+            const float nz = (float)outv[6 * bb + 3 * d + 2];
+            float lb = sp + sn;
+            if (a.loss_scaling) lb = lb / nz;
+            float* ps = a.persample + ((int64_t)d * a.B + bb) * 4;
+            ps[0] = sp; ps[1] = sn; ps[2] = nz; ps[3] = lb;
+            dir += lb;
+        }
+        total += dir;
+    }
+    const int comps = a.overwrite_intermediate ? 4 : 5;
+    float sm = (float)outv[6 * a.B + 0];
+    for (int j = 1; j < comps; ++j) sm += (float)outv[6 * a.B + j];
+    sm = sm / (float)comps / (float)a.tf;
+    for (int j = 0; j < 5; ++j) a.smooth[j] = (float)outv[6 * a.B + j];
+    a.smooth[5] = sm;
+    a.loss[0] = total + a.weight * sm;
 }
-
 
 // dL/d(images) at one pixel of one direction (loss/flow.py:219-261 differentiated): (d/dcnt+, d/dcnt-,
 // d/dts+, d/dts-) from the pixel's four IWE values, its sample's loss row (nz, loss_b) and the loss
@@ -1041,7 +1019,7 @@ int64_t snnflow_iwe_scratch_floats(int B, int M, int T, int tf, int H, int W) {
 
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
     const int64_t HWp = (int64_t)H * W;
-    return (int)((int64_t)B * loss_tsplit(B, HWp, tf) * loss_chunks(HWp) * LOSS_NV + 1);  // + the completion counter
+    return (int)((int64_t)B * loss_tsplit(B, HWp, tf) * loss_chunks(HWp) * LOSS_NV);
 }
 
 int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
@@ -1060,6 +1038,7 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands), dim3(SPLAT_NT), 0, s, *a, nbands, rec, bins);
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
     hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit);
+    hipLaunchKernelGGL(k_iwe_finalize, dim3(1), dim3(FIN_NT), 0, s, *a, tsplit * chunks);
     SNN_CHECK_LAUNCH();
     return 0;
 }

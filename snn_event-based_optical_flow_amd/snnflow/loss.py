@@ -26,8 +26,7 @@ class _Scratch:
     def get(self, B, H, W, tf, device):
         key = (B, H, W, tf, device)
         if self.key != key:
-            # (zeroed once: its last word is the loss rows' completion counter, which the kernel resets)
-            self.acc = torch.zeros(lib.snnflow_iwe_acc_doubles(B, H, W, tf), dtype=torch.float64, device=device)
+            self.acc = torch.empty(lib.snnflow_iwe_acc_doubles(B, H, W, tf), dtype=torch.float64, device=device)
             self.dummy = torch.zeros(8, device=device)  # pointer for empty event windows (never read)
             self.key = key
         return self
