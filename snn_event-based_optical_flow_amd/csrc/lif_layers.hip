@@ -3968,8 +3968,8 @@ static int slot_top_blocks(int c, int B, int H, int W) {
     return (int)((npix + ppb * items - 1) / (ppb * items));
 }
 
-// Tiles per block of the C = 8 tile pipelines (0: the one-tile-per-block bodies).  Defaults from
-// SNNFLOW_PIPE_FWD / SNNFLOW_PIPE_BWD at load time; snnflow_set_pipe overrides (A/B, tests).
+// Tiles per block of the C = 8 forward tile pipeline (0: the one-tile-per-block body).  Default from
+// SNNFLOW_PIPE_FWD at load time; snnflow_set_pipe overrides (A/B, tests).
 static int env_int(const char* name, int dflt) {
     const char* v = getenv(name);
     return v && *v ? atoi(v) : dflt;
