@@ -129,9 +129,6 @@ __device__ inline const float* mask_of(const snnflow_iwe_loss_args& a, int b, in
 #ifndef SNNFLOW_SPLAT_FIXED
 #define SNNFLOW_SPLAT_FIXED 1
 #endif
-#ifndef SNNFLOW_FAST_PG
-#define SNNFLOW_FAST_PG 0
-#endif
 constexpr bool kSplatFixed = SNNFLOW_SPLAT_FIXED != 0;
 constexpr int SPLAT_NT = 1024, SB_BAND = 1024, WB_NT = 1024, WB_U = 2, kMaxSBands = 2048;  // H W <= 2^21 pixels
 // the loss backward's bins (k_iwe_bin / k_iwe_wbin, k_iwe_bwd_band): bands of GB_BAND pixels
@@ -737,13 +734,7 @@ __global__ __launch_bounds__(BIN_NT) void k_iwe_bin(snnflow_iwe_loss_args a, int
 struct GevLds {
     unsigned long long hi[2][GB_BAND], lo[2][GB_BAND];
 };
-// SNNFLOW_PG_SHARE: each neighbour pair's term computed once per block (F_r, F_d, F_dr, F_ur of the pairs
-// (q, q+1), (q, q+W), (q, q+W+1), (q, q-W+1) in LDS, the 8 terms of a pixel gathered from them in the
-// same order: the same floats), instead of twice (once by each pixel of the pair).
-#ifndef SNNFLOW_PG_SHARE
-#define SNNFLOW_PG_SHARE 0
-#endif
-__host__ __device__ inline int gb_stage_floats(int W) { return (SNNFLOW_PG_SHARE ? 7 : 3) * (GB_BAND + 2 * W + 2); }
+__host__ __device__ inline int gb_stage_floats(int W) { return 3 * (GB_BAND + 2 * W + 2); }
 
 __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a, const float* g_loss, float* g_flows,
                                                         const float4* __restrict__ rec4, const float* __restrict__ rec1,
@@ -815,35 +806,12 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
         // d(term)/d(flow of 'a') for the pair ('a', 'b'); 'b' receives the negative
         auto pg = [&](float ax, float ay, float am, float bx, float by, float bm) {
             const float dd = (ax - bx) + (ay - by);
-            const float mk = sm ? am * bm : 1.0f;
-#if SNNFLOW_FAST_PG  // timing attribution only (approximate sqrt / division; results differ in the last bits)
-            const float c = __builtin_amdgcn_sqrtf(dd * dd + 1e-6f);
-            return ((mk * gsm) * __builtin_amdgcn_rcpf(2.0f * c)) * (2.0f * dd);
-#else
             const float c = charb(dd);
+            const float mk = sm ? am * bm : 1.0f;
             return ((mk * gsm) / (2.0f * c)) * (2.0f * dd);
-#endif
         };
         const int Wd = a.W;
         const int off[8] = {1, -1, Wd, -Wd, Wd + 1, -Wd - 1, -Wd + 1, Wd - 1};
-#if SNNFLOW_PG_SHARE
-        // the forward pairs' terms over the staged range (index e = pixel - lo): F_r for pixels
-        // [p0 - 1, p0 + B), F_d [p0 - W, p0 + B), F_dr [p0 - W - 1, p0 + B), F_ur [p0, p0 + B + W - 1)
-        float* const Fr = nbs + 3 * S;
-        float* const Fd = Fr + S;
-        float* const Fdr = Fd + S;
-        float* const Fur = Fdr + S;
-        for (int e = tid; e < S; e += GB_NT) {
-            const int q = lo + e;
-            const float ax = sx[e], ay = sy[e], am = smk[e];
-            if (q >= p0 - 1 && q < p0 + GB_BAND && e + 1 < S) Fr[e] = pg(ax, ay, am, sx[e + 1], sy[e + 1], smk[e + 1]);
-            if (q >= p0 - Wd && q < p0 + GB_BAND && e + Wd < S) Fd[e] = pg(ax, ay, am, sx[e + Wd], sy[e + Wd], smk[e + Wd]);
-            if (e + Wd + 1 < S && q < p0 + GB_BAND) Fdr[e] = pg(ax, ay, am, sx[e + Wd + 1], sy[e + Wd + 1], smk[e + Wd + 1]);
-            if (q >= p0 && q < p0 + GB_BAND + Wd - 1 && e - Wd + 1 >= 0)
-                Fur[e] = pg(ax, ay, am, sx[e - Wd + 1], sy[e - Wd + 1], smk[e - Wd + 1]);
-        }
-        __syncthreads();
-#endif
 #pragma unroll
         for (int k = 0; k < PPT; ++k) {
             const int j = tid + k * GB_NT;
@@ -854,18 +822,6 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
             const int c0 = p - lo;
             const float cx = sx[c0], cy = sy[c0], cm = smk[c0];
             float v = 0.0f;
-#if SNNFLOW_PG_SHARE
-            // right +F_r[p], left -F_r[p-1], down +F_d[p], up -F_d[p-W], down-right +F_dr[p],
-            // up-left -F_dr[p-W-1], up-right +F_ur[p], down-left -F_ur[p+W-1]
-            if (ok[0]) v += Fr[c0];
-            if (ok[1]) v -= Fr[c0 - 1];
-            if (ok[2]) v += Fd[c0];
-            if (ok[3]) v -= Fd[c0 - Wd];
-            if (ok[4]) v += Fdr[c0];
-            if (ok[5]) v -= Fdr[c0 - Wd - 1];
-            if (ok[6]) v += Fur[c0];
-            if (ok[7]) v -= Fur[c0 + Wd - 1];
-#else
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 if (!ok[q]) continue;
@@ -873,7 +829,6 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
                 if (q % 2 == 0) v += pg(cx, cy, cm, sx[e], sy[e], smk[e]);
                 else v -= pg(sx[e], sy[e], smk[e], cx, cy, cm);
             }
-#endif
             if (t + 1 < a.tf && dt_terms) v += pg(cx, cy, cm, nx_[k], ny_[k], nm_[k]);
             if (dt_terms && t >= 1) v -= pg(px_[k], py_[k], pm_[k], cx, cy, cm);
             smooth[k] = v;
