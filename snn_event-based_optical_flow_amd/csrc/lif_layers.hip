@@ -2283,9 +2283,7 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
         }
         __syncthreads();
         if constexpr (PF) {
-        if constexpr (PF) {
             if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
-        }
         }
 
         // compute: this wave's tile rows r = rg, rg + RG, ...
