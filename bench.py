@@ -289,8 +289,11 @@ def main():
         sync_grads()
         update()
 
-    # warmup (eager; builds workspaces, optimizer state, persistent state buffers)
-    s_side = torch.cuda.Stream(dev)
+    # warmup (eager; builds workspaces, optimizer state, persistent state buffers).  Before a graph
+    # capture it runs on a side stream; the eager loop warms up on the stream it is timed on (autograd's
+    # AccumulateGrad nodes keep the stream they were created on: a side-stream warmup would put a
+    # cross-stream wait behind every parameter's gradient in each timed backward)
+    s_side = torch.cuda.Stream(dev) if not args.no_graph else torch.cuda.current_stream(dev)
     s_side.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s_side):
         for i in range(max(args.warmup, 3)):

@@ -466,10 +466,16 @@ def ptr(t):
     return t.data_ptr()
 
 
+_HIP_SEEN = False  # a HIP device was visible once (torch.cuda.is_available() costs ~3 us a call)
+
+
 def stream_ptr(device=None):
     """Raw HIP stream of the current stream on `device` (torch's getter without the Stream object)."""
-    if not torch.cuda.is_available():
-        raise SnnflowError("snnflow kernels need a HIP device (none visible); there is no CPU fallback")
+    global _HIP_SEEN
+    if not _HIP_SEEN:
+        if not torch.cuda.is_available():
+            raise SnnflowError("snnflow kernels need a HIP device (none visible); there is no CPU fallback")
+        _HIP_SEEN = True
     if isinstance(device, str):
         device = torch.device(device)
     idx = device.index if isinstance(device, torch.device) else device

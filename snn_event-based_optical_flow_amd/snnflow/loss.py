@@ -62,9 +62,20 @@ class EventWarpingFn(torch.autograd.Function):
         if len(evs) > _lib.MAX_WINDOWS:
             raise _lib.SnnflowError(f"EventWarping: at most {_lib.MAX_WINDOWS} windows per loss")
         flows_c = [f.float().contiguous() for f in flows]  # [B, 2, H, W] each, no copy when already so
+        B, H, W = evs[0].shape[0], meta["H"], meta["W"]
+        # the kernels index every tensor by (B, H, W): a mis-shaped one would be read out of bounds
         for f in flows_c:
             _lib.require_device(f, "flow")
-        B, H, W = evs[0].shape[0], meta["H"], meta["W"]
+            if tuple(f.shape) != (B, 2, H, W):
+                raise _lib.SnnflowError(f"EventWarping: flow of shape {tuple(f.shape)}, expected {(B, 2, H, W)} "
+                                        "(event_flow_association takes a list of flow maps)")
+        for e, p in zip(evs, windows[1]):
+            if e.dim() != 3 or e.shape[0] != B or e.shape[2] != 4 or tuple(p.shape) != (B, e.shape[1], 2):
+                raise _lib.SnnflowError(f"EventWarping: events {tuple(e.shape)} / polarity masks {tuple(p.shape)}, "
+                                        f"expected [{B}, N, 4] / [{B}, N, 2]")
+        for m in windows[2]:
+            if tuple(m.shape) != (B, 1, H, W):
+                raise _lib.SnnflowError(f"EventWarping: mask of shape {tuple(m.shape)}, expected {(B, 1, H, W)}")
         scr = scr.get(B, H, W, len(flows_c), dev)
         images = torch.empty(lib.snnflow_iwe_scratch_floats(B, meta["off"][-1], meta["T"], len(flows_c), H, W), device=dev)
         persample = torch.empty(2 * B * 4, device=dev)

@@ -1720,3 +1720,35 @@ def test_per_step_chain_backward_batched(dev, case):
             worst = max(worst, e)
             assert e <= 1e-5, (case, n, e)
     print(f"\n[{case}] batched chain backward vs per-node: worst gradient rel-L2 {worst:.2e}")
+
+
+def test_iwe_loss_rejects_misshaped_inputs(dev):
+    """EventWarping validates what its kernels index by (B, H, W): a flow tensor passed where the
+    reference takes a list of flow maps (``list(tensor)`` splits it into per-sample [2, H, W] maps),
+    events / polarity masks of another batch, a mask of another resolution -- each raises instead of
+    being read out of bounds."""
+    import snnflow
+    from snnflow import _lib
+
+    H, W, B, N = 32, 32, 2, 100
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    gen = torch.Generator().manual_seed(5)
+    ev = torch.stack([torch.rand(B, N, generator=gen), torch.randint(0, H, (B, N), generator=gen).float(),
+                      torch.randint(0, W, (B, N), generator=gen).float(), torch.ones(B, N)], dim=2).to(dev)
+    pol = torch.stack([torch.ones(B, N), torch.zeros(B, N)], dim=2).to(dev)
+    mask = torch.ones(B, 1, H, W, device=dev)
+    flow = torch.zeros(B, 2, H, W, device=dev, requires_grad=True)
+    cases = [(flow, ev, pol, mask),                                 # bare tensor: B maps of [2, H, W]
+             ([flow], ev[:1], pol[:1], mask),                       # events of another batch
+             ([flow], ev, pol[:, :, :1], mask),                     # one polarity column
+             ([flow], ev, pol, torch.ones(B, 1, H, 2 * W, device=dev))]  # mask of another resolution
+    for fl, e, p, m in cases:
+        lf = snnflow.EventWarping(cfg, dev)
+        lf.event_flow_association(fl, e, p, m)
+        with pytest.raises(_lib.SnnflowError):
+            lf()
+    lf = snnflow.EventWarping(cfg, dev)  # and the well-formed call still runs
+    lf.event_flow_association([flow], ev, pol, mask)
+    lf().backward()
+    assert flow.grad is not None and bool(torch.isfinite(flow.grad).all())
