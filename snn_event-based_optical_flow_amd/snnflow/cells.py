@@ -82,10 +82,10 @@ def _check_supported(kernel_size, stride, quantization_config, tebn, mpbn, norm,
         raise NotImplementedError("snnflow cells implement the reference's 3x3 / stride-1 convolutions")
     if quantization_config is not None and quantization_config.get("enabled", False):
         raise NotImplementedError("quantized (brevitas) cells are out of scope (DESIGN.md)")
-    if norm is not None:
-        raise NotImplementedError("norm='weight'/'group' variants are not implemented")
-    if not detach and mpbn:
-        raise NotImplementedError("detach=False together with MPBN is not implemented")
+    if norm not in (None, "weight"):
+        # GroupNorm of the conv inputs (:277-279 / :506-509) would feed non-spike values into the
+        # recurrent conv, whose kernels take spikes (0/1) there
+        raise NotImplementedError("norm='group' is not implemented (norm=None and norm='weight' are)")
 
 
 class _SnnTorchCellBase(nn.Module):
@@ -117,6 +117,23 @@ class _SnnTorchCellBase(nn.Module):
         self.mpbn_enabled = bool(mpbn)
         self.detach = bool(detach)
         self.exporting = False
+        # norm="weight" (:274-276 / :500-504): nn.utils.weight_norm on the convolutions, as the reference
+        # applies it (state-dict keys ff.weight_g / ff.weight_v); the effective weight g v / ||v|| is
+        # formed per call (_params) and the cell kernels run on it, autograd taking its gradient to g, v
+        self.weight_norm = False
+
+    def _apply_weight_norm(self):
+        import warnings
+        with warnings.catch_warnings():  # (torch deprecates the hook-based form; its keys are the reference's)
+            warnings.simplefilter("ignore", FutureWarning)
+            self.ff = nn.utils.weight_norm(self.ff)
+            if self.recurrent:
+                self.rec = nn.utils.weight_norm(self.rec)
+        self.weight_norm = True
+
+    @staticmethod
+    def _conv_weight(conv, normed):
+        return torch._weight_norm(conv.weight_v, conv.weight_g, 0) if normed else conv.weight
 
     @property
     def batch_norm(self):
@@ -139,9 +156,9 @@ class _SnnTorchCellBase(nn.Module):
         return spk, state
 
     def _params(self, timestep=None):
-        ps = [self.ff.weight]
+        ps = [self._conv_weight(self.ff, self.weight_norm)]
         if self.recurrent:
-            ps.append(self.rec.weight)
+            ps.append(self._conv_weight(self.rec, self.weight_norm))
         if self.tebn_enabled:  # BN(x) * p_t == BN with (weight * p_t, bias * p_t)
             bw, bb = self.bn.affine(timestep)
         else:
@@ -162,6 +179,8 @@ class SNNtorch_ConvLIF(_SnnTorchCellBase):
         _check_supported(kernel_size, stride, quantization_config, tebn, mpbn, norm, detach, activation)
         self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset, stride,
                     tebn, num_timesteps, mpbn, detach)
+        if norm == "weight":
+            self._apply_weight_norm()
 
 
 class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
@@ -179,6 +198,8 @@ class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
             raise NotImplementedError("recurrent cells with input_size != hidden_size are not compiled")
         self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset,
                     1, tebn, num_timesteps, mpbn, detach)
+        if norm == "weight":
+            self._apply_weight_norm()
 
 
 class ConvLayer(nn.Module):
@@ -253,8 +274,8 @@ class CellFn(torch.autograd.Function):
         dev = x.device
         s = _lib.stream_ptr(dev)
         _lib.call("threshold clamp", lib.snnflow_prep_weights, None, C, 1, None, None, ptr(cell.lif.threshold), s)
-        wff = _prep(cell.ff.weight, s)
-        wrec = _prep(cell.rec.weight, s) if cell.recurrent else (None, None)
+        wff = _prep(params[0], s)  # the conv weights as passed (weight norm: the effective g v / ||v||)
+        wrec = _prep(params[1], s) if cell.recurrent else (None, None)
         ws = _cell_ws(B, H, W, C, dev)
         if prev_state is None:
             cache = cell.lif.mem
@@ -363,11 +384,11 @@ class CellFn(torch.autograd.Function):
         st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
         st.s_prev = _ptr_t(sp) if cell.recurrent else None
         _lib.call("wgrad", lib.snnflow_wgrad, ctypes.byref(wa), s)
-        g_wff = torch.empty_like(cell.ff.weight)
+        g_wff = torch.empty(cell.hidden_size, cin, 3, 3, device=dev)
         descs = [_lib.SlabDesc(ptr(slab_ff), ptr(g_wff), g_wff.numel())]
         g_wrec = None
         if cell.recurrent:
-            g_wrec = torch.empty_like(cell.rec.weight)
+            g_wrec = torch.empty(C, C, 3, 3, device=dev)
             descs.append(_lib.SlabDesc(ptr(slab_rec), ptr(g_wrec), g_wrec.numel()))
         arr = (_lib.SlabDesc * len(descs))(*descs)
         _lib.call("slab_reduce", lib.snnflow_slab_reduce, arr, len(descs), ws.nblk, s)

@@ -158,8 +158,10 @@ class _FireNetBase(BaseModel):
 
     def _cellwise(self):
         """Cells called one by one (each an autograd node on the HIP cell kernels): forward hooks
-        registered, or TEBN / MPBN cells (their extra normalisation sits between the fused kernels)."""
-        return self._hooked() or any(c.tebn_enabled or c.mpbn_enabled for c in self._mods()[:-1])
+        registered, TEBN / MPBN cells (their extra normalisation sits between the fused kernels), or
+        weight-normalised convolutions (the effective weights are formed per call)."""
+        return self._hooked() or any(c.tebn_enabled or c.mpbn_enabled or getattr(c, "weight_norm", False)
+                                     for c in self._mods()[:-1])
 
     def _input(self, event_voxel, event_cnt):
         if self.encoding == "voxel":

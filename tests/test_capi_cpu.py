@@ -311,3 +311,27 @@ def test_clip_adam_state_dict_loads_into_torch_adam():
     m = opt2._state(params)
     assert float(m[3]) == 5.0
     assert torch.equal(m[1][:12], topt.state[twin[0]]["exp_avg"].reshape(-1))
+
+
+def test_cell_constructor_options():
+    """SNNtorch_ConvLIF(Recurrent) constructor options (SNNtorch_spiking_submodules.py:124-567):
+    norm="weight" registers nn.utils.weight_norm's weight_g / weight_v (the reference's state-dict
+    keys) and the cell's conv weights are the effective g v / ||v||; detach=False with MPBN builds;
+    norm="group" and stride 2 raise NotImplementedError (not silently ignored)."""
+    import torch
+
+    import snnflow
+
+    for cls in (snnflow.SNNtorch_ConvLIF, snnflow.SNNtorch_ConvLIFRecurrent):
+        c = cls(8, 8, 3, norm="weight")
+        keys = set(c.state_dict())
+        assert {"ff.weight_g", "ff.weight_v"} <= keys and "ff.weight" not in keys
+        assert (("rec.weight_g" in keys) == cls.recurrent)
+        w = c._params()[0]
+        assert torch.allclose(w, torch._weight_norm(c.ff.weight_v, c.ff.weight_g, 0))
+        assert w.requires_grad  # the gradient reaches weight_g / weight_v through the reparametrisation
+        cls(8, 8, 3, detach=False, mpbn=True)
+        with pytest.raises(NotImplementedError):
+            cls(8, 8, 3, norm="group")
+    with pytest.raises(NotImplementedError):
+        snnflow.SNNtorch_ConvLIF(8, 8, 3, stride=2)

@@ -1235,22 +1235,24 @@ def test_subtract_reset_cell_vs_oracle(dev, recurrent):
                                                    for n, a in cell.named_parameters()], ORACLE_GRAD_TOL)
 
 
-@pytest.mark.parametrize("recurrent,hard", [(False, True), (True, True), (False, False), (True, False)])
-def test_detach_false_cell_vs_oracle(dev, recurrent, hard):
+@pytest.mark.parametrize("recurrent,hard,mpbn", [(False, True, False), (True, True, False), (False, False, False),
+                                                (True, False, False), (False, True, True), (True, True, True)])
+def test_detach_false_cell_vs_oracle(dev, recurrent, hard, mpbn):
     """SNNtorch_ConvLIF(Recurrent)(detach=False) (SNNtorch_spiking_submodules.py:309-311: the
     membrane output keeps its graph, BPTT through the membrane): 4 calls, the first two chained
     through prev_state, the third with prev_state=None (snn.Leaky continues from its non-detached
     membrane cache), the fourth chained again; the loss uses spikes AND final membranes, so the
-    membrane-output gradient path (mem_grad_in) and its threshold part are exercised.  Every
-    parameter gradient and the input gradients against SnnTorchCellRef."""
+    membrane-output gradient path (mem_grad_in) and its threshold part are exercised.  With ``mpbn``
+    the state's membrane is MPBN(mem_out) (:313-317), whose gradient reaches the LIF through the
+    non-detached membrane.  Every parameter gradient and the input gradients against SnnTorchCellRef."""
     import snnflow
     from oracle import lif_ref
 
     torch.manual_seed(41)
     C, B, H, W = 8, 2, 24, 40
     cls = snnflow.SNNtorch_ConvLIFRecurrent if recurrent else snnflow.SNNtorch_ConvLIF
-    cell = cls(C, C, 3, hard_reset=hard, detach=False, thresh=(0.2, 0.4)).to(dev).train()
-    ref = lif_ref.SnnTorchCellRef(C, C, 3, recurrent=recurrent, hard_reset=hard, detach=False).train()
+    cell = cls(C, C, 3, hard_reset=hard, detach=False, thresh=(0.2, 0.4), mpbn=mpbn).to(dev).train()
+    ref = lif_ref.SnnTorchCellRef(C, C, 3, recurrent=recurrent, hard_reset=hard, detach=False, mpbn=mpbn).train()
     ref.load_state_dict({k: v.detach().cpu() for k, v in cell.state_dict().items()}, strict=False)
     gen = torch.Generator().manual_seed(43)
     xs = [(torch.rand(B, C, H, W, generator=gen) * 2.0).requires_grad_(True) for _ in range(4)]
@@ -1752,3 +1754,75 @@ def test_iwe_loss_rejects_misshaped_inputs(dev):
     lf.event_flow_association([flow], ev, pol, mask)
     lf().backward()
     assert flow.grad is not None and bool(torch.isfinite(flow.grad).all())
+
+
+@pytest.mark.parametrize("recurrent", [False, True])
+def test_weight_norm_cell_vs_oracle(dev, recurrent):
+    """SNNtorch_ConvLIF(Recurrent)(norm="weight") (SNNtorch_spiking_submodules.py:274-276 / :500-504:
+    nn.utils.weight_norm on ff (and rec), parameters weight_g / weight_v): 3 chained calls against
+    SnnTorchCellRef running on the effective weights g v / ||v||; spikes and states match, and the
+    weight_g / weight_v gradients equal the reference's weight gradient taken through the same
+    reparametrisation (torch._weight_norm on the CPU, the checker side); an optimizer-style in-place
+    update of weight_v between calls is seen by the next call."""
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(47)
+    C, B, H, W = 8, 2, 24, 40
+    cls = snnflow.SNNtorch_ConvLIFRecurrent if recurrent else snnflow.SNNtorch_ConvLIF
+    cell = cls(C, C, 3, thresh=(0.2, 0.4), norm="weight").to(dev).train()
+    keys = set(cell.state_dict())
+    assert {"ff.weight_g", "ff.weight_v"} <= keys and "ff.weight" not in keys
+    if recurrent:
+        assert {"rec.weight_g", "rec.weight_v"} <= keys
+    with torch.no_grad():
+        cell.ff.weight_v.mul_(1.3)  # moves ||v|| away from g: the normalisation is not the identity
+        cell.ff.weight_g.mul_(0.9)
+    convs = ["ff"] + (["rec"] if recurrent else [])
+    gv = {c: (getattr(cell, c).weight_g.detach().cpu().clone().requires_grad_(True),
+              getattr(cell, c).weight_v.detach().cpu().clone().requires_grad_(True)) for c in convs}
+    ref = lif_ref.SnnTorchCellRef(C, C, 3, recurrent=recurrent).train()
+    sd = {k: v.detach().cpu() for k, v in cell.state_dict().items() if "weight_g" not in k and "weight_v" not in k}
+    ref.load_state_dict(sd, strict=False)
+    eff = {c: torch._weight_norm(gv[c][1], gv[c][0], 0) for c in convs}
+    with torch.no_grad():
+        for c in convs:
+            getattr(ref, c).weight.copy_(eff[c])
+    gen = torch.Generator().manual_seed(53)
+    xs = [(torch.rand(B, C, H, W, generator=gen) * 2.0) for _ in range(3)]
+    st = rst = None
+    loss = rloss = 0.0
+    wgt = torch.linspace(0.5, 1.5, C).view(1, C, 1, 1)
+    for x in xs:
+        spk, st = cell(x.to(dev), st)
+        rspk, rst = ref(x, rst)
+        np.testing.assert_array_equal(spk.detach().cpu().numpy(), rspk.detach().numpy())
+        np.testing.assert_allclose(st.detach().cpu().numpy(), rst.detach().numpy(), rtol=1e-5, atol=1e-5)
+        loss = loss + (spk * wgt.to(dev)).sum()
+        rloss = rloss + (rspk * wgt).sum()
+    loss.backward()
+    rloss.backward()
+    pairs = []
+    for c in convs:
+        g_w = getattr(ref, c).weight.grad
+        g_ref, v_ref = torch.autograd.grad(eff[c], gv[c], g_w)
+        pairs.append((f"{c}.weight_v", getattr(cell, c).weight_v.grad.cpu().numpy(), v_ref.numpy()))
+        # dL/dg is the projection of dL/dw on v / ||v||, ~0 here: the train-mode BatchNorm after the conv
+        # is invariant to an output channel's weight scale, so g only sees rounding -- compared on the
+        # scale of dL/dw instead of its own
+        d = (getattr(cell, c).weight_g.grad.cpu() - g_ref).norm() / g_w.norm()
+        print(f"[weight norm rec={recurrent}] {c}.weight_g |d| / |dL/dw| = {d:.2e}")
+        assert d < ORACLE_GRAD_TOL, (c, float(d))
+    rp = dict(ref.named_parameters())
+    pairs += [(n, a.grad.cpu().numpy(), rp[n].grad.numpy()) for n, a in cell.named_parameters()
+              if "weight_g" not in n and "weight_v" not in n]
+    _grad_check(f"weight norm rec={recurrent}", pairs, ORACLE_GRAD_TOL)
+    # a weight update between calls is picked up (the effective weight is formed per call)
+    x0 = xs[0].to(dev)
+    with torch.no_grad():
+        cell.lif.mem = None
+        s_a, _ = cell(x0, None)
+        cell.ff.weight_v.mul_(-1.0)
+        cell.lif.mem = None
+        s_b, _ = cell(x0, None)
+    assert not torch.equal(s_a, s_b)
