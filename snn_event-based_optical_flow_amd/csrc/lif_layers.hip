@@ -3672,9 +3672,13 @@ int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
         if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: lif_in requires cin == c");
         if (a.wt_rec) hipLaunchKernelGGL((k_conv_fwd<C, C, true, true, SP>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_conv_fwd<C, C, true, false, SP>), grid, block, 0, s, a);
-    } else if (a.wt_rec) {
-        if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: recurrent cell requires cin == c");
-        hipLaunchKernelGGL((k_conv_fwd<C, C, false, true, SP>), grid, block, 0, s, a);
+    } else if (a.wt_rec) {  // recurrent cell: input channels C, or the narrow event inputs
+        if (a.cin == C) hipLaunchKernelGGL((k_conv_fwd<C, C, false, true, SP>), grid, block, 0, s, a);
+        else if (a.cin == 1) hipLaunchKernelGGL((k_conv_fwd<1, C, false, true, SP>), grid, block, 0, s, a);
+        else if (a.cin == 2) hipLaunchKernelGGL((k_conv_fwd<2, C, false, true, SP>), grid, block, 0, s, a);
+        else if (a.cin == 4) hipLaunchKernelGGL((k_conv_fwd<4, C, false, true, SP>), grid, block, 0, s, a);
+        else if (a.cin == 5) hipLaunchKernelGGL((k_conv_fwd<5, C, false, true, SP>), grid, block, 0, s, a);
+        else SNN_FAIL(SNNFLOW_E_CHANNELS, "conv_fwd: recurrent cell with unsupported cin (1, 2, 4, 5 or c)");
     } else {
         if (a.cin == 1) hipLaunchKernelGGL((k_conv_fwd<1, C, false, false, SP>), grid, block, 0, s, a);
         else if (a.cin == 2) hipLaunchKernelGGL((k_conv_fwd<2, C, false, false, SP>), grid, block, 0, s, a);
@@ -3708,9 +3712,13 @@ int layer_bwd_c(const snnflow_layer_bwd_args& a, hipStream_t s) {
             else hipLaunchKernelGGL((k_layer_bwd<C, C, true, false, SP, C >= 16>), grid, block, 0, s, a);
         } else if (a.wt_bwd_rec) hipLaunchKernelGGL((k_layer_bwd<C, C, true, true, SP>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_layer_bwd<C, C, true, false, SP>), grid, block, 0, s, a);
-    } else if (a.wt_bwd_rec) {
-        if (a.cin != C) SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: recurrent cell requires cin == c");
-        hipLaunchKernelGGL((k_layer_bwd<C, C, false, true, SP>), grid, block, 0, s, a);
+    } else if (a.wt_bwd_rec) {  // recurrent cell: input channels C, or the narrow event inputs
+        if (a.cin == C) hipLaunchKernelGGL((k_layer_bwd<C, C, false, true, SP>), grid, block, 0, s, a);
+        else if (a.cin == 1) hipLaunchKernelGGL((k_layer_bwd<1, C, false, true, 1>), grid, block1, 0, s, a);
+        else if (a.cin == 2) hipLaunchKernelGGL((k_layer_bwd<2, C, false, true, 1>), grid, block1, 0, s, a);
+        else if (a.cin == 4) hipLaunchKernelGGL((k_layer_bwd<4, C, false, true, 1>), grid, block1, 0, s, a);
+        else if (a.cin == 5) hipLaunchKernelGGL((k_layer_bwd<5, C, false, true, 1>), grid, block1, 0, s, a);
+        else SNN_FAIL(SNNFLOW_E_CHANNELS, "layer_bwd: recurrent cell with unsupported cin (1, 2, 4, 5 or c)");
     } else {
         if (a.cin == 1) hipLaunchKernelGGL((k_layer_bwd<1, C, false, false, 1>), grid, block1, 0, s, a);
         else if (a.cin == 2) hipLaunchKernelGGL((k_layer_bwd<2, C, false, false, 1>), grid, block1, 0, s, a);

@@ -194,8 +194,8 @@ class SNNtorch_ConvLIFRecurrent(_SnnTorchCellBase):
                  mpbn=False):
         super().__init__()
         _check_supported(kernel_size, 1, quantization_config, tebn, mpbn, norm, detach, activation)
-        if input_size != hidden_size:
-            raise NotImplementedError("recurrent cells with input_size != hidden_size are not compiled")
+        if input_size != hidden_size and input_size not in (1, 2, 4, 5):
+            raise NotImplementedError("recurrent cells take input_size == hidden_size or 1, 2, 4, 5 (event inputs)")
         self._build(input_size, hidden_size, kernel_size, leak, thresh, learn_leak, learn_thresh, hard_reset,
                     1, tebn, num_timesteps, mpbn, detach)
         if norm == "weight":

@@ -335,3 +335,6 @@ def test_cell_constructor_options():
             cls(8, 8, 3, norm="group")
     with pytest.raises(NotImplementedError):
         snnflow.SNNtorch_ConvLIF(8, 8, 3, stride=2)
+    snnflow.SNNtorch_ConvLIFRecurrent(2, 8, 3)  # narrow event input into a recurrent cell
+    with pytest.raises(NotImplementedError):
+        snnflow.SNNtorch_ConvLIFRecurrent(3, 8, 3)

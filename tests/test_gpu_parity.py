@@ -1826,3 +1826,39 @@ def test_weight_norm_cell_vs_oracle(dev, recurrent):
         cell.lif.mem = None
         s_b, _ = cell(x0, None)
     assert not torch.equal(s_a, s_b)
+
+
+@pytest.mark.parametrize("cin,C", [(2, 8), (4, 16), (1, 4), (5, 32)])
+def test_recurrent_cell_narrow_input_vs_oracle(dev, cin, C):
+    """SNNtorch_ConvLIFRecurrent with input_size != hidden_size (SNNtorch_spiking_submodules.py:452-453:
+    ff is input_size -> hidden_size, rec hidden_size -> hidden_size), the event-input widths 1, 2, 4, 5:
+    3 calls chained through prev_state (the recurrent conv on the previous spikes) against
+    SnnTorchCellRef -- spikes, states, every parameter gradient and the input gradients."""
+    import snnflow
+    from oracle import lif_ref
+
+    torch.manual_seed(59)
+    B, H, W = 2, 24, 40
+    cell = snnflow.SNNtorch_ConvLIFRecurrent(cin, C, 3, thresh=(0.2, 0.4)).to(dev).train()
+    ref = lif_ref.SnnTorchCellRef(cin, C, 3, recurrent=True).train()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in cell.state_dict().items()}, strict=False)
+    gen = torch.Generator().manual_seed(61)
+    xs = [(torch.rand(B, cin, H, W, generator=gen) * 3.0).requires_grad_(True) for _ in range(3)]
+    xd = [x.detach().to(dev).requires_grad_(True) for x in xs]
+    st = rst = None
+    loss = rloss = 0.0
+    wgt = torch.linspace(0.5, 1.5, C).view(1, C, 1, 1)
+    for x, xg in zip(xs, xd):
+        spk, st = cell(xg, st)
+        rspk, rst = ref(x, rst)
+        np.testing.assert_array_equal(spk.detach().cpu().numpy(), rspk.detach().numpy())
+        np.testing.assert_allclose(st.detach().cpu().numpy(), rst.detach().numpy(), rtol=1e-5, atol=1e-5)
+        loss = loss + (spk * wgt.to(dev)).sum()
+        rloss = rloss + (rspk * wgt).sum()
+    assert float(torch.stack([s.detach().float().mean() for s in (spk,)]).sum()) > 0.0  # spikes happen
+    loss.backward()
+    rloss.backward()
+    rp = dict(ref.named_parameters())
+    pairs = [(n, a.grad.cpu().numpy(), rp[n].grad.numpy()) for n, a in cell.named_parameters()]
+    pairs += [(f"x{i}", a.grad.cpu().numpy(), b.grad.numpy()) for i, (a, b) in enumerate(zip(xd, xs))]
+    _grad_check(f"rec cell cin={cin} C={C}", pairs, ORACLE_GRAD_TOL)
