@@ -12,6 +12,10 @@
  *   activations  NHWC  [B][H][W][C]          (torch channels_last)
  *   cell state   [2][B][H][W][C]  (mem, spk)  (reference: torch.stack([mem, spk]))
  *   flow map     NCHW  [B][2][H][W]
+ *   spike bits   [B][H][W] words of c bits (c = 8: uint8, 16: uint16, 32: uint32), ABI 39: channel ch
+ *                of a pixel is bit (ch % 4) * (c / 4) + ch / 4 (SNNFLOW_SPK_BIT) -- an exact, 32x narrower
+ *                copy of a spike plane (spikes are 0/1) that the wavefront forward writes and the
+ *                recurrent convs and the deferred weight gradients read (c = 16 / 32)
  *   weights      torch [Cout][Cin][3][3]; kernels read the transposed copies made by
  *                snnflow_prep_weights.
  *
@@ -28,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 38
+#define SNNFLOW_ABI_VERSION 39
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -128,6 +132,11 @@ typedef struct snnflow_conv_fwd_args {
     /* ABI 33: 1 = store only the membrane half of prev_state (a caller whose spike half is never read:
      * a feed-forward layer's intermediate time steps in a window -- the backward recomputes the spikes) */
     int state_spk_skip;
+    /* ABI 39, optional (lif_in = 1, cin == c in {8, 16, 32}; not the c = 8 tile pipeline): prev_spk_bits
+     * receives the spike bit plane of the previous layer (the spikes the LIF of this task computes; interior
+     * pixels of every tile, i.e. every pixel); s_prev_bits, if set, replaces s_prev (the previous-step spikes
+     * of this layer as a bit plane: exact 0/1 by construction) */
+    uint8_t* prev_spk_bits; const uint8_t* s_prev_bits;
 } snnflow_conv_fwd_args;
 int snnflow_conv_fwd(const snnflow_conv_fwd_args* a, void* stream);
 int snnflow_conv_blocks(int B, int H, int W);
@@ -155,6 +164,9 @@ typedef struct snnflow_neuron_grad {
 } snnflow_neuron_grad;
 
 /* Number of doubles of a backward accumulator for c channels (3c LIF/BN sums + 2c+2 pred). */
+/* Bit of channel ch in a pixel word of a c-channel spike bit plane (ABI 39). */
+#define SNNFLOW_SPK_BIT(c, ch) (((ch) % 4) * ((c) / 4) + (ch) / 4)
+
 #define SNNFLOW_BWD_ACC(c) (5 * (c) + 2) /* sums per layer; storage SNNFLOW_ACC_LEN(SNNFLOW_BWD_ACC(c)) */
 
 /* ---- backward of the top layer: [pred backward] + LIF/ATan surrogate backward
@@ -273,6 +285,8 @@ typedef struct snnflow_wgrad_step {
     const float* s_prev;        /* NHWC previous-step spikes (rec conv input) or NULL */
     const float* stats;         /* [2][c] mean, invstd; NULL: no BatchNorm (G = g_cur, ConvLIF) */
     const float* bnc;           /* [2][c] grad_mean, k (ignored without stats) */
+    /* ABI 39, optional (cin == c in {16, 32}, exact_inputs): x / s_prev as spike bit planes (replace them) */
+    const uint8_t* x_bits; const uint8_t* s_prev_bits;
 } snnflow_wgrad_step;
 #define SNNFLOW_MAX_WGRAD_STEPS 32
 typedef struct snnflow_wgrad_args {

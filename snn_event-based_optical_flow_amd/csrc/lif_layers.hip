@@ -377,7 +377,10 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     const int part = thread_part(), co0 = part * CO;
     const int H = a.H, W = a.W;
     const Tile tl = block_tile(H, W, g);
-    const bool has_rec = REC && a.s_prev != nullptr;
+    // previous-step spikes: an fp32 NHWC plane (s_prev) or a spike bit plane (s_prev_bits, ABI 39)
+    [[maybe_unused]] constexpr bool SBITS = REC && (C == 8 || C == 16 || C == 32);
+    const bool rec_bits = SBITS && a.s_prev_bits != nullptr;
+    const bool has_rec = REC && (a.s_prev != nullptr || rec_bits);
     [[maybe_unused]] constexpr bool TR = LIF_IN && CIN == C;
     [[maybe_unused]] constexpr int TK = REC ? 1 : 0;
     TRACE_AT(TR, TK, 0);
@@ -408,8 +411,14 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         }
     }
     float4 rs[PF_REC ? Halo4<C, NTB>::R : 1];
+    [[maybe_unused]] unsigned rsb[PF_REC && SBITS ? Halo4<C, NTB>::R : 1];
     if constexpr (PF_REC) {
-        if (has_rec) halo_load<C, NTB, (C <= 8), SC1>(a.s_prev, tl, H, W, rs);
+        if constexpr (SBITS) {
+            if (rec_bits) halo_load_bits<C, NTB>(a.s_prev_bits, tl, H, W, rsb);
+            else if (has_rec) halo_load<C, NTB, (C <= 8), SC1>(a.s_prev, tl, H, W, rs);
+        } else {
+            if (has_rec) halo_load<C, NTB, (C <= 8), SC1>(a.s_prev, tl, H, W, rs);
+        }
     }
     if constexpr (LIF_IN) {
         constexpr int R = Halo4<CIN, NTB>::R, Q = CIN / 4;
@@ -433,6 +442,9 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
         float4* st4 = reinterpret_cast<float4*>(a.prev_state);
         const int qt = tid % Q;
         const LifCoef kc[4] = {coef[4 * qt], coef[4 * qt + 1], coef[4 * qt + 2], coef[4 * qt + 3]};
+        // the previous layer's spike bit plane (ABI 39): interior pixels, one word per pixel
+        constexpr bool OBITS = CIN == C && (C == 8 || C == 16 || C == 32);
+        uint8_t* const obits = OBITS ? a.prev_spk_bits : nullptr;
         auto halo_lif = [&](auto zr_c) {
             constexpr bool ZR = decltype(zr_c)::value;
 #pragma unroll
@@ -442,15 +454,22 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                     const int p = e / Q;
                     const int r = p / HWD, cc = p - r * HWD;
                     const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+                    const bool img = in_image(h, w, H, W), inner = img && r >= 1 && r <= TH && cc >= 1 && cc <= TW;
                     float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (in_image(h, w, H, W)) {
+                    if (img) {
                         const Lif4 o = lif_step4(ry[i], rm[i], kc, ZR);
                         sv = o.s;
-                        if (r >= 1 && r <= TH && cc >= 1 && cc <= TW) {
+                        if (inner) {
                             const int64_t k = (((int64_t)tl.b * H + h) * W + w) * Q + qt;
                             // write-through: read again only at the next time step (measured -1 us per launch)
                             st_state4(st4, k, o.mout);
                             if (!a.state_spk_skip) st_state4(st4, plane4 + k, o.s);
+                        }
+                    }
+                    if constexpr (OBITS) {
+                        if (obits != nullptr) {
+                            const unsigned wb = spk_pack_wave<CIN>(sv, tid & 63);
+                            if (inner && qt == 0) spk_store_bits<CIN>(obits, ((int64_t)tl.b * H + h) * W + w, wb);
                         }
                     }
                     if constexpr (L::BT) {
@@ -483,8 +502,21 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
     }
     // previous-step spikes exact in bf16 (0/1; always so on the engine path) -> bf16 MFMA; a wave with an
     // inexact value sets an LDS flag (cleared at kernel start) instead of __syncthreads_and's barriers
+    if constexpr (PF_REC && SBITS) {
+        if (rec_bits) {  // exact 0/1 by construction
+            constexpr int Q = C / 4;
+#pragma unroll
+            for (int i = 0; i < Halo4<C, NTB>::R; ++i) {
+                const int e = tid + i * NTB;
+                if (e < Halo4<C, NTB>::E) {
+                    const int p = e / Q, q = e - p * Q;
+                    *reinterpret_cast<float4*>(rtile + p * Pad<C>::v + 4 * q) = spk_quad<C>(rsb[i], q);
+                }
+            }
+        }
+    }
     if constexpr (PF_REC) {
-        if (has_rec) {
+        if (has_rec && !(SBITS && rec_bits)) {
             halo_store<C, NTB>(rtile, rs);
             bool ok = true;
 #pragma unroll
@@ -525,7 +557,12 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                     rt = rtile;
                 } else {
                     __syncthreads();
-                    stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    if constexpr (SBITS) {
+                        if (rec_bits) stage_nhwc_bits<C, NTB>(a.s_prev_bits, tl, H, W, tile);
+                        else stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    } else {
+                        stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    }
                     __syncthreads();
                 }
                 ar.zero();
@@ -565,7 +602,12 @@ __device__ void conv_fwd_body(const snnflow_conv_fwd_args& a, const Grid g, floa
                     rt = rtile;
                 } else {
                     __syncthreads();
-                    stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    if constexpr (SBITS) {
+                        if (rec_bits) stage_nhwc_bits<C, NTB>(a.s_prev_bits, tl, H, W, tile);
+                        else stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    } else {
+                        stage_nhwc<C, NTB>(a.s_prev, tl, H, W, tile);
+                    }
                     __syncthreads();
                 }
                 float r[CO];
@@ -2197,7 +2239,8 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
     }
 
     float4 rg4[O::R], ry4[O::R], rx[RX], rs[REC ? RX : 1];
-    bool dense = false, has_s = false;
+    unsigned rxb[RX], rsb[REC ? RX : 1];  // x / s_prev as spike bit-plane words (ABI 39)
+    bool dense = false, has_s = false, xbits = false, sbits = false;
     auto issue = [&](int t) {
         const float* gp = ap->steps[t].g_cur;
         const float* yp = ap->steps[t].y;
@@ -2213,11 +2256,15 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
             ry4[i] = ok ? reinterpret_cast<const float4*>(yp)[k] : z4;
         }
         const auto& sp = ap->steps[t];
-        dense = sp.xs_c == 1 && sp.xs_w == C && sp.xs_h == (int64_t)W * C && sp.xs_b == (int64_t)H * W * C;
-        if (dense) halo_load<C, NTB>(sp.x, tl, H, W, rx);
-        has_s = REC && sp.s_prev != nullptr;
+        xbits = sp.x_bits != nullptr;
+        dense = xbits || (sp.xs_c == 1 && sp.xs_w == C && sp.xs_h == (int64_t)W * C && sp.xs_b == (int64_t)H * W * C);
+        if (xbits) halo_load_bits<C, NTB>(sp.x_bits, tl, H, W, rxb);
+        else if (dense) halo_load<C, NTB>(sp.x, tl, H, W, rx);
+        sbits = REC && sp.s_prev_bits != nullptr;
+        has_s = REC && (sp.s_prev != nullptr || sbits);
         if constexpr (REC) {
-            if (has_s) halo_load<C, NTB>(sp.s_prev, tl, H, W, rs);
+            if (sbits) halo_load_bits<C, NTB>(sp.s_prev_bits, tl, H, W, rsb);
+            else if (has_s) halo_load<C, NTB>(sp.s_prev, tl, H, W, rs);
         }
     };
     // halo float4 element (pixel p, quad q) -> 4 bf16 of the channel-major tile
@@ -2255,8 +2302,14 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
                 d[3 * Gm::GS] = gv.w;
             }
         }
-        const bool dense_t = dense, has_s_t = has_s;
-        if (dense_t) {
+        const bool dense_t = dense, has_s_t = has_s, xbits_t = xbits, sbits_t = sbits;
+        if (xbits_t) {
+#pragma unroll
+            for (int i = 0; i < RX; ++i) {
+                const int e = tid + i * NTB;
+                if (e < Halo4<C, NTB>::E) put_halo(Xt, e, spk_quad<C>(rxb[i], e % Q));
+            }
+        } else if (dense_t) {
 #pragma unroll
             for (int i = 0; i < RX; ++i) {
                 const int e = tid + i * NTB;
@@ -2273,7 +2326,13 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
             }
         }
         if constexpr (REC) {
-            if (has_s_t) {
+            if (sbits_t) {
+#pragma unroll
+                for (int i = 0; i < RX; ++i) {
+                    const int e = tid + i * NTB;
+                    if (e < Halo4<C, NTB>::E) put_halo(St, e, spk_quad<C>(rsb[i], e % Q));
+                }
+            } else if (has_s_t) {
 #pragma unroll
                 for (int i = 0; i < RX; ++i) {
                     const int e = tid + i * NTB;
@@ -2449,8 +2508,17 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_bf32(snnflow_wgrad_args) {
         d[3 * XS] = __builtin_bit_cast(unsigned short, (__bf16)v.w);
     };
     // the conv input of step t (x or s_prev) into X^T: dense NHWC halo, or an element-wise gather
-    auto stage_x = [&](const float* src, int64_t sb, int64_t sc, int64_t sh, int64_t sw, bool dense) {
-        if (dense) {  // two batches of loads (12 VGPRs each: the accumulators stay live)
+    auto stage_x = [&](const float* src, int64_t sb, int64_t sc, int64_t sh, int64_t sw, bool dense,
+                       const uint8_t* bits) {
+        if (bits) {  // spike bit plane (ABI 39): one word per element, all loads in flight at once
+            unsigned rb[RX];
+            halo_load_bits<C, NTB>(bits, tl, H, W, rb);
+#pragma unroll
+            for (int i = 0; i < RX; ++i) {
+                const int e = tid + i * NTB;
+                if (e < Halo4<C, NTB>::E) put_halo(e, spk_quad<C>(rb[i], e % Q));
+            }
+        } else if (dense) {  // two batches of loads (12 VGPRs each: the accumulators stay live)
             constexpr int RH = (RX + 1) / 2;
 #pragma unroll
             for (int h2 = 0; h2 < RX; h2 += RH) {
@@ -2562,13 +2630,13 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_bf32(snnflow_wgrad_args) {
             }
         }
         const bool dense = sp.xs_c == 1 && sp.xs_w == C && sp.xs_h == (int64_t)W * C && sp.xs_b == (int64_t)H * W * C;
-        stage_x(sp.x, sp.xs_b, sp.xs_c, sp.xs_h, sp.xs_w, dense);
+        stage_x(sp.x, sp.xs_b, sp.xs_c, sp.xs_h, sp.xs_w, dense, sp.x_bits);
         __syncthreads();
         compute(acc[0]);
         if constexpr (REC) {
-            if (sp.s_prev != nullptr) {
+            if (sp.s_prev != nullptr || sp.s_prev_bits != nullptr) {
                 __syncthreads();  // X^T reads done
-                stage_x(sp.s_prev, 0, 0, 0, 0, true);
+                stage_x(sp.s_prev, 0, 0, 0, 0, true, sp.s_prev_bits);
                 __syncthreads();
                 compute(acc[NS - 1]);
             }
@@ -2603,6 +2671,213 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_bf32(snnflow_wgrad_args) {
             }
         }
         __syncthreads();
+    }
+}
+
+// C = 32 weight gradients from spike bit planes (ABI 39: the deferred weight gradients of the
+// wavefront path).  k_wgrad_bf32's arithmetic, slab layout and wave split (wave w: ci-tile w & 1, co-tile
+// (w >> 1) & 1, tile rows (w >> 2) + 2 i, all 9 taps), with
+//   * the conv input of a step as one 32-bit word per halo pixel (1.4 KB per tile instead of 44 KB of
+//     fp32 spikes), expanded to the channel-major bf16 X^T tile by the thread of that pixel;
+//   * the next step's loads -- g_cur and y of the tile (8 float4 per thread) and the halo word -- issued
+//     right after this step's tiles are staged, so they fly during this step's matrix-core work
+//     (k_wgrad_bf32 loads each step after the previous one's MFMAs: its fp32 input halo would not fit
+//     beside a prefetch in 128 registers);
+//   * a recurrent layer's two convs as two block sets (source 0: x -> slab_ff; 1: s_prev -> slab_rec), each
+//     block one source with 36 accumulator registers per wave like a feed-forward layer (k_wgrad_bf<32,
+//     true> holds both: 256 registers, one block per CU).  Block b: XCD b % 8, source (b / 8) & 1, tile
+//     (b % 8) + 8 (b / 16): the two sources of a tile run on one XCD at about the same time, so the second
+//     read of G's inputs is an L2 hit.
+// A step whose input has no bit plane (s_prev at t = 0: the caller's initial state) stages the fp32 plane;
+// without either it adds nothing.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT * 2, 4) void k_wgrad_b32(snnflow_wgrad_args) {
+    constexpr int C = 32, NTB = NT * 2, Q = C / 4;
+    constexpr int GS = NT + 4, XS = 10 * 40 + 8;
+    using O = Own4<C, NTB>;
+    constexpr int GF = C * GS, XF = C * XS / 2;
+    constexpr int RF = 4 * 9 * 256;  // one source's row-group exchange [4 tg][9][64][4]
+    static_assert(RF <= GF + XF, "exchange fits the staging pool");
+    static_assert(HN <= NTB, "one halo pixel per thread");
+    __shared__ __attribute__((aligned(16))) float pool[GF + XF];
+    float* const Gt = pool;
+    unsigned short* const Xt = reinterpret_cast<unsigned short*>(pool + GF);
+    __shared__ BnBwdLds coef[SNNFLOW_MAX_WGRAD_STEPS][C];
+
+    const cwgrad_ptr ap = (cwgrad_ptr)__builtin_amdgcn_kernarg_segment_ptr();
+    const int tid = threadIdx.x, lane = tid & 63, m = lane & 15, g = lane >> 4;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nt = wv & 1, mt = (wv >> 1) & 1, rg = wv >> 2;
+    const int nsrc = ap->rec ? 2 : 1;
+    const int b = blockIdx.x, src = nsrc == 2 ? (b >> 3) & 1 : 0;
+    const int bt = nsrc == 2 ? (b & 7) + 8 * (b >> 4) : b;  // tile block index (block_tile's XCD order)
+    const int H = ap->H, W = ap->W, nsteps = ap->nsteps;
+    const int nbt = ap->B * tiles_per_image(H, W);
+    if (bt >= nbt) return;  // padding block (recurrent grid: 2 x the tile count rounded up to 8)
+    const Tile tl = block_tile(H, W, Grid{bt, nbt});
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+    for (int e = tid; e < nsteps * C; e += NTB) {
+        const int t = e / C, c = e - t * C;
+        const float* st = ap->steps[t].stats;
+        const float* bc = ap->steps[t].bnc;
+        BnBwdLds k = {0.f, 1.f, 0.f, 0.f, 1.f};
+        if (st) {
+            k.mean = st[c];
+            k.inv = st[C + c];
+            k.gm = bc[c];
+            k.k = bc[C + c];
+            k.w = ap->bn_weight[c];
+        }
+        coef[t][c] = k;
+    }
+
+    // the halo pixel of this thread (tid < HN)
+    const int hr = tid / HWD, hc = tid - hr * HWD;
+    const int hh = tl.h0 + hr - 1, hw = tl.w0 + hc - 1;
+    const bool hok = tid < HN && in_image(hh, hw, H, W);
+    const int64_t hpix = hok ? ((int64_t)tl.b * H + hh) * W + hw : 0;
+    auto in_bits = [&](int t) { return src == 0 ? ap->steps[t].x_bits : ap->steps[t].s_prev_bits; };
+
+    float4 rg4[O::R], ry4[O::R];
+    unsigned xw = 0u;
+    auto issue = [&](int t) {
+        const auto& sp = ap->steps[t];
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            const int p = e / Q, q = e - p * Q;
+            const int ty = p / TW, tx = p - ty * TW;
+            const int h = tl.h0 + ty, w = tl.w0 + tx;
+            const bool ok = e < O::E && h < H && w < W;
+            const int64_t k = ok ? (((int64_t)tl.b * H + h) * W + w) * Q + q : 0;
+            rg4[i] = ok ? reinterpret_cast<const float4*>(sp.g_cur)[k] : z4;
+            ry4[i] = ok ? reinterpret_cast<const float4*>(sp.y)[k] : z4;
+        }
+        const uint8_t* xb = in_bits(t);
+        xw = (xb != nullptr && hok) ? spk_load_bits<C>(xb, hpix) : 0u;
+    };
+
+    f32x4 acc[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // this wave's MFMAs of the staged step: rows r = rg, rg + 2, ..., the 9 taps of (nt, mt)
+    auto compute = [&]() {
+#pragma unroll 1
+        for (int r = rg; r < TH; r += 2) {
+            bf16x8 ah, am, al;
+            {
+                const int co = mt * 16 + m;
+                const float* srcg = Gt + co * GS + r * TW + 8 * g;
+                const float4 u = *reinterpret_cast<const float4*>(srcg), v = *reinterpret_cast<const float4*>(srcg + 4);
+                const float a8[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const __bf16 h = (__bf16)a8[j];
+                    const float r1 = a8[j] - (float)h;
+                    const __bf16 md = (__bf16)r1;
+                    ah[j] = h;
+                    am[j] = md;
+                    al[j] = (__bf16)(r1 - (float)md);
+                }
+            }
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+                const unsigned short* T = Xt + (nt * 16 + m) * XS + (r + ky) * 40 + 8 * g;
+                const u32x4 u = *reinterpret_cast<const u32x4*>(T);
+                const uint2 v = *reinterpret_cast<const uint2*>(T + 8);
+                const unsigned int w6[5] = {u.x, u.y, u.z, u.w, v.x};
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+                    u32x4 bw;
+                    if (kx == 0) bw = u32x4{w6[0], w6[1], w6[2], w6[3]};
+                    else if (kx == 2) bw = u32x4{w6[1], w6[2], w6[3], w6[4]};
+                    else bw = u32x4{__builtin_amdgcn_alignbit(w6[1], w6[0], 16), __builtin_amdgcn_alignbit(w6[2], w6[1], 16),
+                                    __builtin_amdgcn_alignbit(w6[3], w6[2], 16), __builtin_amdgcn_alignbit(w6[4], w6[3], 16)};
+                    const bf16x8 bb = __builtin_bit_cast(bf16x8, bw);
+                    f32x4& o = acc[ky * 3 + kx];
+                    o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bb, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bb, o, 0, 0, 0);
+                    o = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bb, o, 0, 0, 0);
+                }
+            }
+        }
+    };
+
+    issue(0);
+    __syncthreads();  // coef
+    for (int t = 0; t < nsteps; ++t) {
+        const auto& sp = ap->steps[t];
+        // G^T = BN backward of g_cur (zero outside the image), from the prefetched registers
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < O::E) {
+                const int p = e / Q, q = e - p * Q;
+                const int ty = p / TW, tx = p - ty * TW;
+                const bool img = tl.h0 + ty < H && tl.w0 + tx < W;
+                const float4 gv = img ? bn_bwd4(rg4[i], ry4[i], &coef[t][4 * q]) : z4;
+                float* d = Gt + (4 * q) * GS + p;
+                d[0] = gv.x;
+                d[GS] = gv.y;
+                d[2 * GS] = gv.z;
+                d[3 * GS] = gv.w;
+            }
+        }
+        // X^T: the conv input of step t (bit plane: the halo pixel's word -> 32 bf16 0 / 1)
+        const uint8_t* xb = in_bits(t);
+        const float* xf = src == 0 ? sp.x : sp.s_prev;
+        const bool have = xb != nullptr || xf != nullptr;
+        if (xb != nullptr) {
+            if (tid < HN) {
+                unsigned short* d = Xt + hr * 40 + hc;
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    d[c * XS] = ((xw >> SNNFLOW_SPK_BIT(C, c)) & 1u) ? (unsigned short)0x3F80 : (unsigned short)0;
+            }
+        } else if (xf != nullptr) {  // fp32 NHWC plane (s_prev at t = 0), element-wise
+            for (int e = tid; e < HN * Q; e += NTB) {
+                const int64_t k = halo_idx4<C>(e, tl, H, W);
+                const float4 v = k >= 0 ? reinterpret_cast<const float4*>(xf)[k] : z4;
+                const int p = e / Q, q = e - p * Q;
+                const int r = p / HWD, cc = p - r * HWD;
+                unsigned short* d = Xt + (4 * q) * XS + r * 40 + cc;
+                d[0] = __builtin_bit_cast(unsigned short, (__bf16)v.x);
+                d[XS] = __builtin_bit_cast(unsigned short, (__bf16)v.y);
+                d[2 * XS] = __builtin_bit_cast(unsigned short, (__bf16)v.z);
+                d[3 * XS] = __builtin_bit_cast(unsigned short, (__bf16)v.w);
+            }
+        }
+        __syncthreads();
+        if (t + 1 < nsteps) issue(t + 1);  // step t+1's loads fly during step t's MFMAs
+        if (have) compute();
+        __syncthreads();  // before the next step overwrites the tiles
+    }
+
+    // row group 1 adds into row group 0 through LDS (fixed order)
+    const int64_t blk = bt;
+    const int accumulate = ap->accumulate;
+    float* red = pool;
+    const int tg = wv & 3;
+    if (rg == 1) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) *reinterpret_cast<f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4) = acc[j];
+    }
+    __syncthreads();
+    if (rg == 0) {
+        float* slab = (src == 0 ? ap->slab_ff : ap->slab_rec) + blk * (C * C * 9);
+        const int ci = nt * 16 + m;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+            const f32x4 v = acc[j] + *reinterpret_cast<const f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4);
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) {
+                const int co = mt * 16 + 4 * g + r4;
+                float* d = slab + ((int64_t)co * C + ci) * 9 + j;
+                *d = accumulate ? *d + v[r4] : v[r4];
+            }
+        }
     }
 }
 
@@ -2930,6 +3205,7 @@ __device__ inline void globalize(snnflow_conv_fwd_args& a) {
     SNN_G(a.x); SNN_G(a.prev_y); SNN_G(a.prev_mem); SNN_G(a.prev_acc); SNN_G(a.prev_stats);
     globalize(a.prev);
     SNN_G(a.prev_state); SNN_G(a.wt_ff); SNN_G(a.wt_rec); SNN_G(a.wt_ff_t); SNN_G(a.wt_rec_t); SNN_G(a.s_prev);
+    SNN_G(a.prev_spk_bits); SNN_G(a.s_prev_bits);
     SNN_G(a.y); SNN_G(a.acc); SNN_G(a.zero0); SNN_G(a.zero1); SNN_G(a.wf_ff); SNN_G(a.wf_rec);
 }
 __device__ inline void globalize(snnflow_lif_fwd_args& a) {
@@ -3797,6 +4073,9 @@ static int conv_fwd_check(const snnflow_conv_fwd_args* a) {
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: cin == c needs the backward-layout weights wt_ff_t / wt_rec_t");
     if (a->lif_in ? (!a->prev_y || !a->prev_state || (a->prev.bn_train && !a->prev_acc)) : !a->x)
         SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: missing input");
+    const bool bits_ok = a->cin == a->c && (a->c == 8 || a->c == 16 || a->c == 32);
+    if ((a->prev_spk_bits && !(bits_ok && a->lif_in)) || (a->s_prev_bits && !(bits_ok && a->wt_rec)))
+        SNN_FAIL(SNNFLOW_E_ARG, "conv_fwd: spike bit planes need cin == c in {8, 16, 32} (and lif_in / a recurrent conv)");
     return 0;
 }
 
@@ -4033,7 +4312,8 @@ int snnflow_fwd_slot(const snnflow_conv_fwd_args* conv, int nconv, const snnflow
             SNN_FAIL(SNNFLOW_E_CHANNELS, "fwd_slot: c = 16 / 32 runs the LIFFireNet task kinds only");
         p.conv[i] = a;
         p.nblk[i] = snnflow_conv_blocks(B, H, W);
-        if (c == 8 && g_pipe_fwd > 0 && (kind == SK_LIF || kind == SK_LIF_REC) && pipe_fits(B, H, W, c))
+        if (c == 8 && g_pipe_fwd > 0 && (kind == SK_LIF || kind == SK_LIF_REC) && pipe_fits(B, H, W, c) &&
+            !a.prev_spk_bits && !a.s_prev_bits)  // (the tile pipeline reads and writes fp32 spike planes only)
             kind = kind == SK_LIF ? SK_LIF_P : SK_LIF_REC_P;
         p.kind[i] = kind;
     }
@@ -4174,13 +4454,22 @@ int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block) {
 }
 int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : 0; }
 
+static int g_wg_bits = env_int("SNNFLOW_WG_BITS", 1);  // A/B: 0 = k_wgrad_bf32 / k_wgrad_bf on the bit planes
+static bool wgrad_all_x_bits(const snnflow_wgrad_args* a) {
+    for (int t = 0; t < a->nsteps; ++t)
+        if (!a->steps[t].x_bits) return false;
+    return true;
+}
+
 int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
     if (!a || a->B <= 0 || a->H <= 0 || a->W <= 0 || a->nsteps <= 0 || a->nsteps > SNNFLOW_MAX_WGRAD_STEPS ||
         !a->slab_ff || (a->rec && !a->slab_rec))
         SNN_FAIL(SNNFLOW_E_ARG, "wgrad: bad args");
     for (int t = 0; t < a->nsteps; ++t) {
         const snnflow_wgrad_step& st = a->steps[t];
-        if (!st.g_cur || !st.y || !st.x || (st.stats && !st.bnc)) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: incomplete step");
+        if (!st.g_cur || !st.y || !(st.x || st.x_bits) || (st.stats && !st.bnc)) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: incomplete step");
+        if ((st.x_bits || st.s_prev_bits) && !(a->exact_inputs && a->cin == a->c && (a->c == 8 || a->c == 16 || a->c == 32)))
+            SNN_FAIL(SNNFLOW_E_ARG, "wgrad: spike bit planes need exact_inputs and cin == c in {8, 16, 32}");
         if (st.stats && !a->bn_weight) SNN_FAIL(SNNFLOW_E_ARG, "wgrad: BatchNorm step needs bn_weight");
     }
     const hipStream_t s = (hipStream_t)stream;
@@ -4215,6 +4504,10 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
         } else if (c == 16) {
             if (a->rec) hipLaunchKernelGGL((k_wgrad_bf<16, true>), grid, blk, 0, s, *a);
             else hipLaunchKernelGGL((k_wgrad_bf<16, false>), grid, blk, 0, s, *a);
+        } else if (g_wg_bits && wgrad_all_x_bits(a)) {
+            // spike bit planes with the next step's loads in flight (k_wgrad_b32); recurrent layers as
+            // two block sets (x and s_prev)
+            hipLaunchKernelGGL(k_wgrad_b32, dim3(a->rec ? 2 * ((grid.x + 7) / 8 * 8) : grid.x), blk, 0, s, *a);
         } else {
             // feed-forward layers: k_wgrad_bf32 (two blocks per CU: 197 -> 164 us per cfg2 layer);
             // recurrent ones keep k_wgrad_bf (the split form's second staging pass measured 296 -> 315 us)

@@ -269,6 +269,55 @@ __device__ inline void halo_store(float* tile, const float4 (&r)[Halo4<CH, NTH>:
     }
 }
 
+// ---- spike bit planes (ABI 39): a pixel's CH spikes in one CH-bit word, channel ch at bit
+// (ch % 4) * (CH / 4) + ch / 4 (SNNFLOW_SPK_BIT): in the quad-per-lane halo loops (element e = pixel *
+// Q + quad, the Q = CH / 4 lanes of a pixel consecutive in the wave) spike j of every quad is one
+// ballot, and the pixel's word is Q-bit slices of the four ballots.
+template <int CH>
+__device__ inline unsigned spk_load_bits(const uint8_t* __restrict__ p, int64_t pix) {
+    static_assert(CH == 8 || CH == 16 || CH == 32, "bit-plane widths");
+    if constexpr (CH == 8) return p[pix];
+    else if constexpr (CH == 16) return reinterpret_cast<const uint16_t*>(p)[pix];
+    else return reinterpret_cast<const uint32_t*>(p)[pix];
+}
+template <int CH>
+__device__ inline void spk_store_bits(uint8_t* __restrict__ p, int64_t pix, unsigned w) {
+    if constexpr (CH == 8) p[pix] = (uint8_t)w;
+    else if constexpr (CH == 16) reinterpret_cast<uint16_t*>(p)[pix] = (uint16_t)w;
+    else reinterpret_cast<uint32_t*>(p)[pix] = w;
+}
+// channels 4q .. 4q+3 of a pixel word as exact 0/1 floats
+template <int CH>
+__device__ inline float4 spk_quad(unsigned w, int q) {
+    constexpr int Q = CH / 4;
+    return make_float4((float)((w >> q) & 1u), (float)((w >> (Q + q)) & 1u), (float)((w >> (2 * Q + q)) & 1u),
+                       (float)((w >> (3 * Q + q)) & 1u));
+}
+// The word of this lane's pixel from the spikes s of the wave's quad-per-lane elements (every lane of
+// the wave that holds an element calls it; the result is meaningful in every lane of the pixel).
+template <int CH>
+__device__ inline unsigned spk_pack_wave(const float4& s, int lane) {
+    constexpr int Q = CH / 4;
+    const unsigned long long b0 = __builtin_amdgcn_ballot_w64(s.x != 0.f), b1 = __builtin_amdgcn_ballot_w64(s.y != 0.f);
+    const unsigned long long b2 = __builtin_amdgcn_ballot_w64(s.z != 0.f), b3 = __builtin_amdgcn_ballot_w64(s.w != 0.f);
+    const int sh = lane & ~(Q - 1);
+    constexpr unsigned m = (1u << Q) - 1u;
+    return ((unsigned)(b0 >> sh) & m) | (((unsigned)(b1 >> sh) & m) << Q) | (((unsigned)(b2 >> sh) & m) << (2 * Q)) |
+           (((unsigned)(b3 >> sh) & m) << (3 * Q));
+}
+// halo words of a bit plane in halo_load's element order (element e = pixel * (CH/4) + quad; 0 outside
+// the image): one word per element, expanded with spk_quad(w, e % (CH/4)) where it is used
+template <int CH, int NTH = NT>
+__device__ inline void halo_load_bits(const uint8_t* __restrict__ src, const Tile& tl, int H, int W,
+                                      unsigned (&r)[Halo4<CH, NTH>::R]) {
+    constexpr int Q = CH / 4;
+#pragma unroll
+    for (int i = 0; i < Halo4<CH, NTH>::R; ++i) {
+        const int64_t k = halo_idx4<CH>(threadIdx.x + i * NTH, tl, H, W);
+        r[i] = (k >= 0) ? spk_load_bits<CH>(src, k / Q) : 0u;
+    }
+}
+
 // Per-channel LIF coefficients: I = y*alpha + shift (torch CPU BN transform order:
 // alpha = invstd*gamma, shift = bias - mean*alpha), beta clamped to [0,1].
 struct LifCoef { float alpha, shift, beta, theta; };

@@ -54,6 +54,19 @@ __device__ void stage_nhwc(const float* __restrict__ x, const Tile& tl, int H, i
     }
 }
 
+// The same from a spike bit plane (ABI 39): exact 0/1 floats
+template <int C, int NTH = NT>
+__device__ void stage_nhwc_bits(const uint8_t* __restrict__ bits, const Tile& tl, int H, int W, float* tile) {
+    constexpr int P = Pad<C>::v, Q = C / 4;
+    for (int e = threadIdx.x; e < HN * Q; e += NTH) {
+        const int p = e / Q, q = e - p * Q;
+        const int r = p / HWD, cc = p - r * HWD;
+        const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
+        const unsigned wb = in_image(h, w, H, W) ? spk_load_bits<C>(bits, ((int64_t)tl.b * H + h) * W + w) : 0u;
+        *reinterpret_cast<float4*>(tile + p * P + 4 * q) = spk_quad<C>(wb, q);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // 3x3 convolution of one output pixel (outputs [co0, co0+CO)) from an LDS halo tile.
 // wt: [3][3][CIN][C]; co0 must be wave-uniform (scalar weight loads).

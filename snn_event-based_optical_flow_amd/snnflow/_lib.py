@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 38
+ABI_VERSION = 39
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -39,7 +39,7 @@ class ConvFwdArgs(ctypes.Structure):
                 ("prev", Neuron), ("prev_state", P),
                 ("wt_ff", P), ("wt_rec", P), ("wt_ff_t", P), ("wt_rec_t", P), ("s_prev", P),
                 ("y", P), ("acc", P), ("zero0", P), ("zero1", P), ("zero_n", I32),
-                ("wf_ff", P), ("wf_rec", P), ("state_spk_skip", I32)]
+                ("wf_ff", P), ("wf_rec", P), ("state_spk_skip", I32), ("prev_spk_bits", P), ("s_prev_bits", P)]
 
 
 class EvalFwdArgs(ctypes.Structure):
@@ -87,7 +87,7 @@ MAX_WGRAD_STEPS = 32
 
 class WgradStep(ctypes.Structure):
     _fields_ = [("g_cur", P), ("y", P), ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64),
-                ("s_prev", P), ("stats", P), ("bnc", P)]
+                ("s_prev", P), ("stats", P), ("bnc", P), ("x_bits", P), ("s_prev_bits", P)]
 
 
 class WgradArgs(ctypes.Structure):

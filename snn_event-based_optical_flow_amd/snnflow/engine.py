@@ -17,6 +17,7 @@ gradient additions.
 """
 import ctypes
 import operator
+import os
 
 import torch
 
@@ -197,10 +198,12 @@ class FireNetEngine:
         self.pending_layers = []  # per pending step: the layers whose weight gradients are still deferred
         self.slab_live = [False] * self.L      # slab rows of layer l hold partial sums of this chain
         self.fuse_wgrad = self.C == 8          # wavefront backward computes layers >= 1's dW in place
+        # forward_sequence: spike bit planes between its kernels (ABI 39; SNNFLOW_SPK_BITS=0: the fp32 spike
+        # half of the states everywhere, as before)
+        self.spk_bits = os.environ.get("SNNFLOW_SPK_BITS", "1") != "0"
         # per-step autograd nodes of one BPTT chain (the reference loop's T model() calls): their backwards
         # are collected and issued at the chain's first step as wavefront launches (FireNetStep, _Chain);
         # SNNFLOW_DEFER_BWD=0: every node runs its own step's backward
-        import os
         self.defer_backward = os.environ.get("SNNFLOW_DEFER_BWD", "1") != "0"
         self.keep_seq_states = False  # FireNetSequence: expose every step's states (activity log)
         self.capture_states = False   # tests: keep every step's states of forward_sequence in seq_states
@@ -408,15 +411,21 @@ class FireNetEngine:
             a.exact_inputs = 1 if l > 0 else 0
             a.bn_weight = ptr(self.cells[l].bn.weight)
             a.slab_ff, a.slab_rec = ptr(ws.slab_ff[l]), _ptr_t(ws.slab_rec[l])
-            for k, (gcur, bnc, ys, stats, x, states, s_prev, _) in enumerate(chunk):
+            for k, (gcur, bnc, ys, stats, x, states, s_prev, _, bits) in enumerate(chunk):
                 st = a.steps[k]
                 st.g_cur, st.y, st.stats, st.bnc = gcur[l], ys[l], stats[l], bnc[l]
+                xb, sb = bits if bits is not None else (None, None)
                 if l == 0:
                     st.x = ptr(x)
                     st.xs_b, st.xs_c, st.xs_h, st.xs_w = _x_strides(x)
+                elif xb is not None and xb[l - 1] is not None:  # layer l-1's spikes as a bit plane (ABI 39)
+                    st.x_bits = xb[l - 1]
                 else:
                     st.x, (st.xs_b, st.xs_c, st.xs_h, st.xs_w) = _spk_half(states[l - 1])
-                st.s_prev = _ptr_t(s_prev[l]) if rec else None
+                if rec and sb is not None and sb[l] is not None:
+                    st.s_prev_bits = sb[l]
+                else:
+                    st.s_prev = _ptr_t(s_prev[l]) if rec else None
             _lib.call(f"wgrad[{l}]", lib.snnflow_wgrad, ctypes.byref(a), stream)
             self.slab_live[l] = True
 
@@ -448,7 +457,8 @@ class FireNetEngine:
             return
         L = self.L
         steps = (_lib.FireNetWgradStep * len(self.pending))()
-        for k, (gcur, bnc, ys, stats, x, states, s_prev, _) in enumerate(self.pending):
+        for k, (gcur, bnc, ys, stats, x, states, s_prev, _, bits) in enumerate(self.pending):
+            assert bits is None, "the step driver's deferred weight gradients read fp32 spike planes"
             st = steps[k]
             st.g_cur, st.bnc, st.ys, st.stats = gcur.base, bnc.base, ys.base, stats.base
             st.x = x.data_ptr()
@@ -933,7 +943,7 @@ def _chain_backward_batched(eng, steps):
             st = steps[t]
             x, ys, stats = st.saved[:3]
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys), _Rows(stats), x, st.saved[4:4 + L],
-                                st.ptrs[1], (st.saved, buf)))
+                                st.ptrs[1], (st.saved, buf), None))
             eng.pending_layers.append((0,) if fuse else tuple(range(L)))
         eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
     except Exception:
@@ -998,7 +1008,7 @@ def _step_backward(eng, ctx, g_states=None):
     bnc_t = torch.empty(L, 2, C, device=dev)           # BN backward coefficients (grad_mean, k)
     gcur, bnc, ys, stats = _Rows(gcur_t), _Rows(bnc_t), _Rows(ys), _Rows(stats)
     # pending: row pointers for the deferred wgrad + the tensors behind them (kept alive)
-    eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev, (keep, gcur_t, bnc_t, saved)))
+    eng.pending.append((gcur, bnc, ys, stats, x, states, s_prev, (keep, gcur_t, bnc_t, saved), None))
     eng.pending_layers.append(tuple(range(L)))
     # (the deferred weight gradients stay on this stream after the chain: a side stream
     # overlapping them with the root step's chain measured slower under graph replay,
@@ -1175,8 +1185,23 @@ class FireNetSequence(torch.autograd.Function):
         # keeps every step's states
         fuse = bool(eng.fuse_wgrad)  # decided once: the backward must see the same choice (ctx.fuse)
 
+        # spike bit planes (ABI 39, C = 16 / 32, whose weight gradients are deferred): task l >= 1 of step t
+        # writes layer l-1's spikes of step t as one C-bit word per pixel (the top layer's are not
+        # written); the recurrent convs at t >= 1 and the deferred weight gradients read those instead of
+        # the fp32 spike half of the states.  (C = 8 fuses the weight gradients into the backward, which
+        # recomputes the spikes; there the bit planes measured no faster: the recurrent layers' fp32
+        # planes stay.)
+        bits_on = eng.spk_bits and C in (16, 32) and not fuse
+        need_bits = [bits_on and l < L - 1 for l in range(L)]
+        bits = (torch.empty(T, L, B * H * W * C // 8, dtype=torch.uint8, device=dev) if any(need_bits)
+                else None)
+        bptr = [[bits[t, l].data_ptr() if need_bits[l] else None for l in range(L)] for t in range(T)]
+
         def spk_skip(l, t):
-            return fuse and t < T - 1 and not eng.rec[l] and not eng.keep_seq_states
+            # the spike half of layer l's state at t < T-1 is read by nobody when its readers take the bit
+            # plane, or (fused weight gradients) when the layer is feed-forward: the next step's LIF reads
+            # the membrane half and the backward recomputes the spikes
+            return t < T - 1 and not eng.keep_seq_states and ((fuse and not eng.rec[l]) or need_bits[l])
         for tasks in wavefront_slots(T, L + 1):
             convs, top = [], None
             for k, t in tasks:
@@ -1185,6 +1210,10 @@ class FireNetSequence(torch.autograd.Function):
                                        s_prev[t], facc[t], neurons, train, wfwd, wbwd)
                     if k >= 1 and spk_skip(k - 1, t):
                         a.state_spk_skip = 1
+                    if k >= 1 and need_bits[k - 1]:
+                        a.prev_spk_bits = bptr[t][k - 1]
+                    if eng.rec[k] and t >= 1 and need_bits[k]:
+                        a.s_prev_bits, a.s_prev = bptr[t - 1][k], None
                     convs.append(a)
                 else:
                     top = _fwd_top_args(eng, B, H, W, ys[t], stats[t], states[t], mem_in[t], facc[t], neurons,
@@ -1206,6 +1235,8 @@ class FireNetSequence(torch.autograd.Function):
         ctx.eng = eng
         ctx.T = T
         ctx.fuse = fuse
+        ctx.bptr = bptr
+        ctx.bits = bits  # (the backward's readers run before the next forward can reuse it: a plain attribute)
         ctx.root = root
         ctx.ext = ext
         ctx.shape = (B, H, W, cin0)
@@ -1290,9 +1321,10 @@ class FireNetSequence(torch.autograd.Function):
         # layers >= 1: dW inside the backward slot tasks (wslab_*); the forward's choice (it skipped the
         # spike planes the fused form never reads), not the engine flag's value now
         fuse = ctx.fuse
+        bptr = ctx.bptr
         for t in range(T - 1, -1, -1):
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys[t]), _Rows(stats[t]), xs[t], states[t], s_prev[t],
-                                (gcur, bnc, ys, stats)))
+                                (gcur, bnc, ys, stats, ctx.bits), (bptr[t], bptr[t - 1] if t >= 1 else [None] * L)))
             eng.pending_layers.append((0,) if fuse else tuple(range(L)))
         try:
             # backward kernel j of step t: j = 0 top (pred + LIF of layer L-1), j >= 1 layer L-j;

@@ -434,15 +434,17 @@ def test_clip_adam_matches_torch(dev, C):
         np.testing.assert_array_equal(m[1].cpu().numpy(), opt._moments[1].cpu().numpy())
 
 
-def _window_run(dev, wins, C, keep):
+def _window_run(dev, wins, C, keep, bits=True):
     """forward_sequence + EventWarping + backward of one window at full size, with the engine either
     keeping every step's states (capture_states: nothing skipped, as test_cfg2_train_step_vs_oracle
-    runs it) or not (the bench: the unread spike planes and state-gradient halves are skipped)."""
+    runs it) or not (the bench: the unread spike planes and state-gradient halves are skipped); `bits`:
+    the spike bit planes between the kernels (ABI 39) or the fp32 spike half of the states."""
     import snnflow
 
     model = _new_model(C).to(dev).train()
     B, _, H, W = wins[0]["event_cnt"].shape
     model.engine.capture_states = keep
+    model.engine.spk_bits = bits
     outs = model.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
     if keep:
         model.engine.seq_states = None
@@ -480,6 +482,37 @@ def test_bench_window_skips_bit_identical(dev, tag, B, H):
     for l, (a, b) in enumerate(zip(keep[3], skip[3])):
         assert torch.equal(a, b), f"final state of layer {l}"
     print(f"\n[{tag}] capture on / off: loss {keep[1]:.9g}, {len(names)} gradients, {len(keep[3])} final states identical")
+
+
+@pytest.mark.parametrize("C,B", [(16, 4), (32, 8)], ids=["C16", "C32"])
+def test_spike_bit_planes_bit_identical(dev, C, B):
+    """The spike bit planes (ABI 39, C = 16 / 32: the forward writes each layer's spikes as one C-bit word
+    per pixel; the recurrent convs and the deferred weight gradients read them, and the fp32 spike half
+    of the intermediate states is no longer stored)
+    against the fp32 spike planes (engine.spk_bits off, every state written): one full window at 128x128,
+    T = 10 x 1000 events -- flows, loss, every parameter gradient and the final states the same bits."""
+    from snnflow.synthetic import make_window
+
+    T, N, H = 10, 1000, 128
+    gen = torch.Generator(device=dev).manual_seed(1)
+    wins = [make_window(B, N, H, H, gen, dev) for _ in range(T)]
+    ref = _window_run(dev, wins, C, True, bits=False)
+    got = _window_run(dev, wins, C, False, bits=True)
+    for t, (a, b) in enumerate(zip(ref[0], got[0])):
+        assert torch.equal(a, b), f"flow of step {t}"
+    assert ref[1] == got[1], (ref[1], got[1])
+    names = [n for n, _ in _new_model(C).named_parameters()]
+    worst = 0.0
+    for n, a, b in zip(names, ref[2], got[2]):
+        d = float((a - b).abs().max() / a.abs().max().clamp_min(1e-30))
+        worst = max(worst, d)
+        # the fp64 batch-sum atomics may reorder between two runs and round a BatchNorm-backward
+        # coefficient to a neighbouring fp32 value (C = 16: 1.5e-7 measured); a wrong spike bit would
+        # move a gradient by orders of magnitude more
+        assert d <= 1e-5, f"gradient of {n}: max rel |d| {d:.3e}"
+    for l, (a, b) in enumerate(zip(ref[3], got[3])):
+        assert torch.equal(a, b), f"final state of layer {l}"
+    print(f"\n[C={C} B={B}] bit planes vs fp32 spikes: loss {ref[1]:.9g}, worst gradient rel diff {worst:.3e}")
 
 
 def test_bench_graph_pingpong_matches_eager(dev):

@@ -1,15 +1,13 @@
 #!/bin/bash
-# A/B of environment settings on the default bench line (alternating runs).
-#   ENVS="name:VAR=val[,VAR2=val] ..." (a "base" run with nothing set comes first in every round)
+# Environment A/B on one box: tools/gpu_envab.sh "<bench args>" "VAR=a" "VAR=b" [reps]
+# alternates the bench line under each environment setting; prints ms_per_step and the kernel averages.
 set -u
-O=gpurun_out/envab${ABTAG:-}
+ARGS=$1; A=$2; B=$3; N=${4:-2}
+O=gpurun_out/envab
 mkdir -p $O
-run() {  # name, env assignments (comma separated)
-  local n=$1 e=$2
-  env $(echo $e | tr ',' ' ') timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $O/bench_$n.json 2> $O/bench_$n.err || { echo "bench $n failed"; tail -20 $O/bench_$n.err; return 4; }
-  python -c "import json;d=json.load(open('$O/bench_$n.json'));print('$n', d['ms_per_step'], d['value'], {k:v['avg_us'] for k,v in list(d['kernels'].items())[:6]})"
-}
-for rep in 1 2; do
-  run base_$rep "SNNFLOW_NONE=1" || exit 4
-  for spec in ${ENVS:-}; do run ${spec%%:*}_$rep ${spec#*:} || exit 4; done
+for i in $(seq $N); do
+  for E in "$A" "$B"; do
+    env $E timeout -k 10 300 python bench.py --no-cpu-baseline $ARGS > $O/run.json 2> $O/run.err || { tail -20 $O/run.err; exit 4; }
+    python -c "import json;d=json.load(open('$O/run.json'));print('$E', d['ms_per_step'], {k:v['avg_us'] for k,v in list(d['kernels'].items())[:6]})"
+  done
 done
