@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--eval", action="store_true",
                    help="LIFFireNet evaluation pass instead of the train step (eval_flow.py:208-338): model.eval(), "
                         "no autograd, T windows forward + rounded per-polarity IWE + AEE per window")
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the N>1 step path (process group, forward + backward graph, SUM all-reduce of the flat "
+                        "gradient buffer, update graph) even at one rank: the RCCL code path rehearsed at world size 1")
     p.add_argument("--dp-check", action="store_true",
                    help="N>1 correctness check of this very step path (gloo rehearsal): the all-reduced "
                         "gradient == the sum of the ranks' own gradients, parameters identical after the update")
@@ -196,8 +199,12 @@ def main():
     if share:  # rehearsal: several ranks on one device (gloo)
         local = local % torch.cuda.device_count()
     backend = None
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher: a one-rank group on this host
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                              LOCAL_RANK="0")
         torch.cuda.set_device(local)
         backend = resolve_backend(args.dist_backend, torch.cuda.device_count(), share)
         dist.init_process_group(backend, init_method="env://")
@@ -205,7 +212,7 @@ def main():
     if args.eval:
         if args.model != "LIFFireNet":
             raise SystemExit("bench.py --eval: LIFFireNet only")
-        return eval_main(args, world, rank, dev, backend)
+        return eval_main(args, world, rank, dev, backend, dist_on)
 
     import snnflow
     from snnflow import _lib
@@ -308,7 +315,7 @@ def main():
     # flat gradient buffer, then that batch's update graph (clip + Adam read the graph's gradients).
     # Every capture starts from set_to_none gradients, so each graph owns its gradient buffer.
     graphs, upds, flats = [], [], []
-    multi = world == 1
+    multi = not dist_on  # one graph holds the whole step (no collective between forward+backward and update)
     if not args.no_graph:
         n_graphs = len(pool)
         if not unet and not args.per_step:
@@ -353,7 +360,7 @@ def main():
         _dp_check(world, rank, step_parts=(graphs, upds, flats, fwd_bwd, sync_grads, update, opt), params=params)
         dist.destroy_process_group()
         return
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     prof = None
@@ -365,14 +372,14 @@ def main():
     for i in range(args.steps):
         step(i)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if prof is not None:
         import pstats
         prof.disable()
         pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(30)
-    if world > 1:
+    if dist_on:
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -419,7 +426,7 @@ def main():
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 
@@ -457,7 +464,7 @@ def _dp_check(world, rank, step_parts, params):
     for t in locals_[1:]:
         want = want + t.double()
     err = float((reduced.double() - want).abs().max() / max(float(want.abs().max()), 1e-30))
-    distinct = float(max((t - locals_[0]).abs().max() for t in locals_[1:]))
+    distinct = float(max((t - locals_[0]).abs().max() for t in locals_[1:])) if world > 1 else 0.0
     if graphs:
         upds[1 % len(graphs)].replay()
     else:
@@ -466,7 +473,7 @@ def _dp_check(world, rank, step_parts, params):
     pflat = torch.cat([p.detach().reshape(-1).cpu() for p in params])
     ps = [torch.empty_like(pflat) for _ in range(world)]
     dist.all_gather(ps, pflat)
-    pdiff = float(max((t - ps[0]).abs().max() for t in ps[1:]))
+    pdiff = float(max((t - ps[0]).abs().max() for t in ps[1:])) if world > 1 else 0.0
     if rank == 0:
         print(json.dumps({"dp_check": {"world": world, "backend": dist.get_backend(), "grad_numel": local.numel(), "allreduce_rel_err": err,
                                        "ranks_local_grads_differ_by": distinct, "param_max_diff_after_update": pdiff}}),
@@ -484,7 +491,7 @@ def perturb_running_stats(model, seed=3):
             m.running_var.copy_(0.5 + torch.rand(m.running_var.shape, generator=g))
 
 
-def eval_main(args, world, rank, dev, backend):
+def eval_main(args, world, rank, dev, backend, dist_on=False):
     """`--eval`: the reference's evaluation loop (eval_flow.py:208-338) on synthetic windows.  One
     step = T windows of B sequences: model.eval() forward (BatchNorm on running statistics, no
     autograd; forward_sequence's wavefront launches), then per window the rounded per-polarity IWE
@@ -607,7 +614,7 @@ def eval_main(args, world, rank, dev, backend):
             "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu, "configs0": cfg1,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

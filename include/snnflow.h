@@ -413,6 +413,12 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream);
  * g_flows), and writes the band once.  H * W <= 2^21, W <= 1791. */
 int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, float* g_flows, void* stream);
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf);
+/* ABI 39: device-side argument faults the kernels detected and skipped instead of reading out of bounds
+ * (bit 1: a forward bin segment outside its window's records, k_iwe_splat; bit 2: the same in the
+ * backward, k_iwe_bwd_band -- a corrupted or stale images scratch).  Synchronises the device; clear != 0
+ * resets the flags.  Returns the flag bits (>= 0) or an error code.  (Diagnostics: SNNFLOW_FAULT_INJECT=1 / 2
+ * at library load corrupts one bin-table entry before k_iwe_splat / k_iwe_bwd_band, for tests.) */
+int snnflow_device_errors(int clear);
 /* floats of the images scratch (ABI 38: the IWEs and both binnings of the events; H * W <= 2^21) */
 int64_t snnflow_iwe_scratch_floats(int B, int M, int T, int tf, int H, int W);
 

@@ -174,6 +174,14 @@ int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet
     for (int t = 0; t < T; ++t)
         if (!q->ys[t] || !q->stats[t] || !q->flow[t] || !q->states[t])
             SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: incomplete step");
+    // every launch's layer-task count, checked before the first launch (the call refuses cleanly or runs
+    // to completion: no half-written gradients or slab rows)
+    for (int d = 0; d < K + 2 * (T - 1); ++d) {
+        int n = 0;
+        for (int j = 1; j < K; ++j)
+            if ((d - j) >= 0 && (d - j) % 2 == 0 && (d - j) / 2 < T) ++n;
+        if (n > SNNFLOW_MAX_SLOT_TASKS) SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: too many layers for a launch");
+    }
     // gradient of step t's incoming state of layer l (t >= 1: inside the chain, recurrent layers only)
     auto g_in = [&](int t, int l) -> float* {
         if (t == 0) return q->g_prev0[l];

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <cmath>
+#include <cstdlib>
 
 #include "snnflow_dev.h"
 #include "snnflow_warp.h"
@@ -369,6 +370,17 @@ __global__ __launch_bounds__(WB_NT) void k_iwe_wbin(snnflow_iwe_loss_args a, int
     }
 }
 
+// Device-side argument faults of the loss kernels (snnflow_device_errors): a bin table whose segment
+// lies outside its window's record region (a corrupted or stale scratch) is skipped and flagged here
+// instead of being read out of bounds.  Bit 1: k_iwe_splat, bit 2: k_iwe_bwd_band.
+__device__ unsigned int g_snnflow_dev_err = 0u;
+
+// Test hook (SNNFLOW_FAULT_INJECT=1|2 at library load): overwrite one entry of the forward's (1) or the
+// backward's (2) bin table after it is formed, so the checks above can be exercised on the GPU.
+__global__ void k_iwe_corrupt_bins(int* bins, int n) {
+    if (threadIdx.x == 0 && n > 1) bins[1] = 1 << 28;
+}
+
 __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a, int nbands, const float4* __restrict__ rec,
                                                         const int* __restrict__ bins) {
     __shared__ SplatLds img;
@@ -385,8 +397,15 @@ __global__ __launch_bounds__(SPLAT_NT) void k_iwe_splat(snnflow_iwe_loss_args a,
         int len = 0;
         if (tid < a.T) {
             const int* bo = bins + ((int64_t)b * a.T + tid) * (nb2 + 1);
-            const int s0 = bo[j];
+            int s0 = bo[j];
             len = bo[j + 1] - s0;
+            // the segment must lie in the window's region of R * 2 records per event
+            const int64_t cap = (int64_t)R * 2 * (a.off[tid + 1] - a.off[tid]);
+            if (s0 < 0 || len < 0 || (int64_t)s0 + len > cap) {
+                atomicOr(&g_snnflow_dev_err, 1u);
+                s0 = 0;
+                len = 0;
+            }
             seg0[tid] = (int64_t)R * 2 * ((int64_t)b * a.M + a.off[tid]) + s0;  // record index of the segment's start
         }
         int x = len;
@@ -791,6 +810,10 @@ __global__ __launch_bounds__(GB_NT) void k_iwe_bwd_band(snnflow_iwe_loss_args a,
         e0 = bo[band];
         e1 = bo[band + 1];
         base = (int64_t)b * a.M + i0;
+        if (e0 < 0 || e1 < e0 || e1 > i1 - i0) {  // the bin must lie in the window's records
+            if (tid == 0) atomicOr(&g_snnflow_dev_err, 2u);
+            e0 = e1 = 0;
+        }
     }
     for (int j = tid; j < 2 * GB_BAND; j += GB_NT) (&acc.hi[0][0])[j] = 0, (&acc.lo[0][0])[j] = 0;
     const float* fl = a.flows[a.tf == 1 ? 0 : t] + (int64_t)b * 2 * HWp;
@@ -1017,6 +1040,25 @@ int64_t snnflow_iwe_scratch_floats(int B, int M, int T, int tf, int H, int W) {
     return LossScratch(B, M, T, tf, H, W).total;
 }
 
+static int fault_inject_env() {
+    const char* v = getenv("SNNFLOW_FAULT_INJECT");
+    return v ? atoi(v) : 0;
+}
+static const int g_fault_inject = fault_inject_env();
+
+int snnflow_device_errors(int clear) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return snnflow_set_error((int)e, hipGetErrorString(e));
+    unsigned v = 0u;
+    e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_snnflow_dev_err), sizeof(v), 0, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && clear) {
+        const unsigned z = 0u;
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_snnflow_dev_err), &z, sizeof(z), 0, hipMemcpyHostToDevice);
+    }
+    if (e != hipSuccess) return snnflow_set_error((int)e, hipGetErrorString(e));
+    return (int)v;
+}
+
 int snnflow_iwe_acc_doubles(int B, int H, int W, int tf) {
     const int64_t HWp = (int64_t)H * W;
     return (int)((int64_t)B * loss_tsplit(B, HWp, tf) * loss_chunks(HWp) * LOSS_NV);
@@ -1035,6 +1077,7 @@ int snnflow_iwe_loss_fwd(const snnflow_iwe_loss_args* a, void* stream) {
     hipLaunchKernelGGL(k_iwe_wbin, dim3(a->B * a->T), dim3(WB_NT), 0, s, *a, nbands, rec, bins, nbg,
                        reinterpret_cast<float4*>(a->images + ls.rec4), a->images + ls.rec1,
                        reinterpret_cast<int*>(a->images + ls.gbins));
+    if (g_fault_inject == 1) hipLaunchKernelGGL(k_iwe_corrupt_bins, dim3(1), dim3(64), 0, s, bins, 2 * nbands + 1);
     hipLaunchKernelGGL(k_iwe_splat, dim3(a->B * 2 * nbands), dim3(SPLAT_NT), 0, s, *a, nbands, rec, bins);
     const int chunks = loss_chunks(HWp), tsplit = loss_tsplit(a->B, HWp, a->tf);
     hipLaunchKernelGGL(k_iwe_loss, dim3(a->B * tsplit * chunks), dim3(NT), 0, s, *a, chunks, tsplit);
@@ -1060,6 +1103,7 @@ int snnflow_iwe_loss_bwd(const snnflow_iwe_loss_args* a, const float* g_loss, fl
     int* bins = reinterpret_cast<int*>(a->images + ls.gbins);
     if (a->M > 0 && a->tf != a->T)
         hipLaunchKernelGGL(k_iwe_bin, dim3(a->B * a->tf), dim3(BIN_NT), 0, s, *a, nbands, rec4, rec1, bins);
+    if (g_fault_inject == 2 && a->M > 0) hipLaunchKernelGGL(k_iwe_corrupt_bins, dim3(1), dim3(64), 0, s, bins, nbands + 1);
     hipLaunchKernelGGL(k_iwe_bwd_band, dim3(a->B * a->tf * nbands), dim3(GB_NT), gb_lds, s, *a, g_loss, g_flows,
                        rec4, rec1, bins, nbands, a->M > 0 ? 1 : 0);
     SNN_CHECK_LAUNCH();

@@ -5,6 +5,7 @@ Drop-in for the reference's ``models.model`` (LIFFireNet family), its spiking ce
 ``libsnnflow.so`` (include/snnflow.h).  Importing fails loudly if the library is missing.
 """
 from . import _lib  # noqa: F401  (loads libsnnflow.so or raises)
+from ._lib import SnnflowError, check_device_errors
 from .cells import ConvLayer, Leaky, SNNtorch_ConvLIF, SNNtorch_ConvLIFRecurrent
 from .norm import MPBN, TEBN
 from .convlif import ConvLIF, ConvLIFRecurrent
@@ -20,4 +21,4 @@ __all__ = ["LIFFireNet", "LIFFireNet_short", "LIFFireFlowNet", "LIFFireFlowNet_s
            "SNNtorch_ConvLIFRecurrent", "ConvLIF", "ConvLIFRecurrent", "ConvLayer", "Leaky", "EventWarping", "AEE",
            "NEE", "AAE", "NAAE", "AE_ofMeans", "AAE_Weighted", "AAE_Filtered", "SpikingRecEVFlowNet",
            "SpikingMultiResUNetRecurrent", "SpikingRecurrentConvLayer", "SpikingResidualBlock", "SpikingUpsampleConvLayer",
-           "ClipAdam"]
+           "ClipAdam", "SnnflowError", "check_device_errors"]

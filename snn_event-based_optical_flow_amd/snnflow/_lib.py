@@ -309,6 +309,7 @@ EXPORTS = {
     "snnflow_slab_reduce": (I32, [ctypes.POINTER(SlabDesc), I32, I32, P]),
     "snnflow_iwe_loss_fwd": (I32, [ctypes.POINTER(IweLossArgs), P]),
     "snnflow_iwe_loss_bwd": (I32, [ctypes.POINTER(IweLossArgs), P, P, P]),
+    "snnflow_device_errors": (I32, [I32]),
     "snnflow_iwe_scratch_floats": (I64, [I32, I32, I32, I32, I32, I32]),
     "snnflow_iwe_acc_doubles": (I32, [I32, I32, I32, I32]),
     "snnflow_iwe_corners": (I32, [P, P, I32, I32, F32, I32, I32, F32, I32, P, P, P]),
@@ -384,6 +385,21 @@ class SnnflowError(RuntimeError):
 def check(rc, what):
     if rc != 0:
         raise SnnflowError(f"{what} failed ({rc}): {lib.snnflow_last_error().decode(errors='replace')}")
+
+
+_DEVICE_FAULTS = {1: "event-warping forward: a bin segment outside its window's records (k_iwe_splat)",
+                  2: "event-warping backward: a bin segment outside its window's records (k_iwe_bwd_band)"}
+
+
+def check_device_errors(clear=True):
+    """Raise SnnflowError if a kernel flagged (and skipped) a device-side argument fault since the last
+    check -- e.g. a corrupted or stale loss scratch (snnflow_device_errors).  Synchronises the device."""
+    rc = lib.snnflow_device_errors(1 if clear else 0)
+    if rc < 0 or rc > 0xFFFF:
+        check(rc, "device_errors")
+    if rc:
+        what = "; ".join(v for k, v in _DEVICE_FAULTS.items() if rc & k) or f"flags {rc:#x}"
+        raise SnnflowError(f"device-side fault detected and skipped: {what}")
 
 
 class KernelTimer:

@@ -386,12 +386,24 @@ class FireNetEngine:
         return m[1], m[2]
 
     def open_chain(self, device):
+        self.bwd_task = torch._C._current_graph_task_id()
         self.slab_live = [False] * self.L
         self.flat_layout = self.flat_layout_for(self.param_list())
         o, n, _ = self.flat_layout[-1]
         self.flat = torch.empty(o + n, device=device)
         self.flat_views = True  # (gradient destinations are addressed through flat_layout)
         self.bwd_open = True
+
+    def drop_stale_chain(self):
+        """A backward chain left open by an earlier backward pass that never reached the chain's first step
+        (autograd.grad / backward(inputs=...) on an intermediate state) is abandoned: its partial weight
+        gradients and pending steps would otherwise be added to this pass's."""
+        if self.bwd_open and getattr(self, "bwd_task", None) != torch._C._current_graph_task_id():
+            if self.ws is not None:
+                self.ws.reset_acc()
+            self.bwd_open = False
+            self.pending, self.pending_layers = [], []
+            self.prep_stale = True
 
     def launch_wgrad(self, l, B, H, W, cin0, ws, stream, steps=None):
         """Deferred weight gradients of layer l over the given pending time steps (default: all;
@@ -724,15 +736,18 @@ class FireNetStep(torch.autograd.Function):
         ws = eng.workspace(B, H, W, dev)
         wfwd, wbwd = eng.prep_weights(s, refresh=eng.prep_stale)
         eng.prep_stale = False
-        ys = torch.empty(L, B, H, W, C, device=dev)
-        stats = torch.empty(L, 2, C, device=dev)
-        # all L states of the step in one allocation, back to back (a state hand-over, e.g. the
-        # bench's graph-replay detach, is then a single contiguous copy)
+        # one allocation per step: the L states back to back (a state hand-over, e.g. the bench's
+        # graph-replay detach, is then a single contiguous copy), then the pre-BN currents, the flow
+        # and the statistics (views; the per-window loop pays one allocator call instead of four)
         n1 = 2 * B * H * W * C
-        st_all = torch.empty(L * n1, device=dev)
-        sst = nhwc_state_strides(B, C, H, W)
-        states = [st_all.as_strided((2, B, C, H, W), sst, l * n1) for l in range(L)]
-        flow = torch.empty(B, 2, H, W, device=dev)
+        ny = L * B * H * W * C
+        buf = torch.empty(L * n1 + ny + 2 * B * H * W + L * 2 * C, device=dev)
+        st_all = buf[:L * n1]
+        ys = buf[L * n1:L * n1 + ny].view(L, B, H, W, C)
+        flow = buf[L * n1 + ny:L * n1 + ny + 2 * B * H * W].view(B, 2, H, W)
+        stats = buf[L * n1 + ny + 2 * B * H * W:].view(L, 2, C)
+        # [L][2][B][H][W][C] storage as L states [2, B, C, H, W] (nhwc_state_strides), in one unbind
+        states = list(st_all.view(L, 2, B, H, W, C).permute(0, 1, 2, 5, 3, 4).unbind(0))
 
         # incoming membranes / previous spikes as pointers; `keep` holds their tensors (the whole
         # previous state, or the cell's membrane cache) for the backward and the deferred wgrad
@@ -796,6 +811,10 @@ class FireNetStep(torch.autograd.Function):
         ctx.eng = eng
         ctx.root = root
         ctx.chain = chain
+        # (deferred backward) the incoming recurrent states a caller may read the gradient of, and the
+        # chain's parameter anchor, whose node runs only in backward passes that want parameter gradients
+        ctx.prev_rec = [p for l, p in enumerate(prev) if p is not None and eng.rec[l] and p.requires_grad]
+        ctx.anchor_fn = getattr(rest[L], "grad_fn", None) if len(rest) > L else None
         ctx.ext = ext
         ctx.shape = (B, H, W, cin0)
         ctx.has_prev = [p is not None for p in prev]
@@ -810,16 +829,40 @@ class FireNetStep(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_flow, *g_states):
         eng, chain = ctx.eng, ctx.chain
+        eng.drop_stale_chain()
         st = _StepBwd(ctx, g_flow, g_states)
         if chain.defer:
-            if not ctx.root:  # collected; the chain's first step (the last node autograd calls) runs them
-                chain.steps.append(st)
-                return (None,) * (3 + eng.L)
+            if chain.steps and chain.steps[0].task != st.task:  # left by an earlier pass that stopped early
+                chain.steps = []
+            if not ctx.root:
+                if _defer_ok(ctx):  # collected; the chain's first step (the last node autograd calls) runs them
+                    chain.steps.append(st)
+                    return (None,) * (3 + eng.L)
+                # the gradient of this step's incoming states is read (retain_grad, a hook), or this pass will
+                # not reach the chain's first step (autograd.grad / backward(inputs=...) of an intermediate
+                # state): this step and the later ones collected so far run now, one after the other, and
+                # return their input gradients to autograd
+                steps = [st] + chain.steps[::-1]
+                chain.steps = []
+                return _chain_backward(eng, steps, batched=False)
             steps = [st] + chain.steps[::-1]  # time order
             chain.steps = []
             if len(steps) > 1:
                 return _chain_backward(eng, steps)
         return _step_backward(eng, st)
+
+
+def _defer_ok(ctx):
+    """May a non-first step of a chain hand its backward to the chain's first step?  Not when a caller
+    reads the gradient of one of its incoming recurrent states (retain_grad or a tensor hook: the
+    batched form never hands those to autograd), and not when this backward pass will not run the
+    parameter anchor's node (no parameter gradients wanted: autograd.grad or backward(inputs=...) of an
+    intermediate state -- the first step may then never run)."""
+    for p in ctx.prev_rec:
+        if p.retains_grad or p._backward_hooks:
+            return False
+    a = ctx.anchor_fn
+    return a is None or torch._C._will_engine_execute_node(a)
 
 
 class _Chain:
@@ -838,16 +881,17 @@ class _Chain:
 class _StepBwd:
     """One FireNetStep's backward inputs, unpacked from its ctx (autograd frees a node's saved tensors
     once its backward returns; these references keep them for the chain's first step)."""
-    __slots__ = ("saved", "ptrs", "shape", "root", "ext", "has_prev", "needs", "g_flow", "g_states")
+    __slots__ = ("saved", "ptrs", "shape", "root", "ext", "has_prev", "needs", "g_flow", "g_states", "task")
 
     def __init__(self, ctx, g_flow, g_states):
+        self.task = torch._C._current_graph_task_id()
         self.saved = list(ctx.saved_tensors)
         self.ptrs, self.shape, self.root, self.ext = ctx.ptrs, ctx.shape, ctx.root, ctx.ext
         self.has_prev, self.needs = ctx.has_prev, ctx.needs_input_grad
         self.g_flow, self.g_states = g_flow, g_states
 
 
-def _chain_backward(eng, steps):
+def _chain_backward(eng, steps, batched=True):
     """The backwards of a chain's steps (time order; steps[0] is the chain's first step), issued by the
     first step's node.  Without external gradients on intermediate states, one snnflow_firenet_bwd_seq
     call: the T x (L+1) layer-steps as 2(T-1)+L+1 wavefront launches (FireNetSequence's schedule and
@@ -857,7 +901,15 @@ def _chain_backward(eng, steps):
     step's input gradients."""
     L = eng.L
     T = len(steps)
-    if _lib.TIMER is None and all(g is None for st in steps[:-1] for g in st.g_states):
+    B, H, W, _ = steps[0].shape
+    n1 = 2 * B * H * W * eng.C
+    for t in range(1, T):  # step t reads step t-1's states (one allocation, L states back to back)
+        base = steps[t - 1].saved[4].data_ptr()
+        if any(steps[t].ptrs[0][l] != base + 4 * l * n1 for l in range(L)):
+            eng.drop_stale_chain()
+            raise _lib.SnnflowError("deferred chain backward: the collected steps are not one BPTT chain "
+                                    "(set model.engine.defer_backward = False for this use)")
+    if batched and _lib.TIMER is None and all(g is None for st in steps[:-1] for g in st.g_states):
         return _chain_backward_batched(eng, steps)
     nxt = None
     for t in range(T - 1, -1, -1):
@@ -1274,6 +1326,7 @@ class FireNetSequence(torch.autograd.Function):
 
         dev = xs[0].device
         s = _lib.stream_ptr(dev)
+        eng.drop_stale_chain()
         eng.workspace(B, H, W, dev)
         ws = eng.ws
         wfwd, wbwd = eng.prep_weights(s, refresh=False)

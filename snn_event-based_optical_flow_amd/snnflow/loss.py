@@ -3,13 +3,19 @@
 
 ``event_flow_association`` only records the per-window tensors, which the kernels read
 in place through per-window pointer tables (nothing is concatenated).  ``forward`` runs
-three kernels: the warp + bilinear splat of every event into the 8 IWEs (forward/backward
-warp x {count, timestamp} x polarity) with LDS-privatised image bands; per (pixel,
-window) loss and Charbonnier smoothness terms reduced to per-block rows; a fixed-order
-fp64 reduction of the rows into the loss.  The backward runs three more: per (pixel,
-window) image and smoothness gradients; the events of every (sample, window) binned by
-the pixel band of their own pixel; per band, each event's gradient gathered from the 4
-corners of both warps and summed onto its pixel's flow in exact fixed point.
+four kernels (include/snnflow.h snnflow_iwe_loss_fwd): k_iwe_wbin bins every event of a
+(sample, window) by the 1024-pixel band of its warped corners (and, with one flow per window,
+by the 512-pixel band of its own pixel for the backward); k_iwe_splat splats each band's
+records into the 8 IWEs (forward/backward warp x {count, timestamp} x polarity) in exact
+two-word fixed point; k_iwe_loss reduces the per (pixel, window) loss and Charbonnier
+smoothness terms to per-block rows; k_iwe_finalize sums the rows in a fixed fp64 order.
+The backward (snnflow_iwe_loss_bwd) is ONE kernel, k_iwe_bwd_band -- or two when the flows
+are fewer than the windows (tf != T: k_iwe_bin forms the own-pixel binning first): per
+(sample, flow window, band) the smoothness gradient of its pixels and each binned event's
+flow gradient, formed at the 4 corners of both warps from the IWE values there and summed
+onto its pixel's flow in exact fixed point.  The images scratch therefore holds the IWEs
+AND both event binnings, and must be kept from the forward to the backward.  A corrupted
+bin table is skipped and flagged (snnflow.check_device_errors), never read out of bounds.
 """
 import ctypes
 

@@ -16,6 +16,7 @@ Difference, documented: the reference multiplies the flow by ``dt_gt / dt_input`
 plain broadcasting, which is only per-sample for a batch of one; here the ratio is applied
 per sample for any batch size (identical for B = 1 and for scalar dt).
 """
+import collections
 import ctypes
 
 import torch
@@ -23,6 +24,8 @@ import torch
 from . import _lib
 from ._lib import lib, ptr
 from .iwe import compute_pol_iwe
+
+_AEE_SCRATCH_STREAMS = 8  # AEE scratch buffers kept per metric object (one per stream, LRU)
 
 
 class BaseValidationLoss(torch.nn.Module):
@@ -108,13 +111,17 @@ class AEE(BaseValidationLoss):
         # the scratch carries the kernel's completion counter acc[0] (zero between calls: the last
         # block resets it), so it must never be shared by launches that can overlap: one scratch per
         # stream (a graph replays on the stream it was captured on, in order with eager calls there)
+        # (a stream handle may be reused after its stream is destroyed: harmless, the counter is zero
+        # between calls).  At most _AEE_SCRATCH_STREAMS streams are kept, least recently used dropped.
         stream = _lib.stream_ptr(flow.device)
-        scratch = self.__dict__.setdefault("_aee_acc", {})
+        scratch = self.__dict__.setdefault("_aee_acc", collections.OrderedDict())
         key = (flow.device, stream)
-        acc = scratch.get(key)
+        acc = scratch.pop(key, None)
         if acc is None or acc.numel() < n:
             acc = torch.zeros(n, dtype=torch.float64, device=flow.device)  # counter acc[0]: zero, kept zero
-            scratch[key] = acc
+        scratch[key] = acc  # most recently used last
+        while len(scratch) > _AEE_SCRATCH_STREAMS:
+            scratch.popitem(last=False)
         aee = torch.empty(B, device=flow.device)
         pct = torch.empty(B, device=flow.device)
         a = _lib.AeeArgs()

@@ -78,16 +78,17 @@ class ClipAdam(torch.optim.Optimizer):
                     p.grad.requires_grad_(False)
                 p.grad.zero_()
 
-    def _fast_args(self, params):
+    def _fast_args(self, params, grads):
         """The launch arguments of the previous step, reused when the parameter set, the hyper-
         parameters, the moments and the gradient layout relative to the buffer start are unchanged
-        (the eager loop gets a new gradient buffer every step, at the same relative offsets)."""
+        (the eager loop gets a new gradient buffer every step, at the same relative offsets).  One pass
+        over the parameters (the per-window loop calls this once per step)."""
         c = self.__dict__.get("_args_cache")
         if c is None or c[0] != tuple(map(id, params)) or self._moments is None or c[4] is not self._moments:
             return None
-        ptrs = [p.grad.data_ptr() for p in params]
+        ptrs = tuple(g.data_ptr() for g in grads)
         base = min(ptrs)
-        if (c[1] != tuple(x - base for x in ptrs) or c[2] != self._hyper() or c[5] != params[0].grad.device
+        if (c[1] != tuple(x - base for x in ptrs) or c[2] != self._hyper() or c[5] != grads[0].device
                 or c[6] != tuple(p.data_ptr() for p in params)):
             return None
         return c[3], base
@@ -122,10 +123,16 @@ class ClipAdam(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         group = self.param_groups[0]
-        params = [p for p in group["params"] if p.grad is not None]
+        allp = group["params"]
+        grads = [p.grad for p in allp]
+        if any(g is None for g in grads):
+            params = [p for p, g in zip(allp, grads) if g is not None]
+            grads = [g for g in grads if g is not None]
+        else:
+            params = allp
         if not params:
             return loss
-        fast = self._fast_args(params)
+        fast = self._fast_args(params, grads)
         if fast is not None:
             a, base = fast
             a.grad = base

@@ -32,7 +32,7 @@ pytestmark = pytest.mark.gpu
 # (G1.bn.weight).  cfg3 sums 2x the pixels per channel and its oracle's own fp32 sums round more:
 # 7.7e-6 (head.bn.bias).  C=32: 2.3e-5 (pred.conv2d.bias: two sums over 1.3 M pixel-steps of terms
 # of both signs; the conv weights 3-4e-6).
-GRAD_TOL = {"cfg2": 6e-6, "cfg3": 1.6e-5, "cfg2-C32": 5e-5}
+GRAD_TOL = {"cfg2": 6e-6, "cfg3": 1.6e-5, "cfg2-C32": 5e-5, "cfg1": 1e-5}
 
 
 def _rel(a, b):
@@ -170,17 +170,18 @@ def _report(tag, r, per_layer):
           + ", ".join(f"{k}={v:.1e}" for k, v in r["grad_rel"].items()))
 
 
-# (tag, batch, resolution, base_num_channels): BASELINE cfg2; cfg3 (256x256, B=4); the README /
-# default-checkpoint width C=32 at the cfg2 shape
-HEADLINE = [("cfg2", 8, 128, 8), ("cfg3", 4, 256, 8), ("cfg2-C32", 8, 128, 32)]
+# (tag, batch, resolution, base_num_channels, windows): BASELINE cfg2; cfg3 (256x256, B=4); the README /
+# default-checkpoint width C=32 at the cfg2 shape; BASELINE configs[0] (cfg1: 128x128, T=5, batch 1 --
+# the degenerate case of the batch statistics: one sequence per BatchNorm batch)
+HEADLINE = [("cfg2", 8, 128, 8, 10), ("cfg3", 4, 256, 8, 10), ("cfg2-C32", 8, 128, 32, 10), ("cfg1", 1, 128, 8, 5)]
 
 
 @pytest.mark.parametrize("path", ["sequence", "per_step"])
-@pytest.mark.parametrize("tag,B,H,C", HEADLINE, ids=[h[0] for h in HEADLINE])
-def test_cfg2_train_step_vs_oracle(dev, path, tag, B, H, C):
+@pytest.mark.parametrize("tag,B,H,C,T", HEADLINE, ids=[h[0] for h in HEADLINE])
+def test_cfg2_train_step_vs_oracle(dev, path, tag, B, H, C, T):
     from snnflow.synthetic import make_window
 
-    T, N = 10, 1000
+    N = 1000
     gen = torch.Generator(device=dev).manual_seed(1)
     wins = [make_window(B, N, H, H, gen, dev) for _ in range(T)]
     cpu_wins = [{k: v.cpu() for k, v in w.items()} for w in wins]
@@ -314,18 +315,19 @@ def test_clip_grad_norm_large_vs_torch(dev):
         np.testing.assert_allclose(p.grad.cpu().numpy(), v.numpy() * coef, rtol=1e-6, atol=1e-12)
 
 
-def test_cfg2_eval_vs_oracle(dev):
+@pytest.mark.parametrize("tag,B,T", [("cfg2", 8, 10), ("cfg1", 1, 5)], ids=["cfg2", "cfg1"])
+def test_cfg2_eval_vs_oracle(dev, tag, B, T):
     """The evaluation path at cfg2's shape (eval_flow.py:208-338: model.eval(), BatchNorm on its
     running statistics, forward only, AEE per window): T = 10 windows of 1000 events at 128 x 128,
     B = 8, through forward_sequence (the wavefront launches the bench's --eval line times) against
     the oracle in eval mode, flip-corrected like the train step (a differing spike must lie within
     1e-4 of the threshold).  Running statistics are perturbed away from (0, 1) so that the eval
     BatchNorm is not the identity.  Flows within 1e-4, AEE of a synthetic ground truth per window
-    within 1e-4 (north star)."""
+    within 1e-4 (north star).  Also at BASELINE configs[0] (T = 5 windows, batch 1)."""
     from oracle import lif_ref
     from snnflow.synthetic import make_window
 
-    B, H, T, N, C = 8, 128, 10, 1000, 8
+    H, N, C = 128, 1000, 8
     gen = torch.Generator(device=dev).manual_seed(7)
     wins = [make_window(B, N, H, H, gen, dev) for _ in range(T)]
     cpu_wins = [{k: v.cpu() for k, v in w.items()} for w in wins]
@@ -360,7 +362,7 @@ def test_cfg2_eval_vs_oracle(dev):
         gt = (torch.rand(B, 2, H, H, generator=gtg) - 0.5) * 8.0
         ours, theirs = _aee_pair(flows[t], rflows[t], gt, cpu_wins[t]["event_mask"], dev)
         worst_aee = max(worst_aee, float(np.abs(ours - theirs).max()))
-    print(f"\n[cfg2 eval] spike flips {flips} (away from the threshold: {hard}); max|dflow| {worst_flow:.2e}; "
+    print(f"\n[{tag} eval] spike flips {flips} (away from the threshold: {hard}); max|dflow| {worst_flow:.2e}; "
           f"max|dAEE| over {T} windows {worst_aee:.2e}")
     assert hard == 0
     assert worst_flow <= 1e-4 and worst_aee <= 1e-4

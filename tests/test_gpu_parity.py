@@ -10,6 +10,8 @@ corner indices: bit-exact.  Spikes: identical except where |v - theta| < 1e-4
 teacher forcing or configurations verified to have no flips).
 """
 import numpy as np
+import os
+
 import pytest
 import torch
 
@@ -1724,6 +1726,77 @@ def test_per_step_chain_backward_batched(dev, case):
     print(f"\n[{case}] batched chain backward vs per-node: worst gradient rel-L2 {worst:.2e}")
 
 
+def test_per_step_chain_intermediate_state_gradients(dev):
+    """Reading the gradient of an intermediate recurrent state of the per-window loop (retain_grad, a
+    tensor hook, torch.autograd.grad with that state as the input) gives the same values whether the
+    engine defers the chain's backward to its first step (defer_backward, the default) or runs every
+    node itself: a node whose incoming state is read, or a pass that will not reach the chain's parameter
+    anchor, runs its backward at once.  A full backward after such a partial pass gives the parameter
+    gradients of a fresh run (the partial pass's open chain is dropped, not added in)."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(22)
+    B, H, W, T = 2, 48, 64, 5
+    base = snnflow.LIFFireNet(lif_ref.make_unet_kwargs(base_num_channels=8)).to(dev).train()
+    gen = torch.Generator(device=dev).manual_seed(6)
+    wins = [make_window(B, 500, H, W, gen, dev) for _ in range(T)]
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+
+    def run(m, mode):
+        m.reset_states()
+        lf = snnflow.EventWarping(cfg, dev)
+        kept, hooked = None, []
+        for t in range(T):
+            w = wins[t]
+            out = m(w["event_voxel"], w["event_cnt"])
+            lf.event_flow_association(out["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            if t == 2:
+                kept = m._states[1]  # G1 (recurrent) after step 2
+                if mode == "retain":
+                    kept.retain_grad()
+                    m._states[4].register_hook(lambda g: hooked.append(g.detach().clone()))
+        loss = lf()
+        if mode == "autograd_grad":
+            (g,) = torch.autograd.grad(loss, [kept], retain_graph=True)
+            loss.backward()  # and then the full pass
+            return g.detach().cpu(), [p.grad.detach().cpu().clone() for p in m.parameters()]
+        loss.backward()
+        return (kept.grad.detach().cpu(), hooked[0].cpu()), [p.grad.detach().cpu().clone() for p in m.parameters()]
+
+    res = {}
+    for defer in (False, True):
+        for mode in ("retain", "autograd_grad"):
+            m = copy.deepcopy(base)
+            m.engine.defer_backward = defer
+            res[(defer, mode)] = run(m, mode)
+
+    def rel(a, b):
+        return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+    (sg_ref, hk_ref), g_ref = res[(False, "retain")]
+    (sg, hk), g = res[(True, "retain")]
+    assert sg_ref.abs().sum() > 0 and hk_ref.abs().sum() > 0
+    e_state, e_hook = rel(sg, sg_ref), rel(hk, hk_ref)
+    e_par = max(rel(a, b) for a, b in zip(g, g_ref))
+    ga_ref, gp_ref = res[(False, "autograd_grad")]
+    ga, gp = res[(True, "autograd_grad")]
+    e_ag = rel(ga, ga_ref)
+    e_ag_state = rel(ga_ref, sg_ref)
+    e_after = max(rel(a, b) for a, b in zip(gp, g_ref))
+    e_after_ref = max(rel(a, b) for a, b in zip(gp_ref, g_ref))
+    print(f"\n[intermediate state grads] retain_grad {e_state:.2e}, hook {e_hook:.2e}, params {e_par:.2e}; "
+          f"autograd.grad {e_ag:.2e} (vs retain_grad {e_ag_state:.2e}); full pass after it {e_after:.2e} "
+          f"(per-node engine {e_after_ref:.2e})")
+    assert e_state <= 1e-5 and e_hook <= 1e-5 and e_par <= 1e-5
+    assert e_ag <= 1e-5 and e_ag_state <= 1e-5
+    assert e_after <= 1e-5 and e_after_ref <= 1e-5
+
+
 def test_iwe_loss_rejects_misshaped_inputs(dev):
     """EventWarping validates what its kernels index by (B, H, W): a flow tensor passed where the
     reference takes a list of flow maps (``list(tensor)`` splits it into per-sample [2, H, W] maps),
@@ -1754,6 +1827,63 @@ def test_iwe_loss_rejects_misshaped_inputs(dev):
     lf.event_flow_association([flow], ev, pol, mask)
     lf().backward()
     assert flow.grad is not None and bool(torch.isfinite(flow.grad).all())
+
+
+_FAULT_SCRIPT = r"""
+import sys, torch
+sys.path[:0] = [REPO, PKG]
+import snnflow
+dev = torch.device("cuda:0")
+H, W, B, N, T = 64, 64, 2, 500, 3
+cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+       "model": {"mask_output": True}}
+gen = torch.Generator().manual_seed(5)
+lf = snnflow.EventWarping(cfg, dev)
+flows = []
+for t in range(T):
+    ev = torch.stack([torch.rand(B, N, generator=gen), torch.randint(0, H, (B, N), generator=gen).float(),
+                      torch.randint(0, W, (B, N), generator=gen).float(), torch.ones(B, N)], dim=2).to(dev)
+    pol = torch.stack([torch.ones(B, N), torch.zeros(B, N)], dim=2).to(dev)
+    f = (0.3 * torch.randn(B, 2, H, W, generator=gen)).to(dev).requires_grad_()
+    flows.append(f)
+    lf.event_flow_association([f], ev, pol, torch.ones(B, 1, H, W, device=dev))
+loss = lf()
+loss.backward()
+try:
+    snnflow.check_device_errors()
+    print("NO-ERROR")
+except snnflow.SnnflowError as e:
+    print("SNNFLOW-ERROR", e)
+snnflow.check_device_errors()  # cleared: a second check is clean
+print("finite", bool(torch.isfinite(loss).item()), all(bool(torch.isfinite(f.grad).all()) for f in flows))
+"""
+
+
+@pytest.mark.parametrize("where", [1, 2], ids=["forward_bins", "backward_bins"])
+def test_iwe_loss_corrupted_bin_table_is_flagged(where):
+    """A corrupted bin table in the loss scratch (the cause of a round-5 probe's device fault: a timing
+    variant of the bin kernel that left its table unwritten) is bounded inside k_iwe_splat /
+    k_iwe_bwd_band: the segment is skipped, the library's device error flag is set, and
+    snnflow.check_device_errors() raises a clean SnnflowError -- no out-of-bounds access, the process and
+    the GPU stay healthy.  The library's fault-injection hook (SNNFLOW_FAULT_INJECT, read at load)
+    overwrites one entry of the forward's (1) or the backward's (2) table, in a fresh process."""
+    import subprocess
+    import sys as _sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = f"REPO, PKG = {repo!r}, {os.path.join(repo, 'snn_event-based_optical_flow_amd')!r}\n" + _FAULT_SCRIPT
+    env = dict(os.environ, SNNFLOW_FAULT_INJECT=str(where))
+    r = subprocess.run([_sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "SNNFLOW-ERROR" in r.stdout, r.stdout + r.stderr
+    want = "k_iwe_splat" if where == 1 else "k_iwe_bwd_band"
+    assert want in r.stdout, r.stdout
+    assert "finite True True" in r.stdout, r.stdout
+    # without the hook the same script is clean
+    env.pop("SNNFLOW_FAULT_INJECT")
+    r = subprocess.run([_sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "NO-ERROR" in r.stdout, r.stdout + r.stderr
+    print(f"\n[fault {where}] {r.stdout.strip().splitlines()[0]}")
 
 
 @pytest.mark.parametrize("recurrent", [False, True])
