@@ -458,8 +458,11 @@ def _dp_check(world, rank, step_parts, params):
         sync_grads()
     torch.cuda.synchronize()
     reduced = grads()
-    locals_ = [torch.empty_like(local) for _ in range(world)]
-    dist.all_gather(locals_, local)
+    # (gathered through device tensors: the nccl backend has no CPU collectives)
+    cdev = flat.device if flat is not None else params[0].device
+    locals_ = [torch.empty_like(local, device=cdev) for _ in range(world)]
+    dist.all_gather(locals_, local.to(cdev))
+    locals_ = [t.cpu() for t in locals_]
     want = locals_[0].double()
     for t in locals_[1:]:
         want = want + t.double()
@@ -470,9 +473,10 @@ def _dp_check(world, rank, step_parts, params):
     else:
         update()
     torch.cuda.synchronize()
-    pflat = torch.cat([p.detach().reshape(-1).cpu() for p in params])
+    pflat = torch.cat([p.detach().reshape(-1) for p in params])
     ps = [torch.empty_like(pflat) for _ in range(world)]
     dist.all_gather(ps, pflat)
+    ps = [t.cpu() for t in ps]
     pdiff = float(max((t - ps[0]).abs().max() for t in ps[1:])) if world > 1 else 0.0
     if rank == 0:
         print(json.dumps({"dp_check": {"world": world, "backend": dist.get_backend(), "grad_numel": local.numel(), "allreduce_rel_err": err,
