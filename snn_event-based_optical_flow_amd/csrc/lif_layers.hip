@@ -44,6 +44,9 @@
 #ifndef SNNFLOW_TRACE
 #define SNNFLOW_TRACE 0
 #endif
+#ifndef SNNFLOW_BWD_GATHER32
+#define SNNFLOW_BWD_GATHER32 1  // C = 32 backward: batch-norm sums gathered by all threads, 2C for every block
+#endif
 #ifndef SNNFLOW_SWZ
 #define SNNFLOW_SWZ 1  // C = 8 recurrent backward: bank-conflict-free LDS layouts of the packed x|s tile and dgrad staging
 #endif
@@ -1447,7 +1450,7 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     // other neuron-gradient sums only block 0 (a third of the loads and of the reduction elsewhere)
     // (C = 32: one gather of all sums -- the second reduction array would take the slot kernel's LDS
     // past two blocks per CU)
-    constexpr int NSUM = SNNFLOW_BWD_ACC(C), NBN = C <= 16 ? 2 * C : NSUM;
+    constexpr int NSUM = SNNFLOW_BWD_ACC(C), NBN = (C <= 16 || SNNFLOW_BWD_GATHER32) ? 2 * C : NSUM;
     const bool lead = g.bid == 0;
     constexpr int NL = NSUM - NBN > 0 ? NSUM - NBN : 1;
     AccGather<NBN> gat;
@@ -1542,6 +1545,11 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     if constexpr (EARLY_G) {
         acc_gather_reduce<NBN>(gat, sums);
         if (NBN < NSUM && lead) acc_gather_reduce<NL>(gat_l, sums + NBN);  // (block-uniform: barriers inside)
+    } else if constexpr (SNNFLOW_BWD_GATHER32) {
+        // C = 32: all NTB threads, the reduction scratch in the pool (not live before stage A)
+        double* red = reinterpret_cast<double*>(lds);
+        acc_gather_pool<NBN, NTB>(a.acc_in, NSUM, sums, red);
+        if (NBN < NSUM && lead) acc_gather_pool<NL, NTB>(a.acc_in + NBN, NSUM, sums + NBN, red);
     } else {
         acc_gather<NBN>(a.acc_in, NSUM, sums);
         if (NBN < NSUM && lead) acc_gather<NL>(a.acc_in + NBN, NSUM, sums + NBN);
@@ -2459,6 +2467,32 @@ __global__ __launch_bounds__(NT * 2, (kWgPf<C, REC> ? 1 : 4)) void k_wgrad_bf(sn
 //   * recurrent cells stage S into the X buffer after the X pass (one X buffer: G^T 33 KB + X^T 26 KB
 //     + BN coefficients 20 KB = 80 KB of LDS, two blocks per CU; <= 128 VGPRs).
 // ---------------------------------------------------------------------------
+// A lane's 36 slab elements of one C = 32 weight-gradient tile pair (rows co0 .. co0+3, column ci, the
+// 9 taps; v(j) gives tap j's four values): written, or added to the old values -- every old value is
+// loaded before the first add (a conditional load per element made the compiler wait 36 round trips).
+template <typename F>
+__device__ inline void slab_rmw_36(float* slab, int co0, int ci, int accumulate, F&& v) {
+    constexpr int C = 32;
+    float old[9][4];
+    if (accumulate) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) old[j][r4] = slab[((int64_t)(co0 + r4) * C + ci) * 9 + j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < 9; ++j)
+#pragma unroll
+            for (int r4 = 0; r4 < 4; ++r4) old[j][r4] = 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const f32x4 x = v(j);
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) slab[((int64_t)(co0 + r4) * C + ci) * 9 + j] = accumulate ? old[j][r4] + x[r4] : x[r4];
+    }
+}
+
 template <bool REC>
 __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_bf32(snnflow_wgrad_args) {
     constexpr int C = 32, NTB = NT * 2, Q = C / 4;
@@ -2659,16 +2693,9 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_bf32(snnflow_wgrad_args) {
         if (rg == 0) {
             float* slab = (sidx == 0 ? ap->slab_ff : ap->slab_rec) + blk * (C * C * 9);
             const int ci = nt * 16 + m;
-#pragma unroll
-            for (int j = 0; j < 9; ++j) {
-                const f32x4 v = acc[sidx][j] + *reinterpret_cast<const f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4);
-#pragma unroll
-                for (int r4 = 0; r4 < 4; ++r4) {
-                    const int co = mt * 16 + 4 * g + r4;
-                    float* d = slab + ((int64_t)co * C + ci) * 9 + j;
-                    *d = accumulate ? *d + v[r4] : v[r4];
-                }
-            }
+            slab_rmw_36(slab, mt * 16 + 4 * g, ci, accumulate, [&](int j) {
+                return acc[sidx][j] + *reinterpret_cast<const f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4);
+            });
         }
         __syncthreads();
     }
@@ -2741,6 +2768,9 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_b32(snnflow_wgrad_args) {
 
     float4 rg4[O::R], ry4[O::R];
     unsigned xw = 0u;
+    // the loads are unconditional (an element outside the image reads element 0; the staging zeroes G
+    // there): a conditional load made the compiler wait for each pair before issuing the next
+    static_assert(O::E % NTB == 0, "every thread holds O::R elements");
     auto issue = [&](int t) {
         const auto& sp = ap->steps[t];
 #pragma unroll
@@ -2749,10 +2779,10 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_b32(snnflow_wgrad_args) {
             const int p = e / Q, q = e - p * Q;
             const int ty = p / TW, tx = p - ty * TW;
             const int h = tl.h0 + ty, w = tl.w0 + tx;
-            const bool ok = e < O::E && h < H && w < W;
+            const bool ok = h < H && w < W;
             const int64_t k = ok ? (((int64_t)tl.b * H + h) * W + w) * Q + q : 0;
-            rg4[i] = ok ? reinterpret_cast<const float4*>(sp.g_cur)[k] : z4;
-            ry4[i] = ok ? reinterpret_cast<const float4*>(sp.y)[k] : z4;
+            rg4[i] = reinterpret_cast<const float4*>(sp.g_cur)[k];
+            ry4[i] = reinterpret_cast<const float4*>(sp.y)[k];
         }
         const uint8_t* xb = in_bits(t);
         xw = (xb != nullptr && hok) ? spk_load_bits<C>(xb, hpix) : 0u;
@@ -2868,16 +2898,9 @@ __global__ __launch_bounds__(NT * 2, 4) void k_wgrad_b32(snnflow_wgrad_args) {
     if (rg == 0) {
         float* slab = (src == 0 ? ap->slab_ff : ap->slab_rec) + blk * (C * C * 9);
         const int ci = nt * 16 + m;
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-            const f32x4 v = acc[j] + *reinterpret_cast<const f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4);
-#pragma unroll
-            for (int r4 = 0; r4 < 4; ++r4) {
-                const int co = mt * 16 + 4 * g + r4;
-                float* d = slab + ((int64_t)co * C + ci) * 9 + j;
-                *d = accumulate ? *d + v[r4] : v[r4];
-            }
-        }
+        slab_rmw_36(slab, mt * 16 + 4 * g, ci, accumulate, [&](int j) {
+            return acc[j] + *reinterpret_cast<const f32x4*>(red + ((tg * 9 + j) * 64 + lane) * 4);
+        });
     }
 }
 
@@ -4454,7 +4477,8 @@ int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block) {
 }
 int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : 0; }
 
-static int g_wg_bits = env_int("SNNFLOW_WG_BITS", 1);  // A/B: 0 = k_wgrad_bf32 / k_wgrad_bf on the bit planes
+static int g_wg_bits = env_int("SNNFLOW_WG_BITS", 1);
+static int g_wg_t32 = env_int("SNNFLOW_WG_T32", 1);  // A/B: 0 = k_wgrad_b32 (channel-major fp32 G^T)  // A/B: 0 = k_wgrad_bf32 / k_wgrad_bf on the bit planes
 static bool wgrad_all_x_bits(const snnflow_wgrad_args* a) {
     for (int t = 0; t < a->nsteps; ++t)
         if (!a->steps[t].x_bits) return false;

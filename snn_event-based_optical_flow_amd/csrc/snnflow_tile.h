@@ -7,6 +7,10 @@
 
 #include "snnflow_dev.h"
 
+#ifndef SNNFLOW_PIN_PF
+#define SNNFLOW_PIN_PF 1  // C = 16 / 32 conv MFMA loops: pin the fragment prefetch one k-step ahead (sched_barrier)
+#endif
+
 namespace snnflow {
 
 // ---------------------------------------------------------------------------
@@ -513,6 +517,10 @@ __device__ void mfma_conv3x3_bf3g(const AT* src, const __bf16* __restrict__ frag
 #pragma unroll
                 for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + ntb + nt) * 3 + q) * 64];
         }
+        // keep the next k-step's fragment loads here, a whole k-step of MFMAs ahead of their use (the
+        // scheduler otherwise sinks them next to their first MFMA under register pressure: an L2 round
+        // trip exposed every few MFMAs)
+        if constexpr (SNNFLOW_PIN_PF) __builtin_amdgcn_sched_barrier(0);
         int tap, c0;
         bf3_k<KIN>(i, g, tap, c0);
         const int ky = tap / 3, kx = tap - 3 * (tap / 3);
@@ -632,6 +640,10 @@ __device__ void mfma_dgrad_bf6g(const __bf16* src3, const __bf16* __restrict__ f
 #pragma unroll
                 for (int q = 0; q < 3; ++q) nxt[nt][q] = fv[(((i + 1) * G::NNT + ntb + nt) * 3 + q) * 64];
         }
+        // keep the next k-step's fragment loads here, a whole k-step of MFMAs ahead of their use (the
+        // scheduler otherwise sinks them next to their first MFMA under register pressure: an L2 round
+        // trip exposed every few MFMAs)
+        if constexpr (SNNFLOW_PIN_PF) __builtin_amdgcn_sched_barrier(0);
         int tap, c0;
         bf3_k<KIN>(i, g, tap, c0);
         const int ky = tap / 3, kx = tap - 3 * (tap / 3);
@@ -879,6 +891,38 @@ __device__ void acc_gather(const double* acc, int n, double* out) {
     constexpr int TPJ = NT / M;
     constexpr int PER = (kAccShards + TPJ - 1) / TPJ;
     __shared__ double red[TPJ * M];
+    const int tid = threadIdx.x, st = acc_stride(n);
+    if (tid < TPJ * M) {
+        const int j = tid % M, g = tid / M;
+        double v[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int sh = g + k * TPJ;
+            v[k] = sh < kAccShards ? acc[sh * st + j] : 0.0;
+        }
+        double sum = 0.0;
+#pragma unroll
+        for (int k = 0; k < PER; ++k) sum += v[k];
+        red[g * M + j] = sum;
+    }
+    __syncthreads();
+    if (tid < M) {
+        double sum = 0.0;
+        for (int g = 0; g < TPJ; ++g) sum += red[g * M + tid];
+        out[tid] = sum;
+    }
+    __syncthreads();
+}
+
+// The same over NTH threads with the reduction scratch supplied by the caller (a region of the
+// block's LDS pool that is not live yet): no static LDS of its own, and TPJ = NTH / M threads per sum,
+// each summing PER = 32 / TPJ shards (C = 32 backward: 2C = 64 sums x 8 threads, 4 loads each,
+// instead of 162 x 1 thread with 32 loads in flight and 32 dependent fp64 adds).
+template <int M, int NTH>
+__device__ void acc_gather_pool(const double* acc, int n, double* out, double* red) {
+    static_assert(M >= 1 && M <= NTH, "acc_gather_pool: M sums");
+    constexpr int TPJ = NTH / M;
+    constexpr int PER = (kAccShards + TPJ - 1) / TPJ;
     const int tid = threadIdx.x, st = acc_stride(n);
     if (tid < TPJ * M) {
         const int j = tid % M, g = tid / M;
