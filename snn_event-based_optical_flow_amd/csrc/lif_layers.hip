@@ -4477,8 +4477,7 @@ int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block) {
 }
 int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : 0; }
 
-static int g_wg_bits = env_int("SNNFLOW_WG_BITS", 1);
-static int g_wg_t32 = env_int("SNNFLOW_WG_T32", 1);  // A/B: 0 = k_wgrad_b32 (channel-major fp32 G^T)  // A/B: 0 = k_wgrad_bf32 / k_wgrad_bf on the bit planes
+static int g_wg_bits = env_int("SNNFLOW_WG_BITS", 1);  // A/B: 0 = k_wgrad_bf32 / k_wgrad_bf on the bit planes
 static bool wgrad_all_x_bits(const snnflow_wgrad_args* a) {
     for (int t = 0; t < a->nsteps; ++t)
         if (!a->steps[t].x_bits) return false;
