@@ -1468,13 +1468,17 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     }
     const NeuronGradRegs ngr =
         load_neuron_grad(a.n, a.stats, C, a.ng, a.accumulate, a.has_pred, a.g_pred_w, a.g_pred_b, g.bid == 0);
-    LifCoef pk = {0.f, 0.f, 0.f, 0.f};
-    float pmu = 0.f;
+    // layer l-1's LIF parameters: the raw values loaded here, the coefficients formed after the halo
+    // loads are issued (formed here, the compiler waited for these loads before issuing the halo's)
+    float praw[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // mean, invstd, gamma, bias, beta, theta
     if constexpr (LIF_IN) {
-        if (tid < CIN) {
-            pk = lif_coef(a.prev, a.prev_stats, CIN, tid);
-            pmu = a.prev_stats[tid];
-        }
+        const int c = tid < CIN ? tid : 0;
+        praw[0] = a.prev_stats[c];
+        praw[1] = a.prev_stats[CIN + c];
+        praw[2] = a.prev.bn_weight[c];
+        praw[3] = a.prev.bn_bias[c];
+        praw[4] = a.prev.beta[c];
+        praw[5] = a.prev.threshold[c];
     }
 
     constexpr bool WL = LB::WL, BF6 = LB::BF6, FLDS = BF6 && C == 8;  // FLDS: fragments in LDS
@@ -1577,8 +1581,13 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
     }
     if constexpr (LIF_IN) {
         if (tid < CIN) {
+            LifCoef pk;  // lif_coef's arithmetic on the raw values
+            pk.alpha = praw[1] * praw[2];
+            pk.shift = praw[3] - praw[0] * pk.alpha;
+            pk.beta = fminf(fmaxf(praw[4], 0.0f), 1.0f);
+            pk.theta = praw[5];
             pcoef[tid] = pk;
-            pmean[tid] = pmu;
+            pmean[tid] = praw[0];
         }
     }
     __syncthreads();

@@ -399,7 +399,11 @@ struct FragStage {
             const int nt = rest % G::NNT, ch = rest / G::NNT, n = nt * 16 + (lane & 15);
             int tap, c0;
             bf3_k<KIN>(ch, lane >> 4, tap, c0);
-            r[i] = (e < E && tap < 9 && n < NOUT) ? wB[(tap * NOUT + n) * KIN + c0 + j] : 0.0f;
+            // unconditional load (index 0 where the element is padding), selected after: a conditional
+            // load made the compiler wait before issuing the next one
+            const bool ok = e < E && tap < 9 && n < NOUT;
+            const float v = wB[ok ? (tap * NOUT + n) * KIN + c0 + j : 0];
+            r[i] = ok ? v : 0.0f;
         }
     }
     // Two convs sharing the A operand in one B operand (NOUT <= 8, one n-tile): columns n < 8 from wB0,
@@ -414,7 +418,9 @@ struct FragStage {
             bf3_k<KIN>(ch, lane >> 4, tap, c0);
             const float* w = n < 8 ? wB0 : wB1;
             const int nn = n & 7;
-            r[i] = (e < E && tap < 9 && nn < NOUT) ? w[(tap * NOUT + nn) * KIN + c0 + j] : 0.0f;
+            const bool ok = e < E && tap < 9 && nn < NOUT;
+            const float v = w[ok ? (tap * NOUT + nn) * KIN + c0 + j : 0];
+            r[i] = ok ? v : 0.0f;
         }
     }
     __device__ inline void store(__bf16* lds) const {
@@ -859,7 +865,9 @@ __device__ inline void acc_gather_load(const double* acc, int n, AccGather<M>& r
 #pragma unroll
     for (int k = 0; k < A::PER; ++k) {
         const int sh = g + k * A::TPJ;
-        r.v[k] = (tid < A::TPJ * M && sh < kAccShards) ? ld_f64<SC1>(acc + sh * st + j) : 0.0;
+        const bool ok = tid < A::TPJ * M && sh < kAccShards;
+        const double v = ld_f64<SC1>(acc + (ok ? sh * st + j : 0));  // unconditional (see FragStage::load)
+        r.v[k] = ok ? v : 0.0;
     }
 }
 

@@ -137,11 +137,27 @@ __device__ inline void dom_pix(const PixDom& d, int n, int& b, int& y, int& x) {
 struct LifQuad { float lam[4], th[4]; };
 __device__ inline LifQuad lif_quad(const snnflow_unet_conv_args& a, int m) {
     LifQuad q;
+    if (a.epi != SNNFLOW_UNET_EPI_LIF) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            q.lam[r] = 0.0f;
+            q.th[r] = 1.0f;
+        }
+        return q;
+    }
+    // the eight loads unconditional (channel clamped to the last one; unused there): one round trip
+    float lk[4], t0[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const bool ok = a.epi == SNNFLOW_UNET_EPI_LIF && m + r < a.M;
-        q.lam[r] = ok ? 1.0f / (1.0f + expf(-a.leak[m + r])) : 0.0f;
-        const float th0 = ok ? a.thresh[m + r] : 1.0f;
+        const int c = m + r < a.M ? m + r : a.M - 1;
+        lk[r] = a.leak[c];
+        t0[r] = a.thresh[c];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const bool ok = m + r < a.M;
+        q.lam[r] = ok ? 1.0f / (1.0f + expf(-lk[r])) : 0.0f;
+        const float th0 = ok ? t0[r] : 1.0f;
         q.th[r] = th0 < 0.01f ? 0.01f : th0;
     }
     return q;
@@ -201,6 +217,85 @@ __device__ inline void conv_epilogue(const snnflow_unet_conv_args& a, const PixD
     *reinterpret_cast<float4*>(a.current + e0) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<uint2*>(a.act + n * a.act_pitch + m) =
         make_uint2((uint32_t)ob16[0] | ((uint32_t)ob16[1] << 16), (uint32_t)ob16[2] | ((uint32_t)ob16[3] << 16));
+}
+
+// The epilogue of a lane's four output quads (channels m .. m+3 of domain pixels nd[j], j = 0..3; lanes
+// whose m >= M or nd[j] >= P skip that quad): every load the four need (the old output values, the
+// previous state, the residual) is issued before the first use -- one round trip instead of one per quad
+// (a load inside conv_epilogue's conditionals made the compiler wait for it before the next quad).
+// Loads of skipped quads read element 0 of the same tensor; the values are not used.
+__device__ inline void conv_epilogue4(const snnflow_unet_conv_args& a, const PixDom& dom, int m, const int (&nd)[4],
+                                      const fx4 (&v)[4], const LifQuad& lq) {
+    const int64_t Pfull = (int64_t)a.B * a.Ho * a.Wo;
+    const int64_t plane = Pfull * a.M;
+    bool ok[4];
+    int64_t n[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ok[j] = m < a.M && nd[j] < dom.P;
+        int ob, oy, ox;
+        dom_pix(dom, ok[j] ? nd[j] : 0, ob, oy, ox);
+        n[j] = ((int64_t)ob * a.Ho + oy) * a.Wo + ox;
+    }
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (a.epi == SNNFLOW_UNET_EPI_STORE) {
+        if (m + 3 >= a.M) {  // a partial channel quad (M not a multiple of 4): element-wise
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (ok[j]) conv_epilogue(a, dom, nd[j], m, v[j][0], v[j][1], v[j][2], v[j][3], lq);
+            return;
+        }
+        float4 old[4] = {z4, z4, z4, z4};
+        if (a.accumulate) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) old[j] = *reinterpret_cast<const float4*>(a.out + (ok[j] ? n[j] * a.ld + m : 0));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!ok[j]) continue;
+            float4 val = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
+            if (a.accumulate) val = make_float4(old[j].x + val.x, old[j].y + val.y, old[j].z + val.z, old[j].w + val.w);
+            *reinterpret_cast<float4*>(a.out + n[j] * a.ld + m) = val;
+        }
+        return;
+    }
+    // ConvLIF (M = hidden channels, a multiple of 4): previous state and residual of all four quads first
+    float4 tv[4] = {z4, z4, z4, z4}, tz[4] = {z4, z4, z4, z4};
+    uint2 rr[4] = {make_uint2(0u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u), make_uint2(0u, 0u)};
+    if (a.prev_state) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t e0 = ok[j] ? n[j] * a.M + m : 0;
+            tv[j] = *reinterpret_cast<const float4*>(a.prev_state + e0);
+            tz[j] = *reinterpret_cast<const float4*>(a.prev_state + plane + e0);
+        }
+    }
+    if (a.residual) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rr[j] = *reinterpret_cast<const uint2*>(a.residual + (ok[j] ? n[j] * a.res_pitch + m : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (!ok[j]) continue;
+        const int64_t e0 = n[j] * a.M + m;
+        const float vp[4] = {tv[j].x, tv[j].y, tv[j].z, tv[j].w}, zp[4] = {tz[j].x, tz[j].y, tz[j].z, tz[j].w};
+        const float rs[4] = {bf2f(rr[j].x & 0xffff), bf2f(rr[j].x >> 16), bf2f(rr[j].y & 0xffff), bf2f(rr[j].y >> 16)};
+        float vo[4], zo[4];
+        uint16_t ob16[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float lam = lq.lam[r], th = lq.th[r];
+            vo[r] = a.hard_reset ? ((vp[r] * lam) * (1.0f - zp[r])) + ((1.0f - lam) * v[j][r])
+                                 : ((vp[r] * lam) + ((1.0f - lam) * v[j][r])) - (zp[r] * th);
+            zo[r] = (vo[r] - th > 0.0f) ? 1.0f : 0.0f;
+            ob16[r] = f2bf(a.residual ? zo[r] + rs[r] : zo[r]);
+        }
+        *reinterpret_cast<float4*>(a.state + e0) = make_float4(vo[0], vo[1], vo[2], vo[3]);
+        *reinterpret_cast<float4*>(a.state + plane + e0) = make_float4(zo[0], zo[1], zo[2], zo[3]);
+        *reinterpret_cast<float4*>(a.current + e0) = make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
+        *reinterpret_cast<uint2*>(a.act + n[j] * a.act_pitch + m) =
+            make_uint2((uint32_t)ob16[0] | ((uint32_t)ob16[1] << 16), (uint32_t)ob16[2] | ((uint32_t)ob16[3] << 16));
+    }
 }
 
 // Segment k of the launch through constant kernarg indices (a dynamic index would copy the array to scratch).
@@ -414,14 +509,13 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
     // epilogue: lane holds rows m .. m+3 (4 consecutive output channels) of domain pixel nd
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
-        const LifQuad lq = lif_quad(a, m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4));
+        const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
+        if (ksplit > 1) {  // split-K: this split's partial sums, reduced by k_unet_conv_reduce
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
-            const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
-            if (nd >= P || m >= a.M) continue;
-            const fx4 v = acc[i][j];
-            if (ksplit > 1) {  // split-K: this split's partial sums, reduced by k_unet_conv_reduce
+            for (int j = 0; j < 4; ++j) {
+                const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
+                if (nd >= P || m >= a.M) continue;
+                const fx4 v = acc[i][j];
                 float* o = a.partial + ((int64_t)split * P + nd) * a.M + m;
                 if (m + 3 < a.M && (a.M & 3) == 0) {
                     *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
@@ -430,10 +524,14 @@ __global__ __launch_bounds__(UNT) void k_unet_conv(snnflow_unet_conv_args a) {
                     for (int r = 0; r < 4; ++r)
                         if (m + r < a.M) o[r] = v[r];
                 }
-                continue;
             }
-            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lq);
+            continue;
         }
+        const LifQuad lq = lif_quad(a, m);
+        const int nd[4] = {n0 + wn * 64 + (lane & 15), n0 + wn * 64 + 16 + (lane & 15), n0 + wn * 64 + 32 + (lane & 15),
+                           n0 + wn * 64 + 48 + (lane & 15)};
+        const fx4 v[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+        conv_epilogue4(a, dom, m, nd, v, lq);
     }
 }
 
@@ -662,14 +760,13 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
 
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
-        const LifQuad lq = lif_quad(a, m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4));
+        const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
+        if (ksplit > 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
-            const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
-            if (nd >= P || m >= a.M) continue;
-            const fx4 v = acc[i][j];
-            if (ksplit > 1) {
+            for (int j = 0; j < 4; ++j) {
+                const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
+                if (nd >= P || m >= a.M) continue;
+                const fx4 v = acc[i][j];
                 float* o = a.partial + ((int64_t)split * P + nd) * a.M + m;
                 if (m + 3 < a.M && (a.M & 3) == 0) {
                     *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
@@ -678,10 +775,14 @@ __global__ __launch_bounds__(UNT) void k_unet_conv_dma(snnflow_unet_conv_args a)
                     for (int r = 0; r < 4; ++r)
                         if (m + r < a.M) o[r] = v[r];
                 }
-                continue;
             }
-            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lq);
+            continue;
         }
+        const LifQuad lq = lif_quad(a, m);
+        const int nd[4] = {n0 + wn * 64 + (lane & 15), n0 + wn * 64 + 16 + (lane & 15), n0 + wn * 64 + 32 + (lane & 15),
+                           n0 + wn * 64 + 48 + (lane & 15)};
+        const fx4 v[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+        conv_epilogue4(a, dom, m, nd, v, lq);
     }
 }
 
@@ -834,14 +935,13 @@ __global__ __launch_bounds__(UNT) void k_unet_dgrad_dma(snnflow_unet_conv_args a
 
 #pragma unroll
     for (int i = 0; i < WMT; ++i) {
-        const LifQuad lq = lif_quad(a, m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4));
+        const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
+        if (ksplit > 1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int m = m0 + wm * 16 * WMT + i * 16 + 4 * (lane >> 4);
-            const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
-            if (nd >= P || m >= a.M) continue;
-            const fx4 v = acc[i][j];
-            if (ksplit > 1) {
+            for (int j = 0; j < 4; ++j) {
+                const int nd = n0 + wn * 64 + j * 16 + (lane & 15);
+                if (nd >= P || m >= a.M) continue;
+                const fx4 v = acc[i][j];
                 float* o = a.partial + ((int64_t)split * P + nd) * a.M + m;
                 if (m + 3 < a.M && (a.M & 3) == 0) {
                     *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
@@ -850,10 +950,14 @@ __global__ __launch_bounds__(UNT) void k_unet_dgrad_dma(snnflow_unet_conv_args a
                     for (int r = 0; r < 4; ++r)
                         if (m + r < a.M) o[r] = v[r];
                 }
-                continue;
             }
-            conv_epilogue(a, dom, nd, m, v[0], v[1], v[2], v[3], lq);
+            continue;
         }
+        const LifQuad lq = lif_quad(a, m);
+        const int nd[4] = {n0 + wn * 64 + (lane & 15), n0 + wn * 64 + 16 + (lane & 15), n0 + wn * 64 + 32 + (lane & 15),
+                           n0 + wn * 64 + 48 + (lane & 15)};
+        const fx4 v[4] = {acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+        conv_epilogue4(a, dom, m, nd, v, lq);
     }
 }
 
