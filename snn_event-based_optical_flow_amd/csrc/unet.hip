@@ -1949,7 +1949,8 @@ int launch_conv(const snnflow_unet_conv_args& a, hipStream_t s) {
 #define SNNFLOW_UNET_DMA 1     // forward convs (exact-in-bf16 inputs) through k_unet_conv_dma
 #endif
 #ifndef SNNFLOW_UNET_NSTAGE
-#define SNNFLOW_UNET_NSTAGE 2  // LDS buffers of k_unet_conv_dma (cfg5: 2 -> 278.6 ms, 3 -> 308.2 ms: 72 KB of LDS, two blocks per CU)
+#define SNNFLOW_UNET_NSTAGE 2  // LDS buffers of k_unet_conv_dma (cfg5: 2 -> 278.6 ms, 3 -> 308.2 ms: 72 KB of LDS, two blocks per CU;
+                               // round 6, 3 or 4 for the M <= 64 tiles only: no change, 4 slower)
 #endif
 template <int WMT, int WM>
 int launch_conv_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
@@ -1979,16 +1980,19 @@ int launch_conv_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
 #ifndef SNNFLOW_UNET_DGRAD_DMA
 #define SNNFLOW_UNET_DGRAD_DMA 1  // input gradients through k_unet_dgrad_dma
 #endif
+// The LDS-DMA input-gradient kernels take one segment, 32-bit buffer offsets over the three planes, taps
+// as a 32-bit mask, 32-bit W offsets; a transposed segment only as a parity class
+inline bool dgrad_dma_ok(const snnflow_unet_conv_args& a) {
+    const snnflow_unet_seg& g = a.seg[0];
+    return !(a.nseg != 1 || a.ksize * a.ksize > 32 || 3LL * a.ksize * a.ksize * a.kct * a.mpad * 32 >= 0x80000000LL ||
+             (2 * a.xpart + (int64_t)a.B * g.H * g.W * g.cpitch) * 2 >= 0x80000000LL ||
+             (g.mode == SNNFLOW_UNET_MODE_T2) != (a.pclass >= 0) || g.mode == SNNFLOW_UNET_MODE_S2);
+}
+
 template <int WMT, int WM>
 int launch_dgrad_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
     using G = ConvGeo<WMT, WM, 3>;
-    const snnflow_unet_seg& g = a.seg[0];
-    // one segment, 32-bit buffer offsets over the three planes, taps as a 32-bit mask, 32-bit W offsets;
-    // a transposed segment only as a parity class
-    if (a.nseg != 1 || a.ksize * a.ksize > 32 || 3LL * a.ksize * a.ksize * a.kct * a.mpad * 32 >= 0x80000000LL ||
-        (2 * a.xpart + (int64_t)a.B * g.H * g.W * g.cpitch) * 2 >= 0x80000000LL ||
-        (g.mode == SNNFLOW_UNET_MODE_T2) != (a.pclass >= 0) || g.mode == SNNFLOW_UNET_MODE_S2)
-        return launch_conv<WMT, WM, 3>(a, s);
+    if (!dgrad_dma_ok(a)) return launch_conv<WMT, WM, 3>(a, s);
     const int P = dom_pixels(a);
     const int ks = a.ksplit > 1 ? a.ksplit : 1;
     const int64_t nb = (int64_t)((a.M + G::BM - 1) / G::BM) * ((P + G::BN - 1) / G::BN) * ks;
@@ -2003,10 +2007,15 @@ int launch_dgrad_dma(const snnflow_unet_conv_args& a, hipStream_t s) {
     return 0;
 }
 
+// Input gradients with M > 64 (M = the forward conv's padded input channels): 96-row tiles where they
+// pad M less than 128-row tiles (the decoders' 2 cx + 6 channels: M = 288 -> 3 x 96 instead of 3 x 128,
+// 544 -> 6 x 96 instead of 5 x 128)
+inline bool dgrad_bm96(int M) { return (M + 95) / 96 * 96 < (M + 127) / 128 * 128; }
+
 // Output tiles of a launch for its tile configuration (the selection of snnflow_unet_conv).
 inline void conv_tile(const snnflow_unet_conv_args& a, int& bm, int& bn) {
     if (a.xparts == 3) {
-        bm = (a.M > 128 && a.M <= 160) ? 160 : (a.M > 64 ? 128 : (a.M > 32 ? 64 : 32));
+        bm = (a.M > 128 && a.M <= 160) ? 160 : (a.M > 64 ? (dgrad_bm96(a.M) ? 96 : 128) : (a.M > 32 ? 64 : 32));
         bn = a.M > 32 ? 128 : 256;
     } else if (a.M > 64) {
         bm = 128; bn = 128;
@@ -2073,12 +2082,14 @@ int snnflow_unet_conv(const snnflow_unet_conv_args* a, void* stream) {
     if (a->xparts == 3) {  // input gradients: the fp32 gradient as three bf16 planes
         if (SNNFLOW_UNET_DGRAD_DMA) {
             if (a->M > 128 && a->M <= 160) return launch_dgrad_dma<5, 2>(*a, s);
+            if (a->M > 64 && dgrad_bm96(a->M)) return launch_dgrad_dma<3, 2>(*a, s);
             if (a->M > 64) return launch_dgrad_dma<4, 2>(*a, s);
             if (a->M > 32) return launch_dgrad_dma<2, 2>(*a, s);
             // M <= 32 keeps the register-staged kernel: its 256-pixel tiles would need 96 KB of LDS
             // and 257 VGPRs double-buffered
         }
         if (a->M > 128 && a->M <= 160) return launch_conv<5, 2, 3>(*a, s);
+        if (a->M > 64 && dgrad_bm96(a->M)) return launch_conv<3, 2, 3>(*a, s);
         if (a->M > 64) return launch_conv<4, 2, 3>(*a, s);
         if (a->M > 32) return launch_conv<2, 2, 3>(*a, s);
         return launch_conv<2, 1, 3>(*a, s);
