@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SNNFLOW_ABI_VERSION 39
+#define SNNFLOW_ABI_VERSION 40
 
 #define SNNFLOW_E_ARG (-1)      /* invalid argument / unsupported shape */
 #define SNNFLOW_E_CHANNELS (-2) /* channel count without a compiled kernel */
@@ -236,6 +236,14 @@ typedef struct snnflow_layer_bwd_args {
      * every (layer, step) task of a pass runs in its own launch, so the accumulation over the steps
      * is a fixed-order read-modify-write (deterministic); snnflow_slab_reduce sums the rows. */
     float* wslab_ff; float* wslab_rec; const float* s_prev; int wslab_accumulate;
+    /* ABI 40, optional: the head's weight gradient fused into its backward task (lif_in = 0, cin 2 or 4,
+     * no recurrent conv, wavefront launches only).  The head task holds G = dL/dy of its tile after
+     * the BN backward and nothing else reads it, so with wslab_ff and x (the layer input, strided as
+     * g_x: [B][cin][H][W] at xs_b, xs_c, xs_h, xs_w)
+     *   dW_ff[co][ci][k] += sum_p G[p][co] x[p + k][ci]
+     * goes to the block's row of wslab_ff (written or added as above; the deferred path's per-tile
+     * per-step order of snnflow_wgrad's vector kernel, one step per call). */
+    const float* x; int64_t xs_b, xs_c, xs_h, xs_w;
 } snnflow_layer_bwd_args;
 int snnflow_layer_bwd(const snnflow_layer_bwd_args* a, void* stream);
 
@@ -864,6 +872,13 @@ typedef struct snnflow_firenet_seq_bwd {
     double* bwd_acc; int64_t acc_stride;
     snnflow_neuron_grad ng[SNNFLOW_MAX_LAYERS];
     float* g_pred_w; float* g_pred_b;
+    /* ABI 40: fuse_head = 1 adds the head's weight gradient of every step to the plan's slab_ff[0] rows
+     * inside the head's backward tasks (layer 0 feed-forward, cin0 2 or 4), reading the step inputs
+     * x[t] (strides xs[t] = b, c, h, w); the caller then leaves layer 0 out of the deferred weight
+     * gradients.  slab_live[0] is read and set like the fused layers'. */
+    int fuse_head;
+    const float* x[SNNFLOW_MAX_WINDOWS];
+    int64_t xs[SNNFLOW_MAX_WINDOWS][4];
 } snnflow_firenet_seq_bwd;
 int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet_seq_bwd* q, int* slab_live,
                             void* stream);

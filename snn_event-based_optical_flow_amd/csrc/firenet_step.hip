@@ -172,8 +172,10 @@ int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet
     for (int l = 0; l < L; ++l) rslot[l] = p->rec[l] ? nrec++ : -1;
     if (T > 1 && nrec && !q->g_out) SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: g_out missing");
     for (int t = 0; t < T; ++t)
-        if (!q->ys[t] || !q->stats[t] || !q->flow[t] || !q->states[t])
+        if (!q->ys[t] || !q->stats[t] || !q->flow[t] || !q->states[t] || (q->fuse_head && !q->x[t]))
             SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: incomplete step");
+    if (q->fuse_head && (p->rec[0] || !(p->cin0 == 2 || p->cin0 == 4) || !p->slab_ff[0]))
+        SNN_FAIL(SNNFLOW_E_ARG, "firenet_bwd_seq: fuse_head needs a feed-forward 2- or 4-channel head and its slab");
     // every launch's layer-task count, checked before the first launch (the call refuses cleanly or runs
     // to completion: no half-written gradients or slab rows)
     for (int d = 0; d < K + 2 * (T - 1); ++d) {
@@ -264,6 +266,13 @@ int snnflow_firenet_bwd_seq(const snnflow_firenet_plan* p, const snnflow_firenet
                 }
             } else {
                 a.cin = p->cin0; a.lif_in = 0;
+                if (q->fuse_head) {  // ABI 40: the head's weight gradient of step t in this task
+                    a.x = q->x[t];
+                    a.xs_b = q->xs[t][0]; a.xs_c = q->xs[t][1]; a.xs_h = q->xs[t][2]; a.xs_w = q->xs[t][3];
+                    a.wslab_ff = p->slab_ff[0];
+                    a.wslab_accumulate = slab_live[0] ? 1 : 0;
+                    slab_live[0] = 1;
+                }
             }
         }
         const int rc = snnflow_bwd_slot(la, nl, has_top ? &tb : nullptr, stream);

@@ -1408,9 +1408,139 @@ __device__ void fused_wgrad_store(const snnflow_layer_bwd_args& a, const Grid& g
     }
 }
 
-template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false, bool WGF = false>
+// Accumulator set of one (conv, thread): item q (tap, co-block of 4, ci-block of VW) and
+// pixel group g of the tile, summed over the steps.  Threads [TOFF, TOFF+NTH) of the block
+// take part; items x groups fill them (groups reduced in fixed order by flush).
+template <int CIN, int C, int NTH, int TOFF>
+struct WAcc {
+    static constexpr int VW = VecW<CIN>::v;
+    static constexpr int Q = 9 * (C / 4) * (CIN / VW);
+    static constexpr int GR0 = (Q >= NTH) ? 1 : NTH / Q;
+    static constexpr int GR = GR0 > 16 ? 16 : GR0;
+    static constexpr int NM = (GR > 1) ? 1 : (Q + NTH - 1) / NTH;
+    static constexpr int SCRATCH = (GR > 1) ? GR * Q * 4 * VW : 1;
+    float acc[NM][4][VW];
+    __device__ void zero() {
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < VW; ++j) acc[m][i][j] = 0.f;
+    }
+    // Gi: interior G tile [NT][Pad<C>] (HG: the halo G tile [HN][Pad<C>] of the backward task, read at
+    // the interior pixels); X: halo input tile [HN][Pad<CIN>]
+    template <bool HG = false>
+    __device__ void step(const float* Gi, const float* X) {
+        constexpr int PC = Pad<C>::v, PX = Pad<CIN>::v;
+        const int tid = (int)threadIdx.x - TOFF;
+        if (tid < 0 || tid >= NTH) return;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const int q = (GR > 1) ? tid % Q : tid + m * NTH;
+            const int g = (GR > 1) ? tid / Q : 0;
+            if ((GR > 1) ? (g >= GR) : (q >= Q)) continue;
+            const int kidx = q % 9, rest = q / 9, cob = rest % (C / 4), cib = rest / (C / 4);
+            const int ky = kidx / 3, kx = kidx % 3;
+#pragma unroll 4
+            for (int p = g; p < NT; p += GR) {
+                const int ty = p / TW, tx = p - ty * TW;
+                const int gp = HG ? (ty + 1) * HWD + tx + 1 : p;
+                const float4 gv4 = *reinterpret_cast<const float4*>(Gi + gp * PC + cob * 4);
+                const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
+                const float* xp = X + ((ty + ky) * HWD + tx + kx) * PX + cib * VW;
+                float xv[VW];
+                if constexpr (VW == 4) {
+                    const float4 v = *reinterpret_cast<const float4*>(xp);
+                    xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
+                } else if constexpr (VW == 2) {
+                    const float2 v = *reinterpret_cast<const float2*>(xp);
+                    xv[0] = v.x; xv[1] = v.y;
+                } else {
+                    xv[0] = xp[0];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) acc[m][i][j] = fmaf(gv[i], xv[j], acc[m][i][j]);
+            }
+        }
+    }
+    // slab element of reduction item e (0 <= e < Q * 4 * VW) of the group-scratch flush
+    static __device__ int slab_index(int e) {
+        const int qq = e / (4 * VW), ij = e - qq * 4 * VW, i = ij / VW, j = ij - i * VW;
+        const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
+        return ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
+    }
+    static constexpr int NOLD = (Q * 4 * VW + NTH - 1) / NTH;  // reduction items per thread
+    // flush (GR > 1) with the slab's old values already in registers (old[k]: item tid + k NTH),
+    // loaded by the caller long before: the read-modify-write then waits on no global load
+    __device__ void flush_prefetched(float* __restrict__ slab, int accumulate, float* scratch, const float (&old)[NOLD]) {
+        static_assert(GR > 1, "group-scratch form");
+        const int tid = (int)threadIdx.x - TOFF;
+        const bool mine = tid >= 0 && tid < NTH;
+        const int q = tid % Q, g = tid / Q;
+        if (mine && g < GR) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < VW; ++j) scratch[((g * Q + q) * 4 + i) * VW + j] = acc[0][i][j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NOLD; ++k) {
+            const int e = tid + k * NTH;
+            if (mine && e < Q * 4 * VW) {
+                float sum = 0.f;
+                for (int gg = 0; gg < GR; ++gg) sum += scratch[gg * Q * 4 * VW + e];
+                slab[slab_index(e)] = accumulate ? old[k] + sum : sum;
+            }
+        }
+    }
+    // cross-group reduction in fixed order, then one write (or add) of the block's slab
+    __device__ void flush(float* __restrict__ slab, int accumulate, float* scratch) {
+        const int tid = (int)threadIdx.x - TOFF;
+        const bool mine = tid >= 0 && tid < NTH;
+        if constexpr (GR > 1) {
+            const int q = tid % Q, g = tid / Q;
+            if (mine && g < GR) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) scratch[((g * Q + q) * 4 + i) * VW + j] = acc[0][i][j];
+            }
+            __syncthreads();
+            for (int e = mine ? tid : Q * 4 * VW; e < Q * 4 * VW; e += NTH) {
+                float sum = 0.f;
+                for (int gg = 0; gg < GR; ++gg) sum += scratch[gg * Q * 4 * VW + e];
+                const int qq = e / (4 * VW), ij = e - qq * 4 * VW, i = ij / VW, j = ij - i * VW;
+                const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
+                const int idx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
+                slab[idx] = accumulate ? slab[idx] + sum : sum;
+            }
+            __syncthreads();
+        } else {
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const int q = tid + m * NTH;
+                if (!mine || q >= Q) continue;
+                const int kk = q % 9, rest = q / 9, cb = rest % (C / 4), ib = rest / (C / 4);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < VW; ++j) {
+                        const int idx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
+                        slab[idx] = accumulate ? slab[idx] + acc[m][i][j] : acc[m][i][j];
+                    }
+            }
+        }
+    }
+};
+
+template <int CIN, int C, bool LIF_IN, bool REC, int SPLIT, bool BFG = false, bool WGF = false, bool HWG = false>
 __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, float* lds) {
     using LB = LayerBwdLds<CIN, C, LIF_IN, REC, SPLIT, BFG>;
+    static_assert(!HWG || (!LIF_IN && !REC && !kMfma<CIN, C>), "fused head weight gradient: feed-forward head tasks");
     static_assert(!WGF || (LIF_IN && C == 8 && CIN == 8 && SPLIT == 2 && LB::BF6 && LB::FR >= kWgfFloats),
                   "fused weight gradients: C = 8 LIF-fed layers with LDS weight fragments");
     constexpr int NTB = NT * SPLIT;
@@ -1504,6 +1634,31 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
             if (a.wt_bwd_ff) fs_x.load(a.wt_fwd_ff);
             if constexpr (REC) {
                 if (a.g_state_prev) fs_r.load(a.wt_fwd_rec);
+            }
+        }
+    }
+    // fused head weight gradient (ABI 40): its input halo and the slab row's old values are loaded here,
+    // with the task's other loads, so that neither is waited on after the BN backward
+    using HAF = WAcc<HWG ? CIN : 4, HWG ? C : 4, NTB, 0>;
+    constexpr int HXR = HWG ? (HN * CIN + NTB - 1) / NTB : 1;
+    [[maybe_unused]] const bool hwg = HWG && a.wslab_ff != nullptr && a.x != nullptr;
+    [[maybe_unused]] float hx[HXR], hold[HAF::NOLD];
+    if constexpr (HWG) {
+        if (hwg) {
+            const float* xb = a.x + (int64_t)tl.b * a.xs_b;
+#pragma unroll
+            for (int i = 0; i < HXR; ++i) {
+                const int e = tid + i * NTB;
+                const int ci = e / HN, p = e - ci * HN;  // channel-major: the plane reads coalesce
+                const int r = p / HWD, cc = p - r * HWD;
+                const int hh = tl.h0 + r - 1, ww = tl.w0 + cc - 1;
+                hx[i] = (e < HN * CIN && in_image(hh, ww, H, W)) ? xb[ci * a.xs_c + hh * a.xs_h + ww * a.xs_w] : 0.0f;
+            }
+            const float* srow = a.wslab_ff + (int64_t)g.bid * (C * CIN * 9);
+#pragma unroll
+            for (int k = 0; k < HAF::NOLD; ++k) {
+                const int e = tid + k * NTB;
+                hold[k] = (a.wslab_accumulate && e < C * CIN * 9) ? srow[HAF::slab_index(e < C * CIN * 9 ? e : 0)] : 0.0f;
             }
         }
     }
@@ -1817,6 +1972,28 @@ __device__ void layer_bwd_body(const snnflow_layer_bwd_args& a, const Grid g, fl
 #pragma unroll
             for (int ci = 0; ci < CI; ++ci) gb[(ci0 + ci) * a.gxs_c] = gx[ci];
         }
+        if constexpr (HWG) {
+            // the head's weight gradient of this step (ABI 40): G (fp32 halo tile, zero outside the image)
+            // is intact; the input halo and the accumulators' group scratch go behind it.  The arithmetic
+            // of k_wgrad's vector path (WAcc) for one step, added to the block's slab row.
+            if (hwg) {
+                float* X = lds + LB::G;
+#pragma unroll
+                for (int i = 0; i < HXR; ++i) {
+                    const int e = tid + i * NTB;
+                    if (e < HN * CIN) {
+                        const int ci = e / HN, p = e - ci * HN;
+                        X[p * Pad<CIN>::v + ci] = hx[i];
+                    }
+                }
+                HAF af;
+                af.zero();
+                __syncthreads();
+                af.template step<true>(G, X);
+                __syncthreads();  // G and X read: the group scratch of the flush overlays them
+                af.flush_prefetched(a.wslab_ff + (int64_t)g.bid * (C * CIN * 9), a.wslab_accumulate, lds, hold);
+            }
+        }
     }
 }
 
@@ -1836,101 +2013,6 @@ void k_layer_bwd(snnflow_layer_bwd_args a) {
 // and the block writes its slab once.
 // ---------------------------------------------------------------------------
 typedef const __attribute__((address_space(4))) snnflow_wgrad_args* cwgrad_ptr;
-
-// Accumulator set of one (conv, thread): item q (tap, co-block of 4, ci-block of VW) and
-// pixel group g of the tile, summed over the steps.  Threads [TOFF, TOFF+NTH) of the block
-// take part; items x groups fill them (groups reduced in fixed order by flush).
-template <int CIN, int C, int NTH, int TOFF>
-struct WAcc {
-    static constexpr int VW = VecW<CIN>::v;
-    static constexpr int Q = 9 * (C / 4) * (CIN / VW);
-    static constexpr int GR0 = (Q >= NTH) ? 1 : NTH / Q;
-    static constexpr int GR = GR0 > 16 ? 16 : GR0;
-    static constexpr int NM = (GR > 1) ? 1 : (Q + NTH - 1) / NTH;
-    static constexpr int SCRATCH = (GR > 1) ? GR * Q * 4 * VW : 1;
-    float acc[NM][4][VW];
-    __device__ void zero() {
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < VW; ++j) acc[m][i][j] = 0.f;
-    }
-    // Gi: interior G tile [NT][Pad<C>]; X: halo input tile [HN][Pad<CIN>]
-    __device__ void step(const float* Gi, const float* X) {
-        constexpr int PC = Pad<C>::v, PX = Pad<CIN>::v;
-        const int tid = (int)threadIdx.x - TOFF;
-        if (tid < 0 || tid >= NTH) return;
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            const int q = (GR > 1) ? tid % Q : tid + m * NTH;
-            const int g = (GR > 1) ? tid / Q : 0;
-            if ((GR > 1) ? (g >= GR) : (q >= Q)) continue;
-            const int kidx = q % 9, rest = q / 9, cob = rest % (C / 4), cib = rest / (C / 4);
-            const int ky = kidx / 3, kx = kidx % 3;
-#pragma unroll 4
-            for (int p = g; p < NT; p += GR) {
-                const int ty = p / TW, tx = p - ty * TW;
-                const float4 gv4 = *reinterpret_cast<const float4*>(Gi + p * PC + cob * 4);
-                const float gv[4] = {gv4.x, gv4.y, gv4.z, gv4.w};
-                const float* xp = X + ((ty + ky) * HWD + tx + kx) * PX + cib * VW;
-                float xv[VW];
-                if constexpr (VW == 4) {
-                    const float4 v = *reinterpret_cast<const float4*>(xp);
-                    xv[0] = v.x; xv[1] = v.y; xv[2] = v.z; xv[3] = v.w;
-                } else if constexpr (VW == 2) {
-                    const float2 v = *reinterpret_cast<const float2*>(xp);
-                    xv[0] = v.x; xv[1] = v.y;
-                } else {
-                    xv[0] = xp[0];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) acc[m][i][j] = fmaf(gv[i], xv[j], acc[m][i][j]);
-            }
-        }
-    }
-    // cross-group reduction in fixed order, then one write (or add) of the block's slab
-    __device__ void flush(float* __restrict__ slab, int accumulate, float* scratch) {
-        const int tid = (int)threadIdx.x - TOFF;
-        const bool mine = tid >= 0 && tid < NTH;
-        if constexpr (GR > 1) {
-            const int q = tid % Q, g = tid / Q;
-            if (mine && g < GR) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) scratch[((g * Q + q) * 4 + i) * VW + j] = acc[0][i][j];
-            }
-            __syncthreads();
-            for (int e = mine ? tid : Q * 4 * VW; e < Q * 4 * VW; e += NTH) {
-                float sum = 0.f;
-                for (int gg = 0; gg < GR; ++gg) sum += scratch[gg * Q * 4 * VW + e];
-                const int qq = e / (4 * VW), ij = e - qq * 4 * VW, i = ij / VW, j = ij - i * VW;
-                const int kk = qq % 9, rest = qq / 9, cb = rest % (C / 4), ib = rest / (C / 4);
-                const int idx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
-                slab[idx] = accumulate ? slab[idx] + sum : sum;
-            }
-            __syncthreads();
-        } else {
-#pragma unroll
-            for (int m = 0; m < NM; ++m) {
-                const int q = tid + m * NTH;
-                if (!mine || q >= Q) continue;
-                const int kk = q % 9, rest = q / 9, cb = rest % (C / 4), ib = rest / (C / 4);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < VW; ++j) {
-                        const int idx = ((cb * 4 + i) * CIN + ib * VW + j) * 9 + kk;
-                        slab[idx] = accumulate ? slab[idx] + acc[m][i][j] : acc[m][i][j];
-                    }
-            }
-        }
-    }
-};
 
 // Matrix-core weight gradient of one block (C >= 16, CIN % 16 == 0): per tap,
 //   dW_tap[co][ci] += sum_p G[p][co] * X[halo(p, tap)][ci]
@@ -3261,6 +3343,7 @@ __device__ inline void globalize(snnflow_layer_bwd_args& a) {
     globalize(a.prev);
     SNN_G(a.prev_g_state); SNN_G(a.prev_g_cur); SNN_G(a.prev_g_mem); SNN_G(a.acc_out); SNN_G(a.zero0);
     SNN_G(a.zero1); SNN_G(a.wd_ff); SNN_G(a.wd_rec); SNN_G(a.wslab_ff); SNN_G(a.wslab_rec); SNN_G(a.s_prev);
+    SNN_G(a.x);
 }
 __device__ inline void globalize(snnflow_eval_fwd_args& a) {
     SNN_G(a.x); SNN_G(a.s_in); SNN_G(a.mem_prev); SNN_G(a.s_prev); SNN_G(a.wt_ff); SNN_G(a.wt_rec);
@@ -3928,6 +4011,11 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L
     // regions, which the pool holds for every task kind
     static_assert(C != 8 || SlotLds<C>::BWD >= LayerBwdLds<C, C, true, true, 2>::FLOATS, "fused wgrad staging");
     static_assert(C != 8 || 2 * LayerBwdLds<C, C, true, true, 2>::FR >= NT * Pad<C>::v, "dgrad staging size");
+    // fused head weight gradients: input halo and the accumulators' group scratch behind the G tile
+    static_assert(SlotLds<C>::BWD >= LayerBwdLds<2, C, false, false, 2>::G + HN * Pad<2>::v &&
+                      SlotLds<C>::BWD >= LayerBwdLds<4, C, false, false, 2>::G + HN * Pad<4>::v &&
+                      SlotLds<C>::BWD >= WAcc<2, C, 2 * NT, 0>::SCRATCH && SlotLds<C>::BWD >= WAcc<4, C, 2 * NT, 0>::SCRATCH,
+                  "fused head weight gradient staging");
     typedef const __attribute__((address_space(4))) BwdSlotParams* cptr;
     const cptr pp = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
     Grid g;
@@ -3943,8 +4031,8 @@ __global__ __launch_bounds__(NT * 2, C == 8 ? SNNFLOW_BWD_SLOT_WAVES : SNNFLOW_L
         }                                                     \
         break;                                                \
     }
-        BWD_LAYER(true, SK_HEAD2, 2, C, false, false, 2)
-        BWD_LAYER(true, SK_HEAD4, 4, C, false, false, 2)
+        BWD_LAYER(true, SK_HEAD2, 2, C, false, false, 2, false, false, true)
+        BWD_LAYER(true, SK_HEAD4, 4, C, false, false, 2, false, false, true)
         BWD_LAYER(false, SK_PLAIN, C, C, false, false, 2)
         BWD_LAYER(false, SK_PLAIN_REC, C, C, false, true, 2)
         BWD_LAYER(true, SK_LIF, C, C, true, false, 2, SlotLds<C>::BFG, C == 8)
@@ -4003,7 +4091,7 @@ int conv_fwd_c(const snnflow_conv_fwd_args& a, hipStream_t s) {
 // needs no gradient and it has no recurrent state gradient to produce) only finishes its neuron
 // gradients and BN-backward coefficients, which block 0 does: one block.
 int layer_bwd_blocks(const snnflow_layer_bwd_args& a) {
-    const bool pixels = a.lif_in || (a.g_x && a.wt_bwd_ff) || (a.wt_bwd_rec && a.g_state_prev);
+    const bool pixels = a.lif_in || (a.g_x && a.wt_bwd_ff) || (a.wt_bwd_rec && a.g_state_prev) || (a.wslab_ff && a.x);
     return pixels ? snnflow_conv_blocks(a.B, a.H, a.W) : 1;
 }
 
@@ -4447,8 +4535,10 @@ int snnflow_bwd_slot(const snnflow_layer_bwd_args* layer, int nlayer, const snnf
             SNN_FAIL(SNNFLOW_E_CHANNELS, "bwd_slot: c = 16 / 32 runs the LIFFireNet task kinds only");
         // the fused weight gradients exist for the C = 8 LIF-fed tasks only: anywhere else the layer's
         // weight gradient would be silently lost
-        if ((a.wslab_ff || a.wslab_rec) && !(c == 8 && (kind == SK_LIF || kind == SK_LIF_REC)))
-            SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: wslab_ff / wslab_rec need a c = 8 LIF-fed task");
+        // (ABI 40: and the feed-forward head tasks given their input x)
+        const bool head_wg = (kind == SK_HEAD2 || kind == SK_HEAD4) && a.x != nullptr && !a.wslab_rec && !a.wt_bwd_rec;
+        if ((a.wslab_ff || a.wslab_rec) && !(c == 8 && (kind == SK_LIF || kind == SK_LIF_REC)) && !head_wg)
+            SNN_FAIL(SNNFLOW_E_ARG, "bwd_slot: wslab_ff / wslab_rec need a c = 8 LIF-fed task or a head task with x");
         p.layer[i] = a;
         p.kind[i] = kind;
         p.nblk[i] = layer_bwd_blocks(a);
@@ -4487,6 +4577,7 @@ int snnflow_set_pipe(int fwd_tiles_per_block, int bwd_tiles_per_block) {
 int snnflow_get_pipe(int which) { return which == 0 ? g_pipe_fwd : 0; }
 
 static int g_wg_bits = env_int("SNNFLOW_WG_BITS", 1);  // A/B: 0 = k_wgrad_bf32 / k_wgrad_bf on the bit planes
+static int g_wg_head_sp2 = env_int("SNNFLOW_WG_HEAD_SP2", 1);
 static bool wgrad_all_x_bits(const snnflow_wgrad_args* a) {
     for (int t = 0; t < a->nsteps; ++t)
         if (!a->steps[t].x_bits) return false;
@@ -4511,7 +4602,11 @@ int snnflow_wgrad(const snnflow_wgrad_args* a, void* stream) {
 #define WG_LAUNCH(CI_, CC_, REC_)                                                                          \
     do {                                                                                                   \
         constexpr int SP_ = (CC_ == 8 || CC_ == 16 || (CC_ == 32 && CI_ % 16 == 0)) ? 2 : 1;              \
-        hipLaunchKernelGGL((k_wgrad<CI_, CC_, REC_, SP_>), grid, dim3(NT * SP_), 0, s, *a);               \
+        constexpr int SP2_ = (CC_ == 32 && CI_ == 2 && !REC_) ? 2 : SP_;                                  \
+        if (SP2_ != SP_ && !g_wg_head_sp2)                                                                \
+            hipLaunchKernelGGL((k_wgrad<CI_, CC_, REC_, SP_>), grid, dim3(NT * SP_), 0, s, *a);           \
+        else                                                                                              \
+            hipLaunchKernelGGL((k_wgrad<CI_, CC_, REC_, SP2_>), grid, dim3(NT * SP2_), 0, s, *a);         \
     } while (0)
 #define WG_PICK(CI_, CC_)                                                                                  \
     do {                                                                                                   \

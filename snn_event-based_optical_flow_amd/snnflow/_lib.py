@@ -18,7 +18,7 @@ F32 = ctypes.c_float
 F64 = ctypes.c_double
 
 TILE_H, TILE_W = 8, 32
-ABI_VERSION = 39
+ABI_VERSION = 40
 THETA_SCRATCH = 1024 * 32  # SNNFLOW_THETA_SCRATCH
 
 
@@ -79,7 +79,8 @@ class LayerBwdArgs(ctypes.Structure):
                 ("prev_y", P), ("prev_mem", P), ("prev_stats", P), ("prev", Neuron),
                 ("prev_g_state", P), ("prev_g_cur", P), ("prev_g_mem", P), ("acc_out", P),
                 ("zero0", P), ("zero1", P), ("zero_n", I32), ("wd_ff", P), ("wd_rec", P),
-                ("wslab_ff", P), ("wslab_rec", P), ("s_prev", P), ("wslab_accumulate", I32)]
+                ("wslab_ff", P), ("wslab_rec", P), ("s_prev", P), ("wslab_accumulate", I32),
+                ("x", P), ("xs_b", I64), ("xs_c", I64), ("xs_h", I64), ("xs_w", I64)]
 
 
 MAX_WGRAD_STEPS = 32
@@ -257,7 +258,8 @@ class FireNetSeqBwd(ctypes.Structure):
                 ("gflow_sb", I64 * MAX_WINDOWS), ("gflow_sc", I64 * MAX_WINDOWS),
                 ("mem_in0", PL), ("s_prev0", PL), ("g_prev0", PL), ("ext0", I32 * MAX_LAYERS), ("g_state_last", PL),
                 ("g_out", P), ("g_cur", P), ("bnc", P), ("bwd_acc", P), ("acc_stride", I64),
-                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P)]
+                ("ng", NeuronGrad * MAX_LAYERS), ("g_pred_w", P), ("g_pred_b", P),
+                ("fuse_head", I32), ("x", P * MAX_WINDOWS), ("xs", (I64 * 4) * MAX_WINDOWS)]
 
 
 class FireNetWgradStep(ctypes.Structure):

@@ -206,6 +206,11 @@ class FireNetEngine:
         self.pending_layers = []  # per pending step: the layers whose weight gradients are still deferred
         self.slab_live = [False] * self.L      # slab rows of layer l hold partial sums of this chain
         self.fuse_wgrad = self.C == 8          # wavefront backward computes layers >= 1's dW in place
+        # wavefront backward adds the head's dW of each step inside the head's backward task (ABI 40).
+        # Measured (profiles/r06/fuse_head_ab.txt): C = 32 -35 us per step (the deferred k_wgrad<2, 32> gone,
+        # the slots +2-4 us per launch); C = 8 neutral to +5 us, so off there.  SNNFLOW_FUSE_HEAD=0 / 1 forces.
+        fh = os.environ.get("SNNFLOW_FUSE_HEAD")
+        self.fuse_head = (self.C >= 16) if fh is None else fh != "0"
         # forward_sequence: spike bit planes between its kernels (ABI 39; SNNFLOW_SPK_BITS=0: the fp32 spike
         # half of the states everywhere, as before)
         self.spk_bits = os.environ.get("SNNFLOW_SPK_BITS", "1") != "0"
@@ -981,6 +986,14 @@ def _chain_backward_batched(eng, steps):
     q.T, q.fresh = T, 1 if fresh else 0
     fuse = bool(eng.fuse_wgrad) and C == 8
     q.fused = 1 if fuse else 0
+    xs0 = [st.saved[0] for st in steps]
+    fuse_head = (bool(eng.fuse_head) and not eng.rec[0] and cin0 in (2, 4)
+                 and all(x.dim() == 4 and x.dtype == torch.float32 for x in xs0))
+    q.fuse_head = 1 if fuse_head else 0
+    if fuse_head:
+        for t, x in enumerate(xs0):
+            q.x[t] = x.data_ptr()
+            q.xs[t][0], q.xs[t][1], q.xs[t][2], q.xs[t][3] = _x_strides(x)
     q.ys[:T] = [st.saved[1].data_ptr() for st in steps]
     q.stats[:T] = [st.saved[2].data_ptr() for st in steps]
     q.flow[:T] = [st.saved[3].data_ptr() for st in steps]
@@ -1019,7 +1032,7 @@ def _chain_backward_batched(eng, steps):
             x, ys, stats = st.saved[:3]
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys), _Rows(stats), x, st.saved[4:4 + L],
                                 st.ptrs[1], (st.saved, buf), None))
-            eng.pending_layers.append((0,) if fuse else tuple(range(L)))
+            eng.pending_layers.append(tuple(l for l in range(L) if not ((fuse and l > 0) or (fuse_head and l == 0))))
         eng.flush_weight_grads(B, H, W, cin0, ws, glayers, s, plan)
     except Exception:
         eng.ws.reset_acc()
@@ -1397,11 +1410,14 @@ class FireNetSequence(torch.autograd.Function):
         # layers >= 1: dW inside the backward slot tasks (wslab_*); the forward's choice (it skipped the
         # spike planes the fused form never reads), not the engine flag's value now
         fuse = ctx.fuse
+        # the head's dW inside its backward tasks (ABI 40): a feed-forward 2- / 4-channel head
+        fuse_head = (bool(eng.fuse_head) and not eng.rec[0] and cin0 in (2, 4)
+                     and all(x.dim() == 4 and x.dtype == torch.float32 for x in xs))
         bptr = ctx.bptr
         for t in range(T - 1, -1, -1):
             eng.pending.append((_Rows(gcur[t]), _Rows(bnc[t]), _Rows(ys[t]), _Rows(stats[t]), xs[t], states[t], s_prev[t],
                                 (gcur, bnc, ys, stats, ctx.bits), (bptr[t], bptr[t - 1] if t >= 1 else [None] * L)))
-            eng.pending_layers.append((0,) if fuse else tuple(range(L)))
+            eng.pending_layers.append(tuple(l for l in range(L) if not ((fuse and l > 0) or (fuse_head and l == 0))))
         try:
             # backward kernel j of step t: j = 0 top (pred + LIF of layer L-1), j >= 1 layer L-j;
             # in reversed time tau = T-1-t the dependencies have the forward's shape: (j-1, tau)
@@ -1427,6 +1443,12 @@ class FireNetSequence(torch.autograd.Function):
                             # the spike half of g_into), so that plane is not zero-filled; step 0's is
                             # returned to autograd and is
                             a.zero_mem_half = 0
+                        if fuse_head and l == 0:
+                            a.x = xs[t].data_ptr()
+                            a.xs_b, a.xs_c, a.xs_h, a.xs_w = _x_strides(xs[t])
+                            a.wslab_ff = ws.slab_ff[0].data_ptr()
+                            a.wslab_accumulate = 1 if eng.slab_live[0] else 0
+                            eng.slab_live[0] = True
                         if fuse and l > 0:
                             a.wslab_ff = ws.slab_ff[l].data_ptr()
                             if eng.rec[l]:

@@ -1992,3 +1992,47 @@ def test_recurrent_cell_narrow_input_vs_oracle(dev, cin, C):
     pairs = [(n, a.grad.cpu().numpy(), rp[n].grad.numpy()) for n, a in cell.named_parameters()]
     pairs += [(f"x{i}", a.grad.cpu().numpy(), b.grad.numpy()) for i, (a, b) in enumerate(zip(xd, xs))]
     _grad_check(f"rec cell cin={cin} C={C}", pairs, ORACLE_GRAD_TOL)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [8, 32])
+def test_fused_head_weight_gradient_matches_deferred(dev, C):
+    """ABI 40: the head's weight gradient added inside its wavefront backward tasks (fuse_head) against
+    the deferred snnflow_wgrad form, two BPTT windows: every other gradient equal up to the fp64 batch-sum
+    atomics' order, the head's conv weight up to the order of the fp32 sums over the steps (per step into
+    the slab row vs across the steps in registers)."""
+    import copy
+
+    import snnflow
+    from oracle import lif_ref
+    from snnflow.synthetic import make_window
+
+    torch.manual_seed(11)
+    kw = lif_ref.make_unet_kwargs(base_num_channels=C)
+    ma = snnflow.LIFFireNet(dict(kw)).to(dev).train()
+    mb = copy.deepcopy(ma)
+    ma.engine.fuse_head, mb.engine.fuse_head = False, True
+    H, W, B, T = 64, 72, 2, 4
+    cfg = {"loader": {"resolution": [H, W]}, "loss": {"flow_regul_weight": 0.001, "overwrite_intermediate": False},
+           "model": {"mask_output": True}}
+    ea, eb = snnflow.EventWarping(cfg, dev), snnflow.EventWarping(cfg, dev)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for it in range(2):
+        wins = [make_window(B, 400, H, W, gen, dev) for _ in range(T)]
+        for m, e in ((ma, ea), (mb, eb)):
+            outs = m.forward_sequence([w["event_voxel"] for w in wins], [w["event_cnt"] for w in wins])
+            for o, w in zip(outs, wins):
+                e.event_flow_association(o["flow"], w["event_list"], w["event_list_pol_mask"], w["event_mask"])
+            m.zero_grad(set_to_none=True)
+            e().backward()
+        for (n, a), (_, b) in zip(ma.named_parameters(), mb.named_parameters()):
+            if n == "head.ff.weight":
+                r = _rel(b.grad.cpu().numpy(), a.grad.cpu().numpy())
+                print(f"[fuse_head C={C} it {it}] head.ff.weight rel {r:.3e}")
+                assert r < 1e-6, (it, n, r)
+            else:  # the same kernels; only the fp64 batch-sum atomics may add in another order
+                assert _rel(b.grad.cpu().numpy(), a.grad.cpu().numpy()) < 1e-6, (it, n)
+        ma.detach_states()
+        mb.detach_states()
+        ea.reset()
+        eb.reset()
