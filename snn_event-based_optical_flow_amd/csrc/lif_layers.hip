@@ -2145,12 +2145,19 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
         coef[t][c] = k;
     }
 
-    float4 rg[O::R], ry[O::R], rx[RX], rs[RS];
     // narrow strided inputs (the head's NCHW event counts): element-wise register prefetch
     constexpr int RXS = XV ? 1 : (HN * CIN + NTB - 1) / NTB;
-    float rxs[RXS];
-    bool dense = false, has_s = false;
-    auto issue = [&](int t) {  // loads of step t into registers
+    // one step's loads in registers, D steps in flight.  D = 3 for the C = 8 feed-forward layers (the
+    // deferred head of the wavefront path, 18 registers per step) measured 33.4-35.0 -> 36.2-36.8 us per
+    // cfg2 step (profiles/r06/fuse_head_ab.txt): the head's per-step time is not load latency; D = 1.
+    struct Pf {
+        float4 rg[O::R], ry[O::R], rx[RX], rs[RS];
+        float rxs[RXS];
+        bool dense, has_s;
+    };
+    constexpr int D = 1;
+    Pf pf[D];
+    auto issue = [&](int t, Pf& f) {  // loads of step t into registers
         const float* g = ap->steps[t].g_cur;
         const float* y = ap->steps[t].y;
 #pragma unroll
@@ -2161,17 +2168,17 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
             const int h = tl.h0 + ty, w = tl.w0 + tx;
             const bool ok = e < O::E && h < H && w < W;
             const int64_t k = ok ? (((int64_t)tl.b * H + h) * W + w) * O::Q + q : 0;
-            rg[i] = ok ? reinterpret_cast<const float4*>(g)[k] : z4;
-            ry[i] = ok ? reinterpret_cast<const float4*>(y)[k] : z4;
+            f.rg[i] = ok ? reinterpret_cast<const float4*>(g)[k] : z4;
+            f.ry[i] = ok ? reinterpret_cast<const float4*>(y)[k] : z4;
         }
         const float* sx = ap->steps[t].x;
         const float* sp = ap->steps[t].s_prev;
-        dense = false;
+        f.dense = false;
         if constexpr (XV)
-            dense = ap->steps[t].xs_c == 1 && ap->steps[t].xs_w == CIN && ap->steps[t].xs_h == (int64_t)W * CIN &&
-                    ap->steps[t].xs_b == (int64_t)H * W * CIN;
+            f.dense = ap->steps[t].xs_c == 1 && ap->steps[t].xs_w == CIN && ap->steps[t].xs_h == (int64_t)W * CIN &&
+                      ap->steps[t].xs_b == (int64_t)H * W * CIN;
         if constexpr (XV) {
-            if (dense) halo_load<CIN, NTB>(sx, tl, H, W, rx);
+            if (f.dense) halo_load<CIN, NTB>(sx, tl, H, W, f.rx);
         } else {
             const auto& st = ap->steps[t];
             const float* xb = sx + (int64_t)tl.b * st.xs_b;
@@ -2181,12 +2188,44 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
                 const int ci = e / HN, p = e - ci * HN;  // channel-major: plane reads coalesce
                 const int r = p / HWD, cc = p - r * HWD;
                 const int h = tl.h0 + r - 1, w = tl.w0 + cc - 1;
-                rxs[i] = (e < HN * CIN && in_image(h, w, H, W)) ? xb[ci * st.xs_c + h * st.xs_h + w * st.xs_w] : 0.0f;
+                f.rxs[i] = (e < HN * CIN && in_image(h, w, H, W)) ? xb[ci * st.xs_c + h * st.xs_h + w * st.xs_w] : 0.0f;
             }
         }
-        has_s = REC && sp != nullptr;
+        f.has_s = REC && sp != nullptr;
         if constexpr (REC) {
-            if (has_s) halo_load<C, NTB>(sp, tl, H, W, rs);
+            if (f.has_s) halo_load<C, NTB>(sp, tl, H, W, f.rs);
+        }
+    };
+    // stage step t: G on the tile interior, x and s_prev halos
+    auto stage = [&](int t, const Pf& f) {
+#pragma unroll
+        for (int i = 0; i < O::R; ++i) {
+            const int e = tid + i * NTB;
+            if (e < O::E) {
+                const int p = e / O::Q, q = e - p * O::Q;
+                const int ty = p / TW, tx = p - ty * TW;
+                const bool img = tl.h0 + ty < H && tl.w0 + tx < W;  // G = 0 outside the image
+                *reinterpret_cast<float4*>(Gi + p * PC + 4 * q) = img ? bn_bwd4(f.rg[i], f.ry[i], &coef[t][4 * q]) : z4;
+            }
+        }
+        if constexpr (XV) {
+            if (f.dense) halo_store<CIN, NTB>(X, f.rx);
+        }
+        if constexpr (!XV) {
+#pragma unroll
+            for (int i = 0; i < RXS; ++i) {
+                const int e = tid + i * NTB;
+                if (e < HN * CIN) {
+                    const int ci = e / HN, p = e - ci * HN;
+                    X[p * PI_ + ci] = f.rxs[i];
+                }
+            }
+        } else if (!f.dense) {
+            stage_strided<CIN, NTB>(ap->steps[t].x, ap->steps[t].xs_b, ap->steps[t].xs_c, ap->steps[t].xs_h,
+                                    ap->steps[t].xs_w, tl, H, W, X);
+        }
+        if constexpr (REC) {
+            if (f.has_s) halo_store<C, NTB>(S, f.rs);
         }
     };
 
@@ -2199,51 +2238,29 @@ __global__ __launch_bounds__(NT * SPLIT) void k_wgrad(snnflow_wgrad_args) {
         af.zero();
         if constexpr (REC) ar.zero();
     }
-    issue(0);
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+        if (k < nsteps) issue(k, pf[k]);
     __syncthreads();  // coef
-    for (int t = 0; t < nsteps; ++t) {
-        // stage step t: G on the tile interior, x and s_prev halos
+    for (int t0 = 0; t0 < nsteps; t0 += D) {
 #pragma unroll
-        for (int i = 0; i < O::R; ++i) {
-            const int e = tid + i * NTB;
-            if (e < O::E) {
-                const int p = e / O::Q, q = e - p * O::Q;
-                const int ty = p / TW, tx = p - ty * TW;
-                const bool img = tl.h0 + ty < H && tl.w0 + tx < W;  // G = 0 outside the image
-                *reinterpret_cast<float4*>(Gi + p * PC + 4 * q) = img ? bn_bwd4(rg[i], ry[i], &coef[t][4 * q]) : z4;
-            }
-        }
-        const bool dense_t = dense, has_s_t = has_s;
-        if constexpr (XV) {
-            if (dense_t) halo_store<CIN, NTB>(X, rx);
-        }
-        if constexpr (!XV) {
-#pragma unroll
-            for (int i = 0; i < RXS; ++i) {
-                const int e = tid + i * NTB;
-                if (e < HN * CIN) {
-                    const int ci = e / HN, p = e - ci * HN;
-                    X[p * PI_ + ci] = rxs[i];
+        for (int k = 0; k < D; ++k) {
+            const int t = t0 + k;
+            if (t >= nsteps) break;
+            stage(t, pf[k]);
+            const bool has_s_t = pf[k].has_s;
+            __syncthreads();
+            if (t + D < nsteps) issue(t + D, pf[k]);  // step t+D's loads fly during the next D steps' math
+            if constexpr (MF) {
+                am.step(Gi, X, S, has_s_t);
+            } else {
+                af.step(Gi, X);
+                if constexpr (REC) {
+                    if (has_s_t) ar.step(Gi, S);
                 }
             }
-        } else if (!dense_t) {
-            stage_strided<CIN, NTB>(ap->steps[t].x, ap->steps[t].xs_b, ap->steps[t].xs_c, ap->steps[t].xs_h,
-                                    ap->steps[t].xs_w, tl, H, W, X);
+            __syncthreads();
         }
-        if constexpr (REC) {
-            if (has_s_t) halo_store<C, NTB>(S, rs);
-        }
-        __syncthreads();
-        if (t + 1 < nsteps) issue(t + 1);  // next step's loads fly during this step's math
-        if constexpr (MF) {
-            am.step(Gi, X, S, has_s_t);
-        } else {
-            af.step(Gi, X);
-            if constexpr (REC) {
-                if (has_s_t) ar.step(Gi, S);
-            }
-        }
-        __syncthreads();
     }
     const int64_t blk = blockIdx.x;
     if constexpr (MF) {
