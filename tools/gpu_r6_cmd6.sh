@@ -1,5 +1,6 @@
 #!/bin/bash
-# k_wgrad_b32 time split: DIAG 0 normal, 1 no MFMA phase, 2 no G loads, 3 neither (C = 32 line, per-layer wgrad times).
+# k_wgrad_b32 time split (ran against a diagnostic build, not kept, that compiled k_wgrad_b32<DIAG> variants selected by SNNFLOW_WG_DIAG):
+# DIAG 0 normal, 1 no MFMA phase, 2 no G loads, 3 neither (C = 32 line, per-layer wgrad times).
 set -u
 O=gpurun_out/r6c6
 mkdir -p $O
