@@ -2036,3 +2036,42 @@ def test_fused_head_weight_gradient_matches_deferred(dev, C):
         mb.detach_states()
         ea.reset()
         eb.reset()
+
+
+def _slab_reduce_order(slab):
+    """k_slab_reduce's fp64 order per element (16 row groups g; in each, rows g, g+16, ... into four
+    interleaved accumulators, (s0 + s1) + (s2 + s3); the groups added in order), cast to fp32."""
+    nblk, _ = slab.shape
+    x = slab.astype(np.float64)
+    tot = np.zeros(slab.shape[1])
+    for g in range(16):
+        s = [np.zeros(slab.shape[1]) for _ in range(4)]
+        b = g
+        while b + 48 < nblk:
+            for k in range(4):
+                s[k] = s[k] + x[b + 16 * k]
+            b += 64
+        while b < nblk:
+            s[0] = s[0] + x[b]
+            b += 16
+        tot = tot + ((s[0] + s[1]) + (s[2] + s[3]))
+    return tot.astype(np.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("elems,nblk", [(144, 512), (9216, 512), (72, 37), (1152, 100), (45, 130)])
+def test_slab_reduce_fixed_order(dev, elems, nblk):
+    """snnflow_slab_reduce equals the documented fixed fp64 order bit for bit (several slabs in one call,
+    row counts with and without a remainder group).  A 16-B-load form of the kernel (4 elements per thread)
+    passed this too but ran slower (C = 8 7.8 -> 16 us: a quarter of the blocks), so the scalar one stays."""
+    from snnflow import _lib
+
+    gen = torch.Generator().manual_seed(elems * 7 + nblk)
+    slabs = [torch.randn(nblk, elems, generator=gen) * (10.0 ** k) for k in (-3, 0)]
+    d_slabs = [s.to(dev) for s in slabs]
+    outs = [torch.empty(elems, device=dev) for _ in slabs]
+    descs = (_lib.SlabDesc * 2)(*[_lib.SlabDesc(s.data_ptr(), o.data_ptr(), elems) for s, o in zip(d_slabs, outs)])
+    _lib.call("slab_reduce", _lib.lib.snnflow_slab_reduce, descs, 2, nblk, _lib.stream_ptr(dev))
+    torch.cuda.synchronize()
+    for s, o in zip(slabs, outs):
+        np.testing.assert_array_equal(o.cpu().numpy(), _slab_reduce_order(s.numpy()))
